@@ -1,0 +1,49 @@
+// Shared helpers for the libmuz HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/muz.h"
+
+#define MUZ_HOST_CHECK(cond)           \
+  do {                                 \
+    if (!(cond)) return MUZ_E_INVALID; \
+  } while (0)
+
+#define MUZ_HIP_RET(expr)                  \
+  do {                                     \
+    hipError_t _e = (expr);                \
+    if (_e != hipSuccess) return (int)_e;  \
+  } while (0)
+
+static inline int muz_last_launch_error() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MUZ_OK : (int)e;
+}
+
+// ---- JAX integer semantics ----------------------------------------------------------
+// Python/JAX floor division and modulo (x // y, x % y with the sign of y).
+__device__ __forceinline__ int fdiv(int a, int b) {
+  int q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+__device__ __forceinline__ int fmodp(int a, int b) {
+  int r = a % b;
+  if (r != 0 && ((r < 0) != (b < 0))) r += b;
+  return r;
+}
+// jnp gather index: a negative index is normalised ONCE (i + n), then clamped to [0, n-1].
+__device__ __forceinline__ int jidx(int i, int n) {
+  i = (i < 0) ? i + n : i;
+  return i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+}
+
+// Dynamic index into a small register array without a scratch round trip.
+template <int N>
+__device__ __forceinline__ int rsel(const int (&a)[N], int i) {
+  int r = a[0];
+#pragma unroll
+  for (int j = 1; j < N; ++j) r = (i == j) ? a[j] : r;
+  return r;
+}

@@ -1,0 +1,327 @@
+// Deterministic MADN rules as per-lane device functions (one board per wavefront lane).
+//
+// Restates MADN/deterministic_madn.py (reference) for the GPU:
+//   valid_action 299-393, env_step 170-257, no_step 283-297, encode_board 395-438,
+//   set_pins_on_board 259-271, refill_action_set 273-281, is_player_done/get_winner 122-168,
+//   check_goal_path_for_pin{,2} utils/utility_funcs.py:142-184.
+// Pins / action sets / player live in VGPRs; the board of each lane is staged in LDS
+// ([cell][lane] bytes) so the data-dependent board lookups are LDS reads, not scratch.
+#pragma once
+#include "common.hpp"
+
+namespace muz {
+
+constexpr int kCells = 56;     // 4*distance + 16, distance fixed at 10
+constexpr int kTrack = 40;     // board_size
+constexpr int kDist = 10;
+
+enum : uint32_t {
+  R_TEAMS = 1u << 0,
+  R_FREE_PIN = 1u << 1,
+  R_CIRCULAR = 1u << 2,
+  R_START_BLOCK = 1u << 3,
+  R_JUMP_GOAL = 1u << 4,
+  R_FRIENDLY = 1u << 5,
+  R_START_ON_1 = 1u << 6,
+  R_BONUS_6 = 1u << 7,
+  R_MUST_TRAVERSE = 1u << 8,
+};
+
+// Rule constants after env_reset's layout fix-up (deterministic_madn.py:62-78).
+struct DetConsts {
+  int P;
+  int starting_player;
+  uint32_t flags;
+  int start[4];
+  int target[4];
+  int goal[4][4];
+};
+
+struct DetLane {
+  int pins[16];   // [p*4 + k]
+  int aset[24];   // [p*6 + m]
+  int cp;         // current_player (unsubstituted)
+  int done;
+  int reward;
+};
+
+// LDS view of one lane's board: cell c of this lane at base[c * bs].
+struct BoardView {
+  int8_t* base;
+  int bs;
+  __device__ __forceinline__ int at(int cell) const { return base[cell * bs]; }
+  __device__ __forceinline__ void set(int cell, int v) const { base[cell * bs] = (int8_t)v; }
+};
+
+__device__ __forceinline__ bool has(uint32_t f, uint32_t bit) { return (f & bit) != 0; }
+
+__device__ __forceinline__ int pin_of(const DetLane& s, int p, int k) { return rsel(s.pins, p * 4 + k); }
+__device__ __forceinline__ int aset_of(const DetLane& s, int p, int m) { return rsel(s.aset, p * 6 + m); }
+
+__device__ __forceinline__ int cst(const int (&a)[4], int i) { return rsel(a, i); }
+
+__device__ __forceinline__ int goal_of(const DetConsts& c, int p, int g) {
+  int r = c.goal[0][0];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int h = 0; h < 4; ++h) r = (p == q && g == h) ? c.goal[q][h] : r;
+  return r;
+}
+
+// is_player_done (deterministic_madn.py:122-137): all four goal cells of `p` hold a pin.
+__device__ __forceinline__ bool player_done(const DetConsts& c, const BoardView& b, int p) {
+  if (p >= c.P) return false;
+  bool all = true;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) all &= b.at(goal_of(c, p, g)) >= 0;
+  return all;
+}
+
+// Team substitution (deterministic_madn.py:184, 310).
+__device__ __forceinline__ int sub_player(const DetConsts& c, const BoardView& b, int cp0) {
+  return (has(c.flags, R_TEAMS) && player_done(c, b, cp0)) ? (cp0 + 2) % 4 : cp0;
+}
+
+// get_winner (deterministic_madn.py:139-168) as a 4-bit mask.
+__device__ __forceinline__ uint32_t winners(const DetConsts& c, const BoardView& b) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) d |= player_done(c, b, p) ? (1u << p) : 0u;
+  if (!has(c.flags, R_TEAMS)) return d;
+  bool t0 = (d & 1u) && (d & 4u);
+  bool t1 = (d & 2u) && (d & 8u);
+  if ((t0 && t1) || !(t0 || t1)) return 0u;
+  return t0 ? 0x5u : 0xAu;
+}
+
+// all(board[goal[g]] != cp for lo < g < hi)   (check_goal_path_for_pin{,2})
+__device__ __forceinline__ bool goal_path_free(const DetConsts& c, const BoardView& b, int cp, int lo, int hi) {
+  bool ok = true;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    if (lo < g && g < hi) ok &= b.at(goal_of(c, cp, g)) != cp;
+  return ok;
+}
+
+// valid_action (deterministic_madn.py:299-393) -> 24-bit mask, bit pin*6 + (move-1).
+__device__ __forceinline__ uint32_t det_legal(const DetConsts& c, const DetLane& s, const BoardView& b) {
+  const uint32_t F = c.flags;
+  const int cp0 = s.cp;
+  const int cp = sub_player(c, b, cp0);
+  const int tgt = cst(c.target, cp);
+  const int g0 = goal_of(c, cp, 0), g3 = goal_of(c, cp, 3);
+  const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
+  const int start_cp = cst(c.start, cp);
+  const bool home_ok = b.at(start_cp) != cp0;   // compares the UNSUBSTITUTED player (line 390)
+  bool pos[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pos[q] = (q < c.P) ? (b.at(cst(c.start, q)) == q) : false;
+  uint32_t avail = 0;
+#pragma unroll
+  for (int m = 0; m < 6; ++m) avail |= (aset_of(s, cp, m) > 0) ? (1u << m) : 0u;
+
+  uint32_t mask = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cur = pin_of(s, cp, i);
+    const bool in_goal = (cur == goal_of(c, cp, 0)) | (cur == goal_of(c, cp, 1)) | (cur == goal_of(c, cp, 2)) |
+                         (cur == goal_of(c, cp, 3));
+    const int nsb = fmodp(fdiv(cur, kDist) + 1, c.P);
+#pragma unroll
+    for (int m = 1; m <= 6; ++m) {
+      bool res;
+      if (cur == -1) {
+        res = (m == 6 || (m == 1 && has(F, R_START_ON_1))) && home_ok;
+      } else {
+        const int moved = cur + m;
+        const int fitted = fmodp(moved, kTrack);
+        int x = moved - tgt - mt;
+        res = (b.at(fitted) != cp) || has(F, R_FRIENDLY);
+        const int nsa = fdiv(fitted, kDist);
+        const int nsa_j = jidx(nsa, c.P);
+        const bool trav = cst(c.start, jidx(nsb, c.P)) == cst(c.start, nsa_j);
+        const bool pos_a = pos[0] & (nsa_j == 0) | pos[1] & (nsa_j == 1) | pos[2] & (nsa_j == 2) | pos[3] & (nsa_j == 3);
+        if (has(F, R_START_BLOCK) && trav) res = (!pos_a || cur == start_cp) && res;
+        if (mt && has(F, R_START_BLOCK) && trav && pos_a) x = 0;
+        if (!has(F, R_CIRCULAR) && cur <= tgt && (x > 4 || (x == 0 && mt))) res = false;
+        if (4 >= x && x > 0 && cur <= tgt) {
+          const bool A = has(F, R_CIRCULAR) && res;
+          const bool B = b.at(goal_of(c, cp, jidx(x - 1, 4))) != cp;
+          const bool C = has(F, R_JUMP_GOAL) || goal_path_free(c, b, cp, -1, x);
+          res = A || (B && C);
+        }
+        if (in_goal) {
+          const bool D = has(F, R_JUMP_GOAL) || goal_path_free(c, b, cp, cur - g0, moved - g0 + 1);
+          res = (moved <= g3) && (b.at(jidx(moved, kCells)) != cp) && D;
+        }
+      }
+      if (res) mask |= 1u << (i * 6 + (m - 1));
+    }
+  }
+  // & valid_actions (action_set > 0) per move column
+  uint32_t col = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) col |= avail << (i * 6);
+  return mask & col;
+}
+
+// set_pins_on_board (deterministic_madn.py:259-271) into the lane's LDS board.
+__device__ __forceinline__ void rebuild_board(const DetConsts& c, const DetLane& s, const BoardView& b) {
+  for (int cell = 0; cell < kCells; ++cell) b.set(cell, -1);
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (p < c.P) {
+        const int pos = s.pins[p * 4 + k];
+        if (pos >= 0 && pos < kCells) b.set(pos, p);
+      }
+}
+
+// env_step (deterministic_madn.py:170-257) with (pin, move).  Updates s and the LDS board.
+// Returns the reward; s.done / s.reward / s.cp updated like the reference.
+__device__ __forceinline__ int det_step(const DetConsts& c, DetLane& s, const BoardView& b, int pin, int move) {
+  const uint32_t F = c.flags;
+  const int player_id = s.cp;
+  const int cp = sub_player(c, b, player_id);
+  const uint32_t legal = det_legal(c, s, b);
+  const int mi = jidx(move - 1, 6);
+  const int pi = jidx(pin, 4);
+  const bool invalid = ((legal >> (pi * 6 + mi)) & 1u) == 0u;
+  const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
+  const int tgt = cst(c.target, cp);
+  const int g0 = goal_of(c, cp, 0);
+  const int cur = pin_of(s, cp, pi);
+  const int moved = cur + move;
+  const int fitted = fmodp(moved, kTrack);
+  const int x = moved - tgt - mt;
+  const bool in_goal = (cur == g0) | (cur == goal_of(c, cp, 1)) | (cur == goal_of(c, cp, 2)) |
+                       (cur == goal_of(c, cp, 3));
+  const bool a = in_goal ? goal_path_free(c, b, cp, cur - g0, moved - g0 + 1) : goal_path_free(c, b, cp, -1, x);
+  const int gx = goal_of(c, cp, jidx(x - 1, 4));
+  const bool A = (b.at(gx) != cp) && (has(F, R_JUMP_GOAL) || a);
+  int new_pos;
+  if (cur == -1)
+    new_pos = cst(c.start, cp);
+  else if (in_goal)
+    new_pos = moved;
+  else if (4 >= x && x > 0 && A && cur <= tgt)
+    new_pos = gx;
+  else
+    new_pos = fitted;
+  const int pin_at = b.at(jidx(new_pos, kCells));
+  if (!invalid) {
+    if (pin_at != -1 && (pin_at != cp || has(F, R_FRIENDLY))) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (q == pin_at && s.pins[q * 4 + k] == new_pos) s.pins[q * 4 + k] = -1;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j == cp * 4 + pi) s.pins[j] = new_pos;
+    rebuild_board(c, s, b);
+  }
+  // action set: decrement [cp, move-1]; if the row empties, refill row current_player of the
+  // PRE-step set (refill_action_set, lines 235-240 + 281).
+  const int curr = aset_of(s, cp, mi);
+  const int nv = (invalid || curr == 0) ? curr : curr - 1;
+  bool row_empty = true;
+#pragma unroll
+  for (int m = 0; m < 6; ++m) row_empty &= ((m == mi) ? nv : aset_of(s, cp, m)) == 0;
+  if (row_empty) {
+#pragma unroll
+    for (int j = 0; j < 24; ++j)
+      if (j / 6 == player_id) s.aset[j] = 4;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 24; ++j)
+      if (j == cp * 6 + mi) s.aset[j] = nv;
+  }
+  const uint32_t w = winners(c, b);
+  const int reward = s.done ? 0 : (invalid ? -1 : (int)((w >> cp) & 1u));
+  const int done = (s.done || w != 0u) ? 1 : 0;
+  s.cp = (done || (has(F, R_BONUS_6) && move == 6)) ? player_id : (player_id + 1) % c.P;
+  s.done = done;
+  s.reward = reward;
+  return reward;
+}
+
+// no_step (deterministic_madn.py:283-297).
+__device__ __forceinline__ void det_nostep(const DetConsts& c, DetLane& s) {
+#pragma unroll
+  for (int j = 0; j < 24; ++j)
+    if (j / 6 == s.cp) s.aset[j] = 4;
+  s.cp = (s.cp + 1) % c.P;
+}
+
+// ---- SoA load / store -----------------------------------------------------------------
+__device__ __forceinline__ void det_load(const DetConsts& c, const muz_detmadn_soa& st, int g, DetLane& s,
+                                         const BoardView& b) {
+  const int S = st.stride;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int v = st.pins[min(j, c.P * 4 - 1) * S + g];
+    s.pins[j] = (j < c.P * 4) ? v : -1;
+  }
+#pragma unroll
+  for (int j = 0; j < 24; ++j) {
+    const int v = st.action_set[min(j, c.P * 6 - 1) * S + g];
+    s.aset[j] = (j < c.P * 6) ? v : 0;
+  }
+  s.cp = st.current_player[g];
+  s.done = st.done[g] ? 1 : 0;
+  s.reward = st.reward[g];
+  for (int cell = 0; cell < kCells; ++cell) b.set(cell, st.board[cell * S + g]);
+}
+
+__device__ __forceinline__ void det_store(const DetConsts& c, const muz_detmadn_soa& st, int g, const DetLane& s,
+                                          const BoardView& b, bool board_dirty) {
+  const int S = st.stride;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (j < c.P * 4) st.pins[j * S + g] = (int8_t)s.pins[j];
+#pragma unroll
+  for (int j = 0; j < 24; ++j)
+    if (j < c.P * 6) st.action_set[j * S + g] = (int8_t)s.aset[j];
+  st.current_player[g] = (int8_t)s.cp;
+  st.done[g] = (uint8_t)s.done;
+  st.reward[g] = (int8_t)s.reward;
+  if (board_dirty)
+    for (int cell = 0; cell < kCells; ++cell) st.board[cell * S + g] = (int8_t)b.at(cell);
+}
+
+// encode_board value of channel ch at cell w (deterministic_madn.py:395-438).
+// C = P + 2 + P + 6P; board cell lookups go through `cell_owner(src)`.
+template <class CellFn>
+__device__ __forceinline__ int det_encode_value(const DetConsts& c, const DetLane& s, int ch, int w,
+                                                CellFn cell_owner) {
+  const int P = c.P, cp = s.cp;
+  const int src = (w < kTrack) ? fmodp(w + kDist * cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * cp, 16);
+  const int v = cell_owner(src);
+  auto rolled = [&](int i) { return (i + cp) % P; };
+  if (ch < P) return v == rolled(ch) ? 1 : 0;
+  if (ch == P) {  // team channel
+    if (has(c.flags, R_TEAMS)) return (v == rolled(0) ? 1 : 0) + (v == rolled(2) ? 1 : 0);
+    return v == rolled(0) ? 1 : 0;
+  }
+  if (ch == P + 1) {  // opponent channel
+    if (has(c.flags, R_TEAMS)) return (v == rolled(1) ? 1 : 0) + (v == rolled(3) ? 1 : 0);
+    int n = 0;
+    for (int i = 1; i < P; ++i) n += (v == rolled(i)) ? 1 : 0;
+    return n;
+  }
+  if (ch < 2 * P + 2) {  // pins at home of rolled player
+    const int p = rolled(ch - P - 2);
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) n += (pin_of(s, p, k) == -1) ? 1 : 0;
+    return n;
+  }
+  const int a = ch - (2 * P + 2);
+  return aset_of(s, rolled(a / 6), a % 6);
+}
+
+}  // namespace muz

@@ -1,0 +1,65 @@
+"""The CPU oracle against the reference's own golden step vectors (CPU only)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import detmadn as dm
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+DET_CASES = _load("detmadn_step_cases.json")
+
+
+def det_env_from_case(c):
+    """MADN/test.py:932-944: env_reset(2 players) + replace(pins, board, current_player)."""
+    r = c["rules"]
+    pins = np.array(c["pins"], dtype=np.int8)
+    env = dm.env_reset(num_players=len(pins), distance=10,
+                       enable_circular_board=r["enable_circular_board"],
+                       enable_jump_in_goal_area=r["enable_jump_in_goal_area"],
+                       enable_start_blocking=r["enable_start_blocking"],
+                       enable_friendly_fire=r["enable_friendly_fire"],
+                       enable_start_on_1=r.get("enable_start_on_1", False),
+                       must_traverse_start=r.get("must_traverse_start", False))
+    return env.replace(pins=pins, board=dm.set_pins_on_board(env.board, pins), current_player=c["player"])
+
+
+@pytest.mark.parametrize("case", DET_CASES, ids=[c["source"] for c in DET_CASES])
+def test_oracle_detmadn_golden(case):
+    env = det_env_from_case(case)
+    env2, reward, done = dm.env_step(env, (case["pin"], case["move"]))
+    assert np.array_equal(env2.pins, np.array(case["expected_valid"]))
+
+
+def test_oracle_detmadn_reset_selfplay_rules():
+    env = dm.env_reset(num_players=4, distance=10, starting_player=0, **dm.SELFPLAY_RULES)
+    assert env.rules["enable_teams"]
+    assert env.pins[:, 0].tolist() == [0, 10, 20, 30]
+    assert env.board[[0, 10, 20, 30]].tolist() == [0, 1, 2, 3]
+    assert env.target.tolist() == [39, 9, 19, 29]
+    obs = dm.encode_board(env)
+    assert obs.shape == (34, 56)
+    env2 = dm.env_reset(num_players=2, **dm.SELFPLAY_RULES)
+    assert not env2.rules["enable_teams"]          # forced off below 4 players (line 67)
+    assert env2.start.tolist() == [0, 10]           # layout fix-up (lines 70-74)
+    assert dm.encode_board(env2).shape == (18, 56)
+
+
+def test_oracle_detmadn_refill_quirk():
+    """deterministic_madn.py:235-240: refilling restores the PRE-step set, row = current player."""
+    env = dm.env_reset(num_players=2, enable_circular_board=False, enable_start_on_1=True)
+    aset = np.zeros((2, 6), np.int8)
+    aset[0, 5] = 1
+    pins = np.array([[5, -1, -1, -1], [-1, -1, -1, -1]], np.int8)
+    env = env.replace(pins=pins, board=dm.set_pins_on_board(env.board, pins), action_set=aset)
+    env2, r, d = dm.env_step(env, (0, 6))
+    assert r == 0 and env2.pins[0, 0] == 11
+    assert env2.action_set[0].tolist() == [4] * 6 and env2.current_player == 0   # bonus turn on 6
