@@ -1,0 +1,221 @@
+// MuZero network kernels: root_inference_fn and recurrent_inference_fn
+// (MuZero_det_MADN/muzero_deterministic_madn.py:621-661) as fused fp32 MFMA kernels.
+#include "nn.hpp"
+
+namespace muz {
+
+// ---------------------------------------------------------------------------------------------------
+// RepresentationNetwork2 spatial stream (lines 86-104): 3 x (Conv1D SAME -> LayerNorm -> ReLU) per game.
+// One game per workgroup; conv1/conv2 are implicit GEMMs on MFMA: the zero-padded input [W+k-1][Cin]
+// is read as a Toeplitz matrix A[w][dk*Cin+ci] = in[(w+dk)*Cin+ci], waves own 16-position row tiles.
+constexpr int kConvRowsPad = 64;          // 56 positions padded to 4 MFMA row tiles
+constexpr int kPreLd = 64 + 4;
+
+// LayerNorm over channels for 56 positions, 4 lanes per position.
+template <int N>
+__device__ __forceinline__ void ln_positions(const float* pre, float* out, int out_row0, const muz_ln& P) {
+  const int pos = threadIdx.x >> 2, q = threadIdx.x & 3;
+  if (pos >= 56) return;
+  constexpr int PER = N / 4;
+  float v[PER], s = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = pre[pos * kPreLd + q + 4 * i];
+    s += v[i];
+    s2 += v[i] * v[i];
+  }
+  s += __shfl_xor(s, 1, 4);
+  s += __shfl_xor(s, 2, 4);
+  s2 += __shfl_xor(s2, 1, 4);
+  s2 += __shfl_xor(s2, 2, 4);
+  const float mean = s / (float)N, mean2 = s2 / (float)N;
+  const float inv = 1.0f / sqrtf(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = q + 4 * i;
+    out[(out_row0 + pos) * N + c] = fmaxf((v[i] - mean) * (inv * P.scale[c]) + P.bias[c], 0.f);
+  }
+}
+
+template <int KB>
+__device__ __forceinline__ void conv_mfma(const muz_dense& L, const float* in, int cin, float* pre) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mfma_rows16<4>(L.w, KB, in + (wv * 16) * cin, cin, acc);
+  const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int col = t * 16 + r;
+    const float bb = L.b[col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pre[(wv * 16 + 4 * g + i) * kPreLd + col] = acc[t][i] + bb;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w R, const float* __restrict__ obs, int C, int n,
+                                                   float* __restrict__ convout) {
+  __shared__ __attribute__((aligned(16))) float in0[58 * 6];
+  __shared__ __attribute__((aligned(16))) float c1in[66 * 32];
+  __shared__ __attribute__((aligned(16))) float pre[kConvRowsPad * kPreLd];
+  __shared__ __attribute__((aligned(16))) float c2in[68 * 64];
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* o = obs + (size_t)g * C * 56;
+  for (int i = tid; i < 58 * 6; i += 256) {
+    const int w = i / 6 - 1, ch = i % 6;
+    in0[i] = (w >= 0 && w < 56) ? o[ch * 56 + w] : 0.f;
+  }
+  for (int i = tid; i < 66 * 32; i += 256) c1in[i] = 0.f;
+  for (int i = tid; i < 68 * 64; i += 256) c2in[i] = 0.f;
+  __syncthreads();
+  // Conv_0 (K = 3*6 = 18, N = 32) on VALU
+  for (int i = tid; i < 56 * 32; i += 256) {
+    const int w = i >> 5, co = i & 31;
+    float s = 0.f;
+#pragma unroll
+    for (int dk = 0; dk < 3; ++dk)
+#pragma unroll
+      for (int ci = 0; ci < 6; ++ci) s += in0[(w + dk) * 6 + ci] * R.conv0.w[(dk * 6 + ci) * 32 + co];
+    pre[w * kPreLd + co] = s + R.conv0.b[co];
+  }
+  __syncthreads();
+  ln_positions<32>(pre, c1in, 1, R.ln0);   // pad 1 row on each side for k=3
+  __syncthreads();
+  conv_mfma<6>(R.conv1, c1in, 32, pre);     // K = 3*32 = 96
+  __syncthreads();
+  ln_positions<64>(pre, c2in, 2, R.ln1);   // pad 2 rows for k=5
+  __syncthreads();
+  conv_mfma<20>(R.conv2, c2in, 64, pre);    // K = 5*64 = 320
+  __syncthreads();
+  ln_positions<64>(pre, c2in, 0, R.ln2);   // reuse c2in rows 0..55 as the flattened output
+  __syncthreads();
+  float* dst = convout + (size_t)g * 3584;
+  for (int i = tid; i < 3584; i += 256) dst[i] = c2in[i];   // flatten (w, ch) -> w*64 + ch
+}
+
+// Rest of RepresentationNetwork2 + PredictionNetwork4 on 16-game tiles.
+__global__ __launch_bounds__(256) void k_root_dense(muz_net_w Wt, const float* __restrict__ obs,
+                                                    const float* __restrict__ convout, int n, float* prior_logits,
+                                                    float* value, float* embedding) {
+  __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
+  const Arena a = Arena::carve(smem);
+  const muz_repr_w& R = Wt.repr;
+  const int C = Wt.obs_channels, A = Wt.num_actions;
+  const int g0 = blockIdx.x * kRows;
+  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int gr = g0 + row;
+  const bool valid = gr < n;
+  // global stream input: x[:, 6:, 0]
+  const int Kg = C - 6;
+  for (int c = sub; c < 32; c += 16) a.E[row * LDE + c] = (valid && c < Kg) ? obs[((size_t)gr * C + 6 + c) * 56] : 0.f;
+  // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16)
+  dense16<4>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW);
+  __syncthreads();
+  ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, R.ln3);
+  dense16<1>(R.d1, Kg, 64, a.E, LDE, a.X, LD);
+  __syncthreads();
+  ln16<64, LN_RELU>(a.X, LD, a.X, LD, R.ln4);
+  __syncthreads();
+  dense16<1>(R.d2, 64, 64, a.X, LD, a.W + 256, LDW);
+  __syncthreads();
+  ln16<64, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, R.ln5);
+  __syncthreads();
+  dense16<4>(R.d3, 320, LAT, a.W, LDW, a.X, LD);
+  __syncthreads();
+  ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, R.ln6);
+  __syncthreads();
+#pragma unroll 1
+  for (int b = 0; b < 6; ++b) resblock16(R.rb[b], a.X, a.T, a.U);
+  dense16<4>(R.d4, LAT, LAT, a.X, LD, a.T, LD);
+  __syncthreads();
+  minmax16(a.T, LD);
+  __syncthreads();
+  if (valid)
+    for (int c = sub; c < LAT; c += 16) embedding[(size_t)gr * LAT + c] = a.T[row * LD + c];
+  __syncthreads();
+  pred16(Wt.pred, A, a.T, a);
+  if (valid) {
+    for (int c = sub; c < A; c += 16) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
+    if (sub == 0) value[gr] = a.v0[row];
+  }
+}
+
+// recurrent_inference_fn on 16-row tiles.
+__global__ __launch_bounds__(256) void k_recurrent(muz_net_w Wt, const int32_t* __restrict__ action,
+                                                   const float* __restrict__ emb, int n, float* reward,
+                                                   float* discount, float* prior_logits, float* value,
+                                                   float* next_emb) {
+  __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
+  __shared__ int act[kRows];
+  const Arena a = Arena::carve(smem);
+  const int A = Wt.num_actions;
+  const int g0 = blockIdx.x * kRows;
+  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int gr = g0 + row;
+  const bool valid = gr < n;
+  for (int c = sub; c < LAT; c += 16) a.L[row * LD + c] = valid ? emb[(size_t)gr * LAT + c] : 0.f;
+  if (sub == 0) act[row] = valid ? action[gr] : 0;
+  __syncthreads();
+  dyn16(Wt.dyn, A, act, a);
+  if (valid) {
+    for (int c = sub; c < LAT; c += 16) next_emb[(size_t)gr * LAT + c] = a.T[row * LD + c];
+    if (sub == 0) {
+      reward[gr] = a.v1[row];
+      discount[gr] = a.v2[row];
+    }
+  }
+  __syncthreads();
+  pred16(Wt.pred, A, a.T, a);
+  if (valid) {
+    for (int c = sub; c < A; c += 16) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
+    if (sub == 0) value[gr] = a.v0[row];
+  }
+}
+
+int check_net(const muz_net_w* w) {
+  if (!w) return MUZ_E_INVALID;
+  if (w->num_actions != MUZ_DET_ACTIONS) return MUZ_E_UNSUPPORTED;
+  if (w->obs_channels < 7 || w->obs_channels > 38) return MUZ_E_UNSUPPORTED;
+  return MUZ_OK;
+}
+
+}  // namespace muz
+
+using namespace muz;
+
+extern "C" {
+
+int64_t muz_nets_root_scratch_bytes(int32_t n) {
+  const int64_t rows = ((int64_t)n + kRows - 1) / kRows * kRows;
+  return rows * 3584 * (int64_t)sizeof(float);
+}
+
+int muz_nets_root(const muz_net_w* w, const float* obs, int32_t n, void* scratch, float* prior_logits, float* value,
+                  float* embedding, void* stream) {
+  int rc = check_net(w);
+  if (rc) return rc;
+  MUZ_HOST_CHECK(n >= 0 && obs && scratch && prior_logits && value && embedding);
+  if (n == 0) return MUZ_OK;
+  hipStream_t s = (hipStream_t)stream;
+  float* conv = (float*)scratch;
+  k_repr_conv<<<n, 256, 0, s>>>(w->repr, obs, w->obs_channels, n, conv);
+  rc = muz_last_launch_error();
+  if (rc) return rc;
+  k_root_dense<<<(n + kRows - 1) / kRows, 256, 0, s>>>(*w, obs, conv, n, prior_logits, value, embedding);
+  return muz_last_launch_error();
+}
+
+int muz_nets_recurrent(const muz_net_w* w, const int32_t* action, const float* embedding, int32_t n, float* reward,
+                       float* discount, float* prior_logits, float* value, float* next_embedding, void* stream) {
+  int rc = check_net(w);
+  if (rc) return rc;
+  MUZ_HOST_CHECK(n >= 0 && action && embedding && reward && discount && prior_logits && value && next_embedding);
+  if (n == 0) return MUZ_OK;
+  k_recurrent<<<(n + kRows - 1) / kRows, 256, 0, (hipStream_t)stream>>>(*w, action, embedding, n, reward, discount,
+                                                                         prior_logits, value, next_embedding);
+  return muz_last_launch_error();
+}
+
+}  // extern "C"

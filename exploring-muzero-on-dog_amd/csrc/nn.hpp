@@ -1,0 +1,304 @@
+// Fused fp32 MLP building blocks for 16-row tiles on CDNA4 MFMA (v_mfma_f32_16x16x4_f32).
+//
+// A workgroup of 4 waves owns a tile of 16 rows (games).  Activations live in LDS
+// ([16][ld] fp32 rows); a dense layer out = A[16][K] @ W[K][N] + b splits its N columns over the
+// 4 waves (NT 16-column tiles each).  Per 16-deep k-block a lane reads ONE float4 of A from
+// LDS (row lane&15, k = kb*16 + 4*(lane>>4) + j, j = 0..3) and NT float4 of pre-packed weights
+// straight from global memory (L2/MALL resident, streamed once per tile), then issues 4*NT
+// MFMAs.  The f32-input MFMA is an exact k-ordered fma chain, so only the reduction order
+// differs from the fp32 reference.  Row-wise ops (LayerNorm, min-max) use 16 lanes per row.
+#pragma once
+#include "common.hpp"
+
+namespace muz {
+
+constexpr int kRows = 16;
+constexpr int kWaves = 4;
+constexpr int kThreads = kRows * 16;   // 256
+constexpr int LAT = 256;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// acc[t] += A[16 rows][K] @ Wgroup[K][NT*16]  (KB = K/16 k-blocks; Wg = packed weights of this group)
+template <int NT>
+__device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB, const float* A, int lda,
+                                            f32x4 (&acc)[NT]) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const f32x4* wp = reinterpret_cast<const f32x4*>(Wg) + lane * NT;
+  const int wstep = 64 * NT;   // f32x4 per k-block
+  const float* ap = A + r * lda + 4 * g;
+  f32x4 b0[NT], b1[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) b0[t] = wp[t];
+  for (int kb = 0; kb < KB; kb += 2) {
+    const bool has1 = kb + 1 < KB;
+    if (has1) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b1[t] = wp[(kb + 1) * wstep + t];
+    }
+    f32x4 a = *reinterpret_cast<const f32x4*>(ap + kb * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[j], b0[t][j], acc[t]);
+    if (has1) {
+      if (kb + 2 < KB) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) b0[t] = wp[(kb + 2) * wstep + t];
+      }
+      a = *reinterpret_cast<const f32x4*>(ap + (kb + 1) * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[j], b1[t][j], acc[t]);
+    }
+  }
+}
+
+// Dense layer over the tile: out[16][N] = A @ W + b, waves split N (NT tiles of 16 columns each).
+// A may live in LDS or global memory.  Caller synchronises before/after.
+template <int NT>
+__device__ __forceinline__ void dense16(const muz_dense& L, int K, int N, const float* A, int lda, float* out,
+                                        int ldo) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int KB = (K + 15) >> 4;
+  const int col0 = wv * NT * 16;
+  if (col0 >= N) return;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mfma_rows16<NT>(L.w + (size_t)wv * KB * 64 * NT * 4, KB, A, lda, acc);
+  const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = col0 + t * 16 + r;
+    if (col < N) {
+      const float bb = L.b[col];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[(4 * g + i) * ldo + col] = acc[t][i] + bb;
+    }
+  }
+}
+
+// ---- row-wise ops: thread t -> row t>>4, lane-in-row t&15 -----------------------------------------
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __shfl_xor(v, 8, 16);
+  v += __shfl_xor(v, 4, 16);
+  v += __shfl_xor(v, 2, 16);
+  v += __shfl_xor(v, 1, 16);
+  return v;
+}
+__device__ __forceinline__ float row_max16(float v) {
+  v = fmaxf(v, __shfl_xor(v, 8, 16));
+  v = fmaxf(v, __shfl_xor(v, 4, 16));
+  v = fmaxf(v, __shfl_xor(v, 2, 16));
+  v = fmaxf(v, __shfl_xor(v, 1, 16));
+  return v;
+}
+__device__ __forceinline__ float row_min16(float v) {
+  v = fminf(v, __shfl_xor(v, 8, 16));
+  v = fminf(v, __shfl_xor(v, 4, 16));
+  v = fminf(v, __shfl_xor(v, 2, 16));
+  v = fminf(v, __shfl_xor(v, 1, 16));
+  return v;
+}
+
+enum LnMode { LN_PLAIN = 0, LN_RELU = 1, LN_RESID_RELU = 2 };
+
+// Flax LayerNorm (eps 1e-6, fast variance) of in[16][N] -> out.
+//   LN_PLAIN: out = y;  LN_RELU: out = relu(y);  LN_RESID_RELU: out = relu(out + y)  (ResBlock tail)
+template <int N, int MODE>
+__device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int ldo, const muz_ln& P) {
+  constexpr int PER = N / 16;
+  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  float v[PER];
+  float s = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = in[row * ldi + sub + 16 * i];
+    s += v[i];
+    s2 += v[i] * v[i];
+  }
+  s = row_sum16(s);
+  s2 = row_sum16(s2);
+  const float mean = s / (float)N;
+  const float mean2 = s2 / (float)N;
+  const float var = fmaxf(0.f, mean2 - mean * mean);
+  const float inv = 1.0f / sqrtf(var + 1e-6f);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = sub + 16 * i;
+    float y = (v[i] - mean) * (inv * P.scale[c]) + P.bias[c];
+    if (MODE == LN_RELU) y = fmaxf(y, 0.f);
+    if (MODE == LN_RESID_RELU) y = fmaxf(out[row * ldo + c] + y, 0.f);
+    out[row * ldo + c] = y;
+  }
+}
+
+// x <- (x - min) / (max - min + 1e-8) per row of 256 (Repr2 139-140, Dyn4 435-437).
+__device__ __forceinline__ void minmax16(float* buf, int ld) {
+  constexpr int PER = LAT / 16;
+  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  float v[PER];
+  float lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = buf[row * ld + sub + 16 * i];
+    lo = fminf(lo, v[i]);
+    hi = fmaxf(hi, v[i]);
+  }
+  lo = row_min16(lo);
+  hi = row_max16(hi);
+  const float den = hi - lo + 1e-8f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) buf[row * ld + sub + 16 * i] = (v[i] - lo) / den;
+}
+
+__device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
+  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  for (int c = sub; c < n; c += 16) buf[row * ld + col0 + c] = fmaxf(buf[row * ld + col0 + c], 0.f);
+}
+
+// ---- LDS arena of a 16-row tile ---------------------------------------------------------------------
+constexpr int LD = LAT + 4;      // 260: row stride of 256-wide buffers (keeps b128 reads 16B aligned)
+constexpr int LDW = 512 + 4;     // wide buffer (FiLM scale|shift 512, pred heads 384, concat 320)
+constexpr int LDE = 64 + 4;      // small buffer (action embed, global features)
+constexpr int kArenaFloats = 4 * kRows * LD + kRows * LDW + kRows * LDE + 4 * kRows;
+
+struct Arena {
+  float* L;   // latent input (parent embedding)           [16][LD]
+  float* X;   // working activation                        [16][LD]
+  float* T;   // scratch / next latent                     [16][LD]
+  float* U;   // scratch / pred heads                      [16][LD]
+  float* W;   // wide scratch                              [16][LDW]
+  float* E;   // small scratch                             [16][LDE]
+  float* v0;  // per-row scalars: value                    [16]
+  float* v1;  // reward                                    [16]
+  float* v2;  // discount                                  [16]
+  float* v3;  // spare                                     [16]
+  __device__ static Arena carve(float* base) {
+    Arena a;
+    a.L = base;
+    a.X = a.L + kRows * LD;
+    a.T = a.X + kRows * LD;
+    a.U = a.T + kRows * LD;
+    a.W = a.U + kRows * LD;
+    a.E = a.W + kRows * LDW;
+    a.v0 = a.E + kRows * LDE;
+    a.v1 = a.v0 + kRows;
+    a.v2 = a.v1 + kRows;
+    a.v3 = a.v2 + kRows;
+    return a;
+  }
+};
+
+// ResBlock (muzero_deterministic_madn.py:12-24): X <- relu(X + LN1(D1(relu(LN0(D0(X))))))
+__device__ __forceinline__ void resblock16(const muz_resblock& R, float* X, float* T, float* U) {
+  dense16<4>(R.d0, LAT, LAT, X, LD, T, LD);
+  __syncthreads();
+  ln16<LAT, LN_RELU>(T, LD, T, LD, R.ln0);
+  __syncthreads();
+  dense16<4>(R.d1, LAT, LAT, T, LD, U, LD);
+  __syncthreads();
+  ln16<LAT, LN_RESID_RELU>(U, LD, X, LD, R.ln1);
+  __syncthreads();
+}
+
+// small dot head: out[row] = b + sum_k in[row][k] * w[k][col] for one column (16 lanes per row)
+__device__ __forceinline__ float head_dot16(const float* in, int ld, int K, const float* w, int ncol, int col,
+                                            float b) {
+  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  float s = 0.f;
+  for (int k = sub; k < K; k += 16) s += in[row * ld + k] * w[k * ncol + col];
+  return row_sum16(s) + b;
+}
+
+// PredictionNetwork4 (muzero_deterministic_madn.py:549-583) on the latent in `lat` ([16][LD]).
+// Leaves policy logits in a.U[:, 0:A] and tanh value in a.v0.  Clobbers X, T, U, W.
+__device__ __forceinline__ void pred16(const muz_pred_w& P, int A, const float* lat, const Arena& a) {
+  ln16<LAT, LN_PLAIN>(lat, LD, a.X, LD, P.ln0);
+  __syncthreads();
+  resblock16(P.rb[0], a.X, a.T, a.U);
+  resblock16(P.rb[1], a.X, a.T, a.U);
+  dense16<6>(P.d03, LAT, 384, a.X, LD, a.W, LDW);     // [policy Dense_0 | value Dense_3]
+  __syncthreads();
+  ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, P.ln1);
+  ln16<128, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, P.ln3);
+  __syncthreads();
+  dense16<2>(P.d1, LAT, 128, a.W, LDW, a.T, LD);      // policy Dense_1
+  dense16<1>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD);  // value Dense_4 (X is free now)
+  __syncthreads();
+  ln16<128, LN_RELU>(a.T, LD, a.T, LD, P.ln2);
+  relu16(a.X, LD, 0, 64);
+  __syncthreads();
+  dense16<1>(P.d2, 128, A, a.T, LD, a.U, LD);         // policy logits
+  {
+    const float v = head_dot16(a.X, LD, 64, P.d5.w, 1, 0, P.d5.b[0]);
+    if ((threadIdx.x & 15) == 0) a.v0[threadIdx.x >> 4] = tanhf(v);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) {
+  // sum(softmax(l) * [-1, 0, 1])  (recurrent_inference_fn 648-653)
+  const float m = fmaxf(fmaxf(l0, l1), l2);
+  const float e0 = expf(l0 - m), e1 = expf(l1 - m), e2 = expf(l2 - m);
+  const float z = e0 + e1 + e2;
+  return (e0 / z) * -1.0f + (e1 / z) * 0.0f + (e2 / z) * 1.0f;
+}
+
+// DynamicsNetwork4 (muzero_deterministic_madn.py:391-457): latent a.L, action per row in act[16].
+// Leaves the next latent in a.T, reward / discount expectations in a.v1 / a.v2.  Clobbers X, U, W, E.
+__device__ __forceinline__ void dyn16(const muz_dyn_w& D, int A, const int* act, const Arena& a) {
+  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int ar = act[row];
+  const bool oh = ar >= 0 && ar < A;   // jax.nn.one_hot: out-of-range -> zero row
+  // action embedding: relu(one_hot @ W0 + b0) == relu(W0[a] + b0)
+  for (int c = sub; c < 64; c += 16) a.E[row * LDE + c] = fmaxf((oh ? D.d0.w[ar * 64 + c] : 0.f) + D.d0.b[c], 0.f);
+  ln16<LAT, LN_PLAIN>(a.L, LD, a.X, LD, D.ln0);
+  __syncthreads();
+  dense16<8>(D.d12, 64, 512, a.E, LDE, a.W, LDW);     // [scale | shift]
+  __syncthreads();
+  for (int c = sub; c < LAT; c += 16)
+    a.X[row * LD + c] = a.X[row * LD + c] * (1.0f + a.W[row * LDW + c]) + a.W[row * LDW + 256 + c];
+  __syncthreads();
+  dense16<4>(D.d3, LAT, LAT, a.X, LD, a.T, LD);
+  __syncthreads();
+  ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, D.ln1);
+  __syncthreads();
+  dense16<4>(D.d4, LAT, LAT, a.T, LD, a.X, LD);
+  __syncthreads();
+  ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, D.ln2);
+  __syncthreads();
+  resblock16(D.rb[0], a.X, a.T, a.U);
+  resblock16(D.rb[1], a.X, a.T, a.U);
+  dense16<4>(D.d5, LAT, LAT, a.X, LD, a.T, LD);
+  __syncthreads();
+  for (int c = sub; c < LAT; c += 16) a.T[row * LD + c] = a.L[row * LD + c] + a.T[row * LD + c];
+  __syncthreads();
+  minmax16(a.T, LD);
+  __syncthreads();
+  dense16<2>(D.d67, LAT, 128, a.T, LD, a.W, LDW);     // [reward hidden | discount hidden] latent rows
+  __syncthreads();
+  for (int c = sub; c < 128; c += 16)
+    a.W[row * LDW + c] = fmaxf(a.W[row * LDW + c] + (oh ? D.d67_onehot[ar * 128 + c] : 0.f), 0.f);
+  __syncthreads();
+  float rl[3], dl[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    rl[j] = head_dot16(a.W, LDW, 64, D.reward_head.w, 3, j, D.reward_head.b[j]);
+    dl[j] = head_dot16(a.W + 64, LDW, 64, D.discount_head.w, 3, j, D.discount_head.b[j]);
+  }
+  if (sub == 0) {
+    a.v1[row] = softmax3_support(rl[0], rl[1], rl[2]);
+    a.v2[row] = softmax3_support(dl[0], dl[1], dl[2]);
+  }
+  __syncthreads();
+}
+
+}  // namespace muz

@@ -50,6 +50,49 @@ class MuzDetSoA(ctypes.Structure):
     ]
 
 
+class MuzDense(ctypes.Structure):
+    _fields_ = [("w", vp), ("b", vp)]
+
+
+class MuzLn(ctypes.Structure):
+    _fields_ = [("scale", vp), ("bias", vp)]
+
+
+class MuzResblock(ctypes.Structure):
+    _fields_ = [("d0", MuzDense), ("ln0", MuzLn), ("d1", MuzDense), ("ln1", MuzLn)]
+
+
+class MuzReprW(ctypes.Structure):
+    _fields_ = [("conv0", MuzDense), ("ln0", MuzLn), ("conv1", MuzDense), ("ln1", MuzLn), ("conv2", MuzDense),
+                ("ln2", MuzLn), ("d0", MuzDense), ("ln3", MuzLn), ("d1", MuzDense), ("ln4", MuzLn),
+                ("d2", MuzDense), ("ln5", MuzLn), ("d3", MuzDense), ("ln6", MuzLn), ("rb", MuzResblock * 6),
+                ("d4", MuzDense)]
+
+
+class MuzDynW(ctypes.Structure):
+    _fields_ = [("d0", MuzDense), ("ln0", MuzLn), ("d12", MuzDense), ("d3", MuzDense), ("ln1", MuzLn),
+                ("d4", MuzDense), ("ln2", MuzLn), ("rb", MuzResblock * 2), ("d5", MuzDense), ("d67", MuzDense),
+                ("d67_onehot", vp), ("reward_head", MuzDense), ("discount_head", MuzDense)]
+
+
+class MuzPredW(ctypes.Structure):
+    _fields_ = [("ln0", MuzLn), ("rb", MuzResblock * 2), ("d03", MuzDense), ("ln1", MuzLn), ("d1", MuzDense),
+                ("ln2", MuzLn), ("d2", MuzDense), ("ln3", MuzLn), ("d4", MuzDense), ("d5", MuzDense)]
+
+
+class MuzNetW(ctypes.Structure):
+    _fields_ = [("obs_channels", ctypes.c_int32), ("num_actions", ctypes.c_int32), ("repr", MuzReprW),
+                ("dyn", MuzDynW), ("pred", MuzPredW)]
+
+
+
+class MuzSearchCfg(ctypes.Structure):
+    _fields_ = [("num_simulations", ctypes.c_int32), ("max_depth", ctypes.c_int32),
+                ("max_num_considered", ctypes.c_int32), ("value_scale", ctypes.c_float),
+                ("maxvisit_init", ctypes.c_float), ("gumbel_scale", ctypes.c_float), ("seed", ctypes.c_uint64),
+                ("turn", ctypes.c_int32)]
+
+
 # name -> (restype, argtypes).  Kept in sync with include/muz.h (tests/test_capi.py checks it).
 SIGNATURES = {
     "muz_version": (ctypes.c_char_p, []),
@@ -62,6 +105,13 @@ SIGNATURES = {
     "muz_detmadn_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
+    "muz_nets_root_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32]),
+    "muz_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, ctypes.c_int32, vp, vp, vp, vp, vp]),
+    "muz_nets_recurrent": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp,
+                                          vp]),
+    "muz_search_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.POINTER(MuzSearchCfg)]),
+    "muz_gumbel_search": (ctypes.c_int, [ctypes.POINTER(MuzNetW), ctypes.POINTER(MuzSearchCfg), vp, vp, vp, vp,
+                                         vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp]),
 }
 
 _lib = None

@@ -1,0 +1,225 @@
+"""MuZero networks of MuZero_det_MADN/muzero_deterministic_madn.py on the GPU.
+
+Host side of the fused fp32 MFMA network kernels (csrc/nets.hip, csrc/nn.hpp):
+  * parameter init / layout follow the Flax module tree (paths such as
+    ``dynamics/ResBlock_0/Dense_1/kernel``), so checkpoints map 1:1 (init_muzero_params,
+    lines 706-748);
+  * ``DeviceNet`` packs the dense kernels into the MFMA B-fragment layout documented in
+    include/muz.h, uploads everything as one device buffer and fills ``muz_net_w``;
+  * ``root_inference_fn`` / ``recurrent_inference_fn`` mirror lines 621-661.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import lib as _L
+from .lib import MuzNetW  # struct layout of include/muz.h
+
+LATENT = 256
+
+
+# ---------------------------------------------------------------------------------- parameters
+def _resblock_shapes(s, pre):
+    for d in range(2):
+        s[f"{pre}/Dense_{d}/kernel"] = (LATENT, LATENT)
+        s[f"{pre}/Dense_{d}/bias"] = (LATENT,)
+        s[f"{pre}/LayerNorm_{d}/scale"] = (LATENT,)
+        s[f"{pre}/LayerNorm_{d}/bias"] = (LATENT,)
+
+
+def param_shapes(obs_channels: int, num_actions: int = 24) -> dict:
+    """Flax parameter tree of (RepresentationNetwork2, DynamicsNetwork4, PredictionNetwork4), flattened."""
+    C, A = obs_channels, num_actions
+    s = {}
+    r = "representation"
+    s[f"{r}/Conv_0/kernel"], s[f"{r}/Conv_0/bias"] = (3, 6, 32), (32,)
+    s[f"{r}/Conv_1/kernel"], s[f"{r}/Conv_1/bias"] = (3, 32, 64), (64,)
+    s[f"{r}/Conv_2/kernel"], s[f"{r}/Conv_2/bias"] = (5, 64, 64), (64,)
+    for i, n in enumerate([32, 64, 64, 256, 64, 64, 256]):
+        s[f"{r}/LayerNorm_{i}/scale"] = s[f"{r}/LayerNorm_{i}/bias"] = (n,)
+    for name, (i, o) in {"Dense_0": (56 * 64, 256), "Dense_1": (C - 6, 64), "Dense_2": (64, 64),
+                         "Dense_3": (320, 256), "Dense_4": (256, 256)}.items():
+        s[f"{r}/{name}/kernel"], s[f"{r}/{name}/bias"] = (i, o), (o,)
+    for b in range(6):
+        _resblock_shapes(s, f"{r}/ResBlock_{b}")
+    d = "dynamics"
+    for name, (i, o) in {"Dense_0": (A, 64), "Dense_1": (64, 256), "Dense_2": (64, 256), "Dense_3": (256, 256),
+                         "Dense_4": (256, 256), "Dense_5": (256, 256), "Dense_6": (256 + A, 64),
+                         "reward_head": (64, 3), "Dense_7": (256 + A, 64), "discount_head": (64, 3)}.items():
+        s[f"{d}/{name}/kernel"], s[f"{d}/{name}/bias"] = (i, o), (o,)
+    for i in range(3):
+        s[f"{d}/LayerNorm_{i}/scale"] = s[f"{d}/LayerNorm_{i}/bias"] = (LATENT,)
+    for b in range(2):
+        _resblock_shapes(s, f"{d}/ResBlock_{b}")
+    p = "prediction"
+    for name, (i, o) in {"Dense_0": (256, 256), "Dense_1": (256, 128), "Dense_2": (128, A), "Dense_3": (256, 128),
+                         "Dense_4": (128, 64), "Dense_5": (64, 1)}.items():
+        s[f"{p}/{name}/kernel"], s[f"{p}/{name}/bias"] = (i, o), (o,)
+    for i, n in enumerate([256, 256, 128, 128]):
+        s[f"{p}/LayerNorm_{i}/scale"] = s[f"{p}/LayerNorm_{i}/bias"] = (n,)
+    for b in range(2):
+        _resblock_shapes(s, f"{p}/ResBlock_{b}")
+    return s
+
+
+def init_muzero_params(seed: int, obs_channels: int, num_actions: int = 24) -> dict:
+    """init_muzero_params (lines 706-748) with Flax defaults: lecun_normal kernels (truncated at 2 std),
+    zero biases, unit LayerNorm scales.  Seeded NumPy draws (jax threefry is not reproduced)."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for k, shp in param_shapes(obs_channels, num_actions).items():
+        if k.endswith("kernel"):
+            fan_in = int(np.prod(shp[:-1]))
+            std = math.sqrt(1.0 / fan_in) / 0.87962566103423978
+            out[k] = (np.clip(rng.standard_normal(shp), -2.0, 2.0) * std).astype(np.float32)
+        elif k.endswith("scale"):
+            out[k] = np.ones(shp, np.float32)
+        else:
+            out[k] = np.zeros(shp, np.float32)
+    return out
+
+
+# ---------------------------------------------------------------------------------- packing
+def pack_dense(W: np.ndarray, nw: int, nt: int) -> np.ndarray:
+    """MFMA 16x16x4 B-fragment packing (layout documented in include/muz.h):
+    out[w][kb][lane][t][j] = W[kb*16 + 4*(lane>>4) + j][(w*nt + t)*16 + (lane&15)]."""
+    W = np.asarray(W, np.float32)
+    K, N = W.shape
+    KB = (K + 15) // 16
+    Np = nw * nt * 16
+    if N > Np:
+        raise ValueError(f"N={N} does not fit {nw} groups x {nt} tiles")
+    Wp = np.zeros((KB * 16, Np), np.float32)
+    Wp[:K, :N] = W
+    arr = Wp.reshape(KB, 4, 4, nw, nt, 16).transpose(3, 0, 1, 5, 4, 2)
+    return np.ascontiguousarray(arr).reshape(-1)
+
+
+class DeviceNet:
+    """Packed device copy of a parameter dict + the ``muz_net_w`` table the kernels read."""
+
+    def __init__(self, params: dict, obs_channels: int, num_actions: int = 24, device="cuda"):
+        self.C, self.A = int(obs_channels), int(num_actions)
+        self._chunks = []
+        self._off = 0
+        P = {k: np.asarray(v, np.float32) for k, v in params.items()}
+        self.params = P
+        put = self._put
+        w = MuzNetW()
+        w.obs_channels, w.num_actions = self.C, self.A
+
+        def dense(name, nw=4, nt=4):
+            return (put(pack_dense(P[f"{name}/kernel"], nw, nt)), put(P[f"{name}/bias"]))
+
+        def ln(name):
+            return (put(P[f"{name}/scale"]), put(P[f"{name}/bias"]))
+
+        def rb(pre):
+            return dict(d0=dense(f"{pre}/Dense_0"), ln0=ln(f"{pre}/LayerNorm_0"), d1=dense(f"{pre}/Dense_1"),
+                        ln1=ln(f"{pre}/LayerNorm_1"))
+
+        r, d, p = "representation", "dynamics", "prediction"
+        spec = {"repr": dict(
+            conv0=(put(P[f"{r}/Conv_0/kernel"]), put(P[f"{r}/Conv_0/bias"])), ln0=ln(f"{r}/LayerNorm_0"),
+            conv1=(put(pack_dense(P[f"{r}/Conv_1/kernel"].reshape(96, 64), 1, 4)), put(P[f"{r}/Conv_1/bias"])),
+            ln1=ln(f"{r}/LayerNorm_1"),
+            conv2=(put(pack_dense(P[f"{r}/Conv_2/kernel"].reshape(320, 64), 1, 4)), put(P[f"{r}/Conv_2/bias"])),
+            ln2=ln(f"{r}/LayerNorm_2"), d0=dense(f"{r}/Dense_0"), ln3=ln(f"{r}/LayerNorm_3"),
+            d1=dense(f"{r}/Dense_1", 4, 1), ln4=ln(f"{r}/LayerNorm_4"), d2=dense(f"{r}/Dense_2", 4, 1),
+            ln5=ln(f"{r}/LayerNorm_5"), d3=dense(f"{r}/Dense_3"), ln6=ln(f"{r}/LayerNorm_6"),
+            rb=[rb(f"{r}/ResBlock_{i}") for i in range(6)], d4=dense(f"{r}/Dense_4"))}
+        A = self.A
+        k6, k7 = P[f"{d}/Dense_6/kernel"], P[f"{d}/Dense_7/kernel"]
+        spec["dyn"] = dict(
+            d0=(put(P[f"{d}/Dense_0/kernel"]), put(P[f"{d}/Dense_0/bias"])), ln0=ln(f"{d}/LayerNorm_0"),
+            d12=(put(pack_dense(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1), 4, 8)),
+                 put(np.concatenate([P[f"{d}/Dense_1/bias"], P[f"{d}/Dense_2/bias"]]))),
+            d3=dense(f"{d}/Dense_3"), ln1=ln(f"{d}/LayerNorm_1"), d4=dense(f"{d}/Dense_4"),
+            ln2=ln(f"{d}/LayerNorm_2"), rb=[rb(f"{d}/ResBlock_{i}") for i in range(2)], d5=dense(f"{d}/Dense_5"),
+            d67=(put(pack_dense(np.concatenate([k6[:LATENT], k7[:LATENT]], 1), 4, 2)),
+                 put(np.concatenate([P[f"{d}/Dense_6/bias"], P[f"{d}/Dense_7/bias"]]))),
+            d67_onehot=put(np.concatenate([k6[LATENT:LATENT + A], k7[LATENT:LATENT + A]], 1)),
+            reward_head=(put(P[f"{d}/reward_head/kernel"]), put(P[f"{d}/reward_head/bias"])),
+            discount_head=(put(P[f"{d}/discount_head/kernel"]), put(P[f"{d}/discount_head/bias"])))
+        spec["pred"] = dict(
+            ln0=ln(f"{p}/LayerNorm_0"), rb=[rb(f"{p}/ResBlock_{i}") for i in range(2)],
+            d03=(put(pack_dense(np.concatenate([P[f"{p}/Dense_0/kernel"], P[f"{p}/Dense_3/kernel"]], 1), 4, 6)),
+                 put(np.concatenate([P[f"{p}/Dense_0/bias"], P[f"{p}/Dense_3/bias"]]))),
+            ln1=ln(f"{p}/LayerNorm_1"), d1=dense(f"{p}/Dense_1", 4, 2), ln2=ln(f"{p}/LayerNorm_2"),
+            d2=dense(f"{p}/Dense_2", 4, 1), ln3=ln(f"{p}/LayerNorm_3"), d4=dense(f"{p}/Dense_4", 4, 1),
+            d5=(put(P[f"{p}/Dense_5/kernel"]), put(P[f"{p}/Dense_5/bias"])))
+        host = np.concatenate(self._chunks) if self._chunks else np.zeros(4, np.float32)
+        self.buffer = torch.from_numpy(host).to(device)
+        base = self.buffer.data_ptr()
+        self._fill(w, spec, base)
+        self.w = w
+
+    def _put(self, arr) -> int:
+        a = np.ascontiguousarray(np.asarray(arr, np.float32).reshape(-1))
+        pad = (-a.size) % 4          # keep every array 16-byte aligned for f32x4 loads
+        if pad:
+            a = np.concatenate([a, np.zeros(pad, np.float32)])
+        off = self._off
+        self._chunks.append(a)
+        self._off += a.size
+        return off
+
+    @staticmethod
+    def _fill(struct, spec, base):
+        def addr(off):
+            return base + 4 * off
+        for name, val in spec.items():
+            field = getattr(struct, name)
+            if isinstance(val, int):
+                setattr(struct, name, addr(val))
+            elif isinstance(val, tuple):
+                field.__setattr__(field._fields_[0][0], addr(val[0]))
+                field.__setattr__(field._fields_[1][0], addr(val[1]))
+            elif isinstance(val, list):
+                for i, sub in enumerate(val):
+                    DeviceNet._fill(field[i], sub, base)
+            elif isinstance(val, dict):
+                DeviceNet._fill(field, val, base)
+            else:
+                raise TypeError(name)
+
+
+# ---------------------------------------------------------------------------------- inference
+def root_inference_fn(net: DeviceNet, observation: torch.Tensor, scratch: torch.Tensor | None = None):
+    """root_inference_fn (lines 621-630): obs [B, C, 56] -> (prior_logits [B, A], value [B], embedding [B, 256])."""
+    lib = _L.load()
+    obs = observation.to(dtype=torch.float32).contiguous()
+    B = obs.shape[0]
+    if obs.shape[1] != net.C or obs.shape[2] != 56:
+        raise ValueError(f"observation shape {tuple(obs.shape)} != (B, {net.C}, 56)")
+    dev = obs.device
+    need = lib.muz_nets_root_scratch_bytes(B)
+    if scratch is None or scratch.numel() * scratch.element_size() < need:
+        scratch = torch.empty(need // 4, dtype=torch.float32, device=dev)
+    logits = torch.empty((B, net.A), dtype=torch.float32, device=dev)
+    value = torch.empty((B,), dtype=torch.float32, device=dev)
+    emb = torch.empty((B, LATENT), dtype=torch.float32, device=dev)
+    _L.check(lib.muz_nets_root(net.w, _L.ptr(obs), B, _L.ptr(scratch), _L.ptr(logits), _L.ptr(value), _L.ptr(emb),
+                               _L.stream_ptr()), "muz_nets_root")
+    return logits, value, emb
+
+
+def recurrent_inference_fn(net: DeviceNet, action: torch.Tensor, embedding: torch.Tensor):
+    """recurrent_inference_fn (lines 632-661) -> (reward, discount, prior_logits, value, next_embedding)."""
+    lib = _L.load()
+    emb = embedding.to(dtype=torch.float32).contiguous()
+    act = action.to(device=emb.device, dtype=torch.int32).contiguous()
+    B = emb.shape[0]
+    dev = emb.device
+    reward = torch.empty((B,), dtype=torch.float32, device=dev)
+    discount = torch.empty((B,), dtype=torch.float32, device=dev)
+    logits = torch.empty((B, net.A), dtype=torch.float32, device=dev)
+    value = torch.empty((B,), dtype=torch.float32, device=dev)
+    nxt = torch.empty((B, LATENT), dtype=torch.float32, device=dev)
+    _L.check(lib.muz_nets_recurrent(net.w, _L.ptr(act), _L.ptr(emb), B, _L.ptr(reward), _L.ptr(discount),
+                                    _L.ptr(logits), _L.ptr(value), _L.ptr(nxt), _L.stream_ptr()),
+             "muz_nets_recurrent")
+    return reward, discount, logits, value, nxt

@@ -94,6 +94,113 @@ int muz_detmadn_nostep(const muz_rules* rules, muz_detmadn_soa state, int8_t* re
 int muz_detmadn_encode_f32(const muz_rules* rules, muz_detmadn_soa state, float* obs, int32_t n, void* stream);
 int muz_detmadn_encode_i8(const muz_rules* rules, muz_detmadn_soa state, int8_t* obs, int32_t n, void* stream);
 
+
+/* ---- MuZero networks (MuZero_det_MADN/muzero_deterministic_madn.py) --------------------------
+ * Dense layers used by the MFMA kernels take their kernel W[K][N] PACKED for
+ * v_mfma_f32_16x16x4_f32 B-fragments: [group][K/16][lane 64][tile NT][j 4] with
+ * element = W[kb*16 + 4*(lane>>4) + j][(group*NT + t)*16 + (lane&15)], zero padded
+ * (exploring-muzero-on-dog_amd/nets.py:pack_dense).  Layers marked "plain" are row-major [K][N].
+ * Biases / LayerNorm scale+bias are plain fp32 vectors. */
+typedef struct muz_dense { const float* w; const float* b; } muz_dense;
+typedef struct muz_ln { const float* scale; const float* bias; } muz_ln;
+typedef struct muz_resblock { muz_dense d0; muz_ln ln0; muz_dense d1; muz_ln ln1; } muz_resblock;
+
+/* RepresentationNetwork2 (lines 75-141) */
+typedef struct muz_repr_w {
+  muz_dense conv0;              /* plain [3][6][32] */
+  muz_ln ln0;
+  muz_dense conv1;              /* packed, 1 group, K=96  N=64 */
+  muz_ln ln1;
+  muz_dense conv2;              /* packed, 1 group, K=320 N=64 */
+  muz_ln ln2;
+  muz_dense d0;                 /* packed 3584 -> 256 */
+  muz_ln ln3;
+  muz_dense d1;                 /* packed (C-6) -> 64 (K zero-padded to 16) */
+  muz_ln ln4;
+  muz_dense d2;                 /* packed 64 -> 64 */
+  muz_ln ln5;
+  muz_dense d3;                 /* packed 320 -> 256 */
+  muz_ln ln6;
+  muz_resblock rb[6];
+  muz_dense d4;                 /* packed 256 -> 256 */
+} muz_repr_w;
+
+/* DynamicsNetwork4 (lines 391-457) */
+typedef struct muz_dyn_w {
+  muz_dense d0;                 /* plain [A][64]: one_hot(action) @ W = row gather */
+  muz_ln ln0;
+  muz_dense d12;                /* packed, Dense_1 | Dense_2 fused: 64 -> 512 (FiLM scale | shift) */
+  muz_dense d3;
+  muz_ln ln1;
+  muz_dense d4;
+  muz_ln ln2;
+  muz_resblock rb[2];
+  muz_dense d5;
+  muz_dense d67;                /* packed, Dense_6 | Dense_7 latent rows fused: 256 -> 128 */
+  const float* d67_onehot;      /* plain [A][128]: one-hot rows 256.. of Dense_6 | Dense_7 */
+  muz_dense reward_head;        /* plain [64][3] */
+  muz_dense discount_head;      /* plain [64][3] */
+} muz_dyn_w;
+
+/* PredictionNetwork4 (lines 549-583) */
+typedef struct muz_pred_w {
+  muz_ln ln0;
+  muz_resblock rb[2];
+  muz_dense d03;                /* packed, Dense_0 | Dense_3 fused: 256 -> 384 */
+  muz_ln ln1;
+  muz_dense d1;                 /* packed 256 -> 128 */
+  muz_ln ln2;
+  muz_dense d2;                 /* packed 128 -> A */
+  muz_ln ln3;
+  muz_dense d4;                 /* packed 128 -> 64 */
+  muz_dense d5;                 /* plain [64][1] */
+} muz_pred_w;
+
+typedef struct muz_net_w {
+  int32_t obs_channels;         /* C = 8P+2 */
+  int32_t num_actions;          /* 24 */
+  muz_repr_w repr;
+  muz_dyn_w dyn;
+  muz_pred_w pred;
+} muz_net_w;
+
+/* Scratch bytes muz_nets_root needs for n observations (conv feature maps). */
+int64_t muz_nets_root_scratch_bytes(int32_t n);
+
+/* root_inference_fn (lines 621-630): obs [n][C][56] fp32 -> prior_logits [n][A], value [n], embedding [n][256]. */
+int muz_nets_root(const muz_net_w* w /*host*/, const float* obs, int32_t n, void* scratch, float* prior_logits,
+                  float* value, float* embedding, void* stream);
+
+/* recurrent_inference_fn (lines 632-661): (action [n], embedding [n][256]) ->
+ * reward [n], discount [n] (E[softmax(logits)]·{-1,0,1}), prior_logits [n][A], value [n], next_embedding [n][256]. */
+int muz_nets_recurrent(const muz_net_w* w /*host*/, const int32_t* action, const float* embedding, int32_t n,
+                       float* reward, float* discount, float* prior_logits, float* value, float* next_embedding,
+                       void* stream);
+
+/* ---- Gumbel MuZero search (run_muzero_mcts, muzero_deterministic_madn.py:663-704 -> mctx 0.0.6) ---- */
+typedef struct muz_search_cfg {
+  int32_t num_simulations;      /* S */
+  int32_t max_depth;            /* D */
+  int32_t max_num_considered;   /* 16 (mctx default) */
+  float value_scale;            /* 0.5 (qtransform_completed_by_mix_value) */
+  float maxvisit_init;          /* 50 */
+  float gumbel_scale;           /* = temperature */
+  uint64_t seed;                /* used only when gumbel == NULL */
+  int32_t turn;                 /* mixed into the noise counter when gumbel == NULL */
+} muz_search_cfg;
+
+/* Workspace bytes for n searches (tree arrays + node embeddings). */
+int64_t muz_search_workspace_bytes(int32_t n, const muz_search_cfg* cfg /*host*/);
+
+/* Batched gumbel_muzero_policy.  legal_bits: 24-bit valid_action masks (invalid = ~legal).
+ * gumbel [n][A] already scaled by gumbel_scale, or NULL to draw it on device from (seed, game_id, turn).
+ * game_id [n] (nullable: identity) only feeds the device noise counter.
+ * Outputs: action [n], action_weights [n][A] (softmax of masked prior+completedQ), root_value [n]. */
+int muz_gumbel_search(const muz_net_w* w /*host*/, const muz_search_cfg* cfg /*host*/, const float* root_logits,
+                      const float* root_value, const float* root_embedding, const uint32_t* legal_bits,
+                      const float* gumbel, const int32_t* game_id, int32_t n, void* workspace, int32_t* action,
+                      float* action_weights, float* root_value_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
