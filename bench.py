@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Self-play throughput benchmark: det-MADN, B = 4096 games per GPU, 50-simulation Gumbel MuZero.
+
+Metric (BASELINE.json): self-play env-steps/s (+ MCTS sims/s), det-MADN batch 4096, 1/2/4/8 GPU.
+  * one bench "step" = one play_n_games_v3 call: reset 4096 games on every rank and play them to
+    completion (or max_steps batched turns) with a 50-simulation search per move (SURVEY §8d b);
+  * env-steps = sum of recorded turns (idx) over all games and ranks, exactly game_agent.py:140;
+  * sims/s = searches x S / time.
+Weak scaling: every rank plays its own 4096 games (games are independent; no data-path collective).
+Timing: W untimed warm-up steps, then K steps between barrier + synchronize on both sides,
+max over ranks.  Rank 0 prints ONE JSON line.
+
+Weights are seeded random (Flax-default init; no checkpoints are available), data is synthetic
+(self-generated games), arithmetic is fp32 end to end (the north star's 1e-5 fp32 target).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BATCH = 4096
+S = 50
+D = 25
+MAX_STEPS = 500
+TEMP = 1.0
+PLAYERS = 2
+# Algorithmic work per simulation: DynamicsNetwork4 529,280 MAC + PredictionNetwork4 404,544 MAC
+# (recomputed in DESIGN.md) -> FLOP = 2 x MAC.
+FLOP_PER_SIM = 2 * (529_280 + 404_544)
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--sims", type=int, default=S)
+    ap.add_argument("--depth", type=int, default=D)
+    ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+def reduce_results(dist, device, steps_done, searches, elapsed, search_ms, launches):
+    """Sum work over ranks, max of wall time (the slowest rank bounds the job)."""
+    import torch
+    if dist is None:
+        return steps_done, searches, elapsed, search_ms, launches
+    t = torch.tensor([float(steps_done), float(searches), search_ms, float(launches)], dtype=torch.float64,
+                     device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    m = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    return t[0].item(), t[1].item(), m[0].item(), t[2].item(), t[3].item()
+
+
+def cpu_baseline(seconds, sims, depth, max_steps):
+    """The NumPy restatement (oracle/) of the same workload on the host: a bounded sample of 16 games
+    played until the time budget is used; reports env-steps/s of that sample."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    from oracle import detmadn as dm
+    from oracle import mctx_gumbel as G
+    from oracle import nets as ON
+    from oracle import selfplay as OS
+
+    cores = min(16, len(os.sched_getaffinity(0)))
+    params = ON.init_params(dm.num_channels(PLAYERS), seed=0)
+    n = 16
+    envs = [dm.env_reset(num_players=PLAYERS, **dm.SELFPLAY_RULES) for _ in range(n)]
+    steps = 0
+    t0 = time.perf_counter()
+    turn = 0
+    with threadpool_limits(limits=cores):
+        while time.perf_counter() - t0 < seconds and turn < max_steps:
+            active = [i for i in range(n) if not envs[i].done]
+            if not active:
+                break
+            search = [i for i in active if dm.valid_action(envs[i]).any()]
+            if search:
+                obs = np.stack([dm.encode_board(envs[i]) for i in search]).astype(np.float32)
+                inv = np.stack([~dm.valid_action(envs[i]).flatten() for i in search])
+                gum = np.stack([OS.gumbel_noise(0, i, turn) for i in search])
+                lg, v, e = ON.root_inference(params, obs)
+                act, _, _, _ = G.gumbel_muzero_policy(params, lg, v, e, ON.recurrent_inference, sims, inv, gum,
+                                                      max_depth=depth)
+                for k, i in enumerate(search):
+                    envs[i] = dm.env_step(envs[i], dm.map_action(int(act[k])))[0]
+            for i in active:
+                if i not in search:
+                    envs[i] = dm.no_step(envs[i])[0]
+            steps += len(active)
+            turn += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 2), "unit": "env_steps/s", "cores": cores, "kind": "port",
+            "sample": f"NumPy oracle self-play, {n} games x {turn} turns ({steps} env-steps, S={sims}, D={depth}) "
+                      f"in {dt:.1f}s, BLAS threads={cores}"}
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_env()
+    import torch
+    import muzpkg
+    muzpkg.load()
+    from exploring_muzero_on_dog_amd import game_agent as GA
+    from exploring_muzero_on_dog_amd import nets as N
+    from exploring_muzero_on_dog_amd import detmadn as E
+
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", init_method="env://")
+        dist = tdist
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    C = E.num_channels(PLAYERS)
+    net = N.DeviceNet(N.init_muzero_params(0, C), C, device=device)
+    eng = GA.SelfPlayEngine(net, args.batch, num_players=PLAYERS, max_steps=args.max_steps,
+                            num_simulations=args.sims, max_depth=args.depth, device=device)
+
+    for w in range(args.warmup):
+        eng.play(seed=10_000 * rank + w, temperature=TEMP)
+    torch.cuda.synchronize()
+
+    steps_done = 0
+    searches = 0
+    search_ms = 0.0
+    launches = 0
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        buf = eng.play(seed=10_000 * rank + 1000 + k, temperature=TEMP)
+        st = eng.last_stats
+        steps_done += int(buf["idx"].sum().item())
+        searches += st["searches"]
+        search_ms += st["search_ms"]
+        launches += st["turns"]
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    steps_done, searches, elapsed, search_ms, launches = reduce_results(dist, device, steps_done, searches, elapsed,
+                                                                         search_ms, launches)
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    value = steps_done / elapsed
+    # roofline of the dominant kernel (k_gumbel_search): algorithmic FLOP / HIP-event time of its launches
+    flop = searches * args.sims * FLOP_PER_SIM
+    achieved = flop / (search_ms * 1e-3) / 1e12 if search_ms > 0 else 0.0
+    out = {
+        "metric": "self-play env steps/sec + MCTS sims/sec, det-MADN batch=4096, 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "env_steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (self-generated games, seeded random fp32 weights)",
+        "config": {"workload": f"det-MADN {PLAYERS}p self-play, {args.batch} games/GPU, Gumbel MuZero "
+                               f"S={args.sims} D={args.depth}, max_steps={args.max_steps}, temp={TEMP}",
+                   "games_per_gpu": args.batch, "num_simulations": args.sims, "max_depth": args.depth,
+                   "parallelism": f"independent games, {world} rank(s)"},
+        "sims_per_s": round(searches * args.sims / elapsed, 1),
+        "env_steps": int(steps_done),
+        "searches": int(searches),
+        "roofline": {"bound": "mfma", "kernel": "k_gumbel_search", "achieved": round(achieved, 3),
+                     "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                     "avg_launch_ms": round(search_ms / max(1, launches), 4),
+                     "flop_per_sim": FLOP_PER_SIM, "traffic": None},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.sims, args.depth, args.max_steps)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

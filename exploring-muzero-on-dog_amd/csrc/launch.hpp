@@ -1,0 +1,26 @@
+// Internal (C++) launchers shared between translation units.  `n_dev`, when non-null, is a
+// device-resident row count that overrides `n` (grids are sized for `n`; surplus workgroups exit),
+// so a device-compacted batch can be processed without a host round trip.
+#pragma once
+#include "common.hpp"
+
+namespace muz {
+
+struct SearchArgs {
+  int S, D, max_considered;
+  float value_scale, maxvisit_init, gumbel_scale;
+  unsigned long long seed;
+  int turn;
+};
+
+int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv_scratch,
+                          float* logits, float* value, float* emb, hipStream_t s);
+
+int launch_gumbel_search(const muz_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,
+                         const float* root_emb, const uint32_t* legal, const float* gumbel, const int32_t* game_id,
+                         int n, const int* n_dev, void* workspace, int32_t* action, float* weights, float* value,
+                         hipStream_t s);
+
+int64_t search_workspace_bytes(int n, int S);
+
+}  // namespace muz

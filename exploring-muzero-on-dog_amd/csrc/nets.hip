@@ -1,5 +1,6 @@
 // MuZero network kernels: root_inference_fn and recurrent_inference_fn
 // (MuZero_det_MADN/muzero_deterministic_madn.py:621-661) as fused fp32 MFMA kernels.
+#include "launch.hpp"
 #include "nn.hpp"
 
 namespace muz {
@@ -55,7 +56,9 @@ __device__ __forceinline__ void conv_mfma(const muz_dense& L, const float* in, i
 }
 
 __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w R, const float* __restrict__ obs, int C, int n,
-                                                   float* __restrict__ convout) {
+                                                   const int* __restrict__ n_dev, float* __restrict__ convout) {
+  if (n_dev) n = *n_dev;
+  if ((int)blockIdx.x >= n) return;
   __shared__ __attribute__((aligned(16))) float in0[58 * 6];
   __shared__ __attribute__((aligned(16))) float c1in[66 * 32];
   __shared__ __attribute__((aligned(16))) float pre[kConvRowsPad * kPreLd];
@@ -97,8 +100,11 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w R, const float* __
 
 // Rest of RepresentationNetwork2 + PredictionNetwork4 on 16-game tiles.
 __global__ __launch_bounds__(256) void k_root_dense(muz_net_w Wt, const float* __restrict__ obs,
-                                                    const float* __restrict__ convout, int n, float* prior_logits,
-                                                    float* value, float* embedding) {
+                                                    const float* __restrict__ convout, int n,
+                                                    const int* __restrict__ n_dev, float* prior_logits, float* value,
+                                                    float* embedding) {
+  if (n_dev) n = *n_dev;
+  if ((int)blockIdx.x * kRows >= n) return;
   __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
   const Arena a = Arena::carve(smem);
   const muz_repr_w& R = Wt.repr;
@@ -181,6 +187,15 @@ int check_net(const muz_net_w* w) {
   return MUZ_OK;
 }
 
+int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv, float* logits,
+                          float* value, float* emb, hipStream_t s) {
+  k_repr_conv<<<n, 256, 0, s>>>(w.repr, obs, w.obs_channels, n, n_dev, conv);
+  int rc = muz_last_launch_error();
+  if (rc) return rc;
+  k_root_dense<<<(n + kRows - 1) / kRows, 256, 0, s>>>(w, obs, conv, n, n_dev, logits, value, emb);
+  return muz_last_launch_error();
+}
+
 }  // namespace muz
 
 using namespace muz;
@@ -192,19 +207,15 @@ int64_t muz_nets_root_scratch_bytes(int32_t n) {
   return rows * 3584 * (int64_t)sizeof(float);
 }
 
-int muz_nets_root(const muz_net_w* w, const float* obs, int32_t n, void* scratch, float* prior_logits, float* value,
-                  float* embedding, void* stream) {
+int muz_nets_root(const muz_net_w* w, const float* obs, int32_t n, void* scratch, int64_t scratch_bytes,
+                  float* prior_logits, float* value, float* embedding, void* stream) {
   int rc = check_net(w);
   if (rc) return rc;
   MUZ_HOST_CHECK(n >= 0 && obs && scratch && prior_logits && value && embedding);
+  MUZ_HOST_CHECK(scratch_bytes >= muz_nets_root_scratch_bytes(n));
   if (n == 0) return MUZ_OK;
-  hipStream_t s = (hipStream_t)stream;
-  float* conv = (float*)scratch;
-  k_repr_conv<<<n, 256, 0, s>>>(w->repr, obs, w->obs_channels, n, conv);
-  rc = muz_last_launch_error();
-  if (rc) return rc;
-  k_root_dense<<<(n + kRows - 1) / kRows, 256, 0, s>>>(*w, obs, conv, n, prior_logits, value, embedding);
-  return muz_last_launch_error();
+  return launch_root_inference(*w, obs, n, nullptr, (float*)scratch, prior_logits, value, embedding,
+                               (hipStream_t)stream);
 }
 
 int muz_nets_recurrent(const muz_net_w* w, const int32_t* action, const float* embedding, int32_t n, float* reward,

@@ -8,6 +8,7 @@
 // inter-workgroup traffic (games are independent).  Node scalars (visits, raw value, value) and
 // the current path live in LDS; children arrays and node embeddings live in the workspace (HBM,
 // L2/MALL resident), written lazily when a node is created.
+#include "launch.hpp"
 #include "nn.hpp"
 
 namespace muz {
@@ -54,13 +55,6 @@ static TreeWs carve_ws(void* ws, int n, int N) {
   t.N = N;
   return t;
 }
-
-struct SearchArgs {
-  int S, D, max_considered;
-  float value_scale, maxvisit_init, gumbel_scale;
-  unsigned long long seed;
-  int turn;
-};
 
 // ---- 16-lane (one game) reductions with jnp.argmax tie-breaking (first index wins) -------------------
 __device__ __forceinline__ void argmax16(float& v, int& i) {
@@ -191,7 +185,8 @@ __global__ __launch_bounds__(256, 1) void k_gumbel_search(muz_net_w Wt, SearchAr
                                                           const float* __restrict__ root_emb,
                                                           const uint32_t* __restrict__ legal,
                                                           const float* __restrict__ gumbel_in,
-                                                          const int32_t* __restrict__ game_id, int n, TreeWs T,
+                                                          const int32_t* __restrict__ game_id, int n,
+                                                          const int* __restrict__ n_dev, TreeWs T,
                                                           int32_t* out_action, float* out_weights,
                                                           float* out_value) {
   __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
@@ -207,6 +202,8 @@ __global__ __launch_bounds__(256, 1) void k_gumbel_search(muz_net_w Wt, SearchAr
   __shared__ int s_act[kRows], s_parent[kRows], s_next[kRows], s_depth[kRows], s_ncons[kRows];
   __shared__ unsigned s_legal[kRows];
 
+  if (n_dev) n = *n_dev;
+  if ((int)blockIdx.x * kRows >= n) return;
   const Arena ar = Arena::carve(smem);
   const int A = Wt.num_actions;
   const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
@@ -489,6 +486,21 @@ __global__ __launch_bounds__(256, 1) void k_gumbel_search(muz_net_w Wt, SearchAr
   }
 }
 
+int64_t search_workspace_bytes(int n, int S) {
+  const int N = S + 1;
+  return (int64_t)ws_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4;
+}
+
+int launch_gumbel_search(const muz_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,
+                         const float* root_emb, const uint32_t* legal, const float* gumbel, const int32_t* game_id,
+                         int n, const int* n_dev, void* workspace, int32_t* action, float* weights, float* value,
+                         hipStream_t s) {
+  TreeWs T = carve_ws(workspace, n, sa.S + 1);
+  k_gumbel_search<<<(n + kRows - 1) / kRows, 256, 0, s>>>(w, sa, root_logits, root_value, root_emb, legal, gumbel,
+                                                          game_id, n, n_dev, T, action, weights, value);
+  return muz_last_launch_error();
+}
+
 }  // namespace muz
 
 using namespace muz;
@@ -497,14 +509,13 @@ extern "C" {
 
 int64_t muz_search_workspace_bytes(int32_t n, const muz_search_cfg* cfg) {
   if (!cfg || n < 0) return -1;
-  const int N = cfg->num_simulations + 1;
-  return (int64_t)ws_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4;
+  return search_workspace_bytes(n, cfg->num_simulations);
 }
 
 int muz_gumbel_search(const muz_net_w* w, const muz_search_cfg* cfg, const float* root_logits, const float* root_value,
                       const float* root_embedding, const uint32_t* legal_bits, const float* gumbel,
-                      const int32_t* game_id, int32_t n, void* workspace, int32_t* action, float* action_weights,
-                      float* root_value_out, void* stream) {
+                      const int32_t* game_id, int32_t n, void* workspace, int64_t workspace_bytes, int32_t* action,
+                      float* action_weights, float* root_value_out, void* stream) {
   if (!w || !cfg) return MUZ_E_INVALID;
   if (w->num_actions != MUZ_DET_ACTIONS) return MUZ_E_UNSUPPORTED;
   if (cfg->num_simulations < 1 || cfg->num_simulations > kMaxSims) return MUZ_E_UNSUPPORTED;
@@ -512,6 +523,7 @@ int muz_gumbel_search(const muz_net_w* w, const muz_search_cfg* cfg, const float
   if (cfg->max_num_considered < 1) return MUZ_E_UNSUPPORTED;
   MUZ_HOST_CHECK(n >= 0 && root_logits && root_value && root_embedding && legal_bits && workspace && action &&
                  action_weights && root_value_out);
+  MUZ_HOST_CHECK(workspace_bytes >= search_workspace_bytes(n, cfg->num_simulations));
   if (n == 0) return MUZ_OK;
   SearchArgs sa;
   sa.S = cfg->num_simulations;
@@ -522,11 +534,8 @@ int muz_gumbel_search(const muz_net_w* w, const muz_search_cfg* cfg, const float
   sa.gumbel_scale = cfg->gumbel_scale;
   sa.seed = cfg->seed;
   sa.turn = cfg->turn;
-  TreeWs T = carve_ws(workspace, n, sa.S + 1);
-  k_gumbel_search<<<(n + kRows - 1) / kRows, 256, 0, (hipStream_t)stream>>>(
-      *w, sa, root_logits, root_value, root_embedding, legal_bits, gumbel, game_id, n, T, action, action_weights,
-      root_value_out);
-  return muz_last_launch_error();
+  return launch_gumbel_search(*w, sa, root_logits, root_value, root_embedding, legal_bits, gumbel, game_id, n, nullptr,
+                              workspace, action, action_weights, root_value_out, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,88 @@
+"""Batched MuZero self-play on the GPU (host mirror of MuZero_det_MADN/game_agent.py).
+
+``play_n_games_v3`` keeps the reference signature's meaning (game_agent.py:185-192): reset
+``num_envs`` games, play them to completion (or ``max_steps`` batched turns) with a Gumbel-MuZero
+search per move, and return the trajectory buffers as a dict of device tensors
+(obs, act, rew, val, pol, mask, player, team, discount, idx) shaped [num_envs, max_steps, ...].
+The whole loop runs natively in libmuz.so (muz_detmadn_selfplay): no per-turn Python, no
+host<->device copy inside a turn.  ``obs`` is int8 (values 0..4); the reference stores fp32.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import detmadn as E
+from . import lib as _L
+from . import mcts as M
+from . import nets as N
+
+# MuZero_det_MADN/game_agent.py:12-22
+RULES = dict(E.SELFPLAY_RULES)
+
+
+class SelfPlayEngine:
+    """Owns the device state, trajectory buffers and workspace for repeated self-play calls."""
+
+    def __init__(self, net: N.DeviceNet, num_envs: int, num_players: int = 4, max_steps: int = 550,
+                 num_simulations: int = 50, max_depth: int = 25, rules: dict | None = None, starting_player=0,
+                 device="cuda"):
+        self.net = net
+        self.n, self.P, self.T = int(num_envs), int(num_players), int(max_steps)
+        self.S, self.D = int(num_simulations), int(max_depth)
+        self.C = E.num_channels(self.P)
+        if net.C != self.C:
+            raise ValueError(f"network expects {net.C} observation channels, {self.P} players give {self.C}")
+        r = dict(RULES if rules is None else rules)
+        self.rules = E.make_rules(self.P, starting_player=starting_player, **r)
+        self.state = E._alloc(self.n, self.P, self.rules, device)
+        n, T, A = self.n, self.T, net.A
+        z = dict(device=device)
+        self.buffers = {
+            "obs": torch.empty((n, T, self.C, E.CELLS), dtype=torch.int8, **z),
+            "act": torch.empty((n, T), dtype=torch.int32, **z),
+            "rew": torch.empty((n, T), dtype=torch.int32, **z),
+            "val": torch.empty((n, T), dtype=torch.float32, **z),
+            "pol": torch.empty((n, T, A), dtype=torch.float32, **z),
+            "mask": torch.empty((n, T), dtype=torch.float32, **z),
+            "player": torch.empty((n, T), dtype=torch.int32, **z),
+            "team": torch.empty((n, T), dtype=torch.int32, **z),
+            "discount": torch.empty((n, T), dtype=torch.int32, **z),
+            "idx": torch.empty((n,), dtype=torch.int32, **z),
+        }
+        lib = _L.load()
+        cfg = M.make_cfg(self.S, self.D)
+        nbytes = lib.muz_selfplay_workspace_bytes(n, self.C, cfg)
+        self.workspace = torch.empty((nbytes,), dtype=torch.uint8, **z)
+        self.last_turns = 0
+        self.last_stats = None
+
+    def traj(self) -> _L.MuzTraj:
+        t = _L.MuzTraj()
+        for k in ("obs", "act", "rew", "val", "pol", "mask", "player", "team", "discount", "idx"):
+            setattr(t, k, self.buffers[k].data_ptr())
+        t.max_steps = self.T
+        return t
+
+    def play(self, seed: int, temperature: float = 1.0, stream=None, timing: bool = True) -> dict:
+        """One play_n_games_v3 call.  The native loop synchronises its stream before returning.
+        With ``timing`` the search launches are bracketed by HIP events (see ``last_stats``)."""
+        lib = _L.load()
+        cfg = M.make_cfg(self.S, self.D, temperature=temperature, seed=seed)
+        st = _L.MuzSpStats()
+        _L.check(lib.muz_detmadn_selfplay(self.rules, self.net.w, cfg, self.state.soa(), self.traj(), self.n,
+                                          _L.ptr(self.workspace), _L.nbytes(self.workspace),
+                                          ctypes.byref(st) if timing else None,
+                                          _L.stream_ptr(stream)), "muz_detmadn_selfplay")
+        self.last_stats = {"turns": st.turns, "searches": st.searches, "search_ms": st.search_ms,
+                           "total_ms": st.total_ms} if timing else None
+        self.last_turns = st.turns if timing else -1
+        return self.buffers
+
+
+def play_n_games_v3(net: N.DeviceNet, seed: int, num_envs: int, num_simulation: int, max_depth: int,
+                    max_steps: int, temp: float, num_players: int = 4, rules: dict | None = None) -> dict:
+    """play_n_games_v3 (game_agent.py:185-192) -> trajectory buffers (device tensors)."""
+    eng = SelfPlayEngine(net, num_envs, num_players, max_steps, num_simulation, max_depth, rules)
+    return eng.play(seed, temp)

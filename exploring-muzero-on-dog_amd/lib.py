@@ -93,6 +93,16 @@ class MuzSearchCfg(ctypes.Structure):
                 ("turn", ctypes.c_int32)]
 
 
+class MuzTraj(ctypes.Structure):
+    _fields_ = [("obs", vp), ("act", vp), ("rew", vp), ("val", vp), ("pol", vp), ("mask", vp), ("player", vp),
+                ("team", vp), ("discount", vp), ("idx", vp), ("max_steps", ctypes.c_int32)]
+
+
+class MuzSpStats(ctypes.Structure):
+    _fields_ = [("turns", ctypes.c_int32), ("searches", ctypes.c_int64), ("search_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double)]
+
+
 # name -> (restype, argtypes).  Kept in sync with include/muz.h (tests/test_capi.py checks it).
 SIGNATURES = {
     "muz_version": (ctypes.c_char_p, []),
@@ -106,12 +116,17 @@ SIGNATURES = {
     "muz_detmadn_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_nets_root_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32]),
-    "muz_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, ctypes.c_int32, vp, vp, vp, vp, vp]),
+    "muz_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp,
+                                     vp]),
     "muz_nets_recurrent": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp,
                                           vp]),
     "muz_search_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.POINTER(MuzSearchCfg)]),
     "muz_gumbel_search": (ctypes.c_int, [ctypes.POINTER(MuzNetW), ctypes.POINTER(MuzSearchCfg), vp, vp, vp, vp,
-                                         vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp]),
+                                         vp, vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp, vp]),
+    "muz_selfplay_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(MuzSearchCfg)]),
+    "muz_detmadn_selfplay": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzNetW),
+                                            ctypes.POINTER(MuzSearchCfg), MuzDetSoA, MuzTraj, ctypes.c_int32, vp,
+                                            ctypes.c_int64, ctypes.POINTER(MuzSpStats), vp]),
 }
 
 _lib = None
@@ -153,3 +168,7 @@ def stream_ptr(stream=None):
 
 def ptr(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def nbytes(t):
+    return t.numel() * t.element_size()

@@ -28,7 +28,7 @@ class SearchWorkspace:
         cfg = make_cfg(num_simulations, 1)
         self.batch, self.S = batch, num_simulations
         nbytes = lib.muz_search_workspace_bytes(batch, cfg)
-        self.tree = torch.empty((nbytes + 15) // 16 * 4, dtype=torch.float32, device=device)
+        self.tree = torch.empty((nbytes,), dtype=torch.uint8, device=device)
         self.scratch = torch.empty(lib.muz_nets_root_scratch_bytes(batch) // 4, dtype=torch.float32, device=device)
 
     def fits(self, batch, S):
@@ -70,7 +70,8 @@ def gumbel_muzero_policy(net: _N.DeviceNet, root_logits, root_value, root_embedd
     lb = legal_bits.to(device=dev, dtype=torch.int32).contiguous()
     _L.check(lib.muz_gumbel_search(net.w, cfg, _L.ptr(root_logits.contiguous()), _L.ptr(root_value.contiguous()),
                                    _L.ptr(root_embedding.contiguous()), _L.ptr(lb), _L.ptr(g), _L.ptr(gid), B,
-                                   _L.ptr(workspace.tree), _L.ptr(action), _L.ptr(weights), _L.ptr(value),
+                                   _L.ptr(workspace.tree), _L.nbytes(workspace.tree), _L.ptr(action), _L.ptr(weights),
+                                   _L.ptr(value),
                                    _L.stream_ptr()), "muz_gumbel_search")
     return PolicyOutput(action, weights), value
 

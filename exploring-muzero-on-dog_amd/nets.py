@@ -202,8 +202,8 @@ def root_inference_fn(net: DeviceNet, observation: torch.Tensor, scratch: torch.
     logits = torch.empty((B, net.A), dtype=torch.float32, device=dev)
     value = torch.empty((B,), dtype=torch.float32, device=dev)
     emb = torch.empty((B, LATENT), dtype=torch.float32, device=dev)
-    _L.check(lib.muz_nets_root(net.w, _L.ptr(obs), B, _L.ptr(scratch), _L.ptr(logits), _L.ptr(value), _L.ptr(emb),
-                               _L.stream_ptr()), "muz_nets_root")
+    _L.check(lib.muz_nets_root(net.w, _L.ptr(obs), B, _L.ptr(scratch), _L.nbytes(scratch), _L.ptr(logits),
+                               _L.ptr(value), _L.ptr(emb), _L.stream_ptr()), "muz_nets_root")
     return logits, value, emb
 
 

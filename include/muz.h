@@ -168,8 +168,8 @@ typedef struct muz_net_w {
 int64_t muz_nets_root_scratch_bytes(int32_t n);
 
 /* root_inference_fn (lines 621-630): obs [n][C][56] fp32 -> prior_logits [n][A], value [n], embedding [n][256]. */
-int muz_nets_root(const muz_net_w* w /*host*/, const float* obs, int32_t n, void* scratch, float* prior_logits,
-                  float* value, float* embedding, void* stream);
+int muz_nets_root(const muz_net_w* w /*host*/, const float* obs, int32_t n, void* scratch, int64_t scratch_bytes,
+                  float* prior_logits, float* value, float* embedding, void* stream);
 
 /* recurrent_inference_fn (lines 632-661): (action [n], embedding [n][256]) ->
  * reward [n], discount [n] (E[softmax(logits)]·{-1,0,1}), prior_logits [n][A], value [n], next_embedding [n][256]. */
@@ -198,8 +198,44 @@ int64_t muz_search_workspace_bytes(int32_t n, const muz_search_cfg* cfg /*host*/
  * Outputs: action [n], action_weights [n][A] (softmax of masked prior+completedQ), root_value [n]. */
 int muz_gumbel_search(const muz_net_w* w /*host*/, const muz_search_cfg* cfg /*host*/, const float* root_logits,
                       const float* root_value, const float* root_embedding, const uint32_t* legal_bits,
-                      const float* gumbel, const int32_t* game_id, int32_t n, void* workspace, int32_t* action,
-                      float* action_weights, float* root_value_out, void* stream);
+                      const float* gumbel, const int32_t* game_id, int32_t n, void* workspace,
+                      int64_t workspace_bytes, int32_t* action, float* action_weights, float* root_value_out,
+                      void* stream);
+
+/* ---- self-play (MuZero_det_MADN/game_agent.py:50-192) ----------------------------------------------
+ * Trajectory buffers [n][T] per game, T = max_steps, mirroring play_batch_of_games_jitted's dict
+ * (game_agent.py:158-169); obs is stored int8 (values 0..4, the reference keeps them as fp32). */
+typedef struct muz_traj {
+  int8_t* obs;        /* [n][T][C][56] */
+  int32_t* act;       /* [n][T]  action index, -1 on no-move turns */
+  int32_t* rew;       /* [n][T]  reward class {0:-1, 1:0, 2:+1} */
+  float* val;         /* [n][T]  root value (search_tree.summary().value) */
+  float* pol;         /* [n][T][24] action_weights */
+  float* mask;        /* [n][T]  1 = search turn, 0 = no-move turn */
+  int32_t* player;    /* [n][T]  current player before the move */
+  int32_t* team;      /* [n][T]  player % 2 with teams, else -1 */
+  int32_t* discount;  /* [n][T]  discount class {0: other side moves next, 1: terminal, 2: same side} */
+  int32_t* idx;       /* [n]     recorded steps per game */
+  int32_t max_steps;  /* T */
+} muz_traj;
+
+/* Optional per-call statistics (host struct).  search_ms sums HIP-event durations of the search
+ * kernel launches (events are recorded only when stats != NULL). */
+typedef struct muz_sp_stats {
+  int32_t turns;      /* batched turns that found an active game */
+  int64_t searches;   /* MCTS searches run (sum over turns of games with a legal move) */
+  double search_ms;   /* device time of the Gumbel-search launches */
+  double total_ms;    /* device time of the whole call */
+} muz_sp_stats;
+
+int64_t muz_selfplay_workspace_bytes(int32_t n, int32_t obs_channels, const muz_search_cfg* cfg /*host*/);
+
+/* play_n_games_v3 + play_batch_of_games_jitted: reset n games (rules->starting_player), then play
+ * until every game is done or max_steps turns ran.  Searches use cfg (S, D, temperature = gumbel_scale,
+ * device Gumbel noise from cfg->seed).  stats (host, nullable) receives turns / searches / timings. */
+int muz_detmadn_selfplay(const muz_rules* rules /*host*/, const muz_net_w* w /*host*/,
+                         const muz_search_cfg* cfg /*host*/, muz_detmadn_soa state, muz_traj traj, int32_t n,
+                         void* workspace, int64_t workspace_bytes, muz_sp_stats* stats /*host*/, void* stream);
 
 #ifdef __cplusplus
 }

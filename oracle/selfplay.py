@@ -1,0 +1,100 @@
+"""CPU oracle: batched self-play bookkeeping of MuZero_det_MADN/game_agent.py:50-183 (TEST INFRASTRUCTURE ONLY).
+
+Drives the env oracle (oracle/detmadn.py) and a Gumbel search (oracle/mctx_gumbel.py) with
+injected networks, and records the same buffers as play_batch_of_games_jitted.  The per-move
+Gumbel noise follows the engine's counter RNG (``gumbel_noise``) so that both sides see the same
+noise; the reference draws it with jax threefry (parity of the noise source: unpinned).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import detmadn as dm
+from oracle import mctx_gumbel as G
+
+M64 = (1 << 64) - 1
+TINY = np.finfo(np.float32).tiny
+
+
+def _mix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
+    return x ^ (x >> 31)
+
+
+def gumbel_noise(seed, gid, turn, A=24, scale=1.0):
+    """Counter-based Gumbel draw of the engine (csrc/search.hip:gumbel_noise): -log(-log(U[tiny,1)))."""
+    out = np.empty(A, np.float32)
+    for a in range(A):
+        h = _mix64((seed & M64) ^ _mix64(((gid & 0xFFFFFFFF) << 32) | (turn & 0xFFFFFFFF))
+                   ^ (((a + 1) * 0xD6E8FEB86659FD93) & M64))
+        u = np.float32((h >> 40) * (1.0 / 16777216.0))
+        u = max(u, np.float32(TINY))
+        out[a] = np.float32(scale) * (-np.log(-np.log(np.float32(u))))
+    return out.astype(np.float32)
+
+
+def play_batch_of_games(params, root_fn, recurrent_fn, envs, num_simulations, max_depth, max_steps, temp, seed):
+    """game_agent.py:50-183 over a list of oracle envs.  root_fn(params, obs[B,C,56]) -> (logits, value, emb)."""
+    n = len(envs)
+    P = envs[0].num_players
+    C = dm.num_channels(P)
+    T = max_steps
+    teams = envs[0].rules["enable_teams"]
+    buf = {
+        "obs": np.zeros((n, T, C, 56), np.int8), "act": np.zeros((n, T), np.int32),
+        "rew": np.zeros((n, T), np.int32), "val": np.zeros((n, T), np.float32),
+        "pol": np.zeros((n, T, 24), np.float32), "mask": np.zeros((n, T), np.float32),
+        "player": np.zeros((n, T), np.int32), "team": np.full((n, T), -1, np.int32),
+        "discount": np.zeros((n, T), np.int32), "idx": np.zeros(n, np.int32),
+    }
+    dones = np.zeros(n, bool)
+    step = 0
+    while (~dones).any() and step < max_steps:
+        search, nomove = [], []
+        for i in range(n):
+            if dones[i]:
+                continue
+            va = dm.valid_action(envs[i]).flatten()
+            (search if va.any() else nomove).append((i, va))
+        if search:
+            obs = np.stack([dm.encode_board(envs[i]) for i, _ in search]).astype(np.float32)
+            invalid = np.stack([~va for _, va in search])
+            gum = np.stack([gumbel_noise(seed, i, step, scale=temp) for i, _ in search])
+            lg, v, e = root_fn(params, obs)
+            act, w, rv, _ = G.gumbel_muzero_policy(params, lg, v, e, recurrent_fn, num_simulations, invalid, gum,
+                                                   max_depth=max_depth)
+            for k, (i, _) in enumerate(search):
+                env = envs[i]
+                t = buf["idx"][i]
+                cpb = env.current_player
+                teamb = cpb % 2 if teams else -1
+                nxt, r, nd = dm.env_step(env, dm.map_action(int(act[k])))
+                nteam = nxt.current_player % 2 if teams else -1
+                buf["obs"][i, t] = obs[k].astype(np.int8)
+                buf["act"][i, t] = act[k]
+                buf["rew"][i, t] = 2 if (nd and r > 0) else (0 if (nd and r < 0) else 1)
+                buf["val"][i, t] = rv[k]
+                buf["pol"][i, t] = w[k]
+                buf["mask"][i, t] = 1.0
+                buf["player"][i, t] = cpb
+                buf["team"][i, t] = teamb
+                buf["discount"][i, t] = 1 if nd else ((2 if teamb == nteam else 0) if teams
+                                                      else (2 if cpb == nxt.current_player else 0))
+                buf["idx"][i] = t + 1
+                envs[i] = nxt
+                dones[i] = nd
+        for i, _ in nomove:
+            env = envs[i]
+            t = buf["idx"][i]
+            buf["act"][i, t] = -1
+            buf["rew"][i, t] = 1
+            buf["player"][i, t] = env.current_player
+            buf["team"][i, t] = env.current_player % 2 if teams else -1
+            buf["discount"][i, t] = 1
+            buf["idx"][i] = t + 1
+            envs[i], _, nd = dm.no_step(env)
+            dones[i] = nd
+        step += 1
+    return buf, step
