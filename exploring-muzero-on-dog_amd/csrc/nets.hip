@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w R, const float* __
 }
 
 // Rest of RepresentationNetwork2 + PredictionNetwork4 on 16-game tiles.
-__global__ __launch_bounds__(256) void k_root_dense(muz_net_w Wt, const float* __restrict__ obs,
+__global__ __launch_bounds__(kThreads) void k_root_dense(muz_net_w Wt, const float* __restrict__ obs,
                                                     const float* __restrict__ convout, int n,
                                                     const int* __restrict__ n_dev, float* prior_logits, float* value,
                                                     float* embedding) {
@@ -110,14 +110,14 @@ __global__ __launch_bounds__(256) void k_root_dense(muz_net_w Wt, const float* _
   const muz_repr_w& R = Wt.repr;
   const int C = Wt.obs_channels, A = Wt.num_actions;
   const int g0 = blockIdx.x * kRows;
-  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int row = trow(), sub = tsub();
   const int gr = g0 + row;
   const bool valid = gr < n;
   // global stream input: x[:, 6:, 0]
   const int Kg = C - 6;
-  for (int c = sub; c < 32; c += 16) a.E[row * LDE + c] = (valid && c < Kg) ? obs[((size_t)gr * C + 6 + c) * 56] : 0.f;
+  a.E[row * LDE + sub] = (valid && sub < Kg) ? obs[((size_t)gr * C + 6 + sub) * 56] : 0.f;
   // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16)
-  dense16<4>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW);
+  dense16<2>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, R.ln3);
   dense16<1>(R.d1, Kg, 64, a.E, LDE, a.X, LD);
@@ -128,28 +128,28 @@ __global__ __launch_bounds__(256) void k_root_dense(muz_net_w Wt, const float* _
   __syncthreads();
   ln16<64, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, R.ln5);
   __syncthreads();
-  dense16<4>(R.d3, 320, LAT, a.W, LDW, a.X, LD);
+  dense16<2>(R.d3, 320, LAT, a.W, LDW, a.X, LD);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, R.ln6);
   __syncthreads();
 #pragma unroll 1
   for (int b = 0; b < 6; ++b) resblock16(R.rb[b], a.X, a.T, a.U);
-  dense16<4>(R.d4, LAT, LAT, a.X, LD, a.T, LD);
+  dense16<2>(R.d4, LAT, LAT, a.X, LD, a.T, LD);
   __syncthreads();
   minmax16(a.T, LD);
   __syncthreads();
   if (valid)
-    for (int c = sub; c < LAT; c += 16) embedding[(size_t)gr * LAT + c] = a.T[row * LD + c];
+    for (int c = sub; c < LAT; c += kRowLanes) embedding[(size_t)gr * LAT + c] = a.T[row * LD + c];
   __syncthreads();
   pred16(Wt.pred, A, a.T, a);
   if (valid) {
-    for (int c = sub; c < A; c += 16) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
+    for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
     if (sub == 0) value[gr] = a.v0[row];
   }
 }
 
 // recurrent_inference_fn on 16-row tiles.
-__global__ __launch_bounds__(256) void k_recurrent(muz_net_w Wt, const int32_t* __restrict__ action,
+__global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int32_t* __restrict__ action,
                                                    const float* __restrict__ emb, int n, float* reward,
                                                    float* discount, float* prior_logits, float* value,
                                                    float* next_emb) {
@@ -158,15 +158,15 @@ __global__ __launch_bounds__(256) void k_recurrent(muz_net_w Wt, const int32_t* 
   const Arena a = Arena::carve(smem);
   const int A = Wt.num_actions;
   const int g0 = blockIdx.x * kRows;
-  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int row = trow(), sub = tsub();
   const int gr = g0 + row;
   const bool valid = gr < n;
-  for (int c = sub; c < LAT; c += 16) a.L[row * LD + c] = valid ? emb[(size_t)gr * LAT + c] : 0.f;
+  for (int c = sub; c < LAT; c += kRowLanes) a.L[row * LD + c] = valid ? emb[(size_t)gr * LAT + c] : 0.f;
   if (sub == 0) act[row] = valid ? action[gr] : 0;
   __syncthreads();
   dyn16(Wt.dyn, A, act, a);
   if (valid) {
-    for (int c = sub; c < LAT; c += 16) next_emb[(size_t)gr * LAT + c] = a.T[row * LD + c];
+    for (int c = sub; c < LAT; c += kRowLanes) next_emb[(size_t)gr * LAT + c] = a.T[row * LD + c];
     if (sub == 0) {
       reward[gr] = a.v1[row];
       discount[gr] = a.v2[row];
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void k_recurrent(muz_net_w Wt, const int32_t* 
   __syncthreads();
   pred16(Wt.pred, A, a.T, a);
   if (valid) {
-    for (int c = sub; c < A; c += 16) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
+    for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
     if (sub == 0) value[gr] = a.v0[row];
   }
 }
@@ -192,7 +192,7 @@ int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int
   k_repr_conv<<<n, 256, 0, s>>>(w.repr, obs, w.obs_channels, n, n_dev, conv);
   int rc = muz_last_launch_error();
   if (rc) return rc;
-  k_root_dense<<<(n + kRows - 1) / kRows, 256, 0, s>>>(w, obs, conv, n, n_dev, logits, value, emb);
+  k_root_dense<<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, obs, conv, n, n_dev, logits, value, emb);
   return muz_last_launch_error();
 }
 
@@ -224,7 +224,7 @@ int muz_nets_recurrent(const muz_net_w* w, const int32_t* action, const float* e
   if (rc) return rc;
   MUZ_HOST_CHECK(n >= 0 && action && embedding && reward && discount && prior_logits && value && next_embedding);
   if (n == 0) return MUZ_OK;
-  k_recurrent<<<(n + kRows - 1) / kRows, 256, 0, (hipStream_t)stream>>>(*w, action, embedding, n, reward, discount,
+  k_recurrent<<<(n + kRows - 1) / kRows, kThreads, 0, (hipStream_t)stream>>>(*w, action, embedding, n, reward, discount,
                                                                          prior_logits, value, next_embedding);
   return muz_last_launch_error();
 }

@@ -1,20 +1,22 @@
 // Fused fp32 MLP building blocks for 16-row tiles on CDNA4 MFMA (v_mfma_f32_16x16x4_f32).
 //
-// A workgroup of 4 waves owns a tile of 16 rows (games).  Activations live in LDS
-// ([16][ld] fp32 rows); a dense layer out = A[16][K] @ W[K][N] + b splits its N columns over the
-// 4 waves (NT 16-column tiles each).  Per 16-deep k-block a lane reads ONE float4 of A from
+// A workgroup of 8 waves (two per SIMD, so one wave's weight loads hide under the other's MFMAs)
+// owns a tile of 16 rows (games).  Activations live in LDS ([16][ld] fp32 rows); a dense layer
+// out = A[16][K] @ W[K][N] + b splits its N columns over the 8 waves (NT 16-column tiles each).  Per 16-deep k-block a lane reads ONE float4 of A from
 // LDS (row lane&15, k = kb*16 + 4*(lane>>4) + j, j = 0..3) and NT float4 of pre-packed weights
 // straight from global memory (L2/MALL resident, streamed once per tile), then issues 4*NT
-// MFMAs.  The f32-input MFMA is an exact k-ordered fma chain, so only the reduction order
-// differs from the fp32 reference.  Row-wise ops (LayerNorm, min-max) use 16 lanes per row.
+// MFMAs, with the weights of the next two k-blocks in flight.  The f32-input MFMA is an exact
+// k-ordered fma chain, so only the reduction order differs from the fp32 reference.  Row-wise ops
+// (LayerNorm, min-max) use 32 lanes (half a wave) per row.
 #pragma once
 #include "common.hpp"
 
 namespace muz {
 
 constexpr int kRows = 16;
-constexpr int kWaves = 4;
-constexpr int kThreads = kRows * 16;   // 256
+constexpr int kRowLanes = 32;                 // lanes per row in row-wise phases
+constexpr int kThreads = kRows * kRowLanes;   // 512
+constexpr int kWaves = kThreads / 64;         // 8
 constexpr int LAT = 256;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -23,7 +25,9 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// acc[t] += A[16 rows][K] @ Wgroup[K][NT*16]  (KB = K/16 k-blocks; Wg = packed weights of this group)
+// acc[t] += A[16 rows][K] @ Wgroup[K][NT*16]  (KB = K/16 k-blocks; Wg = packed weights of this group).
+// Weights for k-blocks kb+1 and kb+2 are in flight while kb is multiplied (3-deep register ring,
+// written out as a 3-way unrolled loop so every buffer index is a compile-time constant).
 template <int NT>
 __device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB, const float* A, int lda,
                                             f32x4 (&acc)[NT]) {
@@ -32,32 +36,33 @@ __device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB
   const f32x4* wp = reinterpret_cast<const f32x4*>(Wg) + lane * NT;
   const int wstep = 64 * NT;   // f32x4 per k-block
   const float* ap = A + r * lda + 4 * g;
-  f32x4 b0[NT], b1[NT];
+  f32x4 b0[NT], b1[NT], b2[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) b0[t] = wp[t];
-  for (int kb = 0; kb < KB; kb += 2) {
-    const bool has1 = kb + 1 < KB;
-    if (has1) {
+  if (KB > 1) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) b1[t] = wp[(kb + 1) * wstep + t];
+    for (int t = 0; t < NT; ++t) b1[t] = wp[wstep + t];
+  }
+  // step kb: issue k-block kb+2 into `nxt` (the buffer consumed at step kb-1), multiply `cur` (= kb)
+  auto step = [&](int kb, const f32x4 (&cur)[NT], f32x4 (&nxt)[NT]) {
+    if (kb + 2 < KB) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) nxt[t] = wp[(kb + 2) * wstep + t];
     }
-    f32x4 a = *reinterpret_cast<const f32x4*>(ap + kb * 16);
+    const f32x4 a = *reinterpret_cast<const f32x4*>(ap + kb * 16);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[j], b0[t][j], acc[t]);
-    if (has1) {
-      if (kb + 2 < KB) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) b0[t] = wp[(kb + 2) * wstep + t];
-      }
-      a = *reinterpret_cast<const f32x4*>(ap + (kb + 1) * 16);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[j], b1[t][j], acc[t]);
-    }
+      for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[j], cur[t][j], acc[t]);
+  };
+  int kb = 0;
+  for (; kb + 3 <= KB; kb += 3) {
+    step(kb, b0, b2);
+    step(kb + 1, b1, b0);
+    step(kb + 2, b2, b1);
   }
+  if (kb < KB) step(kb, b0, b2);
+  if (kb + 1 < KB) step(kb + 1, b1, b0);
 }
 
 // Dense layer over the tile: out[16][N] = A @ W + b, waves split N (NT tiles of 16 columns each).
@@ -85,26 +90,32 @@ __device__ __forceinline__ void dense16(const muz_dense& L, int K, int N, const 
   }
 }
 
-// ---- row-wise ops: thread t -> row t>>4, lane-in-row t&15 -----------------------------------------
-__device__ __forceinline__ float row_sum16(float v) {
-  v += __shfl_xor(v, 8, 16);
-  v += __shfl_xor(v, 4, 16);
-  v += __shfl_xor(v, 2, 16);
-  v += __shfl_xor(v, 1, 16);
+// ---- row-wise ops: thread t -> row t/32, lane-in-row t%32 (half a wave per row) ---------------------
+__device__ __forceinline__ int trow() { return threadIdx.x >> 5; }
+__device__ __forceinline__ int tsub() { return threadIdx.x & 31; }
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m, 32);
   return v;
 }
-__device__ __forceinline__ float row_max16(float v) {
-  v = fmaxf(v, __shfl_xor(v, 8, 16));
-  v = fmaxf(v, __shfl_xor(v, 4, 16));
-  v = fmaxf(v, __shfl_xor(v, 2, 16));
-  v = fmaxf(v, __shfl_xor(v, 1, 16));
+__device__ __forceinline__ float row_max(float v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 32));
   return v;
 }
-__device__ __forceinline__ float row_min16(float v) {
-  v = fminf(v, __shfl_xor(v, 8, 16));
-  v = fminf(v, __shfl_xor(v, 4, 16));
-  v = fminf(v, __shfl_xor(v, 2, 16));
-  v = fminf(v, __shfl_xor(v, 1, 16));
+__device__ __forceinline__ float row_min(float v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v = fminf(v, __shfl_xor(v, m, 32));
+  return v;
+}
+__device__ __forceinline__ int row_isum(int v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m, 32);
+  return v;
+}
+__device__ __forceinline__ int row_imax(int v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, 32));
   return v;
 }
 
@@ -114,25 +125,25 @@ enum LnMode { LN_PLAIN = 0, LN_RELU = 1, LN_RESID_RELU = 2 };
 //   LN_PLAIN: out = y;  LN_RELU: out = relu(y);  LN_RESID_RELU: out = relu(out + y)  (ResBlock tail)
 template <int N, int MODE>
 __device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int ldo, const muz_ln& P) {
-  constexpr int PER = N / 16;
-  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  constexpr int PER = N / kRowLanes;
+  const int row = trow(), sub = tsub();
   float v[PER];
   float s = 0.f, s2 = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    v[i] = in[row * ldi + sub + 16 * i];
+    v[i] = in[row * ldi + sub + kRowLanes * i];
     s += v[i];
     s2 += v[i] * v[i];
   }
-  s = row_sum16(s);
-  s2 = row_sum16(s2);
+  s = row_sum(s);
+  s2 = row_sum(s2);
   const float mean = s / (float)N;
   const float mean2 = s2 / (float)N;
   const float var = fmaxf(0.f, mean2 - mean * mean);
   const float inv = 1.0f / sqrtf(var + 1e-6f);
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = sub + 16 * i;
+    const int c = sub + kRowLanes * i;
     float y = (v[i] - mean) * (inv * P.scale[c]) + P.bias[c];
     if (MODE == LN_RELU) y = fmaxf(y, 0.f);
     if (MODE == LN_RESID_RELU) y = fmaxf(out[row * ldo + c] + y, 0.f);
@@ -142,26 +153,26 @@ __device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int l
 
 // x <- (x - min) / (max - min + 1e-8) per row of 256 (Repr2 139-140, Dyn4 435-437).
 __device__ __forceinline__ void minmax16(float* buf, int ld) {
-  constexpr int PER = LAT / 16;
-  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  constexpr int PER = LAT / kRowLanes;
+  const int row = trow(), sub = tsub();
   float v[PER];
   float lo = INFINITY, hi = -INFINITY;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    v[i] = buf[row * ld + sub + 16 * i];
+    v[i] = buf[row * ld + sub + kRowLanes * i];
     lo = fminf(lo, v[i]);
     hi = fmaxf(hi, v[i]);
   }
-  lo = row_min16(lo);
-  hi = row_max16(hi);
+  lo = row_min(lo);
+  hi = row_max(hi);
   const float den = hi - lo + 1e-8f;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) buf[row * ld + sub + 16 * i] = (v[i] - lo) / den;
+  for (int i = 0; i < PER; ++i) buf[row * ld + sub + kRowLanes * i] = (v[i] - lo) / den;
 }
 
 __device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
-  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
-  for (int c = sub; c < n; c += 16) buf[row * ld + col0 + c] = fmaxf(buf[row * ld + col0 + c], 0.f);
+  const int row = trow(), sub = tsub();
+  for (int c = sub; c < n; c += kRowLanes) buf[row * ld + col0 + c] = fmaxf(buf[row * ld + col0 + c], 0.f);
 }
 
 // ---- LDS arena of a 16-row tile ---------------------------------------------------------------------
@@ -199,11 +210,11 @@ struct Arena {
 
 // ResBlock (muzero_deterministic_madn.py:12-24): X <- relu(X + LN1(D1(relu(LN0(D0(X))))))
 __device__ __forceinline__ void resblock16(const muz_resblock& R, float* X, float* T, float* U) {
-  dense16<4>(R.d0, LAT, LAT, X, LD, T, LD);
+  dense16<2>(R.d0, LAT, LAT, X, LD, T, LD);
   __syncthreads();
   ln16<LAT, LN_RELU>(T, LD, T, LD, R.ln0);
   __syncthreads();
-  dense16<4>(R.d1, LAT, LAT, T, LD, U, LD);
+  dense16<2>(R.d1, LAT, LAT, T, LD, U, LD);
   __syncthreads();
   ln16<LAT, LN_RESID_RELU>(U, LD, X, LD, R.ln1);
   __syncthreads();
@@ -212,10 +223,10 @@ __device__ __forceinline__ void resblock16(const muz_resblock& R, float* X, floa
 // small dot head: out[row] = b + sum_k in[row][k] * w[k][col] for one column (16 lanes per row)
 __device__ __forceinline__ float head_dot16(const float* in, int ld, int K, const float* w, int ncol, int col,
                                             float b) {
-  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int row = trow(), sub = tsub();
   float s = 0.f;
-  for (int k = sub; k < K; k += 16) s += in[row * ld + k] * w[k * ncol + col];
-  return row_sum16(s) + b;
+  for (int k = sub; k < K; k += kRowLanes) s += in[row * ld + k] * w[k * ncol + col];
+  return row_sum(s) + b;
 }
 
 // PredictionNetwork4 (muzero_deterministic_madn.py:549-583) on the latent in `lat` ([16][LD]).
@@ -225,12 +236,12 @@ __device__ __forceinline__ void pred16(const muz_pred_w& P, int A, const float* 
   __syncthreads();
   resblock16(P.rb[0], a.X, a.T, a.U);
   resblock16(P.rb[1], a.X, a.T, a.U);
-  dense16<6>(P.d03, LAT, 384, a.X, LD, a.W, LDW);     // [policy Dense_0 | value Dense_3]
+  dense16<3>(P.d03, LAT, 384, a.X, LD, a.W, LDW);     // [policy Dense_0 | value Dense_3]
   __syncthreads();
   ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, P.ln1);
   ln16<128, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, P.ln3);
   __syncthreads();
-  dense16<2>(P.d1, LAT, 128, a.W, LDW, a.T, LD);      // policy Dense_1
+  dense16<1>(P.d1, LAT, 128, a.W, LDW, a.T, LD);      // policy Dense_1
   dense16<1>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD);  // value Dense_4 (X is free now)
   __syncthreads();
   ln16<128, LN_RELU>(a.T, LD, a.T, LD, P.ln2);
@@ -239,7 +250,7 @@ __device__ __forceinline__ void pred16(const muz_pred_w& P, int A, const float* 
   dense16<1>(P.d2, 128, A, a.T, LD, a.U, LD);         // policy logits
   {
     const float v = head_dot16(a.X, LD, 64, P.d5.w, 1, 0, P.d5.b[0]);
-    if ((threadIdx.x & 15) == 0) a.v0[threadIdx.x >> 4] = tanhf(v);
+    if (tsub() == 0) a.v0[trow()] = tanhf(v);
   }
   __syncthreads();
 }
@@ -255,37 +266,38 @@ __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) 
 // DynamicsNetwork4 (muzero_deterministic_madn.py:391-457): latent a.L, action per row in act[16].
 // Leaves the next latent in a.T, reward / discount expectations in a.v1 / a.v2.  Clobbers X, U, W, E.
 __device__ __forceinline__ void dyn16(const muz_dyn_w& D, int A, const int* act, const Arena& a) {
-  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int row = trow(), sub = tsub();
   const int ar = act[row];
   const bool oh = ar >= 0 && ar < A;   // jax.nn.one_hot: out-of-range -> zero row
   // action embedding: relu(one_hot @ W0 + b0) == relu(W0[a] + b0)
-  for (int c = sub; c < 64; c += 16) a.E[row * LDE + c] = fmaxf((oh ? D.d0.w[ar * 64 + c] : 0.f) + D.d0.b[c], 0.f);
+  for (int c = sub; c < 64; c += kRowLanes)
+    a.E[row * LDE + c] = fmaxf((oh ? D.d0.w[ar * 64 + c] : 0.f) + D.d0.b[c], 0.f);
   ln16<LAT, LN_PLAIN>(a.L, LD, a.X, LD, D.ln0);
   __syncthreads();
-  dense16<8>(D.d12, 64, 512, a.E, LDE, a.W, LDW);     // [scale | shift]
+  dense16<4>(D.d12, 64, 512, a.E, LDE, a.W, LDW);     // [scale | shift]
   __syncthreads();
-  for (int c = sub; c < LAT; c += 16)
+  for (int c = sub; c < LAT; c += kRowLanes)
     a.X[row * LD + c] = a.X[row * LD + c] * (1.0f + a.W[row * LDW + c]) + a.W[row * LDW + 256 + c];
   __syncthreads();
-  dense16<4>(D.d3, LAT, LAT, a.X, LD, a.T, LD);
+  dense16<2>(D.d3, LAT, LAT, a.X, LD, a.T, LD);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, D.ln1);
   __syncthreads();
-  dense16<4>(D.d4, LAT, LAT, a.T, LD, a.X, LD);
+  dense16<2>(D.d4, LAT, LAT, a.T, LD, a.X, LD);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, D.ln2);
   __syncthreads();
   resblock16(D.rb[0], a.X, a.T, a.U);
   resblock16(D.rb[1], a.X, a.T, a.U);
-  dense16<4>(D.d5, LAT, LAT, a.X, LD, a.T, LD);
+  dense16<2>(D.d5, LAT, LAT, a.X, LD, a.T, LD);
   __syncthreads();
-  for (int c = sub; c < LAT; c += 16) a.T[row * LD + c] = a.L[row * LD + c] + a.T[row * LD + c];
+  for (int c = sub; c < LAT; c += kRowLanes) a.T[row * LD + c] = a.L[row * LD + c] + a.T[row * LD + c];
   __syncthreads();
   minmax16(a.T, LD);
   __syncthreads();
-  dense16<2>(D.d67, LAT, 128, a.T, LD, a.W, LDW);     // [reward hidden | discount hidden] latent rows
+  dense16<1>(D.d67, LAT, 128, a.T, LD, a.W, LDW);     // [reward hidden | discount hidden] latent rows
   __syncthreads();
-  for (int c = sub; c < 128; c += 16)
+  for (int c = sub; c < 128; c += kRowLanes)
     a.W[row * LDW + c] = fmaxf(a.W[row * LDW + c] + (oh ? D.d67_onehot[ar * 128 + c] : 0.f), 0.f);
   __syncthreads();
   float rl[3], dl[3];

@@ -2,7 +2,7 @@
 // MuZero_det_MADN/muzero_deterministic_madn.py:663-704) as ONE persistent kernel per search.
 //
 // A workgroup owns 16 games for the whole search: for every simulation it walks the 16 trees
-// (16 lanes per game, two actions per lane, wavefront shuffles for every reduction), gathers the
+// (32 lanes per game, one action per lane, wavefront shuffles for every reduction), gathers the
 // 16 parent embeddings into LDS, runs DynamicsNetwork4 + PredictionNetwork4 on MFMA over the
 // 16-row tile, expands, and backs up.  No kernel boundary between simulations and no
 // inter-workgroup traffic (games are independent).  Node scalars (visits, raw value, value) and
@@ -56,31 +56,17 @@ static TreeWs carve_ws(void* ws, int n, int N) {
   return t;
 }
 
-// ---- 16-lane (one game) reductions with jnp.argmax tie-breaking (first index wins) -------------------
-__device__ __forceinline__ void argmax16(float& v, int& i) {
+// ---- one game per 32 lanes (half a wave), one action per lane; jnp.argmax tie-break (first index) ----
+__device__ __forceinline__ void row_argmax(float& v, int& i) {
 #pragma unroll
-  for (int m = 8; m >= 1; m >>= 1) {
-    const float ov = __shfl_xor(v, m, 16);
-    const int oi = __shfl_xor(i, m, 16);
+  for (int m = 16; m >= 1; m >>= 1) {
+    const float ov = __shfl_xor(v, m, 32);
+    const int oi = __shfl_xor(i, m, 32);
     if (ov > v || (ov == v && oi < i)) {
       v = ov;
       i = oi;
     }
   }
-}
-__device__ __forceinline__ int isum16(int v) {
-  v += __shfl_xor(v, 8, 16);
-  v += __shfl_xor(v, 4, 16);
-  v += __shfl_xor(v, 2, 16);
-  v += __shfl_xor(v, 1, 16);
-  return v;
-}
-__device__ __forceinline__ int imax16(int v) {
-  v = max(v, __shfl_xor(v, 8, 16));
-  v = max(v, __shfl_xor(v, 4, 16));
-  v = max(v, __shfl_xor(v, 2, 16));
-  v = max(v, __shfl_xor(v, 1, 16));
-  return v;
 }
 
 // seq_halving.get_sequence_of_considered_visits(m, S)[idx] without the table.
@@ -101,68 +87,34 @@ __device__ __forceinline__ int considered_visit(int m, int S, int idx) {
   return v;
 }
 
-// qtransform_completed_by_mix_value over one node's children held as (a0 = sub, a1 = sub + 16).
-struct Kids {
-  float prior[2], value[2], reward[2], disc[2];
-  int visits[2], index[2];
-  bool ok[2];   // action < A
+// One child edge of the current node, held by lane `a` of the game's 32 lanes (ok = a < A).
+struct Kid {
+  float prior, value, reward, disc;
+  int visits, index;
+  bool ok;
 };
 
-__device__ __forceinline__ void completed_q(const Kids& k, float raw, const SearchArgs& sa, float (&cq)[2],
-                                            int& sumv, float& pmax) {
-  float q[2];
-  float pm = -INFINITY;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    q[h] = k.reward[h] + k.disc[h] * k.value[h];
-    if (k.ok[h]) pm = fmaxf(pm, k.prior[h]);
-  }
-  pm = row_max16(pm);
-  float e[2], es = 0.f;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    e[h] = k.ok[h] ? expf(k.prior[h] - pm) : 0.f;
-    es += e[h];
-  }
-  es = row_sum16(es);
-  int sv = 0, mv = 0;
-  float sp = 0.f;
-  float pp[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    pp[h] = fmaxf(kTiny, e[h] / es);
-    if (k.ok[h]) {
-      sv += k.visits[h];
-      mv = max(mv, k.visits[h]);
-      if (k.visits[h] > 0) sp += pp[h];
-    }
-  }
-  sv = isum16(sv);
-  mv = imax16(mv);
-  sp = row_sum16(sp);
-  float wq = 0.f;
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-    if (k.ok[h] && k.visits[h] > 0) wq += pp[h] * q[h] / sp;
-  wq = row_sum16(wq);
+// qtransform_completed_by_mix_value (value_scale, maxvisit_init, rescale, mixed value, eps 1e-8).
+__device__ __forceinline__ float completed_q(const Kid& k, float raw, const SearchArgs& sa, int& sumv, float& pmax) {
+  const float q = k.reward + k.disc * k.value;
+  const float pm = row_max(k.ok ? k.prior : -INFINITY);
+  const float e = k.ok ? expf(k.prior - pm) : 0.f;
+  const float es = row_sum(e);
+  const float pp = fmaxf(kTiny, e / es);
+  const bool vis = k.ok && k.visits > 0;
+  const int sv = row_isum(k.ok ? k.visits : 0);
+  const int mv = row_imax(k.ok ? k.visits : 0);
+  const float sp = row_sum(vis ? pp : 0.f);
+  const float wq = row_sum(vis ? pp * q / sp : 0.f);
   const float mixed = (raw + (float)sv * wq) / (float)(sv + 1);
-  float lo = INFINITY, hi = -INFINITY;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    cq[h] = (k.visits[h] > 0) ? q[h] : mixed;
-    if (k.ok[h]) {
-      lo = fminf(lo, cq[h]);
-      hi = fmaxf(hi, cq[h]);
-    }
-  }
-  lo = row_min16(lo);
-  hi = row_max16(hi);
+  float cq = vis ? q : mixed;
+  const float lo = row_min(k.ok ? cq : INFINITY);
+  const float hi = row_max(k.ok ? cq : -INFINITY);
   const float den = fmaxf(hi - lo, 1e-8f);
   const float scale = (sa.maxvisit_init + (float)mv) * sa.value_scale;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) cq[h] = scale * ((cq[h] - lo) / den);
   sumv = sv;
   pmax = pm;
+  return scale * ((cq - lo) / den);
 }
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
@@ -180,15 +132,11 @@ __device__ __forceinline__ float gumbel_noise(unsigned long long seed, int gid, 
   return -logf(-logf(u));
 }
 
-__global__ __launch_bounds__(256, 1) void k_gumbel_search(muz_net_w Wt, SearchArgs sa, const float* __restrict__ root_logits,
-                                                          const float* __restrict__ root_value,
-                                                          const float* __restrict__ root_emb,
-                                                          const uint32_t* __restrict__ legal,
-                                                          const float* __restrict__ gumbel_in,
-                                                          const int32_t* __restrict__ game_id, int n,
-                                                          const int* __restrict__ n_dev, TreeWs T,
-                                                          int32_t* out_action, float* out_weights,
-                                                          float* out_value) {
+__global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
+    muz_net_w Wt, SearchArgs sa, const float* __restrict__ root_logits, const float* __restrict__ root_value,
+    const float* __restrict__ root_emb, const uint32_t* __restrict__ legal, const float* __restrict__ gumbel_in,
+    const int32_t* __restrict__ game_id, int n, const int* __restrict__ n_dev, TreeWs T, int32_t* out_action,
+    float* out_weights, float* out_value) {
   __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
   __shared__ int s_visits[kRows][kMaxNodes];
   __shared__ float s_raw[kRows][kMaxNodes];
@@ -198,137 +146,97 @@ __global__ __launch_bounds__(256, 1) void k_gumbel_search(muz_net_w Wt, SearchAr
   __shared__ int p_cvis[kRows][kMaxDepth];
   __shared__ float p_rew[kRows][kMaxDepth];
   __shared__ float p_disc[kRows][kMaxDepth];
-  __shared__ float s_gum[kRows][MUZ_DET_ACTIONS];
-  __shared__ int s_act[kRows], s_parent[kRows], s_next[kRows], s_depth[kRows], s_ncons[kRows];
-  __shared__ unsigned s_legal[kRows];
+  __shared__ int s_act[kRows], s_parent[kRows], s_next[kRows], s_depth[kRows];
 
   if (n_dev) n = *n_dev;
   if ((int)blockIdx.x * kRows >= n) return;
   const Arena ar = Arena::carve(smem);
   const int A = Wt.num_actions;
-  const int row = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int row = trow(), a = tsub();      // this lane holds action `a` of game `row`
   const int g = blockIdx.x * kRows + row;
   const bool valid = g < n;
-  const int a0 = sub, a1 = sub + 16;
-  const bool ok1 = a1 < A;
+  const bool ok = a < A;
+  const int ai = ok ? a : 0;              // in-bounds alias for lanes a >= A
 
   // ---------------- root: instantiate_tree_from_root with masked logits (policies.py _mask_invalid_actions)
+  unsigned lb = 0;
+  int ncons = 0;
+  float gum = 0.f;
   if (valid) {
-    const unsigned lb = legal[g];
+    lb = legal[g];
     const int gid = game_id ? game_id[g] : g;
-    float l0 = root_logits[(size_t)g * A + a0];
-    float l1 = ok1 ? root_logits[(size_t)g * A + a1] : -INFINITY;
-    const float lm = row_max16(fmaxf(l0, l1));
-    const bool inv0 = ((lb >> a0) & 1u) == 0u, inv1 = !ok1 || ((lb >> a1) & 1u) == 0u;
-    l0 = inv0 ? kFMin : l0 - lm;
-    l1 = inv1 ? kFMin : l1 - lm;
-    const size_t b0 = T.ca(g, 0, 0);
-    T.c_prior[b0 + a0] = l0;
-    T.c_index[b0 + a0] = -1;
-    T.c_visits[b0 + a0] = 0;
-    T.c_value[b0 + a0] = 0.f;
-    T.c_reward[b0 + a0] = 0.f;
-    T.c_disc[b0 + a0] = 0.f;
-    if (ok1) {
-      T.c_prior[b0 + a1] = l1;
-      T.c_index[b0 + a1] = -1;
-      T.c_visits[b0 + a1] = 0;
-      T.c_value[b0 + a1] = 0.f;
-      T.c_reward[b0 + a1] = 0.f;
-      T.c_disc[b0 + a1] = 0.f;
+    const float l = ok ? root_logits[(size_t)g * A + ai] : -INFINITY;
+    const float lm = row_max(l);
+    const bool inv = !ok || ((lb >> a) & 1u) == 0u;
+    const size_t b0 = T.ca(g, 0, ai);
+    if (ok) {
+      T.c_prior[b0] = inv ? kFMin : l - lm;
+      T.c_index[b0] = -1;
+      T.c_visits[b0] = 0;
+      T.c_value[b0] = 0.f;
+      T.c_reward[b0] = 0.f;
+      T.c_disc[b0] = 0.f;
+      gum = gumbel_in ? gumbel_in[(size_t)g * A + ai] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, sa.turn, ai);
     }
-    s_gum[row][a0] = gumbel_in ? gumbel_in[(size_t)g * A + a0] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, sa.turn, a0);
-    if (ok1)
-      s_gum[row][a1] = gumbel_in ? gumbel_in[(size_t)g * A + a1] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, sa.turn, a1);
     float* e0 = T.e(g, 0);
-    for (int c = sub; c < LAT; c += 16) e0[c] = root_emb[(size_t)g * LAT + c];
-    if (sub == 0) {
+    for (int c = a; c < LAT; c += kRowLanes) e0[c] = root_emb[(size_t)g * LAT + c];
+    ncons = min(sa.max_considered, __popc(lb & ((1u << A) - 1u)));
+    if (a == 0) {
       const float v = root_value[g];
       s_visits[row][0] = 1;
       s_raw[row][0] = v;
       s_val[row][0] = v;
-      s_legal[row] = lb;
-      s_ncons[row] = min(sa.max_considered, __popc(lb & ((1u << A) - 1u)));
     }
   }
   __syncthreads();
+
+  // one node's children for this lane
+  auto load_kid = [&](int node) {
+    Kid k;
+    const size_t e = T.ca(g, node, ai);
+    k.ok = ok;
+    k.prior = T.c_prior[e];
+    k.value = T.c_value[e];
+    k.reward = T.c_reward[e];
+    k.disc = T.c_disc[e];
+    k.visits = ok ? T.c_visits[e] : 0;
+    k.index = T.c_index[e];
+    return k;
+  };
 
 #pragma unroll 1
   for (int sim = 0; sim < sa.S; ++sim) {
     // ---------------- simulate (search.py simulate): walk from the root
     if (valid) {
       int node = 0, depth = 0, act = 0, nxt = -1;
-      const unsigned lb = s_legal[row];
       while (true) {
-        Kids k;
-        const size_t base = T.ca(g, node, 0);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int a = h ? a1 : a0;
-          k.ok[h] = h ? ok1 : true;
-          const int ai = k.ok[h] ? a : a0;
-          k.prior[h] = T.c_prior[base + ai];
-          k.value[h] = T.c_value[base + ai];
-          k.reward[h] = T.c_reward[base + ai];
-          k.disc[h] = T.c_disc[base + ai];
-          k.visits[h] = k.ok[h] ? T.c_visits[base + ai] : 0;
-          k.index[h] = T.c_index[base + ai];
-        }
-        float cq[2];
+        const Kid k = load_kid(node);
         int sumv;
         float pmax;
-        completed_q(k, s_raw[row][node], sa, cq, sumv, pmax);
-        float sc[2];
+        const float cq = completed_q(k, s_raw[row][node], sa, sumv, pmax);
+        float sc;
         if (depth == 0) {
-          // gumbel_muzero_root_action_selection + seq_halving.score_considered + masked_argmax
-          const int cv = considered_visit(s_ncons[row], sa.S, sumv);
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int a = h ? a1 : a0;
-            const float s = fmaxf(-1e9f, s_gum[row][k.ok[h] ? a : a0] + (k.prior[h] - pmax) + cq[h]) +
-                            (k.visits[h] == cv ? 0.f : -INFINITY);
-            const bool inv = !k.ok[h] || ((lb >> a) & 1u) == 0u;
-            sc[h] = inv ? -INFINITY : s;
-          }
+          // gumbel_muzero_root_action_selection: score_considered + masked_argmax
+          const int cv = considered_visit(ncons, sa.S, sumv);
+          const float s = fmaxf(-1e9f, gum + (k.prior - pmax) + cq) + (k.visits == cv ? 0.f : -INFINITY);
+          sc = (!ok || ((lb >> a) & 1u) == 0u) ? -INFINITY : s;
         } else {
           // gumbel_muzero_interior_action_selection: softmax(prior + cq) - N / (1 + sum N)
-          float z[2], zm = -INFINITY;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            z[h] = k.prior[h] + cq[h];
-            if (k.ok[h]) zm = fmaxf(zm, z[h]);
-          }
-          zm = row_max16(zm);
-          float ez[2], zs = 0.f;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            ez[h] = k.ok[h] ? expf(z[h] - zm) : 0.f;
-            zs += ez[h];
-          }
-          zs = row_sum16(zs);
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            sc[h] = k.ok[h] ? (ez[h] / zs - (float)k.visits[h] / (float)(1 + sumv)) : -INFINITY;
+          const float z = k.prior + cq;
+          const float zm = row_max(ok ? z : -INFINITY);
+          const float ez = ok ? expf(z - zm) : 0.f;
+          const float zs = row_sum(ez);
+          sc = ok ? (ez / zs - (float)k.visits / (float)(1 + sumv)) : -INFINITY;
         }
-        float bv = sc[0];
-        int bi = a0;
-        if (ok1 && (sc[1] > bv)) {
-          bv = sc[1];
-          bi = a1;
-        }
-        argmax16(bv, bi);
-        const int owner = bi & 15;
-        const bool hi = bi >= 16;
-        const int child = __shfl(hi ? k.index[1] : k.index[0], owner, 16);
-        const float rw = __shfl(hi ? k.reward[1] : k.reward[0], owner, 16);
-        const float dc = __shfl(hi ? k.disc[1] : k.disc[0], owner, 16);
-        const int cvis = __shfl(hi ? k.visits[1] : k.visits[0], owner, 16);
-        if (sub == 0) {
+        int bi = a;
+        row_argmax(sc, bi);
+        const int child = __shfl(k.index, bi, 32);
+        if (a == bi) {
           p_node[row][depth] = node;
           p_act[row][depth] = bi;
-          p_rew[row][depth] = rw;
-          p_disc[row][depth] = dc;
-          p_cvis[row][depth] = cvis;
+          p_rew[row][depth] = k.reward;
+          p_disc[row][depth] = k.disc;
+          p_cvis[row][depth] = k.visits;
         }
         act = bi;
         nxt = child;
@@ -336,55 +244,52 @@ __global__ __launch_bounds__(256, 1) void k_gumbel_search(muz_net_w Wt, SearchAr
         if (child == -1 || depth >= sa.D) break;
         node = child;
       }
-      if (sub == 0) {
+      if (a == 0) {
         s_parent[row] = node;
         s_act[row] = act;
         s_next[row] = (nxt == -1) ? sim + 1 : nxt;
         s_depth[row] = depth;
       }
-    } else if (sub == 0) {
+    } else if (a == 0) {
       s_act[row] = 0;
     }
     __syncthreads();
     // ---------------- expand (search.py expand): parent embedding -> recurrent_fn
     {
       const float* pe = valid ? T.e(g, s_parent[row]) : nullptr;
-      for (int c = sub; c < LAT; c += 16) ar.L[row * LD + c] = valid ? pe[c] : 0.f;
+      for (int c = a; c < LAT; c += kRowLanes) ar.L[row * LD + c] = valid ? pe[c] : 0.f;
     }
     __syncthreads();
-    // Launder the weight table once per simulation so the compiler re-derives the ~60 layer
-    // addresses inside the loop instead of pinning them in registers across it.
-    // (Wt is kernel argument 0, so it sits at offset 0 of the kernarg segment.)
+    // Launder the weight table once per simulation so the compiler re-derives the layer addresses
+    // inside the loop instead of pinning them in registers across it.  (Wt is kernel argument 0,
+    // so it sits at offset 0 of the kernarg segment.)
     const muz_net_w* wl = (const muz_net_w*)(__builtin_amdgcn_kernarg_segment_ptr());
     asm volatile("" : "+s"(wl));
     dyn16(wl->dyn, A, s_act, ar);
     const int nx = s_next[row];
     if (valid) {
       float* ne = T.e(g, nx);
-      for (int c = sub; c < LAT; c += 16) ne[c] = ar.T[row * LD + c];
+      for (int c = a; c < LAT; c += kRowLanes) ne[c] = ar.T[row * LD + c];
     }
     __syncthreads();
     pred16(wl->pred, A, ar.T, ar);
     if (valid) {
       const bool fresh = nx == sim + 1;
-      const size_t nb = T.ca(g, nx, 0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int a = h ? a1 : a0;
-        if (h && !ok1) break;
-        T.c_prior[nb + a] = ar.U[row * LD + a];
+      if (ok) {
+        const size_t nb = T.ca(g, nx, a);
+        T.c_prior[nb] = ar.U[row * LD + a];
         if (fresh) {
-          T.c_index[nb + a] = -1;
-          T.c_visits[nb + a] = 0;
-          T.c_value[nb + a] = 0.f;
-          T.c_reward[nb + a] = 0.f;
-          T.c_disc[nb + a] = 0.f;
+          T.c_index[nb] = -1;
+          T.c_visits[nb] = 0;
+          T.c_value[nb] = 0.f;
+          T.c_reward[nb] = 0.f;
+          T.c_disc[nb] = 0.f;
         }
       }
-      if (sub == 0) {
-        const int par = s_parent[row], act = s_act[row];
+      if (a == 0) {
+        const int par = s_parent[row], pa = s_act[row];
         const float v = ar.v0[row], rw = ar.v1[row], dc = ar.v2[row];
-        const size_t eb = T.ca(g, par, act);
+        const size_t eb = T.ca(g, par, pa);
         T.c_index[eb] = nx;
         T.c_reward[eb] = rw;
         T.c_disc[eb] = dc;
@@ -397,13 +302,13 @@ __global__ __launch_bounds__(256, 1) void k_gumbel_search(muz_net_w Wt, SearchAr
         const int d = s_depth[row];
         for (int lvl = d - 1; lvl >= 0; --lvl) {
           const int parent = p_node[row][lvl];
-          const int pa = p_act[row][lvl];
+          const int pact = p_act[row][lvl];
           const int cnt = s_visits[row][parent];
           const float r = (lvl == d - 1) ? rw : p_rew[row][lvl];
           const float dsc = (lvl == d - 1) ? dc : p_disc[row][lvl];
           leaf = r + dsc * leaf;
           const float pv = (s_val[row][parent] * (float)cnt + leaf) / ((float)cnt + 1.0f);
-          const size_t ei = T.ca(g, parent, pa);
+          const size_t ei = T.ca(g, parent, pact);
           T.c_value[ei] = s_val[row][idx];
           T.c_visits[ei] = p_cvis[row][lvl] + 1;
           s_val[row][parent] = pv;
@@ -415,71 +320,27 @@ __global__ __launch_bounds__(256, 1) void k_gumbel_search(muz_net_w Wt, SearchAr
     __syncthreads();
   }
 
-  // ---------------- final action (policies.py gumbel_muzero_policy tail)
+  // ---------------- final action + action_weights (policies.py gumbel_muzero_policy tail)
   if (valid) {
-    Kids k;
-    const size_t base = T.ca(g, 0, 0);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int a = h ? a1 : a0;
-      k.ok[h] = h ? ok1 : true;
-      const int ai = k.ok[h] ? a : a0;
-      k.prior[h] = T.c_prior[base + ai];
-      k.value[h] = T.c_value[base + ai];
-      k.reward[h] = T.c_reward[base + ai];
-      k.disc[h] = T.c_disc[base + ai];
-      k.visits[h] = k.ok[h] ? T.c_visits[base + ai] : 0;
-      k.index[h] = -1;
-    }
-    float cq[2];
+    const Kid k = load_kid(0);
     int sumv;
     float pmax;
-    completed_q(k, s_raw[row][0], sa, cq, sumv, pmax);
-    const unsigned lb = s_legal[row];
-    const int cv = imax16(max(k.visits[0], k.ok[1] ? k.visits[1] : 0));
-    float sc[2], z[2];
-    bool inv[2];
-    float zm = -INFINITY;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int a = h ? a1 : a0;
-      inv[h] = !k.ok[h] || ((lb >> a) & 1u) == 0u;
-      const float s = fmaxf(-1e9f, s_gum[row][k.ok[h] ? a : a0] + (k.prior[h] - pmax) + cq[h]) +
-                      (k.visits[h] == cv ? 0.f : -INFINITY);
-      sc[h] = inv[h] ? -INFINITY : s;
-      z[h] = k.prior[h] + cq[h];
-      if (k.ok[h]) zm = fmaxf(zm, z[h]);
-    }
-    float bv = sc[0];
-    int bi = a0;
-    if (ok1 && sc[1] > bv) {
-      bv = sc[1];
-      bi = a1;
-    }
-    argmax16(bv, bi);
+    const float cq = completed_q(k, s_raw[row][0], sa, sumv, pmax);
+    const bool inv = !ok || ((lb >> a) & 1u) == 0u;
+    const int cv = row_imax(k.visits);   // considered_visit = max(visit_counts)
+    float sc = fmaxf(-1e9f, gum + (k.prior - pmax) + cq) + (k.visits == cv ? 0.f : -INFINITY);
+    sc = inv ? -INFINITY : sc;
+    int bi = a;
+    row_argmax(sc, bi);
     // action_weights = softmax(_mask_invalid_actions(prior + completed_q))
-    zm = row_max16(zm);
-    float ez[2], zs = 0.f;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float zz = inv[h] ? kFMin : z[h] - zm;
-      ez[h] = k.ok[h] ? expf(zz - 0.f) : 0.f;
-    }
-    // softmax subtracts the max of the masked logits (<= 0 here; equals 0 unless all are invalid)
-    float mm = -INFINITY;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      if (k.ok[h]) mm = fmaxf(mm, inv[h] ? kFMin : z[h] - zm);
-    mm = row_max16(mm);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      ez[h] = k.ok[h] ? expf((inv[h] ? kFMin : z[h] - zm) - mm) : 0.f;
-      zs += ez[h];
-    }
-    zs = row_sum16(zs);
-    out_weights[(size_t)g * A + a0] = ez[0] / zs;
-    if (ok1) out_weights[(size_t)g * A + a1] = ez[1] / zs;
-    if (sub == 0) {
+    const float z = k.prior + cq;
+    const float zm = row_max(ok ? z : -INFINITY);
+    const float zz = inv ? kFMin : z - zm;
+    const float mm = row_max(ok ? zz : -INFINITY);
+    const float ez = ok ? expf(zz - mm) : 0.f;
+    const float zs = row_sum(ez);
+    if (ok) out_weights[(size_t)g * A + a] = ez / zs;
+    if (a == 0) {
       out_action[g] = bi;
       out_value[g] = s_val[row][0];
     }
@@ -496,8 +357,8 @@ int launch_gumbel_search(const muz_net_w& w, const SearchArgs& sa, const float* 
                          int n, const int* n_dev, void* workspace, int32_t* action, float* weights, float* value,
                          hipStream_t s) {
   TreeWs T = carve_ws(workspace, n, sa.S + 1);
-  k_gumbel_search<<<(n + kRows - 1) / kRows, 256, 0, s>>>(w, sa, root_logits, root_value, root_emb, legal, gumbel,
-                                                          game_id, n, n_dev, T, action, weights, value);
+  k_gumbel_search<<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, sa, root_logits, root_value, root_emb, legal,
+                                                               gumbel, game_id, n, n_dev, T, action, weights, value);
   return muz_last_launch_error();
 }
 

@@ -19,6 +19,7 @@ from . import lib as _L
 from .lib import MuzNetW  # struct layout of include/muz.h
 
 LATENT = 256
+NW = 8   # waves per 16-row tile workgroup (csrc/nn.hpp kWaves): column groups of the packed layers
 
 
 # ---------------------------------------------------------------------------------- parameters
@@ -111,8 +112,10 @@ class DeviceNet:
         w = MuzNetW()
         w.obs_channels, w.num_actions = self.C, self.A
 
-        def dense(name, nw=4, nt=4):
-            return (put(pack_dense(P[f"{name}/kernel"], nw, nt)), put(P[f"{name}/bias"]))
+        def dense(name, nw=NW, nt=None):
+            k = P[f"{name}/kernel"]
+            nt = nt if nt is not None else -(-k.shape[1] // (16 * nw))
+            return (put(pack_dense(k, nw, nt)), put(P[f"{name}/bias"]))
 
         def ln(name):
             return (put(P[f"{name}/scale"]), put(P[f"{name}/bias"]))
@@ -128,28 +131,28 @@ class DeviceNet:
             ln1=ln(f"{r}/LayerNorm_1"),
             conv2=(put(pack_dense(P[f"{r}/Conv_2/kernel"].reshape(320, 64), 1, 4)), put(P[f"{r}/Conv_2/bias"])),
             ln2=ln(f"{r}/LayerNorm_2"), d0=dense(f"{r}/Dense_0"), ln3=ln(f"{r}/LayerNorm_3"),
-            d1=dense(f"{r}/Dense_1", 4, 1), ln4=ln(f"{r}/LayerNorm_4"), d2=dense(f"{r}/Dense_2", 4, 1),
+            d1=dense(f"{r}/Dense_1"), ln4=ln(f"{r}/LayerNorm_4"), d2=dense(f"{r}/Dense_2"),
             ln5=ln(f"{r}/LayerNorm_5"), d3=dense(f"{r}/Dense_3"), ln6=ln(f"{r}/LayerNorm_6"),
             rb=[rb(f"{r}/ResBlock_{i}") for i in range(6)], d4=dense(f"{r}/Dense_4"))}
         A = self.A
         k6, k7 = P[f"{d}/Dense_6/kernel"], P[f"{d}/Dense_7/kernel"]
         spec["dyn"] = dict(
             d0=(put(P[f"{d}/Dense_0/kernel"]), put(P[f"{d}/Dense_0/bias"])), ln0=ln(f"{d}/LayerNorm_0"),
-            d12=(put(pack_dense(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1), 4, 8)),
+            d12=(put(pack_dense(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1), NW, 4)),
                  put(np.concatenate([P[f"{d}/Dense_1/bias"], P[f"{d}/Dense_2/bias"]]))),
             d3=dense(f"{d}/Dense_3"), ln1=ln(f"{d}/LayerNorm_1"), d4=dense(f"{d}/Dense_4"),
             ln2=ln(f"{d}/LayerNorm_2"), rb=[rb(f"{d}/ResBlock_{i}") for i in range(2)], d5=dense(f"{d}/Dense_5"),
-            d67=(put(pack_dense(np.concatenate([k6[:LATENT], k7[:LATENT]], 1), 4, 2)),
+            d67=(put(pack_dense(np.concatenate([k6[:LATENT], k7[:LATENT]], 1), NW, 1)),
                  put(np.concatenate([P[f"{d}/Dense_6/bias"], P[f"{d}/Dense_7/bias"]]))),
             d67_onehot=put(np.concatenate([k6[LATENT:LATENT + A], k7[LATENT:LATENT + A]], 1)),
             reward_head=(put(P[f"{d}/reward_head/kernel"]), put(P[f"{d}/reward_head/bias"])),
             discount_head=(put(P[f"{d}/discount_head/kernel"]), put(P[f"{d}/discount_head/bias"])))
         spec["pred"] = dict(
             ln0=ln(f"{p}/LayerNorm_0"), rb=[rb(f"{p}/ResBlock_{i}") for i in range(2)],
-            d03=(put(pack_dense(np.concatenate([P[f"{p}/Dense_0/kernel"], P[f"{p}/Dense_3/kernel"]], 1), 4, 6)),
+            d03=(put(pack_dense(np.concatenate([P[f"{p}/Dense_0/kernel"], P[f"{p}/Dense_3/kernel"]], 1), NW, 3)),
                  put(np.concatenate([P[f"{p}/Dense_0/bias"], P[f"{p}/Dense_3/bias"]]))),
-            ln1=ln(f"{p}/LayerNorm_1"), d1=dense(f"{p}/Dense_1", 4, 2), ln2=ln(f"{p}/LayerNorm_2"),
-            d2=dense(f"{p}/Dense_2", 4, 1), ln3=ln(f"{p}/LayerNorm_3"), d4=dense(f"{p}/Dense_4", 4, 1),
+            ln1=ln(f"{p}/LayerNorm_1"), d1=dense(f"{p}/Dense_1"), ln2=ln(f"{p}/LayerNorm_2"),
+            d2=dense(f"{p}/Dense_2"), ln3=ln(f"{p}/LayerNorm_3"), d4=dense(f"{p}/Dense_4"),
             d5=(put(P[f"{p}/Dense_5/kernel"]), put(P[f"{p}/Dense_5/bias"])))
         host = np.concatenate(self._chunks) if self._chunks else np.zeros(4, np.float32)
         self.buffer = torch.from_numpy(host).to(device)
