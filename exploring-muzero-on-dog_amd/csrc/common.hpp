@@ -39,6 +39,29 @@ __device__ __forceinline__ int jidx(int i, int n) {
   return i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
 }
 
+// Address-space qualifiers.  Pointers loaded from structs are generic ("flat") to the compiler;
+// flat loads count on BOTH vmcnt and lgkmcnt, so every LDS wait would also wait for in-flight weight
+// loads.  Weight tables are therefore read through the kernarg segment (AS4 -> scalar loads) and
+// every global array through an AS1 (global) pointer.
+#define AS1 __attribute__((address_space(1)))
+#define AS4 __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ const AS1 T* gp(const T* p) {
+  return (const AS1 T*)p;
+}
+template <class T>
+__device__ __forceinline__ AS1 T* gpw(T* p) {
+  return (AS1 T*)p;
+}
+// kernel argument 0 seen through the kernarg segment (scalar loads), laundered so the compiler
+// re-reads fields at the point of use instead of pinning them all in registers.
+template <class T>
+__device__ __forceinline__ const AS4 T* kernarg0() {
+  const AS4 T* p = (const AS4 T*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // Dynamic index into a small register array without a scratch round trip.
 template <int N>
 __device__ __forceinline__ int rsel(const int (&a)[N], int i) {

@@ -14,7 +14,7 @@ constexpr int kPreLd = 64 + 4;
 
 // LayerNorm over channels for 56 positions, 4 lanes per position.
 template <int N>
-__device__ __forceinline__ void ln_positions(const float* pre, float* out, int out_row0, const muz_ln& P) {
+__device__ __forceinline__ void ln_positions(const float* pre, float* out, int out_row0, const AS4 muz_ln& P) {
   const int pos = threadIdx.x >> 2, q = threadIdx.x & 3;
   if (pos >= 56) return;
   constexpr int PER = N / 4;
@@ -34,12 +34,12 @@ __device__ __forceinline__ void ln_positions(const float* pre, float* out, int o
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = q + 4 * i;
-    out[(out_row0 + pos) * N + c] = fmaxf((v[i] - mean) * (inv * P.scale[c]) + P.bias[c], 0.f);
+    out[(out_row0 + pos) * N + c] = fmaxf((v[i] - mean) * (inv * gp(P.scale)[c]) + gp(P.bias)[c], 0.f);
   }
 }
 
 template <int KB>
-__device__ __forceinline__ void conv_mfma(const muz_dense& L, const float* in, int cin, float* pre) {
+__device__ __forceinline__ void conv_mfma(const AS4 muz_dense& L, const float* in, int cin, float* pre) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   f32x4 acc[4];
 #pragma unroll
@@ -49,16 +49,17 @@ __device__ __forceinline__ void conv_mfma(const muz_dense& L, const float* in, i
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int col = t * 16 + r;
-    const float bb = L.b[col];
+    const float bb = gp(L.b)[col];
 #pragma unroll
     for (int i = 0; i < 4; ++i) pre[(wv * 16 + 4 * g + i) * kPreLd + col] = acc[t][i] + bb;
   }
 }
 
-__global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w R, const float* __restrict__ obs, int C, int n,
+__global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float* __restrict__ obs, int C, int n,
                                                    const int* __restrict__ n_dev, float* __restrict__ convout) {
   if (n_dev) n = *n_dev;
   if ((int)blockIdx.x >= n) return;
+  const AS4 muz_repr_w& R = *kernarg0<muz_repr_w>();   // == Rarg, read through the kernarg segment
   __shared__ __attribute__((aligned(16))) float in0[58 * 6];
   __shared__ __attribute__((aligned(16))) float c1in[66 * 32];
   __shared__ __attribute__((aligned(16))) float pre[kConvRowsPad * kPreLd];
@@ -80,8 +81,8 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w R, const float* __
 #pragma unroll
     for (int dk = 0; dk < 3; ++dk)
 #pragma unroll
-      for (int ci = 0; ci < 6; ++ci) s += in0[(w + dk) * 6 + ci] * R.conv0.w[(dk * 6 + ci) * 32 + co];
-    pre[w * kPreLd + co] = s + R.conv0.b[co];
+      for (int ci = 0; ci < 6; ++ci) s += in0[(w + dk) * 6 + ci] * gp(R.conv0.w)[(dk * 6 + ci) * 32 + co];
+    pre[w * kPreLd + co] = s + gp(R.conv0.b)[co];
   }
   __syncthreads();
   ln_positions<32>(pre, c1in, 1, R.ln0);   // pad 1 row on each side for k=3
@@ -107,7 +108,8 @@ __global__ __launch_bounds__(kThreads) void k_root_dense(muz_net_w Wt, const flo
   if ((int)blockIdx.x * kRows >= n) return;
   __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
   const Arena a = Arena::carve(smem);
-  const muz_repr_w& R = Wt.repr;
+  const AS4 muz_net_w* W = kernarg0<muz_net_w>();   // == Wt, read through the kernarg segment
+  const AS4 muz_repr_w& R = W->repr;
   const int C = Wt.obs_channels, A = Wt.num_actions;
   const int g0 = blockIdx.x * kRows;
   const int row = trow(), sub = tsub();
@@ -117,31 +119,34 @@ __global__ __launch_bounds__(kThreads) void k_root_dense(muz_net_w Wt, const flo
   const int Kg = C - 6;
   a.E[row * LDE + sub] = (valid && sub < Kg) ? obs[((size_t)gr * C + 6 + sub) * 56] : 0.f;
   // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16)
-  dense16<2>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW);
+  Pf pf;
+  pf_issue<2>(pf, &R.d0, 3584, LAT);
+  dense16<2, 1>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW, pf, &R.d1, Kg, 64, true);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, R.ln3);
-  dense16<1>(R.d1, Kg, 64, a.E, LDE, a.X, LD);
+  dense16<1, 1>(R.d1, Kg, 64, a.E, LDE, a.X, LD, pf, &R.d2, 64, 64);
   __syncthreads();
   ln16<64, LN_RELU>(a.X, LD, a.X, LD, R.ln4);
   __syncthreads();
-  dense16<1>(R.d2, 64, 64, a.X, LD, a.W + 256, LDW);
+  dense16<1, 2>(R.d2, 64, 64, a.X, LD, a.W + 256, LDW, pf, &R.d3, 320, LAT);
   __syncthreads();
   ln16<64, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, R.ln5);
   __syncthreads();
-  dense16<2>(R.d3, 320, LAT, a.W, LDW, a.X, LD);
+  dense16<2, 2>(R.d3, 320, LAT, a.W, LDW, a.X, LD, pf, &R.rb[0].d0, LAT, LAT);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, R.ln6);
   __syncthreads();
 #pragma unroll 1
-  for (int b = 0; b < 6; ++b) resblock16(R.rb[b], a.X, a.T, a.U);
-  dense16<2>(R.d4, LAT, LAT, a.X, LD, a.T, LD);
+  for (int b = 0; b < 6; ++b)
+    resblock16<2>(R.rb[b], a.X, a.T, a.U, pf, b < 5 ? &R.rb[b + 1].d0 : &R.d4, LAT, LAT);
+  dense16<2, 2>(R.d4, LAT, LAT, a.X, LD, a.T, LD, pf, &W->pred.rb[0].d0, LAT, LAT);
   __syncthreads();
   minmax16(a.T, LD);
   __syncthreads();
   if (valid)
     for (int c = sub; c < LAT; c += kRowLanes) embedding[(size_t)gr * LAT + c] = a.T[row * LD + c];
   __syncthreads();
-  pred16(Wt.pred, A, a.T, a);
+  pred16<1>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
   if (valid) {
     for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
     if (sub == 0) value[gr] = a.v0[row];
@@ -163,8 +168,11 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
   const bool valid = gr < n;
   for (int c = sub; c < LAT; c += kRowLanes) a.L[row * LD + c] = valid ? emb[(size_t)gr * LAT + c] : 0.f;
   if (sub == 0) act[row] = valid ? action[gr] : 0;
+  const AS4 muz_net_w* W = kernarg0<muz_net_w>();   // == Wt, read through the kernarg segment
+  Pf pf;
+  pf_issue<4>(pf, &W->dyn.d12, 64, 512);
   __syncthreads();
-  dyn16(Wt.dyn, A, act, a);
+  dyn16<2>(W->dyn, A, act, a, pf, &W->pred.rb[0].d0, LAT, LAT);
   if (valid) {
     for (int c = sub; c < LAT; c += kRowLanes) next_emb[(size_t)gr * LAT + c] = a.T[row * LD + c];
     if (sub == 0) {
@@ -173,7 +181,7 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
     }
   }
   __syncthreads();
-  pred16(Wt.pred, A, a.T, a);
+  pred16<1>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
   if (valid) {
     for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
     if (sub == 0) value[gr] = a.v0[row];

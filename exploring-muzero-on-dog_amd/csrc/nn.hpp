@@ -26,30 +26,28 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 }
 
 // acc[t] += A[16 rows][K] @ Wgroup[K][NT*16]  (KB = K/16 k-blocks; Wg = packed weights of this group).
-// Weights for k-blocks kb+1 and kb+2 are in flight while kb is multiplied (3-deep register ring,
-// written out as a 3-way unrolled loop so every buffer index is a compile-time constant).
-template <int NT>
-__device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB, const float* A, int lda,
-                                            f32x4 (&acc)[NT]) {
+// b0 / b1 hold k-blocks 0 and 1 on entry.  Weights for k-blocks kb+1 and kb+2 are in flight while kb is
+// multiplied (3-deep register ring, written as a 3-way unrolled loop so every index is static).
+template <int NT, bool AG>
+__device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int KB, const float* A, int lda,
+                                               f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT]) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
-  const f32x4* wp = reinterpret_cast<const f32x4*>(Wg) + lane * NT;
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(Wg)) + lane * NT;
   const int wstep = 64 * NT;   // f32x4 per k-block
   const float* ap = A + r * lda + 4 * g;
-  f32x4 b0[NT], b1[NT], b2[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) b0[t] = wp[t];
-  if (KB > 1) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) b1[t] = wp[wstep + t];
-  }
+  auto lda4 = [&](int kb) -> f32x4 {
+    if constexpr (AG) return *gp(reinterpret_cast<const f32x4*>(ap + kb * 16));
+    else return *reinterpret_cast<const f32x4*>(ap + kb * 16);
+  };
+  f32x4 b2[NT];
   // step kb: issue k-block kb+2 into `nxt` (the buffer consumed at step kb-1), multiply `cur` (= kb)
   auto step = [&](int kb, const f32x4 (&cur)[NT], f32x4 (&nxt)[NT]) {
     if (kb + 2 < KB) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) nxt[t] = wp[(kb + 2) * wstep + t];
     }
-    const f32x4 a = *reinterpret_cast<const f32x4*>(ap + kb * 16);
+    const f32x4 a = lda4(kb);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -65,25 +63,85 @@ __device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB
   if (kb + 1 < KB) step(kb + 1, b1, b0);
 }
 
-// Dense layer over the tile: out[16][N] = A @ W + b, waves split N (NT tiles of 16 columns each).
-// A may live in LDS or global memory.  Caller synchronises before/after.
 template <int NT>
-__device__ __forceinline__ void dense16(const muz_dense& L, int K, int N, const float* A, int lda, float* out,
-                                        int ldo) {
+__device__ __forceinline__ void mfma_ring(const float* __restrict__ Wg, int KB, const float* A, int lda,
+                                          f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT], bool a_global) {
+  if (a_global)
+    mfma_ring_impl<NT, true>(Wg, KB, A, lda, acc, b0, b1);
+  else
+    mfma_ring_impl<NT, false>(Wg, KB, A, lda, acc, b0, b1);
+}
+
+template <int NT>
+__device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB, const float* A, int lda,
+                                            f32x4 (&acc)[NT]) {
+  const int lane = threadIdx.x & 63;
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(Wg)) + lane * NT;
+  f32x4 b0[NT], b1[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    b0[t] = wp[t];
+    b1[t] = KB > 1 ? wp[64 * NT + t] : b0[t];
+  }
+  mfma_ring_impl<NT, false>(Wg, KB, A, lda, acc, b0, b1);
+}
+
+// ---- cross-layer weight prefetch ----------------------------------------------------------------
+// Every dense layer issues the first two k-blocks of the NEXT layer's weights for this wave before its
+// epilogue, so the loads fly across the epilogue, the barrier and the LayerNorm pass in between.
+constexpr int kPfMax = 4;
+struct Pf {
+  f32x4 v0[kPfMax], v1[kPfMax];
+};
+
+__device__ __forceinline__ const float* wave_group(const AS4 muz_dense& L, int KB, int NT) {
+  return L.w + (size_t)(threadIdx.x >> 6) * KB * 64 * NT * 4;
+}
+
+template <int NT>
+__device__ __forceinline__ void pf_issue(Pf& pf, const AS4 muz_dense* L, int K, int N) {
+  static_assert(NT <= kPfMax, "prefetch buffer too small");
+  if (!L) return;
+  const int KB = (K + 15) >> 4;
+  if ((threadIdx.x >> 6) * NT * 16 >= N) return;
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(wave_group(*L, KB, NT))) + (threadIdx.x & 63) * NT;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    pf.v0[t] = wp[t];
+    if (KB > 1) pf.v1[t] = wp[64 * NT + t];
+  }
+}
+
+// Dense layer over the tile: out[16][N] = A @ W + b, waves split N (NT tiles of 16 columns each).
+// `pf` holds this layer's first k-blocks on entry and the next layer's (Ln: K=Kn, N=Nn, NTN tiles)
+// on exit.  A may live in LDS or global memory.  Caller synchronises before/after.
+template <int NT, int NTN>
+__device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
+                                        int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
+                                        bool a_global = false) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int KB = (K + 15) >> 4;
   const int col0 = wv * NT * 16;
-  if (col0 >= N) return;
-  f32x4 acc[NT];
+  if (col0 >= N) {
+    pf_issue<NTN>(pf, Ln, Kn, Nn);
+    return;
+  }
+  f32x4 acc[NT], b0[NT], b1[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mfma_rows16<NT>(L.w + (size_t)wv * KB * 64 * NT * 4, KB, A, lda, acc);
+  for (int t = 0; t < NT; ++t) {
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    b0[t] = pf.v0[t];
+    b1[t] = pf.v1[t];
+  }
+  mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global);
+  pf_issue<NTN>(pf, Ln, Kn, Nn);
   const int r = lane & 15, g = lane >> 4;
+  const AS1 float* bias = gp(L.b);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = col0 + t * 16 + r;
     if (col < N) {
-      const float bb = L.b[col];
+      const float bb = bias[col];
 #pragma unroll
       for (int i = 0; i < 4; ++i) out[(4 * g + i) * ldo + col] = acc[t][i] + bb;
     }
@@ -124,9 +182,17 @@ enum LnMode { LN_PLAIN = 0, LN_RELU = 1, LN_RESID_RELU = 2 };
 // Flax LayerNorm (eps 1e-6, fast variance) of in[16][N] -> out.
 //   LN_PLAIN: out = y;  LN_RELU: out = relu(y);  LN_RESID_RELU: out = relu(out + y)  (ResBlock tail)
 template <int N, int MODE>
-__device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int ldo, const muz_ln& P) {
+__device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int ldo, const AS4 muz_ln& P) {
   constexpr int PER = N / kRowLanes;
   const int row = trow(), sub = tsub();
+  const AS1 float* scale = gp(P.scale);
+  const AS1 float* shift = gp(P.bias);
+  float sc[PER], sh[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {   // parameter loads first, so they overlap the statistics
+    sc[i] = scale[sub + kRowLanes * i];
+    sh[i] = shift[sub + kRowLanes * i];
+  }
   float v[PER];
   float s = 0.f, s2 = 0.f;
 #pragma unroll
@@ -144,7 +210,7 @@ __device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int l
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = sub + kRowLanes * i;
-    float y = (v[i] - mean) * (inv * P.scale[c]) + P.bias[c];
+    float y = (v[i] - mean) * (inv * sc[i]) + sh[i];
     if (MODE == LN_RELU) y = fmaxf(y, 0.f);
     if (MODE == LN_RESID_RELU) y = fmaxf(out[row * ldo + c] + y, 0.f);
     out[row * ldo + c] = y;
@@ -209,21 +275,25 @@ struct Arena {
 };
 
 // ResBlock (muzero_deterministic_madn.py:12-24): X <- relu(X + LN1(D1(relu(LN0(D0(X))))))
-__device__ __forceinline__ void resblock16(const muz_resblock& R, float* X, float* T, float* U) {
-  dense16<2>(R.d0, LAT, LAT, X, LD, T, LD);
+// pf: rb.d0 on entry, (Ln: Kn x Nn, NTN tiles) on exit.
+template <int NTN>
+__device__ __forceinline__ void resblock16(const AS4 muz_resblock& R, float* X, float* T, float* U, Pf& pf,
+                                           const AS4 muz_dense* Ln, int Kn, int Nn) {
+  dense16<2, 2>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT);
   __syncthreads();
   ln16<LAT, LN_RELU>(T, LD, T, LD, R.ln0);
   __syncthreads();
-  dense16<2>(R.d1, LAT, LAT, T, LD, U, LD);
+  dense16<2, NTN>(R.d1, LAT, LAT, T, LD, U, LD, pf, Ln, Kn, Nn);
   __syncthreads();
   ln16<LAT, LN_RESID_RELU>(U, LD, X, LD, R.ln1);
   __syncthreads();
 }
 
-// small dot head: out[row] = b + sum_k in[row][k] * w[k][col] for one column (16 lanes per row)
-__device__ __forceinline__ float head_dot16(const float* in, int ld, int K, const float* w, int ncol, int col,
+// small dot head: out[row] = b + sum_k in[row][k] * w[k][col] for one column (32 lanes per row)
+__device__ __forceinline__ float head_dot16(const float* in, int ld, int K, const float* w_, int ncol, int col,
                                             float b) {
   const int row = trow(), sub = tsub();
+  const AS1 float* w = gp(w_);
   float s = 0.f;
   for (int k = sub; k < K; k += kRowLanes) s += in[row * ld + k] * w[k * ncol + col];
   return row_sum(s) + b;
@@ -231,25 +301,28 @@ __device__ __forceinline__ float head_dot16(const float* in, int ld, int K, cons
 
 // PredictionNetwork4 (muzero_deterministic_madn.py:549-583) on the latent in `lat` ([16][LD]).
 // Leaves policy logits in a.U[:, 0:A] and tanh value in a.v0.  Clobbers X, T, U, W.
-__device__ __forceinline__ void pred16(const muz_pred_w& P, int A, const float* lat, const Arena& a) {
+// pf: rb[0].d0 on entry, (Ln, NTN tiles) on exit.
+template <int NTN>
+__device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const float* lat, const Arena& a, Pf& pf,
+                                       const AS4 muz_dense* Ln, int Kn, int Nn) {
   ln16<LAT, LN_PLAIN>(lat, LD, a.X, LD, P.ln0);
   __syncthreads();
-  resblock16(P.rb[0], a.X, a.T, a.U);
-  resblock16(P.rb[1], a.X, a.T, a.U);
-  dense16<3>(P.d03, LAT, 384, a.X, LD, a.W, LDW);     // [policy Dense_0 | value Dense_3]
+  resblock16<2>(P.rb[0], a.X, a.T, a.U, pf, &P.rb[1].d0, LAT, LAT);
+  resblock16<3>(P.rb[1], a.X, a.T, a.U, pf, &P.d03, LAT, 384);
+  dense16<3, 1>(P.d03, LAT, 384, a.X, LD, a.W, LDW, pf, &P.d1, LAT, 128);   // [policy Dense_0 | value Dense_3]
   __syncthreads();
   ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, P.ln1);
   ln16<128, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, P.ln3);
   __syncthreads();
-  dense16<1>(P.d1, LAT, 128, a.W, LDW, a.T, LD);      // policy Dense_1
-  dense16<1>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD);  // value Dense_4 (X is free now)
+  dense16<1, 1>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &P.d4, 128, 64);     // policy Dense_1
+  dense16<1, 1>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, A);  // value Dense_4 (X is free)
   __syncthreads();
   ln16<128, LN_RELU>(a.T, LD, a.T, LD, P.ln2);
   relu16(a.X, LD, 0, 64);
   __syncthreads();
-  dense16<1>(P.d2, 128, A, a.T, LD, a.U, LD);         // policy logits
+  dense16<1, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn);         // policy logits
   {
-    const float v = head_dot16(a.X, LD, 64, P.d5.w, 1, 0, P.d5.b[0]);
+    const float v = head_dot16(a.X, LD, 64, P.d5.w, 1, 0, gp(P.d5.b)[0]);
     if (tsub() == 0) a.v0[trow()] = tanhf(v);
   }
   __syncthreads();
@@ -265,46 +338,52 @@ __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) 
 
 // DynamicsNetwork4 (muzero_deterministic_madn.py:391-457): latent a.L, action per row in act[16].
 // Leaves the next latent in a.T, reward / discount expectations in a.v1 / a.v2.  Clobbers X, U, W, E.
-__device__ __forceinline__ void dyn16(const muz_dyn_w& D, int A, const int* act, const Arena& a) {
+// pf: d12 on entry, (Ln, NTN tiles) on exit.
+template <int NTN>
+__device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const int* act, const Arena& a, Pf& pf,
+                                      const AS4 muz_dense* Ln, int Kn, int Nn) {
   const int row = trow(), sub = tsub();
   const int ar = act[row];
   const bool oh = ar >= 0 && ar < A;   // jax.nn.one_hot: out-of-range -> zero row
   // action embedding: relu(one_hot @ W0 + b0) == relu(W0[a] + b0)
+  const AS1 float* w0 = gp(D.d0.w);
+  const AS1 float* b0 = gp(D.d0.b);
   for (int c = sub; c < 64; c += kRowLanes)
-    a.E[row * LDE + c] = fmaxf((oh ? D.d0.w[ar * 64 + c] : 0.f) + D.d0.b[c], 0.f);
+    a.E[row * LDE + c] = fmaxf((oh ? w0[ar * 64 + c] : 0.f) + b0[c], 0.f);
   ln16<LAT, LN_PLAIN>(a.L, LD, a.X, LD, D.ln0);
   __syncthreads();
-  dense16<4>(D.d12, 64, 512, a.E, LDE, a.W, LDW);     // [scale | shift]
+  dense16<4, 2>(D.d12, 64, 512, a.E, LDE, a.W, LDW, pf, &D.d3, LAT, LAT);     // [scale | shift]
   __syncthreads();
   for (int c = sub; c < LAT; c += kRowLanes)
     a.X[row * LD + c] = a.X[row * LD + c] * (1.0f + a.W[row * LDW + c]) + a.W[row * LDW + 256 + c];
   __syncthreads();
-  dense16<2>(D.d3, LAT, LAT, a.X, LD, a.T, LD);
+  dense16<2, 2>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, D.ln1);
   __syncthreads();
-  dense16<2>(D.d4, LAT, LAT, a.T, LD, a.X, LD);
+  dense16<2, 2>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, D.ln2);
   __syncthreads();
-  resblock16(D.rb[0], a.X, a.T, a.U);
-  resblock16(D.rb[1], a.X, a.T, a.U);
-  dense16<2>(D.d5, LAT, LAT, a.X, LD, a.T, LD);
+  resblock16<2>(D.rb[0], a.X, a.T, a.U, pf, &D.rb[1].d0, LAT, LAT);
+  resblock16<2>(D.rb[1], a.X, a.T, a.U, pf, &D.d5, LAT, LAT);
+  dense16<2, 1>(D.d5, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d67, LAT, 128);
   __syncthreads();
   for (int c = sub; c < LAT; c += kRowLanes) a.T[row * LD + c] = a.L[row * LD + c] + a.T[row * LD + c];
   __syncthreads();
   minmax16(a.T, LD);
   __syncthreads();
-  dense16<1>(D.d67, LAT, 128, a.T, LD, a.W, LDW);     // [reward hidden | discount hidden] latent rows
+  dense16<1, NTN>(D.d67, LAT, 128, a.T, LD, a.W, LDW, pf, Ln, Kn, Nn);   // [reward | discount] hidden
   __syncthreads();
+  const AS1 float* w67 = gp(D.d67_onehot);
   for (int c = sub; c < 128; c += kRowLanes)
-    a.W[row * LDW + c] = fmaxf(a.W[row * LDW + c] + (oh ? D.d67_onehot[ar * 128 + c] : 0.f), 0.f);
+    a.W[row * LDW + c] = fmaxf(a.W[row * LDW + c] + (oh ? w67[ar * 128 + c] : 0.f), 0.f);
   __syncthreads();
   float rl[3], dl[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    rl[j] = head_dot16(a.W, LDW, 64, D.reward_head.w, 3, j, D.reward_head.b[j]);
-    dl[j] = head_dot16(a.W + 64, LDW, 64, D.discount_head.w, 3, j, D.discount_head.b[j]);
+    rl[j] = head_dot16(a.W, LDW, 64, D.reward_head.w, 3, j, gp(D.reward_head.b)[j]);
+    dl[j] = head_dot16(a.W + 64, LDW, 64, D.discount_head.w, 3, j, gp(D.discount_head.b)[j]);
   }
   if (sub == 0) {
     a.v1[row] = softmax3_support(rl[0], rl[1], rl[2]);

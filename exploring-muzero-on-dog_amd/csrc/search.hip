@@ -13,6 +13,23 @@
 
 namespace muz {
 
+// Diagnostic build only (make DIAG=1): per-phase shader-clock totals of the search kernel.
+#ifdef MUZ_STAMPS
+__device__ unsigned long long g_muz_stamps[8];
+#define MUZ_STAMP(i)                                                          \
+  do {                                                                        \
+    if (threadIdx.x == 0) {                                                   \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();             \
+      st_acc[i] += _t - st_last;                                              \
+      st_last = _t;                                                           \
+    }                                                                         \
+  } while (0)
+#else
+#define MUZ_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 constexpr int kMaxSims = 100;              // S <= 100 (config (e) uses 100)
 constexpr int kMaxNodes = kMaxSims + 1;
 constexpr int kMaxDepth = 64;
@@ -30,7 +47,14 @@ struct TreeWs {
   float* emb;
   int N;
   __device__ __forceinline__ size_t ca(int g, int node, int a) const { return ((size_t)g * N + node) * kAPad + a; }
-  __device__ __forceinline__ float* e(int g, int node) const { return emb + ((size_t)g * N + node) * LAT; }
+  __device__ __forceinline__ AS1 float* e(int g, int node) const { return gpw(emb) + ((size_t)g * N + node) * LAT; }
+  // global-address-space views (see common.hpp: keeps LDS waits independent of global loads)
+  __device__ __forceinline__ AS1 int32_t* index() const { return gpw(c_index); }
+  __device__ __forceinline__ AS1 float* prior() const { return gpw(c_prior); }
+  __device__ __forceinline__ AS1 float* value() const { return gpw(c_value); }
+  __device__ __forceinline__ AS1 int32_t* visits() const { return gpw(c_visits); }
+  __device__ __forceinline__ AS1 float* reward() const { return gpw(c_reward); }
+  __device__ __forceinline__ AS1 float* disc() const { return gpw(c_disc); }
 };
 
 static inline size_t ws_children_bytes(int64_t n, int N) { return (size_t)n * N * kAPad * 4; }
@@ -157,6 +181,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
   const bool valid = g < n;
   const bool ok = a < A;
   const int ai = ok ? a : 0;              // in-bounds alias for lanes a >= A
+#ifdef MUZ_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---------------- root: instantiate_tree_from_root with masked logits (policies.py _mask_invalid_actions)
   unsigned lb = 0;
@@ -170,15 +198,15 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     const bool inv = !ok || ((lb >> a) & 1u) == 0u;
     const size_t b0 = T.ca(g, 0, ai);
     if (ok) {
-      T.c_prior[b0] = inv ? kFMin : l - lm;
-      T.c_index[b0] = -1;
-      T.c_visits[b0] = 0;
-      T.c_value[b0] = 0.f;
-      T.c_reward[b0] = 0.f;
-      T.c_disc[b0] = 0.f;
+      T.prior()[b0] = inv ? kFMin : l - lm;
+      T.index()[b0] = -1;
+      T.visits()[b0] = 0;
+      T.value()[b0] = 0.f;
+      T.reward()[b0] = 0.f;
+      T.disc()[b0] = 0.f;
       gum = gumbel_in ? gumbel_in[(size_t)g * A + ai] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, sa.turn, ai);
     }
-    float* e0 = T.e(g, 0);
+    AS1 float* e0 = T.e(g, 0);
     for (int c = a; c < LAT; c += kRowLanes) e0[c] = root_emb[(size_t)g * LAT + c];
     ncons = min(sa.max_considered, __popc(lb & ((1u << A) - 1u)));
     if (a == 0) {
@@ -195,17 +223,20 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     Kid k;
     const size_t e = T.ca(g, node, ai);
     k.ok = ok;
-    k.prior = T.c_prior[e];
-    k.value = T.c_value[e];
-    k.reward = T.c_reward[e];
-    k.disc = T.c_disc[e];
-    k.visits = ok ? T.c_visits[e] : 0;
-    k.index = T.c_index[e];
+    k.prior = T.prior()[e];
+    k.value = T.value()[e];
+    k.reward = T.reward()[e];
+    k.disc = T.disc()[e];
+    k.visits = ok ? T.visits()[e] : 0;
+    k.index = T.index()[e];
     return k;
   };
 
+  Pf pf;   // first k-blocks of the next dense layer (crosses the select / expand phases)
+  pf_issue<4>(pf, &kernarg0<muz_net_w>()->dyn.d12, 64, 512);
 #pragma unroll 1
   for (int sim = 0; sim < sa.S; ++sim) {
+    MUZ_STAMP(0);
     // ---------------- simulate (search.py simulate): walk from the root
     if (valid) {
       int node = 0, depth = 0, act = 0, nxt = -1;
@@ -254,45 +285,48 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
       s_act[row] = 0;
     }
     __syncthreads();
+    MUZ_STAMP(1);   // select
     // ---------------- expand (search.py expand): parent embedding -> recurrent_fn
     {
-      const float* pe = valid ? T.e(g, s_parent[row]) : nullptr;
+      const AS1 float* pe = valid ? T.e(g, s_parent[row]) : nullptr;
       for (int c = a; c < LAT; c += kRowLanes) ar.L[row * LD + c] = valid ? pe[c] : 0.f;
     }
     __syncthreads();
-    // Launder the weight table once per simulation so the compiler re-derives the layer addresses
-    // inside the loop instead of pinning them in registers across it.  (Wt is kernel argument 0,
-    // so it sits at offset 0 of the kernarg segment.)
-    const muz_net_w* wl = (const muz_net_w*)(__builtin_amdgcn_kernarg_segment_ptr());
-    asm volatile("" : "+s"(wl));
-    dyn16(wl->dyn, A, s_act, ar);
+    MUZ_STAMP(2);   // gather
+    // Weight table = kernel argument 0, read through the kernarg segment and laundered once per
+    // simulation so the compiler re-derives the layer addresses inside the loop.
+    const AS4 muz_net_w* wl = kernarg0<muz_net_w>();
+    dyn16<2>(wl->dyn, A, s_act, ar, pf, &wl->pred.rb[0].d0, LAT, LAT);
+    MUZ_STAMP(3);   // dynamics
     const int nx = s_next[row];
     if (valid) {
-      float* ne = T.e(g, nx);
+      AS1 float* ne = T.e(g, nx);
       for (int c = a; c < LAT; c += kRowLanes) ne[c] = ar.T[row * LD + c];
     }
     __syncthreads();
-    pred16(wl->pred, A, ar.T, ar);
+    MUZ_STAMP(4);   // embedding write
+    pred16<4>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d12, 64, 512);
+    MUZ_STAMP(5);   // prediction
     if (valid) {
       const bool fresh = nx == sim + 1;
       if (ok) {
         const size_t nb = T.ca(g, nx, a);
-        T.c_prior[nb] = ar.U[row * LD + a];
+        T.prior()[nb] = ar.U[row * LD + a];
         if (fresh) {
-          T.c_index[nb] = -1;
-          T.c_visits[nb] = 0;
-          T.c_value[nb] = 0.f;
-          T.c_reward[nb] = 0.f;
-          T.c_disc[nb] = 0.f;
+          T.index()[nb] = -1;
+          T.visits()[nb] = 0;
+          T.value()[nb] = 0.f;
+          T.reward()[nb] = 0.f;
+          T.disc()[nb] = 0.f;
         }
       }
       if (a == 0) {
         const int par = s_parent[row], pa = s_act[row];
         const float v = ar.v0[row], rw = ar.v1[row], dc = ar.v2[row];
         const size_t eb = T.ca(g, par, pa);
-        T.c_index[eb] = nx;
-        T.c_reward[eb] = rw;
-        T.c_disc[eb] = dc;
+        T.index()[eb] = nx;
+        T.reward()[eb] = rw;
+        T.disc()[eb] = dc;
         s_raw[row][nx] = v;
         s_val[row][nx] = v;
         s_visits[row][nx] = fresh ? 1 : s_visits[row][nx] + 1;
@@ -309,8 +343,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
           leaf = r + dsc * leaf;
           const float pv = (s_val[row][parent] * (float)cnt + leaf) / ((float)cnt + 1.0f);
           const size_t ei = T.ca(g, parent, pact);
-          T.c_value[ei] = s_val[row][idx];
-          T.c_visits[ei] = p_cvis[row][lvl] + 1;
+          T.value()[ei] = s_val[row][idx];
+          T.visits()[ei] = p_cvis[row][lvl] + 1;
           s_val[row][parent] = pv;
           s_visits[row][parent] = cnt + 1;
           idx = parent;
@@ -318,7 +352,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
       }
     }
     __syncthreads();
+    MUZ_STAMP(6);   // expand + backward
   }
+#ifdef MUZ_STAMPS
+  if (threadIdx.x == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_muz_stamps[i], st_acc[i]);
+#endif
 
   // ---------------- final action + action_weights (policies.py gumbel_muzero_policy tail)
   if (valid) {
@@ -398,5 +437,17 @@ int muz_gumbel_search(const muz_net_w* w, const muz_search_cfg* cfg, const float
   return launch_gumbel_search(*w, sa, root_logits, root_value, root_embedding, legal_bits, gumbel, game_id, n, nullptr,
                               workspace, action, action_weights, root_value_out, (hipStream_t)stream);
 }
+
+#ifdef MUZ_STAMPS
+int muz_diag_stamps(unsigned long long* host_out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_muz_stamps), sizeof(unsigned long long) * 8);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_muz_stamps), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
 
 }  // extern "C"

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmuz.so")
+# MUZ_LIB selects an alternative build (e.g. the stamp-instrumented libmuz_diag.so); default in-tree.
+LIB_PATH = os.environ.get("MUZ_LIB") or os.path.join(_HERE, "libmuz.so")
 
 c_i8p = ctypes.POINTER(ctypes.c_int8)
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
