@@ -45,13 +45,13 @@ __device__ __forceinline__ void conv_mfma(const AS4 muz_dense& L, const float* i
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   mfma_rows16<4>(L.w, KB, in + (wv * 16) * cin, cin, acc);
+  // out^T layout (see dense16): lane (r, g) holds columns t*16 + 4g .. +3 of position wv*16 + r
   const int r = lane & 15, g = lane >> 4;
+  const AS1 f32x4* bias4 = gp(reinterpret_cast<const f32x4*>(L.b));
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int col = t * 16 + r;
-    const float bb = gp(L.b)[col];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pre[(wv * 16 + 4 * g + i) * kPreLd + col] = acc[t][i] + bb;
+    const int col = t * 16 + 4 * g;
+    *reinterpret_cast<f32x4*>(pre + (wv * 16 + r) * kPreLd + col) = acc[t] + bias4[col >> 2];
   }
 }
 
@@ -117,29 +117,29 @@ __global__ __launch_bounds__(kThreads) void k_root_dense(muz_net_w Wt, const flo
   const bool valid = gr < n;
   // global stream input: x[:, 6:, 0]
   const int Kg = C - 6;
-  a.E[row * LDE + sub] = (valid && sub < Kg) ? obs[((size_t)gr * C + 6 + sub) * 56] : 0.f;
+  if (sub < 32) a.E[row * LDE + sub] = (valid && sub < Kg) ? obs[((size_t)gr * C + 6 + sub) * 56] : 0.f;
   // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16)
   Pf pf;
-  pf_issue<2>(pf, &R.d0, 3584, LAT);
-  dense16<2, 1>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW, pf, &R.d1, Kg, 64, true);
+  pf_issue<NT256>(pf, &R.d0, 3584, LAT);
+  dense16<NT256, NT64>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW, pf, &R.d1, Kg, 64, true);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, R.ln3);
-  dense16<1, 1>(R.d1, Kg, 64, a.E, LDE, a.X, LD, pf, &R.d2, 64, 64);
+  dense16<NT64, NT64>(R.d1, Kg, 64, a.E, LDE, a.X, LD, pf, &R.d2, 64, 64);
   __syncthreads();
   ln16<64, LN_RELU>(a.X, LD, a.X, LD, R.ln4);
   __syncthreads();
-  dense16<1, 2>(R.d2, 64, 64, a.X, LD, a.W + 256, LDW, pf, &R.d3, 320, LAT);
+  dense16<NT64, NT256>(R.d2, 64, 64, a.X, LD, a.W + 256, LDW, pf, &R.d3, 320, LAT);
   __syncthreads();
   ln16<64, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, R.ln5);
   __syncthreads();
-  dense16<2, 2>(R.d3, 320, LAT, a.W, LDW, a.X, LD, pf, &R.rb[0].d0, LAT, LAT);
+  dense16<NT256, NT256>(R.d3, 320, LAT, a.W, LDW, a.X, LD, pf, &R.rb[0].d0, LAT, LAT);
   __syncthreads();
   ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, R.ln6);
   __syncthreads();
 #pragma unroll 1
   for (int b = 0; b < 6; ++b)
-    resblock16<2>(R.rb[b], a.X, a.T, a.U, pf, b < 5 ? &R.rb[b + 1].d0 : &R.d4, LAT, LAT);
-  dense16<2, 2>(R.d4, LAT, LAT, a.X, LD, a.T, LD, pf, &W->pred.rb[0].d0, LAT, LAT);
+    resblock16<NT256>(R.rb[b], a.X, a.T, a.U, pf, b < 5 ? &R.rb[b + 1].d0 : &R.d4, LAT, LAT);
+  dense16<NT256, NT256>(R.d4, LAT, LAT, a.X, LD, a.T, LD, pf, &W->pred.rb[0].d0, LAT, LAT);
   __syncthreads();
   minmax16(a.T, LD);
   __syncthreads();
@@ -170,9 +170,9 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
   if (sub == 0) act[row] = valid ? action[gr] : 0;
   const AS4 muz_net_w* W = kernarg0<muz_net_w>();   // == Wt, read through the kernarg segment
   Pf pf;
-  pf_issue<4>(pf, &W->dyn.d12, 64, 512);
+  pf_issue<NT512>(pf, &W->dyn.d12, 64, 512);
   __syncthreads();
-  dyn16<2>(W->dyn, A, act, a, pf, &W->pred.rb[0].d0, LAT, LAT);
+  dyn16<NT256>(W->dyn, A, act, a, pf, &W->pred.rb[0].d0, LAT, LAT);
   if (valid) {
     for (int c = sub; c < LAT; c += kRowLanes) next_emb[(size_t)gr * LAT + c] = a.T[row * LD + c];
     if (sub == 0) {
@@ -209,6 +209,8 @@ int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int
 using namespace muz;
 
 extern "C" {
+
+int32_t muz_tile_waves(void) { return kWaves; }
 
 int64_t muz_nets_root_scratch_bytes(int32_t n) {
   const int64_t rows = ((int64_t)n + kRows - 1) / kRows * kRows;

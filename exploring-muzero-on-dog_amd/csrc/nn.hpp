@@ -13,11 +13,61 @@
 
 namespace muz {
 
+#ifndef MUZ_TILE_WAVES
+#define MUZ_TILE_WAVES 8   // waves per 16-row tile workgroup: 8 (2 per SIMD) or 16 (4 per SIMD)
+#endif
 constexpr int kRows = 16;
-constexpr int kRowLanes = 32;                 // lanes per row in row-wise phases
-constexpr int kThreads = kRows * kRowLanes;   // 512
-constexpr int kWaves = kThreads / 64;         // 8
+constexpr int kWaves = MUZ_TILE_WAVES;
+constexpr int kThreads = kWaves * 64;          // 512 / 1024
+constexpr int kRowLanes = kThreads / kRows;    // lanes per row in row-wise phases: 32 / 64
 constexpr int LAT = 256;
+// ---- diagnostic fine-grained stamps (make EXTRA=-DMUZ_STAMPS2); compiled out otherwise -------------
+enum { ST_MFMA = 0, ST_EPI = 1, ST_BAR = 2, ST_ROW = 3, ST_SEL = 4, ST_OTHER = 5, ST_N = 8 };
+#ifdef MUZ_STAMPS2
+__device__ unsigned long long g_st2[ST_N];
+struct StampState {
+  unsigned long long last, acc[ST_N];
+};
+__device__ __forceinline__ StampState& st_state() {
+  __shared__ StampState s;
+  return s;
+}
+__device__ __forceinline__ void st_begin() {
+  if (threadIdx.x == 0) {
+    StampState& s = st_state();
+    for (int i = 0; i < ST_N; ++i) s.acc[i] = 0;
+    s.last = __builtin_amdgcn_s_memtime();
+  }
+}
+__device__ __forceinline__ void ST(int cat) {
+  if (threadIdx.x == 0) {
+    StampState& s = st_state();
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    s.acc[cat] += t - s.last;
+    s.last = t;
+  }
+}
+__device__ __forceinline__ void st_end() {
+  if (threadIdx.x == 0)
+    for (int i = 0; i < ST_N; ++i) atomicAdd(&g_st2[i], st_state().acc[i]);
+}
+#define SYNC()         \
+  do {                 \
+    ST(ST_OTHER);      \
+    __syncthreads();   \
+    ST(ST_BAR);        \
+  } while (0)
+#else
+__device__ __forceinline__ void st_begin() {}
+__device__ __forceinline__ void ST(int) {}
+__device__ __forceinline__ void st_end() {}
+#define SYNC() __syncthreads()
+#endif
+
+// 16-column MFMA tiles per wave for a layer of N outputs (waves split N)
+constexpr int nt_for(int N) { return (N + 16 * kWaves - 1) / (16 * kWaves); }
+constexpr int NT64 = nt_for(64), NT128 = nt_for(128), NT256 = nt_for(256), NT384 = nt_for(384),
+              NT512 = nt_for(512), NTA = nt_for(24);
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -28,6 +78,13 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // acc[t] += A[16 rows][K] @ Wgroup[K][NT*16]  (KB = K/16 k-blocks; Wg = packed weights of this group).
 // b0 / b1 hold k-blocks 0 and 1 on entry.  Weights for k-blocks kb+1 and kb+2 are in flight while kb is
 // multiplied (3-deep register ring, written as a 3-way unrolled loop so every index is static).
+#ifndef MUZ_RING_DEPTH
+#define MUZ_RING_DEPTH 2   // k-blocks of weights in flight ahead of the one being multiplied (2 or 3)
+#endif
+#ifndef MUZ_A_PRELOAD
+#define MUZ_A_PRELOAD 1    // read the A fragment of k-block kb+1 from LDS before kb's MFMAs
+#endif
+
 template <int NT, bool AG>
 __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int KB, const float* A, int lda,
                                                f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT]) {
@@ -40,27 +97,54 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
     if constexpr (AG) return *gp(reinterpret_cast<const f32x4*>(ap + kb * 16));
     else return *reinterpret_cast<const f32x4*>(ap + kb * 16);
   };
-  f32x4 b2[NT];
-  // step kb: issue k-block kb+2 into `nxt` (the buffer consumed at step kb-1), multiply `cur` (= kb)
-  auto step = [&](int kb, const f32x4 (&cur)[NT], f32x4 (&nxt)[NT]) {
-    if (kb + 2 < KB) {
+  constexpr int D = MUZ_RING_DEPTH;
+  f32x4 a0 = lda4(0), a1 = a0;
+  // step kb: issue k-block kb+D into `nxt` (the buffer consumed at step kb-1), read A of kb+1,
+  // multiply `cur` (= kb) with A of kb
+  auto step = [&](int kb, const f32x4 (&cur)[NT], f32x4 (&nxt)[NT], const f32x4& acur, f32x4& anxt) {
+    if (kb + D < KB) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) nxt[t] = wp[(kb + 2) * wstep + t];
+      for (int t = 0; t < NT; ++t) nxt[t] = wp[(kb + D) * wstep + t];
     }
-    const f32x4 a = lda4(kb);
+    f32x4 a;
+    if (MUZ_A_PRELOAD) {
+      if (kb + 1 < KB) anxt = lda4(kb + 1);
+      a = acur;
+    } else {
+      a = lda4(kb);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[j], cur[t][j], acc[t]);
+      for (int t = 0; t < NT; ++t) acc[t] = mfma4(cur[t][j], a[j], acc[t]);   // D = W^T A^T
   };
   int kb = 0;
-  for (; kb + 3 <= KB; kb += 3) {
-    step(kb, b0, b2);
-    step(kb + 1, b1, b0);
-    step(kb + 2, b2, b1);
+  if constexpr (D == 2) {
+    f32x4 b2[NT];
+    for (; kb + 3 <= KB; kb += 3) {
+      step(kb, b0, b2, a0, a1);
+      step(kb + 1, b1, b0, a1, a0);
+      step(kb + 2, b2, b1, a0, a1);
+      a0 = a1;
+    }
+    if (kb < KB) step(kb, b0, b2, a0, a1);
+    if (kb + 1 < KB) step(kb + 1, b1, b0, a1, a0);
+  } else {
+    f32x4 b2[NT], b3[NT];
+    if (KB > 2) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b2[t] = wp[2 * wstep + t];
+    }
+    for (; kb + 4 <= KB; kb += 4) {
+      step(kb, b0, b3, a0, a1);
+      step(kb + 1, b1, b0, a1, a0);
+      step(kb + 2, b2, b1, a0, a1);
+      step(kb + 3, b3, b2, a1, a0);
+    }
+    if (kb < KB) step(kb, b0, b3, a0, a1);
+    if (kb + 1 < KB) step(kb + 1, b1, b0, a1, a0);
+    if (kb + 2 < KB) step(kb + 2, b2, b1, a0, a1);
   }
-  if (kb < KB) step(kb, b0, b2);
-  if (kb + 1 < KB) step(kb + 1, b1, b0);
 }
 
 template <int NT>
@@ -89,7 +173,7 @@ __device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB
 // ---- cross-layer weight prefetch ----------------------------------------------------------------
 // Every dense layer issues the first two k-blocks of the NEXT layer's weights for this wave before its
 // epilogue, so the loads fly across the epilogue, the barrier and the LayerNorm pass in between.
-constexpr int kPfMax = 4;
+constexpr int kPfMax = NT512;
 struct Pf {
   f32x4 v0[kPfMax], v1[kPfMax];
 };
@@ -126,54 +210,57 @@ __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, co
     pf_issue<NTN>(pf, Ln, Kn, Nn);
     return;
   }
-  f32x4 acc[NT], b0[NT], b1[NT];
+  const int r = lane & 15, g = lane >> 4;
+  const AS1 f32x4* bias4 = gp(reinterpret_cast<const f32x4*>(L.b));
+  f32x4 acc[NT], b0[NT], b1[NT], bb[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
+    const int col = col0 + t * 16 + 4 * g;
+    bb[t] = col < N ? bias4[col >> 2] : f32x4{0.f, 0.f, 0.f, 0.f};   // lands under the MFMA loop
     acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     b0[t] = pf.v0[t];
     b1[t] = pf.v1[t];
   }
+  ST(ST_OTHER);
   mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global);
+  ST(ST_MFMA);
   pf_issue<NTN>(pf, Ln, Kn, Nn);
-  const int r = lane & 15, g = lane >> 4;
-  const AS1 float* bias = gp(L.b);
+  // The MFMA computes out^T (weights as the A operand), so lane (r, g) holds 4 CONSECUTIVE output
+  // columns of row r: one 16-byte bias load and one ds_write_b128 per tile.
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int col = col0 + t * 16 + r;
-    if (col < N) {
-      const float bb = bias[col];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) out[(4 * g + i) * ldo + col] = acc[t][i] + bb;
-    }
+    const int col = col0 + t * 16 + 4 * g;
+    if (col < N) *reinterpret_cast<f32x4*>(out + r * ldo + col) = acc[t] + bb[t];
   }
+  ST(ST_EPI);
 }
 
 // ---- row-wise ops: thread t -> row t/32, lane-in-row t%32 (half a wave per row) ---------------------
-__device__ __forceinline__ int trow() { return threadIdx.x >> 5; }
-__device__ __forceinline__ int tsub() { return threadIdx.x & 31; }
+__device__ __forceinline__ int trow() { return threadIdx.x / kRowLanes; }
+__device__ __forceinline__ int tsub() { return threadIdx.x % kRowLanes; }
 __device__ __forceinline__ float row_sum(float v) {
 #pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m, 32);
+  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, kRowLanes);
   return v;
 }
 __device__ __forceinline__ float row_max(float v) {
 #pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 32));
+  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, kRowLanes));
   return v;
 }
 __device__ __forceinline__ float row_min(float v) {
 #pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) v = fminf(v, __shfl_xor(v, m, 32));
+  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v = fminf(v, __shfl_xor(v, m, kRowLanes));
   return v;
 }
 __device__ __forceinline__ int row_isum(int v) {
 #pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m, 32);
+  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, kRowLanes);
   return v;
 }
 __device__ __forceinline__ int row_imax(int v) {
 #pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, 32));
+  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, kRowLanes));
   return v;
 }
 
@@ -181,25 +268,60 @@ enum LnMode { LN_PLAIN = 0, LN_RELU = 1, LN_RESID_RELU = 2 };
 
 // Flax LayerNorm (eps 1e-6, fast variance) of in[16][N] -> out.
 //   LN_PLAIN: out = y;  LN_RELU: out = relu(y);  LN_RESID_RELU: out = relu(out + y)  (ResBlock tail)
-template <int N, int MODE>
-__device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int ldo, const AS4 muz_ln& P) {
-  constexpr int PER = N / kRowLanes;
-  const int row = trow(), sub = tsub();
-  const AS1 float* scale = gp(P.scale);
-  const AS1 float* shift = gp(P.bias);
-  float sc[PER], sh[PER];
+// Row-wise vector layout: lane `sub` of a row owns float4 columns sub*4 + i*4*kRowLanes.
+template <int N>
+struct RowVec {
+  static constexpr int V = (N >= 4 * kRowLanes) ? N / (4 * kRowLanes) : 1;
+  static __device__ __forceinline__ bool active(int sub) { return N >= 4 * kRowLanes || sub * 4 < N; }
+  static __device__ __forceinline__ int col(int sub, int i) { return sub * 4 + i * 4 * kRowLanes; }
+};
+
+__device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void sts4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ f32x4 relu4(f32x4 v) {
+  return f32x4{fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
+}
+
+// LayerNorm parameters of this lane's columns, loaded early (before the preceding dense layer's MFMA
+// loop) so their L2 latency hides under it.
+template <int N>
+struct LnP {
+  f32x4 sc[RowVec<N>::V], sh[RowVec<N>::V];
+};
+template <int N>
+__device__ __forceinline__ LnP<N> ln_load(const AS4 muz_ln& P) {
+  using RV = RowVec<N>;
+  LnP<N> p;
+  const int sub = tsub();
+  const AS1 f32x4* scale = gp(reinterpret_cast<const f32x4*>(P.scale));
+  const AS1 f32x4* shift = gp(reinterpret_cast<const f32x4*>(P.bias));
+  if (RV::active(sub)) {
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {   // parameter loads first, so they overlap the statistics
-    sc[i] = scale[sub + kRowLanes * i];
-    sh[i] = shift[sub + kRowLanes * i];
+    for (int i = 0; i < RV::V; ++i) {
+      p.sc[i] = scale[RV::col(sub, i) >> 2];
+      p.sh[i] = shift[RV::col(sub, i) >> 2];
+    }
   }
-  float v[PER];
+  return p;
+}
+
+template <int N, int MODE>
+__device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int ldo, const LnP<N>& p) {
+  using RV = RowVec<N>;
+  const int row = trow(), sub = tsub();
+  const bool act = RV::active(sub);
+  f32x4 v[RV::V];
   float s = 0.f, s2 = 0.f;
+  if (act) {
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    v[i] = in[row * ldi + sub + kRowLanes * i];
-    s += v[i];
-    s2 += v[i] * v[i];
+    for (int i = 0; i < RV::V; ++i) {
+      v[i] = lds4(in + row * ldi + RV::col(sub, i));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s += v[i][q];
+        s2 += v[i][q] * v[i][q];
+      }
+    }
   }
   s = row_sum(s);
   s2 = row_sum(s2);
@@ -207,38 +329,56 @@ __device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int l
   const float mean2 = s2 / (float)N;
   const float var = fmaxf(0.f, mean2 - mean * mean);
   const float inv = 1.0f / sqrtf(var + 1e-6f);
+  if (act) {
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = sub + kRowLanes * i;
-    float y = (v[i] - mean) * (inv * sc[i]) + sh[i];
-    if (MODE == LN_RELU) y = fmaxf(y, 0.f);
-    if (MODE == LN_RESID_RELU) y = fmaxf(out[row * ldo + c] + y, 0.f);
-    out[row * ldo + c] = y;
+    for (int i = 0; i < RV::V; ++i) {
+      const int c = RV::col(sub, i);
+      f32x4 y;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y[q] = (v[i][q] - mean) * (inv * p.sc[i][q]) + p.sh[i][q];
+      if (MODE == LN_RELU) y = relu4(y);
+      if (MODE == LN_RESID_RELU) y = relu4(lds4(out + row * ldo + c) + y);
+      sts4(out + row * ldo + c, y);
+    }
   }
+  ST(ST_ROW);
+}
+
+template <int N, int MODE>
+__device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int ldo, const AS4 muz_ln& P) {
+  ln16<N, MODE>(in, ldi, out, ldo, ln_load<N>(P));
 }
 
 // x <- (x - min) / (max - min + 1e-8) per row of 256 (Repr2 139-140, Dyn4 435-437).
 __device__ __forceinline__ void minmax16(float* buf, int ld) {
-  constexpr int PER = LAT / kRowLanes;
+  using RV = RowVec<LAT>;
   const int row = trow(), sub = tsub();
-  float v[PER];
+  f32x4 v[RV::V];
   float lo = INFINITY, hi = -INFINITY;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    v[i] = buf[row * ld + sub + kRowLanes * i];
-    lo = fminf(lo, v[i]);
-    hi = fmaxf(hi, v[i]);
+  for (int i = 0; i < RV::V; ++i) {
+    v[i] = lds4(buf + row * ld + RV::col(sub, i));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      lo = fminf(lo, v[i][q]);
+      hi = fmaxf(hi, v[i][q]);
+    }
   }
   lo = row_min(lo);
   hi = row_max(hi);
   const float den = hi - lo + 1e-8f;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) buf[row * ld + sub + kRowLanes * i] = (v[i] - lo) / den;
+  for (int i = 0; i < RV::V; ++i) {
+    f32x4 y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = (v[i][q] - lo) / den;
+    sts4(buf + row * ld + RV::col(sub, i), y);
+  }
 }
 
 __device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
   const int row = trow(), sub = tsub();
-  for (int c = sub; c < n; c += kRowLanes) buf[row * ld + col0 + c] = fmaxf(buf[row * ld + col0 + c], 0.f);
+  for (int c = sub * 4; c < n; c += 4 * kRowLanes) sts4(buf + row * ld + col0 + c, relu4(lds4(buf + row * ld + col0 + c)));
 }
 
 // ---- LDS arena of a 16-row tile ---------------------------------------------------------------------
@@ -279,24 +419,41 @@ struct Arena {
 template <int NTN>
 __device__ __forceinline__ void resblock16(const AS4 muz_resblock& R, float* X, float* T, float* U, Pf& pf,
                                            const AS4 muz_dense* Ln, int Kn, int Nn) {
-  dense16<2, 2>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT);
-  __syncthreads();
-  ln16<LAT, LN_RELU>(T, LD, T, LD, R.ln0);
-  __syncthreads();
-  dense16<2, NTN>(R.d1, LAT, LAT, T, LD, U, LD, pf, Ln, Kn, Nn);
-  __syncthreads();
-  ln16<LAT, LN_RESID_RELU>(U, LD, X, LD, R.ln1);
-  __syncthreads();
+  const LnP<LAT> p0 = ln_load<LAT>(R.ln0);
+  dense16<NT256, NT256>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT);
+  SYNC();
+  ln16<LAT, LN_RELU>(T, LD, T, LD, p0);
+  SYNC();
+  const LnP<LAT> p1 = ln_load<LAT>(R.ln1);
+  dense16<NT256, NTN>(R.d1, LAT, LAT, T, LD, U, LD, pf, Ln, Kn, Nn);
+  SYNC();
+  ln16<LAT, LN_RESID_RELU>(U, LD, X, LD, p1);
+  SYNC();
 }
 
-// small dot head: out[row] = b + sum_k in[row][k] * w[k][col] for one column (32 lanes per row)
-__device__ __forceinline__ float head_dot16(const float* in, int ld, int K, const float* w_, int ncol, int col,
-                                            float b) {
-  const int row = trow(), sub = tsub();
-  const AS1 float* w = gp(w_);
+// 64-input heads: weights of this lane's inputs k = sub + i*kRowLanes, loaded early.
+constexpr int kHeadPer = 64 / kRowLanes;
+struct HeadW {
+  float w[3][kHeadPer];
+  float b[3];
+};
+__device__ __forceinline__ HeadW head_load(const AS4 muz_dense& H, int ncol) {
+  HeadW h;
+  const AS1 float* w = gp(H.w);
+  const AS1 float* b = gp(H.b);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    h.b[j] = j < ncol ? b[j] : 0.f;
+#pragma unroll
+    for (int i = 0; i < kHeadPer; ++i) h.w[j][i] = j < ncol ? w[(tsub() + i * kRowLanes) * ncol + j] : 0.f;
+  }
+  return h;
+}
+__device__ __forceinline__ float head_dot(const float* in, int ld, const HeadW& h, int j) {
   float s = 0.f;
-  for (int k = sub; k < K; k += kRowLanes) s += in[row * ld + k] * w[k * ncol + col];
-  return row_sum(s) + b;
+#pragma unroll
+  for (int i = 0; i < kHeadPer; ++i) s += in[trow() * ld + tsub() + i * kRowLanes] * h.w[j][i];
+  return row_sum(s) + h.b[j];
 }
 
 // PredictionNetwork4 (muzero_deterministic_madn.py:549-583) on the latent in `lat` ([16][LD]).
@@ -306,26 +463,30 @@ template <int NTN>
 __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const float* lat, const Arena& a, Pf& pf,
                                        const AS4 muz_dense* Ln, int Kn, int Nn) {
   ln16<LAT, LN_PLAIN>(lat, LD, a.X, LD, P.ln0);
-  __syncthreads();
-  resblock16<2>(P.rb[0], a.X, a.T, a.U, pf, &P.rb[1].d0, LAT, LAT);
-  resblock16<3>(P.rb[1], a.X, a.T, a.U, pf, &P.d03, LAT, 384);
-  dense16<3, 1>(P.d03, LAT, 384, a.X, LD, a.W, LDW, pf, &P.d1, LAT, 128);   // [policy Dense_0 | value Dense_3]
-  __syncthreads();
-  ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, P.ln1);
-  ln16<128, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, P.ln3);
-  __syncthreads();
-  dense16<1, 1>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &P.d4, 128, 64);     // policy Dense_1
-  dense16<1, 1>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, A);  // value Dense_4 (X is free)
-  __syncthreads();
-  ln16<128, LN_RELU>(a.T, LD, a.T, LD, P.ln2);
+  SYNC();
+  resblock16<NT256>(P.rb[0], a.X, a.T, a.U, pf, &P.rb[1].d0, LAT, LAT);
+  resblock16<NT384>(P.rb[1], a.X, a.T, a.U, pf, &P.d03, LAT, 384);
+  const LnP<LAT> p1 = ln_load<LAT>(P.ln1);
+  const LnP<128> p3 = ln_load<128>(P.ln3);
+  dense16<NT384, NT128>(P.d03, LAT, 384, a.X, LD, a.W, LDW, pf, &P.d1, LAT, 128);   // [policy Dense_0 | value Dense_3]
+  SYNC();
+  ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, p1);
+  ln16<128, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, p3);
+  SYNC();
+  const LnP<128> p2 = ln_load<128>(P.ln2);
+  const HeadW hv = head_load(P.d5, 1);
+  dense16<NT128, NT64>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &P.d4, 128, 64);     // policy Dense_1
+  dense16<NT64, NTA>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, A);  // value Dense_4 (X is free)
+  SYNC();
+  ln16<128, LN_RELU>(a.T, LD, a.T, LD, p2);
   relu16(a.X, LD, 0, 64);
-  __syncthreads();
-  dense16<1, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn);         // policy logits
+  SYNC();
+  dense16<NTA, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn);         // policy logits
   {
-    const float v = head_dot16(a.X, LD, 64, P.d5.w, 1, 0, gp(P.d5.b)[0]);
+    const float v = head_dot(a.X, LD, hv, 0);
     if (tsub() == 0) a.v0[trow()] = tanhf(v);
   }
-  __syncthreads();
+  SYNC();
 }
 
 __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) {
@@ -351,45 +512,54 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const int* 
   for (int c = sub; c < 64; c += kRowLanes)
     a.E[row * LDE + c] = fmaxf((oh ? w0[ar * 64 + c] : 0.f) + b0[c], 0.f);
   ln16<LAT, LN_PLAIN>(a.L, LD, a.X, LD, D.ln0);
-  __syncthreads();
-  dense16<4, 2>(D.d12, 64, 512, a.E, LDE, a.W, LDW, pf, &D.d3, LAT, LAT);     // [scale | shift]
-  __syncthreads();
-  for (int c = sub; c < LAT; c += kRowLanes)
-    a.X[row * LD + c] = a.X[row * LD + c] * (1.0f + a.W[row * LDW + c]) + a.W[row * LDW + 256 + c];
-  __syncthreads();
-  dense16<2, 2>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT);
-  __syncthreads();
-  ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, D.ln1);
-  __syncthreads();
-  dense16<2, 2>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT);
-  __syncthreads();
-  ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, D.ln2);
-  __syncthreads();
-  resblock16<2>(D.rb[0], a.X, a.T, a.U, pf, &D.rb[1].d0, LAT, LAT);
-  resblock16<2>(D.rb[1], a.X, a.T, a.U, pf, &D.d5, LAT, LAT);
-  dense16<2, 1>(D.d5, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d67, LAT, 128);
-  __syncthreads();
-  for (int c = sub; c < LAT; c += kRowLanes) a.T[row * LD + c] = a.L[row * LD + c] + a.T[row * LD + c];
-  __syncthreads();
+  SYNC();
+  const LnP<LAT> p1 = ln_load<LAT>(D.ln1);
+  dense16<NT512, NT256>(D.d12, 64, 512, a.E, LDE, a.W, LDW, pf, &D.d3, LAT, LAT);     // [scale | shift]
+  SYNC();
+  for (int c = sub * 4; c < LAT; c += 4 * kRowLanes) {
+    const f32x4 x = lds4(a.X + row * LD + c), sc = lds4(a.W + row * LDW + c), sh = lds4(a.W + row * LDW + 256 + c);
+    sts4(a.X + row * LD + c, x * (1.0f + sc) + sh);
+  }
+  SYNC();
+  dense16<NT256, NT256>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT);
+  SYNC();
+  ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, p1);
+  SYNC();
+  const LnP<LAT> p2 = ln_load<LAT>(D.ln2);
+  dense16<NT256, NT256>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT);
+  SYNC();
+  ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, p2);
+  SYNC();
+  resblock16<NT256>(D.rb[0], a.X, a.T, a.U, pf, &D.rb[1].d0, LAT, LAT);
+  resblock16<NT256>(D.rb[1], a.X, a.T, a.U, pf, &D.d5, LAT, LAT);
+  const HeadW hr = head_load(D.reward_head, 3);
+  const HeadW hd = head_load(D.discount_head, 3);
+  dense16<NT256, NT128>(D.d5, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d67, LAT, 128);
+  SYNC();
+  for (int c = sub * 4; c < LAT; c += 4 * kRowLanes)
+    sts4(a.T + row * LD + c, lds4(a.L + row * LD + c) + lds4(a.T + row * LD + c));
+  SYNC();
   minmax16(a.T, LD);
-  __syncthreads();
-  dense16<1, NTN>(D.d67, LAT, 128, a.T, LD, a.W, LDW, pf, Ln, Kn, Nn);   // [reward | discount] hidden
-  __syncthreads();
-  const AS1 float* w67 = gp(D.d67_onehot);
-  for (int c = sub; c < 128; c += kRowLanes)
-    a.W[row * LDW + c] = fmaxf(a.W[row * LDW + c] + (oh ? w67[ar * 128 + c] : 0.f), 0.f);
-  __syncthreads();
+  SYNC();
+  dense16<NT128, NTN>(D.d67, LAT, 128, a.T, LD, a.W, LDW, pf, Ln, Kn, Nn);   // [reward | discount] hidden
+  SYNC();
+  const AS1 f32x4* w67 = gp(reinterpret_cast<const f32x4*>(D.d67_onehot));
+  for (int c = sub * 4; c < 128; c += 4 * kRowLanes) {
+    const f32x4 h = lds4(a.W + row * LDW + c);
+    sts4(a.W + row * LDW + c, relu4(oh ? h + w67[(ar * 128 + c) >> 2] : h));
+  }
+  SYNC();
   float rl[3], dl[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    rl[j] = head_dot16(a.W, LDW, 64, D.reward_head.w, 3, j, gp(D.reward_head.b)[j]);
-    dl[j] = head_dot16(a.W + 64, LDW, 64, D.discount_head.w, 3, j, gp(D.discount_head.b)[j]);
+    rl[j] = head_dot(a.W, LDW, hr, j);
+    dl[j] = head_dot(a.W + 64, LDW, hd, j);
   }
   if (sub == 0) {
     a.v1[row] = softmax3_support(rl[0], rl[1], rl[2]);
     a.v2[row] = softmax3_support(dl[0], dl[1], dl[2]);
   }
-  __syncthreads();
+  SYNC();
 }
 
 }  // namespace muz

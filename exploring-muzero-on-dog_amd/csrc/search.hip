@@ -83,9 +83,9 @@ static TreeWs carve_ws(void* ws, int n, int N) {
 // ---- one game per 32 lanes (half a wave), one action per lane; jnp.argmax tie-break (first index) ----
 __device__ __forceinline__ void row_argmax(float& v, int& i) {
 #pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) {
-    const float ov = __shfl_xor(v, m, 32);
-    const int oi = __shfl_xor(i, m, 32);
+  for (int m = kRowLanes / 2; m >= 1; m >>= 1) {
+    const float ov = __shfl_xor(v, m, kRowLanes);
+    const int oi = __shfl_xor(i, m, kRowLanes);
     if (ov > v || (ov == v && oi < i)) {
       v = ov;
       i = oi;
@@ -232,8 +232,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     return k;
   };
 
+  st_begin();
   Pf pf;   // first k-blocks of the next dense layer (crosses the select / expand phases)
-  pf_issue<4>(pf, &kernarg0<muz_net_w>()->dyn.d12, 64, 512);
+  pf_issue<NT512>(pf, &kernarg0<muz_net_w>()->dyn.d12, 64, 512);
 #pragma unroll 1
   for (int sim = 0; sim < sa.S; ++sim) {
     MUZ_STAMP(0);
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
         }
         int bi = a;
         row_argmax(sc, bi);
-        const int child = __shfl(k.index, bi, 32);
+        const int child = __shfl(k.index, bi, kRowLanes);
         if (a == bi) {
           p_node[row][depth] = node;
           p_act[row][depth] = bi;
@@ -284,7 +285,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     } else if (a == 0) {
       s_act[row] = 0;
     }
-    __syncthreads();
+    ST(ST_SEL);
+    SYNC();
     MUZ_STAMP(1);   // select
     // ---------------- expand (search.py expand): parent embedding -> recurrent_fn
     {
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     // Weight table = kernel argument 0, read through the kernarg segment and laundered once per
     // simulation so the compiler re-derives the layer addresses inside the loop.
     const AS4 muz_net_w* wl = kernarg0<muz_net_w>();
-    dyn16<2>(wl->dyn, A, s_act, ar, pf, &wl->pred.rb[0].d0, LAT, LAT);
+    dyn16<NT256>(wl->dyn, A, s_act, ar, pf, &wl->pred.rb[0].d0, LAT, LAT);
     MUZ_STAMP(3);   // dynamics
     const int nx = s_next[row];
     if (valid) {
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     }
     __syncthreads();
     MUZ_STAMP(4);   // embedding write
-    pred16<4>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d12, 64, 512);
+    pred16<NT512>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d12, 64, 512);
     MUZ_STAMP(5);   // prediction
     if (valid) {
       const bool fresh = nx == sim + 1;
@@ -358,6 +360,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
   if (threadIdx.x == 0)
     for (int i = 0; i < 8; ++i) atomicAdd(&g_muz_stamps[i], st_acc[i]);
 #endif
+  st_end();
 
   // ---------------- final action + action_weights (policies.py gumbel_muzero_policy tail)
   if (valid) {
@@ -437,6 +440,18 @@ int muz_gumbel_search(const muz_net_w* w, const muz_search_cfg* cfg, const float
   return launch_gumbel_search(*w, sa, root_logits, root_value, root_embedding, legal_bits, gumbel, game_id, n, nullptr,
                               workspace, action, action_weights, root_value_out, (hipStream_t)stream);
 }
+
+#ifdef MUZ_STAMPS2
+int muz_diag_stamps2(unsigned long long* host_out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_st2), sizeof(unsigned long long) * ST_N);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    unsigned long long z[ST_N] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_st2), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
 
 #ifdef MUZ_STAMPS
 int muz_diag_stamps(unsigned long long* host_out, int reset) {

@@ -19,7 +19,6 @@ from . import lib as _L
 from .lib import MuzNetW  # struct layout of include/muz.h
 
 LATENT = 256
-NW = 8   # waves per 16-row tile workgroup (csrc/nn.hpp kWaves): column groups of the packed layers
 
 
 # ---------------------------------------------------------------------------------- parameters
@@ -84,6 +83,11 @@ def init_muzero_params(seed: int, obs_channels: int, num_actions: int = 24) -> d
 
 
 # ---------------------------------------------------------------------------------- packing
+def nt_for(N: int, nw: int) -> int:
+    """16-column MFMA tiles per wave for a layer of N outputs split over nw waves (csrc/nn.hpp:nt_for)."""
+    return -(-N // (16 * nw))
+
+
 def pack_dense(W: np.ndarray, nw: int, nt: int) -> np.ndarray:
     """MFMA 16x16x4 B-fragment packing (layout documented in include/muz.h):
     out[w][kb][lane][t][j] = W[kb*16 + 4*(lane>>4) + j][(w*nt + t)*16 + (lane&15)]."""
@@ -104,6 +108,8 @@ class DeviceNet:
 
     def __init__(self, params: dict, obs_channels: int, num_actions: int = 24, device="cuda"):
         self.C, self.A = int(obs_channels), int(num_actions)
+        NW = _L.load().muz_tile_waves()   # column groups of the packed 16-row layers (csrc/nn.hpp kWaves)
+        self.waves = NW
         self._chunks = []
         self._off = 0
         P = {k: np.asarray(v, np.float32) for k, v in params.items()}
@@ -112,9 +118,10 @@ class DeviceNet:
         w = MuzNetW()
         w.obs_channels, w.num_actions = self.C, self.A
 
-        def dense(name, nw=NW, nt=None):
+        def dense(name, nw=None, nt=None):
+            nw = NW if nw is None else nw
             k = P[f"{name}/kernel"]
-            nt = nt if nt is not None else -(-k.shape[1] // (16 * nw))
+            nt = nt if nt is not None else nt_for(k.shape[1], nw)
             return (put(pack_dense(k, nw, nt)), put(P[f"{name}/bias"]))
 
         def ln(name):
@@ -138,18 +145,18 @@ class DeviceNet:
         k6, k7 = P[f"{d}/Dense_6/kernel"], P[f"{d}/Dense_7/kernel"]
         spec["dyn"] = dict(
             d0=(put(P[f"{d}/Dense_0/kernel"]), put(P[f"{d}/Dense_0/bias"])), ln0=ln(f"{d}/LayerNorm_0"),
-            d12=(put(pack_dense(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1), NW, 4)),
+            d12=(put(pack_dense(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1), NW, nt_for(512, NW))),
                  put(np.concatenate([P[f"{d}/Dense_1/bias"], P[f"{d}/Dense_2/bias"]]))),
             d3=dense(f"{d}/Dense_3"), ln1=ln(f"{d}/LayerNorm_1"), d4=dense(f"{d}/Dense_4"),
             ln2=ln(f"{d}/LayerNorm_2"), rb=[rb(f"{d}/ResBlock_{i}") for i in range(2)], d5=dense(f"{d}/Dense_5"),
-            d67=(put(pack_dense(np.concatenate([k6[:LATENT], k7[:LATENT]], 1), NW, 1)),
+            d67=(put(pack_dense(np.concatenate([k6[:LATENT], k7[:LATENT]], 1), NW, nt_for(128, NW))),
                  put(np.concatenate([P[f"{d}/Dense_6/bias"], P[f"{d}/Dense_7/bias"]]))),
             d67_onehot=put(np.concatenate([k6[LATENT:LATENT + A], k7[LATENT:LATENT + A]], 1)),
             reward_head=(put(P[f"{d}/reward_head/kernel"]), put(P[f"{d}/reward_head/bias"])),
             discount_head=(put(P[f"{d}/discount_head/kernel"]), put(P[f"{d}/discount_head/bias"])))
         spec["pred"] = dict(
             ln0=ln(f"{p}/LayerNorm_0"), rb=[rb(f"{p}/ResBlock_{i}") for i in range(2)],
-            d03=(put(pack_dense(np.concatenate([P[f"{p}/Dense_0/kernel"], P[f"{p}/Dense_3/kernel"]], 1), NW, 3)),
+            d03=(put(pack_dense(np.concatenate([P[f"{p}/Dense_0/kernel"], P[f"{p}/Dense_3/kernel"]], 1), NW, nt_for(384, NW))),
                  put(np.concatenate([P[f"{p}/Dense_0/bias"], P[f"{p}/Dense_3/bias"]]))),
             ln1=ln(f"{p}/LayerNorm_1"), d1=dense(f"{p}/Dense_1"), ln2=ln(f"{p}/LayerNorm_2"),
             d2=dense(f"{p}/Dense_2"), ln3=ln(f"{p}/LayerNorm_3"), d4=dense(f"{p}/Dense_4"),

@@ -97,7 +97,7 @@ int muz_detmadn_encode_i8(const muz_rules* rules, muz_detmadn_soa state, int8_t*
 
 /* ---- MuZero networks (MuZero_det_MADN/muzero_deterministic_madn.py) --------------------------
  * Dense layers used by the MFMA kernels take their kernel W[K][N] PACKED for
- * v_mfma_f32_16x16x4_f32 B-fragments: [group][K/16][lane 64][tile NT][j 4] with
+ * v_mfma_f32_16x16x4_f32 B-fragments: [group][K/16][lane 64][tile NT][j 4] (group = wave, see muz_tile_waves) with
  * element = W[kb*16 + 4*(lane>>4) + j][(group*NT + t)*16 + (lane&15)], zero padded
  * (exploring-muzero-on-dog_amd/nets.py:pack_dense).  Layers marked "plain" are row-major [K][N].
  * Biases / LayerNorm scale+bias are plain fp32 vectors. */
@@ -163,6 +163,10 @@ typedef struct muz_net_w {
   muz_dyn_w dyn;
   muz_pred_w pred;
 } muz_net_w;
+
+/* Waves per 16-row tile workgroup the kernels were built for = number of column groups in the packed
+ * layout of every 16-row dense layer (the host packs weights with this value). */
+int32_t muz_tile_waves(void);
 
 /* Scratch bytes muz_nets_root needs for n observations (conv feature maps). */
 int64_t muz_nets_root_scratch_bytes(int32_t n);
