@@ -25,10 +25,10 @@ __device__ __forceinline__ void ln_positions(const float* pre, float* out, int o
     s += v[i];
     s2 += v[i] * v[i];
   }
-  s += __shfl_xor(s, 1, 4);
-  s += __shfl_xor(s, 2, 4);
-  s2 += __shfl_xor(s2, 1, 4);
-  s2 += __shfl_xor(s2, 2, 4);
+  s += dpp<DPP_XOR1>(s);
+  s += dpp<DPP_XOR2>(s);
+  s2 += dpp<DPP_XOR1>(s2);
+  s2 += dpp<DPP_XOR2>(s2);
   const float mean = s / (float)N, mean2 = s2 / (float)N;
   const float inv = 1.0f / sqrtf(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
 #pragma unroll
@@ -159,20 +159,18 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
                                                    float* discount, float* prior_logits, float* value,
                                                    float* next_emb) {
   __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
-  __shared__ int act[kRows];
   const Arena a = Arena::carve(smem);
   const int A = Wt.num_actions;
   const int g0 = blockIdx.x * kRows;
   const int row = trow(), sub = tsub();
   const int gr = g0 + row;
   const bool valid = gr < n;
-  for (int c = sub; c < LAT; c += kRowLanes) a.L[row * LD + c] = valid ? emb[(size_t)gr * LAT + c] : 0.f;
-  if (sub == 0) act[row] = valid ? action[gr] : 0;
   const AS4 muz_net_w* W = kernarg0<muz_net_w>();   // == Wt, read through the kernarg segment
+  const int ar = valid ? action[gr] : 0;
+  const DynIn din = dyn_load(W->dyn, A, valid ? gp(emb) + (size_t)gr * LAT : nullptr, ar);
   Pf pf;
-  pf_issue<NT512>(pf, &W->dyn.d12, 64, 512);
-  __syncthreads();
-  dyn16<NT256>(W->dyn, A, act, a, pf, &W->pred.rb[0].d0, LAT, LAT);
+  pf_issue<NT256>(pf, &W->dyn.d3, LAT, LAT);
+  dyn16<NT256>(W->dyn, A, din, ar, a, pf, &W->pred.rb[0].d0, LAT, LAT);
   if (valid) {
     for (int c = sub; c < LAT; c += kRowLanes) next_emb[(size_t)gr * LAT + c] = a.T[row * LD + c];
     if (sub == 0) {
@@ -180,7 +178,7 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
       discount[gr] = a.v2[row];
     }
   }
-  __syncthreads();
+  // no barrier: pred16 reads a.T in its first pass and overwrites it only after its first SYNC
   pred16<1>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
   if (valid) {
     for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
@@ -188,8 +186,26 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
   }
 }
 
+// dyn.film[a][0:256 | 256:512] = Dense_1 | Dense_2 (relu(Dense_0(one_hot(a))))  (Dyn4 lines 399-411):
+// FiLM scale | shift depend on the action only.  Row A = zero one-hot (out-of-range action).
+// One workgroup per action row, one thread per output column; d12 is read in its packed layout.
+__global__ __launch_bounds__(512) void k_film(muz_dyn_w D, int A) {
+  __shared__ float e[64];
+  const int a = blockIdx.x, n = threadIdx.x;
+  if (n < 64) e[n] = fmaxf((a < A ? D.d0.w[a * 64 + n] : 0.f) + D.d0.b[n], 0.f);
+  __syncthreads();
+  const int w = (n >> 4) / NT512, t = (n >> 4) % NT512;
+  float acc = 0.f;
+  for (int k = 0; k < 64; ++k) {
+    const int kb = k >> 4, lane = ((k & 15) >> 2) * 16 + (n & 15), j = k & 3;
+    acc = fmaf(e[k], D.d12.w[((((size_t)w * 4 + kb) * 64 + lane) * NT512 + t) * 4 + j], acc);
+  }
+  D.film[a * 512 + n] = acc + D.d12.b[n];
+}
+
 int check_net(const muz_net_w* w) {
   if (!w) return MUZ_E_INVALID;
+  if (!w->dyn.film) return MUZ_E_INVALID;
   if (w->num_actions != MUZ_DET_ACTIONS) return MUZ_E_UNSUPPORTED;
   if (w->obs_channels < 7 || w->obs_channels > 38) return MUZ_E_UNSUPPORTED;
   return MUZ_OK;
@@ -211,6 +227,13 @@ using namespace muz;
 extern "C" {
 
 int32_t muz_tile_waves(void) { return kWaves; }
+
+int muz_net_prepare(const muz_net_w* w, void* stream) {
+  if (!w || !w->dyn.film || !w->dyn.d0.w || !w->dyn.d0.b || !w->dyn.d12.w || !w->dyn.d12.b) return MUZ_E_INVALID;
+  if (w->num_actions != MUZ_DET_ACTIONS) return MUZ_E_UNSUPPORTED;
+  k_film<<<w->num_actions + 1, 512, 0, (hipStream_t)stream>>>(w->dyn, w->num_actions);
+  return muz_last_launch_error();
+}
 
 int64_t muz_nets_root_scratch_bytes(int32_t n) {
   const int64_t rows = ((int64_t)n + kRows - 1) / kRows * kRows;

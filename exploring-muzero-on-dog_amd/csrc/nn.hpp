@@ -106,6 +106,9 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
 #pragma unroll
       for (int t = 0; t < NT; ++t) nxt[t] = wp[(kb + D) * wstep + t];
     }
+    // Pin the issue point: without this the machine scheduler sinks each weight load next to its
+    // first MFMA (one step of cover instead of D) once the loop is fully unrolled.
+    __builtin_amdgcn_sched_barrier(0);
     f32x4 a;
     if (MUZ_A_PRELOAD) {
       if (kb + 1 < KB) anxt = lda4(kb + 1);
@@ -173,7 +176,7 @@ __device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB
 // ---- cross-layer weight prefetch ----------------------------------------------------------------
 // Every dense layer issues the first two k-blocks of the NEXT layer's weights for this wave before its
 // epilogue, so the loads fly across the epilogue, the barrier and the LayerNorm pass in between.
-constexpr int kPfMax = NT512;
+constexpr int kPfMax = NT384;
 struct Pf {
   f32x4 v0[kPfMax], v1[kPfMax];
 };
@@ -238,30 +241,73 @@ __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, co
 // ---- row-wise ops: thread t -> row t/32, lane-in-row t%32 (half a wave per row) ---------------------
 __device__ __forceinline__ int trow() { return threadIdx.x / kRowLanes; }
 __device__ __forceinline__ int tsub() { return threadIdx.x % kRowLanes; }
-__device__ __forceinline__ float row_sum(float v) {
-#pragma unroll
-  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, kRowLanes);
+// Row reductions on the DPP / permlane network instead of ds_bpermute (which goes through the LDS
+// crossbar): xor-1 and xor-2 as quad_perm, then half-row and row mirrors, then a permlane swap across
+// the two 16-lane rows of a 32-lane row (and across wave halves for 64-lane rows).  Every lane of a
+// row ends with the same bits: each step combines a commutative pair in both lanes.
+template <class T>
+__device__ __forceinline__ unsigned as_u(T v) {
+  return __builtin_bit_cast(unsigned, v);
+}
+template <class T>
+__device__ __forceinline__ T from_u(unsigned u) {
+  return __builtin_bit_cast(T, u);
+}
+template <int CTRL, class T>
+__device__ __forceinline__ T dpp(T v) {
+  return from_u<T>((unsigned)__builtin_amdgcn_update_dpp(0, (int)as_u(v), CTRL, 0xF, 0xF, false));
+}
+enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140 };
+template <class T>
+struct LoHi {
+  T lo, hi;
+};
+// {value of the lower 16-lane row, value of the upper one} of each 32-lane group, in every lane.
+// (The two results are copied to plain scalars before the bit cast: bit-casting the vector element
+// directly loses the second result in this compiler.)
+template <class T>
+__device__ __forceinline__ LoHi<T> swap16(T v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(as_u(v), as_u(v), false, false);
+  const unsigned lo = p[0], hi = p[1];
+  return {from_u<T>(lo), from_u<T>(hi)};
+}
+template <class T>
+__device__ __forceinline__ LoHi<T> swap32(T v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(as_u(v), as_u(v), false, false);
+  const unsigned lo = p[0], hi = p[1];
+  return {from_u<T>(lo), from_u<T>(hi)};
+}
+template <class T, class F>
+__device__ __forceinline__ T row_reduce(T v, F f) {
+  static_assert(kRowLanes == 32 || kRowLanes == 64, "row width");
+  v = f(v, dpp<DPP_XOR1>(v));
+  v = f(v, dpp<DPP_XOR2>(v));
+  v = f(v, dpp<DPP_HALF_MIRROR>(v));
+  v = f(v, dpp<DPP_MIRROR>(v));
+  {
+    const LoHi<T> p = swap16(v);
+    v = f(p.lo, p.hi);
+  }
+  if constexpr (kRowLanes == 64) {
+    const LoHi<T> p = swap32(v);
+    v = f(p.lo, p.hi);
+  }
   return v;
+}
+__device__ __forceinline__ float row_sum(float v) {
+  return row_reduce(v, [](float x, float y) { return x + y; });
 }
 __device__ __forceinline__ float row_max(float v) {
-#pragma unroll
-  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, kRowLanes));
-  return v;
+  return row_reduce(v, [](float x, float y) { return fmaxf(x, y); });
 }
 __device__ __forceinline__ float row_min(float v) {
-#pragma unroll
-  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v = fminf(v, __shfl_xor(v, m, kRowLanes));
-  return v;
+  return row_reduce(v, [](float x, float y) { return fminf(x, y); });
 }
 __device__ __forceinline__ int row_isum(int v) {
-#pragma unroll
-  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, kRowLanes);
-  return v;
+  return row_reduce(v, [](int x, int y) { return x + y; });
 }
 __device__ __forceinline__ int row_imax(int v) {
-#pragma unroll
-  for (int m = kRowLanes / 2; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, kRowLanes));
-  return v;
+  return row_reduce(v, [](int x, int y) { return max(x, y); });
 }
 
 enum LnMode { LN_PLAIN = 0, LN_RELU = 1, LN_RESID_RELU = 2 };
@@ -500,27 +546,72 @@ __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) 
 // DynamicsNetwork4 (muzero_deterministic_madn.py:391-457): latent a.L, action per row in act[16].
 // Leaves the next latent in a.T, reward / discount expectations in a.v1 / a.v2.  Clobbers X, U, W, E.
 // pf: d12 on entry, (Ln, NTN tiles) on exit.
+// Dyn4 inputs of this thread's row, loaded as soon as the parent node and action are known (end of the
+// tree walk) so their latency hides under the selection barrier: the parent latent (RowVec<LAT> layout),
+// the action's FiLM rows and LayerNorm_0's parameters.  FiLM scale | shift depend on the action only
+// (Dense_1/2(relu(Dense_0(one_hot(a))))), so they come from the per-weight-set table dyn.film
+// (muz_net_prepare); row A is the zero one-hot of an out-of-range action.
+struct DynIn {
+  f32x4 lat[RowVec<LAT>::V], sc[RowVec<LAT>::V], sh[RowVec<LAT>::V];
+  LnP<LAT> ln0;
+};
+__device__ __forceinline__ DynIn dyn_load(const AS4 muz_dyn_w& D, int A, const AS1 float* lat, int action) {
+  using RV = RowVec<LAT>;
+  DynIn in;
+  const int sub = tsub();
+  const int fr = (action >= 0 && action < A) ? action : A;
+  const AS1 f32x4* film = gp(reinterpret_cast<const f32x4*>(D.film)) + fr * (2 * LAT / 4);
+#pragma unroll
+  for (int i = 0; i < RV::V; ++i) {
+    const int c = RV::col(sub, i);
+    in.lat[i] = lat ? *reinterpret_cast<const AS1 f32x4*>(lat + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    in.sc[i] = film[c >> 2];
+    in.sh[i] = film[(LAT + c) >> 2];
+  }
+  in.ln0 = ln_load<LAT>(D.ln0);
+  return in;
+}
+
+// DynamicsNetwork4 (muzero_deterministic_madn.py:391-457) on the tile.  `in` = this thread's row inputs,
+// `ar` = this row's action.  Out: next latent in a.T, reward / discount support values in a.v1 / a.v2.
+// pf: d3 on entry, (Ln: Kn x Nn, NTN tiles) on exit.
 template <int NTN>
-__device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const int* act, const Arena& a, Pf& pf,
+__device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn& in, int ar, const Arena& a, Pf& pf,
                                       const AS4 muz_dense* Ln, int Kn, int Nn) {
+  using RV = RowVec<LAT>;
   const int row = trow(), sub = tsub();
-  const int ar = act[row];
   const bool oh = ar >= 0 && ar < A;   // jax.nn.one_hot: out-of-range -> zero row
-  // action embedding: relu(one_hot @ W0 + b0) == relu(W0[a] + b0)
-  const AS1 float* w0 = gp(D.d0.w);
-  const AS1 float* b0 = gp(D.d0.b);
-  for (int c = sub; c < 64; c += kRowLanes)
-    a.E[row * LDE + c] = fmaxf((oh ? w0[ar * 64 + c] : 0.f) + b0[c], 0.f);
-  ln16<LAT, LN_PLAIN>(a.L, LD, a.X, LD, D.ln0);
-  SYNC();
-  const LnP<LAT> p1 = ln_load<LAT>(D.ln1);
-  dense16<NT512, NT256>(D.d12, 64, 512, a.E, LDE, a.W, LDW, pf, &D.d3, LAT, LAT);     // [scale | shift]
-  SYNC();
-  for (int c = sub * 4; c < LAT; c += 4 * kRowLanes) {
-    const f32x4 x = lds4(a.X + row * LD + c), sc = lds4(a.W + row * LDW + c), sh = lds4(a.W + row * LDW + 256 + c);
-    sts4(a.X + row * LD + c, x * (1.0f + sc) + sh);
+  // LayerNorm_0 of the latent + FiLM, in registers: X = LN0(L) * (1 + scale) + shift; L kept for the skip
+  {
+    float s = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < RV::V; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s += in.lat[i][q];
+        s2 += in.lat[i][q] * in.lat[i][q];
+      }
+    s = row_sum(s);
+    s2 = row_sum(s2);
+    const float mean = s / (float)LAT;
+    const float mean2 = s2 / (float)LAT;
+    const float inv = 1.0f / sqrtf(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
+#pragma unroll
+    for (int i = 0; i < RV::V; ++i) {
+      const int c = RV::col(sub, i);
+      f32x4 x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float y = (in.lat[i][q] - mean) * (inv * in.ln0.sc[i][q]) + in.ln0.sh[i][q];
+        x[q] = y * (1.0f + in.sc[i][q]) + in.sh[i][q];
+      }
+      sts4(a.X + row * LD + c, x);
+      sts4(a.L + row * LD + c, in.lat[i]);
+    }
+    ST(ST_ROW);
   }
   SYNC();
+  const LnP<LAT> p1 = ln_load<LAT>(D.ln1);
   dense16<NT256, NT256>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT);
   SYNC();
   ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, p1);

@@ -82,14 +82,30 @@ static TreeWs carve_ws(void* ws, int n, int N) {
 
 // ---- one game per 32 lanes (half a wave), one action per lane; jnp.argmax tie-break (first index) ----
 __device__ __forceinline__ void row_argmax(float& v, int& i) {
-#pragma unroll
-  for (int m = kRowLanes / 2; m >= 1; m >>= 1) {
-    const float ov = __shfl_xor(v, m, kRowLanes);
-    const int oi = __shfl_xor(i, m, kRowLanes);
+  // (value, index) pairs under the order "larger value, then smaller index" (jnp.argmax tie-break)
+  auto pick = [](float& v, int& i, float ov, int oi) {
     if (ov > v || (ov == v && oi < i)) {
       v = ov;
       i = oi;
     }
+  };
+  pick(v, i, dpp<DPP_XOR1>(v), dpp<DPP_XOR1>(i));
+  pick(v, i, dpp<DPP_XOR2>(v), dpp<DPP_XOR2>(i));
+  pick(v, i, dpp<DPP_HALF_MIRROR>(v), dpp<DPP_HALF_MIRROR>(i));
+  pick(v, i, dpp<DPP_MIRROR>(v), dpp<DPP_MIRROR>(i));
+  {
+    const LoHi<float> pv = swap16(v);
+    const LoHi<int> pi = swap16(i);
+    v = pv.lo;
+    i = pi.lo;
+    pick(v, i, pv.hi, pi.hi);
+  }
+  if constexpr (kRowLanes == 64) {
+    const LoHi<float> pv = swap32(v);
+    const LoHi<int> pi = swap32(i);
+    v = pv.lo;
+    i = pi.lo;
+    pick(v, i, pv.hi, pi.hi);
   }
 }
 
@@ -171,6 +187,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
   __shared__ float p_rew[kRows][kMaxDepth];
   __shared__ float p_disc[kRows][kMaxDepth];
   __shared__ int s_act[kRows], s_parent[kRows], s_next[kRows], s_depth[kRows];
+  __shared__ float s_rootv[kRows];
 
   if (n_dev) n = *n_dev;
   if ((int)blockIdx.x * kRows >= n) return;
@@ -190,22 +207,24 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
   unsigned lb = 0;
   int ncons = 0;
   float gum = 0.f;
+  // The root's children live in registers (lane a holds child a) for the whole search: the root is
+  // visited by every simulation, so its edge data never goes through HBM.
+  Kid rk;
+  rk.ok = ok;
+  rk.prior = kFMin;
+  rk.value = 0.f;
+  rk.reward = 0.f;
+  rk.disc = 0.f;
+  rk.visits = 0;
+  rk.index = -1;
   if (valid) {
     lb = legal[g];
     const int gid = game_id ? game_id[g] : g;
     const float l = ok ? root_logits[(size_t)g * A + ai] : -INFINITY;
     const float lm = row_max(l);
     const bool inv = !ok || ((lb >> a) & 1u) == 0u;
-    const size_t b0 = T.ca(g, 0, ai);
-    if (ok) {
-      T.prior()[b0] = inv ? kFMin : l - lm;
-      T.index()[b0] = -1;
-      T.visits()[b0] = 0;
-      T.value()[b0] = 0.f;
-      T.reward()[b0] = 0.f;
-      T.disc()[b0] = 0.f;
-      gum = gumbel_in ? gumbel_in[(size_t)g * A + ai] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, sa.turn, ai);
-    }
+    rk.prior = inv ? kFMin : l - lm;
+    if (ok) gum = gumbel_in ? gumbel_in[(size_t)g * A + ai] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, sa.turn, ai);
     AS1 float* e0 = T.e(g, 0);
     for (int c = a; c < LAT; c += kRowLanes) e0[c] = root_emb[(size_t)g * LAT + c];
     ncons = min(sa.max_considered, __popc(lb & ((1u << A) - 1u)));
@@ -234,15 +253,20 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
 
   st_begin();
   Pf pf;   // first k-blocks of the next dense layer (crosses the select / expand phases)
-  pf_issue<NT512>(pf, &kernarg0<muz_net_w>()->dyn.d12, 64, 512);
+  pf_issue<NT256>(pf, &kernarg0<muz_net_w>()->dyn.d3, LAT, LAT);
 #pragma unroll 1
   for (int sim = 0; sim < sa.S; ++sim) {
     MUZ_STAMP(0);
+    // Weight table = kernel argument 0, read through the kernarg segment and laundered once per
+    // simulation so the compiler re-derives the layer addresses inside the loop.
+    const AS4 muz_net_w* wl = kernarg0<muz_net_w>();
+    DynIn din;
+    int dact = 0;
     // ---------------- simulate (search.py simulate): walk from the root
     if (valid) {
       int node = 0, depth = 0, act = 0, nxt = -1;
       while (true) {
-        const Kid k = load_kid(node);
+        const Kid k = depth == 0 ? rk : load_kid(node);
         int sumv;
         float pmax;
         const float cq = completed_q(k, s_raw[row][node], sa, sumv, pmax);
@@ -276,38 +300,34 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
         if (child == -1 || depth >= sa.D) break;
         node = child;
       }
+      // expand's inputs (parent embedding, FiLM rows of the action): issued by the game's own lanes now,
+      // they land while the other games finish their walks
+      din = dyn_load(wl->dyn, A, T.e(g, node), act);
+      dact = act;
       if (a == 0) {
         s_parent[row] = node;
         s_act[row] = act;
         s_next[row] = (nxt == -1) ? sim + 1 : nxt;
         s_depth[row] = depth;
       }
-    } else if (a == 0) {
-      s_act[row] = 0;
+    } else {
+      din = dyn_load(wl->dyn, A, nullptr, 0);
+      if (a == 0) s_act[row] = 0;
     }
     ST(ST_SEL);
     SYNC();
     MUZ_STAMP(1);   // select
-    // ---------------- expand (search.py expand): parent embedding -> recurrent_fn
-    {
-      const AS1 float* pe = valid ? T.e(g, s_parent[row]) : nullptr;
-      for (int c = a; c < LAT; c += kRowLanes) ar.L[row * LD + c] = valid ? pe[c] : 0.f;
-    }
-    __syncthreads();
-    MUZ_STAMP(2);   // gather
-    // Weight table = kernel argument 0, read through the kernarg segment and laundered once per
-    // simulation so the compiler re-derives the layer addresses inside the loop.
-    const AS4 muz_net_w* wl = kernarg0<muz_net_w>();
-    dyn16<NT256>(wl->dyn, A, s_act, ar, pf, &wl->pred.rb[0].d0, LAT, LAT);
+    // ---------------- expand (search.py expand): recurrent_fn on the 16 parents
+    dyn16<NT256>(wl->dyn, A, din, dact, ar, pf, &wl->pred.rb[0].d0, LAT, LAT);
     MUZ_STAMP(3);   // dynamics
     const int nx = s_next[row];
     if (valid) {
       AS1 float* ne = T.e(g, nx);
       for (int c = a; c < LAT; c += kRowLanes) ne[c] = ar.T[row * LD + c];
     }
-    __syncthreads();
+    // no barrier: pred16 reads ar.T in its first pass and overwrites it only after its first SYNC
     MUZ_STAMP(4);   // embedding write
-    pred16<NT512>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d12, 64, 512);
+    pred16<NT256>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d3, LAT, LAT);
     MUZ_STAMP(5);   // prediction
     if (valid) {
       const bool fresh = nx == sim + 1;
@@ -322,13 +342,20 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
           T.disc()[nb] = 0.f;
         }
       }
+      const int par = s_parent[row], pa = s_act[row];
+      if (par == 0 && a == pa) {   // a root edge: registers
+        rk.index = nx;
+        rk.reward = ar.v1[row];
+        rk.disc = ar.v2[row];
+      }
       if (a == 0) {
-        const int par = s_parent[row], pa = s_act[row];
         const float v = ar.v0[row], rw = ar.v1[row], dc = ar.v2[row];
-        const size_t eb = T.ca(g, par, pa);
-        T.index()[eb] = nx;
-        T.reward()[eb] = rw;
-        T.disc()[eb] = dc;
+        if (par != 0) {
+          const size_t eb = T.ca(g, par, pa);
+          T.index()[eb] = nx;
+          T.reward()[eb] = rw;
+          T.disc()[eb] = dc;
+        }
         s_raw[row][nx] = v;
         s_val[row][nx] = v;
         s_visits[row][nx] = fresh ? 1 : s_visits[row][nx] + 1;
@@ -344,13 +371,24 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
           const float dsc = (lvl == d - 1) ? dc : p_disc[row][lvl];
           leaf = r + dsc * leaf;
           const float pv = (s_val[row][parent] * (float)cnt + leaf) / ((float)cnt + 1.0f);
-          const size_t ei = T.ca(g, parent, pact);
-          T.value()[ei] = s_val[row][idx];
-          T.visits()[ei] = p_cvis[row][lvl] + 1;
+          if (lvl > 0) {
+            const size_t ei = T.ca(g, parent, pact);
+            T.value()[ei] = s_val[row][idx];
+            T.visits()[ei] = p_cvis[row][lvl] + 1;
+          } else {
+            s_rootv[row] = s_val[row][idx];
+          }
           s_val[row][parent] = pv;
           s_visits[row][parent] = cnt + 1;
           idx = parent;
         }
+      }
+      // the root edge of this path (level 0): its lane takes the value lane 0 just backed up
+      // (same wave: LDS operations of one wave complete in order)
+      __builtin_amdgcn_wave_barrier();
+      if (a == p_act[row][0]) {
+        rk.value = s_rootv[row];
+        rk.visits += 1;
       }
     }
     __syncthreads();
@@ -364,7 +402,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
 
   // ---------------- final action + action_weights (policies.py gumbel_muzero_policy tail)
   if (valid) {
-    const Kid k = load_kid(0);
+    const Kid& k = rk;
     int sumv;
     float pmax;
     const float cq = completed_q(k, s_raw[row][0], sa, sumv, pmax);

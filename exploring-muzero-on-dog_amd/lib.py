@@ -73,7 +73,8 @@ class MuzReprW(ctypes.Structure):
 class MuzDynW(ctypes.Structure):
     _fields_ = [("d0", MuzDense), ("ln0", MuzLn), ("d12", MuzDense), ("d3", MuzDense), ("ln1", MuzLn),
                 ("d4", MuzDense), ("ln2", MuzLn), ("rb", MuzResblock * 2), ("d5", MuzDense), ("d67", MuzDense),
-                ("d67_onehot", vp), ("reward_head", MuzDense), ("discount_head", MuzDense)]
+                ("d67_onehot", vp), ("reward_head", MuzDense), ("discount_head", MuzDense),
+                ("film", vp)]
 
 
 class MuzPredW(ctypes.Structure):
@@ -117,6 +118,7 @@ SIGNATURES = {
     "muz_detmadn_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_tile_waves": (ctypes.c_int32, []),
+    "muz_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzNetW), ctypes.c_void_p]),
     "muz_nets_root_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "muz_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp,
                                      vp]),

@@ -10,6 +10,7 @@ Host side of the fused fp32 MFMA network kernels (csrc/nets.hip, csrc/nn.hpp):
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
@@ -153,7 +154,8 @@ class DeviceNet:
                  put(np.concatenate([P[f"{d}/Dense_6/bias"], P[f"{d}/Dense_7/bias"]]))),
             d67_onehot=put(np.concatenate([k6[LATENT:LATENT + A], k7[LATENT:LATENT + A]], 1)),
             reward_head=(put(P[f"{d}/reward_head/kernel"]), put(P[f"{d}/reward_head/bias"])),
-            discount_head=(put(P[f"{d}/discount_head/kernel"]), put(P[f"{d}/discount_head/bias"])))
+            discount_head=(put(P[f"{d}/discount_head/kernel"]), put(P[f"{d}/discount_head/bias"])),
+            film=put(np.zeros((A + 1) * 2 * LATENT, np.float32)))
         spec["pred"] = dict(
             ln0=ln(f"{p}/LayerNorm_0"), rb=[rb(f"{p}/ResBlock_{i}") for i in range(2)],
             d03=(put(pack_dense(np.concatenate([P[f"{p}/Dense_0/kernel"], P[f"{p}/Dense_3/kernel"]], 1), NW, nt_for(384, NW))),
@@ -166,6 +168,9 @@ class DeviceNet:
         base = self.buffer.data_ptr()
         self._fill(w, spec, base)
         self.w = w
+        lib = _L.load()
+        with torch.cuda.device(self.buffer.device):
+            _L.check(lib.muz_net_prepare(ctypes.byref(w), _L.stream_ptr()), "muz_net_prepare")
 
     def _put(self, arr) -> int:
         a = np.ascontiguousarray(np.asarray(arr, np.float32).reshape(-1))

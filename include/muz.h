@@ -140,6 +140,9 @@ typedef struct muz_dyn_w {
   const float* d67_onehot;      /* plain [A][128]: one-hot rows 256.. of Dense_6 | Dense_7 */
   muz_dense reward_head;        /* plain [64][3] */
   muz_dense discount_head;      /* plain [64][3] */
+  float* film;                  /* derived [A+1][512], filled by muz_net_prepare: FiLM scale | shift of
+                                   each action (lines 399-411 depend on the action only); row A = the
+                                   zero one-hot of an out-of-range action */
 } muz_dyn_w;
 
 /* PredictionNetwork4 (lines 549-583) */
@@ -167,6 +170,13 @@ typedef struct muz_net_w {
 /* Waves per 16-row tile workgroup the kernels were built for = number of column groups in the packed
  * layout of every 16-row dense layer (the host packs weights with this value). */
 int32_t muz_tile_waves(void);
+
+/* Fills the derived tables of a weight set (dyn.film) from its raw layers; call once after the weights
+ * change and before any muz_nets_recurrent / muz_gumbel_search / muz_detmadn_selfplay on them.
+ * Replaces nothing in the reference: the FiLM sub-graph of DynamicsNetwork4.__call__
+ * (MuZero_det_MADN/muzero_deterministic_madn.py:398-411) depends on the action only, so it is
+ * evaluated once per action instead of once per simulation. */
+int muz_net_prepare(const muz_net_w* w, void* stream);
 
 /* Scratch bytes muz_nets_root needs for n observations (conv feature maps). */
 int64_t muz_nets_root_scratch_bytes(int32_t n);
