@@ -31,6 +31,10 @@ PLAYERS = 2
 # Algorithmic work per simulation: DynamicsNetwork4 529,280 MAC + PredictionNetwork4 404,544 MAC
 # (recomputed in DESIGN.md) -> FLOP = 2 x MAC.
 FLOP_PER_SIM = 2 * (529_280 + 404_544)
+# What the kernel executes per simulation: the FiLM sub-graph (Dense_0 -> Dense_1|Dense_2) depends on the
+# action only and is tabulated once per weight set (muz_net_prepare), and one-hot products are row
+# gathers: Dyn4 491,904 MAC (d3, d4, 2 ResBlocks, d5, Dense_6|7 latent rows, heads) + Pred4 404,544 MAC.
+EXEC_FLOP_PER_SIM = 2 * (491_904 + 404_544)
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
 
 
@@ -111,6 +115,17 @@ def cpu_baseline(seconds, sims, depth, max_steps):
                       f"in {dt:.1f}s, BLAS threads={cores}"}
 
 
+def measured_traffic():
+    """HBM bytes per k_gumbel_search launch from the newest committed PMC summary (profiles/*_traffic.json,
+    written by profiles/summarize_profile.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return None, None
+    t = json.load(open(files[-1]))
+    return t.get("bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     args = parse()
     rank, world, local = dist_env()
@@ -167,6 +182,7 @@ def main():
         return
     value = steps_done / elapsed
     # roofline of the dominant kernel (k_gumbel_search): algorithmic FLOP / HIP-event time of its launches
+    traffic, traffic_src = measured_traffic()
     flop = searches * args.sims * FLOP_PER_SIM
     achieved = flop / (search_ms * 1e-3) / 1e12 if search_ms > 0 else 0.0
     out = {
@@ -193,7 +209,9 @@ def main():
                      "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
                      "avg_launch_ms": round(search_ms / max(1, launches), 4),
-                     "flop_per_sim": FLOP_PER_SIM, "traffic": None},
+                     "flop_per_sim": FLOP_PER_SIM, "executed_flop_per_sim": EXEC_FLOP_PER_SIM,
+                     "executed_frac": round(achieved * EXEC_FLOP_PER_SIM / FLOP_PER_SIM / PEAK_FP32_MFMA_TFLOPS, 4),
+                     "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src},
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.sims, args.depth, args.max_steps)

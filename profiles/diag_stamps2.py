@@ -4,7 +4,7 @@
     MUZ_LIB=$PWD/exploring-muzero-on-dog_amd/variants/libmuz_st2.so python profiles/diag_stamps2.py
 
 Wave 0 of each workgroup stamps: MFMA loops, dense epilogues, barrier waits, row ops (LayerNorm...),
-tree selection, other.  Shares only (stamps perturb the schedule)."""
+tree selection, other, expansion + backup, elementwise passes + heads.  Shares only (stamps perturb the schedule)."""
 import ctypes
 import os
 import sys
@@ -20,7 +20,7 @@ from exploring_muzero_on_dog_amd import lib as L  # noqa: E402
 from exploring_muzero_on_dog_amd import mcts as M  # noqa: E402
 from exploring_muzero_on_dog_amd import nets as N  # noqa: E402
 
-CATS = ["mfma-loops", "dense-epilogue", "barrier-wait", "row-ops", "select", "other"]
+CATS = ["mfma-loops", "dense-epilogue", "barrier-wait", "row-ops", "select", "other", "expand+backup", "passes+heads", "dense-entry"]
 
 
 def main():
@@ -38,13 +38,13 @@ def main():
     ws = M.SearchWorkspace(B, 50)
     M.gumbel_muzero_policy(net, lg, v, e, bits, 50, 25, 1.0, seed=1, workspace=ws)
     torch.cuda.synchronize()
-    buf = (ctypes.c_uint64 * 8)()
+    buf = (ctypes.c_uint64 * 12)()
     fn(buf, 1)
     for r in range(3):
         M.gumbel_muzero_policy(net, lg, v, e, bits, 50, 25, 1.0, seed=r, workspace=ws)
     torch.cuda.synchronize()
     fn(buf, 0)
-    tot = sum(buf[i] for i in range(6))
+    tot = sum(buf[i] for i in range(12))
     wg_sims = 3 * ((B + 15) // 16) * 50
     print(f"B={B}: {tot / wg_sims:.0f} cycles per workgroup-simulation")
     for i, c in enumerate(CATS):

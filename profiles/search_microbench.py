@@ -16,7 +16,8 @@ import torch  # noqa: E402
 from exploring_muzero_on_dog_amd import mcts as M  # noqa: E402
 from exploring_muzero_on_dog_amd import nets as N  # noqa: E402
 
-FLOP_PER_SIM = 2 * (529_280 + 404_544)
+FLOP_PER_SIM = 2 * (529_280 + 404_544)        # algorithmic
+EXEC_FLOP_PER_SIM = 2 * (491_904 + 404_544)   # executed (FiLM tabulated, one-hot rows gathered)
 
 
 def main():
