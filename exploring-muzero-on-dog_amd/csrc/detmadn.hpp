@@ -25,6 +25,7 @@ enum : uint32_t {
   R_START_ON_1 = 1u << 6,
   R_BONUS_6 = 1u << 7,
   R_MUST_TRAVERSE = 1u << 8,
+  R_DICE_RETHROW = 1u << 9,   // classic only
 };
 
 // Rule constants after env_reset's layout fix-up (deterministic_madn.py:62-78).

@@ -32,6 +32,7 @@ static inline int make_det_consts(const muz_rules* r, DetConsts* c) {
   if (r->enable_start_on_1) f |= R_START_ON_1;
   if (r->enable_bonus_turn_on_6) f |= R_BONUS_6;
   if (r->must_traverse_start) f |= R_MUST_TRAVERSE;
+  if (r->enable_dice_rethrow) f |= R_DICE_RETHROW;
   c->flags = f;
   int p = 0;
   for (int i = 0; i < 4; ++i) {

@@ -22,7 +22,8 @@ constexpr int kThreads = kWaves * 64;          // 512 / 1024
 constexpr int kRowLanes = kThreads / kRows;    // lanes per row in row-wise phases: 32 / 64
 constexpr int LAT = 256;
 // ---- diagnostic fine-grained stamps (make EXTRA=-DMUZ_STAMPS2); compiled out otherwise -------------
-enum { ST_MFMA = 0, ST_EPI = 1, ST_BAR = 2, ST_ROW = 3, ST_SEL = 4, ST_OTHER = 5, ST_N = 8 };
+enum { ST_MFMA = 0, ST_EPI = 1, ST_BAR = 2, ST_ROW = 3, ST_SEL = 4, ST_OTHER = 5, ST_TREE = 6, ST_PASS = 7, ST_DENTRY = 8,
+       ST_N = 12 };
 #ifdef MUZ_STAMPS2
 __device__ unsigned long long g_st2[ST_N];
 struct StampState {
@@ -224,7 +225,7 @@ __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, co
     b0[t] = pf.v0[t];
     b1[t] = pf.v1[t];
   }
-  ST(ST_OTHER);
+  ST(ST_DENTRY);
   mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global);
   ST(ST_MFMA);
   pf_issue<NTN>(pf, Ln, Kn, Nn);
@@ -526,12 +527,14 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
   SYNC();
   ln16<128, LN_RELU>(a.T, LD, a.T, LD, p2);
   relu16(a.X, LD, 0, 64);
+  ST(ST_PASS);
   SYNC();
   dense16<NTA, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn);         // policy logits
   {
     const float v = head_dot(a.X, LD, hv, 0);
     if (tsub() == 0) a.v0[trow()] = tanhf(v);
   }
+  ST(ST_PASS);
   SYNC();
 }
 
@@ -543,9 +546,6 @@ __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) 
   return (e0 / z) * -1.0f + (e1 / z) * 0.0f + (e2 / z) * 1.0f;
 }
 
-// DynamicsNetwork4 (muzero_deterministic_madn.py:391-457): latent a.L, action per row in act[16].
-// Leaves the next latent in a.T, reward / discount expectations in a.v1 / a.v2.  Clobbers X, U, W, E.
-// pf: d12 on entry, (Ln, NTN tiles) on exit.
 // Dyn4 inputs of this thread's row, loaded as soon as the parent node and action are known (end of the
 // tree walk) so their latency hides under the selection barrier: the parent latent (RowVec<LAT> layout),
 // the action's FiLM rows and LayerNorm_0's parameters.  FiLM scale | shift depend on the action only
@@ -629,8 +629,10 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
   SYNC();
   for (int c = sub * 4; c < LAT; c += 4 * kRowLanes)
     sts4(a.T + row * LD + c, lds4(a.L + row * LD + c) + lds4(a.T + row * LD + c));
+  ST(ST_PASS);
   SYNC();
   minmax16(a.T, LD);
+  ST(ST_PASS);
   SYNC();
   dense16<NT128, NTN>(D.d67, LAT, 128, a.T, LD, a.W, LDW, pf, Ln, Kn, Nn);   // [reward | discount] hidden
   SYNC();
@@ -639,6 +641,7 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
     const f32x4 h = lds4(a.W + row * LDW + c);
     sts4(a.W + row * LDW + c, relu4(oh ? h + w67[(ar * 128 + c) >> 2] : h));
   }
+  ST(ST_PASS);
   SYNC();
   float rl[3], dl[3];
 #pragma unroll
@@ -650,6 +653,7 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
     a.v1[row] = softmax3_support(rl[0], rl[1], rl[2]);
     a.v2[row] = softmax3_support(dl[0], dl[1], dl[2]);
   }
+  ST(ST_PASS);
   SYNC();
 }
 

@@ -326,6 +326,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
       for (int c = a; c < LAT; c += kRowLanes) ne[c] = ar.T[row * LD + c];
     }
     // no barrier: pred16 reads ar.T in its first pass and overwrites it only after its first SYNC
+    ST(ST_TREE);
     MUZ_STAMP(4);   // embedding write
     pred16<NT256>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d3, LAT, LAT);
     MUZ_STAMP(5);   // prediction
@@ -391,7 +392,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
         rk.visits += 1;
       }
     }
-    __syncthreads();
+    ST(ST_TREE);
+    SYNC();
     MUZ_STAMP(6);   // expand + backward
   }
 #ifdef MUZ_STAMPS

@@ -36,6 +36,7 @@ class MuzRules(ctypes.Structure):
         ("enable_start_on_1", ctypes.c_int32),
         ("enable_bonus_turn_on_6", ctypes.c_int32),
         ("must_traverse_start", ctypes.c_int32),
+        ("enable_dice_rethrow", ctypes.c_int32),
     ]
 
 
@@ -47,6 +48,18 @@ class MuzDetSoA(ctypes.Structure):
         ("reward", vp),
         ("done", vp),
         ("action_set", vp),
+        ("stride", ctypes.c_int32),
+    ]
+
+
+class MuzClassicSoA(ctypes.Structure):
+    _fields_ = [
+        ("board", vp),
+        ("pins", vp),
+        ("current_player", vp),
+        ("reward", vp),
+        ("done", vp),
+        ("die", vp),
         ("stride", ctypes.c_int32),
     ]
 
@@ -117,6 +130,15 @@ SIGNATURES = {
     "muz_detmadn_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
+    "muz_classic_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, ctypes.c_int32, vp]),
+    "muz_classic_set_die": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
+    "muz_classic_dice_probs": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, ctypes.c_int32, vp]),
+    "muz_classic_throw_die": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, ctypes.c_int32, vp]),
+    "muz_classic_legal": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
+    "muz_classic_step": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, vp, ctypes.c_int32, vp]),
+    "muz_classic_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, ctypes.c_int32, vp]),
+    "muz_classic_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
+    "muz_classic_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_tile_waves": (ctypes.c_int32, []),
     "muz_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzNetW), ctypes.c_void_p]),
     "muz_nets_root_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32]),

@@ -50,6 +50,7 @@ typedef struct muz_rules {
   int32_t enable_start_on_1;
   int32_t enable_bonus_turn_on_6;
   int32_t must_traverse_start;
+  int32_t enable_dice_rethrow;  /* classic only (classic_madn.py:66, dice_probabilities 208-228) */
 } muz_rules;
 
 /* Deterministic-MADN batch state, SoA (deterministic_madn.py:24-40).
@@ -63,6 +64,20 @@ typedef struct muz_detmadn_soa {
   int8_t* action_set;     /* [P*6][stride]      remaining copies of moves 1..6    */
   int32_t stride;         /* >= n                                                 */
 } muz_detmadn_soa;
+
+/* Classic-MADN batch state, SoA (classic_madn.py:33-49): the det fields without the action set, plus
+ * the die of the turn (set by muz_classic_set_die / muz_classic_throw_die before legal / step). */
+typedef struct muz_classic_soa {
+  int8_t* board;          /* [56][stride] */
+  int8_t* pins;           /* [P*4][stride] */
+  int8_t* current_player; /* [stride] */
+  int8_t* reward;         /* [stride] */
+  uint8_t* done;          /* [stride] */
+  int8_t* die;            /* [stride]       1..6 (0 after reset) */
+  int32_t stride;
+} muz_classic_soa;
+
+#define MUZ_CLASSIC_ACTIONS 4   /* pin index */
 
 /* ---- library ---------------------------------------------------------------- */
 const char* muz_version(void);                 /* host string */
@@ -94,6 +109,38 @@ int muz_detmadn_nostep(const muz_rules* rules, muz_detmadn_soa state, int8_t* re
 int muz_detmadn_encode_f32(const muz_rules* rules, muz_detmadn_soa state, float* obs, int32_t n, void* stream);
 int muz_detmadn_encode_i8(const muz_rules* rules, muz_detmadn_soa state, int8_t* obs, int32_t n, void* stream);
 
+
+/* ---- classic MADN environment (MADN/classic_madn.py) -------------------------------------- */
+
+/* env_reset (classic_madn.py:51-131); game_agent_stochastic.py:25-44 batch_reset. */
+int muz_classic_reset(const muz_rules* rules /*host*/, muz_classic_soa state, int32_t n, void* stream);
+
+/* set_die (classic_madn.py:244-255): die[b] (1..6) into the state. */
+int muz_classic_set_die(const muz_rules* rules, muz_classic_soa state, const int32_t* die, int32_t n, void* stream);
+
+/* dice_probabilities (208-228) -> probs[b][6] fp32; soft_locked[b] (is_soft_locked 180-206) may be null. */
+int muz_classic_dice_probs(const muz_rules* rules, muz_classic_soa state, float* probs, uint8_t* soft_locked,
+                           int32_t n, void* stream);
+
+/* throw_die (230-242) with the uniform draw as an input: die = jax.random.choice([1..6], p=dice_probabilities)
+ * evaluated as 1 + searchsorted_left(cumsum(p), cumsum(p)[5] * (1 - uniform[b])).  die_out may be null. */
+int muz_classic_throw_die(const muz_rules* rules, muz_classic_soa state, const float* uniform, int32_t* die_out,
+                          int32_t n, void* stream);
+
+/* valid_action (367-461): legal_bits[b] bit pin (4 bits), for the die in the state. */
+int muz_classic_legal(const muz_rules* rules, muz_classic_soa state, uint32_t* legal_bits, int32_t n, void* stream);
+
+/* env_step (257-337) moving pin[b] by the state's die.  reward/done may be null. */
+int muz_classic_step(const muz_rules* rules, muz_classic_soa state, const int32_t* pin, int8_t* reward,
+                     uint8_t* done, int32_t n, void* stream);
+
+/* no_step (353-365): advance the player. */
+int muz_classic_nostep(const muz_rules* rules, muz_classic_soa state, int8_t* reward, uint8_t* done, int32_t n,
+                       void* stream);
+
+/* encode_board (463-497): obs[b][c][w], C = 2P+3 (last channel = die), W = 56. */
+int muz_classic_encode_f32(const muz_rules* rules, muz_classic_soa state, float* obs, int32_t n, void* stream);
+int muz_classic_encode_i8(const muz_rules* rules, muz_classic_soa state, int8_t* obs, int32_t n, void* stream);
 
 /* ---- MuZero networks (MuZero_det_MADN/muzero_deterministic_madn.py) --------------------------
  * Dense layers used by the MFMA kernels take their kernel W[K][N] PACKED for

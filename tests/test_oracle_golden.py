@@ -63,3 +63,57 @@ def test_oracle_detmadn_refill_quirk():
     env2, r, d = dm.env_step(env, (0, 6))
     assert r == 0 and env2.pins[0, 0] == 11
     assert env2.action_set[0].tolist() == [4] * 6 and env2.current_player == 0   # bonus turn on 6
+
+
+# ---- classic MADN (MADN/test.py:7-475) -------------------------------------------------------------
+from oracle import classic_madn as cm  # noqa: E402
+
+CLASSIC_CASES = _load("classic_madn_step_cases.json")
+
+
+def classic_env_from_case(c):
+    """MADN/test.py:461-472: env_reset(2 players) + replace(pins, board, current_player) + set_die(move)."""
+    r = c["rules"]
+    pins = np.array(c["pins"], dtype=np.int8)
+    env = cm.env_reset(num_players=len(pins), distance=10,
+                       enable_circular_board=r["enable_circular_board"],
+                       enable_jump_in_goal_area=r["enable_jump_in_goal_area"],
+                       enable_start_blocking=r["enable_start_blocking"],
+                       enable_friendly_fire=r["enable_friendly_fire"],
+                       enable_start_on_1=r.get("enable_start_on_1", False),
+                       must_traverse_start=r.get("must_traverse_start", False))
+    env = env.replace(pins=pins, board=cm.set_pins_on_board(env.board, pins), current_player=c["player"])
+    return cm.set_die(env, c["move"])
+
+
+@pytest.mark.parametrize("case", CLASSIC_CASES, ids=[c["source"] for c in CLASSIC_CASES])
+def test_oracle_classic_golden(case):
+    env = classic_env_from_case(case)
+    valid = cm.valid_action(env)
+    env2, reward, done = cm.env_step(env, case["pin"])
+    assert valid[case["pin"]] or reward == -1                 # MADN/test.py:474
+    assert np.array_equal(env2.pins, np.array(case["expected_valid"]))
+
+
+def test_oracle_classic_dice():
+    env = cm.env_reset(num_players=4, **cm.SELFPLAY_RULES)
+    # initial free pin on start, 3 at home: not soft-locked (a pin is on the track)
+    assert not cm.is_soft_locked(env)
+    assert np.allclose(cm.dice_probabilities(env), 1 / 6)
+    pins = env.pins.copy()
+    pins[0] = [-1, -1, -1, -1]
+    env = env.replace(pins=pins, board=cm.set_pins_on_board(env.board, pins))
+    assert cm.is_soft_locked(env)                              # nobody out: locked
+    assert np.allclose(cm.dice_probabilities(env), np.array([76, 16, 16, 16, 16, 76]) / 216)
+    pins[0] = [43, -1, -1, -1]                                 # last goal cell of player 0 (40..43)
+    env = env.replace(pins=pins, board=cm.set_pins_on_board(env.board, pins))
+    assert cm.is_soft_locked(env)
+    pins[0] = [42, -1, -1, -1]
+    env = env.replace(pins=pins, board=cm.set_pins_on_board(env.board, pins))
+    assert not cm.is_soft_locked(env)
+    # uniform -> die: u close to 1 gives r close to 0 -> die 1; u = 0 gives r = total -> die 6
+    p = cm.NORMAL_DICE_DISTRIBUTION
+    assert cm.choice_from_uniform(p, 0.999) == 1 and cm.choice_from_uniform(p, 0.0) == 6
+    counts = np.bincount([cm.choice_from_uniform(p, u) for u in np.linspace(0, 1, 6000, endpoint=False)], minlength=7)
+    assert np.all(np.abs(counts[1:] - 1000) <= 2)
+    assert cm.encode_board(env).shape == (11, 56)
