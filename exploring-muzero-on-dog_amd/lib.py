@@ -113,6 +113,17 @@ class MuzTraj(ctypes.Structure):
                 ("team", vp), ("discount", vp), ("idx", vp), ("max_steps", ctypes.c_int32)]
 
 
+class MuzRing(ctypes.Structure):
+    _fields_ = [("obs", vp), ("act", vp), ("rew", vp), ("val", vp), ("pol", vp), ("mask", vp), ("player", vp),
+                ("team", vp), ("discount", vp), ("ep_len", vp), ("capacity", ctypes.c_int32),
+                ("max_steps", ctypes.c_int32), ("obs_channels", ctypes.c_int32), ("num_actions", ctypes.c_int32)]
+
+
+class MuzSample(ctypes.Structure):
+    _fields_ = [("observations", vp), ("actions", vp), ("rewards", vp), ("policies", vp), ("values", vp),
+                ("masks", vp), ("target_values", vp), ("discount_targets", vp)]
+
+
 class MuzSpStats(ctypes.Structure):
     _fields_ = [("turns", ctypes.c_int32), ("searches", ctypes.c_int64), ("search_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double)]
@@ -140,6 +151,9 @@ SIGNATURES = {
     "muz_classic_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_tile_waves": (ctypes.c_int32, []),
+    "muz_ring_save": (ctypes.c_int, [MuzRing, MuzTraj, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]),
+    "muz_ring_sample": (ctypes.c_int, [MuzRing, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                       vp, MuzSample, vp]),
     "muz_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzNetW), ctypes.c_void_p]),
     "muz_nets_root_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "muz_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp,

@@ -1,0 +1,144 @@
+"""Device-resident replay ring (host mirror of MuZero_det_MADN/vec_replay_buffer.py:9-264).
+
+``VectorizedReplayBuffer`` keeps the reference's constructor, attributes (``position``, ``size``,
+``bootstrap_value_target``) and methods:
+
+* ``save_games_from_buffers(buffers)`` takes the self-play buffer dict (device tensors, as returned by
+  ``game_agent.SelfPlayEngine.play``) and copies every game with ``idx > 0`` into the next ring slots
+  ON DEVICE (``muz_ring_save``): no host round trip of the trajectories;
+* ``sample_batch()`` draws the episode / start indices exactly like the reference (numpy legacy
+  ``randint`` calls in the same order, from ``rng`` -- the ``np.random`` module by default, as in the
+  reference, or a seeded ``np.random.RandomState``), then gathers the batch and computes the value
+  targets on device (``muz_ring_sample``).  The result is a dict of device tensors with the reference's
+  keys and shapes.
+
+Storage: observations int8 (the encoder's values are 0..4), everything else as in the reference, all
+in HBM: capacity 20000 x T 550 x C 34 needs 21 GB instead of the reference's 84 GB host fp32 array.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import lib as _L
+
+GAMMA = 0.997
+TERMINAL_RATIO = 0.25
+CELLS = 56
+
+
+class VectorizedReplayBuffer:
+    def __init__(self, capacity: int, batch_size: int, unroll_steps: int, td_steps: int, obs_shape=(14, 56),
+                 action_dim=24, max_episode_length=500, bootstrap_value_target=True, device="cuda", rng=None):
+        C, W = obs_shape
+        if W != CELLS:
+            raise ValueError("observations must be [C, 56]")
+        if td_steps > max_episode_length:
+            raise ValueError("td_steps > max_episode_length")
+        self.capacity, self.batch_size = int(capacity), int(batch_size)
+        self.unroll_steps, self.td_steps = int(unroll_steps), int(td_steps)
+        self.obs_shape, self.action_dim = (int(C), CELLS), int(action_dim)
+        self.max_episode_length = int(max_episode_length)
+        self.bootstrap_value_target = bool(bootstrap_value_target)
+        self.position = 0
+        self.size = 0
+        self.rng = np.random if rng is None else rng
+        self.device = torch.device(device)
+        cap, T = self.capacity, self.max_episode_length
+        z = dict(device=self.device)
+        self.observations = torch.zeros((cap, T, C, CELLS), dtype=torch.int8, **z)
+        self.actions = torch.zeros((cap, T), dtype=torch.int32, **z)
+        self.rewards = torch.zeros((cap, T), dtype=torch.int32, **z)
+        self.root_values = torch.zeros((cap, T), dtype=torch.float32, **z)
+        self.child_visits = torch.zeros((cap, T, self.action_dim), dtype=torch.float32, **z)
+        self.masks = torch.zeros((cap, T), dtype=torch.float32, **z)
+        self.players = torch.zeros((cap, T), dtype=torch.int32, **z)
+        self.teams = torch.zeros((cap, T), dtype=torch.int32, **z)
+        self.discounts = torch.zeros((cap, T), dtype=torch.int32, **z)
+        self.episode_lengths = torch.zeros((cap,), dtype=torch.int32, **z)
+        # host copy of the lengths: the index draws need them (the reference reads its own array)
+        self._ep_len_host = np.zeros(cap, np.int32)
+        # 0.997 ** n as NumPy evaluates GAMMA ** int_array (float64 pow), n = 0..T
+        self.gamma_pow = torch.from_numpy(np.power(GAMMA, np.arange(T + 1).astype(np.float64))).to(self.device)
+        self._count = torch.zeros((1,), dtype=torch.int32, **z)
+
+    def ring(self) -> _L.MuzRing:
+        r = _L.MuzRing()
+        r.obs, r.act, r.rew = self.observations.data_ptr(), self.actions.data_ptr(), self.rewards.data_ptr()
+        r.val, r.pol, r.mask = self.root_values.data_ptr(), self.child_visits.data_ptr(), self.masks.data_ptr()
+        r.player, r.team, r.discount = self.players.data_ptr(), self.teams.data_ptr(), self.discounts.data_ptr()
+        r.ep_len = self.episode_lengths.data_ptr()
+        r.capacity, r.max_steps = self.capacity, self.max_episode_length
+        r.obs_channels, r.num_actions = self.obs_shape[0], self.action_dim
+        return r
+
+    @staticmethod
+    def _traj(b: dict) -> _L.MuzTraj:
+        t = _L.MuzTraj()
+        for k in ("obs", "act", "rew", "val", "pol", "mask", "player", "team", "discount", "idx"):
+            setattr(t, k, b[k].data_ptr())
+        t.max_steps = b["act"].shape[1]
+        return t
+
+    def save_games_from_buffers(self, all_buffers: dict):
+        """vec_replay_buffer.py:36-61 on device."""
+        b = all_buffers
+        n = b["idx"].shape[0]
+        if b["obs"].dtype != torch.int8 or tuple(b["obs"].shape[2:]) != self.obs_shape:
+            raise ValueError("expected int8 observations of shape [n, T, C, 56]")
+        slots = torch.empty((n,), dtype=torch.int32, device=self.device)
+        _L.check(_L.load().muz_ring_save(self.ring(), self._traj(b), n, self.position, _L.ptr(slots),
+                                         _L.ptr(self._count), _L.stream_ptr()), "muz_ring_save")
+        count = int(self._count.item())
+        sl = slots.cpu().numpy()
+        lens = b["idx"].cpu().numpy()
+        keep = sl >= 0
+        self._ep_len_host[sl[keep]] = lens[keep]
+        self.position = (self.position + count) % self.capacity
+        self.size = min(self.size + count, self.capacity)
+
+    def draw_indices(self):
+        """vec_replay_buffer.py:72-99: the reference's numpy draws, in its order."""
+        n_terminal = int(self.batch_size * TERMINAL_RATIO)
+        n_normal = self.batch_size - n_terminal
+        r = self.rng
+        ep_n = r.randint(0, self.size, size=n_normal)
+        len_n = self._ep_len_host[ep_n]
+        t_n = r.randint(0, (len_n - 1) + 1)
+        ep_t = r.randint(0, self.size, size=n_terminal)
+        len_t = self._ep_len_host[ep_t]
+        max_k = np.minimum(self.unroll_steps - 1, len_t - 1)
+        term_k = np.array([r.randint(0, int(m) + 1) for m in max_k])
+        t_t = np.maximum(len_t - 1 - term_k, 0)
+        return np.concatenate([ep_n, ep_t]).astype(np.int32), np.concatenate([t_n, t_t]).astype(np.int32)
+
+    def sample_at(self, ep_indices, t_starts) -> dict:
+        """The deterministic part of sample_batch (vec_replay_buffer.py:101-264), on device."""
+        B = len(ep_indices)
+        K = self.unroll_steps + 1
+        C, A = self.obs_shape[0], self.action_dim
+        z = dict(device=self.device)
+        out = {
+            "observations": torch.empty((B, C, CELLS), dtype=torch.float32, **z),
+            "actions": torch.empty((B, K - 1), dtype=torch.int32, **z),
+            "rewards": torch.empty((B, K - 1), dtype=torch.int32, **z),
+            "policies": torch.empty((B, K, A), dtype=torch.float32, **z),
+            "values": torch.empty((B, K), dtype=torch.float32, **z),
+            "masks": torch.empty((B, K), dtype=torch.float32, **z),
+            "target_values": torch.empty((B, K), dtype=torch.float32, **z),
+            "discount_targets": torch.empty((B, K - 1), dtype=torch.int32, **z),
+        }
+        s = _L.MuzSample()
+        for k in out:
+            setattr(s, k, out[k].data_ptr())
+        ep = torch.as_tensor(np.asarray(ep_indices, np.int32)).to(self.device)
+        ts = torch.as_tensor(np.asarray(t_starts, np.int32)).to(self.device)
+        _L.check(_L.load().muz_ring_sample(self.ring(), _L.ptr(ep), _L.ptr(ts), B, self.unroll_steps, self.td_steps,
+                                           int(self.bootstrap_value_target), _L.ptr(self.gamma_pow), s,
+                                           _L.stream_ptr()), "muz_ring_sample")
+        return out
+
+    def sample_batch(self) -> dict:
+        """vec_replay_buffer.py:63-264."""
+        ep, t = self.draw_indices()
+        return self.sample_at(ep, t)

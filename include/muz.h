@@ -298,6 +298,55 @@ int muz_detmadn_selfplay(const muz_rules* rules /*host*/, const muz_net_w* w /*h
                          const muz_search_cfg* cfg /*host*/, muz_detmadn_soa state, muz_traj traj, int32_t n,
                          void* workspace, int64_t workspace_bytes, muz_sp_stats* stats /*host*/, void* stream);
 
+/* ---- device replay ring (MuZero_det_MADN/vec_replay_buffer.py) ------------------------------
+ * The reference's VectorizedReplayBuffer keeps [capacity][T] host NumPy arrays (obs fp32, 84 GB at
+ * capacity 20000, T 550, C 34).  Here the ring lives in HBM, obs int8 (values 0..4, exact):
+ * 21 GB at the same size.  save copies finished games device-to-device from the self-play
+ * trajectory buffers; sample gathers a training batch and computes the value targets on device. */
+typedef struct muz_ring {
+  int8_t* obs;        /* [cap][T][C][56] */
+  int32_t* act;       /* [cap][T] */
+  int32_t* rew;       /* [cap][T] reward class */
+  float* val;         /* [cap][T] root value */
+  float* pol;         /* [cap][T][A] child visits (action weights) */
+  float* mask;        /* [cap][T] */
+  int32_t* player;    /* [cap][T] */
+  int32_t* team;      /* [cap][T] */
+  int32_t* discount;  /* [cap][T] discount class */
+  int32_t* ep_len;    /* [cap] */
+  int32_t capacity;
+  int32_t max_steps;  /* T (= the trajectory buffers' max_steps) */
+  int32_t obs_channels;
+  int32_t num_actions;
+} muz_ring;
+
+/* A training batch, sample_batch's return dict (vec_replay_buffer.py:256-264), K = unroll_steps + 1. */
+typedef struct muz_sample {
+  float* observations;        /* [B][C][56] */
+  int32_t* actions;           /* [B][K-1] */
+  int32_t* rewards;           /* [B][K-1] */
+  float* policies;            /* [B][K][A] */
+  float* values;              /* [B][K] */
+  float* masks;               /* [B][K] */
+  float* target_values;       /* [B][K] */
+  int32_t* discount_targets;  /* [B][K-1] */
+} muz_sample;
+
+/* save_games_from_buffers (vec_replay_buffer.py:36-61): game i with traj.idx[i] > 0 goes to ring slot
+ * (position + r_i) % capacity, r_i = number of such games before i (later games win a slot that wraps
+ * twice, as in the sequential loop).  slot_out[i] (device int32[n], required) = its slot or -1;
+ * count_out (device int32[1]) = number of games with idx > 0 (the host advances position / size). */
+int muz_ring_save(muz_ring ring, muz_traj traj, int32_t n, int32_t position, int32_t* slot_out, int32_t* count_out,
+                  void* stream);
+
+/* sample_batch (vec_replay_buffer.py:63-264) for given episode / start indices (the reference draws them
+ * with np.random; the host mirror draws them the same way).  gamma_pow (device double[max_steps + 1]) =
+ * 0.997 ** n as NumPy computes it; targets are evaluated in double and rounded to float like the
+ * reference (NumPy float64, then jnp.array). */
+int muz_ring_sample(muz_ring ring, const int32_t* ep_idx, const int32_t* t_start, int32_t batch, int32_t unroll_steps,
+                    int32_t td_steps, int32_t bootstrap_value_target, const double* gamma_pow, muz_sample out,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,87 @@
+"""Device replay ring (muz_ring_save / muz_ring_sample) vs the replay oracle (GPU).
+
+Both sides get the same trajectories and the same seeded numpy draws; ring contents and every sampled
+tensor must be identical (integers bit-exact, floats bit-exact: the targets are double-then-float on
+both sides).  Covers zero-length games, ring wrap-around within one call and across calls, padding of
+windows past the episode end, bootstrap on / off, and real self-play buffers."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.replay import VectorizedReplayBuffer as OracleRB
+from tests.test_replay_oracle import make_buffers
+
+pytestmark = pytest.mark.gpu
+
+
+def _R():
+    from exploring_muzero_on_dog_amd import replay as R
+    return R
+
+
+def to_dev(b):
+    return {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in b.items()}
+
+
+def assert_ring_equal(dev, ora):
+    assert (dev.position, dev.size) == (ora.position, ora.size)
+    lens = dev.episode_lengths.cpu().numpy()
+    assert np.array_equal(lens, ora.episode_lengths)
+    obs = dev.observations.cpu().numpy()
+    fields = [("actions", "actions"), ("rewards", "rewards"), ("root_values", "root_values"),
+              ("child_visits", "child_visits"), ("masks", "masks"), ("players", "players"), ("teams", "teams"),
+              ("discounts", "discounts")]
+    host = {a: getattr(dev, a).cpu().numpy() for a, _ in fields}
+    for s in range(ora.size):
+        L = lens[s]
+        assert np.array_equal(obs[s, :L].astype(np.float32), ora.observations[s, :L]), s
+        for a, b in fields:
+            assert np.array_equal(host[a][s, :L], getattr(ora, b)[s, :L]), (a, s)
+
+
+def assert_sample_equal(d, o):
+    for k, v in o.items():
+        got = d[k].cpu().numpy()
+        assert got.dtype == v.dtype, k
+        assert np.array_equal(got, v), (k, np.argwhere(got != v)[:5])
+
+
+@pytest.mark.parametrize("boot", [False, True])
+def test_ring_save_and_sample_synthetic(cuda, boot):
+    R = _R()
+    T, C, cap = 64, 18, 23
+    dev = R.VectorizedReplayBuffer(cap, 96, 10, 7, obs_shape=(C, 56), max_episode_length=T,
+                                   bootstrap_value_target=boot, rng=np.random.RandomState(5))
+    ora = OracleRB(cap, 96, 10, 7, obs_shape=(C, 56), max_episode_length=T, bootstrap_value_target=boot,
+                   rng=np.random.RandomState(5))
+    rng = np.random.default_rng(11)
+    for call in range(4):
+        lengths = rng.integers(0, T + 1, 17 if call else 30)   # call 0 wraps inside one call (30 > 23)
+        lengths[::5] = 0
+        b = make_buffers(lengths, T, C=C, seed=call)
+        b["team"][1::2] = (b["player"][1::2] % 2)                # some team-mode games
+        dev.save_games_from_buffers(to_dev(b))
+        ora.save_games_from_buffers(b)
+        assert_ring_equal(dev, ora)
+        for _ in range(3):
+            assert_sample_equal(dev.sample_batch(), ora.sample_batch())
+
+
+def test_ring_with_selfplay_buffers(cuda):
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import game_agent as GA
+    from exploring_muzero_on_dog_amd import nets as N
+    R = _R()
+    C = E.num_channels(4)
+    net = N.DeviceNet(N.init_muzero_params(0, C), C)
+    eng = GA.SelfPlayEngine(net, 40, num_players=4, max_steps=80, num_simulations=8, max_depth=6)
+    bufs = eng.play(seed=3)
+    host = {k: v.cpu().numpy() for k, v in bufs.items()}
+    dev = R.VectorizedReplayBuffer(64, 128, 10, 50, obs_shape=(C, 56), max_episode_length=80,
+                                   rng=np.random.RandomState(1))
+    ora = OracleRB(64, 128, 10, 50, obs_shape=(C, 56), max_episode_length=80, rng=np.random.RandomState(1))
+    for _ in range(2):
+        dev.save_games_from_buffers(bufs)
+        ora.save_games_from_buffers(host)
+    assert_ring_equal(dev, ora)
+    assert_sample_equal(dev.sample_batch(), ora.sample_batch())
