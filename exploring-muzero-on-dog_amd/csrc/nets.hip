@@ -99,8 +99,10 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
   for (int i = tid; i < 3584; i += 256) dst[i] = c2in[i];   // flatten (w, ch) -> w*64 + ch
 }
 
-// Rest of RepresentationNetwork2 + PredictionNetwork4 on 16-game tiles.
-__global__ __launch_bounds__(kThreads) void k_root_dense(muz_net_w Wt, const float* __restrict__ obs,
+// Rest of RepresentationNetwork2 + PredictionNetwork4 on 16-game tiles.  NW = muz_net_w (det) or
+// muz_classic_net_w (classic): both carry obs_channels, num_actions, repr and pred.
+template <class NW>
+__global__ __launch_bounds__(kThreads) void k_root_dense(NW Wt, const float* __restrict__ obs,
                                                     const float* __restrict__ convout, int n,
                                                     const int* __restrict__ n_dev, float* prior_logits, float* value,
                                                     float* embedding) {
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(kThreads) void k_root_dense(muz_net_w Wt, const flo
   if ((int)blockIdx.x * kRows >= n) return;
   __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
   const Arena a = Arena::carve(smem);
-  const AS4 muz_net_w* W = kernarg0<muz_net_w>();   // == Wt, read through the kernarg segment
+  const AS4 NW* W = kernarg0<NW>();   // == Wt, read through the kernarg segment
   const AS4 muz_repr_w& R = W->repr;
   const int C = Wt.obs_channels, A = Wt.num_actions;
   const int g0 = blockIdx.x * kRows;
@@ -211,13 +213,24 @@ int check_net(const muz_net_w* w) {
   return MUZ_OK;
 }
 
-int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv, float* logits,
-                          float* value, float* emb, hipStream_t s) {
+template <class NW>
+static int launch_root_impl(const NW& w, const float* obs, int n, const int* n_dev, float* conv, float* logits,
+                            float* value, float* emb, hipStream_t s) {
   k_repr_conv<<<n, 256, 0, s>>>(w.repr, obs, w.obs_channels, n, n_dev, conv);
   int rc = muz_last_launch_error();
   if (rc) return rc;
-  k_root_dense<<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, obs, conv, n, n_dev, logits, value, emb);
+  k_root_dense<NW><<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, obs, conv, n, n_dev, logits, value, emb);
   return muz_last_launch_error();
+}
+
+int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv, float* logits,
+                          float* value, float* emb, hipStream_t s) {
+  return launch_root_impl(w, obs, n, n_dev, conv, logits, value, emb, s);
+}
+
+int launch_root_inference(const muz_classic_net_w& w, const float* obs, int n, const int* n_dev, float* conv,
+                          float* logits, float* value, float* emb, hipStream_t s) {
+  return launch_root_impl(w, obs, n, n_dev, conv, logits, value, emb, s);
 }
 
 }  // namespace muz

@@ -479,27 +479,39 @@ __device__ __forceinline__ void resblock16(const AS4 muz_resblock& R, float* X, 
 }
 
 // 64-input heads: weights of this lane's inputs k = sub + i*kRowLanes, loaded early.
-constexpr int kHeadPer = 64 / kRowLanes;
-struct HeadW {
-  float w[3][kHeadPer];
+// K-input heads (K = 32 or 64) with up to 3 outputs: weights of this lane's inputs
+// k = sub + i*kRowLanes, loaded early.
+template <int K>
+struct HeadK {
+  static constexpr int kPer = (K + kRowLanes - 1) / kRowLanes;
+  float w[3][kPer];
   float b[3];
 };
-__device__ __forceinline__ HeadW head_load(const AS4 muz_dense& H, int ncol) {
-  HeadW h;
+using HeadW = HeadK<64>;
+template <int K = 64>
+__device__ __forceinline__ HeadK<K> head_load(const AS4 muz_dense& H, int ncol) {
+  HeadK<K> h;
   const AS1 float* w = gp(H.w);
   const AS1 float* b = gp(H.b);
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     h.b[j] = j < ncol ? b[j] : 0.f;
 #pragma unroll
-    for (int i = 0; i < kHeadPer; ++i) h.w[j][i] = j < ncol ? w[(tsub() + i * kRowLanes) * ncol + j] : 0.f;
+    for (int i = 0; i < HeadK<K>::kPer; ++i) {
+      const int k = tsub() + i * kRowLanes;
+      h.w[j][i] = (j < ncol && k < K) ? w[k * ncol + j] : 0.f;
+    }
   }
   return h;
 }
-__device__ __forceinline__ float head_dot(const float* in, int ld, const HeadW& h, int j) {
+template <int K>
+__device__ __forceinline__ float head_dot(const float* in, int ld, const HeadK<K>& h, int j) {
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < kHeadPer; ++i) s += in[trow() * ld + tsub() + i * kRowLanes] * h.w[j][i];
+  for (int i = 0; i < HeadK<K>::kPer; ++i) {
+    const int k = tsub() + i * kRowLanes;
+    if (k < K) s += in[trow() * ld + k] * h.w[j][i];
+  }
   return row_sum(s) + h.b[j];
 }
 

@@ -10,6 +10,7 @@
 // L2/MALL resident), written lazily when a node is created.
 #include "launch.hpp"
 #include "nn.hpp"
+#include "rng.hpp"
 
 namespace muz {
 
@@ -35,7 +36,6 @@ constexpr int kMaxNodes = kMaxSims + 1;
 constexpr int kMaxDepth = 64;
 constexpr int kAPad = 32;                  // children arrays padded to 32 actions
 constexpr float kFMin = -3.4028234663852886e38f;   // jnp.finfo(float32).min
-constexpr float kTiny = 1.1754943508222875e-38f;   // jnp.finfo(float32).tiny
 
 struct TreeWs {
   int32_t* c_index;
@@ -140,7 +140,7 @@ __device__ __forceinline__ float completed_q(const Kid& k, float raw, const Sear
   const float pm = row_max(k.ok ? k.prior : -INFINITY);
   const float e = k.ok ? expf(k.prior - pm) : 0.f;
   const float es = row_sum(e);
-  const float pp = fmaxf(kTiny, e / es);
+  const float pp = fmaxf(kTinyF, e / es);
   const bool vis = k.ok && k.visits > 0;
   const int sv = row_isum(k.ok ? k.visits : 0);
   const int mv = row_imax(k.ok ? k.visits : 0);
@@ -155,21 +155,6 @@ __device__ __forceinline__ float completed_q(const Kid& k, float raw, const Sear
   sumv = sv;
   pmax = pm;
   return scale * ((cq - lo) / den);
-}
-
-__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-// jax.random.gumbel semantics on our own counter RNG: -log(-log(U[tiny, 1)))
-__device__ __forceinline__ float gumbel_noise(unsigned long long seed, int gid, int turn, int a) {
-  const unsigned long long h =
-      mix64(seed ^ mix64(((unsigned long long)(unsigned)gid << 32) | (unsigned)turn) ^ (unsigned long long)(a + 1) * 0xD6E8FEB86659FD93ull);
-  float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-  u = fmaxf(u, kTiny);
-  return -logf(-logf(u));
 }
 
 __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(

@@ -101,6 +101,29 @@ class MuzNetW(ctypes.Structure):
 
 
 
+class MuzSdynW(ctypes.Structure):
+    _fields_ = [("act_embed", MuzDense), ("act_input_ln", MuzLn), ("act_film", MuzDense), ("act_dense1", MuzDense),
+                ("act_ln1", MuzLn), ("act_dense2", MuzDense), ("act_ln2", MuzLn), ("act_rb", MuzResblock * 2),
+                ("act_proj", MuzDense), ("rc", MuzDense), ("reward_onehot", vp), ("reward_head", MuzDense),
+                ("discount_dense", MuzDense), ("discount_ln", MuzLn), ("discount_head", MuzDense),
+                ("chance_embed", MuzDense), ("chance_input_ln", MuzLn), ("chance_film", MuzDense),
+                ("chance_dense1", MuzDense), ("chance_ln1", MuzLn), ("chance_dense2", MuzDense), ("chance_ln2", MuzLn),
+                ("chance_rb", MuzResblock * 2), ("chance_proj", MuzDense), ("act_film_tab", vp),
+                ("chance_film_tab", vp)]
+
+
+class MuzClassicNetW(ctypes.Structure):
+    _fields_ = [("obs_channels", ctypes.c_int32), ("num_actions", ctypes.c_int32), ("repr", MuzReprW),
+                ("sdyn", MuzSdynW), ("pred", MuzPredW)]
+
+
+class MuzStochCfg(ctypes.Structure):
+    _fields_ = [("num_simulations", ctypes.c_int32), ("max_depth", ctypes.c_int32),
+                ("dirichlet_fraction", ctypes.c_float), ("dirichlet_alpha", ctypes.c_float),
+                ("pb_c_init", ctypes.c_float), ("pb_c_base", ctypes.c_float), ("temperature", ctypes.c_float),
+                ("turn", ctypes.c_int32), ("seed", ctypes.c_uint64)]
+
+
 class MuzSearchCfg(ctypes.Structure):
     _fields_ = [("num_simulations", ctypes.c_int32), ("max_depth", ctypes.c_int32),
                 ("max_num_considered", ctypes.c_int32), ("value_scale", ctypes.c_float),
@@ -154,6 +177,16 @@ SIGNATURES = {
     "muz_ring_save": (ctypes.c_int, [MuzRing, MuzTraj, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]),
     "muz_ring_sample": (ctypes.c_int, [MuzRing, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                        vp, MuzSample, vp]),
+    "muz_classic_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzClassicNetW), vp]),
+    "muz_classic_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzClassicNetW), vp, ctypes.c_int32, vp, ctypes.c_int64,
+                                             vp, vp, vp, vp]),
+    "muz_classic_nets_decision": (ctypes.c_int, [ctypes.POINTER(MuzClassicNetW), vp, vp, ctypes.c_int32, vp, vp, vp,
+                                                 vp, vp, vp]),
+    "muz_classic_nets_chance": (ctypes.c_int, [ctypes.POINTER(MuzClassicNetW), vp, vp, ctypes.c_int32, vp, vp, vp,
+                                               vp]),
+    "muz_stochastic_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    "muz_stochastic_search": (ctypes.c_int, [ctypes.POINTER(MuzClassicNetW), ctypes.POINTER(MuzStochCfg), vp, vp, vp,
+                                             vp, vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp, vp]),
     "muz_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzNetW), ctypes.c_void_p]),
     "muz_nets_root_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "muz_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp,

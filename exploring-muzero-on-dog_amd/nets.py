@@ -104,73 +104,16 @@ def pack_dense(W: np.ndarray, nw: int, nt: int) -> np.ndarray:
     return np.ascontiguousarray(arr).reshape(-1)
 
 
-class DeviceNet:
-    """Packed device copy of a parameter dict + the ``muz_net_w`` table the kernels read."""
+class _Packer:
+    """Builds one device buffer of packed parameters and fills a ctypes weight table from a nested spec
+    (leaf = offset in floats, (w, b) pair = muz_dense / muz_ln, list = array field, dict = sub-struct)."""
 
-    def __init__(self, params: dict, obs_channels: int, num_actions: int = 24, device="cuda"):
+    def __init__(self, params: dict, obs_channels: int, num_actions: int):
         self.C, self.A = int(obs_channels), int(num_actions)
-        NW = _L.load().muz_tile_waves()   # column groups of the packed 16-row layers (csrc/nn.hpp kWaves)
-        self.waves = NW
+        self.waves = _L.load().muz_tile_waves()   # column groups of the packed 16-row layers (csrc/nn.hpp kWaves)
         self._chunks = []
         self._off = 0
-        P = {k: np.asarray(v, np.float32) for k, v in params.items()}
-        self.params = P
-        put = self._put
-        w = MuzNetW()
-        w.obs_channels, w.num_actions = self.C, self.A
-
-        def dense(name, nw=None, nt=None):
-            nw = NW if nw is None else nw
-            k = P[f"{name}/kernel"]
-            nt = nt if nt is not None else nt_for(k.shape[1], nw)
-            return (put(pack_dense(k, nw, nt)), put(P[f"{name}/bias"]))
-
-        def ln(name):
-            return (put(P[f"{name}/scale"]), put(P[f"{name}/bias"]))
-
-        def rb(pre):
-            return dict(d0=dense(f"{pre}/Dense_0"), ln0=ln(f"{pre}/LayerNorm_0"), d1=dense(f"{pre}/Dense_1"),
-                        ln1=ln(f"{pre}/LayerNorm_1"))
-
-        r, d, p = "representation", "dynamics", "prediction"
-        spec = {"repr": dict(
-            conv0=(put(P[f"{r}/Conv_0/kernel"]), put(P[f"{r}/Conv_0/bias"])), ln0=ln(f"{r}/LayerNorm_0"),
-            conv1=(put(pack_dense(P[f"{r}/Conv_1/kernel"].reshape(96, 64), 1, 4)), put(P[f"{r}/Conv_1/bias"])),
-            ln1=ln(f"{r}/LayerNorm_1"),
-            conv2=(put(pack_dense(P[f"{r}/Conv_2/kernel"].reshape(320, 64), 1, 4)), put(P[f"{r}/Conv_2/bias"])),
-            ln2=ln(f"{r}/LayerNorm_2"), d0=dense(f"{r}/Dense_0"), ln3=ln(f"{r}/LayerNorm_3"),
-            d1=dense(f"{r}/Dense_1"), ln4=ln(f"{r}/LayerNorm_4"), d2=dense(f"{r}/Dense_2"),
-            ln5=ln(f"{r}/LayerNorm_5"), d3=dense(f"{r}/Dense_3"), ln6=ln(f"{r}/LayerNorm_6"),
-            rb=[rb(f"{r}/ResBlock_{i}") for i in range(6)], d4=dense(f"{r}/Dense_4"))}
-        A = self.A
-        k6, k7 = P[f"{d}/Dense_6/kernel"], P[f"{d}/Dense_7/kernel"]
-        spec["dyn"] = dict(
-            d0=(put(P[f"{d}/Dense_0/kernel"]), put(P[f"{d}/Dense_0/bias"])), ln0=ln(f"{d}/LayerNorm_0"),
-            d12=(put(pack_dense(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1), NW, nt_for(512, NW))),
-                 put(np.concatenate([P[f"{d}/Dense_1/bias"], P[f"{d}/Dense_2/bias"]]))),
-            d3=dense(f"{d}/Dense_3"), ln1=ln(f"{d}/LayerNorm_1"), d4=dense(f"{d}/Dense_4"),
-            ln2=ln(f"{d}/LayerNorm_2"), rb=[rb(f"{d}/ResBlock_{i}") for i in range(2)], d5=dense(f"{d}/Dense_5"),
-            d67=(put(pack_dense(np.concatenate([k6[:LATENT], k7[:LATENT]], 1), NW, nt_for(128, NW))),
-                 put(np.concatenate([P[f"{d}/Dense_6/bias"], P[f"{d}/Dense_7/bias"]]))),
-            d67_onehot=put(np.concatenate([k6[LATENT:LATENT + A], k7[LATENT:LATENT + A]], 1)),
-            reward_head=(put(P[f"{d}/reward_head/kernel"]), put(P[f"{d}/reward_head/bias"])),
-            discount_head=(put(P[f"{d}/discount_head/kernel"]), put(P[f"{d}/discount_head/bias"])),
-            film=put(np.zeros((A + 1) * 2 * LATENT, np.float32)))
-        spec["pred"] = dict(
-            ln0=ln(f"{p}/LayerNorm_0"), rb=[rb(f"{p}/ResBlock_{i}") for i in range(2)],
-            d03=(put(pack_dense(np.concatenate([P[f"{p}/Dense_0/kernel"], P[f"{p}/Dense_3/kernel"]], 1), NW, nt_for(384, NW))),
-                 put(np.concatenate([P[f"{p}/Dense_0/bias"], P[f"{p}/Dense_3/bias"]]))),
-            ln1=ln(f"{p}/LayerNorm_1"), d1=dense(f"{p}/Dense_1"), ln2=ln(f"{p}/LayerNorm_2"),
-            d2=dense(f"{p}/Dense_2"), ln3=ln(f"{p}/LayerNorm_3"), d4=dense(f"{p}/Dense_4"),
-            d5=(put(P[f"{p}/Dense_5/kernel"]), put(P[f"{p}/Dense_5/bias"])))
-        host = np.concatenate(self._chunks) if self._chunks else np.zeros(4, np.float32)
-        self.buffer = torch.from_numpy(host).to(device)
-        base = self.buffer.data_ptr()
-        self._fill(w, spec, base)
-        self.w = w
-        lib = _L.load()
-        with torch.cuda.device(self.buffer.device):
-            _L.check(lib.muz_net_prepare(ctypes.byref(w), _L.stream_ptr()), "muz_net_prepare")
+        self.params = {k: np.asarray(v, np.float32) for k, v in params.items()}
 
     def _put(self, arr) -> int:
         a = np.ascontiguousarray(np.asarray(arr, np.float32).reshape(-1))
@@ -182,24 +125,95 @@ class DeviceNet:
         self._off += a.size
         return off
 
+    def _dense_k(self, k, b):
+        return (self._put(pack_dense(k, self.waves, nt_for(k.shape[1], self.waves))), self._put(b))
+
+    def _dense(self, name):
+        return self._dense_k(self.params[f"{name}/kernel"], self.params[f"{name}/bias"])
+
+    def _plain(self, name):
+        return (self._put(self.params[f"{name}/kernel"]), self._put(self.params[f"{name}/bias"]))
+
+    def _ln(self, name):
+        return (self._put(self.params[f"{name}/scale"]), self._put(self.params[f"{name}/bias"]))
+
+    def _rb(self, pre):
+        return dict(d0=self._dense(f"{pre}/Dense_0"), ln0=self._ln(f"{pre}/LayerNorm_0"), d1=self._dense(f"{pre}/Dense_1"),
+                    ln1=self._ln(f"{pre}/LayerNorm_1"))
+
+    def _repr_spec(self):
+        P, put, r = self.params, self._put, "representation"
+        return dict(
+            conv0=(put(P[f"{r}/Conv_0/kernel"]), put(P[f"{r}/Conv_0/bias"])), ln0=self._ln(f"{r}/LayerNorm_0"),
+            conv1=(put(pack_dense(P[f"{r}/Conv_1/kernel"].reshape(96, 64), 1, 4)), put(P[f"{r}/Conv_1/bias"])),
+            ln1=self._ln(f"{r}/LayerNorm_1"),
+            conv2=(put(pack_dense(P[f"{r}/Conv_2/kernel"].reshape(320, 64), 1, 4)), put(P[f"{r}/Conv_2/bias"])),
+            ln2=self._ln(f"{r}/LayerNorm_2"), d0=self._dense(f"{r}/Dense_0"), ln3=self._ln(f"{r}/LayerNorm_3"),
+            d1=self._dense(f"{r}/Dense_1"), ln4=self._ln(f"{r}/LayerNorm_4"), d2=self._dense(f"{r}/Dense_2"),
+            ln5=self._ln(f"{r}/LayerNorm_5"), d3=self._dense(f"{r}/Dense_3"), ln6=self._ln(f"{r}/LayerNorm_6"),
+            rb=[self._rb(f"{r}/ResBlock_{i}") for i in range(6)], d4=self._dense(f"{r}/Dense_4"))
+
+    def _pred_spec(self):
+        P, p = self.params, "prediction"
+        return dict(
+            ln0=self._ln(f"{p}/LayerNorm_0"), rb=[self._rb(f"{p}/ResBlock_{i}") for i in range(2)],
+            d03=self._dense_k(np.concatenate([P[f"{p}/Dense_0/kernel"], P[f"{p}/Dense_3/kernel"]], 1),
+                              np.concatenate([P[f"{p}/Dense_0/bias"], P[f"{p}/Dense_3/bias"]])),
+            ln1=self._ln(f"{p}/LayerNorm_1"), d1=self._dense(f"{p}/Dense_1"), ln2=self._ln(f"{p}/LayerNorm_2"),
+            d2=self._dense(f"{p}/Dense_2"), ln3=self._ln(f"{p}/LayerNorm_3"), d4=self._dense(f"{p}/Dense_4"),
+            d5=self._plain(f"{p}/Dense_5"))
+
+    def _upload(self, w, spec, device):
+        host = np.concatenate(self._chunks) if self._chunks else np.zeros(4, np.float32)
+        self.buffer = torch.from_numpy(host).to(device)
+        self._fill(w, spec, self.buffer.data_ptr())
+        self.w = w
+
     @staticmethod
     def _fill(struct, spec, base):
-        def addr(off):
-            return base + 4 * off
         for name, val in spec.items():
             field = getattr(struct, name)
             if isinstance(val, int):
-                setattr(struct, name, addr(val))
+                setattr(struct, name, base + 4 * val)
             elif isinstance(val, tuple):
-                field.__setattr__(field._fields_[0][0], addr(val[0]))
-                field.__setattr__(field._fields_[1][0], addr(val[1]))
+                field.__setattr__(field._fields_[0][0], base + 4 * val[0])
+                field.__setattr__(field._fields_[1][0], base + 4 * val[1])
             elif isinstance(val, list):
                 for i, sub in enumerate(val):
-                    DeviceNet._fill(field[i], sub, base)
+                    _Packer._fill(field[i], sub, base)
             elif isinstance(val, dict):
-                DeviceNet._fill(field, val, base)
+                _Packer._fill(field, val, base)
             else:
                 raise TypeError(name)
+
+
+class DeviceNet(_Packer):
+    """Packed device copy of a det-MADN parameter dict + the ``muz_net_w`` table the kernels read."""
+
+    def __init__(self, params: dict, obs_channels: int, num_actions: int = 24, device="cuda"):
+        super().__init__(params, obs_channels, num_actions)
+        P, put, A, d = self.params, self._put, self.A, "dynamics"
+        w = MuzNetW()
+        w.obs_channels, w.num_actions = self.C, self.A
+        k6, k7 = P[f"{d}/Dense_6/kernel"], P[f"{d}/Dense_7/kernel"]
+        spec = {"repr": self._repr_spec()}
+        spec["dyn"] = dict(
+            d0=self._plain(f"{d}/Dense_0"), ln0=self._ln(f"{d}/LayerNorm_0"),
+            d12=self._dense_k(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1),
+                              np.concatenate([P[f"{d}/Dense_1/bias"], P[f"{d}/Dense_2/bias"]])),
+            d3=self._dense(f"{d}/Dense_3"), ln1=self._ln(f"{d}/LayerNorm_1"), d4=self._dense(f"{d}/Dense_4"),
+            ln2=self._ln(f"{d}/LayerNorm_2"), rb=[self._rb(f"{d}/ResBlock_{i}") for i in range(2)],
+            d5=self._dense(f"{d}/Dense_5"),
+            d67=self._dense_k(np.concatenate([k6[:LATENT], k7[:LATENT]], 1),
+                              np.concatenate([P[f"{d}/Dense_6/bias"], P[f"{d}/Dense_7/bias"]])),
+            d67_onehot=put(np.concatenate([k6[LATENT:LATENT + A], k7[LATENT:LATENT + A]], 1)),
+            reward_head=self._plain(f"{d}/reward_head"), discount_head=self._plain(f"{d}/discount_head"),
+            film=put(np.zeros((A + 1) * 2 * LATENT, np.float32)))
+        spec["pred"] = self._pred_spec()
+        self._upload(w, spec, device)
+        lib = _L.load()
+        with torch.cuda.device(self.buffer.device):
+            _L.check(lib.muz_net_prepare(ctypes.byref(w), _L.stream_ptr()), "muz_net_prepare")
 
 
 # ---------------------------------------------------------------------------------- inference

@@ -1,0 +1,152 @@
+"""Stochastic MuZero for classic MADN on the GPU (host mirror of MuZero_Classic_MADN/muzero_classic_madn.py).
+
+* ``DeviceClassicNet`` packs a flat parameter dict (Flax paths, see oracle/classic_nets.py) into the
+  ``muz_classic_net_w`` table and fills the FiLM tables (``muz_classic_net_prepare``);
+* ``root_inference_fn`` (453-462), ``decision_recurrent_fn`` (414-432), ``chance_recurrent_fn`` (434-451);
+* ``run_stochastic_muzero_mcts`` (464-517): ``mctx.stochastic_muzero_policy`` as one HIP launch.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import lib as _L
+from .nets import LATENT, _Packer
+
+A_CLASSIC = 4
+CHANCE = 6
+
+
+class DeviceClassicNet(_Packer):
+    def __init__(self, params: dict, obs_channels: int, device="cuda"):
+        super().__init__(params, obs_channels, A_CLASSIC)
+        P, put, A, d = self.params, self._put, self.A, "dynamics"
+        w = _L.MuzClassicNetW()
+        w.obs_channels, w.num_actions = self.C, self.A
+        rd = P[f"{d}/reward_dense/kernel"]
+
+        def cat(n1, n2):
+            return self._dense_k(np.concatenate([P[f"{d}/{n1}/kernel"], P[f"{d}/{n2}/kernel"]], 1),
+                                 np.concatenate([P[f"{d}/{n1}/bias"], P[f"{d}/{n2}/bias"]]))
+
+        spec = {"repr": self._repr_spec(), "pred": self._pred_spec()}
+        spec["sdyn"] = dict(
+            act_embed=self._plain(f"{d}/act_embed"), act_input_ln=self._ln(f"{d}/act_input_ln"),
+            act_film=cat("act_film_scale", "act_film_shift"),
+            act_dense1=self._dense(f"{d}/act_dense1"), act_ln1=self._ln(f"{d}/act_ln1"),
+            act_dense2=self._dense(f"{d}/act_dense2"), act_ln2=self._ln(f"{d}/act_ln2"),
+            act_rb=[self._rb(f"{d}/ResBlock_{i}") for i in range(2)], act_proj=self._dense(f"{d}/act_proj"),
+            rc=self._dense_k(np.concatenate([rd[:LATENT], P[f"{d}/chance_head/kernel"]], 1),
+                             np.concatenate([P[f"{d}/reward_dense/bias"], P[f"{d}/chance_head/bias"]])),
+            reward_onehot=put(rd[LATENT:LATENT + A]), reward_head=self._plain(f"{d}/reward_head"),
+            discount_dense=self._dense(f"{d}/discount_dense"), discount_ln=self._ln(f"{d}/discount_ln"),
+            discount_head=self._plain(f"{d}/discount_head"),
+            chance_embed=self._plain(f"{d}/chance_embed"), chance_input_ln=self._ln(f"{d}/chance_input_ln"),
+            chance_film=cat("chance_film_scale", "chance_film_shift"),
+            chance_dense1=self._dense(f"{d}/chance_dense1"), chance_ln1=self._ln(f"{d}/chance_ln1"),
+            chance_dense2=self._dense(f"{d}/chance_dense2"), chance_ln2=self._ln(f"{d}/chance_ln2"),
+            chance_rb=[self._rb(f"{d}/ResBlock_{i}") for i in range(2, 4)],
+            chance_proj=self._dense(f"{d}/chance_proj"),
+            act_film_tab=put(np.zeros((A + 1) * 2 * LATENT, np.float32)),
+            chance_film_tab=put(np.zeros((CHANCE + 1) * 2 * LATENT, np.float32)))
+        self._upload(w, spec, device)
+        with torch.cuda.device(self.buffer.device):
+            _L.check(_L.load().muz_classic_net_prepare(ctypes.byref(w), _L.stream_ptr()), "muz_classic_net_prepare")
+
+
+def _f32(t):
+    return t.to(dtype=torch.float32).contiguous()
+
+
+def root_inference_fn(net: DeviceClassicNet, observation: torch.Tensor, scratch: torch.Tensor | None = None):
+    """root_inference_fn (453-462): obs [B, 2P+3, 56] -> (prior_logits [B, 4], value [B], embedding [B, 256])."""
+    lib = _L.load()
+    obs = _f32(observation)
+    B, dev = obs.shape[0], obs.device
+    if obs.shape[1] != net.C or obs.shape[2] != 56:
+        raise ValueError(f"observation shape {tuple(obs.shape)} != (B, {net.C}, 56)")
+    need = lib.muz_nets_root_scratch_bytes(B)
+    if scratch is None or _L.nbytes(scratch) < need:
+        scratch = torch.empty(need // 4, dtype=torch.float32, device=dev)
+    logits = torch.empty((B, A_CLASSIC), dtype=torch.float32, device=dev)
+    value = torch.empty((B,), dtype=torch.float32, device=dev)
+    emb = torch.empty((B, LATENT), dtype=torch.float32, device=dev)
+    _L.check(lib.muz_classic_nets_root(net.w, _L.ptr(obs), B, _L.ptr(scratch), _L.nbytes(scratch), _L.ptr(logits),
+                                       _L.ptr(value), _L.ptr(emb), _L.stream_ptr()), "muz_classic_nets_root")
+    return logits, value, emb
+
+
+def decision_recurrent_fn(net: DeviceClassicNet, action: torch.Tensor, embedding: torch.Tensor):
+    """decision_recurrent_fn (414-432) -> (chance_logits [B,6], afterstate_value [B], afterstate [B,256],
+    reward [B], discount [B]) -- the reference appends reward / discount to the afterstate."""
+    emb = _f32(embedding)
+    B, dev = emb.shape[0], emb.device
+    act = action.to(device=dev, dtype=torch.int32).contiguous()
+    after = torch.empty((B, LATENT), dtype=torch.float32, device=dev)
+    reward = torch.empty((B,), dtype=torch.float32, device=dev)
+    discount = torch.empty((B,), dtype=torch.float32, device=dev)
+    cl = torch.empty((B, CHANCE), dtype=torch.float32, device=dev)
+    av = torch.empty((B,), dtype=torch.float32, device=dev)
+    _L.check(_L.load().muz_classic_nets_decision(net.w, _L.ptr(act), _L.ptr(emb), B, _L.ptr(after), _L.ptr(reward),
+                                                 _L.ptr(discount), _L.ptr(cl), _L.ptr(av), _L.stream_ptr()),
+             "muz_classic_nets_decision")
+    return cl, av, after, reward, discount
+
+
+def chance_recurrent_fn(net: DeviceClassicNet, chance: torch.Tensor, afterstate: torch.Tensor):
+    """chance_recurrent_fn (434-451) -> (action_logits [B,4], value [B], next_embedding [B,256])."""
+    after = _f32(afterstate)
+    B, dev = after.shape[0], after.device
+    ch = chance.to(device=dev, dtype=torch.int32).contiguous()
+    nxt = torch.empty((B, LATENT), dtype=torch.float32, device=dev)
+    logits = torch.empty((B, A_CLASSIC), dtype=torch.float32, device=dev)
+    value = torch.empty((B,), dtype=torch.float32, device=dev)
+    _L.check(_L.load().muz_classic_nets_chance(net.w, _L.ptr(ch), _L.ptr(after), B, _L.ptr(nxt), _L.ptr(logits),
+                                               _L.ptr(value), _L.stream_ptr()), "muz_classic_nets_chance")
+    return logits, value, nxt
+
+
+def make_cfg(num_simulations, max_depth, temperature=1.0, seed=0, turn=0, dirichlet_fraction=0.25,
+             dirichlet_alpha=0.3, pb_c_init=1.25, pb_c_base=19652.0) -> _L.MuzStochCfg:
+    c = _L.MuzStochCfg()
+    c.num_simulations, c.max_depth = int(num_simulations), int(max_depth)
+    c.dirichlet_fraction, c.dirichlet_alpha = float(dirichlet_fraction), float(dirichlet_alpha)
+    c.pb_c_init, c.pb_c_base, c.temperature = float(pb_c_init), float(pb_c_base), float(temperature)
+    c.seed, c.turn = int(seed) & ((1 << 64) - 1), int(turn)
+    return c
+
+
+def stochastic_muzero_policy(net: DeviceClassicNet, root_logits, root_value, root_emb, legal_bits, num_simulations,
+                             max_depth, temperature=1.0, seed=0, turn=0, dirichlet=None, gumbel=None, game_id=None,
+                             workspace: torch.Tensor | None = None):
+    """mctx.stochastic_muzero_policy as called by run_stochastic_muzero_mcts (464-517).
+    Returns (action [B], action_weights [B, 4], root_value [B] clipped to [-1, 1])."""
+    lib = _L.load()
+    B, dev = root_logits.shape[0], root_logits.device
+    need = lib.muz_stochastic_workspace_bytes(B, num_simulations)
+    if workspace is None or _L.nbytes(workspace) < need:
+        workspace = torch.empty((need,), dtype=torch.uint8, device=dev)
+    action = torch.empty((B,), dtype=torch.int32, device=dev)
+    weights = torch.empty((B, A_CLASSIC), dtype=torch.float32, device=dev)
+    value = torch.empty((B,), dtype=torch.float32, device=dev)
+    cfg = make_cfg(num_simulations, max_depth, temperature, seed, turn)
+    lg, rv, re = _f32(root_logits), _f32(root_value), _f32(root_emb)
+    lb = legal_bits.to(device=dev, dtype=torch.int32).contiguous()
+    dn = None if dirichlet is None else _f32(dirichlet.to(dev))
+    gm = None if gumbel is None else _f32(gumbel.to(dev))
+    gi = None if game_id is None else game_id.to(device=dev, dtype=torch.int32).contiguous()
+    _L.check(lib.muz_stochastic_search(net.w, ctypes.byref(cfg), _L.ptr(lg), _L.ptr(rv), _L.ptr(re), _L.ptr(lb),
+                                       _L.ptr(dn), _L.ptr(gm), _L.ptr(gi), B, _L.ptr(workspace), _L.nbytes(workspace),
+                                       _L.ptr(action), _L.ptr(weights), _L.ptr(value), _L.stream_ptr()),
+             "muz_stochastic_search")
+    return action, weights, value
+
+
+def run_stochastic_muzero_mcts(net: DeviceClassicNet, observations, legal_bits, num_simulations, max_depth,
+                               temperature, seed=0, turn=0, **kw):
+    """run_stochastic_muzero_mcts (464-517): root inference + search."""
+    logits, value, emb = root_inference_fn(net, observations)
+    return stochastic_muzero_policy(net, logits, value, emb, legal_bits, num_simulations, max_depth, temperature,
+                                    seed=seed, turn=turn, **kw)

@@ -298,6 +298,96 @@ int muz_detmadn_selfplay(const muz_rules* rules /*host*/, const muz_net_w* w /*h
                          const muz_search_cfg* cfg /*host*/, muz_detmadn_soa state, muz_traj traj, int32_t n,
                          void* workspace, int64_t workspace_bytes, muz_sp_stats* stats /*host*/, void* stream);
 
+/* ---- Stochastic MuZero for classic MADN (MuZero_Classic_MADN/muzero_classic_madn.py) ----------
+ * Same packing conventions as the det networks.  RepresentationNetwork2 (69-135) and
+ * PredictionNetwork4 (192-226, A = 4) reuse muz_repr_w / muz_pred_w. */
+
+/* StochasticDynamicsNetwork4 (314-408). */
+typedef struct muz_sdyn_w {
+  /* action_dynamics (329-371) */
+  muz_dense act_embed;          /* plain [A][64] */
+  muz_ln act_input_ln;
+  muz_dense act_film;           /* packed, act_film_scale | act_film_shift fused: 64 -> 512 */
+  muz_dense act_dense1;
+  muz_ln act_ln1;
+  muz_dense act_dense2;
+  muz_ln act_ln2;
+  muz_resblock act_rb[2];
+  muz_dense act_proj;
+  muz_dense rc;                 /* packed, reward_dense afterstate rows | chance_head fused: 256 -> 70 */
+  const float* reward_onehot;   /* plain [A][64]: one-hot rows 256.. of reward_dense */
+  muz_dense reward_head;        /* plain [64][3] */
+  muz_dense discount_dense;     /* packed 256 -> 32, applied to the INPUT latent (366) */
+  muz_ln discount_ln;           /* 32 */
+  muz_dense discount_head;      /* plain [32][3] */
+  /* chance_dynamics (373-408) */
+  muz_dense chance_embed;       /* plain [6][64] */
+  muz_ln chance_input_ln;
+  muz_dense chance_film;        /* packed 64 -> 512 */
+  muz_dense chance_dense1;
+  muz_ln chance_ln1;
+  muz_dense chance_dense2;
+  muz_ln chance_ln2;
+  muz_resblock chance_rb[2];
+  muz_dense chance_proj;
+  float* act_film_tab;          /* derived [A+1][512]  (muz_classic_net_prepare) */
+  float* chance_film_tab;       /* derived [6+1][512] */
+} muz_sdyn_w;
+
+typedef struct muz_classic_net_w {
+  int32_t obs_channels;         /* 2P+3 */
+  int32_t num_actions;          /* 4 */
+  muz_repr_w repr;
+  muz_sdyn_w sdyn;
+  muz_pred_w pred;
+} muz_classic_net_w;
+
+#define MUZ_CHANCE_OUTCOMES 6
+
+/* Fills sdyn.act_film_tab / chance_film_tab from the raw layers (the FiLM sub-graphs depend on the
+ * action / chance outcome only).  Call after the weights change. */
+int muz_classic_net_prepare(const muz_classic_net_w* w, void* stream);
+
+/* root_inference_fn (453-462): Repr2 + Pred4 -> prior_logits [n][4], value [n], embedding [n][256]. */
+int muz_classic_nets_root(const muz_classic_net_w* w, const float* obs, int32_t n, void* scratch,
+                          int64_t scratch_bytes, float* prior_logits, float* value, float* embedding, void* stream);
+
+/* decision_recurrent_fn (414-432): afterstate [n][256], reward / discount [n] (support expectations the
+ * reference appends to the afterstate), chance_logits [n][6], afterstate_value [n]. */
+int muz_classic_nets_decision(const muz_classic_net_w* w, const int32_t* action, const float* embedding, int32_t n,
+                              float* afterstate, float* reward, float* discount, float* chance_logits,
+                              float* afterstate_value, void* stream);
+
+/* chance_recurrent_fn (434-451): next_embedding [n][256], action_logits [n][4], value [n]. */
+int muz_classic_nets_chance(const muz_classic_net_w* w, const int32_t* chance, const float* afterstate, int32_t n,
+                            float* next_embedding, float* action_logits, float* value, void* stream);
+
+/* mctx.stochastic_muzero_policy as called by run_stochastic_muzero_mcts (464-517). */
+typedef struct muz_stoch_cfg {
+  int32_t num_simulations;      /* S <= 100 */
+  int32_t max_depth;            /* D <= 64 */
+  float dirichlet_fraction;     /* 0.25 */
+  float dirichlet_alpha;        /* 0.3 */
+  float pb_c_init;              /* 1.25 */
+  float pb_c_base;              /* 19652 */
+  float temperature;
+  int32_t turn;                 /* counter-RNG stream */
+  uint64_t seed;
+} muz_stoch_cfg;
+
+int64_t muz_stochastic_workspace_bytes(int32_t n, int32_t num_simulations);
+
+/* root: prior_logits [n][4], value [n], embedding [n][256] (muz_classic_nets_root); legal_bits bit a = pin a
+ * legal.  dirichlet [n][4] / gumbel [n][4] are the root noise sample and the Gumbel draws of the final
+ * categorical; null = the engine's counter RNG (Gamma(alpha) sampler / -log(-log U)).  The 1e-7
+ * tie-break uniforms always come from the counter RNG (seed, game, turn, sim, depth, action).
+ * Outputs: action [n], action_weights [n][4] (visit distribution), root_value [n] clipped to [-1, 1]. */
+int muz_stochastic_search(const muz_classic_net_w* w, const muz_stoch_cfg* cfg, const float* root_logits,
+                          const float* root_value, const float* root_embedding, const uint32_t* legal_bits,
+                          const float* dirichlet, const float* gumbel, const int32_t* game_id, int32_t n,
+                          void* workspace, int64_t workspace_bytes, int32_t* action, float* action_weights,
+                          float* root_value_out, void* stream);
+
 /* ---- device replay ring (MuZero_det_MADN/vec_replay_buffer.py) ------------------------------
  * The reference's VectorizedReplayBuffer keeps [capacity][T] host NumPy arrays (obs fp32, 84 GB at
  * capacity 20000, T 550, C 34).  Here the ring lives in HBM, obs int8 (values 0..4, exact):
