@@ -26,4 +26,19 @@ int launch_gumbel_search(const muz_net_w& w, const SearchArgs& sa, const float* 
 
 int64_t search_workspace_bytes(int n, int S);
 
+// Stochastic MuZero (stochastic.hip)
+struct SArgs {
+  int S, D, A;
+  float dir_frac, dir_alpha, pb_c_init, pb_c_base, temperature;
+  unsigned long long seed;
+  int turn;
+};
+SArgs make_sargs(const muz_stoch_cfg& cfg, int A);
+int launch_stochastic_search(const muz_classic_net_w& w, const SArgs& sa, const float* root_logits,
+                             const float* root_value, const float* root_emb, const uint32_t* legal,
+                             const float* dirichlet, const float* gumbel, const int32_t* game_id, int n, const int* n_dev,
+                             void* workspace, int32_t* action, float* weights, float* value, hipStream_t s);
+int64_t stochastic_workspace_bytes(int n, int S);
+int check_classic_net(const muz_classic_net_w* w);
+
 }  // namespace muz

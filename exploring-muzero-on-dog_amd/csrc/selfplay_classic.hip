@@ -1,42 +1,50 @@
-// Native self-play driver for deterministic MADN: play_n_games_v3 / play_batch_of_games_jitted
-// (MuZero_det_MADN/game_agent.py:50-192) as a host loop of stream-ordered HIP launches.
+// Native self-play driver for classic MADN with Stochastic MuZero: play_n_games_v3 /
+// play_batch_of_games_jitted of MuZero_Classic_MADN/game_agent_stochastic.py:52-257, as a host loop of
+// stream-ordered HIP launches (same structure as the det driver, selfplay.hip).
 //
-// Per turn: legal masks + active flags for every game -> deterministic device compaction of the
-// games that search (has a legal move) -> encode their observations -> root inference ->
-// persistent Gumbel search -> env_step / no_step + trajectory records.  Unlike the reference's
-// vmap-of-cond, finished games and no-move turns cost no network work, and there is no host round
-// trip inside a turn: batch sizes live on the device (`counts`), surplus workgroups exit early.
-// The host checks the active-game count two turns late (pinned memory + events), so the GPU queue
-// never drains; the at most two trailing turns it launches find no active game and record nothing.
-#include "detmadn.hpp"
+// Per turn: throw the die of every active game (counter RNG -> throw_die) + legal masks + flags ->
+// device compaction of the games that search -> encode -> root inference -> stochastic search ->
+// env_step / no_step + trajectory records (incl. the die and the next state's dice distribution).
+#include "classic.hpp"
+#include "compact.hpp"
 #include "host_consts.hpp"
 #include "launch.hpp"
-#include "compact.hpp"
+#include "rng.hpp"
 
 namespace muz {
 
-constexpr int kSpBlock = 256;
+constexpr int kCsBlock = 256;
+constexpr unsigned long long kDieStream = 0xD1CE5EEDF00DULL;
 
-__global__ __launch_bounds__(kSpBlock) void k_sp_flags(DetConsts c, muz_detmadn_soa st, uint32_t* legal, int32_t* flag,
-                                                       int n) {
-  __shared__ int8_t sboard[kCells * kSpBlock];
-  const int g = blockIdx.x * kSpBlock + threadIdx.x;
+// Die of the turn: u = U[0,1) from (seed ^ kDieStream, game, turn), die = throw_die(env, u).
+__device__ __forceinline__ float die_uniform(unsigned long long seed, int g, int turn) {
+  return u24(mix64(game_key(seed ^ kDieStream, g, turn)));
+}
+
+__global__ __launch_bounds__(kCsBlock) void k_cs_flags(DetConsts c, muz_classic_soa st, unsigned long long seed,
+                                                       int turn, uint32_t* legal, int32_t* flag, int n) {
+  __shared__ int8_t sboard[kCells * kCsBlock];
+  const int g = blockIdx.x * kCsBlock + threadIdx.x;
   if (g >= n) return;
-  if (st.done[g]) {
+  if (st.done[g]) {   // do_skip_step: nothing happens to a finished game
     flag[g] = 0;
     legal[g] = 0;
     return;
   }
-  BoardView b{sboard + threadIdx.x, kSpBlock};
-  DetLane s;
-  det_load(c, st, g, s, b);
-  const uint32_t l = det_legal(c, s, b);
+  BoardView b{sboard + threadIdx.x, kCsBlock};
+  ClsLane s;
+  cls_load(c, st, g, s, b);
+  float p[6];
+  cls_dice_probs(c, cls_soft_locked(c, s, b), p);
+  s.die = cls_choice(p, die_uniform(seed, g, turn));
+  st.die[g] = (int8_t)s.die;
+  const uint32_t l = cls_legal(c, s, b);
   legal[g] = l;
-  flag[g] = l ? 1 : 2;   // 1: search + env_step, 2: no legal move -> no_step (game_agent.py:119)
+  flag[g] = l ? 1 : 2;
 }
 
-// Observation of every searching game (compacted order) + its int8 trajectory record.
-__global__ __launch_bounds__(64) void k_sp_encode(DetConsts c, muz_detmadn_soa st, const int32_t* list,
+// Observation (after the die) of every searching game, compacted order, + its int8 record.
+__global__ __launch_bounds__(64) void k_cs_encode(DetConsts c, muz_classic_soa st, const int32_t* list,
                                                   const int32_t* counts, const uint32_t* legal, uint32_t* legal_c,
                                                   float* obs, int8_t* traj_obs, const int32_t* idx, int T) {
   const int sl = blockIdx.x;
@@ -46,74 +54,72 @@ __global__ __launch_bounds__(64) void k_sp_encode(DetConsts c, muz_detmadn_soa s
   const int g = list[sl];
   if (w == 0) legal_c[sl] = legal[g];
   const int S = st.stride;
-  DetLane s;
+  ClsLane s;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int v = st.pins[min(j, c.P * 4 - 1) * S + g];
     s.pins[j] = (j < c.P * 4) ? v : -1;
   }
-#pragma unroll
-  for (int j = 0; j < 24; ++j) {
-    const int v = st.action_set[min(j, c.P * 6 - 1) * S + g];
-    s.aset[j] = (j < c.P * 6) ? v : 0;
-  }
   s.cp = st.current_player[g];
-  const int C = 8 * c.P + 2;
+  s.die = st.die[g];
+  const int C = 2 * c.P + 3;
   float* o = obs + (size_t)sl * C * kCells;
   int8_t* to = traj_obs + ((size_t)g * T + idx[g]) * C * kCells;
   auto owner = [&](int cell) { return (int)st.board[cell * S + g]; };
   for (int ch = 0; ch < C; ++ch) {
-    const int v = det_encode_value(c, s, ch, w, owner);
+    const int v = cls_encode_value(c, s, ch, w, owner);
     o[ch * kCells + w] = (float)v;
     to[ch * kCells + w] = (int8_t)v;
   }
 }
 
-// Apply the searched action (env_step) or no_step, and write the trajectory record
-// (game_agent.py:79-141).
-__global__ __launch_bounds__(kSpBlock) void k_sp_apply(DetConsts c, muz_detmadn_soa st, const int32_t* flag,
+// do_mcts / do_skip + the buffer update (game_agent_stochastic.py:104-174).
+__global__ __launch_bounds__(kCsBlock) void k_cs_apply(DetConsts c, muz_classic_soa st, const int32_t* flag,
                                                        const int32_t* slot, const int32_t* s_action,
                                                        const float* s_weights, const float* s_value, muz_traj tr,
-                                                       int n) {
-  __shared__ int8_t sboard[kCells * kSpBlock];
-  const int g = blockIdx.x * kSpBlock + threadIdx.x;
+                                                       muz_traj_chance ch, int n) {
+  __shared__ int8_t sboard[kCells * kCsBlock];
+  const int g = blockIdx.x * kCsBlock + threadIdx.x;
   if (g >= n) return;
   const int f = flag[g];
   if (f == 0) return;
-  BoardView b{sboard + threadIdx.x, kSpBlock};
-  DetLane s;
-  det_load(c, st, g, s, b);
+  BoardView b{sboard + threadIdx.x, kCsBlock};
+  ClsLane s;
+  cls_load(c, st, g, s, b);
   const bool teams = has(c.flags, R_TEAMS);
   const int T = tr.max_steps;
   const int t = tr.idx[g];
   const size_t rec = (size_t)g * T + t;
   const int cp_before = s.cp;
   const int team_before = teams ? cp_before % 2 : -1;
+  const int die = s.die;
   int act, rew_cls, disc_cls;
   float val, mask;
   if (f == 1) {
     const int sl = slot[g];
     act = s_action[sl];
-    const int r = det_step(c, s, b, fdiv(act, 6), fmodp(act, 6) + 1);
+    const int r = cls_step(c, s, b, act);
     const bool nd = s.done != 0;
-    const int next_player = s.cp;
-    const int next_team = teams ? next_player % 2 : -1;
+    const int next_team = teams ? s.cp % 2 : -1;
     rew_cls = (nd && r > 0) ? 2 : ((nd && r < 0) ? 0 : 1);
-    disc_cls = nd ? 1 : (teams ? (team_before == next_team ? 2 : 0) : (cp_before == next_player ? 2 : 0));
+    disc_cls = nd ? 1 : (teams ? (team_before == next_team ? 2 : 0) : (cp_before == s.cp ? 2 : 0));
     val = s_value[sl];
     mask = 1.f;
-    float* pol = tr.pol + rec * MUZ_DET_ACTIONS;
-    for (int a = 0; a < MUZ_DET_ACTIONS; ++a) pol[a] = s_weights[(size_t)sl * MUZ_DET_ACTIONS + a];
-    det_store(c, st, g, s, b, true);
+    for (int a = 0; a < MUZ_CLASSIC_ACTIONS; ++a)
+      tr.pol[rec * MUZ_CLASSIC_ACTIONS + a] = s_weights[(size_t)sl * MUZ_CLASSIC_ACTIONS + a];
   } else {
-    det_nostep(c, s);   // obs / policy records stay zero (buffers are zeroed per call)
+    s.cp = (s.cp + 1) % c.P;   // no_step (353-365); obs / policy records stay zero
     act = -1;
     rew_cls = 1;
     disc_cls = 1;
     val = 0.f;
     mask = 0.f;
-    det_store(c, st, g, s, b, false);
   }
+  cls_store(c, st, g, s, b);
+  float p[6];
+  cls_dice_probs(c, cls_soft_locked(c, s, b), p);   // dice_probabilities(next_env) (line 162)
+  for (int i = 0; i < 6; ++i) ch.dice_dist[rec * 6 + i] = p[i];
+  ch.dice[rec] = die;
   tr.act[rec] = act;
   tr.rew[rec] = rew_cls;
   tr.val[rec] = val;
@@ -124,7 +130,7 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_apply(DetConsts c, muz_detmadn_
   tr.idx[g] = t + 1;
 }
 
-__global__ void k_det_reset_sp(DetConsts c, muz_detmadn_soa st, int n) {
+__global__ void k_cs_reset(DetConsts c, muz_classic_soa st, int n) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;
   const int S = st.stride;
@@ -132,15 +138,15 @@ __global__ void k_det_reset_sp(DetConsts c, muz_detmadn_soa st, int n) {
   for (int cell = 0; cell < kCells; ++cell) st.board[cell * S + g] = -1;
   for (int p = 0; p < c.P; ++p) {
     for (int k = 0; k < 4; ++k) st.pins[(p * 4 + k) * S + g] = (int8_t)((fp && k == 0) ? c.start[p] : -1);
-    for (int m = 0; m < 6; ++m) st.action_set[(p * 6 + m) * S + g] = 4;
     if (fp) st.board[c.start[p] * S + g] = (int8_t)p;
   }
   st.current_player[g] = (int8_t)c.starting_player;
   st.reward[g] = 0;
   st.done[g] = 0;
+  st.die[g] = 0;
 }
 
-struct SpWs {
+struct CsWs {
   void* tree;
   float* conv;
   float* obs;
@@ -158,18 +164,18 @@ struct SpWs {
   int32_t* counts;
 };
 
-static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+static inline size_t cal256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static size_t sp_carve(char* base, int n, int C, int S, SpWs* w) {
+static size_t cs_carve(char* base, int n, int C, int S, CsWs* w) {
   const size_t n16 = (size_t)((n + 15) / 16 * 16);
   size_t off = 0;
   auto take = [&](size_t bytes) {
     char* p = base ? base + off : nullptr;
-    off += al256(bytes);
+    off += cal256(bytes);
     return p;
   };
-  SpWs t;
-  t.tree = take((size_t)search_workspace_bytes(n, S));
+  CsWs t;
+  t.tree = take((size_t)stochastic_workspace_bytes(n, S));
   t.conv = (float*)take(n16 * 3584 * 4);
   t.obs = (float*)take(n16 * C * kCells * 4);
   t.legal = (uint32_t*)take((size_t)n * 4);
@@ -177,11 +183,11 @@ static size_t sp_carve(char* base, int n, int C, int S, SpWs* w) {
   t.flag = (int32_t*)take((size_t)n * 4);
   t.slot = (int32_t*)take((size_t)n * 4);
   t.list = (int32_t*)take((size_t)n * 4);
-  t.root_logits = (float*)take(n16 * MUZ_DET_ACTIONS * 4);
+  t.root_logits = (float*)take(n16 * MUZ_CLASSIC_ACTIONS * 4);
   t.root_value = (float*)take(n16 * 4);
   t.root_emb = (float*)take(n16 * 256 * 4);
   t.action = (int32_t*)take(n16 * 4);
-  t.weights = (float*)take(n16 * MUZ_DET_ACTIONS * 4);
+  t.weights = (float*)take(n16 * MUZ_CLASSIC_ACTIONS * 4);
   t.value = (float*)take(n16 * 4);
   t.counts = (int32_t*)take(64);
   if (w) *w = t;
@@ -194,62 +200,55 @@ using namespace muz;
 
 extern "C" {
 
-int64_t muz_selfplay_workspace_bytes(int32_t n, int32_t obs_channels, const muz_search_cfg* cfg) {
-  if (!cfg || n < 0) return -1;
-  return (int64_t)sp_carve(nullptr, n, obs_channels, cfg->num_simulations, nullptr);
+int64_t muz_classic_selfplay_workspace_bytes(int32_t n, int32_t obs_channels, const muz_stoch_cfg* cfg) {
+  if (!cfg || n < 0 || cfg->num_simulations < 1) return -1;
+  return (int64_t)cs_carve(nullptr, n, obs_channels, cfg->num_simulations, nullptr);
 }
 
-int muz_detmadn_selfplay(const muz_rules* rules, const muz_net_w* w, const muz_search_cfg* cfg, muz_detmadn_soa st,
-                         muz_traj tr, int32_t n, void* workspace, int64_t workspace_bytes, muz_sp_stats* stats,
-                         void* stream) {
+int muz_classic_selfplay(const muz_rules* rules, const muz_classic_net_w* w, const muz_stoch_cfg* cfg,
+                         muz_classic_soa st, muz_traj tr, muz_traj_chance ch, int32_t n, void* workspace,
+                         int64_t workspace_bytes, muz_sp_stats* stats, void* stream) {
   DetConsts c;
   int rc = make_det_consts(rules, &c);
   if (rc) return rc;
-  if (!w || !cfg) return MUZ_E_INVALID;
-  if (w->obs_channels != 8 * c.P + 2 || w->num_actions != MUZ_DET_ACTIONS) return MUZ_E_UNSUPPORTED;
+  if (!cfg) return MUZ_E_INVALID;
+  if ((rc = check_classic_net(w))) return rc;
+  if (w->obs_channels != 2 * c.P + 3) return MUZ_E_UNSUPPORTED;
   MUZ_HOST_CHECK(n >= 0 && st.stride >= n && workspace && tr.max_steps > 0 && tr.obs && tr.act && tr.rew &&
-                 tr.val && tr.pol && tr.mask && tr.player && tr.team && tr.discount && tr.idx);
+                 tr.val && tr.pol && tr.mask && tr.player && tr.team && tr.discount && tr.idx && ch.dice &&
+                 ch.dice_dist);
   if (cfg->num_simulations < 1 || cfg->num_simulations > 100 || cfg->max_depth < 1 || cfg->max_depth > 64)
     return MUZ_E_UNSUPPORTED;
   if (stats) *stats = muz_sp_stats{};
-  MUZ_HOST_CHECK(workspace_bytes >= (int64_t)sp_carve(nullptr, n, w->obs_channels, cfg->num_simulations, nullptr));
+  MUZ_HOST_CHECK(workspace_bytes >= (int64_t)cs_carve(nullptr, n, w->obs_channels, cfg->num_simulations, nullptr));
   if (n == 0) return MUZ_OK;
   hipStream_t s = (hipStream_t)stream;
   const int C = w->obs_channels;
   const int T = tr.max_steps;
-  SpWs ws;
-  sp_carve((char*)workspace, n, C, cfg->num_simulations, &ws);
+  CsWs ws;
+  cs_carve((char*)workspace, n, C, cfg->num_simulations, &ws);
 
-  // play_n_games_v3: batch_reset + zeroed buffers (init_buffers, game_agent.py:158-169)
-  k_det_reset_sp<<<(n + 255) / 256, 256, 0, s>>>(c, st, n);
+  k_cs_reset<<<(n + 255) / 256, 256, 0, s>>>(c, st, n);
   const size_t nt = (size_t)n * T;
   MUZ_HIP_RET(hipMemsetAsync(tr.obs, 0, nt * C * kCells, s));
   MUZ_HIP_RET(hipMemsetAsync(tr.act, 0, nt * 4, s));
   MUZ_HIP_RET(hipMemsetAsync(tr.rew, 0, nt * 4, s));
   MUZ_HIP_RET(hipMemsetAsync(tr.val, 0, nt * 4, s));
-  MUZ_HIP_RET(hipMemsetAsync(tr.pol, 0, nt * MUZ_DET_ACTIONS * 4, s));
+  MUZ_HIP_RET(hipMemsetAsync(tr.pol, 0, nt * MUZ_CLASSIC_ACTIONS * 4, s));
   MUZ_HIP_RET(hipMemsetAsync(tr.mask, 0, nt * 4, s));
   MUZ_HIP_RET(hipMemsetAsync(tr.player, 0, nt * 4, s));
   MUZ_HIP_RET(hipMemsetAsync(tr.team, 0xFF, nt * 4, s));   // jnp.full(..., -1)
   MUZ_HIP_RET(hipMemsetAsync(tr.discount, 0, nt * 4, s));
   MUZ_HIP_RET(hipMemsetAsync(tr.idx, 0, (size_t)n * 4, s));
+  MUZ_HIP_RET(hipMemsetAsync(ch.dice, 0, nt * 4, s));
+  MUZ_HIP_RET(hipMemsetAsync(ch.dice_dist, 0, nt * 6 * 4, s));
 
-  SearchArgs sa;
-  sa.S = cfg->num_simulations;
-  sa.D = cfg->max_depth;
-  sa.max_considered = cfg->max_num_considered;
-  sa.value_scale = cfg->value_scale;
-  sa.maxvisit_init = cfg->maxvisit_init;
-  sa.gumbel_scale = cfg->gumbel_scale;
-  sa.seed = cfg->seed;
-
+  SArgs sa = make_sargs(*cfg, w->num_actions);
   constexpr int kLag = 2, kRing = 4;
-  // host_counts[turn][0] = games searching this turn, [1] = games active at the start of this turn
   int32_t* host_counts = nullptr;
   MUZ_HIP_RET(hipHostMalloc((void**)&host_counts, (size_t)T * 2 * sizeof(int32_t), hipHostMallocDefault));
   hipEvent_t ev[kRing];
   for (int i = 0; i < kRing; ++i) (void)hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
-  // optional per-turn timing of the search launch (stats != null)
   hipEvent_t* tev = nullptr;
   if (stats) {
     tev = new hipEvent_t[2 * (size_t)T];
@@ -267,30 +266,29 @@ int muz_detmadn_selfplay(const muz_rules* rules, const muz_net_w* w, const muz_s
       (void)hipEventSynchronize(ev[k]);
       if (host_counts[2 * (turn - kLag) + 1] == 0) break;
     }
-    k_sp_flags<<<(n + kSpBlock - 1) / kSpBlock, kSpBlock, 0, s>>>(c, st, ws.legal, ws.flag, n);
+    k_cs_flags<<<(n + kCsBlock - 1) / kCsBlock, kCsBlock, 0, s>>>(c, st, cfg->seed, turn, ws.legal, ws.flag, n);
     k_sp_compact<<<1, kScanThreads, 0, s>>>(ws.flag, n, ws.list, ws.slot, ws.counts);
     (void)hipMemcpyAsync(&host_counts[2 * turn], ws.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s);
     (void)hipEventRecord(ev[turn % kRing], s);
-    k_sp_encode<<<n, 64, 0, s>>>(c, st, ws.list, ws.counts, ws.legal, ws.legal_c, ws.obs, tr.obs, tr.idx, T);
+    k_cs_encode<<<n, 64, 0, s>>>(c, st, ws.list, ws.counts, ws.legal, ws.legal_c, ws.obs, tr.obs, tr.idx, T);
     if ((rc = muz_last_launch_error())) break;
     if ((rc = launch_root_inference(*w, ws.obs, n, ws.counts, ws.conv, ws.root_logits, ws.root_value, ws.root_emb,
                                     s)))
       break;
     sa.turn = turn;
     if (tev) (void)hipEventRecord(tev[2 * turn], s);
-    if ((rc = launch_gumbel_search(*w, sa, ws.root_logits, ws.root_value, ws.root_emb, ws.legal_c, nullptr, ws.list, n, ws.counts, ws.tree, ws.action, ws.weights,
-                                   ws.value, s)))
+    if ((rc = launch_stochastic_search(*w, sa, ws.root_logits, ws.root_value, ws.root_emb, ws.legal_c, nullptr, nullptr,
+                                       ws.list, n, ws.counts, ws.tree, ws.action, ws.weights, ws.value, s)))
       break;
     if (tev) (void)hipEventRecord(tev[2 * turn + 1], s);
-    k_sp_apply<<<(n + kSpBlock - 1) / kSpBlock, kSpBlock, 0, s>>>(c, st, ws.flag, ws.slot, ws.action, ws.weights,
-                                                                   ws.value, tr, n);
+    k_cs_apply<<<(n + kCsBlock - 1) / kCsBlock, kCsBlock, 0, s>>>(c, st, ws.flag, ws.slot, ws.action, ws.weights,
+                                                                   ws.value, tr, ch, n);
     if ((rc = muz_last_launch_error())) break;
     ++turns;
   }
   (void)hipEventRecord(t1, s);
   (void)hipStreamSynchronize(s);
   if (stats) {
-    // turns whose start found no active game recorded nothing: count the turns the reference would run
     int active_turns = 0;
     long long searches = 0;
     double search_ms = 0.0;

@@ -72,13 +72,6 @@ static STree carve_stree(void* ws, int n, int N) {
   return t;
 }
 
-struct SArgs {
-  int S, D, A;
-  float dir_frac, dir_alpha, pb_c_init, pb_c_base, temperature;
-  unsigned long long seed;
-  int turn;
-};
-
 struct SKid {
   float prior, value, reward, disc;
   int visits, index;
@@ -490,6 +483,32 @@ int64_t stochastic_workspace_bytes(int n, int S) {
   return (int64_t)(6 * stree_child_bytes(n, N) + (size_t)n * N * LAT * 4 + (size_t)n * N * 2 * 4);
 }
 
+SArgs make_sargs(const muz_stoch_cfg& cfg, int A) {
+  SArgs sa;
+  sa.S = cfg.num_simulations;
+  sa.D = cfg.max_depth;
+  sa.A = A;
+  sa.dir_frac = cfg.dirichlet_fraction;
+  sa.dir_alpha = cfg.dirichlet_alpha;
+  sa.pb_c_init = cfg.pb_c_init;
+  sa.pb_c_base = cfg.pb_c_base;
+  sa.temperature = cfg.temperature;
+  sa.seed = cfg.seed;
+  sa.turn = cfg.turn;
+  return sa;
+}
+
+int launch_stochastic_search(const muz_classic_net_w& w, const SArgs& sa, const float* root_logits,
+                             const float* root_value, const float* root_emb, const uint32_t* legal,
+                             const float* dirichlet, const float* gumbel, const int32_t* game_id, int n, const int* n_dev,
+                             void* workspace, int32_t* action, float* weights, float* value, hipStream_t s) {
+  const STree T = carve_stree(workspace, n, sa.S + 1);
+  k_stochastic_search<<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, sa, root_logits, root_value, root_emb, legal,
+                                                                   dirichlet, gumbel, game_id, n, n_dev, T, action,
+                                                                   weights, value);
+  return muz_last_launch_error();
+}
+
 int check_classic_net(const muz_classic_net_w* w) {
   if (!w) return MUZ_E_INVALID;
   if (w->num_actions != kCls) return MUZ_E_UNSUPPORTED;
@@ -567,22 +586,9 @@ int muz_stochastic_search(const muz_classic_net_w* w, const muz_stoch_cfg* cfg, 
   if (cfg->max_depth < 1 || cfg->max_depth > kSMaxDepth) return MUZ_E_UNSUPPORTED;
   MUZ_HOST_CHECK(workspace_bytes >= stochastic_workspace_bytes(n, cfg->num_simulations));
   if (n == 0) return MUZ_OK;
-  SArgs sa;
-  sa.S = cfg->num_simulations;
-  sa.D = cfg->max_depth;
-  sa.A = w->num_actions;
-  sa.dir_frac = cfg->dirichlet_fraction;
-  sa.dir_alpha = cfg->dirichlet_alpha;
-  sa.pb_c_init = cfg->pb_c_init;
-  sa.pb_c_base = cfg->pb_c_base;
-  sa.temperature = cfg->temperature;
-  sa.seed = cfg->seed;
-  sa.turn = cfg->turn;
-  const STree T = carve_stree(workspace, n, cfg->num_simulations + 1);
-  k_stochastic_search<<<(n + kRows - 1) / kRows, kThreads, 0, (hipStream_t)stream>>>(
-      *w, sa, root_logits, root_value, root_embedding, legal_bits, dirichlet, gumbel, game_id, n, nullptr, T, action,
-      action_weights, root_value_out);
-  return muz_last_launch_error();
+  return launch_stochastic_search(*w, make_sargs(*cfg, w->num_actions), root_logits, root_value, root_embedding,
+                                  legal_bits, dirichlet, gumbel, game_id, n, nullptr, workspace, action, action_weights,
+                                  root_value_out, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,82 @@
+"""Batched Stochastic-MuZero self-play for classic MADN on the GPU (host mirror of
+MuZero_Classic_MADN/game_agent_stochastic.py).
+
+``StochasticSelfPlayEngine.play`` = ``play_n_games_v3`` (234-257) + ``play_batch_of_games_jitted``
+(52-218): the whole loop runs natively (muz_classic_selfplay).  Buffers: the det keys with
+``pol`` [n, T, 4], plus ``dice`` [n, T] and ``dice_dist`` [n, T, 6]; ``obs`` is int8.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import classic as E
+from . import lib as _L
+from . import stochastic as ST
+
+# MuZero_Classic_MADN/game_agent_stochastic.py:13-24
+RULES = dict(E.SELFPLAY_RULES)
+
+
+class StochasticSelfPlayEngine:
+    def __init__(self, net: ST.DeviceClassicNet, num_envs: int, num_players: int = 4, max_steps: int = 550,
+                 num_simulations: int = 50, max_depth: int = 25, rules: dict | None = None, starting_player=0,
+                 device="cuda"):
+        self.net = net
+        self.n, self.P, self.T = int(num_envs), int(num_players), int(max_steps)
+        self.S, self.D = int(num_simulations), int(max_depth)
+        self.C = E.num_channels(self.P)
+        if net.C != self.C:
+            raise ValueError(f"network expects {net.C} observation channels, {self.P} players give {self.C}")
+        self.rules = E.make_rules(self.P, starting_player=starting_player, **dict(RULES if rules is None else rules))
+        self.state = E._alloc(self.n, self.P, self.rules, device)
+        n, T = self.n, self.T
+        z = dict(device=device)
+        self.buffers = {
+            "obs": torch.empty((n, T, self.C, E.CELLS), dtype=torch.int8, **z),
+            "act": torch.empty((n, T), dtype=torch.int32, **z),
+            "rew": torch.empty((n, T), dtype=torch.int32, **z),
+            "val": torch.empty((n, T), dtype=torch.float32, **z),
+            "pol": torch.empty((n, T, ST.A_CLASSIC), dtype=torch.float32, **z),
+            "mask": torch.empty((n, T), dtype=torch.float32, **z),
+            "dice": torch.empty((n, T), dtype=torch.int32, **z),
+            "dice_dist": torch.empty((n, T, ST.CHANCE), dtype=torch.float32, **z),
+            "player": torch.empty((n, T), dtype=torch.int32, **z),
+            "team": torch.empty((n, T), dtype=torch.int32, **z),
+            "discount": torch.empty((n, T), dtype=torch.int32, **z),
+            "idx": torch.empty((n,), dtype=torch.int32, **z),
+        }
+        cfg = ST.make_cfg(self.S, self.D)
+        self.workspace = torch.empty((_L.load().muz_classic_selfplay_workspace_bytes(n, self.C, cfg),),
+                                     dtype=torch.uint8, **z)
+        self.last_turns = 0
+        self.last_stats = None
+
+    def play(self, seed: int, temperature: float = 1.0, dirichlet_fraction: float = 0.25, stream=None,
+             timing: bool = True) -> dict:
+        lib = _L.load()
+        cfg = ST.make_cfg(self.S, self.D, temperature=temperature, seed=seed, dirichlet_fraction=dirichlet_fraction)
+        t = _L.MuzTraj()
+        for k in ("obs", "act", "rew", "val", "pol", "mask", "player", "team", "discount", "idx"):
+            setattr(t, k, self.buffers[k].data_ptr())
+        t.max_steps = self.T
+        ch = _L.MuzTrajChance()
+        ch.dice, ch.dice_dist = self.buffers["dice"].data_ptr(), self.buffers["dice_dist"].data_ptr()
+        st = _L.MuzSpStats()
+        _L.check(lib.muz_classic_selfplay(self.rules, self.net.w, ctypes.byref(cfg), self.state.soa(), t, ch, self.n,
+                                          _L.ptr(self.workspace), _L.nbytes(self.workspace),
+                                          ctypes.byref(st) if timing else None, _L.stream_ptr(stream)),
+                 "muz_classic_selfplay")
+        self.last_stats = {"turns": st.turns, "searches": st.searches, "search_ms": st.search_ms,
+                           "total_ms": st.total_ms} if timing else None
+        self.last_turns = st.turns if timing else -1
+        return self.buffers
+
+
+def play_n_games_v3(net: ST.DeviceClassicNet, seed: int, num_envs: int, num_simulation: int, max_depth: int,
+                    max_steps: int, temp: float) -> dict:
+    """game_agent_stochastic.py:234-257 (the reset seeds only feed jax's unused random start)."""
+    eng = StochasticSelfPlayEngine(net, num_envs, max_steps=max_steps, num_simulations=num_simulation,
+                                   max_depth=max_depth)
+    return eng.play(seed, temp)

@@ -147,6 +147,10 @@ class MuzSample(ctypes.Structure):
                 ("masks", vp), ("target_values", vp), ("discount_targets", vp)]
 
 
+class MuzTrajChance(ctypes.Structure):
+    _fields_ = [("dice", vp), ("dice_dist", vp)]
+
+
 class MuzSpStats(ctypes.Structure):
     _fields_ = [("turns", ctypes.c_int32), ("searches", ctypes.c_int64), ("search_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double)]
@@ -187,6 +191,11 @@ SIGNATURES = {
     "muz_stochastic_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     "muz_stochastic_search": (ctypes.c_int, [ctypes.POINTER(MuzClassicNetW), ctypes.POINTER(MuzStochCfg), vp, vp, vp,
                                              vp, vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp, vp]),
+    "muz_classic_selfplay_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32,
+                                                              ctypes.POINTER(MuzStochCfg)]),
+    "muz_classic_selfplay": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzClassicNetW),
+                                            ctypes.POINTER(MuzStochCfg), MuzClassicSoA, MuzTraj, MuzTrajChance,
+                                            ctypes.c_int32, vp, ctypes.c_int64, ctypes.POINTER(MuzSpStats), vp]),
     "muz_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzNetW), ctypes.c_void_p]),
     "muz_nets_root_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "muz_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp,

@@ -271,7 +271,7 @@ typedef struct muz_traj {
   int32_t* act;       /* [n][T]  action index, -1 on no-move turns */
   int32_t* rew;       /* [n][T]  reward class {0:-1, 1:0, 2:+1} */
   float* val;         /* [n][T]  root value (search_tree.summary().value) */
-  float* pol;         /* [n][T][24] action_weights */
+  float* pol;         /* [n][T][A] action_weights (A = 24 det, 4 classic) */
   float* mask;        /* [n][T]  1 = search turn, 0 = no-move turn */
   int32_t* player;    /* [n][T]  current player before the move */
   int32_t* team;      /* [n][T]  player % 2 with teams, else -1 */
@@ -387,6 +387,24 @@ int muz_stochastic_search(const muz_classic_net_w* w, const muz_stoch_cfg* cfg, 
                           const float* dirichlet, const float* gumbel, const int32_t* game_id, int32_t n,
                           void* workspace, int64_t workspace_bytes, int32_t* action, float* action_weights,
                           float* root_value_out, void* stream);
+
+/* Chance records of the stochastic self-play buffers (game_agent_stochastic.py:165-172). */
+typedef struct muz_traj_chance {
+  int32_t* dice;      /* [n][T]     die of the turn (1..6) */
+  float* dice_dist;   /* [n][T][6]  dice_probabilities of the state AFTER the turn (line 162) */
+} muz_traj_chance;
+
+int64_t muz_classic_selfplay_workspace_bytes(int32_t n, int32_t obs_channels, const muz_stoch_cfg* cfg /*host*/);
+
+/* play_n_games_v3 + play_batch_of_games_jitted of MuZero_Classic_MADN/game_agent_stochastic.py:52-257:
+ * reset n games, then per turn throw the die (counter RNG: uniform(seed, game, turn) through throw_die),
+ * search games with a legal pin (run_stochastic_muzero_mcts with cfg; cfg->turn is set per turn), step or
+ * no_step, and record obs / act / rew class / root value / visit policy [n][T][4] / mask / player / team /
+ * discount class / dice / dice_dist until every game is done or max_steps turns ran. */
+int muz_classic_selfplay(const muz_rules* rules /*host*/, const muz_classic_net_w* w /*host*/,
+                         const muz_stoch_cfg* cfg /*host*/, muz_classic_soa state, muz_traj traj,
+                         muz_traj_chance chance, int32_t n, void* workspace, int64_t workspace_bytes,
+                         muz_sp_stats* stats /*host*/, void* stream);
 
 /* ---- device replay ring (MuZero_det_MADN/vec_replay_buffer.py) ------------------------------
  * The reference's VectorizedReplayBuffer keeps [capacity][T] host NumPy arrays (obs fp32, 84 GB at
