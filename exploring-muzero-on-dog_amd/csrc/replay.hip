@@ -45,7 +45,8 @@ __global__ __launch_bounds__(kRingScan) void k_ring_slots(const int32_t* idx, in
 }
 
 // One workgroup per (game, chunk of kCopySteps steps).  obs rows are C*56 bytes (multiple of 8).
-__global__ __launch_bounds__(256) void k_ring_copy(muz_ring ring, muz_traj tr, const int32_t* slot, int n) {
+__global__ __launch_bounds__(256) void k_ring_copy(muz_ring ring, muz_traj tr, muz_traj_chance ch, const int32_t* slot,
+                                                   int n) {
   const int g = blockIdx.y;
   const int s = slot[g];
   if (s < 0) return;
@@ -74,7 +75,11 @@ __global__ __launch_bounds__(256) void k_ring_copy(muz_ring ring, muz_traj tr, c
     ring.player[dst_row + t] = tr.player[src_row + t];
     ring.team[dst_row + t] = tr.team[src_row + t];
     ring.discount[dst_row + t] = tr.discount[src_row + t];
+    if (ring.dice) ring.dice[dst_row + t] = ch.dice[src_row + t];
   }
+  if (ring.dice_dist)
+    for (int i = threadIdx.x; i < (t1 - t0) * 6; i += blockDim.x)
+      ring.dice_dist[(dst_row + t0) * 6 + i] = ch.dice_dist[(src_row + t0) * 6 + i];
   if (blockIdx.x == 0 && threadIdx.x == 0) ring.ep_len[s] = L;
 }
 
@@ -111,10 +116,15 @@ __global__ __launch_bounds__(256) void k_ring_sample(muz_ring ring, const int32_
       o.actions[(size_t)b * (K - 1) + k] = valid ? ring.act[row + sc] : 0;
       o.rewards[(size_t)b * (K - 1) + k] = valid ? ring.rew[row + sc] : 1;
       o.discount_targets[(size_t)b * (K - 1) + k] = valid ? ring.discount[row + sc] : 1;
+      if (o.dice_outcomes && ring.dice)   // dice index 0..5; padding 0 (vec_replay_buffer_stochastic.py:266, 280)
+        o.dice_outcomes[(size_t)b * (K - 1) + k] = valid ? max(ring.dice[row + sc] - 1, 0) : 0;
+      if (o.dice_probs && ring.dice_dist)
+        for (int i = 0; i < 6; ++i)
+          o.dice_probs[((size_t)b * (K - 1) + k) * 6 + i] = valid ? ring.dice_dist[(row + sc) * 6 + i] : 1.0f / 6.0f;
     }
     // value target (7.3 - 7.7)
     double z = 0.0;
-    if (f_rew == 2) z = (tm == -1) ? (f_pl == pl ? 1.0 : -1.0) : (f_tm == tm ? 1.0 : -1.0);
+    if (ring.won_if_positive ? f_rew > 0 : f_rew == 2) z = (tm == -1) ? (f_pl == pl ? 1.0 : -1.0) : (f_tm == tm ? 1.0 : -1.0);
     const int steps = L - 1 - sq;
     const bool boot_from_value = steps >= TD;
     const int bi = min(sq + TD, L - 1);
@@ -135,9 +145,12 @@ using namespace muz;
 
 extern "C" {
 
-int muz_ring_save(muz_ring ring, muz_traj traj, int32_t n, int32_t position, int32_t* slot_out, int32_t* count_out,
-                  void* stream) {
+int muz_ring_save(muz_ring ring, muz_traj traj, const muz_traj_chance* chance, int32_t n, int32_t position,
+                  int32_t* slot_out, int32_t* count_out, void* stream) {
   MUZ_HOST_CHECK(n >= 0 && slot_out && count_out && traj.idx && traj.obs && ring.obs && ring.ep_len);
+  MUZ_HOST_CHECK((ring.dice == nullptr) == (ring.dice_dist == nullptr));
+  MUZ_HOST_CHECK(!ring.dice || (chance && chance->dice && chance->dice_dist));
+  const muz_traj_chance ch = chance ? *chance : muz_traj_chance{nullptr, nullptr};
   MUZ_HOST_CHECK(ring.capacity > 0 && position >= 0 && position < ring.capacity);
   MUZ_HOST_CHECK(traj.max_steps > 0 && traj.max_steps <= ring.max_steps);
   MUZ_HOST_CHECK(ring.obs_channels > 0 && ring.num_actions > 0);
@@ -146,7 +159,7 @@ int muz_ring_save(muz_ring ring, muz_traj traj, int32_t n, int32_t position, int
   int rc = muz_last_launch_error();
   if (rc || n == 0) return rc;
   dim3 grid((traj.max_steps + kCopySteps - 1) / kCopySteps, n);
-  k_ring_copy<<<grid, 256, 0, s>>>(ring, traj, slot_out, n);
+  k_ring_copy<<<grid, 256, 0, s>>>(ring, traj, ch, slot_out, n);
   return muz_last_launch_error();
 }
 

@@ -139,12 +139,14 @@ class MuzTraj(ctypes.Structure):
 class MuzRing(ctypes.Structure):
     _fields_ = [("obs", vp), ("act", vp), ("rew", vp), ("val", vp), ("pol", vp), ("mask", vp), ("player", vp),
                 ("team", vp), ("discount", vp), ("ep_len", vp), ("capacity", ctypes.c_int32),
-                ("max_steps", ctypes.c_int32), ("obs_channels", ctypes.c_int32), ("num_actions", ctypes.c_int32)]
+                ("max_steps", ctypes.c_int32), ("obs_channels", ctypes.c_int32), ("num_actions", ctypes.c_int32),
+                ("won_if_positive", ctypes.c_int32), ("dice", vp), ("dice_dist", vp)]
 
 
 class MuzSample(ctypes.Structure):
     _fields_ = [("observations", vp), ("actions", vp), ("rewards", vp), ("policies", vp), ("values", vp),
-                ("masks", vp), ("target_values", vp), ("discount_targets", vp)]
+                ("masks", vp), ("target_values", vp), ("discount_targets", vp), ("dice_outcomes", vp),
+                ("dice_probs", vp)]
 
 
 class MuzTrajChance(ctypes.Structure):
@@ -178,7 +180,7 @@ SIGNATURES = {
     "muz_classic_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_tile_waves": (ctypes.c_int32, []),
-    "muz_ring_save": (ctypes.c_int, [MuzRing, MuzTraj, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]),
+    "muz_ring_save": (ctypes.c_int, [MuzRing, MuzTraj, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]),
     "muz_ring_sample": (ctypes.c_int, [MuzRing, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                        vp, MuzSample, vp]),
     "muz_classic_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzClassicNetW), vp]),

@@ -17,6 +17,8 @@ in HBM: capacity 20000 x T 550 x C 34 needs 21 GB instead of the reference's 84 
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -70,7 +72,14 @@ class VectorizedReplayBuffer:
         r.ep_len = self.episode_lengths.data_ptr()
         r.capacity, r.max_steps = self.capacity, self.max_episode_length
         r.obs_channels, r.num_actions = self.obs_shape[0], self.action_dim
+        r.won_if_positive = 0
         return r
+
+    def _chance(self, b: dict):
+        return None
+
+    def _extra_outputs(self, B, K, z):
+        return {}
 
     @staticmethod
     def _traj(b: dict) -> _L.MuzTraj:
@@ -87,8 +96,10 @@ class VectorizedReplayBuffer:
         if b["obs"].dtype != torch.int8 or tuple(b["obs"].shape[2:]) != self.obs_shape:
             raise ValueError("expected int8 observations of shape [n, T, C, 56]")
         slots = torch.empty((n,), dtype=torch.int32, device=self.device)
-        _L.check(_L.load().muz_ring_save(self.ring(), self._traj(b), n, self.position, _L.ptr(slots),
-                                         _L.ptr(self._count), _L.stream_ptr()), "muz_ring_save")
+        ch = self._chance(b)
+        _L.check(_L.load().muz_ring_save(self.ring(), self._traj(b), None if ch is None else ctypes.byref(ch), n,
+                                         self.position, _L.ptr(slots), _L.ptr(self._count), _L.stream_ptr()),
+                 "muz_ring_save")
         count = int(self._count.item())
         sl = slots.cpu().numpy()
         lens = b["idx"].cpu().numpy()
@@ -128,6 +139,7 @@ class VectorizedReplayBuffer:
             "target_values": torch.empty((B, K), dtype=torch.float32, **z),
             "discount_targets": torch.empty((B, K - 1), dtype=torch.int32, **z),
         }
+        out.update(self._extra_outputs(B, K, z))
         s = _L.MuzSample()
         for k in out:
             setattr(s, k, out[k].data_ptr())
@@ -142,3 +154,33 @@ class VectorizedReplayBuffer:
         """vec_replay_buffer.py:63-264."""
         ep, t = self.draw_indices()
         return self.sample_at(ep, t)
+
+
+class VectorizedReplayBufferStochastic(VectorizedReplayBuffer):
+    """MuZero_Classic_MADN/vec_replay_buffer_stochastic.py:10-297 on device: the det ring plus the dice
+    outcomes / distributions of each step; "game won" = final reward class > 0 (line 194); batches also
+    carry dice_outcomes (die - 1) and dice_probs."""
+
+    def __init__(self, capacity: int, batch_size: int, unroll_steps: int, td_steps: int, obs_shape=(11, 56),
+                 action_dim=4, max_episode_length=500, bootstrap_value_target=True, device="cuda", rng=None):
+        super().__init__(capacity, batch_size, unroll_steps, td_steps, obs_shape, action_dim, max_episode_length,
+                         bootstrap_value_target, device, rng)
+        self.actions.fill_(-1)
+        cap, T = self.capacity, self.max_episode_length
+        self.dice_outcomes = torch.full((cap, T), -1, dtype=torch.int32, device=self.device)
+        self.dice_distributions = torch.zeros((cap, T, 6), dtype=torch.float32, device=self.device)
+
+    def ring(self) -> _L.MuzRing:
+        r = super().ring()
+        r.won_if_positive = 1
+        r.dice, r.dice_dist = self.dice_outcomes.data_ptr(), self.dice_distributions.data_ptr()
+        return r
+
+    def _chance(self, b: dict):
+        ch = _L.MuzTrajChance()
+        ch.dice, ch.dice_dist = b["dice"].data_ptr(), b["dice_dist"].data_ptr()
+        return ch
+
+    def _extra_outputs(self, B, K, z):
+        return {"dice_outcomes": torch.empty((B, K - 1), dtype=torch.int32, **z),
+                "dice_probs": torch.empty((B, K - 1, 6), dtype=torch.float32, **z)}

@@ -426,6 +426,10 @@ typedef struct muz_ring {
   int32_t max_steps;  /* T (= the trajectory buffers' max_steps) */
   int32_t obs_channels;
   int32_t num_actions;
+  /* VectorizedReplayBufferStochastic (MuZero_Classic_MADN/vec_replay_buffer_stochastic.py): */
+  int32_t won_if_positive;  /* 1: "game won" is final reward class > 0 (stochastic buffer, line 194), 0: == 2 */
+  int32_t* dice;            /* [cap][T] or null (det) */
+  float* dice_dist;         /* [cap][T][6] or null */
 } muz_ring;
 
 /* A training batch, sample_batch's return dict (vec_replay_buffer.py:256-264), K = unroll_steps + 1. */
@@ -438,14 +442,16 @@ typedef struct muz_sample {
   float* masks;               /* [B][K] */
   float* target_values;       /* [B][K] */
   int32_t* discount_targets;  /* [B][K-1] */
+  int32_t* dice_outcomes;     /* [B][K-1] die - 1, 0 when padded (stochastic buffer); null = not produced */
+  float* dice_probs;          /* [B][K-1][6] dice distribution, uniform when padded; null = not produced */
 } muz_sample;
 
 /* save_games_from_buffers (vec_replay_buffer.py:36-61): game i with traj.idx[i] > 0 goes to ring slot
  * (position + r_i) % capacity, r_i = number of such games before i (later games win a slot that wraps
  * twice, as in the sequential loop).  slot_out[i] (device int32[n], required) = its slot or -1;
  * count_out (device int32[1]) = number of games with idx > 0 (the host advances position / size). */
-int muz_ring_save(muz_ring ring, muz_traj traj, int32_t n, int32_t position, int32_t* slot_out, int32_t* count_out,
-                  void* stream);
+int muz_ring_save(muz_ring ring, muz_traj traj, const muz_traj_chance* chance /*host, null for det*/, int32_t n,
+                  int32_t position, int32_t* slot_out, int32_t* count_out, void* stream);
 
 /* sample_batch (vec_replay_buffer.py:63-264) for given episode / start indices (the reference draws them
  * with np.random; the host mirror draws them the same way).  gamma_pow (device double[max_steps + 1]) =

@@ -87,6 +87,9 @@ class VectorizedReplayBuffer:
 
     def sample_at(self, ep_indices, t_starts):
         """The deterministic part of sample_batch (vec_replay_buffer.py:101-264) for given indices."""
+        return self._sample_common(ep_indices, t_starts, won=lambda fr: fr == 2)
+
+    def _sample_common(self, ep_indices, t_starts, won):
         K = self.unroll_steps + 1
         TD = self.td_steps
         B = ep_indices.shape[0]
@@ -108,7 +111,7 @@ class VectorizedReplayBuffer:
         discount_targets = self.discounts[epb[:, :-1], seqc[:, :-1]]
         seq_players = self.players[epb, seqc]
         seq_teams = self.teams[epb, seqc]
-        won = final_rewards[:, None] == 2
+        won = won(final_rewards[:, None])
         single = seq_teams == -1
         z = np.where(won, np.where(single, np.where(final_players[:, None] == seq_players, 1.0, -1.0),
                                    np.where(final_teams[:, None] == seq_teams, 1.0, -1.0)), 0.0)
@@ -139,3 +142,46 @@ class VectorizedReplayBuffer:
         """vec_replay_buffer.py:63-264."""
         ep, t = self.draw_indices()
         return self.sample_at(ep, t)
+
+
+class VectorizedReplayBufferStochastic(VectorizedReplayBuffer):
+    """MuZero_Classic_MADN/vec_replay_buffer_stochastic.py:10-297: the det buffer plus dice outcomes and
+    dice distributions, "game won" = final reward class > 0 (line 194, a quirk kept as is), and the
+    batch keys dice_outcomes (die - 1, padding 0) / dice_probs (padding uniform)."""
+
+    def __init__(self, capacity, batch_size, unroll_steps, td_steps, obs_shape=(11, 56), action_dim=4,
+                 max_episode_length=500, bootstrap_value_target=True, rng=None):
+        super().__init__(capacity, batch_size, unroll_steps, td_steps, obs_shape, action_dim, max_episode_length,
+                         bootstrap_value_target, rng)
+        self.actions[:] = -1
+        self.dice_outcomes = np.full((capacity, max_episode_length), -1, dtype=np.int32)
+        self.dice_distributions = np.zeros((capacity, max_episode_length, 6), dtype=np.float32)
+
+    def save_games_from_buffers(self, b):
+        lengths = np.asarray(b["idx"])
+        pos0 = self.position
+        slots = []
+        for i in range(lengths.shape[0]):
+            if int(lengths[i]) > 0:
+                slots.append((i, (pos0 + len(slots)) % self.capacity))
+        super().save_games_from_buffers(b)
+        for i, pos in slots:
+            L = int(lengths[i])
+            self.dice_outcomes[pos, :L] = np.asarray(b["dice"][i, :L])
+            self.dice_distributions[pos, :L] = np.asarray(b["dice_dist"][i, :L])
+
+    def sample_at(self, ep_indices, t_starts):
+        out = self._sample_common(ep_indices, t_starts, won=lambda fr: fr > 0)
+        K = self.unroll_steps + 1
+        ep_lengths = self.episode_lengths[ep_indices]
+        seq = t_starts[:, None] + np.arange(K)[None, :]
+        valid = seq < ep_lengths[:, None]
+        seqc = np.minimum(seq, ep_lengths[:, None] - 1)
+        epb = np.broadcast_to(ep_indices[:, None], seq.shape)
+        dice = self.dice_outcomes[epb[:, :-1], seqc[:, :-1]]
+        dice = np.where(valid[:, :-1], dice, 0)
+        probs = np.where(valid[:, :-1, None], self.dice_distributions[epb[:, :-1], seqc[:, :-1]],
+                         np.full(6, 1.0 / 6.0, dtype=np.float32))
+        out["dice_outcomes"] = np.maximum(dice - 1, 0).astype(np.int32)
+        out["dice_probs"] = probs.astype(np.float32)
+        return out

@@ -85,3 +85,29 @@ def test_ring_with_selfplay_buffers(cuda):
         ora.save_games_from_buffers(host)
     assert_ring_equal(dev, ora)
     assert_sample_equal(dev.sample_batch(), ora.sample_batch())
+
+
+def test_stochastic_ring_with_classic_selfplay(cuda):
+    """vec_replay_buffer_stochastic.py: dice outcomes / distributions, the `final reward class > 0` rule."""
+    from oracle import classic_madn as cm
+    from oracle import classic_nets as CN
+    from oracle.replay import VectorizedReplayBufferStochastic as OracleRBS
+    from exploring_muzero_on_dog_amd import game_agent_stochastic as GS
+    from exploring_muzero_on_dog_amd import stochastic as S
+    R = _R()
+    C = cm.num_channels(4)
+    net = S.DeviceClassicNet(CN.init_params(C, seed=4), C)
+    eng = GS.StochasticSelfPlayEngine(net, 24, max_steps=90, num_simulations=8, max_depth=6)
+    bufs = eng.play(seed=9)
+    host = {k: v.cpu().numpy() for k, v in bufs.items()}
+    dev = R.VectorizedReplayBufferStochastic(30, 64, 10, 20, obs_shape=(C, 56), max_episode_length=90,
+                                             rng=np.random.RandomState(2))
+    ora = OracleRBS(30, 64, 10, 20, obs_shape=(C, 56), max_episode_length=90, rng=np.random.RandomState(2))
+    for _ in range(2):                                          # 48 games into 30 slots: wraps
+        dev.save_games_from_buffers(bufs)
+        ora.save_games_from_buffers(host)
+    assert_ring_equal(dev, ora)
+    assert np.array_equal(dev.dice_outcomes.cpu().numpy()[:, :90][ora.episode_lengths[:, None] > np.arange(90)],
+                          ora.dice_outcomes[ora.episode_lengths[:, None] > np.arange(90)])
+    for _ in range(2):
+        assert_sample_equal(dev.sample_batch(), ora.sample_batch())
