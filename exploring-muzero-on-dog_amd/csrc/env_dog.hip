@@ -1,0 +1,592 @@
+// Batched DOG environment kernels + C ABI (include/muz.h).  One wavefront per game, 4 games per
+// 256-thread workgroup; the game's state is staged in LDS (dog.hpp: DogG).
+#include "dog.hpp"
+#include "host_consts.hpp"
+
+namespace muz {
+
+constexpr int kDogGamesPerBlock = 4;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- SoA <-> LDS ---------------------------------------------------------------------------------
+__device__ __forceinline__ void dog_load(const DetConsts& c, const muz_dog_soa& st, int g, DogG& s, int lane) {
+  const int S = st.stride;
+  for (int i = lane; i < kCells; i += 64) s.board[i] = st.board[i * S + g];
+  if (lane < 16) s.pins[lane] = lane < c.P * 4 ? st.pins[lane * S + g] : (int8_t)-1;
+  for (int i = lane; i < 4 * kDogCards; i += 64) s.hands[i / kDogCards][i % kDogCards] = i < c.P * kDogCards ? st.hands[i * S + g] : 0;
+  if (lane < kDogCards) s.deck[lane] = st.deck[lane * S + g];
+  if (lane < 4) s.swap_choices[lane] = st.swap_choices[lane * S + g];
+  if (lane == 0) {
+    s.cp = st.current_player[g];
+    s.round_starter = st.round_starter[g];
+    s.phase = st.phase[g];
+    s.hand_size = st.hand_size[g];
+    s.done = st.done[g] ? 1 : 0;
+    s.reward = st.reward[g];
+    s.deal = st.deal[g];
+  }
+  wave_sync();
+}
+
+__device__ __forceinline__ void dog_store(const DetConsts& c, const muz_dog_soa& st, int g, const DogG& s, int lane) {
+  wave_sync();
+  const int S = st.stride;
+  for (int i = lane; i < kCells; i += 64) st.board[i * S + g] = s.board[i];
+  if (lane < c.P * 4) st.pins[lane * S + g] = s.pins[lane];
+  for (int i = lane; i < c.P * kDogCards; i += 64) st.hands[i * S + g] = s.hands[i / kDogCards][i % kDogCards];
+  if (lane < kDogCards) st.deck[lane * S + g] = s.deck[lane];
+  if (lane < 4) st.swap_choices[lane * S + g] = s.swap_choices[lane];
+  if (lane == 0) {
+    st.current_player[g] = (int8_t)s.cp;
+    st.round_starter[g] = (int8_t)s.round_starter;
+    st.phase[g] = (int8_t)s.phase;
+    st.hand_size[g] = (int8_t)s.hand_size;
+    st.done[g] = (uint8_t)s.done;
+    st.reward[g] = (int8_t)s.reward;
+    st.deal[g] = s.deal;
+  }
+}
+
+// ---- distribute_cards (dog.py:201-298), all lanes ---------------------------------------------------
+__device__ __forceinline__ float deal_key(unsigned long long seed, int gid, unsigned deal, int k) {
+  return u24(mix64(game_key(seed ^ kDealStream, gid, (int)deal) ^ (unsigned long long)(k + 1) * 0xA24BAED4963EE407ull));
+}
+
+__device__ void dog_deal(const DetConsts& c, DogG& s, unsigned long long seed, int gid, int lane) {
+  const int P = c.P;
+  const int q = s.hand_size;
+  if (lane == 0) {
+    int tot = 0;
+    for (int k = 0; k < kDogCards; ++k) tot += s.deck[k];
+    if (tot < q * P) {   // reset_deck (dog.py:188-191): card 0 gets 6 + 2 * (joker enabled)
+      for (int k = 0; k < kDogCards; ++k) s.deck[k] = 8;
+      s.deck[0] = 8;
+    }
+    int p = 0;
+    for (int k = 0; k < kDogCards; ++k)
+      for (int j = 0; j < s.deck[k] && p < kMaxPool; ++j) s.pool[p++] = (int8_t)k;
+    for (; p < kMaxPool; ++p) s.pool[p] = (int8_t)kDogCards;   // dummies
+  }
+  wave_sync();
+  for (int k = lane; k < kMaxPool; k += 64) s.key[k] = s.pool[k] == kDogCards ? 2.0f : deal_key(seed, gid, s.deal, k);
+  wave_sync();
+  // stable argsort: rank = #smaller keys + #equal keys at a lower index
+  for (int k = lane; k < kMaxPool; k += 64) {
+    const float kk = s.key[k];
+    int r = 0;
+    for (int j = 0; j < kMaxPool; ++j) {
+      const float kj = s.key[j];
+      r += (kj < kk) || (kj == kk && j < k);
+    }
+    s.shuffled[r] = s.pool[k];
+  }
+  wave_sync();
+  if (lane == 0) {
+    for (int p = 0; p < P; ++p)
+      for (int sl = 0; sl < q && sl < 6; ++sl) {
+        const int card = s.shuffled[p * q + sl];
+        if (card < kDogCards) {
+          s.hands[p][card] = (int8_t)(s.hands[p][card] + 1);
+          s.deck[card] = (int8_t)(s.deck[card] - 1);
+        }
+      }
+    const int rs = s.round_starter == -1 ? s.cp : (s.round_starter + 1) % P;
+    s.cp = rs;
+    s.round_starter = rs;
+    for (int i = 0; i < 4; ++i) s.swap_choices[i] = -1;
+    s.phase = (has(c.flags, R_TEAMS) && P == 4) ? 1 : 0;
+    s.hand_size = q == 2 ? 6 : q - 1;
+    s.deal = s.deal + 1;
+  }
+  wave_sync();
+}
+
+// ---- transitions (lane 0) ---------------------------------------------------------------------------
+__device__ __forceinline__ void dog_rebuild(const DetConsts& c, DogG& s) {
+  for (int i = 0; i < kCells; ++i) s.board[i] = -1;
+  for (int p = 0; p < c.P; ++p)
+    for (int k = 0; k < 4; ++k) {
+      const int pos = s.pins[p * 4 + k];
+      if (pos >= 0 && pos < kCells) s.board[pos] = (int8_t)p;
+    }
+}
+
+// winner / reward / done of a step_* function (dog.py:782-786 ...)
+__device__ __forceinline__ void dog_finish(const DetConsts& c, const DogG& s, int cp, bool invalid, int& reward,
+                                           int& done) {
+  const uint32_t w = dog_winners(c, s.board);
+  done = (s.done || w) ? 1 : 0;
+  reward = s.done ? 0 : (invalid ? -1 : (int)((w >> cp) & 1u));
+}
+
+__device__ void dog_step_swap(const DetConsts& c, DogG& s, int cp, int pin, int pos, int& reward, int& done) {
+  const bool invalid = !dog_val_swap(c, s, cp, pin, pos);
+  if (!invalid) {
+    const int sp = s.board[pos];
+    const int pp = s.pins[cp * 4 + pin];
+    s.board[pos] = (int8_t)cp;
+    s.board[pp] = (int8_t)sp;
+    s.pins[cp * 4 + pin] = (int8_t)pos;
+    for (int k = 0; k < 4; ++k)
+      if (s.pins[sp * 4 + k] == pos) s.pins[sp * 4 + k] = (int8_t)pp;
+  }
+  dog_finish(c, s, cp, invalid, reward, done);
+}
+
+__device__ void dog_capture_move(const DetConsts& c, DogG& s, int cp, int pin, int npos, bool invalid, int& reward,
+                                 int& done) {
+  if (!invalid) {
+    const int at = s.board[jidx(npos, kCells)];
+    if (at != -1 && (at != cp || has(c.flags, R_FRIENDLY)))
+      for (int k = 0; k < 4; ++k)
+        if (s.pins[at * 4 + k] == npos) s.pins[at * 4 + k] = -1;
+    s.pins[cp * 4 + pin] = (int8_t)npos;
+    dog_rebuild(c, s);
+  }
+  dog_finish(c, s, cp, invalid, reward, done);
+}
+
+__device__ void dog_step_normal(const DetConsts& c, DogG& s, int cp, int pin, int move, int& reward, int& done) {
+  const uint32_t F = c.flags;
+  const bool invalid = !dog_val_normal(c, s, cp, pin, move);
+  const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
+  const int tgt = cst(c.target, cp);
+  const int g0 = dgoal(c, cp, 0);
+  const int cur = s.pins[cp * 4 + pin];
+  const int moved = cur + move;
+  const int fitted = fmodp(moved, kTrack);
+  const int x = moved - tgt - mt;
+  const bool ing = in_goal_p(c, cp, cur);
+  const bool a = ing ? dog_goal_free(c, s.board, cp, cur - g0, moved - g0 + 1) : dog_goal_free(c, s.board, cp, -1, x);
+  const int gx = dgoal(c, cp, jidx(x - 1, 4));
+  const bool A = (s.board[gx] != cp) && (has(F, R_JUMP_GOAL) || a);
+  int npos;
+  if (cur == -1)
+    npos = cst(c.start, cp);
+  else if (ing)
+    npos = moved;
+  else if (4 >= x && x > 0 && A && cur <= tgt)
+    npos = gx;
+  else
+    npos = fitted;
+  dog_capture_move(c, s, cp, pin, npos, invalid, reward, done);
+}
+
+__device__ void dog_step_neg(const DetConsts& c, DogG& s, int cp, int pin, int& reward, int& done, int move = -4) {
+  const bool invalid = !dog_val_neg(c, s, cp, pin, move);
+  dog_capture_move(c, s, cp, pin, fmodp(s.pins[cp * 4 + pin] + move, kTrack), invalid, reward, done);
+}
+
+// path bits [si, ei] (wrap when si > ei) inside [0, N); empty for a pin at home or not moving
+__device__ __forceinline__ unsigned long long path_bits(int si, int ei, int N, bool same_area) {
+  if (si == -1 || ei == -1 || (same_area && si == ei)) return 0ull;
+  const unsigned long long full = N >= 64 ? ~0ull : ((1ull << N) - 1ull);
+  auto ge = [&](int a) { return a <= 0 ? full : (a >= N ? 0ull : (full & ~((1ull << a) - 1ull))); };   // idx >= a
+  auto le = [&](int b) { return b < 0 ? 0ull : (b >= N - 1 ? full : ((1ull << (b + 1)) - 1ull)); };    // idx <= b
+  return si <= ei ? (ge(si) & le(ei)) : (ge(si) | le(ei));
+}
+
+__device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d)[4], int& reward, int& done) {
+  const uint32_t F = c.flags;
+  const bool invalid = !dog_val7(c, s, cp, d);
+  const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
+  const int tgt = cst(c.target, cp);
+  int cur[4], moved[4], npos[4];
+  bool ing[4];
+  for (int k = 0; k < 4; ++k) {
+    cur[k] = s.pins[cp * 4 + k];
+    moved[k] = cur[k] + d[k];
+    ing[k] = in_goal_p(c, cp, cur[k]);
+  }
+  bool occ[4];
+  for (int g = 0; g < 4; ++g) {
+    bool o = false;
+    for (int k = 0; k < 4; ++k) o |= (ing[k] ? moved[k] : cur[k]) == dgoal(c, cp, g);
+    occ[g] = o;
+  }
+  for (int k = 0; k < 4; ++k) {
+    const int x = moved[k] - tgt - mt;
+    bool a = true;
+    if (!ing[k])
+      for (int g = 0; g < 4; ++g)
+        if (-1 < g && g < x) a &= !occ[g];
+    const bool A = has(F, R_JUMP_GOAL) || a;
+    if (cur[k] == -1)
+      npos[k] = -1;
+    else if (ing[k])
+      npos[k] = moved[k];
+    else if (4 >= x && x > 0 && A && cur[k] <= tgt)
+      npos[k] = dgoal(c, cp, jidx(x - 1, 4));
+    else
+      npos[k] = fmodp(moved[k], kTrack);
+  }
+  // get_path_matrix (utils 237-303), rows as 56-bit masks
+  unsigned long long row[4];
+  bool cross = false;
+  const int g0 = dgoal(c, cp, 0);
+  for (int k = 0; k < 4; ++k) {
+    const bool A0 = in_goal_p(c, cp, cur[k]), B0 = in_goal_p(c, cp, npos[k]);
+    cross |= A0 != B0;
+    row[k] = (A0 == B0) ? path_bits(cur[k], npos[k], kTrack, true)
+                        : (path_bits(cur[k], tgt, kTrack, false) | path_bits(g0, npos[k], kCells, false));
+  }
+  if (cross)
+    for (int k = 0; k < 4; ++k) row[k] |= 1ull << cst(c.start, cp);
+  const unsigned long long anyp = row[0] | row[1] | row[2] | row[3];
+  if (!invalid) {
+    bool hit[16];
+    for (int p = 0; p < c.P; ++p)
+      for (int k = 0; k < 4; ++k) hit[p * 4 + k] = (anyp >> jidx(s.pins[p * 4 + k], kCells)) & 1ull;
+    for (int k = 0; k < 4; ++k) {
+      unsigned long long other = 0;
+      for (int j = 0; j < 4; ++j)
+        if (j != k) other |= row[j];
+      hit[cp * 4 + k] = ((other >> jidx(cur[k], kCells)) & 1ull) && ((other >> jidx(npos[k], kCells)) & 1ull);
+    }
+    for (int k = 0; k < 4; ++k) s.pins[cp * 4 + k] = (int8_t)npos[k];
+    for (int j = 0; j < c.P * 4; ++j)
+      if (hit[j]) s.pins[j] = -1;
+    dog_rebuild(c, s);
+  }
+  dog_finish(c, s, cp, invalid, reward, done);
+}
+
+// next player holding cards after the UNSUBSTITUTED current player (fori_loop of dog.py:1042-1046)
+__device__ __forceinline__ int dog_next_with_cards(const DetConsts& c, const DogG& s, int& total) {
+  int nxt = -1;
+  total = 0;
+  for (int p = 0; p < c.P; ++p) {
+    int h = 0;
+    for (int k = 0; k < kDogCards; ++k) h += s.hands[p][k];
+    total += h;
+  }
+  for (int i = 0; i < c.P; ++i) {
+    const int cand = (s.cp + i + 1) % c.P;
+    int h = 0;
+    for (int k = 0; k < kDogCards; ++k) h += s.hands[cand][k];
+    if (nxt == -1 && h > 0) nxt = cand;
+  }
+  return nxt;
+}
+
+// env_step (dog.py:1117-1131) on lane 0; returns 1 when a deal must follow.
+__device__ int dog_env_step(const DetConsts& c, DogG& s, int action, int& reward, int& done) {
+  if (s.phase == 1) {   // env_step_swap_phase (1077-1114): no validity check
+    const int card = action - kDogPlay;
+    const int cp0 = s.cp;
+    const int ci = card < 0 ? card + kDogCards : card;   // .at[cp, card].add(-1): normalise once, drop OOB
+    if (ci >= 0 && ci < kDogCards) s.hands[cp0][ci] = (int8_t)(s.hands[cp0][ci] - 1);
+    s.swap_choices[cp0] = (int8_t)card;                   // jnp.int8(card_idx) wraps
+    const int nxt = (cp0 + 1) % c.P;
+    if (nxt == s.round_starter) {
+      const int partner[4] = {2, 3, 0, 1};
+      for (int p = 0; p < c.P; ++p) {
+        const int rc = s.swap_choices[partner[p]];
+        if (rc >= 0 && rc < kDogCards) s.hands[p][rc] = (int8_t)(s.hands[p][rc] + 1);
+      }
+      for (int i = 0; i < 4; ++i) s.swap_choices[i] = -1;
+      s.phase = 0;
+      s.cp = s.round_starter;
+    } else {
+      s.cp = nxt;
+    }
+    s.reward = 0;
+    reward = 0;
+    done = s.done;
+    return 0;
+  }
+  // env_step_play_phase (986-1062)
+  const int cp = dog_sub(c, s);
+  const bool joker = action < kDogBase;
+  const int act = ((action % kDogBase) + kDogBase) % kDogBase;
+  const int card = joker ? 0 : dog_base_card(act);
+  if (s.hands[cp][card] <= 0) {
+    reward = -1;
+    done = s.done;
+  } else if (act < kDogSwaps) {
+    dog_step_swap(c, s, cp, act / kCells, act % kCells, reward, done);
+  } else if (act < kDogNormalBase) {
+    int d[4];
+    for (int k = 0; k < 4; ++k) d[k] = c_dists7[act - kDogSwaps][k];
+    dog_step_hot7(c, s, cp, d, reward, done);
+  } else if (act < kDogNegBase) {
+    const int na = act - kDogNormalBase;
+    int mv = na % 12 + 1;
+    mv += mv >= 7 ? 1 : 0;
+    dog_step_normal(c, s, cp, na / 12, mv, reward, done);
+  } else {
+    dog_step_neg(c, s, cp, act - kDogNegBase, reward, done);
+  }
+  if (reward != -1) s.hands[cp][card] = (int8_t)(s.hands[cp][card] - 1);
+  int total;
+  const int nxt = dog_next_with_cards(c, s, total);
+  s.cp = done ? cp : nxt;
+  s.reward = reward;
+  s.done = done;
+  return ((total == 0 || nxt == -1) && !done) ? 1 : 0;
+}
+
+// no_step (dog.py:713-752) on lane 0; returns 1 when a deal must follow.
+__device__ int dog_no_step(const DetConsts& c, DogG& s) {
+  for (int k = 0; k < kDogCards; ++k) s.hands[s.cp][k] = 0;
+  int total;
+  const int nxt = dog_next_with_cards(c, s, total);
+  if (total > 0 && nxt != -1) {
+    s.cp = nxt;
+    return 0;
+  }
+  return 1;
+}
+
+// ---- kernels ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dog_reset(DetConsts c, muz_dog_soa st, unsigned long long seed, int n) {
+  __shared__ DogG sg[kDogGamesPerBlock];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = blockIdx.x * kDogGamesPerBlock + w;
+  if (g >= n) return;
+  DogG& s = sg[w];
+  const bool fp = has(c.flags, R_FREE_PIN);
+  if (lane < 16) {
+    const int p = lane / 4, k = lane % 4;
+    s.pins[lane] = (int8_t)((p < c.P) ? ((fp && k == 0) ? c.start[p] : -1) : -1);
+  }
+  for (int i = lane; i < 4 * kDogCards; i += 64) s.hands[i / kDogCards][i % kDogCards] = 0;
+  if (lane < kDogCards) s.deck[lane] = lane == 0 ? 6 : 8;   // env_reset: joker 6, others 8 (dog.py:143-145)
+  if (lane == 0) {
+    s.cp = c.starting_player;
+    s.round_starter = -1;
+    s.phase = 0;
+    s.hand_size = 6;
+    s.done = 0;
+    s.reward = 0;
+    s.deal = 0;
+  }
+  wave_sync();
+  if (lane == 0) dog_rebuild(c, s);
+  wave_sync();
+  dog_deal(c, s, seed, g, lane);
+  dog_store(c, st, g, s, lane);
+}
+
+__global__ __launch_bounds__(256) void k_dog_legal(DetConsts c, muz_dog_soa st, uint32_t* mask, int n) {
+  __shared__ DogG sg[kDogGamesPerBlock];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = blockIdx.x * kDogGamesPerBlock + w;
+  if (g >= n) return;
+  DogG& s = sg[w];
+  dog_load(c, st, g, s, lane);
+  const int cp = dog_sub(c, s);
+  if (s.phase == 0) {
+    for (int r = 0; r < 7; ++r) {
+      const int i = r * 64 + lane;
+      const bool v = i < kDogBase && dog_base_valid(c, s, cp, i);
+      const unsigned long long b = __ballot(v);
+      if (lane == 0) s.base[r] = b;
+    }
+    wave_sync();
+  }
+  uint32_t* out = mask + (size_t)g * kDogWords;
+  for (int r = 0; r < 13; ++r) {
+    const int a = r * 64 + lane;
+    bool v = false;
+    if (a < kDogActions) {
+      if (s.phase == 0) {
+        if (a < kDogPlay) {
+          const int i = a % kDogBase;
+          const bool bv = (s.base[i >> 6] >> (i & 63)) & 1ull;
+          v = bv && (a < kDogBase ? s.hands[cp][0] > 0 : s.hands[cp][dog_base_card(i)] > 0);
+        }
+      } else if (a >= kDogPlay) {
+        v = s.hands[s.cp][a - kDogPlay] > 0;
+      }
+    }
+    const unsigned long long b = __ballot(v);
+    if (lane == 0) {
+      if (2 * r < kDogWords) out[2 * r] = (uint32_t)b;
+      if (2 * r + 1 < kDogWords) out[2 * r + 1] = (uint32_t)(b >> 32);
+    }
+  }
+}
+
+// mode 0: env_step(action[g]); mode 1: no_step.  action < 0 with mode 0 = no_step as well.
+__global__ __launch_bounds__(256) void k_dog_step(DetConsts c, muz_dog_soa st, const int32_t* action, int mode,
+                                                  unsigned long long seed, int8_t* reward, uint8_t* done, int n) {
+  __shared__ DogG sg[kDogGamesPerBlock];
+  __shared__ int need_deal[kDogGamesPerBlock];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = blockIdx.x * kDogGamesPerBlock + w;
+  if (g >= n) return;
+  DogG& s = sg[w];
+  dog_load(c, st, g, s, lane);
+  if (lane == 0) {
+    int r = 0, d = s.done;
+    int deal;
+    if (mode == 1 || action[g] < 0) {
+      deal = dog_no_step(c, s);
+      r = 0;
+      d = s.done;
+    } else {
+      deal = dog_env_step(c, s, action[g], r, d);
+    }
+    need_deal[w] = deal;
+    if (reward) reward[g] = (int8_t)r;
+    if (done) done[g] = (uint8_t)d;
+  }
+  wave_sync();
+  if (need_deal[w]) dog_deal(c, s, seed, g, lane);
+  dog_store(c, st, g, s, lane);
+}
+
+// One step_* function of dog.py on its own (the form DOG/test.py calls): kind 0 step_swap(pin, pos),
+// 1 step_normal_move(pin, move), 2 step_neg_move(pin, move), 3 step_hot_7(d0..d3).  Board and pins change;
+// hands, turn and the state's reward / done fields do not (the reference returns them separately).
+__global__ __launch_bounds__(256) void k_dog_step_move(DetConsts c, muz_dog_soa st, const int32_t* kind,
+                                                       const int32_t* args, int8_t* reward, uint8_t* done, int n) {
+  __shared__ DogG sg[kDogGamesPerBlock];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = blockIdx.x * kDogGamesPerBlock + w;
+  if (g >= n) return;
+  DogG& s = sg[w];
+  dog_load(c, st, g, s, lane);
+  if (lane == 0) {
+    const int cp = dog_sub(c, s);
+    const int k = kind[g];
+    const int a0 = args[4 * g], a1 = args[4 * g + 1];
+    int r = 0, d = s.done;
+    if (k == 0) {
+      dog_step_swap(c, s, cp, a0 < 0 ? 0 : (a0 > 3 ? 3 : a0), a1 < 0 ? 0 : (a1 > kCells - 1 ? kCells - 1 : a1), r, d);
+    } else if (k == 1) {
+      dog_step_normal(c, s, cp, a0 & 3, a1, r, d);
+    } else if (k == 2) {
+      dog_step_neg(c, s, cp, a0 & 3, r, d, a1);
+    } else {
+      const int dd[4] = {args[4 * g], args[4 * g + 1], args[4 * g + 2], args[4 * g + 3]};
+      dog_step_hot7(c, s, cp, dd, r, d);
+    }
+    if (reward) reward[g] = (int8_t)r;
+    if (done) done[g] = (uint8_t)d;
+  }
+  dog_store(c, st, g, s, lane);
+}
+
+// Uniform random legal action (config (d)'s policy): the k-th set bit, k = floor(u * popcount); -1 if none.
+__global__ __launch_bounds__(256) void k_dog_random_action(const uint32_t* mask, const float* uniform,
+                                                           unsigned long long seed, int turn, int32_t* action, int n) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const uint32_t* m = mask + (size_t)g * kDogWords;
+  int tot = 0;
+  for (int i = 0; i < kDogWords; ++i) tot += __popc(m[i]);
+  if (tot == 0) {
+    action[g] = -1;
+    return;
+  }
+  const float u = uniform ? uniform[g] : u24(mix64(game_key(seed ^ 0x52A4D0DA11ull, g, turn)));
+  int k = (int)(u * (float)tot);
+  k = k >= tot ? tot - 1 : k;
+  int a = -1;
+  for (int i = 0; i < kDogWords && a < 0; ++i) {
+    const int pc = __popc(m[i]);
+    if (k < pc) {
+      uint32_t x = m[i];
+      for (int j = 0; j < k; ++j) x &= x - 1;   // drop the k lowest set bits
+      a = i * 32 + __ffs(x) - 1;
+    } else {
+      k -= pc;
+    }
+  }
+  action[g] = a;
+}
+
+static int dog_consts(const muz_rules* rules, DetConsts* c) {
+  int rc = make_det_consts(rules, c);
+  if (rc) return rc;
+  if (rules->disable_swapping || rules->disable_hot_seven || rules->disable_joker) return MUZ_E_UNSUPPORTED;
+  return MUZ_OK;
+}
+
+static int dog_tables_ready() {
+  static bool done = false;
+  if (done) return MUZ_OK;
+  int8_t t[kDogHot][4];
+  int i = 0;
+  for (int a = 0; a <= 7; ++a)
+    for (int b = 0; b <= 7; ++b)
+      for (int cc = 0; cc <= 7; ++cc) {
+        const int d = 7 - a - b - cc;
+        if (d >= 0) {
+          t[i][0] = (int8_t)a;
+          t[i][1] = (int8_t)b;
+          t[i][2] = (int8_t)cc;
+          t[i][3] = (int8_t)d;
+          ++i;
+        }
+      }
+  MUZ_HIP_RET(hipMemcpyToSymbol(HIP_SYMBOL(c_dists7), t, sizeof(t)));
+  done = true;
+  return MUZ_OK;
+}
+
+}  // namespace muz
+
+using namespace muz;
+
+static inline unsigned dog_blocks(int n) { return (unsigned)((n + kDogGamesPerBlock - 1) / kDogGamesPerBlock); }
+
+#define DOG_PROLOGUE(extra)                           \
+  DetConsts c;                                        \
+  int rc = dog_consts(rules, &c);                     \
+  if (rc) return rc;                                  \
+  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && extra);  \
+  if ((rc = dog_tables_ready())) return rc;           \
+  if (n == 0) return MUZ_OK;
+
+extern "C" {
+
+int muz_dog_reset(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int32_t n, void* stream) {
+  DOG_PROLOGUE(true)
+  k_dog_reset<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, seed, n);
+  return muz_last_launch_error();
+}
+
+int muz_dog_legal(const muz_rules* rules, muz_dog_soa st, uint32_t* mask, int32_t n, void* stream) {
+  DOG_PROLOGUE(mask != nullptr)
+  k_dog_legal<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, mask, n);
+  return muz_last_launch_error();
+}
+
+int muz_dog_step(const muz_rules* rules, muz_dog_soa st, const int32_t* action, uint64_t seed, int8_t* reward,
+                 uint8_t* done, int32_t n, void* stream) {
+  DOG_PROLOGUE(action != nullptr)
+  k_dog_step<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, action, 0, seed, reward, done, n);
+  return muz_last_launch_error();
+}
+
+int muz_dog_nostep(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int8_t* reward, uint8_t* done, int32_t n,
+                   void* stream) {
+  DOG_PROLOGUE(true)
+  k_dog_step<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, nullptr, 1, seed, reward, done, n);
+  return muz_last_launch_error();
+}
+
+int muz_dog_step_move(const muz_rules* rules, muz_dog_soa st, const int32_t* kind, const int32_t* args,
+                      int8_t* reward, uint8_t* done, int32_t n, void* stream) {
+  DOG_PROLOGUE(kind != nullptr && args != nullptr)
+  k_dog_step_move<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, kind, args, reward, done, n);
+  return muz_last_launch_error();
+}
+
+int muz_dog_random_action(const uint32_t* mask, const float* uniform, uint64_t seed, int32_t turn, int32_t* action,
+                          int32_t n, void* stream) {
+  MUZ_HOST_CHECK(n >= 0 && mask && action);
+  if (n == 0) return MUZ_OK;
+  k_dog_random_action<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(mask, uniform, seed, turn, action, n);
+  return muz_last_launch_error();
+}
+
+}  // extern "C"

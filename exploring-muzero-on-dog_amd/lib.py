@@ -37,7 +37,16 @@ class MuzRules(ctypes.Structure):
         ("enable_bonus_turn_on_6", ctypes.c_int32),
         ("must_traverse_start", ctypes.c_int32),
         ("enable_dice_rethrow", ctypes.c_int32),
+        ("disable_swapping", ctypes.c_int32),
+        ("disable_hot_seven", ctypes.c_int32),
+        ("disable_joker", ctypes.c_int32),
     ]
+
+
+class MuzDogSoA(ctypes.Structure):
+    _fields_ = [(k, vp) for k in ("board", "pins", "deck", "hands", "swap_choices", "current_player",
+                                  "round_starter", "phase", "hand_size", "reward", "done", "deal")] + [
+        ("stride", ctypes.c_int32)]
 
 
 class MuzDetSoA(ctypes.Structure):
@@ -170,6 +179,14 @@ SIGNATURES = {
     "muz_detmadn_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
+    "muz_dog_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, ctypes.c_int32, vp]),
+    "muz_dog_legal": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_int32, vp]),
+    "muz_dog_step": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_uint64, vp, vp, ctypes.c_int32,
+                                    vp]),
+    "muz_dog_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, vp, vp, ctypes.c_int32,
+                                      vp]),
+    "muz_dog_step_move": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, vp, vp, vp, ctypes.c_int32, vp]),
+    "muz_dog_random_action": (ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_int32, vp, ctypes.c_int32, vp]),
     "muz_classic_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, ctypes.c_int32, vp]),
     "muz_classic_set_die": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_dice_probs": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, ctypes.c_int32, vp]),

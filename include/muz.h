@@ -51,6 +51,9 @@ typedef struct muz_rules {
   int32_t enable_bonus_turn_on_6;
   int32_t must_traverse_start;
   int32_t enable_dice_rethrow;  /* classic only (classic_madn.py:66, dice_probabilities 208-228) */
+  int32_t disable_swapping;     /* DOG only (dog.py:83-100); the device implements the full 14-card game, */
+  int32_t disable_hot_seven;    /* so a non-zero value is MUZ_E_UNSUPPORTED for the DOG entry points       */
+  int32_t disable_joker;
 } muz_rules;
 
 /* Deterministic-MADN batch state, SoA (deterministic_madn.py:24-40).
@@ -141,6 +144,59 @@ int muz_classic_nostep(const muz_rules* rules, muz_classic_soa state, int8_t* re
 /* encode_board (463-497): obs[b][c][w], C = 2P+3 (last channel = die), W = 56. */
 int muz_classic_encode_f32(const muz_rules* rules, muz_classic_soa state, float* obs, int32_t n, void* stream);
 int muz_classic_encode_i8(const muz_rules* rules, muz_classic_soa state, int8_t* obs, int32_t n, void* stream);
+
+/* ---- DOG environment (DOG/dog.py + utils/utility_funcs.py) ---------------------------------
+ * Action layout (806): [0,396) joker copies, [396,792) real-card copies, each = swaps pin*56+pos [0,224),
+ * hot-7 distribution all_pin_distributions(7)[i] [224,344), normal pin*12+(move index over 1..6,8..13)
+ * [344,392), -4 pin [392,396); [792,806) swap-phase card.  Masks are bitsets uint32[n][26] (bit a%32 of
+ * word a/32).  The deck shuffle draws its 120 keys from a counter RNG instead of jax threefry:
+ *   key_k = U24(mix64(seed ^ 0xDEA1C0DE5EED ^ mix64(game << 32 | deal) ^ (k+1) * 0xA24BAED4963EE407)),
+ * deal = number of distribute_cards calls so far (oracle/dog.py:engine_shuffle_keys restates it). */
+typedef struct muz_dog_soa {
+  int8_t* board;          /* [56][stride] */
+  int8_t* pins;           /* [P*4][stride]  (the reference keeps int32; values -1..55) */
+  int8_t* deck;           /* [14][stride] */
+  int8_t* hands;          /* [P*14][stride] */
+  int8_t* swap_choices;   /* [4][stride] */
+  int8_t* current_player; /* [stride] */
+  int8_t* round_starter;  /* [stride] */
+  int8_t* phase;          /* [stride]  0 play, 1 swap */
+  int8_t* hand_size;      /* [stride]  size of the NEXT deal */
+  int8_t* reward;         /* [stride] */
+  uint8_t* done;          /* [stride] */
+  uint32_t* deal;         /* [stride]  distribute_cards calls (the jax key's role) */
+  int32_t stride;
+} muz_dog_soa;
+
+#define MUZ_DOG_ACTIONS 806
+#define MUZ_DOG_MASK_WORDS 26
+
+/* env_reset (dog.py:83-186) + the first distribute_cards (201-298) for games [0, n). */
+int muz_dog_reset(const muz_rules* rules /*host*/, muz_dog_soa state, uint64_t seed, int32_t n, void* stream);
+
+/* valid_actions (dog.py:693-711) -> mask[n][26]. */
+int muz_dog_legal(const muz_rules* rules, muz_dog_soa state, uint32_t* mask, int32_t n, void* stream);
+
+/* env_step (dog.py:1117-1131) with action[b] in [0, 806); a negative action applies no_step instead.
+ * A deal that follows draws from `seed`.  reward / done may be null. */
+int muz_dog_step(const muz_rules* rules, muz_dog_soa state, const int32_t* action, uint64_t seed, int8_t* reward,
+                 uint8_t* done, int32_t n, void* stream);
+
+/* no_step (dog.py:713-752). */
+int muz_dog_nostep(const muz_rules* rules, muz_dog_soa state, uint64_t seed, int8_t* reward, uint8_t* done,
+                   int32_t n, void* stream);
+
+/* One step function on its own, the form DOG/test.py calls (dog.py:754-984): kind[b] 0 step_swap(pin, pos),
+ * 1 step_normal_move(pin, move), 2 step_neg_move(pin, move), 3 step_hot_7(dist); args[b][4] = (pin, pos|move,
+ * -, -) or dist[4].  Writes board and pins; reward / done (may be null) are the function's results. */
+int muz_dog_step_move(const muz_rules* rules, muz_dog_soa state, const int32_t* kind, const int32_t* args,
+                      int8_t* reward, uint8_t* done, int32_t n, void* stream);
+
+/* Uniform random legal action (SURVEY config (d) policy): the k-th set bit of mask[b], k = floor(u * count),
+ * u = uniform[b] or, when uniform is null, U24(mix64(seed ^ 0x52A4D0DA11 ^ mix64(b << 32 | turn))).
+ * -1 when the mask is empty (the caller then applies no_step). */
+int muz_dog_random_action(const uint32_t* mask, const float* uniform, uint64_t seed, int32_t turn, int32_t* action,
+                          int32_t n, void* stream);
 
 /* ---- MuZero networks (MuZero_det_MADN/muzero_deterministic_madn.py) --------------------------
  * Dense layers used by the MFMA kernels take their kernel W[K][N] PACKED for

@@ -212,6 +212,46 @@ def default_shuffle_keys(env):
     return np.random.default_rng(1000 + env.deal).random(MAX_CARDS, dtype=np.float32)
 
 
+M64 = 0xFFFFFFFFFFFFFFFF
+DEAL_STREAM = 0xDEA1C0DE5EED
+RANDOM_ACTION_STREAM = 0x52A4D0DA11
+
+
+def _mix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
+    return x ^ (x >> 31)
+
+
+def _u24(h):
+    return np.float32((h >> 40) * (1.0 / 16777216.0))
+
+
+def _game_key(seed, g, turn):
+    return (seed & M64) ^ _mix64(((g & 0xFFFFFFFF) << 32) | (turn & 0xFFFFFFFF))
+
+
+def engine_shuffle_keys(seed, game):
+    """The device engine's deal keys (csrc/env_dog.hip:deal_key, include/muz.h DOG section) for game
+    ``game`` of a batch reset with ``seed``: a ``shuffle_keys`` callback for env_reset / env_step."""
+    def keys(env):
+        base = _game_key(seed ^ DEAL_STREAM, game, env.deal)
+        return np.array([_u24(_mix64(base ^ (((k + 1) * 0xA24BAED4963EE407) & M64))) for k in range(MAX_CARDS)],
+                        np.float32)
+    return keys
+
+
+def engine_random_action(mask, seed, game, turn):
+    """csrc/env_dog.hip:k_dog_random_action with the counter uniform: the k-th legal action."""
+    legal = np.flatnonzero(np.asarray(mask, bool))
+    if legal.size == 0:
+        return -1
+    u = _u24(_mix64(_game_key(seed ^ RANDOM_ACTION_STREAM, game, turn)))
+    k = min(int(np.float32(u) * np.float32(legal.size)), legal.size - 1)
+    return int(legal[k])
+
+
 def is_player_done(num_players, board, goal, player) -> bool:
     if player >= num_players:
         return False
@@ -317,6 +357,51 @@ def val_action_7(env, dist) -> bool:
     return bool(np.all(res & mover))
 
 
+def val_action_7_all(env, dists=DISTS_7_4):
+    """val_action_7 for every row of ``dists`` at once -> bool[n] (the same expressions, broadcast over the
+    distributions; tests/test_dog_oracle.py checks it against the scalar form)."""
+    R = env.rules
+    cp, cur, start, P, pos, _, _ = _common(env, np.zeros(4, np.int64))
+    D = np.asarray(dists, np.int64)
+    n = D.shape[0]
+    moved = cur[None, :] + D
+    fitted = moved % env.board_size
+    target = int(env.target[cp])
+    goal = env.goal[cp].astype(np.int64)
+    mt = int(R["must_traverse_start"])
+    x = moved - target - mt
+    posd = np.tile(pos, (n, 1))
+    posd[:, cp] = np.any((cur == start[cp])[None, :] & (moved == start[cp]), axis=1)
+    if R["enable_circular_board"]:
+        res = np.ones((n, 4), bool)
+    else:
+        res = ~((cur[None, :] <= target) & ((moved > target + 4) | ((x == 0) & bool(mt))))
+    dist10 = env.board_size // 4
+    nsb = ((cur // dist10) + 1) % P
+    nsa = fitted // dist10
+    trav = _g(start, nsb)[None, :] == _g(start, nsa)
+    pa = np.take_along_axis(posd, np.clip(np.where(nsa < 0, nsa + P, nsa), 0, P - 1), axis=1)
+    res = np.where(R["enable_start_blocking"] & trav, ~pa & res, res)
+    x = np.where(bool(mt) & R["enable_start_blocking"] & trav & pa, 0, x)
+    A = R["enable_circular_board"] & res
+    ing = np.isin(cur, goal)
+    tmp = np.where(ing[None, :], moved, cur[None, :])                       # cp's pins on tmp_board
+    occ = np.any(tmp[:, :, None] == goal[None, None, :], axis=1)             # (n, 4 goal cells)
+    ga = np.arange(4)
+    blocked = ((-1 < ga)[None, None, :] & (ga[None, None, :] < x[:, :, None])) & occ[:, None, :]
+    C = R["enable_jump_in_goal_area"] | ~np.any(blocked, axis=2)
+    res = np.where((4 >= x) & (x > 0) & (cur[None, :] <= target), A | C, res)
+    so = np.sign(cur[:, None] - cur[None, :])
+    sn = np.sign(moved[:, :, None] - moved[:, None, :])
+    gin = cur >= env.board_size
+    pairs = gin[:, None] & gin[None, :]
+    Dd = R["enable_jump_in_goal_area"] | ((cur < env.board_size)[None, :] |
+                                          np.all(np.where(pairs[None], so[None] == sn, True), axis=2))
+    res = np.where(ing[None, :], (moved <= goal[-1]) & Dd, res)
+    mover = np.where(cur[None, :] == -1, moved == -1, True)
+    return np.all(res & mover, axis=1)
+
+
 def val_action_normal_move(env, move):
     """dog.py:483-566 -> bool[4]."""
     R = env.rules
@@ -371,7 +456,7 @@ def valid_step_actions(env):
     N = env.total_board_size
     nsw = 4 * N
     swaps = val_swap(env).reshape(-1)
-    hot = np.array([val_action_7(env, d) for d in DISTS_7_4])
+    hot = val_action_7_all(env)
     normal = np.stack([val_action_normal_move(env, m) for m in NORMAL_MOVES])      # (12, 4)
     mask = np.concatenate([[hand[11] > 0], hand[[2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13]] > 0])
     neg = val_neg_move(env, -4)
@@ -630,9 +715,11 @@ def env_step_play_phase(env, action, shuffle_keys=None):
 def env_step_swap_phase(env, card):
     """dog.py:1077-1114 (no validity check in the reference)."""
     hands = env.hands.copy()
-    hands[env.current_player, _si(env.num_cards, card)] -= 1
+    ci = _si(env.num_cards, card)
+    if ci is not None:                       # out-of-range scatter is dropped
+        hands[env.current_player, ci] -= 1
     choices = env.swap_choices.copy()
-    choices[env.current_player] = card
+    choices[env.current_player] = np.array(card, np.int64).astype(np.int8)   # jnp.int8(card_idx) wraps
     nxt = (env.current_player + 1) % env.num_players
     complete = nxt == env.round_starter
     if complete:
