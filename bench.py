@@ -36,6 +36,13 @@ FLOP_PER_SIM = 2 * (529_280 + 404_544)
 # gathers: Dyn4 491,904 MAC (d3, d4, 2 ResBlocks, d5, Dense_6|7 latent rows, heads) + Pred4 404,544 MAC.
 EXEC_FLOP_PER_SIM = 2 * (491_904 + 404_544)
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E
+# Config (c): classic MADN 4p teams.  Algorithmic MAC per simulation (one branch evaluated):
+# decision = StochasticDynamics afterstate path + Pred4(A=4); chance = StochasticDynamics chance path + Pred4.
+CLASSIC_PLAYERS = 4
+# Config (d): DOG 2v2, 1024 games per GPU (8192 over 8 GPUs), uniform random legal policy.
+DOG_BATCH = 1024
+DOG_TURNS_PER_STEP = 16         # one bench step = one muz_dog_random_play launch of 16 turns over the batch
 
 
 def parse():
@@ -49,7 +56,12 @@ def parse():
     ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--workload", choices=("det", "classic", "dog"), default="det",
+                    help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
+    args = ap.parse_args()
+    if args.workload == "dog" and args.batch == BATCH:
+        args.batch = DOG_BATCH
+    return args
 
 
 def dist_env():
@@ -126,8 +138,189 @@ def measured_traffic():
     return t.get("bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+def setup(args):
+    rank, world, local = dist_env()
+    import torch
+    import muzpkg
+    muzpkg.load()
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", init_method="env://")
+        dist = tdist
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    return rank, world, dist, device
+
+
+def timed_region(dist, fn, steps):
+    """barrier + synchronize, K steps, synchronize + barrier; returns the rank's elapsed seconds."""
+    import torch
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        fn(k)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def sum_max(dist, device, sums, elapsed):
+    import torch
+    if dist is None:
+        return sums, elapsed
+    t = torch.tensor([float(x) for x in sums], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    m = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    return [x.item() for x in t], m[0].item()
+
+
+def dog_cpu_baseline(seconds):
+    """oracle/dog.py random legal play (the same engine streams) on one host core, bounded by `seconds`;
+    finished games are replaced by fresh ones so the sample keeps playing."""
+    from oracle import dog as dg
+    n, seed = 8, 5
+
+    def fresh(g):
+        return dg.env_reset(num_players=4, shuffle_keys=dg.engine_shuffle_keys(seed, g), **dg.SELFPLAY_RULES)
+
+    gids = list(range(n))
+    envs = [fresh(g) for g in gids]
+    steps, t, nxt = 0, 0, n
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for i in range(n):
+            if envs[i].done:
+                gids[i], nxt = nxt, nxt + 1
+                envs[i] = fresh(gids[i])
+            g, keys = gids[i], dg.engine_shuffle_keys(seed, gids[i])
+            a = dg.engine_random_action(dg.valid_actions(envs[i]), seed, g, t)
+            envs[i] = (dg.no_step(envs[i], keys) if a < 0 else dg.env_step(envs[i], a, keys))[0]
+            steps += 1
+        t += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 2), "unit": "env_steps/s", "cores": 1, "kind": "port",
+            "sample": f"NumPy oracle DOG random play, {n} concurrent games, {steps} env-steps in {dt:.1f}s"}
+
+
+def run_dog(args):
+    """Config (d): B DOG games per GPU (4p teams, MuZero_DOG/game_agent.py:12-23 rules) advanced by the
+    uniform random legal policy; one bench step = one batched turn (muz_dog_random_turn: legal mask, action
+    choice, env_step / no_step and any deal in one launch).  env-steps = turns of games not yet finished."""
+    import torch
+    rank, world, dist, device = setup(args)
+    from exploring_muzero_on_dog_amd import dog as DG
+    T = DOG_TURNS_PER_STEP
+    rp = DG.RandomPlay(args.batch, seed=4 + 1000 * rank, fused=True)
+    warm = torch.zeros(args.batch, dtype=torch.int32, device=device)
+    for _ in range(args.warmup):
+        rp.play(T, warm, auto_reset=True)
+    env_steps = torch.zeros(args.batch, dtype=torch.int32, device=device)
+    episodes = torch.zeros(args.batch, dtype=torch.int32, device=device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(k):
+        ev[k][0].record()
+        rp.play(T, env_steps, auto_reset=True, episodes=episodes)
+        ev[k][1].record()
+
+    elapsed = timed_region(dist, step, args.steps)
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev)
+    (steps_done, kms, games), elapsed = sum_max(dist, device, [int(env_steps.sum().item()), kernel_ms,
+                                                             int(episodes.sum().item())], elapsed)
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    avg_ms = kms / (args.steps * world)
+    # algorithmic bytes of one launch: the state is read and written once per launch (it stays in LDS
+    # across the T turns), plus the per-game step counter
+    launch_bytes = args.batch * (2 * 156 + 8)   # + env_steps / episodes counters (read + write)
+    achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
+    out = {
+        "metric": "self-play env steps/sec, DOG 2v2 random legal policy (config d)",
+        "value": round(steps_done / elapsed, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "data": "synthetic (seeded deals, counter-RNG random legal actions)", "games_finished": int(games),
+        "config": {"workload": f"DOG 4p teams, {args.batch} games/GPU, uniform random legal action per turn, "
+                               f"{T} turns per step in one launch (state resident in LDS), finished games "
+                               f"restart in place", "games_per_gpu": args.batch,
+                   "turns_per_step": T,
+                   "parallelism": f"independent games, {world} rank(s)"},
+        "roofline": {"bound": "hbm", "kernel": "k_dog_play", "achieved": round(achieved, 2),
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
+                     "avg_launch_ms": round(avg_ms, 5), "bytes_per_launch": launch_bytes,
+                     "note": "latency-bound: 1024 games = 1024 workgroups of 7 waves; HBM is not the limit",
+                     "traffic": None},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = dog_cpu_baseline(min(args.cpu_seconds, 15.0))
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_classic(args):
+    """Config (c): classic MADN 4p teams (game_agent_stochastic.py:13-24 rules), B games per GPU played to
+    the end with a 50-simulation Stochastic MuZero search per move (muz_classic_selfplay)."""
+    rank, world, dist, device = setup(args)
+    from exploring_muzero_on_dog_amd import game_agent_stochastic as GS
+    from exploring_muzero_on_dog_amd import stochastic as ST
+    from exploring_muzero_on_dog_amd import classic as CL
+    C = CL.num_channels(CLASSIC_PLAYERS)
+    net = ST.DeviceClassicNet(ST.init_classic_params(C, seed=0), C, device=device)
+    eng = GS.StochasticSelfPlayEngine(net, args.batch, num_players=CLASSIC_PLAYERS, max_steps=args.max_steps,
+                                      num_simulations=args.sims, max_depth=args.depth, device=device)
+    for w in range(args.warmup):
+        eng.play(seed=10_000 * rank + w, temperature=TEMP)
+    acc = {"steps": 0, "searches": 0, "search_ms": 0.0, "turns": 0}
+
+    def step(k):
+        buf = eng.play(seed=10_000 * rank + 1000 + k, temperature=TEMP)
+        st = eng.last_stats
+        acc["steps"] += int(buf["idx"].sum().item())
+        acc["searches"] += st["searches"]
+        acc["search_ms"] += st["search_ms"]
+        acc["turns"] += st["turns"]
+
+    elapsed = timed_region(dist, step, args.steps)
+    (steps_done, searches, search_ms, turns), elapsed = sum_max(
+        dist, device, [acc["steps"], acc["searches"], acc["search_ms"], acc["turns"]], elapsed)
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    out = {
+        "metric": "self-play env steps/sec + MCTS sims/sec, classic MADN 4p teams (config c)",
+        "value": round(steps_done / elapsed, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (self-generated games, seeded random fp32 weights)",
+        "config": {"workload": f"classic MADN {CLASSIC_PLAYERS}p teams self-play, {args.batch} games/GPU, "
+                               f"Stochastic MuZero S={args.sims} D={args.depth}, max_steps={args.max_steps}",
+                   "games_per_gpu": args.batch, "num_simulations": args.sims, "max_depth": args.depth,
+                   "parallelism": f"independent games, {world} rank(s)"},
+        "sims_per_s": round(searches * args.sims / elapsed, 1),
+        "env_steps": int(steps_done), "searches": int(searches),
+        "search_kernel": {"kernel": "k_stochastic_search", "avg_launch_ms": round(search_ms / max(1, turns), 4)},
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload == "dog":
+        return run_dog(args)
+    if args.workload == "classic":
+        return run_classic(args)
     rank, world, local = dist_env()
     import torch
     import muzpkg

@@ -38,7 +38,8 @@ struct DogG {   // one game in LDS
   float key[kMaxPool];
   int8_t pool[kMaxPool];
   int8_t shuffled[kMaxPool];
-  unsigned long long base[7];   // 396 base validity bits
+  unsigned long long wb[7];     // base validity bits by checking slot (env_dog.hip: dog_check_of)
+  int need_deal;
 };
 
 __device__ __forceinline__ int dgoal(const DetConsts& c, int p, int g) { return goal_of(c, p, g); }

@@ -5,7 +5,11 @@
 
 namespace muz {
 
-constexpr int kDogGamesPerBlock = 4;
+constexpr int kDogGamesPerBlock = 4;   // wave-per-game kernels (reset, explicit-action step)
+#ifndef MUZ_DOG_WPE
+#define MUZ_DOG_WPE 8      // waves per SIMD the play kernel is budgeted for: 4 blocks of 7 waves per CU (measured best)
+#endif
+constexpr int kDogBlockThreads = 448;  // block-per-game kernels: 7 waves = 4 swap, 2 hot-7, 1 normal/-4 checks
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -13,15 +17,26 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+struct WaveSync {   // one wavefront owns the game
+  static constexpr int N = 64;
+  __device__ __forceinline__ void operator()() const { wave_sync(); }
+};
+struct BlockSync {  // a whole workgroup owns the game
+  static constexpr int N = kDogBlockThreads;
+  __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+
 // ---- SoA <-> LDS ---------------------------------------------------------------------------------
-__device__ __forceinline__ void dog_load(const DetConsts& c, const muz_dog_soa& st, int g, DogG& s, int lane) {
+template <class Sync>
+__device__ __forceinline__ void dog_load(const DetConsts& c, const muz_dog_soa& st, int g, DogG& s, int tid) {
   const int S = st.stride;
-  for (int i = lane; i < kCells; i += 64) s.board[i] = st.board[i * S + g];
-  if (lane < 16) s.pins[lane] = lane < c.P * 4 ? st.pins[lane * S + g] : (int8_t)-1;
-  for (int i = lane; i < 4 * kDogCards; i += 64) s.hands[i / kDogCards][i % kDogCards] = i < c.P * kDogCards ? st.hands[i * S + g] : 0;
-  if (lane < kDogCards) s.deck[lane] = st.deck[lane * S + g];
-  if (lane < 4) s.swap_choices[lane] = st.swap_choices[lane * S + g];
-  if (lane == 0) {
+  for (int i = tid; i < kCells; i += Sync::N) s.board[i] = st.board[i * S + g];
+  if (tid < 16) s.pins[tid] = tid < c.P * 4 ? st.pins[tid * S + g] : (int8_t)-1;
+  for (int i = tid; i < 4 * kDogCards; i += Sync::N)
+    s.hands[i / kDogCards][i % kDogCards] = i < c.P * kDogCards ? st.hands[i * S + g] : 0;
+  if (tid < kDogCards) s.deck[tid] = st.deck[tid * S + g];
+  if (tid < 4) s.swap_choices[tid] = st.swap_choices[tid * S + g];
+  if (tid == 0) {
     s.cp = st.current_player[g];
     s.round_starter = st.round_starter[g];
     s.phase = st.phase[g];
@@ -30,18 +45,19 @@ __device__ __forceinline__ void dog_load(const DetConsts& c, const muz_dog_soa& 
     s.reward = st.reward[g];
     s.deal = st.deal[g];
   }
-  wave_sync();
+  Sync()();
 }
 
-__device__ __forceinline__ void dog_store(const DetConsts& c, const muz_dog_soa& st, int g, const DogG& s, int lane) {
-  wave_sync();
+template <class Sync>
+__device__ __forceinline__ void dog_store(const DetConsts& c, const muz_dog_soa& st, int g, const DogG& s, int tid) {
+  Sync()();
   const int S = st.stride;
-  for (int i = lane; i < kCells; i += 64) st.board[i * S + g] = s.board[i];
-  if (lane < c.P * 4) st.pins[lane * S + g] = s.pins[lane];
-  for (int i = lane; i < c.P * kDogCards; i += 64) st.hands[i * S + g] = s.hands[i / kDogCards][i % kDogCards];
-  if (lane < kDogCards) st.deck[lane * S + g] = s.deck[lane];
-  if (lane < 4) st.swap_choices[lane * S + g] = s.swap_choices[lane];
-  if (lane == 0) {
+  for (int i = tid; i < kCells; i += Sync::N) st.board[i * S + g] = s.board[i];
+  if (tid < c.P * 4) st.pins[tid * S + g] = s.pins[tid];
+  for (int i = tid; i < c.P * kDogCards; i += Sync::N) st.hands[i * S + g] = s.hands[i / kDogCards][i % kDogCards];
+  if (tid < kDogCards) st.deck[tid * S + g] = s.deck[tid];
+  if (tid < 4) st.swap_choices[tid * S + g] = s.swap_choices[tid];
+  if (tid == 0) {
     st.current_player[g] = (int8_t)s.cp;
     st.round_starter[g] = (int8_t)s.round_starter;
     st.phase[g] = (int8_t)s.phase;
@@ -57,6 +73,7 @@ __device__ __forceinline__ float deal_key(unsigned long long seed, int gid, unsi
   return u24(mix64(game_key(seed ^ kDealStream, gid, (int)deal) ^ (unsigned long long)(k + 1) * 0xA24BAED4963EE407ull));
 }
 
+template <class Sync>
 __device__ void dog_deal(const DetConsts& c, DogG& s, unsigned long long seed, int gid, int lane) {
   const int P = c.P;
   const int q = s.hand_size;
@@ -72,11 +89,11 @@ __device__ void dog_deal(const DetConsts& c, DogG& s, unsigned long long seed, i
       for (int j = 0; j < s.deck[k] && p < kMaxPool; ++j) s.pool[p++] = (int8_t)k;
     for (; p < kMaxPool; ++p) s.pool[p] = (int8_t)kDogCards;   // dummies
   }
-  wave_sync();
-  for (int k = lane; k < kMaxPool; k += 64) s.key[k] = s.pool[k] == kDogCards ? 2.0f : deal_key(seed, gid, s.deal, k);
-  wave_sync();
+  Sync()();
+  for (int k = lane; k < kMaxPool; k += Sync::N) s.key[k] = s.pool[k] == kDogCards ? 2.0f : deal_key(seed, gid, s.deal, k);
+  Sync()();
   // stable argsort: rank = #smaller keys + #equal keys at a lower index
-  for (int k = lane; k < kMaxPool; k += 64) {
+  for (int k = lane; k < kMaxPool; k += Sync::N) {
     const float kk = s.key[k];
     int r = 0;
     for (int j = 0; j < kMaxPool; ++j) {
@@ -85,7 +102,7 @@ __device__ void dog_deal(const DetConsts& c, DogG& s, unsigned long long seed, i
     }
     s.shuffled[r] = s.pool[k];
   }
-  wave_sync();
+  Sync()();
   if (lane == 0) {
     for (int p = 0; p < P; ++p)
       for (int sl = 0; sl < q && sl < 6; ++sl) {
@@ -103,7 +120,7 @@ __device__ void dog_deal(const DetConsts& c, DogG& s, unsigned long long seed, i
     s.hand_size = q == 2 ? 6 : q - 1;
     s.deal = s.deal + 1;
   }
-  wave_sync();
+  Sync()();
 }
 
 // ---- transitions (lane 0) ---------------------------------------------------------------------------
@@ -239,18 +256,22 @@ __device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d
     for (int k = 0; k < 4; ++k) row[k] |= 1ull << cst(c.start, cp);
   const unsigned long long anyp = row[0] | row[1] | row[2] | row[3];
   if (!invalid) {
-    bool hit[16];
-    for (int p = 0; p < c.P; ++p)
-      for (int k = 0; k < 4; ++k) hit[p * 4 + k] = (anyp >> jidx(s.pins[p * 4 + k], kCells)) & 1ull;
+    uint32_t hit = 0;   // bit p*4+k
+    for (int j = 0; j < c.P * 4; ++j) hit |= (uint32_t)((anyp >> jidx(s.pins[j], kCells)) & 1ull) << j;
+    hit &= ~(0xFu << (4 * cp));
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
       unsigned long long other = 0;
+#pragma unroll
       for (int j = 0; j < 4; ++j)
         if (j != k) other |= row[j];
-      hit[cp * 4 + k] = ((other >> jidx(cur[k], kCells)) & 1ull) && ((other >> jidx(npos[k], kCells)) & 1ull);
+      const bool h = ((other >> jidx(cur[k], kCells)) & 1ull) && ((other >> jidx(npos[k], kCells)) & 1ull);
+      hit |= (uint32_t)h << (4 * cp + k);
     }
+#pragma unroll
     for (int k = 0; k < 4; ++k) s.pins[cp * 4 + k] = (int8_t)npos[k];
     for (int j = 0; j < c.P * 4; ++j)
-      if (hit[j]) s.pins[j] = -1;
+      if ((hit >> j) & 1u) s.pins[j] = -1;
     dog_rebuild(c, s);
   }
   dog_finish(c, s, cp, invalid, reward, done);
@@ -284,9 +305,8 @@ __device__ int dog_env_step(const DetConsts& c, DogG& s, int action, int& reward
     s.swap_choices[cp0] = (int8_t)card;                   // jnp.int8(card_idx) wraps
     const int nxt = (cp0 + 1) % c.P;
     if (nxt == s.round_starter) {
-      const int partner[4] = {2, 3, 0, 1};
-      for (int p = 0; p < c.P; ++p) {
-        const int rc = s.swap_choices[partner[p]];
+      for (int p = 0; p < c.P; ++p) {   // execute_team_swap: partner of p is (p + 2) % 4
+        const int rc = s.swap_choices[(p + 2) & 3];
         if (rc >= 0 && rc < kDogCards) s.hands[p][rc] = (int8_t)(s.hands[p][rc] + 1);
       }
       for (int i = 0; i < 4; ++i) s.swap_choices[i] = -1;
@@ -344,53 +364,75 @@ __device__ int dog_no_step(const DetConsts& c, DogG& s) {
 }
 
 // ---- kernels ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_dog_reset(DetConsts c, muz_dog_soa st, unsigned long long seed, int n) {
-  __shared__ DogG sg[kDogGamesPerBlock];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int g = blockIdx.x * kDogGamesPerBlock + w;
-  if (g >= n) return;
-  DogG& s = sg[w];
+// env_reset (dog.py:83-186) of the game in LDS, first deal included.  `deal` is the deal counter to
+// continue from (0 for a fresh batch; the running count when a finished game is restarted in place, so
+// that the new episode draws new shuffle keys).
+template <class Sync>
+__device__ void dog_reset_lds(const DetConsts& c, DogG& s, unsigned long long seed, int g, unsigned deal, int tid) {
   const bool fp = has(c.flags, R_FREE_PIN);
-  if (lane < 16) {
-    const int p = lane / 4, k = lane % 4;
-    s.pins[lane] = (int8_t)((p < c.P) ? ((fp && k == 0) ? c.start[p] : -1) : -1);
+  if (tid < 16) {
+    const int p = tid / 4, k = tid % 4;
+    s.pins[tid] = (int8_t)((p < c.P) ? ((fp && k == 0) ? c.start[p] : -1) : -1);
   }
-  for (int i = lane; i < 4 * kDogCards; i += 64) s.hands[i / kDogCards][i % kDogCards] = 0;
-  if (lane < kDogCards) s.deck[lane] = lane == 0 ? 6 : 8;   // env_reset: joker 6, others 8 (dog.py:143-145)
-  if (lane == 0) {
+  for (int i = tid; i < 4 * kDogCards; i += Sync::N) s.hands[i / kDogCards][i % kDogCards] = 0;
+  if (tid < kDogCards) s.deck[tid] = tid == 0 ? 6 : 8;   // env_reset: joker 6, others 8 (dog.py:143-145)
+  if (tid < 4) s.swap_choices[tid] = -1;
+  if (tid == 0) {
     s.cp = c.starting_player;
     s.round_starter = -1;
     s.phase = 0;
     s.hand_size = 6;
     s.done = 0;
     s.reward = 0;
-    s.deal = 0;
+    s.deal = deal;
   }
-  wave_sync();
-  if (lane == 0) dog_rebuild(c, s);
-  wave_sync();
-  dog_deal(c, s, seed, g, lane);
-  dog_store(c, st, g, s, lane);
+  Sync()();
+  if (tid == 0) dog_rebuild(c, s);
+  Sync()();
+  dog_deal<Sync>(c, s, seed, g, tid);
 }
 
-__global__ __launch_bounds__(256) void k_dog_legal(DetConsts c, muz_dog_soa st, uint32_t* mask, int n) {
+__global__ __launch_bounds__(256) void k_dog_reset(DetConsts c, muz_dog_soa st, unsigned long long seed, int n) {
   __shared__ DogG sg[kDogGamesPerBlock];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = blockIdx.x * kDogGamesPerBlock + w;
   if (g >= n) return;
   DogG& s = sg[w];
-  dog_load(c, st, g, s, lane);
-  const int cp = dog_sub(c, s);
+  dog_reset_lds<WaveSync>(c, s, seed, g, 0u, lane);
+  dog_store<WaveSync>(c, st, g, s, lane);
+}
+
+// ---- block-per-game legality -----------------------------------------------------------------------
+// Thread t of the 448 checks one base action: waves 0-3 the 224 swaps, waves 4-5 the 120 hot-7 splits,
+// wave 6 the 48 normal moves and 4 "-4" moves, so every wave runs one kind of check (no divergence
+// between kinds).  The result bit of base action i sits at slot dog_slot(i) of s.wb.
+__device__ __forceinline__ int dog_check_of(int tid) {
+  const int w = tid >> 6, l = tid & 63;
+  if (w < 4) return w * 64 + l < kDogSwaps ? w * 64 + l : -1;
+  if (w < 6) return kDogSwaps + (w - 4) * 64 + l < kDogNormalBase ? kDogSwaps + (w - 4) * 64 + l : -1;
+  return l < kDogBase - kDogNormalBase ? kDogNormalBase + l : -1;
+}
+__device__ __forceinline__ int dog_slot(int i) {
+  return i < kDogSwaps ? i : (i < kDogNormalBase ? 256 + i - kDogSwaps : 384 + i - kDogNormalBase);
+}
+
+// Base checks of the game in LDS into s.wb (all threads; ends with a block barrier).  Checks run only for
+// actions whose joker or real card is in the (substituted) player's hand: the others are masked anyway.
+__device__ __forceinline__ void dog_checks_block(const DetConsts& c, DogG& s, int tid) {
   if (s.phase == 0) {
-    for (int r = 0; r < 7; ++r) {
-      const int i = r * 64 + lane;
-      const bool v = i < kDogBase && dog_base_valid(c, s, cp, i);
-      const unsigned long long b = __ballot(v);
-      if (lane == 0) s.base[r] = b;
-    }
-    wave_sync();
+    const int cp = dog_sub(c, s);
+    const int i = dog_check_of(tid);
+    const bool v = i >= 0 && (s.hands[cp][0] > 0 || s.hands[cp][dog_base_card(i)] > 0) && dog_base_valid(c, s, cp, i);
+    const unsigned long long b = __ballot(v);
+    if ((tid & 63) == 0) s.wb[tid >> 6] = b;
   }
-  uint32_t* out = mask + (size_t)g * kDogWords;
+  __syncthreads();
+}
+
+// valid_actions (dog.py:693-711) from s.wb as 13 wave-uniform words (bit a of word a/64); one wave.
+__device__ __forceinline__ void dog_mask_words(const DetConsts& c, const DogG& s, int lane, unsigned long long (&m)[13]) {
+  const int cp = dog_sub(c, s);
+#pragma unroll
   for (int r = 0; r < 13; ++r) {
     const int a = r * 64 + lane;
     bool v = false;
@@ -398,18 +440,119 @@ __global__ __launch_bounds__(256) void k_dog_legal(DetConsts c, muz_dog_soa st, 
       if (s.phase == 0) {
         if (a < kDogPlay) {
           const int i = a % kDogBase;
-          const bool bv = (s.base[i >> 6] >> (i & 63)) & 1ull;
+          const int sl = dog_slot(i);
+          const bool bv = (s.wb[sl >> 6] >> (sl & 63)) & 1ull;
           v = bv && (a < kDogBase ? s.hands[cp][0] > 0 : s.hands[cp][dog_base_card(i)] > 0);
         }
       } else if (a >= kDogPlay) {
         v = s.hands[s.cp][a - kDogPlay] > 0;
       }
     }
-    const unsigned long long b = __ballot(v);
-    if (lane == 0) {
-      if (2 * r < kDogWords) out[2 * r] = (uint32_t)b;
-      if (2 * r + 1 < kDogWords) out[2 * r + 1] = (uint32_t)(b >> 32);
+    m[r] = __ballot(v);
+  }
+}
+
+__global__ __launch_bounds__(kDogBlockThreads) void k_dog_legal(DetConsts c, muz_dog_soa st, uint32_t* mask, int n) {
+  __shared__ DogG s;
+  const int tid = threadIdx.x, g = blockIdx.x;
+  dog_load<BlockSync>(c, st, g, s, tid);
+  dog_checks_block(c, s, tid);
+  if (tid >= 64) return;
+  unsigned long long m[13];
+  dog_mask_words(c, s, tid, m);
+  uint32_t* out = mask + (size_t)g * kDogWords;
+  if (tid < kDogWords) {
+    unsigned long long x = m[0];
+#pragma unroll
+    for (int r = 1; r < 13; ++r)
+      if ((tid >> 1) == r) x = m[r];
+    out[tid] = (tid & 1) ? (uint32_t)(x >> 32) : (uint32_t)x;
+  }
+}
+
+constexpr unsigned long long kRandomActionStream = 0x52A4D0DA11ull;
+
+__device__ __forceinline__ float random_action_uniform(unsigned long long seed, int g, int turn) {
+  return u24(mix64(game_key(seed ^ kRandomActionStream, g, turn)));
+}
+
+// The k-th set bit of a 13-word mask (wave-uniform inputs), -1 when empty; k = floor(u * count).
+__device__ __forceinline__ int kth_legal(const unsigned long long (&m)[13], float u) {
+  int tot = 0;
+#pragma unroll
+  for (int r = 0; r < 13; ++r) tot += __popcll(m[r]);
+  if (tot == 0) return -1;
+  int k = (int)(u * (float)tot);
+  k = k >= tot ? tot - 1 : k;
+  int word = -1, kk = 0;
+  unsigned long long x = 0;
+#pragma unroll
+  for (int r = 0; r < 13; ++r) {   // the word holding the k-th bit, without indexing m[] dynamically
+    const int pc = __popcll(m[r]);
+    if (word < 0) {
+      if (k < pc) {
+        word = r;
+        x = m[r];
+        kk = k;
+      } else {
+        k -= pc;
+      }
     }
+  }
+  for (int j = 0; j < kk; ++j) x &= x - 1;   // drop the kk lowest set bits
+  return word * 64 + __ffsll((long long)x) - 1;
+}
+
+// Config (d)'s actor: `nturns` turns of one game per workgroup with the state resident in LDS --
+// valid_actions -> uniform random legal action (turn0 + t) -> env_step, or no_step when nothing is legal
+// -> deal if needed.  A finished game stops (action -2), or with `auto_reset` restarts in place
+// (dog_reset_lds, deal counter continued) and keeps playing.  env_steps[g] (optional) accumulates the
+// turns played and episodes[g] (optional) the games finished; action / reward / done (optional) are
+// those of the last turn.
+__global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_eu(MUZ_DOG_WPE))) void k_dog_play(DetConsts c, muz_dog_soa st, unsigned long long seed,
+                                                               int turn0, int nturns, int auto_reset,
+                                                               int32_t* action_out, int8_t* reward, uint8_t* done,
+                                                               uint32_t* env_steps, uint32_t* episodes) {
+  __shared__ DogG s;
+  const int tid = threadIdx.x, g = blockIdx.x;
+  if (st.done[g] && !auto_reset) {
+    if (tid == 0) {
+      if (action_out) action_out[g] = -2;
+      if (reward) reward[g] = 0;
+      if (done) done[g] = 1;
+    }
+    return;
+  }
+  dog_load<BlockSync>(c, st, g, s, tid);
+  int played = 0, finished = 0, a = -2, r = 0;
+  for (int t = 0; t < nturns; ++t) {
+    if (s.done) {        // block-uniform: read after a barrier
+      if (!auto_reset) break;
+      dog_reset_lds<BlockSync>(c, s, seed, g, s.deal, tid);
+    }
+    dog_checks_block(c, s, tid);
+    if (tid < 64) {
+      unsigned long long m[13];
+      dog_mask_words(c, s, tid, m);
+      a = kth_legal(m, random_action_uniform(seed, g, turn0 + t));
+      if (tid == 0) {
+        int d = s.done;
+        r = 0;
+        s.need_deal = a < 0 ? dog_no_step(c, s) : dog_env_step(c, s, a, r, d);
+      }
+    }
+    ++played;
+    __syncthreads();
+    if (s.need_deal) dog_deal<BlockSync>(c, s, seed, g, tid);
+    finished += s.done;
+  }
+  dog_store<BlockSync>(c, st, g, s, tid);
+  if (tid == 0) {
+    if (action_out) action_out[g] = a;
+    if (reward) reward[g] = (int8_t)r;
+    if (done) done[g] = (uint8_t)s.done;
+    if (env_steps) env_steps[g] += (uint32_t)played;
+    if (episodes) episodes[g] += (uint32_t)finished;
   }
 }
 
@@ -422,7 +565,7 @@ __global__ __launch_bounds__(256) void k_dog_step(DetConsts c, muz_dog_soa st, c
   const int g = blockIdx.x * kDogGamesPerBlock + w;
   if (g >= n) return;
   DogG& s = sg[w];
-  dog_load(c, st, g, s, lane);
+  dog_load<WaveSync>(c, st, g, s, lane);
   if (lane == 0) {
     int r = 0, d = s.done;
     int deal;
@@ -438,8 +581,8 @@ __global__ __launch_bounds__(256) void k_dog_step(DetConsts c, muz_dog_soa st, c
     if (done) done[g] = (uint8_t)d;
   }
   wave_sync();
-  if (need_deal[w]) dog_deal(c, s, seed, g, lane);
-  dog_store(c, st, g, s, lane);
+  if (need_deal[w]) dog_deal<WaveSync>(c, s, seed, g, lane);
+  dog_store<WaveSync>(c, st, g, s, lane);
 }
 
 // One step_* function of dog.py on its own (the form DOG/test.py calls): kind 0 step_swap(pin, pos),
@@ -452,7 +595,7 @@ __global__ __launch_bounds__(256) void k_dog_step_move(DetConsts c, muz_dog_soa 
   const int g = blockIdx.x * kDogGamesPerBlock + w;
   if (g >= n) return;
   DogG& s = sg[w];
-  dog_load(c, st, g, s, lane);
+  dog_load<WaveSync>(c, st, g, s, lane);
   if (lane == 0) {
     const int cp = dog_sub(c, s);
     const int k = kind[g];
@@ -471,7 +614,7 @@ __global__ __launch_bounds__(256) void k_dog_step_move(DetConsts c, muz_dog_soa 
     if (reward) reward[g] = (int8_t)r;
     if (done) done[g] = (uint8_t)d;
   }
-  dog_store(c, st, g, s, lane);
+  dog_store<WaveSync>(c, st, g, s, lane);
 }
 
 // Uniform random legal action (config (d)'s policy): the k-th set bit, k = floor(u * popcount); -1 if none.
@@ -486,7 +629,7 @@ __global__ __launch_bounds__(256) void k_dog_random_action(const uint32_t* mask,
     action[g] = -1;
     return;
   }
-  const float u = uniform ? uniform[g] : u24(mix64(game_key(seed ^ 0x52A4D0DA11ull, g, turn)));
+  const float u = uniform ? uniform[g] : random_action_uniform(seed, g, turn);
   int k = (int)(u * (float)tot);
   k = k >= tot ? tot - 1 : k;
   int a = -1;
@@ -556,7 +699,7 @@ int muz_dog_reset(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int32_t
 
 int muz_dog_legal(const muz_rules* rules, muz_dog_soa st, uint32_t* mask, int32_t n, void* stream) {
   DOG_PROLOGUE(mask != nullptr)
-  k_dog_legal<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, mask, n);
+  k_dog_legal<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(c, st, mask, n);
   return muz_last_launch_error();
 }
 
@@ -578,6 +721,23 @@ int muz_dog_step_move(const muz_rules* rules, muz_dog_soa st, const int32_t* kin
                       int8_t* reward, uint8_t* done, int32_t n, void* stream) {
   DOG_PROLOGUE(kind != nullptr && args != nullptr)
   k_dog_step_move<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, kind, args, reward, done, n);
+  return muz_last_launch_error();
+}
+
+int muz_dog_random_turn(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int32_t turn, int32_t* action,
+                        int8_t* reward, uint8_t* done, int32_t n, void* stream) {
+  DOG_PROLOGUE(true)
+  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(c, st, seed, turn, 1, 0, action, reward, done, nullptr,
+                                                              nullptr);
+  return muz_last_launch_error();
+}
+
+int muz_dog_random_play(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int32_t turn0, int32_t nturns,
+                        int32_t auto_reset, uint32_t* env_steps, uint32_t* episodes, int32_t n, void* stream) {
+  DOG_PROLOGUE(nturns >= 0)
+  if (nturns == 0) return MUZ_OK;
+  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(c, st, seed, turn0, nturns, auto_reset ? 1 : 0, nullptr,
+                                                              nullptr, nullptr, env_steps, episodes);
   return muz_last_launch_error();
 }
 

@@ -291,13 +291,16 @@ def map_move_to_action(kind: str, pin: int, value: int, joker: bool) -> int:
 class RandomPlay:
     """Config (d)'s actor: B DOG games advanced by a uniform random legal action per turn, all on device
     (legal mask -> random action -> step; no_step when nothing is legal, as the step kernel does for -1).
-    ``turn()`` is one batched env-step; finished games are reset in place by the caller (``play``)."""
+    ``turn()`` is one batched env-step.  ``fused=True`` runs the whole turn as one kernel
+    (muz_dog_random_turn: the mask stays in registers, finished games are skipped); otherwise three
+    launches (legal mask -> random action -> step) that also step finished games, as env_step would."""
 
-    def __init__(self, batch: int, seed=0, num_players=4, **rules):
+    def __init__(self, batch: int, seed=0, num_players=4, fused=True, **rules):
         r = dict(SELFPLAY_RULES)
         r.update(rules)
         self.env = env_reset(batch, num_players=num_players, seed=seed, **r)
         self.seed = int(seed)
+        self.fused = bool(fused)
         self.t = 0
         dev = self.env.board.device
         self.mask = torch.empty((batch, MASK_WORDS), dtype=torch.int32, device=dev)
@@ -309,9 +312,26 @@ class RandomPlay:
 
     def turn(self):
         e, lib, s = self.env, self._lib, _L.stream_ptr()
+        if self.fused:
+            _L.check(lib.muz_dog_random_turn(e.rules, self._soa, ctypes_u64(self.seed), self.t, _L.ptr(self.action),
+                                             _L.ptr(self.reward), _L.ptr(self.done), e.batch, s),
+                     "muz_dog_random_turn")
+            self.t += 1
+            return
         _L.check(lib.muz_dog_legal(e.rules, self._soa, _L.ptr(self.mask), e.batch, s), "muz_dog_legal")
         _L.check(lib.muz_dog_random_action(_L.ptr(self.mask), None, ctypes_u64(self.seed), self.t,
                                            _L.ptr(self.action), e.batch, s), "muz_dog_random_action")
         _L.check(lib.muz_dog_step(e.rules, self._soa, _L.ptr(self.action), ctypes_u64(self.seed),
                                   _L.ptr(self.reward), _L.ptr(self.done), e.batch, s), "muz_dog_step")
         self.t += 1
+
+    def play(self, nturns: int, env_steps: torch.Tensor | None = None, auto_reset: bool = False,
+             episodes: torch.Tensor | None = None):
+        """``nturns`` fused turns in ONE launch (muz_dog_random_play: every game stays in LDS for all of
+        them).  ``env_steps`` / ``episodes`` (int32 [B]) accumulate turns played / games finished; with
+        ``auto_reset`` a finished game restarts in place and keeps playing."""
+        e = self.env
+        _L.check(self._lib.muz_dog_random_play(e.rules, self._soa, ctypes_u64(self.seed), self.t, int(nturns),
+                                               int(bool(auto_reset)), _L.ptr(env_steps), _L.ptr(episodes), e.batch,
+                                               _L.stream_ptr()), "muz_dog_random_play")
+        self.t += int(nturns)

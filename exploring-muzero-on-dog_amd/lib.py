@@ -186,6 +186,10 @@ SIGNATURES = {
     "muz_dog_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, vp, vp, ctypes.c_int32,
                                       vp]),
     "muz_dog_step_move": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, vp, vp, vp, ctypes.c_int32, vp]),
+    "muz_dog_random_turn": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, ctypes.c_int32, vp,
+                                           vp, vp, ctypes.c_int32, vp]),
+    "muz_dog_random_play": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp]),
     "muz_dog_random_action": (ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_int32, vp, ctypes.c_int32, vp]),
     "muz_classic_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, ctypes.c_int32, vp]),
     "muz_classic_set_die": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),

@@ -56,6 +56,45 @@ class DeviceClassicNet(_Packer):
             _L.check(_L.load().muz_classic_net_prepare(ctypes.byref(w), _L.stream_ptr()), "muz_classic_net_prepare")
 
 
+def classic_param_shapes(obs_channels: int, num_actions: int = A_CLASSIC, chance_outcomes: int = 6) -> dict:
+    """Flax tree of (RepresentationNetwork2, StochasticDynamicsNetwork4, PredictionNetwork4) for classic
+    MADN (MuZero_Classic_MADN/muzero_classic_madn.py:69-135, 314-408, 192-226), flattened."""
+    from .nets import _resblock_shapes, param_shapes
+    A, C, L = num_actions, chance_outcomes, LATENT
+    det = param_shapes(obs_channels, A)
+    dense_l = {"act_embed": (A, 64), "act_film_scale": (64, L), "act_film_shift": (64, L), "act_dense1": (L, L),
+               "act_dense2": (L, L), "act_proj": (L, L), "reward_dense": (L + A, 64), "reward_head": (64, 3),
+               "discount_dense": (L, 32), "discount_head": (32, 3), "chance_head": (L, C), "chance_embed": (C, 64),
+               "chance_film_scale": (64, L), "chance_film_shift": (64, L), "chance_dense1": (L, L),
+               "chance_dense2": (L, L), "chance_proj": (L, L)}
+    s = {}
+    for name, (i, o) in dense_l.items():
+        s[f"{name}/kernel"], s[f"{name}/bias"] = (i, o), (o,)
+    for name, n in {"act_input_ln": L, "act_ln1": L, "act_ln2": L, "discount_ln": 32, "chance_input_ln": L,
+                    "chance_ln1": L, "chance_ln2": L}.items():
+        s[f"{name}/scale"], s[f"{name}/bias"] = (n,), (n,)
+    for r in range(4):
+        _resblock_shapes(s, f"ResBlock_{r}")
+    out = {k: v for k, v in det.items() if k.startswith("representation/")}
+    out.update({f"dynamics/{k}": v for k, v in s.items()})
+    out.update({k: v for k, v in det.items() if k.startswith("prediction/")})
+    return out
+
+
+def init_classic_params(obs_channels: int, seed: int = 0) -> dict:
+    """Flax-default initialisation (lecun_normal kernels truncated at 2 std, zero biases, unit LayerNorm
+    scales) from seeded NumPy draws, in classic_param_shapes order."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for k, shp in classic_param_shapes(obs_channels).items():
+        if k.endswith("kernel"):
+            std = np.sqrt(1.0 / int(np.prod(shp[:-1]))) / 0.87962566103423978
+            out[k] = (np.clip(rng.standard_normal(shp), -2.0, 2.0) * std).astype(np.float32)
+        else:
+            out[k] = (np.ones(shp) if k.endswith("scale") else np.zeros(shp)).astype(np.float32)
+    return out
+
+
 def _f32(t):
     return t.to(dtype=torch.float32).contiguous()
 

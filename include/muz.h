@@ -186,6 +186,20 @@ int muz_dog_step(const muz_rules* rules, muz_dog_soa state, const int32_t* actio
 int muz_dog_nostep(const muz_rules* rules, muz_dog_soa state, uint64_t seed, int8_t* reward, uint8_t* done,
                    int32_t n, void* stream);
 
+/* Config (d)'s actor turn in one launch: valid_actions -> the random legal action of muz_dog_random_action
+ * (counter uniform, stream `seed`, `turn`) -> env_step, or no_step when nothing is legal.  Games already
+ * done are not touched (action -2, reward 0, done 1).  action / reward / done may be null. */
+int muz_dog_random_turn(const muz_rules* rules, muz_dog_soa state, uint64_t seed, int32_t turn, int32_t* action,
+                        int8_t* reward, uint8_t* done, int32_t n, void* stream);
+
+/* `nturns` consecutive muz_dog_random_turn turns (turn0, turn0+1, ...) in ONE launch: each workgroup keeps
+ * its game resident in LDS for all turns.  A finished game stops, or with auto_reset != 0 restarts in place
+ * (env_reset + first deal, the deal counter continued so the new episode draws new keys) and keeps playing.
+ * env_steps[b] / episodes[b] (may be null) += turns played / games finished.  Without auto_reset the states
+ * equal nturns separate muz_dog_random_turn calls. */
+int muz_dog_random_play(const muz_rules* rules, muz_dog_soa state, uint64_t seed, int32_t turn0, int32_t nturns,
+                        int32_t auto_reset, uint32_t* env_steps, uint32_t* episodes, int32_t n, void* stream);
+
 /* One step function on its own, the form DOG/test.py calls (dog.py:754-984): kind[b] 0 step_swap(pin, pos),
  * 1 step_normal_move(pin, move), 2 step_neg_move(pin, move), 3 step_hot_7(dist); args[b][4] = (pin, pos|move,
  * -, -) or dist[4].  Writes board and pins; reward / done (may be null) are the function's results. */

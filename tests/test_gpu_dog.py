@@ -182,12 +182,14 @@ def test_dog_lockstep_fuzz(cuda, rule_set):
     assert steps > 1500 and refused > 50 and deals > 20, (steps, refused, nosteps, deals, dones)
 
 
-def test_dog_engine_loop_followed_by_oracle(cuda):
-    """dog.RandomPlay (legal -> random action -> step, device RNG only) for 150 turns; the oracle replays
-    every 16th game with the same counter streams and must land on the same state every turn."""
+@pytest.mark.parametrize("fused", [False, True])
+def test_dog_engine_loop_followed_by_oracle(cuda, fused):
+    """dog.RandomPlay (legal -> random action -> step, device RNG only; three launches or the fused
+    muz_dog_random_turn) for 150 turns; the oracle replays every 16th game with the same counter streams
+    and must land on the same state every turn."""
     D = _D()
     B, seed, T = 256, 99, 150
-    rp = D.RandomPlay(B, seed=seed)
+    rp = D.RandomPlay(B, seed=seed, fused=fused)
     kw = RULE_SETS["selfplay_4p_teams"]
     follow = list(range(0, B, 16))
     envs = {g: reset(kw, seed, g) for g in follow}
@@ -195,6 +197,8 @@ def test_dog_engine_loop_followed_by_oracle(cuda):
     for t in range(T):
         rp.turn()
         for g in follow:
+            if fused and envs[g].done:
+                continue          # the fused turn leaves finished games alone
             a = dg.engine_random_action(dg.valid_actions(envs[g]), seed, g, t)
             envs[g] = (dg.no_step(envs[g], keys[g]) if a < 0 else dg.env_step(envs[g], a, keys[g]))[0]
         if t % 10 == 9 or t == T - 1:
@@ -202,3 +206,58 @@ def test_dog_engine_loop_followed_by_oracle(cuda):
             sub = {k: v[follow] for k, v in host.items()}
             bad = diff(sub, [envs[g] for g in follow])
             assert bad is None, (t, bad)
+
+
+def test_dog_multi_turn_kernel_equals_single_turns(cuda):
+    """muz_dog_random_play(20 turns, one launch) == 20 x muz_dog_random_turn, state and step counts."""
+    D = _D()
+    B, seed = 300, 7
+    a, b = D.RandomPlay(B, seed=seed), D.RandomPlay(B, seed=seed)
+    steps = torch.zeros(B, dtype=torch.int32, device="cuda")
+    for chunk in (1, 7, 12):
+        for _ in range(chunk):
+            a.turn()
+        b.play(chunk, steps)
+        ha, hb = D.to_host(a.env), D.to_host(b.env)
+        for k in ha:
+            assert np.array_equal(ha[k], hb[k]), k
+    assert int(steps.sum()) == B * 20 - 0 or int(steps.min()) >= 1
+    want = 20 - 0
+    done = D.to_host(b.env)["done"]
+    assert (steps.cpu().numpy()[done == 0] == want).all()
+
+
+def test_dog_auto_reset_followed_by_oracle(cuda):
+    """muz_dog_random_play with auto_reset over 1500 turns (longer than a random game): finished games
+    restart in place with the deal counter continued; the oracle follows 8 games through their restarts."""
+    D = _D()
+    B, seed, T, chunk = 128, 3, 1500, 100
+    rp = D.RandomPlay(B, seed=seed)
+    kw = RULE_SETS["selfplay_4p_teams"]
+    follow = list(range(0, B, 16))
+    envs = {g: reset(kw, seed, g) for g in follow}
+    keys = {g: dg.engine_shuffle_keys(seed, g) for g in follow}
+    steps = torch.zeros(B, dtype=torch.int32, device="cuda")
+    eps = torch.zeros(B, dtype=torch.int32, device="cuda")
+    n_eps = {g: 0 for g in follow}
+    for t0 in range(0, T, chunk):
+        rp.play(chunk, steps, auto_reset=True, episodes=eps)
+        for t in range(t0, t0 + chunk):
+            for g in follow:
+                e = envs[g]
+                if e.done:      # dog_reset_lds: env_reset, deal counter continued
+                    base = e.deal
+                    e = dg.env_reset(num_players=4, shuffle_keys=lambda x, b=base, k=keys[g]: k(x.replace(deal=x.deal + b)),
+                                     **dg.SELFPLAY_RULES)
+                    e = e.replace(deal=e.deal + base)
+                a = dg.engine_random_action(dg.valid_actions(e), seed, g, t)
+                e = (dg.no_step(e, keys[g]) if a < 0 else dg.env_step(e, a, keys[g]))[0]
+                n_eps[g] += int(e.done)
+                envs[g] = e
+        host = D.to_host(rp.env)
+        bad = diff({k: v[follow] for k, v in host.items()}, [envs[g] for g in follow])
+        assert bad is None, (t0, bad)
+    assert (steps.cpu().numpy() == T).all()
+    e_dev = eps.cpu().numpy()
+    assert all(e_dev[g] == n_eps[g] for g in follow)
+    assert e_dev.sum() > B // 2, "random DOG games end within ~1000 turns; restarts must have happened"

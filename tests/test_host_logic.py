@@ -92,3 +92,12 @@ def test_table_free_considered_visits_equal_mctx_table():
         for m in range(17):
             for i in range(S):
                 assert considered_visit_closed_form(m, S, i) == table[m, i], (S, m, i)
+
+
+def test_classic_param_shapes_match_oracle():
+    from exploring_muzero_on_dog_amd import stochastic as ST
+    from oracle import classic_nets as CN
+    for C in (7, 11):
+        assert ST.classic_param_shapes(C) == CN.param_shapes(C)
+    a, b = ST.init_classic_params(11, seed=3), CN.init_params(11, seed=3)
+    assert list(a) == list(b) and all(np.array_equal(a[k], b[k]) for k in a)
