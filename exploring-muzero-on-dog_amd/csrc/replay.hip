@@ -44,43 +44,83 @@ __global__ __launch_bounds__(kRingScan) void k_ring_slots(const int32_t* idx, in
   if (t == 0) count[0] = total;
 }
 
-// One workgroup per (game, chunk of kCopySteps steps).  obs rows are C*56 bytes (multiple of 8).
-__global__ __launch_bounds__(256) void k_ring_copy(muz_ring ring, muz_traj tr, muz_traj_chance ch, const int32_t* slot,
-                                                   int n) {
+// The per-step fields of a trajectory store (self-play buffers, packed transfer rows, or the ring).
+struct Rows {
+  int8_t* obs;
+  int32_t *act, *rew;
+  float *val, *pol, *mask;
+  int32_t *player, *team, *discount, *dice;
+  float* dice_dist;
+};
+__host__ __device__ inline Rows rows_of(const muz_traj& t, const muz_traj_chance& c) {
+  return Rows{t.obs, t.act, t.rew, t.val, t.pol, t.mask, t.player, t.team, t.discount, c.dice, c.dice_dist};
+}
+__host__ __device__ inline Rows rows_of(const muz_ring& r) {
+  return Rows{r.obs, r.act, r.rew, r.val, r.pol, r.mask, r.player, r.team, r.discount, r.dice, r.dice_dist};
+}
+
+// Copy game g's steps [0, len[g]) from row src_row(g) to row dst_row(g), one workgroup per (game, chunk
+// of kCopySteps steps).  Rows are laid out [row][field]; obs rows are C*56 bytes (a multiple of 8) and
+// move as 8-byte words.  src_row = src_off ? src_off[g] : g*src_T; dst_row = dst_off ? dst_off[g] :
+// slot[g]*dst_T (slot < 0: not copied).  dice / dice_dist move when both sides have them.
+__global__ __launch_bounds__(256) void k_rows_copy(Rows src, Rows dst, const int32_t* len, const int64_t* src_off,
+                                                   int src_T, const int64_t* dst_off, const int32_t* slot, int dst_T,
+                                                   int C, int A, int32_t* ep_len) {
   const int g = blockIdx.y;
-  const int s = slot[g];
+  const int s = slot ? slot[g] : 0;
   if (s < 0) return;
-  const int L = tr.idx[g];
+  const int L = len[g];
   const int t0 = blockIdx.x * kCopySteps;
   if (t0 >= L) return;
   const int t1 = min(L, t0 + kCopySteps);
-  const int T = tr.max_steps, A = ring.num_actions;
-  const size_t src_row = (size_t)g * T, dst_row = (size_t)s * ring.max_steps;
-  // observations: contiguous [t0, t1) x C x 56 bytes, copied as 8-byte words
-  const size_t ob = (size_t)ring.obs_channels * 56;
+  const size_t src_row = src_off ? (size_t)src_off[g] : (size_t)g * src_T;
+  const size_t dst_row = dst_off ? (size_t)dst_off[g] : (size_t)s * dst_T;
+  const size_t ob = (size_t)C * 56;
   const size_t nw = (size_t)(t1 - t0) * ob / 8;
-  const AS1 uint64_t* so = reinterpret_cast<const AS1 uint64_t*>(gp(tr.obs) + (src_row + t0) * ob);
-  AS1 uint64_t* dob = reinterpret_cast<AS1 uint64_t*>(gpw(ring.obs) + (dst_row + t0) * ob);
+  const AS1 uint64_t* so = reinterpret_cast<const AS1 uint64_t*>(gp(src.obs) + (src_row + t0) * ob);
+  AS1 uint64_t* dob = reinterpret_cast<AS1 uint64_t*>(gpw(dst.obs) + (dst_row + t0) * ob);
   for (size_t i = threadIdx.x; i < nw; i += blockDim.x) dob[i] = so[i];
-  // policies [t][A] floats
   const int np = (t1 - t0) * A;
-  for (int i = threadIdx.x; i < np; i += blockDim.x)
-    gpw(ring.pol)[(dst_row + t0) * A + i] = gp(tr.pol)[(src_row + t0) * A + i];
-  // per-step scalars
+  for (int i = threadIdx.x; i < np; i += blockDim.x) gpw(dst.pol)[(dst_row + t0) * A + i] = gp(src.pol)[(src_row + t0) * A + i];
+  const bool chance = dst.dice && src.dice;
   for (int t = t0 + (int)threadIdx.x; t < t1; t += blockDim.x) {
-    ring.act[dst_row + t] = tr.act[src_row + t];
-    ring.rew[dst_row + t] = tr.rew[src_row + t];
-    ring.val[dst_row + t] = tr.val[src_row + t];
-    ring.mask[dst_row + t] = tr.mask[src_row + t];
-    ring.player[dst_row + t] = tr.player[src_row + t];
-    ring.team[dst_row + t] = tr.team[src_row + t];
-    ring.discount[dst_row + t] = tr.discount[src_row + t];
-    if (ring.dice) ring.dice[dst_row + t] = ch.dice[src_row + t];
+    dst.act[dst_row + t] = src.act[src_row + t];
+    dst.rew[dst_row + t] = src.rew[src_row + t];
+    dst.val[dst_row + t] = src.val[src_row + t];
+    dst.mask[dst_row + t] = src.mask[src_row + t];
+    dst.player[dst_row + t] = src.player[src_row + t];
+    dst.team[dst_row + t] = src.team[src_row + t];
+    dst.discount[dst_row + t] = src.discount[src_row + t];
+    if (chance) dst.dice[dst_row + t] = src.dice[src_row + t];
   }
-  if (ring.dice_dist)
+  if (chance)
     for (int i = threadIdx.x; i < (t1 - t0) * 6; i += blockDim.x)
-      ring.dice_dist[(dst_row + t0) * 6 + i] = ch.dice_dist[(src_row + t0) * 6 + i];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ring.ep_len[s] = L;
+      dst.dice_dist[(dst_row + t0) * 6 + i] = src.dice_dist[(src_row + t0) * 6 + i];
+  if (ep_len && blockIdx.x == 0 && threadIdx.x == 0) ep_len[s] = L;
+}
+
+// Exclusive scan of the game lengths (int64 row offsets of the packed layout) + total rows.
+__global__ __launch_bounds__(kRingScan) void k_len_scan(const int32_t* len, int n, int64_t* off, int64_t* total) {
+  __shared__ long long part[kRingScan];
+  const int t = threadIdx.x;
+  const int chunk = (n + kRingScan - 1) / kRingScan;
+  const int lo = min(n, t * chunk), hi = min(n, lo + chunk);
+  long long cnt = 0;
+  for (int g = lo; g < hi; ++g) cnt += max(len[g], 0);
+  part[t] = cnt;
+  __syncthreads();
+  for (int o = 1; o < kRingScan; o <<= 1) {
+    const long long v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  long long r = part[t] - cnt;
+  for (int g = lo; g < hi; ++g) {
+    off[g] = r;
+    r += max(len[g], 0);
+  }
+  if (t == kRingScan - 1) total[0] = part[t];
 }
 
 // sample_batch for one batch element per workgroup (vec_replay_buffer.py:101-264).
@@ -159,7 +199,51 @@ int muz_ring_save(muz_ring ring, muz_traj traj, const muz_traj_chance* chance, i
   int rc = muz_last_launch_error();
   if (rc || n == 0) return rc;
   dim3 grid((traj.max_steps + kCopySteps - 1) / kCopySteps, n);
-  k_ring_copy<<<grid, 256, 0, s>>>(ring, traj, ch, slot_out, n);
+  k_rows_copy<<<grid, 256, 0, s>>>(rows_of(traj, ch), rows_of(ring), traj.idx, nullptr, traj.max_steps, nullptr,
+                                   slot_out, ring.max_steps, ring.obs_channels, ring.num_actions, ring.ep_len);
+  return muz_last_launch_error();
+}
+
+int muz_traj_offsets(const int32_t* len, int32_t n, int64_t* row_offset, int64_t* total_rows, void* stream) {
+  MUZ_HOST_CHECK(n >= 0 && len && row_offset && total_rows);
+  k_len_scan<<<1, kRingScan, 0, (hipStream_t)stream>>>(len, n, row_offset, total_rows);
+  return muz_last_launch_error();
+}
+
+int muz_traj_pack(muz_traj traj, const muz_traj_chance* chance, const int64_t* row_offset, int32_t n,
+                  int32_t obs_channels, int32_t num_actions, muz_traj packed, const muz_traj_chance* packed_chance,
+                  void* stream) {
+  MUZ_HOST_CHECK(n >= 0 && traj.idx && traj.obs && packed.obs && row_offset && traj.max_steps > 0);
+  MUZ_HOST_CHECK(obs_channels > 0 && num_actions > 0);
+  MUZ_HOST_CHECK((chance == nullptr) == (packed_chance == nullptr));
+  const muz_traj_chance ch = chance ? *chance : muz_traj_chance{nullptr, nullptr};
+  const muz_traj_chance pch = packed_chance ? *packed_chance : muz_traj_chance{nullptr, nullptr};
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return MUZ_OK;
+  if (packed.idx && packed.idx != traj.idx)
+    MUZ_HIP_RET(hipMemcpyAsync(packed.idx, traj.idx, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+  dim3 grid((traj.max_steps + kCopySteps - 1) / kCopySteps, n);
+  k_rows_copy<<<grid, 256, 0, s>>>(rows_of(traj, ch), rows_of(packed, pch), traj.idx, nullptr, traj.max_steps,
+                                   row_offset, nullptr, 0, obs_channels, num_actions, nullptr);
+  return muz_last_launch_error();
+}
+
+int muz_ring_save_packed(muz_ring ring, muz_traj packed, const muz_traj_chance* chance, const int64_t* row_offset,
+                         int32_t n, int32_t max_len, int32_t position, int32_t* slot_out, int32_t* count_out,
+                         void* stream) {
+  MUZ_HOST_CHECK(n >= 0 && slot_out && count_out && packed.idx && packed.obs && row_offset && ring.obs && ring.ep_len);
+  MUZ_HOST_CHECK((ring.dice == nullptr) == (ring.dice_dist == nullptr));
+  MUZ_HOST_CHECK(!ring.dice || (chance && chance->dice && chance->dice_dist));
+  MUZ_HOST_CHECK(ring.capacity > 0 && position >= 0 && position < ring.capacity);
+  MUZ_HOST_CHECK(max_len >= 0 && max_len <= ring.max_steps);
+  const muz_traj_chance ch = chance ? *chance : muz_traj_chance{nullptr, nullptr};
+  hipStream_t s = (hipStream_t)stream;
+  k_ring_slots<<<1, kRingScan, 0, s>>>(packed.idx, n, position, ring.capacity, slot_out, count_out);
+  int rc = muz_last_launch_error();
+  if (rc || n == 0 || max_len == 0) return rc;
+  dim3 grid((max_len + kCopySteps - 1) / kCopySteps, n);
+  k_rows_copy<<<grid, 256, 0, s>>>(rows_of(packed, ch), rows_of(ring), packed.idx, row_offset, 0, nullptr, slot_out,
+                                   ring.max_steps, ring.obs_channels, ring.num_actions, ring.ep_len);
   return muz_last_launch_error();
 }
 

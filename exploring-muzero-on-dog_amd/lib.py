@@ -201,6 +201,10 @@ SIGNATURES = {
     "muz_classic_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_tile_waves": (ctypes.c_int32, []),
+    "muz_traj_offsets": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp]),
+    "muz_traj_pack": (ctypes.c_int, [MuzTraj, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, MuzTraj, vp, vp]),
+    "muz_ring_save_packed": (ctypes.c_int, [MuzRing, MuzTraj, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            vp, vp, vp]),
     "muz_ring_save": (ctypes.c_int, [MuzRing, MuzTraj, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]),
     "muz_ring_sample": (ctypes.c_int, [MuzRing, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                        vp, MuzSample, vp]),

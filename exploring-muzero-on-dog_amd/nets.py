@@ -211,9 +211,13 @@ class DeviceNet(_Packer):
             film=put(np.zeros((A + 1) * 2 * LATENT, np.float32)))
         spec["pred"] = self._pred_spec()
         self._upload(w, spec, device)
-        lib = _L.load()
+        self.prepare()
+
+    def prepare(self):
+        """Re-derive the per-action FiLM table from the packed weights (after they change in place, e.g.
+        a parameter broadcast from the learner)."""
         with torch.cuda.device(self.buffer.device):
-            _L.check(lib.muz_net_prepare(ctypes.byref(w), _L.stream_ptr()), "muz_net_prepare")
+            _L.check(_L.load().muz_net_prepare(ctypes.byref(self.w), _L.stream_ptr()), "muz_net_prepare")
 
 
 # ---------------------------------------------------------------------------------- inference

@@ -100,9 +100,32 @@ class VectorizedReplayBuffer:
         _L.check(_L.load().muz_ring_save(self.ring(), self._traj(b), None if ch is None else ctypes.byref(ch), n,
                                          self.position, _L.ptr(slots), _L.ptr(self._count), _L.stream_ptr()),
                  "muz_ring_save")
+        self._advance(slots, b["idx"])
+
+    def save_packed(self, packed: dict):
+        """Games packed by transfer.pack (possibly received from another rank by transfer.gather_packed)
+        into the ring, with the same slot rule as save_games_from_buffers."""
+        from .transfer import chance_struct, traj_struct
+        n = packed["idx"].shape[0]
+        if n == 0:
+            return
+        if tuple(packed["obs"].shape[1:]) != self.obs_shape or packed["pol"].shape[1] != self.action_dim:
+            raise ValueError("packed games do not match the ring's observation / action shape")
+        max_len = int(packed["idx"].max().item())
+        if max_len > self.max_episode_length:
+            raise ValueError("a packed game is longer than max_episode_length")
+        slots = torch.empty((n,), dtype=torch.int32, device=self.device)
+        ch = chance_struct(packed) if self._chance(packed) is not None else None
+        _L.check(_L.load().muz_ring_save_packed(self.ring(), traj_struct(packed), None if ch is None else ctypes.byref(ch),
+                                                _L.ptr(packed["row_offset"]), n, max_len, self.position,
+                                                _L.ptr(slots), _L.ptr(self._count), _L.stream_ptr()),
+                 "muz_ring_save_packed")
+        self._advance(slots, packed["idx"])
+
+    def _advance(self, slots, idx):
         count = int(self._count.item())
         sl = slots.cpu().numpy()
-        lens = b["idx"].cpu().numpy()
+        lens = idx.cpu().numpy()
         keep = sl >= 0
         self._ep_len_host[sl[keep]] = lens[keep]
         self.position = (self.position + count) % self.capacity

@@ -52,8 +52,13 @@ class DeviceClassicNet(_Packer):
             act_film_tab=put(np.zeros((A + 1) * 2 * LATENT, np.float32)),
             chance_film_tab=put(np.zeros((CHANCE + 1) * 2 * LATENT, np.float32)))
         self._upload(w, spec, device)
+        self.prepare()
+
+    def prepare(self):
+        """Re-derive the action / chance FiLM tables from the packed weights."""
         with torch.cuda.device(self.buffer.device):
-            _L.check(_L.load().muz_classic_net_prepare(ctypes.byref(w), _L.stream_ptr()), "muz_classic_net_prepare")
+            _L.check(_L.load().muz_classic_net_prepare(ctypes.byref(self.w), _L.stream_ptr()),
+                     "muz_classic_net_prepare")
 
 
 def classic_param_shapes(obs_channels: int, num_actions: int = A_CLASSIC, chance_outcomes: int = 6) -> dict:

@@ -1,0 +1,124 @@
+"""Actors -> learner trajectory transfer and learner -> actors weight broadcast.
+
+The north star places one self-play actor per GPU and a single learner rank that receives every actor's
+finished games over RCCL (xGMI point-to-point links), into a device-resident replay ring.  The
+reference has no such path: its actors are the same process as the learner, and finished games go
+device -> host with ``np.array`` and are copied slot by slot (vec_replay_buffer.py:36-61).
+
+* ``pack(buffers)``: an actor packs its games' ``[0, idx)`` steps into contiguous rows on its GPU
+  (``muz_traj_offsets`` + ``muz_traj_pack``): no padding to T crosses the link.
+* ``gather_packed(packed, dst)``: the packed rows of every rank arrive at rank ``dst`` -- one
+  ``all_gather`` of (games, rows) per rank, then ``batch_isend_irecv`` of each field (one message per
+  field and actor; each actor drives its own xGMI link to the learner, so the transfers run link-parallel).
+* ``VectorizedReplayBuffer.save_packed`` (replay.py) writes received rows into the ring directly
+  (``muz_ring_save_packed``).
+* ``broadcast_weights(net, src)``: the packed fp32 weight arena is ONE tensor, so a parameter update is
+  one ``broadcast``; receivers re-derive their FiLM tables (``net.prepare()``).
+
+``gather_packed`` / ``broadcast_weights`` are backend-agnostic (RCCL for device tensors, gloo for CPU
+tensors in the multi-process tests).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import lib as _L
+
+CELLS = 56
+
+
+def fields(obs_channels: int, num_actions: int, chance: bool):
+    """(name, dtype, per-row shape) of a packed game store, in transfer order."""
+    f = [("obs", torch.int8, (obs_channels, CELLS)), ("act", torch.int32, ()), ("rew", torch.int32, ()),
+         ("val", torch.float32, ()), ("pol", torch.float32, (num_actions,)), ("mask", torch.float32, ()),
+         ("player", torch.int32, ()), ("team", torch.int32, ()), ("discount", torch.int32, ())]
+    if chance:
+        f += [("dice", torch.int32, ()), ("dice_dist", torch.float32, (6,))]
+    return f
+
+
+def traj_struct(rows: dict, max_steps: int = 0) -> _L.MuzTraj:
+    t = _L.MuzTraj()
+    for k in ("obs", "act", "rew", "val", "pol", "mask", "player", "team", "discount", "idx"):
+        setattr(t, k, rows[k].data_ptr() if rows.get(k) is not None and rows[k].numel() else 0)
+    t.max_steps = int(max_steps)
+    return t
+
+
+def chance_struct(rows: dict):
+    if "dice" not in rows:
+        return None
+    c = _L.MuzTrajChance()
+    c.dice = rows["dice"].data_ptr() if rows["dice"].numel() else 0
+    c.dice_dist = rows["dice_dist"].data_ptr() if rows["dice_dist"].numel() else 0
+    return c
+
+
+def pack(buffers: dict) -> dict:
+    """Self-play buffers ([n, T] layout, game_agent / game_agent_stochastic) -> packed rows on the same
+    device: every field [R, ...] with R = sum(idx), plus ``idx`` [n] and ``row_offset`` [n] (int64)."""
+    n, T = buffers["act"].shape
+    C, A = buffers["obs"].shape[2], buffers["pol"].shape[2]
+    dev = buffers["act"].device
+    chance = "dice" in buffers
+    lib, s = _L.load(), _L.stream_ptr()
+    off = torch.empty((n,), dtype=torch.int64, device=dev)
+    tot = torch.empty((1,), dtype=torch.int64, device=dev)
+    _L.check(lib.muz_traj_offsets(_L.ptr(buffers["idx"]), n, _L.ptr(off), _L.ptr(tot), s), "muz_traj_offsets")
+    R = int(tot.item())
+    out = {name: torch.empty((R,) + shp, dtype=dt, device=dev) for name, dt, shp in fields(C, A, chance)}
+    out["idx"] = torch.empty((n,), dtype=torch.int32, device=dev)
+    out["row_offset"] = off
+    src_ch, dst_ch = chance_struct(buffers), chance_struct(out)
+    _L.check(lib.muz_traj_pack(traj_struct(buffers, T), None if src_ch is None else ctypes.byref(src_ch), _L.ptr(off),
+                               n, C, A, traj_struct(out), None if dst_ch is None else ctypes.byref(dst_ch), s),
+             "muz_traj_pack")
+    return out
+
+
+def gather_packed(packed: dict, obs_channels: int, num_actions: int, chance: bool = False, dst: int = 0,
+                  group=None) -> list | None:
+    """Every rank's packed games -> rank ``dst`` (a list indexed by source rank, its own included);
+    None on the other ranks.  Tensors stay on their device (RCCL) or CPU (gloo)."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = packed["idx"].device
+    meta = torch.tensor([packed["idx"].shape[0], packed["act"].shape[0]], dtype=torch.int64, device=dev)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    spec = fields(obs_channels, num_actions, chance)
+    order = [("idx", torch.int32, None), ("row_offset", torch.int64, None)] + spec
+    ops, result = [], None
+    if rank == dst:
+        result = []
+        for r in range(world):
+            n, R = (int(x) for x in metas[r].tolist())
+            if r == dst:
+                result.append(packed)
+                continue
+            got = {}
+            for name, dt, shp in order:
+                t = torch.empty((n,) if shp is None else (R,) + shp, dtype=dt, device=dev)
+                got[name] = t
+                if t.numel():
+                    ops.append(dist.P2POp(dist.irecv, t, dist.get_global_rank(group, r) if group else r, group))
+            result.append(got)
+    else:
+        for name, _, _ in order:
+            t = packed[name].contiguous()
+            if t.numel():
+                ops.append(dist.P2POp(dist.isend, t, dist.get_global_rank(group, dst) if group else dst, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return result
+
+
+def broadcast_weights(net, src: int = 0, group=None):
+    """Learner -> actors parameter update: one broadcast of the packed weight arena, then the derived
+    FiLM tables are rebuilt on every rank."""
+    dist.broadcast(net.buffer, src=src, group=group)
+    if hasattr(net, "prepare"):
+        net.prepare()

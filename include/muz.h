@@ -531,6 +531,27 @@ int muz_ring_sample(muz_ring ring, const int32_t* ep_idx, const int32_t* t_start
                     int32_t td_steps, int32_t bootstrap_value_target, const double* gamma_pow, muz_sample out,
                     void* stream);
 
+/* ---- trajectory transfer (actors -> learner; north star: RCCL gather into one learner rank) ------
+ * The reference moves finished games device -> host with np.array and copies them slot by slot
+ * (vec_replay_buffer.py:36-61).  Here an actor PACKS its games' [0, idx) steps into contiguous rows
+ * (no padding to T), the packed rows travel rank -> learner over RCCL point-to-point, and the learner
+ * writes them into its ring without unpacking.  Packed layout = a muz_traj whose arrays are indexed by
+ * row (row_offset[g] + t) instead of g*T + t; idx = the game lengths. */
+
+/* row_offset[g] = exclusive prefix sum of max(len, 0); total_rows[0] = sum (device int64). */
+int muz_traj_offsets(const int32_t* len, int32_t n, int64_t* row_offset, int64_t* total_rows, void* stream);
+
+/* Pack traj ([n][T] layout) into `packed` rows at row_offset (from muz_traj_offsets); packed.idx (may be
+ * null) receives the lengths.  chance / packed_chance: both null or both set (classic dice fields). */
+int muz_traj_pack(muz_traj traj, const muz_traj_chance* chance, const int64_t* row_offset, int32_t n,
+                  int32_t obs_channels, int32_t num_actions, muz_traj packed, const muz_traj_chance* packed_chance,
+                  void* stream);
+
+/* muz_ring_save for packed rows: same slot rule, max_len = the longest game (bounds the grid). */
+int muz_ring_save_packed(muz_ring ring, muz_traj packed, const muz_traj_chance* chance, const int64_t* row_offset,
+                         int32_t n, int32_t max_len, int32_t position, int32_t* slot_out, int32_t* count_out,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -111,3 +111,66 @@ def test_stochastic_ring_with_classic_selfplay(cuda):
                           ora.dice_outcomes[ora.episode_lengths[:, None] > np.arange(90)])
     for _ in range(2):
         assert_sample_equal(dev.sample_batch(), ora.sample_batch())
+
+
+def _host_pack(host, T):
+    """NumPy reference of transfer.pack: rows [0, idx) of every game, concatenated in game order."""
+    lens = host["idx"]
+    out = {k: np.concatenate([host[k][g, :lens[g]] for g in range(len(lens))]) for k in host if k != "idx"}
+    out["idx"] = lens
+    out["row_offset"] = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    return out
+
+
+def _assert_rings_identical(a, b):
+    assert (a.position, a.size) == (b.position, b.size)
+    for k in ("observations", "actions", "rewards", "root_values", "child_visits", "masks", "players", "teams",
+              "discounts", "episode_lengths") + (("dice_outcomes", "dice_distributions") if hasattr(a, "dice_outcomes")
+                                                  else ()):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
+def test_pack_and_save_packed_det(cuda):
+    """transfer.pack == NumPy packing, and a ring fed with packed rows == a ring fed with the buffers."""
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import game_agent as GA
+    from exploring_muzero_on_dog_amd import nets as N
+    from exploring_muzero_on_dog_amd import transfer as TR
+    R = _R()
+    C = E.num_channels(4)
+    net = N.DeviceNet(N.init_muzero_params(0, C), C)
+    eng = GA.SelfPlayEngine(net, 40, num_players=4, max_steps=80, num_simulations=8, max_depth=6)
+    bufs = eng.play(seed=5)
+    packed = TR.pack(bufs)
+    want = _host_pack({k: v.cpu().numpy() for k, v in bufs.items()}, 80)
+    for k, v in want.items():
+        assert np.array_equal(packed[k].cpu().numpy(), v), k
+    a = R.VectorizedReplayBuffer(50, 64, 10, 20, obs_shape=(C, 56), max_episode_length=80)
+    b = R.VectorizedReplayBuffer(50, 64, 10, 20, obs_shape=(C, 56), max_episode_length=80)
+    for _ in range(2):                                           # 80 games into 50 slots: wraps
+        a.save_games_from_buffers(bufs)
+        b.save_packed(packed)
+    _assert_rings_identical(a, b)
+
+
+def test_pack_and_save_packed_classic_dice(cuda):
+    from oracle import classic_nets as CN
+    from exploring_muzero_on_dog_amd import classic as CL
+    from exploring_muzero_on_dog_amd import game_agent_stochastic as GS
+    from exploring_muzero_on_dog_amd import stochastic as S
+    from exploring_muzero_on_dog_amd import transfer as TR
+    R = _R()
+    C = CL.num_channels(4)
+    net = S.DeviceClassicNet(CN.init_params(C, seed=4), C)
+    eng = GS.StochasticSelfPlayEngine(net, 24, max_steps=90, num_simulations=8, max_depth=6)
+    bufs = eng.play(seed=2)
+    packed = TR.pack(bufs)
+    want = _host_pack({k: v.cpu().numpy() for k, v in bufs.items()}, 90)
+    for k, v in want.items():
+        assert np.array_equal(packed[k].cpu().numpy(), v), k
+    a = R.VectorizedReplayBufferStochastic(30, 64, 10, 20, obs_shape=(C, 56), max_episode_length=90)
+    b = R.VectorizedReplayBufferStochastic(30, 64, 10, 20, obs_shape=(C, 56), max_episode_length=90)
+    for _ in range(2):
+        a.save_games_from_buffers(bufs)
+        b.save_packed(packed)
+    _assert_rings_identical(a, b)
