@@ -2,8 +2,10 @@
 """Self-play throughput benchmark: det-MADN, B = 4096 games per GPU, 50-simulation Gumbel MuZero.
 
 Metric (BASELINE.json): self-play env-steps/s (+ MCTS sims/s), det-MADN batch 4096, 1/2/4/8 GPU.
-  * one bench "step" = one play_n_games_v3 call: reset 4096 games on every rank and play them to
-    completion (or max_steps batched turns) with a 50-simulation search per move (SURVEY §8d b);
+  * one bench "step" = 8 x 4096 complete games per rank with a 50-simulation search per move (SURVEY
+    §8d b), played 4096 at a time: the self-play batch is 4096 concurrent games, and a game that ends
+    hands its lane to the next game (muz_detmadn_selfplay_stream).  --games 0 times the reference's
+    own unit instead, one play_n_games_v3 call of 4096 games whose batch shrinks as games finish;
   * env-steps = sum of recorded turns (idx) over all games and ranks, exactly game_agent.py:140;
   * sims/s = searches x S / time.
 Weak scaling: every rank plays its own 4096 games (games are independent; no data-path collective).
@@ -23,6 +25,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BATCH = 4096
+# One det bench step streams 8 x 4096 games through the 4096 concurrently played games (lanes): a lane
+# whose game ends starts the next game, so searches run on a full batch instead of shrinking with the
+# finished games as one play_n_games_v3 batch does (its tail averages ~54 % active games).  Each game's
+# record is identical to the batch call's (tests/test_gpu_selfplay.py::test_stream_equals_batch).
+STREAM_GENERATIONS = 8
 S = 50
 D = 25
 MAX_STEPS = 500
@@ -56,11 +63,16 @@ def parse():
     ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--games", type=int, default=-1,
+                    help="det: games per step streamed through the --batch lanes (default 8 x batch; 0 = one "
+                         "batch of --batch games, the reference's play_n_games_v3 call)")
     ap.add_argument("--workload", choices=("det", "classic", "dog"), default="det",
                     help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
     args = ap.parse_args()
     if args.workload == "dog" and args.batch == BATCH:
         args.batch = DOG_BATCH
+    if args.games < 0:
+        args.games = STREAM_GENERATIONS * args.batch
     return args
 
 
@@ -343,8 +355,13 @@ def main():
     eng = GA.SelfPlayEngine(net, args.batch, num_players=PLAYERS, max_steps=args.max_steps,
                             num_simulations=args.sims, max_depth=args.depth, device=device)
 
+    def play(seed):
+        if args.games:
+            return eng.play_stream(args.games, seed=seed, temperature=TEMP)
+        return eng.play(seed=seed, temperature=TEMP)
+
     for w in range(args.warmup):
-        eng.play(seed=10_000 * rank + w, temperature=TEMP)
+        play(10_000 * rank + w)
     torch.cuda.synchronize()
 
     steps_done = 0
@@ -356,7 +373,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        buf = eng.play(seed=10_000 * rank + 1000 + k, temperature=TEMP)
+        buf = play(10_000 * rank + 1000 + k)
         st = eng.last_stats
         steps_done += int(buf["idx"].sum().item())
         searches += st["searches"]
@@ -392,8 +409,10 @@ def main():
         "dtype": "f32",
         "data": "synthetic (self-generated games, seeded random fp32 weights)",
         "config": {"workload": f"det-MADN {PLAYERS}p self-play, {args.batch} games/GPU, Gumbel MuZero "
-                               f"S={args.sims} D={args.depth}, max_steps={args.max_steps}, temp={TEMP}",
-                   "games_per_gpu": args.batch, "num_simulations": args.sims, "max_depth": args.depth,
+                               f"S={args.sims} D={args.depth}, max_steps={args.max_steps}, temp={TEMP}"
+                               + (f", {args.games} games per step streamed through the {args.batch} lanes"
+                                  if args.games else ""),
+                   "games_per_gpu": args.batch, "games_per_step": args.games or args.batch, "num_simulations": args.sims, "max_depth": args.depth,
                    "parallelism": f"independent games, {world} rank(s)"},
         "sims_per_s": round(searches * args.sims / elapsed, 1),
         "env_steps": int(steps_done),

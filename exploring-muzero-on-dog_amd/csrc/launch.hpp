@@ -11,6 +11,11 @@ struct SearchArgs {
   float value_scale, maxvisit_init, gumbel_scale;
   unsigned long long seed;
   int turn;
+  // Optional noise keys of a self-play driver: the game id of lane l is key_game[l] (else l) and its
+  // turn key_turn[game id] (else `turn`) -- the game's own step count, so a game draws the same noise
+  // whichever lane and global turn it is played in.
+  const int32_t* key_game = nullptr;
+  const int32_t* key_turn = nullptr;
 };
 
 int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv_scratch,

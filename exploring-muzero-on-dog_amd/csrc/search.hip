@@ -204,12 +204,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
   rk.index = -1;
   if (valid) {
     lb = legal[g];
-    const int gid = game_id ? game_id[g] : g;
+    const int lane = game_id ? game_id[g] : g;
+    const int gid = sa.key_game ? sa.key_game[lane] : lane;
+    const int gturn = sa.key_turn ? sa.key_turn[gid] : sa.turn;
     const float l = ok ? root_logits[(size_t)g * A + ai] : -INFINITY;
     const float lm = row_max(l);
     const bool inv = !ok || ((lb >> a) & 1u) == 0u;
     rk.prior = inv ? kFMin : l - lm;
-    if (ok) gum = gumbel_in ? gumbel_in[(size_t)g * A + ai] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, sa.turn, ai);
+    if (ok) gum = gumbel_in ? gumbel_in[(size_t)g * A + ai] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, gturn, ai);
     AS1 float* e0 = T.e(g, 0);
     for (int c = a; c < LAT; c += kRowLanes) e0[c] = root_emb[(size_t)g * LAT + c];
     ncons = min(sa.max_considered, __popc(lb & ((1u << A) - 1u)));

@@ -81,6 +81,35 @@ class SelfPlayEngine:
         return self.buffers
 
 
+    def play_stream(self, num_games: int, seed: int, temperature: float = 1.0, stream=None,
+                    timing: bool = True) -> dict:
+        """``num_games`` games through this engine's ``num_envs`` lanes (muz_detmadn_selfplay_stream): a
+        lane whose game ends starts the next one, so every search runs on a full batch until the last
+        games.  Game k's trajectory equals game k of ``play`` on a batch of ``num_games``.  Returns
+        buffers shaped [num_games, max_steps, ...] (reused across calls of the same size)."""
+        lib = _L.load()
+        num_games = int(num_games)
+        if getattr(self, "_sbuf_n", None) != num_games:
+            z = dict(device=self.buffers["act"].device)
+            self._sbuf = {k: torch.empty((num_games,) + tuple(v.shape[1:]), dtype=v.dtype, **z)
+                          for k, v in self.buffers.items()}
+            self._sbuf_n = num_games
+        t = _L.MuzTraj()
+        for k in ("obs", "act", "rew", "val", "pol", "mask", "player", "team", "discount", "idx"):
+            setattr(t, k, self._sbuf[k].data_ptr())
+        t.max_steps = self.T
+        cfg = M.make_cfg(self.S, self.D, temperature=temperature, seed=seed)
+        st = _L.MuzSpStats()
+        _L.check(lib.muz_detmadn_selfplay_stream(self.rules, self.net.w, cfg, self.state.soa(), t, num_games, self.n,
+                                                 _L.ptr(self.workspace), _L.nbytes(self.workspace),
+                                                 ctypes.byref(st) if timing else None, _L.stream_ptr(stream)),
+                 "muz_detmadn_selfplay_stream")
+        self.last_stats = {"turns": st.turns, "searches": st.searches, "search_ms": st.search_ms,
+                           "total_ms": st.total_ms} if timing else None
+        self.last_turns = st.turns if timing else -1
+        return self._sbuf
+
+
 def play_n_games_v3(net: N.DeviceNet, seed: int, num_envs: int, num_simulation: int, max_depth: int,
                     max_steps: int, temp: float, num_players: int = 4, rules: dict | None = None) -> dict:
     """play_n_games_v3 (game_agent.py:185-192) -> trajectory buffers (device tensors)."""

@@ -236,6 +236,10 @@ SIGNATURES = {
     "muz_detmadn_selfplay": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzNetW),
                                             ctypes.POINTER(MuzSearchCfg), MuzDetSoA, MuzTraj, ctypes.c_int32, vp,
                                             ctypes.c_int64, ctypes.POINTER(MuzSpStats), vp]),
+    "muz_detmadn_selfplay_stream": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzNetW),
+                                                   ctypes.POINTER(MuzSearchCfg), MuzDetSoA, MuzTraj, ctypes.c_int32,
+                                                   ctypes.c_int32, vp, ctypes.c_int64, ctypes.POINTER(MuzSpStats),
+                                                   vp]),
 }
 
 _lib = None

@@ -368,6 +368,17 @@ int muz_detmadn_selfplay(const muz_rules* rules /*host*/, const muz_net_w* w /*h
                          const muz_search_cfg* cfg /*host*/, muz_detmadn_soa state, muz_traj traj, int32_t n,
                          void* workspace, int64_t workspace_bytes, muz_sp_stats* stats /*host*/, void* stream);
 
+/* The same self-play, streamed: num_games games through `lanes` concurrently played lanes (state stride
+ * >= lanes, workspace = muz_selfplay_workspace_bytes(lanes, ...)).  Lane l starts game l; whenever a game
+ * ends (done, or max_steps recorded) its lane takes the next game number (deterministic, lane order) and
+ * is reset, so the search batch stays full until the last games.  traj is [num_games][T]; game k's
+ * record, including its Gumbel noise (keyed by game number and the game's own step), is identical to
+ * game k of a muz_detmadn_selfplay batch of num_games games. */
+int muz_detmadn_selfplay_stream(const muz_rules* rules /*host*/, const muz_net_w* w /*host*/,
+                                const muz_search_cfg* cfg /*host*/, muz_detmadn_soa state, muz_traj traj,
+                                int32_t num_games, int32_t lanes, void* workspace, int64_t workspace_bytes,
+                                muz_sp_stats* stats /*host*/, void* stream);
+
 /* ---- Stochastic MuZero for classic MADN (MuZero_Classic_MADN/muzero_classic_madn.py) ----------
  * Same packing conventions as the det networks.  RepresentationNetwork2 (69-135) and
  * PredictionNetwork4 (192-226, A = 4) reuse muz_repr_w / muz_pred_w. */

@@ -76,3 +76,22 @@ def test_selfplay_default_config_runs_and_is_deterministic(cuda):
     pol = b1["pol"].cpu().numpy()
     s = pol.sum(-1)
     assert np.allclose(s[mask > 0], 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("P,games,lanes,T", [(2, 40, 16, 300), (4, 37, 8, 60)])
+def test_stream_equals_batch(cuda, P, games, lanes, T):
+    """muz_detmadn_selfplay_stream: `games` games through `lanes` refilled lanes give exactly the
+    trajectories of one muz_detmadn_selfplay batch of `games` (noise keyed by game and own step;
+    T = 60 truncates most 4p games at max_steps)."""
+    GA, N = _mods()
+    C = dm.num_channels(P)
+    net = N.DeviceNet(N.init_muzero_params(3, C), C)
+    batch = GA.SelfPlayEngine(net, games, num_players=P, max_steps=T, num_simulations=8, max_depth=6)
+    want = {k: v.clone() for k, v in batch.play(99, 1.0).items()}
+    eng = GA.SelfPlayEngine(net, lanes, num_players=P, max_steps=T, num_simulations=8, max_depth=6)
+    got = eng.play_stream(games, 99, 1.0)
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
+    st = eng.last_stats
+    assert st["searches"] == batch.last_stats["searches"]
+    assert st["turns"] >= batch.last_stats["turns"]
