@@ -49,6 +49,16 @@ class MuzDogSoA(ctypes.Structure):
         ("stride", ctypes.c_int32)]
 
 
+class MuzTttState(ctypes.Structure):
+    _fields_ = [("board", ctypes.c_int8 * 9), ("current_player", ctypes.c_int8), ("reward", ctypes.c_int8),
+                ("done", ctypes.c_uint8), ("memory", ctypes.c_int8 * 6)]
+
+
+class MuzTttPolicyOut(ctypes.Structure):
+    _fields_ = [("action", ctypes.c_int32), ("visits", ctypes.c_int32 * 9), ("action_weights", ctypes.c_double * 9),
+                ("value", ctypes.c_double)]
+
+
 class MuzDetSoA(ctypes.Structure):
     _fields_ = [
         ("board", vp),
@@ -201,6 +211,15 @@ SIGNATURES = {
     "muz_classic_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_tile_waves": (ctypes.c_int32, []),
+    "muz_ttt_reset": (ctypes.c_int, [ctypes.POINTER(MuzTttState)]),
+    "muz_ttt_step": (ctypes.c_int, [ctypes.POINTER(MuzTttState), ctypes.c_int32, vp, vp]),
+    "muz_ttt_policy_logits": (ctypes.c_int, [ctypes.POINTER(MuzTttState), vp]),
+    "muz_ttt_rollout": (ctypes.c_int, [ctypes.POINTER(MuzTttState), ctypes.c_uint64, ctypes.c_uint32, vp]),
+    "muz_ttt_muzero_policy": (ctypes.c_int, [ctypes.POINTER(MuzTttState), ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_double, ctypes.c_uint64, ctypes.c_int32,
+                                             ctypes.POINTER(MuzTttPolicyOut)]),
+    "muz_ttt_match": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
+                                     vp]),
     "muz_traj_offsets": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp]),
     "muz_traj_pack": (ctypes.c_int, [MuzTraj, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, MuzTraj, vp, vp]),
     "muz_ring_save_packed": (ctypes.c_int, [MuzRing, MuzTraj, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,

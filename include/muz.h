@@ -542,6 +542,40 @@ int muz_ring_sample(muz_ring ring, const int32_t* ep_idx, const int32_t* t_start
                     int32_t td_steps, int32_t bootstrap_value_target, const double* gamma_pow, muz_sample out,
                     void* stream);
 
+/* ---- TicTacToe (config (a): CPU plumbing; TicTacToe/TicTacToeV2.py, TicTacToe/mcts.py, eval.py) -------
+ * Host code (no GPU).  The reference's jax keys are replaced by counter streams (csrc/tictactoe.cpp;
+ * restated by oracle/tictactoe.py); tree arithmetic is double. */
+typedef struct muz_ttt_state {
+  int8_t board[9];        /* row-major 3x3: 0 empty, 1 / -1 players */
+  int8_t current_player;  /* 1 or -1 */
+  int8_t reward;
+  uint8_t done;
+  int8_t memory[6];       /* [player (1 -> row 0, -1 -> row 1)][last 3 moves, oldest first], -1 = none */
+} muz_ttt_state;
+
+typedef struct muz_ttt_policy_out {
+  int32_t action;             /* categorical(log(action_weights) / temperature) */
+  int32_t visits[9];          /* root children visit counts */
+  double action_weights[9];   /* visit_probs */
+  double value;               /* root node value */
+} muz_ttt_policy_out;
+
+/* env_reset (TicTacToeV2.py:37-44). */
+int muz_ttt_reset(muz_ttt_state* state);
+/* env_step (46-76) with its quirks (see oracle/tictactoe.py); action 0..8. */
+int muz_ttt_step(muz_ttt_state* state, int32_t action, int8_t* reward, uint8_t* done);
+/* policy_function (97-104) -> logits[9]. */
+int muz_ttt_policy_logits(const muz_ttt_state* state, double* logits);
+/* value_function / rollout (106-123) with the counter stream (seed, eval_id). */
+int muz_ttt_rollout(const muz_ttt_state* state, uint64_t seed, uint32_t eval_id, double* value);
+/* run_mcts (mcts.py:9-23): mctx.muzero_policy, rollout values, qtransform_by_min_max(-1, 1). */
+int muz_ttt_muzero_policy(const muz_ttt_state* root, int32_t num_simulations, int32_t max_depth, double temperature,
+                          uint64_t seed, int32_t turn, muz_ttt_policy_out* out);
+/* eval.py:97-125 / 252-276: MCTS player (argmax of action_weights over empty cells) vs uniform random
+ * player; result = winner * mcts_player, 0 at the ply limit. */
+int muz_ttt_match(int32_t mcts_player, int32_t num_simulations, uint64_t seed, int32_t game, int32_t limit,
+                  int32_t* result);
+
 /* ---- trajectory transfer (actors -> learner; north star: RCCL gather into one learner rank) ------
  * The reference moves finished games device -> host with np.array and copies them slot by slot
  * (vec_replay_buffer.py:36-61).  Here an actor PACKS its games' [0, idx) steps into contiguous rows

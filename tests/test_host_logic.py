@@ -46,7 +46,8 @@ def test_ctypes_struct_layout_matches_header():
                "muz_search_cfg": L.MuzSearchCfg, "muz_classic_soa": L.MuzClassicSoA, "muz_traj": L.MuzTraj,
                "muz_sp_stats": L.MuzSpStats, "muz_ring": L.MuzRing, "muz_sample": L.MuzSample,
                "muz_sdyn_w": L.MuzSdynW, "muz_classic_net_w": L.MuzClassicNetW, "muz_stoch_cfg": L.MuzStochCfg,
-               "muz_traj_chance": L.MuzTrajChance, "muz_dog_soa": L.MuzDogSoA}
+               "muz_traj_chance": L.MuzTrajChance, "muz_dog_soa": L.MuzDogSoA,
+               "muz_ttt_state": L.MuzTttState, "muz_ttt_policy_out": L.MuzTttPolicyOut}
     src = "#include <stdio.h>\n#include <stddef.h>\n#include \"muz.h\"\nint main(){\n"
     for cname in structs:
         src += f'printf("{cname} %zu\\n", sizeof({cname}));\n'
