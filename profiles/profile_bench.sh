@@ -14,7 +14,7 @@ cat $O/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gumbel_search -d $O/pmc_fetch -o run \
-  --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || { tail -20 $O/pmc_fetch.log; exit 1; }
+  --output-format csv -- python3 bench.py --steps 1 --warmup 0 --games 8192 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || { tail -20 $O/pmc_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_gumbel_search -d $O/pmc_write -o run \
-  --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_write.log 2>&1 || { tail -20 $O/pmc_write.log; exit 1; }
+  --output-format csv -- python3 bench.py --steps 1 --warmup 0 --games 8192 --no-cpu-baseline > $O/pmc_write.log 2>&1 || { tail -20 $O/pmc_write.log; exit 1; }
 echo profile-done
