@@ -79,6 +79,20 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // acc[t] += A[16 rows][K] @ Wgroup[K][NT*16]  (KB = K/16 k-blocks; Wg = packed weights of this group).
 // b0 / b1 hold k-blocks 0 and 1 on entry.  Weights for k-blocks kb+1 and kb+2 are in flight while kb is
 // multiplied (3-deep register ring, written as a 3-way unrolled loop so every index is static).
+// Tree traffic (node embeddings, children arrays) is streamed with non-temporal hints so the weights
+// (3.8 MB, read by every simulation of every tile) keep the 4 MB L2 of each XCD (tuning knob).
+#ifndef MUZ_TREE_NT
+#define MUZ_TREE_NT 0   // measured: no gain on MI355X (the weights stay resident either way)
+#endif
+template <class P, class V>
+__device__ __forceinline__ void tree_st(P* p, V v) {
+  if constexpr (MUZ_TREE_NT) __builtin_nontemporal_store(v, p); else *p = v;
+}
+template <class P>
+__device__ __forceinline__ P tree_ld(const P* p) {
+  if constexpr (MUZ_TREE_NT) return __builtin_nontemporal_load(p); else return *p;
+}
+
 #ifndef MUZ_RING_DEPTH
 #define MUZ_RING_DEPTH 2   // k-blocks of weights in flight ahead of the one being multiplied (2 or 3)
 #endif
@@ -576,7 +590,7 @@ __device__ __forceinline__ DynIn dyn_load(const AS4 muz_dyn_w& D, int A, const A
 #pragma unroll
   for (int i = 0; i < RV::V; ++i) {
     const int c = RV::col(sub, i);
-    in.lat[i] = lat ? *reinterpret_cast<const AS1 f32x4*>(lat + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    in.lat[i] = lat ? tree_ld(reinterpret_cast<const AS1 f32x4*>(lat + c)) : f32x4{0.f, 0.f, 0.f, 0.f};
     in.sc[i] = film[c >> 2];
     in.sh[i] = film[(LAT + c) >> 2];
   }

@@ -229,12 +229,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     Kid k;
     const size_t e = T.ca(g, node, ai);
     k.ok = ok;
-    k.prior = T.prior()[e];
-    k.value = T.value()[e];
-    k.reward = T.reward()[e];
-    k.disc = T.disc()[e];
-    k.visits = ok ? T.visits()[e] : 0;
-    k.index = T.index()[e];
+    k.prior = tree_ld(T.prior() + e);
+    k.value = tree_ld(T.value() + e);
+    k.reward = tree_ld(T.reward() + e);
+    k.disc = tree_ld(T.disc() + e);
+    k.visits = ok ? tree_ld(T.visits() + e) : 0;
+    k.index = tree_ld(T.index() + e);
     return k;
   };
 
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     const int nx = s_next[row];
     if (valid) {
       AS1 float* ne = T.e(g, nx);
-      for (int c = a; c < LAT; c += kRowLanes) ne[c] = ar.T[row * LD + c];
+      for (int c = a; c < LAT; c += kRowLanes) tree_st(ne + c, ar.T[row * LD + c]);
     }
     // no barrier: pred16 reads ar.T in its first pass and overwrites it only after its first SYNC
     ST(ST_TREE);
@@ -321,13 +321,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
       const bool fresh = nx == sim + 1;
       if (ok) {
         const size_t nb = T.ca(g, nx, a);
-        T.prior()[nb] = ar.U[row * LD + a];
+        tree_st(T.prior() + nb, ar.U[row * LD + a]);
         if (fresh) {
-          T.index()[nb] = -1;
-          T.visits()[nb] = 0;
-          T.value()[nb] = 0.f;
-          T.reward()[nb] = 0.f;
-          T.disc()[nb] = 0.f;
+          tree_st(T.index() + nb, -1);
+          tree_st(T.visits() + nb, 0);
+          tree_st(T.value() + nb, 0.f);
+          tree_st(T.reward() + nb, 0.f);
+          tree_st(T.disc() + nb, 0.f);
         }
       }
       const int par = s_parent[row], pa = s_act[row];
@@ -340,9 +340,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
         const float v = ar.v0[row], rw = ar.v1[row], dc = ar.v2[row];
         if (par != 0) {
           const size_t eb = T.ca(g, par, pa);
-          T.index()[eb] = nx;
-          T.reward()[eb] = rw;
-          T.disc()[eb] = dc;
+          tree_st(T.index() + eb, nx);
+          tree_st(T.reward() + eb, rw);
+          tree_st(T.disc() + eb, dc);
         }
         s_raw[row][nx] = v;
         s_val[row][nx] = v;
@@ -361,8 +361,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
           const float pv = (s_val[row][parent] * (float)cnt + leaf) / ((float)cnt + 1.0f);
           if (lvl > 0) {
             const size_t ei = T.ca(g, parent, pact);
-            T.value()[ei] = s_val[row][idx];
-            T.visits()[ei] = p_cvis[row][lvl] + 1;
+            tree_st(T.value() + ei, s_val[row][idx]);
+            tree_st(T.visits() + ei, p_cvis[row][lvl] + 1);
           } else {
             s_rootv[row] = s_val[row][idx];
           }

@@ -1,0 +1,59 @@
+"""Learner on the GPU, wired to the device ring and the self-play engine (config (e) loop, small)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nets as ON
+
+pytestmark = pytest.mark.gpu
+
+
+def _mods():
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import game_agent as GA
+    from exploring_muzero_on_dog_amd import learner as L
+    from exploring_muzero_on_dog_amd import nets as N
+    from exploring_muzero_on_dog_amd import replay as R
+    return E, GA, L, N, R
+
+
+def test_learner_loop_and_weight_push(cuda):
+    E, GA, L, N, R = _mods()
+    P = 2
+    C = E.num_channels(P)
+    params = ON.init_params(C, seed=8)
+    net = N.DeviceNet(params, C)
+    eng = GA.SelfPlayEngine(net, 32, num_players=P, max_steps=60, num_simulations=4, max_depth=4)
+    ring = R.VectorizedReplayBuffer(256, 16, 5, 10, obs_shape=(C, 56), max_episode_length=60,
+                                    rng=np.random.RandomState(0))
+    learner = L.Learner(params, C, unroll_steps=5)
+    hist = L.train_loop(learner, eng, ring, iterations=2, train_steps=3, games_per_iteration=48, warmup_calls=1)
+    assert len(hist) == 2 and all(np.isfinite(h["total_loss"]) for h in hist)
+    # the engine now runs the learner's weights: its root inference equals the torch forward
+    obs = torch.from_numpy(np.random.default_rng(1).integers(0, 3, (40, C, 56)).astype(np.float32)).cuda()
+    lg, v, e = N.root_inference_fn(eng.net, obs)
+    with torch.no_grad():
+        te = learner.nets.representation(obs)
+        tl, tv = learner.nets.prediction(te)
+    assert (e - te).abs().max().item() < 2e-5
+    assert (lg - tl).abs().max().item() < 2e-5 and (v - tv[:, 0]).abs().max().item() < 2e-5
+    # and keeps playing
+    buf = eng.play_stream(40, seed=3)
+    assert int(buf["idx"].min()) > 0
+
+
+def test_learner_overfits_one_batch(cuda):
+    E, GA, L, N, R = _mods()
+    C = E.num_channels(2)
+    params = ON.init_params(C, seed=9)
+    net = N.DeviceNet(params, C)
+    eng = GA.SelfPlayEngine(net, 32, num_players=2, max_steps=80, num_simulations=4, max_depth=4)
+    ring = R.VectorizedReplayBuffer(64, 32, 5, 10, obs_shape=(C, 56), max_episode_length=80,
+                                    rng=np.random.RandomState(2))
+    ring.save_games_from_buffers(eng.play(seed=1))
+    batch = ring.sample_batch()
+    learner = L.Learner(params, C, unroll_steps=5)
+    first = float(learner.train_step(batch)["total_loss"])
+    for _ in range(60):
+        last = float(learner.train_step(batch)["total_loss"])
+    assert last < 0.8 * first, (first, last)     # measured 4.07 -> 2.91 after 40 steps
