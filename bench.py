@@ -66,7 +66,8 @@ def parse():
     ap.add_argument("--games", type=int, default=-1,
                     help="det: games per step streamed through the --batch lanes (default 8 x batch; 0 = one "
                          "batch of --batch games, the reference's play_n_games_v3 call)")
-    ap.add_argument("--workload", choices=("det", "classic", "dog"), default="det",
+    ap.add_argument("--train-steps", type=int, default=2500, help="train workload: learner steps per iteration")
+    ap.add_argument("--workload", choices=("det", "classic", "dog", "train"), default="det",
                     help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
     args = ap.parse_args()
     if args.workload == "dog" and args.batch == BATCH:
@@ -327,8 +328,95 @@ def run_classic(args):
         dist.destroy_process_group()
 
 
+def run_train(args):
+    """Config (e): the det-MADN training loop (train_with_reward.py:167-311) at its hyper-parameters --
+    4 players, 1500 games per iteration (S=100, D=50, max_len 550), replay ring 20000 x 550, batch 128,
+    unroll 10, td 50, 2500 learner steps per iteration.  One bench step = one iteration.
+    1 GPU: actor and learner share it.  N GPUs: ranks 0..N-2 are actors (the games split between them,
+    packed and gathered to the learner over RCCL point-to-point), rank N-1 is the learner, which
+    broadcasts the new weights back (one collective) -- SURVEY §8(e)."""
+    import numpy as np
+    import torch
+    rank, world, dist, device = setup(args)
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import game_agent as GA
+    from exploring_muzero_on_dog_amd import learner as LR
+    from exploring_muzero_on_dog_amd import nets as N
+    from exploring_muzero_on_dog_amd import replay as R
+    from exploring_muzero_on_dog_amd import transfer as TR
+    P, GAMES, T, S, D = 4, 1500, 550, 100, 50
+    C = E.num_channels(P)
+    params = N.init_muzero_params(42, C)
+    net = N.DeviceNet(params, C, device=device)
+    learner_rank = world - 1
+    actors = max(world - 1, 1)
+    is_actor = world == 1 or rank != learner_rank
+    is_learner = world == 1 or rank == learner_rank
+    games = (GAMES + actors - 1) // actors
+    eng = GA.SelfPlayEngine(net, games, num_players=P, max_steps=T, num_simulations=S, max_depth=D,
+                            device=device) if is_actor else None
+    ring = R.VectorizedReplayBuffer(20000, 128, 10, 50, obs_shape=(C, 56), max_episode_length=T, device=device,
+                                    rng=np.random.RandomState(rank)) if is_learner else None
+    learner = LR.Learner(params, C, unroll_steps=10, device=device, graph=True) if is_learner else None
+    stats = {"env_steps": 0, "train_steps": 0}
+
+    def iteration(seed, train_steps):
+        buf = eng.play_stream(games, seed=seed + 7919 * rank, temperature=1.0) if is_actor else None
+        if is_actor:
+            stats["env_steps"] += int(buf["idx"].sum().item())
+        if world == 1:
+            ring.save_games_from_buffers(buf)
+        else:
+            packed = TR.pack(buf) if is_actor else _empty_packed(C, device)
+            got = TR.gather_packed(packed, C, 24, dst=learner_rank)
+            if is_learner:
+                for r, p in enumerate(got):
+                    if r != learner_rank:
+                        ring.save_packed(p)
+        if is_learner:
+            for _ in range(train_steps):
+                learner.train_step(ring.sample_batch())
+            stats["train_steps"] += train_steps
+            learner.push_to(net)
+        if world > 1:
+            TR.broadcast_weights(net, src=learner_rank)
+
+    def _empty_packed(C, dev):
+        z = {name: torch.empty((0,) + shp, dtype=dt, device=dev) for name, dt, shp in TR.fields(C, 24, False)}
+        z["idx"] = torch.empty((0,), dtype=torch.int32, device=dev)
+        z["row_offset"] = torch.empty((0,), dtype=torch.int64, device=dev)
+        return z
+
+    for w in range(max(args.warmup, 1)):       # fills the ring and captures the learner's HIP graph
+        iteration(100 * w, 2)
+    stats.update(env_steps=0, train_steps=0)
+    elapsed = timed_region(dist, lambda k: iteration(1000 + k, args.train_steps), args.steps)
+    (env_steps, train_steps), elapsed = sum_max(dist, device, [stats["env_steps"], stats["train_steps"]], elapsed)
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    out = {
+        "metric": "MuZero training iterations/sec, det-MADN 4p (config e: self-play + replay + learner)",
+        "value": round(args.steps / elapsed, 5), "unit": "iterations/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 1), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (self-generated games, seeded random fp32 weights)",
+        "config": {"workload": f"train_with_reward.py config: {GAMES} games/iter (S={S}, D={D}, max_len {T}), "
+                               f"ring 20000, batch 128, unroll 10, td 50, {args.train_steps} learner steps/iter",
+                   "parallelism": "1 GPU (actor + learner)" if world == 1 else
+                   f"{world - 1} actor ranks + 1 learner rank (packed-trajectory gather, weight broadcast)"},
+        "env_steps_per_s": round(env_steps / elapsed, 1), "train_steps_per_s": round(train_steps / elapsed, 2),
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload == "train":
+        return run_train(args)
     if args.workload == "dog":
         return run_dog(args)
     if args.workload == "classic":

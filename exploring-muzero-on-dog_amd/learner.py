@@ -50,13 +50,14 @@ class MuZeroNets:
 
     # ---- layers (oracle/nets.py restates the same Flax semantics) ----------------------------------
     def _dense(self, name, x):
+        if x.dim() == 2:
+            return torch.addmm(self.p[f"{name}/bias"], x, self.p[f"{name}/kernel"])
         return x @ self.p[f"{name}/kernel"] + self.p[f"{name}/bias"]
 
     def _ln(self, name, x):
-        mean = x.mean(-1, keepdim=True)
-        mean2 = (x * x).mean(-1, keepdim=True)
-        var = torch.clamp(mean2 - mean * mean, min=0.0)
-        return (x - mean) * (torch.rsqrt(var + EPS_LN) * self.p[f"{name}/scale"]) + self.p[f"{name}/bias"]
+        # Flax computes the variance as E[x^2] - E[x]^2 (fast variance); the fused two-pass kernel agrees to
+        # ~1e-7 relative on these activations (tests/test_learner.py holds the forward to 1e-5)
+        return F.layer_norm(x, (x.shape[-1],), self.p[f"{name}/scale"], self.p[f"{name}/bias"], EPS_LN)
 
     def _conv(self, name, x):
         """Flax Conv 'SAME', stride 1, NWC input [B, W, Cin] -> [B, W, Cout]."""
@@ -174,49 +175,118 @@ def lr_schedule(step: int, lr0: float = 0.005, steps_per_iteration: int = 2500) 
     return lr
 
 
-class AdamW:
-    """optax.chain(clip_by_global_norm(5.0), adamw(schedule, b1 0.9, b2 0.999, eps 1e-8, weight_decay 1e-4))."""
+def _lr_from_count(count: torch.Tensor, lr0=0.005, steps_per_iteration=2500) -> torch.Tensor:
+    """lr_schedule on a device step counter (no host sync: capturable in a HIP graph)."""
+    lr = torch.full_like(count, lr0)
+    for boundary, scale in ((30, 0.2), (60, 0.2), (85, 0.5)):
+        lr = torch.where(count >= boundary * steps_per_iteration, lr * scale, lr)
+    return lr
 
-    def __init__(self, params: list, max_norm=5.0, b1=0.9, b2=0.999, eps=1e-8, wd=1e-4, schedule=lr_schedule):
+
+class AdamW:
+    """optax.chain(clip_by_global_norm(5.0), adamw(schedule, b1 0.9, b2 0.999, eps 1e-8, weight_decay 1e-4)).
+
+    Multi-tensor (torch._foreach_*) updates with every scalar (step count, learning rate, bias corrections,
+    clip factor) kept on the device, so a whole train step can be captured in one HIP graph."""
+
+    def __init__(self, params: list, max_norm=5.0, b1=0.9, b2=0.999, eps=1e-8, wd=1e-4, lr0=0.005,
+                 steps_per_iteration=2500):
         self.params = params
         self.mu = [torch.zeros_like(p) for p in params]
         self.nu = [torch.zeros_like(p) for p in params]
-        self.count = 0
-        self.max_norm, self.b1, self.b2, self.eps, self.wd, self.schedule = max_norm, b1, b2, eps, wd, schedule
+        dev, dt = params[0].device, params[0].dtype
+        self.count = torch.zeros((), dtype=torch.float64, device=dev)
+        self.max_norm, self.b1, self.b2, self.eps, self.wd = max_norm, b1, b2, eps, wd
+        self.lr0, self.spi = lr0, steps_per_iteration
+        self.dt = dt
 
     @torch.no_grad()
     def step(self):
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
-        g_norm = torch.sqrt(sum(torch.sum(g * g) for g in grads))
-        lr = self.schedule(self.count)
-        self.count += 1
-        c1, c2 = 1.0 - self.b1 ** self.count, 1.0 - self.b2 ** self.count
-        for p, g, m, v in zip(self.params, grads, self.mu, self.nu):
-            g = torch.where(g_norm < self.max_norm, g, g / g_norm * self.max_norm)
-            m.mul_(self.b1).add_((1 - self.b1) * g)
-            v.mul_(self.b2).add_((1 - self.b2) * (g * g))
-            u = (m / c1) / (torch.sqrt(v / c2) + self.eps) + self.wd * p
-            p.sub_(lr * u)
+        g_norm = torch.sqrt(torch.stack([torch.sum(g * g) for g in grads]).sum())
+        trigger = g_norm < self.max_norm
+        denom = torch.where(trigger, torch.ones_like(g_norm), g_norm)
+        mult = torch.where(trigger, torch.ones_like(g_norm), torch.full_like(g_norm, self.max_norm))
+        g = torch._foreach_div(grads, denom)                # clip_by_global_norm: g / ||g|| * max_norm
+        torch._foreach_mul_(g, mult)
+        lr = _lr_from_count(self.count, self.lr0, self.spi).to(self.dt)
+        self.count.add_(1.0)
+        c1 = (1.0 - torch.pow(torch.full_like(self.count, self.b1), self.count)).to(self.dt)
+        c2 = (1.0 - torch.pow(torch.full_like(self.count, self.b2), self.count)).to(self.dt)
+        torch._foreach_mul_(self.mu, self.b1)
+        torch._foreach_add_(self.mu, g, alpha=1.0 - self.b1)
+        gg = torch._foreach_mul(g, g)
+        torch._foreach_mul_(self.nu, self.b2)
+        torch._foreach_add_(self.nu, gg, alpha=1.0 - self.b2)
+        mh = torch._foreach_div(self.mu, c1)
+        vh = torch._foreach_div(self.nu, c2)
+        torch._foreach_sqrt_(vh)
+        torch._foreach_add_(vh, self.eps)
+        u = torch._foreach_div(mh, vh)
+        torch._foreach_add_(u, self.params, alpha=self.wd)
+        torch._foreach_mul_(u, lr)
+        torch._foreach_sub_(self.params, u)
         return g_norm
 
 
 class Learner:
-    """train_step (train_with_reward.py:148-162) on batches sampled from the device ring."""
+    """train_step (train_with_reward.py:148-162) on batches sampled from the device ring.
+
+    ``graph=True`` captures forward + backward + optimizer of one step into a HIP graph on the first call
+    (static batch buffers; later steps copy the batch in and replay): the step is hundreds of small
+    kernels at batch 128, so replaying them as one graph removes the launch overhead."""
+
+    KEYS = ("observations", "actions", "rewards", "policies", "masks", "target_values", "discount_targets")
 
     def __init__(self, params: dict, obs_channels: int, num_actions: int = 24, unroll_steps: int = 10,
-                 device="cuda", **opt):
+                 device="cuda", graph: bool = False, **opt):
         self.nets = MuZeroNets(params, obs_channels, num_actions, device)
         self.opt = AdamW(self.nets.parameters(), **opt)
         self.unroll_steps = int(unroll_steps)
+        self.graph = bool(graph)
+        self._g = None
 
-    def train_step(self, batch: dict) -> dict:
-        for p in self.nets.parameters():
-            p.grad = None
+    def _step(self, batch):
         loss, (v, pl, d, r) = loss_fn(self.nets, batch, self.unroll_steps)
         loss.backward()
         self.opt.step()
         return {"total_loss": loss.detach(), "v_loss": v.detach(), "p_loss": pl.detach(), "d_loss": d.detach(),
                 "r_loss": r.detach()}
+
+    def train_step(self, batch: dict) -> dict:
+        if not self.graph:
+            for p in self.nets.parameters():
+                p.grad = None
+            return self._step(batch)
+        if self._g is None:
+            self._static = {k: batch[k].clone() for k in self.KEYS}
+            # capture-time allocations come from a private pool; warm up the kernels on a side stream first
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                state = ([p.detach().clone() for p in self.nets.parameters()], [m.clone() for m in self.opt.mu],
+                         [v.clone() for v in self.opt.nu], self.opt.count.clone())
+                for p in self.nets.parameters():
+                    p.grad = None
+                self._step(self._static)
+                with torch.no_grad():                  # undo the warm-up update
+                    for p, s in zip(self.nets.parameters(), state[0]):
+                        p.copy_(s)
+                    for m, s in zip(self.opt.mu, state[1]):
+                        m.copy_(s)
+                    for v, s in zip(self.opt.nu, state[2]):
+                        v.copy_(s)
+                    self.opt.count.copy_(state[3])
+            torch.cuda.current_stream().wait_stream(side)
+            for p in self.nets.parameters():
+                p.grad = None
+            self._g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g):
+                self._out = self._step(self._static)
+        for k in self.KEYS:
+            self._static[k].copy_(batch[k])
+        self._g.replay()
+        return self._out
 
     def push_to(self, net: "N.DeviceNet"):
         """Pack the current parameters into the self-play engine's arena (same layout) in place."""

@@ -104,6 +104,8 @@ def test_adamw_step_matches_oracle(clip):
     params = {f"w{i}": rng.standard_normal((5, 7)).astype(np.float32) for i in range(3)}
     tp = [torch.tensor(params[k], requires_grad=True) for k in params]
     opt = L.AdamW(tp)
+    assert all(L.lr_schedule(s) == float(L._lr_from_count(torch.tensor(float(s), dtype=torch.float64)))
+               for s in (0, 74999, 75000, 149999, 150000, 212500, 10 ** 6))
     ora = OL.AdamW(params)
     cur = dict(params)
     for step in range(4):
