@@ -290,12 +290,17 @@ def run_classic(args):
     net = ST.DeviceClassicNet(ST.init_classic_params(C, seed=0), C, device=device)
     eng = GS.StochasticSelfPlayEngine(net, args.batch, num_players=CLASSIC_PLAYERS, max_steps=args.max_steps,
                                       num_simulations=args.sims, max_depth=args.depth, device=device)
+    def play(seed):
+        if args.games:
+            return eng.play_stream(args.games, seed=seed, temperature=TEMP)
+        return eng.play(seed=seed, temperature=TEMP)
+
     for w in range(args.warmup):
-        eng.play(seed=10_000 * rank + w, temperature=TEMP)
+        play(10_000 * rank + w)
     acc = {"steps": 0, "searches": 0, "search_ms": 0.0, "turns": 0}
 
     def step(k):
-        buf = eng.play(seed=10_000 * rank + 1000 + k, temperature=TEMP)
+        buf = play(10_000 * rank + 1000 + k)
         st = eng.last_stats
         acc["steps"] += int(buf["idx"].sum().item())
         acc["searches"] += st["searches"]
@@ -316,7 +321,9 @@ def run_classic(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (self-generated games, seeded random fp32 weights)",
         "config": {"workload": f"classic MADN {CLASSIC_PLAYERS}p teams self-play, {args.batch} games/GPU, "
-                               f"Stochastic MuZero S={args.sims} D={args.depth}, max_steps={args.max_steps}",
+                               f"Stochastic MuZero S={args.sims} D={args.depth}, max_steps={args.max_steps}"
+                               + (f", {args.games} games per step streamed through the {args.batch} lanes"
+                                  if args.games else ""), "games_per_step": args.games or args.batch,
                    "games_per_gpu": args.batch, "num_simulations": args.sims, "max_depth": args.depth,
                    "parallelism": f"independent games, {world} rank(s)"},
         "sims_per_s": round(searches * args.sims / elapsed, 1),

@@ -37,6 +37,9 @@ struct SArgs {
   float dir_frac, dir_alpha, pb_c_init, pb_c_base, temperature;
   unsigned long long seed;
   int turn;
+  // optional noise keys of a self-play driver (see SearchArgs): game id key_game[lane], turn key_turn[game id]
+  const int32_t* key_game = nullptr;
+  const int32_t* key_turn = nullptr;
 };
 SArgs make_sargs(const muz_stoch_cfg& cfg, int A);
 int launch_stochastic_search(const muz_classic_net_w& w, const SArgs& sa, const float* root_logits,

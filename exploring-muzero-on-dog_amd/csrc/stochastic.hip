@@ -212,7 +212,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_stochastic_search(
   const bool valid = g < n;
   const bool ok = a < kAp;                 // a real child slot
   const int ai = ok ? a : 0;
-  const int gid = valid ? (game_id ? game_id[g] : g) : 0;
+  const int lane = valid ? (game_id ? game_id[g] : g) : 0;
+  const int gid = (valid && sa.key_game) ? sa.key_game[lane] : lane;
+  const int gturn = (valid && sa.key_turn) ? sa.key_turn[gid] : sa.turn;
 
   // ---------------- root (policies.py stochastic_muzero_policy: noise, mask, pad with C chance slots)
   unsigned lb = 0;
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_stochastic_search(
     if (dirichlet_in) {
       dn = act_lane ? dirichlet_in[(size_t)g * A + a] : 0.f;
     } else {
-      const float gm = act_lane ? gamma_sample(sa.dir_alpha, mix64(game_key(sa.seed ^ 0x5DEECE66Dull, gid, sa.turn) ^ (unsigned long long)(a + 1))) : 0.f;
+      const float gm = act_lane ? gamma_sample(sa.dir_alpha, mix64(game_key(sa.seed ^ 0x5DEECE66Dull, gid, gturn) ^ (unsigned long long)(a + 1))) : 0.f;
       dn = gm / row_sum(gm);
     }
     const float noisy = (1.f - sa.dir_frac) * pr + sa.dir_frac * dn;
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_stochastic_search(
           const float hi = fmaxf(nv, row_max(ok ? safe : -INFINITY));
           const float vs = ((vis ? q : lo) - lo) / fmaxf(hi - lo, 1e-8f);
           const float ps = sqrtf((float)N) * pb_c * p / (float)(k.visits + 1);
-          const float tb = tiebreak_uniform(sa.seed, gid, sa.turn, sim, depth, ai);
+          const float tb = tiebreak_uniform(sa.seed, gid, gturn, sim, depth, ai);
           sc = vs + ps + 1e-7f * tb;
           if (depth == 0 && (a >= A || ((lb >> a) & 1u) == 0u)) sc = -INFINITY;
           if (!ok) sc = -INFINITY;
@@ -466,7 +468,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_stochastic_search(
     const float w = tot > 0 ? (float)vc / (float)max(tot, 1) : 1.0f / (float)A;
     float lw = act_lane ? logf(w) : -INFINITY;
     lw = (lw - row_max(lw)) / fmaxf(kTinyF, sa.temperature);
-    const float gmb = act_lane ? (gumbel_in ? gumbel_in[(size_t)g * A + a] : gumbel_noise(sa.seed ^ 0xC2B2AE3D27D4EB4Full, gid, sa.turn, a)) : 0.f;
+    const float gmb = act_lane ? (gumbel_in ? gumbel_in[(size_t)g * A + a] : gumbel_noise(sa.seed ^ 0xC2B2AE3D27D4EB4Full, gid, gturn, a)) : 0.f;
     float sc = act_lane ? lw + gmb : -INFINITY;
     int bi = a;
     srow_argmax(sc, bi);

@@ -74,6 +74,35 @@ class StochasticSelfPlayEngine:
         return self.buffers
 
 
+    def play_stream(self, num_games: int, seed: int, temperature: float = 1.0, dirichlet_fraction: float = 0.25,
+                    stream=None, timing: bool = True) -> dict:
+        """``num_games`` games through this engine's lanes (muz_classic_selfplay_stream); game k's record
+        equals game k of ``play`` on a batch of ``num_games``."""
+        lib = _L.load()
+        num_games = int(num_games)
+        if getattr(self, "_sbuf_n", None) != num_games:
+            z = dict(device=self.buffers["act"].device)
+            self._sbuf = {k: torch.empty((num_games,) + tuple(v.shape[1:]), dtype=v.dtype, **z)
+                          for k, v in self.buffers.items()}
+            self._sbuf_n = num_games
+        cfg = ST.make_cfg(self.S, self.D, temperature=temperature, seed=seed, dirichlet_fraction=dirichlet_fraction)
+        t = _L.MuzTraj()
+        for k in ("obs", "act", "rew", "val", "pol", "mask", "player", "team", "discount", "idx"):
+            setattr(t, k, self._sbuf[k].data_ptr())
+        t.max_steps = self.T
+        ch = _L.MuzTrajChance()
+        ch.dice, ch.dice_dist = self._sbuf["dice"].data_ptr(), self._sbuf["dice_dist"].data_ptr()
+        st = _L.MuzSpStats()
+        _L.check(lib.muz_classic_selfplay_stream(self.rules, self.net.w, ctypes.byref(cfg), self.state.soa(), t, ch,
+                                                 num_games, self.n, _L.ptr(self.workspace), _L.nbytes(self.workspace),
+                                                 ctypes.byref(st) if timing else None, _L.stream_ptr(stream)),
+                 "muz_classic_selfplay_stream")
+        self.last_stats = {"turns": st.turns, "searches": st.searches, "search_ms": st.search_ms,
+                           "total_ms": st.total_ms} if timing else None
+        self.last_turns = st.turns if timing else -1
+        return self._sbuf
+
+
 def play_n_games_v3(net: ST.DeviceClassicNet, seed: int, num_envs: int, num_simulation: int, max_depth: int,
                     max_steps: int, temp: float) -> dict:
     """game_agent_stochastic.py:234-257 (the reset seeds only feed jax's unused random start)."""

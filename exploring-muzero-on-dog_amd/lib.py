@@ -242,6 +242,10 @@ SIGNATURES = {
     "muz_classic_selfplay": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzClassicNetW),
                                             ctypes.POINTER(MuzStochCfg), MuzClassicSoA, MuzTraj, MuzTrajChance,
                                             ctypes.c_int32, vp, ctypes.c_int64, ctypes.POINTER(MuzSpStats), vp]),
+    "muz_classic_selfplay_stream": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzClassicNetW),
+                                                   ctypes.POINTER(MuzStochCfg), MuzClassicSoA, MuzTraj, MuzTrajChance,
+                                                   ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_int64,
+                                                   ctypes.POINTER(MuzSpStats), vp]),
     "muz_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzNetW), ctypes.c_void_p]),
     "muz_nets_root_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "muz_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzNetW), vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp,

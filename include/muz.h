@@ -487,6 +487,14 @@ int muz_classic_selfplay(const muz_rules* rules /*host*/, const muz_classic_net_
                          muz_traj_chance chance, int32_t n, void* workspace, int64_t workspace_bytes,
                          muz_sp_stats* stats /*host*/, void* stream);
 
+/* muz_classic_selfplay streamed: num_games games through `lanes` refilled lanes (see
+ * muz_detmadn_selfplay_stream); dice, Dirichlet, tie-break and final-action noise are keyed by game number
+ * and the game's own step, so game k's record equals game k of a muz_classic_selfplay batch. */
+int muz_classic_selfplay_stream(const muz_rules* rules /*host*/, const muz_classic_net_w* w /*host*/,
+                                const muz_stoch_cfg* cfg /*host*/, muz_classic_soa state, muz_traj traj,
+                                muz_traj_chance chance, int32_t num_games, int32_t lanes, void* workspace,
+                                int64_t workspace_bytes, muz_sp_stats* stats /*host*/, void* stream);
+
 /* ---- device replay ring (MuZero_det_MADN/vec_replay_buffer.py) ------------------------------
  * The reference's VectorizedReplayBuffer keeps [capacity][T] host NumPy arrays (obs fp32, 84 GB at
  * capacity 20000, T 550, C 34).  Here the ring lives in HBM, obs int8 (values 0..4, exact):

@@ -81,3 +81,22 @@ def test_classic_selfplay_config_c_shape_runs(cuda):
     dice = b1["dice"].cpu().numpy()
     assert ((dice >= 1) & (dice <= 6))[live].all()
     assert np.allclose(b1["dice_dist"].cpu().numpy().sum(-1)[live], 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("games,lanes,T", [(30, 12, 200), (25, 8, 40)])
+def test_classic_stream_equals_batch(cuda, games, lanes, T):
+    """muz_classic_selfplay_stream == muz_classic_selfplay on a batch of `games` (dice, Dirichlet, tie-break
+    and final noise keyed by game number and own step)."""
+    from oracle import classic_nets as CN
+    from exploring_muzero_on_dog_amd import classic as CL
+    from exploring_muzero_on_dog_amd import game_agent_stochastic as GS
+    from exploring_muzero_on_dog_amd import stochastic as S
+    C = CL.num_channels(4)
+    net = S.DeviceClassicNet(CN.init_params(C, seed=12), C)
+    batch = GS.StochasticSelfPlayEngine(net, games, max_steps=T, num_simulations=6, max_depth=5)
+    want = {k: v.clone() for k, v in batch.play(31, 1.0).items()}
+    eng = GS.StochasticSelfPlayEngine(net, lanes, max_steps=T, num_simulations=6, max_depth=5)
+    got = eng.play_stream(games, 31, 1.0)
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
+    assert eng.last_stats["searches"] == batch.last_stats["searches"]
