@@ -80,3 +80,59 @@ def test_matches_and_results_md():
     r = T.evaluate(200, 5, seed=1)
     # TicTacToe/results.md: "MCTS (5)" vs random bot 97.10 % wins, 2.70 % losses
     assert r["win"] >= 0.9 and r["loss"] <= 0.08, r
+
+
+# ---- checkpoint I/O + the reference's trained policy (TicTacToe/results.md) --------------------------
+import json  # noqa: E402
+import os  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF_CKPT = "/root/reference/TicTacToe/Checkpoints/TicTacToeV2_imp_net_3000ep_00001lr.params"
+
+
+def _ck():
+    import muzpkg
+    muzpkg.load()
+    from exploring_muzero_on_dog_amd import checkpoint as CK
+    return CK
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CKPT), reason="reference checkpoint not present")
+def test_flax_msgpack_roundtrip_is_byte_exact():
+    CK = _ck()
+    raw = open(REF_CKPT, "rb").read()
+    tree = CK.load_flax_msgpack(raw)
+    assert CK.dumps_flax_msgpack(tree) == raw
+    fx = np.load(os.path.join(GOLDEN, "ttt_imp_net_3000ep.npz"))
+    flat = CK.flatten(tree)
+    assert sorted(k.replace("/", "__") for k in flat) == sorted(fx.files)
+    assert all(np.array_equal(flat[k], fx[k.replace("/", "__")]) for k in flat)
+
+
+def test_trained_policy_reproduces_results_md():
+    """The reference's trained ImprovedTicTacToeNet (3000 episodes) against the random bot through this
+    engine's TicTacToeV2: results.md reports 82.2 % wins (444 / 500 as first player, 378 / 500 as second)."""
+    CK = _ck()
+    T = _T()
+    fx = np.load(os.path.join(GOLDEN, "ttt_imp_net_3000ep.npz"))
+    net = T.PolicyNet(CK.unflatten({k.replace("__", "/"): fx[k] for k in fx.files}))
+    want = json.load(open(os.path.join(GOLDEN, "ttt_imp_net_3000ep_results.json")))
+    r = T.evaluate_trained(net, 2000, seed=1)
+    assert abs(r["win"] - want["win"]) < 0.04, r                       # ~4.7 standard errors at n = 2000
+    assert abs(r["wins_as_first"] / 1000 - 444 / 500) < 0.05, r
+    assert abs(r["wins_as_second"] / 1000 - 378 / 500) < 0.06, r
+
+
+def test_muzero_checkpoint_tree_roundtrip(tmp_path):
+    CK = _ck()
+    from oracle import nets as ON
+    flat = ON.init_params(18, seed=2)
+    tree = CK.flat_to_muzero_tree(flat)
+    p = tmp_path / "m.params"
+    CK.save_flax_msgpack(str(p), tree)
+    back = CK.muzero_tree_to_flat(CK.load_flax_msgpack(str(p)))
+    assert set(back) == set(flat) and all(np.array_equal(back[k], flat[k]) for k in flat)
+    s = tmp_path / "m.safetensors"
+    CK.save_flat(str(s), flat)
+    back = CK.load_flat(str(s))
+    assert all(np.array_equal(back[k], flat[k]) for k in flat)
