@@ -102,3 +102,13 @@ def test_classic_param_shapes_match_oracle():
         assert ST.classic_param_shapes(C) == CN.param_shapes(C)
     a, b = ST.init_classic_params(11, seed=3), CN.init_params(11, seed=3)
     assert list(a) == list(b) and all(np.array_equal(a[k], b[k]) for k in a)
+
+
+def test_eval_z_test():
+    """compare_agents_statistically's two-proportion z-test (evaluate_agent.py:680-693)."""
+    import math
+    from exploring_muzero_on_dog_amd import evaluate as EV
+    r = EV.z_test(600, 500, 1000)
+    se = math.sqrt(0.6 * 0.4 / 1000 + 0.5 * 0.5 / 1000)
+    assert abs(r["z"] - 0.1 / se) < 1e-12 and r["significant"] and 0 < r["p"] < 1e-5
+    assert EV.z_test(0, 0, 100) == {"winrate1": 0.0, "winrate2": 0.0, "z": 0.0, "p": 1.0, "significant": False}
