@@ -34,9 +34,9 @@ class MuZeroNets:
     """Flax-named fp32 parameters of (RepresentationNetwork2, DynamicsNetwork4, PredictionNetwork4)."""
 
     def __init__(self, params: dict, obs_channels: int, num_actions: int = 24, device="cuda",
-                 dtype=torch.float32):
+                 dtype=torch.float32, shapes: dict | None = None):
         self.C, self.A = int(obs_channels), int(num_actions)
-        shapes = N.param_shapes(self.C, self.A)
+        shapes = N.param_shapes(self.C, self.A) if shapes is None else shapes
         if set(shapes) != set(params):
             raise ValueError("parameter names differ from nets.param_shapes")
         self.p = {k: torch.tensor(np.asarray(params[k]).reshape(shapes[k]), dtype=dtype, device=device,
@@ -175,10 +175,15 @@ def lr_schedule(step: int, lr0: float = 0.005, steps_per_iteration: int = 2500) 
     return lr
 
 
-def _lr_from_count(count: torch.Tensor, lr0=0.005, steps_per_iteration=2500) -> torch.Tensor:
+DET_LR_BOUNDARIES = ((30, 0.2), (60, 0.2), (85, 0.5))          # train_with_reward.py:361-368
+CLASSIC_LR_BOUNDARIES = ((40, 0.1), (85, 0.2), (105, 0.5))     # train_stochastic.py:415-422
+
+
+def _lr_from_count(count: torch.Tensor, lr0=0.005, steps_per_iteration=2500,
+                   boundaries=DET_LR_BOUNDARIES) -> torch.Tensor:
     """lr_schedule on a device step counter (no host sync: capturable in a HIP graph)."""
     lr = torch.full_like(count, lr0)
-    for boundary, scale in ((30, 0.2), (60, 0.2), (85, 0.5)):
+    for boundary, scale in boundaries:
         lr = torch.where(count >= boundary * steps_per_iteration, lr * scale, lr)
     return lr
 
@@ -190,14 +195,14 @@ class AdamW:
     clip factor) kept on the device, so a whole train step can be captured in one HIP graph."""
 
     def __init__(self, params: list, max_norm=5.0, b1=0.9, b2=0.999, eps=1e-8, wd=1e-4, lr0=0.005,
-                 steps_per_iteration=2500):
+                 steps_per_iteration=2500, boundaries=DET_LR_BOUNDARIES):
         self.params = params
         self.mu = [torch.zeros_like(p) for p in params]
         self.nu = [torch.zeros_like(p) for p in params]
         dev, dt = params[0].device, params[0].dtype
         self.count = torch.zeros((), dtype=torch.float64, device=dev)
         self.max_norm, self.b1, self.b2, self.eps, self.wd = max_norm, b1, b2, eps, wd
-        self.lr0, self.spi = lr0, steps_per_iteration
+        self.lr0, self.spi, self.boundaries = lr0, steps_per_iteration, boundaries
         self.dt = dt
 
     @torch.no_grad()
@@ -209,7 +214,7 @@ class AdamW:
         mult = torch.where(trigger, torch.ones_like(g_norm), torch.full_like(g_norm, self.max_norm))
         g = torch._foreach_div(grads, denom)                # clip_by_global_norm: g / ||g|| * max_norm
         torch._foreach_mul_(g, mult)
-        lr = _lr_from_count(self.count, self.lr0, self.spi).to(self.dt)
+        lr = _lr_from_count(self.count, self.lr0, self.spi, self.boundaries).to(self.dt)
         self.count.add_(1.0)
         c1 = (1.0 - torch.pow(torch.full_like(self.count, self.b1), self.count)).to(self.dt)
         c2 = (1.0 - torch.pow(torch.full_like(self.count, self.b2), self.count)).to(self.dt)
@@ -253,6 +258,9 @@ class Learner:
         return {"total_loss": loss.detach(), "v_loss": v.detach(), "p_loss": pl.detach(), "d_loss": d.detach(),
                 "r_loss": r.detach()}
 
+    def _device_net(self, net):
+        return N.DeviceNet(self.nets.numpy(), net.C, net.A, device=net.buffer.device)
+
     def train_step(self, batch: dict) -> dict:
         if not self.graph:
             for p in self.nets.parameters():
@@ -290,9 +298,133 @@ class Learner:
 
     def push_to(self, net: "N.DeviceNet"):
         """Pack the current parameters into the self-play engine's arena (same layout) in place."""
-        fresh = N.DeviceNet(self.nets.numpy(), net.C, net.A, device=net.buffer.device)
+        fresh = self._device_net(net)
         net.buffer.copy_(fresh.buffer)
         net.prepare()
+
+
+# ---- classic MADN: Stochastic MuZero (MuZero_Classic_MADN/train_stochastic.py) -------------------------
+CLASSIC_SCALING = dict(value=4.0, policy=2.0, chance=0.5, discount=1.0, reward=1.0)   # train_stochastic.py:374-378
+
+
+class ClassicMuZeroNets(MuZeroNets):
+    """Repr2 / Pred4 (A = 4) + StochasticDynamicsNetwork4 (muzero_classic_madn.py:314-408)."""
+
+    def __init__(self, params: dict, obs_channels: int, device="cuda", dtype=torch.float32):
+        from .stochastic import classic_param_shapes
+        super().__init__(params, obs_channels, 4, device, dtype, shapes=classic_param_shapes(obs_channels))
+        self.NC = 6
+
+    def _film_trunk(self, pre, rb0, x_in, e):
+        d = "dynamics"
+        ln = self._ln(f"{d}/{pre}_input_ln", x_in)
+        x = ln * (1.0 + self._dense(f"{d}/{pre}_film_scale", e)) + self._dense(f"{d}/{pre}_film_shift", e)
+        x = F.relu(self._ln(f"{d}/{pre}_ln1", self._dense(f"{d}/{pre}_dense1", x)))
+        x = F.relu(self._ln(f"{d}/{pre}_ln2", self._dense(f"{d}/{pre}_dense2", x)))
+        for r in range(rb0, rb0 + 2):
+            x = self._rb(f"{d}/ResBlock_{r}", x)
+        return self._minmax(x_in + self._dense(f"{d}/{pre}_proj", x))
+
+    def _one_hot(self, a, n, like):
+        return (a.long()[:, None] == torch.arange(n, device=like.device)[None, :]).to(like.dtype)
+
+    def action_dynamics(self, latent, action):
+        """-> (afterstate, reward_logits, chance_logits, discount_logits) (329-371)."""
+        d = "dynamics"
+        oh = self._one_hot(action, self.A, latent)
+        e = F.relu(self._dense(f"{d}/act_embed", oh))
+        after = self._film_trunk("act", 0, latent, e)
+        rl = self._dense(f"{d}/reward_head", F.relu(self._dense(f"{d}/reward_dense", torch.cat([after, oh], -1))))
+        dl = self._dense(f"{d}/discount_head",
+                         F.relu(self._ln(f"{d}/discount_ln", self._dense(f"{d}/discount_dense", latent))))
+        cl = self._dense(f"{d}/chance_head", after)
+        return after, rl, cl, dl
+
+    def chance_dynamics(self, afterstate, chance):
+        """-> next state (373-408)."""
+        e = F.relu(self._dense("dynamics/chance_embed", self._one_hot(chance, self.NC, afterstate)))
+        return self._film_trunk("chance", 2, afterstate, e)
+
+
+def balanced_loss(ce, is_rare, mask, n_valid, w_rare=1.0, w_common=0.1):
+    """train_stochastic.py:25-32 (n_common counts against the clamped n_rare, as the reference does)."""
+    masked_rare = mask * is_rare
+    n_rare = torch.clamp(masked_rare.sum(), min=1.0)
+    n_common = torch.clamp(n_valid - n_rare, min=1.0)
+    return w_rare * (masked_rare * ce).sum() / n_rare + w_common * ((mask - masked_rare) * ce).sum() / n_common
+
+
+def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: float = 0.5):
+    """train_stochastic.py:34-180 -> (total, (value, policy, chance, discount, reward) losses)."""
+    dt = nets.p["prediction/Dense_5/bias"].dtype
+    obs = batch["observations"].to(dt)
+    latent = nets.representation(obs)
+    B, K = batch["actions"].shape
+    dev = obs.device
+    acts = torch.cat([batch["actions"], torch.zeros((B, 1), dtype=batch["actions"].dtype, device=dev)], 1)
+    dice = torch.cat([batch["dice_outcomes"][:, 1:].long(), torch.zeros((B, 2), dtype=torch.long, device=dev)], 1)
+    probs = torch.cat([batch["dice_probs"].to(dt), torch.full((B, 1, 6), 1.0 / 6.0, dtype=dt, device=dev)], 1)
+    ones = torch.ones((B, 1), dtype=torch.int32, device=dev)
+    disc_t = torch.cat([batch["discount_targets"].int(), ones], 1)
+    rew_t = torch.cat([batch["rewards"].int(), ones], 1)
+    sc = CLASSIC_SCALING
+    total = torch.zeros((), dtype=dt, device=dev)
+    sums = [torch.zeros((), dtype=dt, device=dev) for _ in range(5)]
+    for k in range(K + 1):
+        mask = batch["masks"][:, k].to(dt)
+        logits, v = nets.prediction(latent)
+        l_policy = torch.mean(mask * -(batch["policies"][:, k].to(dt) * F.log_softmax(logits, -1)).sum(-1))
+        l_value = torch.mean(mask * (batch["target_values"][:, k].to(dt) - v[:, 0]) ** 2)
+        zero = torch.zeros((), dtype=dt, device=dev)
+        if k < K:
+            n_valid = mask.sum()
+            after, rl, cl, dl = nets.action_dynamics(latent, acts[:, k])
+            rc, dc = rew_t[:, k], disc_t[:, k]
+            tp = probs[:, k]
+            reward_ce = F.cross_entropy(rl, rc.long(), reduction="none")
+            discount_ce = F.cross_entropy(dl, dc.long(), reduction="none")
+            chance_ce = -(tp * F.log_softmax(cl, -1)).sum(-1)
+            non_uniform = ((tp - 1.0 / 6.0) ** 2).sum(-1) > 1e-6
+            l_reward = balanced_loss(reward_ce, (rc != 1).to(dt), mask, n_valid)
+            l_discount = balanced_loss(discount_ce, (dc == 1).to(dt), mask, n_valid)
+            l_chance = balanced_loss(chance_ce, non_uniform.to(dt), mask, n_valid)
+            nxt = nets.chance_dynamics(after, dice[:, k])
+        else:
+            nxt, l_chance, l_discount, l_reward = latent, zero, zero, zero
+        latent = (nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale
+        total = total + (1.0 / unroll_steps) * (sc["value"] * l_value + sc["policy"] * l_policy +
+                                                sc["chance"] * l_chance + sc["discount"] * l_discount +
+                                                sc["reward"] * l_reward)
+        for i, x in enumerate((l_value, l_policy, l_chance, l_discount, l_reward)):
+            sums[i] = sums[i] + x
+    return total, tuple(sums)
+
+
+class StochasticLearner(Learner):
+    """train_step of train_stochastic.py:183-193 (clip 5.0 -> adamw, lr 0.005 x0.1 @ it 40, x0.2 @ 85,
+    x0.5 @ 105 of 2500 steps) on batches of replay.VectorizedReplayBufferStochastic."""
+
+    KEYS = Learner.KEYS + ("dice_outcomes", "dice_probs")
+
+    def __init__(self, params: dict, obs_channels: int, unroll_steps: int = 10, device="cuda", graph: bool = False,
+                 **opt):
+        opt.setdefault("boundaries", CLASSIC_LR_BOUNDARIES)
+        self.nets = ClassicMuZeroNets(params, obs_channels, device)
+        self.opt = AdamW(self.nets.parameters(), **opt)
+        self.unroll_steps = int(unroll_steps)
+        self.graph = bool(graph)
+        self._g = None
+
+    def _step(self, batch):
+        loss, (v, pl, c, d, r) = loss_fn_stochastic(self.nets, batch, self.unroll_steps)
+        loss.backward()
+        self.opt.step()
+        return {"total_loss": loss.detach(), "v_loss": v.detach(), "p_loss": pl.detach(), "c_loss": c.detach(),
+                "d_loss": d.detach(), "r_loss": r.detach()}
+
+    def _device_net(self, net):
+        from .stochastic import DeviceClassicNet
+        return DeviceClassicNet(self.nets.numpy(), net.C, device=net.buffer.device)
 
 
 def train_loop(learner: Learner, engine, ring, iterations: int, train_steps: int, games_per_iteration: int,

@@ -103,3 +103,48 @@ class AdamW:
             u = u + F32(self.wd) * p
             out[k] = (p - lr * u).astype(F32)
         return out
+
+
+# ---- classic MADN: train_stochastic.py:25-180 -----------------------------------------------------------
+def _softmax_ce(logits, probs):
+    return -(probs.astype(np.float64) * _log_softmax(logits)).sum(-1)
+
+
+def balanced_loss(ce, is_rare, mask, n_valid, w_rare=1.0, w_common=0.1):
+    masked_rare = mask * is_rare
+    n_rare = max(np.sum(masked_rare), 1.0)
+    n_common = max(n_valid - n_rare, 1.0)
+    return w_rare * np.sum(masked_rare * ce) / n_rare + w_common * np.sum((mask - masked_rare) * ce) / n_common
+
+
+def loss_fn_stochastic(params, batch, unroll_steps=10):
+    from . import classic_nets as CN
+    latent = ON.representation(params, batch["observations"])
+    K = batch["actions"].shape[1]
+    B = latent.shape[0]
+    acts = np.concatenate([batch["actions"], np.zeros((B, 1), np.int32)], 1)
+    dice = np.concatenate([batch["dice_outcomes"][:, 1:], np.zeros((B, 2), np.int32)], 1)
+    probs = np.concatenate([batch["dice_probs"], np.full((B, 1, 6), 1.0 / 6.0, np.float32)], 1)
+    disc_t = np.concatenate([batch["discount_targets"], np.ones((B, 1), np.int32)], 1)
+    rew_t = np.concatenate([batch["rewards"], np.ones((B, 1), np.int32)], 1)
+    total = 0.0
+    sums = [0.0] * 5
+    for k in range(K + 1):
+        mask = batch["masks"][:, k].astype(np.float64)
+        logits, v = ON.prediction(params, latent)
+        l_policy = np.mean(mask * -(batch["policies"][:, k].astype(np.float64) * _log_softmax(logits)).sum(-1))
+        l_value = np.mean(mask * (batch["target_values"][:, k] - v[:, 0].astype(np.float64)) ** 2)
+        l_chance = l_disc = l_rew = 0.0
+        if k < K:
+            n_valid = np.sum(mask)
+            after, rl, cl, dl = CN.action_dynamics(params, latent, acts[:, k])
+            rc, dc, tp = rew_t[:, k], disc_t[:, k], probs[:, k]
+            l_rew = balanced_loss(_ce_int(rl, rc), (rc != 1).astype(np.float64), mask, n_valid)
+            l_disc = balanced_loss(_ce_int(dl, dc), (dc == 1).astype(np.float64), mask, n_valid)
+            nonu = (((tp.astype(np.float64) - 1.0 / 6.0) ** 2).sum(-1) > 1e-6).astype(np.float64)
+            l_chance = balanced_loss(_softmax_ce(cl, tp), nonu, mask, n_valid)
+            latent = CN.chance_dynamics(params, after, dice[:, k])
+        total += (1.0 / unroll_steps) * (4.0 * l_value + 2.0 * l_policy + 0.5 * l_chance + 1.0 * l_disc + 1.0 * l_rew)
+        for i, x in enumerate((l_value, l_policy, l_chance, l_disc, l_rew)):
+            sums[i] += x
+    return total, tuple(sums)

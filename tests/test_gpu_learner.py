@@ -77,9 +77,47 @@ def test_graph_captured_step_equals_eager(cuda):
         le = eager.train_step(b)
         lg = graph.train_step(b)
         assert abs(float(le["total_loss"]) - float(lg["total_loss"])) <= 1e-5 * abs(float(le["total_loss"]))
-    # Adam normalises each update to ~lr (0.005), so near-zero gradients computed by a different
-    # convolution / GEMM algorithm under capture can move an element by a visible fraction of lr
+    # Adam normalises each update to ~lr (0.005): an element whose gradient is ~0 moves by +-lr on rounding
+    # noise alone (the captured and eager runs may pick different GEMM / convolution algorithms), so the
+    # check is on the bulk of the parameters, not the maximum
+    n = bad = 0
     for k in eager.nets.p:
-        assert (eager.nets.p[k] - graph.nets.p[k]).abs().max().item() < 2e-3, k
-    dev = max((eager.nets.p[k] - graph.nets.p[k]).abs().max().item() for k in eager.nets.p)
-    print("max |param difference| after 4 steps:", dev)
+        d = (eager.nets.p[k] - graph.nets.p[k]).abs()
+        n += d.numel()
+        bad += int((d > 1e-4).sum())
+    assert bad <= 1e-2 * n, (bad, n)      # measured ~0.12 %
+    print("parameters off by > 1e-4 after 4 steps:", bad, "of", n)
+
+
+def test_stochastic_learner_on_classic_ring(cuda):
+    """train_stochastic.py's learner on batches of the stochastic device ring (graph-captured), weights
+    pushed into the classic self-play arena: its root inference equals the torch forward."""
+    from oracle import classic_nets as CN
+    from exploring_muzero_on_dog_amd import classic as CL
+    from exploring_muzero_on_dog_amd import game_agent_stochastic as GS
+    from exploring_muzero_on_dog_amd import learner as L
+    from exploring_muzero_on_dog_amd import replay as R
+    from exploring_muzero_on_dog_amd import stochastic as S
+    C = CL.num_channels(4)
+    params = CN.init_params(C, seed=13)
+    net = S.DeviceClassicNet(params, C)
+    eng = GS.StochasticSelfPlayEngine(net, 32, max_steps=120, num_simulations=6, max_depth=5)
+    ring = R.VectorizedReplayBufferStochastic(64, 32, 5, 10, obs_shape=(C, 56), max_episode_length=120,
+                                              rng=np.random.RandomState(4))
+    ring.save_games_from_buffers(eng.play(seed=3))
+    batch = ring.sample_batch()
+    lr = L.StochasticLearner(params, C, unroll_steps=5, graph=True)
+    first = float(lr.train_step(batch)["total_loss"])
+    for _ in range(40):
+        last = float(lr.train_step(batch)["total_loss"])
+    assert np.isfinite(last) and last < first, (first, last)
+    lr.push_to(net)
+    obs = torch.from_numpy(np.random.default_rng(2).integers(0, 3, (24, C, 56)).astype(np.float32)).cuda()
+    lg, v, e = S.root_inference_fn(net, obs)
+    with torch.no_grad():
+        te = lr.nets.representation(obs)
+        tl, tv = lr.nets.prediction(te)
+    assert (e - te).abs().max().item() < 2e-5 and (lg - tl).abs().max().item() < 2e-5
+    assert (v - tv[:, 0]).abs().max().item() < 2e-5
+    buf = eng.play_stream(20, seed=4)
+    assert int(buf["idx"].min()) > 0

@@ -140,3 +140,26 @@ def test_latent_gradient_scaling():
         loss.backward()
         grads.append(nets.p["representation/Dense_4/kernel"].grad.clone())
     assert torch.allclose(grads[1], 0.5 * grads[0], rtol=1e-9, atol=1e-14)
+
+
+def test_classic_loss_matches_oracle():
+    """train_stochastic.py loss_fn_stochastic: torch vs the NumPy restatement (dice shifted by one step,
+    padded probabilities, balanced chance / reward / discount terms)."""
+    L = _L()
+    from oracle import classic_nets as CN
+    C = 11
+    params = CN.init_params(C, seed=5, randomize_affine=True)
+    nets = L.ClassicMuZeroNets(params, C, device="cpu")
+    rng = np.random.default_rng(4)
+    B, K = 12, 6
+    b = _batch(B, K, C, A=4, seed=5)
+    b["dice_outcomes"] = rng.integers(0, 6, (B, K)).astype(np.int32)
+    pr = rng.random((B, K, 6)).astype(np.float32)
+    pr[::2] = 1.0 / 6.0
+    b["dice_probs"] = (pr / pr.sum(-1, keepdims=True)).astype(np.float32)
+    with torch.no_grad():
+        tot, parts = L.loss_fn_stochastic(nets, _t(b), unroll_steps=K)
+    wt, wparts = OL.loss_fn_stochastic(params, b, unroll_steps=K)
+    assert abs(float(tot) - wt) <= 2e-5 * abs(wt), (float(tot), wt)
+    for x, y in zip(parts, wparts):
+        assert abs(float(x) - y) <= 2e-5 * max(abs(y), 1e-3), (float(x), y)
