@@ -93,19 +93,37 @@ class MuZeroNets:
             h = self._rb(f"{r}/ResBlock_{b}", h)
         return self._minmax(self._dense(f"{r}/Dense_4", h))
 
-    def dynamics(self, latent, action):
+    def dynamics_film(self, action):
+        """The action-only FiLM sub-graph of DynamicsNetwork4 (one_hot -> Dense_0 -> Dense_1 | Dense_2); it
+        does not depend on the latent, so the learner evaluates it for all unroll steps in one batch."""
         d = "dynamics"
-        oh = (action.long()[:, None] == torch.arange(self.A, device=latent.device)[None, :]).to(latent.dtype)
+        oh = (action.long()[:, None] == torch.arange(self.A, device=action.device)[None, :]).to(
+            self.p[f"{d}/Dense_0/bias"].dtype)
         e = F.relu(self._dense(f"{d}/Dense_0", oh))
-        x = self._ln(f"{d}/LayerNorm_0", latent) * (1.0 + self._dense(f"{d}/Dense_1", e)) + self._dense(f"{d}/Dense_2", e)
+        return oh, self._dense(f"{d}/Dense_1", e), self._dense(f"{d}/Dense_2", e)
+
+    def dynamics_trunk(self, latent, scale, shift):
+        """latent -> next latent (the sequential part of the unroll)."""
+        d = "dynamics"
+        x = self._ln(f"{d}/LayerNorm_0", latent) * (1.0 + scale) + shift
         x = F.relu(self._ln(f"{d}/LayerNorm_1", self._dense(f"{d}/Dense_3", x)))
         x = F.relu(self._ln(f"{d}/LayerNorm_2", self._dense(f"{d}/Dense_4", x)))
         for b in range(2):
             x = self._rb(f"{d}/ResBlock_{b}", x)
-        nxt = self._minmax(latent + self._dense(f"{d}/Dense_5", x))
+        return self._minmax(latent + self._dense(f"{d}/Dense_5", x))
+
+    def dynamics_heads(self, nxt, oh):
+        """Reward / discount logits of (next latent, one_hot(action)); row-wise, so batchable over steps."""
+        d = "dynamics"
         ri = torch.cat([nxt, oh], -1)
         rl = self._dense(f"{d}/reward_head", F.relu(self._dense(f"{d}/Dense_6", ri)))
         dl = self._dense(f"{d}/discount_head", F.relu(self._dense(f"{d}/Dense_7", ri)))
+        return rl, dl
+
+    def dynamics(self, latent, action):
+        oh, scale, shift = self.dynamics_film(action)
+        nxt = self.dynamics_trunk(latent, scale, shift)
+        rl, dl = self.dynamics_heads(nxt, oh)
         return nxt, rl, dl
 
     def prediction(self, latent):
@@ -143,24 +161,32 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     ones = torch.ones((B, 1), dtype=torch.int32, device=dev)
     disc_t = torch.cat([batch["discount_targets"].int(), ones], 1)
     rew_t = torch.cat([batch["rewards"].int(), ones], 1)
+    # Only the latent chain is sequential: the action FiLM rows, Pred4 on every step's latent and the
+    # reward / discount heads are row-wise, so each runs once over all K (+1) steps stacked along the batch
+    # (same per-row arithmetic as the step-by-step loop of the reference; far fewer kernel launches).
+    oh, scale, shift = nets.dynamics_film(acts[:, :K].transpose(0, 1).reshape(-1))
+    latents = [latent]
+    for k in range(K):
+        nxt = nets.dynamics_trunk(latents[-1], scale[k * B:(k + 1) * B], shift[k * B:(k + 1) * B])
+        latents.append((nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale)   # gradient scaling (fwd identity)
+    logits_all, v_all = nets.prediction(torch.cat(latents, 0))
+    rl_all, dl_all = nets.dynamics_heads(torch.cat(latents[1:], 0), oh) if K else (None, None)
     total = torch.zeros((), dtype=obs.dtype, device=dev)
     sums = [torch.zeros((), dtype=obs.dtype, device=dev) for _ in range(4)]
     for k in range(K + 1):
         mask = batch["masks"][:, k].to(obs.dtype)
-        logits, v = nets.prediction(latent)
+        logits, v = logits_all[k * B:(k + 1) * B], v_all[k * B:(k + 1) * B]
         l_value = torch.mean(mask * (batch["target_values"][:, k].to(obs.dtype) - v[:, 0]) ** 2)
         l_policy = torch.mean(mask * -(batch["policies"][:, k].to(obs.dtype) * F.log_softmax(logits, -1)).sum(-1))
         step = (1.0 / unroll_steps) * (VALUE_SCALING * l_value + POLICY_SCALING * l_policy)
         if k < K:
-            nxt, rl, dl = nets.dynamics(latent, acts[:, k])
+            rl, dl = rl_all[k * B:(k + 1) * B], dl_all[k * B:(k + 1) * B]
             l_rew = _balanced_ce(rl, rew_t[:, k], mask, 1, 0.1, 1.0)        # neutral 0.1, win/lose 1.0
             l_disc = _balanced_ce(dl, disc_t[:, k], mask, 1, 1.0, 0.1)      # terminal 1.0, other 0.1
         else:
-            nxt, l_rew, l_disc = latent, torch.zeros((), dtype=obs.dtype, device=dev), \
-                torch.zeros((), dtype=obs.dtype, device=dev)
+            l_rew, l_disc = torch.zeros((), dtype=obs.dtype, device=dev), torch.zeros((), dtype=obs.dtype, device=dev)
         total = total + step + (1.0 / unroll_steps) * DISCOUNT_SCALING * l_disc + \
             (1.0 / unroll_steps) * REWARD_SCALING * l_rew
-        latent = (nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale   # gradient scaling (forward identity)
         for i, x in enumerate((l_value, l_policy, l_disc, l_rew)):
             sums[i] = sums[i] + x
     return total, tuple(sums)
@@ -328,22 +354,32 @@ class ClassicMuZeroNets(MuZeroNets):
     def _one_hot(self, a, n, like):
         return (a.long()[:, None] == torch.arange(n, device=like.device)[None, :]).to(like.dtype)
 
-    def action_dynamics(self, latent, action):
-        """-> (afterstate, reward_logits, chance_logits, discount_logits) (329-371)."""
+    def action_embed(self, action):
+        oh = self._one_hot(action, self.A, self.p["dynamics/act_embed/bias"])
+        return oh, F.relu(self._dense("dynamics/act_embed", oh))
+
+    def chance_embed(self, chance):
+        return F.relu(self._dense("dynamics/chance_embed", self._one_hot(chance, self.NC, self.p["dynamics/chance_embed/bias"])))
+
+    def action_heads(self, latent, after, oh):
+        """(reward, chance, discount) logits of action_dynamics; row-wise, batchable over unroll steps."""
         d = "dynamics"
-        oh = self._one_hot(action, self.A, latent)
-        e = F.relu(self._dense(f"{d}/act_embed", oh))
-        after = self._film_trunk("act", 0, latent, e)
         rl = self._dense(f"{d}/reward_head", F.relu(self._dense(f"{d}/reward_dense", torch.cat([after, oh], -1))))
         dl = self._dense(f"{d}/discount_head",
                          F.relu(self._ln(f"{d}/discount_ln", self._dense(f"{d}/discount_dense", latent))))
         cl = self._dense(f"{d}/chance_head", after)
+        return rl, cl, dl
+
+    def action_dynamics(self, latent, action):
+        """-> (afterstate, reward_logits, chance_logits, discount_logits) (329-371)."""
+        oh, e = self.action_embed(action)
+        after = self._film_trunk("act", 0, latent, e)
+        rl, cl, dl = self.action_heads(latent, after, oh)
         return after, rl, cl, dl
 
     def chance_dynamics(self, afterstate, chance):
         """-> next state (373-408)."""
-        e = F.relu(self._dense("dynamics/chance_embed", self._one_hot(chance, self.NC, afterstate)))
-        return self._film_trunk("chance", 2, afterstate, e)
+        return self._film_trunk("chance", 2, afterstate, self.chance_embed(chance))
 
 
 def balanced_loss(ce, is_rare, mask, n_valid, w_rare=1.0, w_common=0.1):
@@ -368,17 +404,31 @@ def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int =
     disc_t = torch.cat([batch["discount_targets"].int(), ones], 1)
     rew_t = torch.cat([batch["rewards"].int(), ones], 1)
     sc = CLASSIC_SCALING
+    # Only the afterstate / state chain is sequential; the embeddings, Pred4 and the action heads run once
+    # over all steps stacked along the batch (same per-row arithmetic, far fewer launches).
+    oh_all, ea_all = nets.action_embed(acts[:, :K].transpose(0, 1).reshape(-1))
+    ec_all = nets.chance_embed(dice[:, :K].transpose(0, 1).reshape(-1))
+    latents, afters = [latent], []
+    for k in range(K):
+        after = nets._film_trunk("act", 0, latents[-1], ea_all[k * B:(k + 1) * B])
+        afters.append(after)
+        nxt = nets._film_trunk("chance", 2, after, ec_all[k * B:(k + 1) * B])
+        latents.append((nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale)
+    logits_all, v_all = nets.prediction(torch.cat(latents, 0))
+    if K:
+        rl_all, cl_all, dl_all = nets.action_heads(torch.cat(latents[:K], 0), torch.cat(afters, 0), oh_all)
     total = torch.zeros((), dtype=dt, device=dev)
     sums = [torch.zeros((), dtype=dt, device=dev) for _ in range(5)]
     for k in range(K + 1):
         mask = batch["masks"][:, k].to(dt)
-        logits, v = nets.prediction(latent)
+        sl = slice(k * B, (k + 1) * B)
+        logits, v = logits_all[sl], v_all[sl]
         l_policy = torch.mean(mask * -(batch["policies"][:, k].to(dt) * F.log_softmax(logits, -1)).sum(-1))
         l_value = torch.mean(mask * (batch["target_values"][:, k].to(dt) - v[:, 0]) ** 2)
         zero = torch.zeros((), dtype=dt, device=dev)
         if k < K:
             n_valid = mask.sum()
-            after, rl, cl, dl = nets.action_dynamics(latent, acts[:, k])
+            rl, cl, dl = rl_all[sl], cl_all[sl], dl_all[sl]
             rc, dc = rew_t[:, k], disc_t[:, k]
             tp = probs[:, k]
             reward_ce = F.cross_entropy(rl, rc.long(), reduction="none")
@@ -388,10 +438,8 @@ def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int =
             l_reward = balanced_loss(reward_ce, (rc != 1).to(dt), mask, n_valid)
             l_discount = balanced_loss(discount_ce, (dc == 1).to(dt), mask, n_valid)
             l_chance = balanced_loss(chance_ce, non_uniform.to(dt), mask, n_valid)
-            nxt = nets.chance_dynamics(after, dice[:, k])
         else:
-            nxt, l_chance, l_discount, l_reward = latent, zero, zero, zero
-        latent = (nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale
+            l_chance, l_discount, l_reward = zero, zero, zero
         total = total + (1.0 / unroll_steps) * (sc["value"] * l_value + sc["policy"] * l_policy +
                                                 sc["chance"] * l_chance + sc["discount"] * l_discount +
                                                 sc["reward"] * l_reward)

@@ -73,10 +73,13 @@ def test_graph_captured_step_equals_eager(cuda):
     batches = [ring.sample_batch() for _ in range(4)]
     eager = L.Learner(params, C, unroll_steps=5)
     graph = L.Learner(params, C, unroll_steps=5, graph=True)
-    for b in batches:
+    for i, b in enumerate(batches):
         le = eager.train_step(b)
         lg = graph.train_step(b)
-        assert abs(float(le["total_loss"]) - float(lg["total_loss"])) <= 1e-5 * abs(float(le["total_loss"]))
+        # step 0 starts from identical parameters; later steps start from parameters that already differ by
+        # the Adam rounding noise described below, so their losses agree less tightly
+        tol = 1e-5 if i == 0 else 1e-4
+        assert abs(float(le["total_loss"]) - float(lg["total_loss"])) <= tol * abs(float(le["total_loss"])), i
     # Adam normalises each update to ~lr (0.005): an element whose gradient is ~0 moves by +-lr on rounding
     # noise alone (the captured and eager runs may pick different GEMM / convolution algorithms), so the
     # check is on the bulk of the parameters, not the maximum
