@@ -437,6 +437,64 @@ __device__ __forceinline__ void minmax16(float* buf, int ld) {
   }
 }
 
+// x <- minmax(x + skip) per row of 256: Dyn4's `latent + Dense_5(x)` (455) fused into the min-max pass.
+// With `ln` (fused Pred4 head, search kernels): also stores the latent row to `emb` (the new node's embedding
+// in the tree, when non-null) and PredictionNetwork4's LayerNorm_0 of it to `lnout`, so pred16 can start with
+// its first ResBlock (same arithmetic, in the same order, as ln16<LAT, LN_PLAIN>).
+__device__ __forceinline__ void skip_minmax16(float* buf, const float* skip, int ld, const LnP<LAT>* ln = nullptr,
+                                              AS1 float* emb = nullptr, float* lnout = nullptr) {
+  using RV = RowVec<LAT>;
+  const int row = trow(), sub = tsub();
+  f32x4 v[RV::V];
+  float lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < RV::V; ++i) {
+    v[i] = lds4(skip + row * ld + RV::col(sub, i)) + lds4(buf + row * ld + RV::col(sub, i));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      lo = fminf(lo, v[i][q]);
+      hi = fmaxf(hi, v[i][q]);
+    }
+  }
+  lo = row_min(lo);
+  hi = row_max(hi);
+  const float den = hi - lo + 1e-8f;
+#pragma unroll
+  for (int i = 0; i < RV::V; ++i) {
+    f32x4 y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = (v[i][q] - lo) / den;
+    sts4(buf + row * ld + RV::col(sub, i), y);
+    v[i] = y;
+  }
+  if (!ln) return;
+  if (emb) {
+#pragma unroll
+    for (int i = 0; i < RV::V; ++i) tree_st(reinterpret_cast<AS1 f32x4*>(emb + RV::col(sub, i)), v[i]);
+  }
+  float s = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < RV::V; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s += v[i][q];
+      s2 += v[i][q] * v[i][q];
+    }
+  s = row_sum(s);
+  s2 = row_sum(s2);
+  const float mean = s / (float)LAT;
+  const float mean2 = s2 / (float)LAT;
+  const float var = fmaxf(0.f, mean2 - mean * mean);
+  const float inv = 1.0f / sqrtf(var + 1e-6f);
+#pragma unroll
+  for (int i = 0; i < RV::V; ++i) {
+    f32x4 y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = (v[i][q] - mean) * (inv * ln->sc[i][q]) + ln->sh[i][q];
+    sts4(lnout + row * ld + RV::col(sub, i), y);
+  }
+}
+
 __device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
   const int row = trow(), sub = tsub();
   for (int c = sub * 4; c < n; c += 4 * kRowLanes) sts4(buf + row * ld + col0 + c, relu4(lds4(buf + row * ld + col0 + c)));
@@ -518,6 +576,19 @@ __device__ __forceinline__ HeadK<K> head_load(const AS4 muz_dense& H, int ncol) 
   }
   return h;
 }
+// sum_k relu(in[k] + add[i]) * w[k] (+ b): a head whose hidden layer's one-hot rows and ReLU are applied
+// as the inputs are read (add[i] = the one-hot weight row at this lane's inputs, 0 without an action).
+template <int K>
+__device__ __forceinline__ float head_dot_relu(const float* in, int ld, const float (&add)[HeadK<K>::kPer],
+                                               const HeadK<K>& h, int j) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < HeadK<K>::kPer; ++i) {
+    const int k = tsub() + i * kRowLanes;
+    if (k < K) s += fmaxf(in[trow() * ld + k] + add[i], 0.f) * h.w[j][i];
+  }
+  return row_sum(s) + h.b[j];
+}
 template <int K>
 __device__ __forceinline__ float head_dot(const float* in, int ld, const HeadK<K>& h, int j) {
   float s = 0.f;
@@ -532,11 +603,15 @@ __device__ __forceinline__ float head_dot(const float* in, int ld, const HeadK<K
 // PredictionNetwork4 (muzero_deterministic_madn.py:549-583) on the latent in `lat` ([16][LD]).
 // Leaves policy logits in a.U[:, 0:A] and tanh value in a.v0.  Clobbers X, T, U, W.
 // pf: rb[0].d0 on entry, (Ln, NTN tiles) on exit.
-template <int NTN>
+// LN0_DONE: the caller already left LayerNorm_0(lat) in a.X (dyn16<.., true>), so the pass and its barrier
+// are skipped.
+template <int NTN, bool LN0_DONE = false>
 __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const float* lat, const Arena& a, Pf& pf,
                                        const AS4 muz_dense* Ln, int Kn, int Nn) {
-  ln16<LAT, LN_PLAIN>(lat, LD, a.X, LD, P.ln0);
-  SYNC();
+  if constexpr (!LN0_DONE) {
+    ln16<LAT, LN_PLAIN>(lat, LD, a.X, LD, P.ln0);
+    SYNC();
+  }
   resblock16<NT256>(P.rb[0], a.X, a.T, a.U, pf, &P.rb[1].d0, LAT, LAT);
   resblock16<NT384>(P.rb[1], a.X, a.T, a.U, pf, &P.d03, LAT, 384);
   const LnP<LAT> p1 = ln_load<LAT>(P.ln1);
@@ -601,9 +676,13 @@ __device__ __forceinline__ DynIn dyn_load(const AS4 muz_dyn_w& D, int A, const A
 // DynamicsNetwork4 (muzero_deterministic_madn.py:391-457) on the tile.  `in` = this thread's row inputs,
 // `ar` = this row's action.  Out: next latent in a.T, reward / discount support values in a.v1 / a.v2.
 // pf: d3 on entry, (Ln: Kn x Nn, NTN tiles) on exit.
-template <int NTN>
+// PRED_LN0: fuse the following pred16's LayerNorm_0 (params `pln0`) into the latent's min-max pass, store the
+// latent to the tree at `emb` there (null: no store), and end without the final barrier; the caller then runs
+// pred16<.., true>, whose first writes (ResBlock_0's Dense_0 into a.T) come after d67 has consumed a.T.
+template <int NTN, bool PRED_LN0 = false>
 __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn& in, int ar, const Arena& a, Pf& pf,
-                                      const AS4 muz_dense* Ln, int Kn, int Nn) {
+                                      const AS4 muz_dense* Ln, int Kn, int Nn, const AS4 muz_ln* pln0 = nullptr,
+                                      AS1 float* emb = nullptr) {
   using RV = RowVec<LAT>;
   const int row = trow(), sub = tsub();
   const bool oh = ar >= 0 && ar < A;   // jax.nn.one_hot: out-of-range -> zero row
@@ -652,35 +731,41 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
   const HeadW hr = head_load(D.reward_head, 3);
   const HeadW hd = head_load(D.discount_head, 3);
   dense16<NT256, NT128>(D.d5, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d67, LAT, 128);
-  SYNC();
-  for (int c = sub * 4; c < LAT; c += 4 * kRowLanes)
-    sts4(a.T + row * LD + c, lds4(a.L + row * LD + c) + lds4(a.T + row * LD + c));
-  ST(ST_PASS);
-  SYNC();
-  minmax16(a.T, LD);
+  // Dense_6 | Dense_7's one-hot rows at this lane's head inputs (k = sub + i*kRowLanes), loaded early
+  float add_r[HeadW::kPer], add_d[HeadW::kPer];
+  {
+    const AS1 float* w67 = gp(D.d67_onehot) + (oh ? ar : 0) * 128;
+#pragma unroll
+    for (int i = 0; i < HeadW::kPer; ++i) {
+      const int k = sub + i * kRowLanes;
+      add_r[i] = (oh && k < 64) ? w67[k] : 0.f;
+      add_d[i] = (oh && k < 64) ? w67[64 + k] : 0.f;
+    }
+  }
+  if constexpr (PRED_LN0) {
+    const LnP<LAT> pl = ln_load<LAT>(*pln0);
+    SYNC();
+    skip_minmax16(a.T, a.L, LD, &pl, emb, a.X);
+  } else {
+    SYNC();
+    skip_minmax16(a.T, a.L, LD);
+  }
   ST(ST_PASS);
   SYNC();
   dense16<NT128, NTN>(D.d67, LAT, 128, a.T, LD, a.W, LDW, pf, Ln, Kn, Nn);   // [reward | discount] hidden
   SYNC();
-  const AS1 f32x4* w67 = gp(reinterpret_cast<const f32x4*>(D.d67_onehot));
-  for (int c = sub * 4; c < 128; c += 4 * kRowLanes) {
-    const f32x4 h = lds4(a.W + row * LDW + c);
-    sts4(a.W + row * LDW + c, relu4(oh ? h + w67[(ar * 128 + c) >> 2] : h));
-  }
-  ST(ST_PASS);
-  SYNC();
   float rl[3], dl[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    rl[j] = head_dot(a.W, LDW, hr, j);
-    dl[j] = head_dot(a.W + 64, LDW, hd, j);
+    rl[j] = head_dot_relu(a.W, LDW, add_r, hr, j);
+    dl[j] = head_dot_relu(a.W + 64, LDW, add_d, hd, j);
   }
   if (sub == 0) {
     a.v1[row] = softmax3_support(rl[0], rl[1], rl[2]);
     a.v2[row] = softmax3_support(dl[0], dl[1], dl[2]);
   }
   ST(ST_PASS);
-  SYNC();
+  if constexpr (!PRED_LN0) SYNC();
 }
 
 }  // namespace muz

@@ -305,17 +305,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     SYNC();
     MUZ_STAMP(1);   // select
     // ---------------- expand (search.py expand): recurrent_fn on the 16 parents
-    dyn16<NT256>(wl->dyn, A, din, dact, ar, pf, &wl->pred.rb[0].d0, LAT, LAT);
-    MUZ_STAMP(3);   // dynamics
+    // the new node's embedding goes to the tree and Pred4's LayerNorm_0 into ar.X straight from Dyn4's
+    // min-max pass (registers), so Pred4 starts with its first ResBlock
     const int nx = s_next[row];
-    if (valid) {
-      AS1 float* ne = T.e(g, nx);
-      for (int c = a; c < LAT; c += kRowLanes) tree_st(ne + c, ar.T[row * LD + c]);
-    }
-    // no barrier: pred16 reads ar.T in its first pass and overwrites it only after its first SYNC
-    ST(ST_TREE);
-    MUZ_STAMP(4);   // embedding write
-    pred16<NT256>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d3, LAT, LAT);
+    dyn16<NT256, true>(wl->dyn, A, din, dact, ar, pf, &wl->pred.rb[0].d0, LAT, LAT, &wl->pred.ln0,
+                       valid ? T.e(g, nx) : nullptr);
+    MUZ_STAMP(3);   // dynamics
+    MUZ_STAMP(4);   // embedding write (fused)
+    pred16<NT256, true>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d3, LAT, LAT);
     MUZ_STAMP(5);   // prediction
     if (valid) {
       const bool fresh = nx == sim + 1;
