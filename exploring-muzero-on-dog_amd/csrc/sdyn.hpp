@@ -97,11 +97,7 @@ __device__ __forceinline__ void film_trunk16(const TrunkW& W, const FilmIn& in, 
   resblock16<NT256>(W.rb[1], a.X, a.T, a.U, pf, W.proj, LAT, LAT);
   dense16<NT256, NTN>(*W.proj, LAT, LAT, a.X, LD, a.T, LD, pf, Ln, Kn, Nn);
   SYNC();
-  for (int c = sub * 4; c < LAT; c += 4 * kRowLanes)
-    sts4(a.T + row * LD + c, lds4(a.L + row * LD + c) + lds4(a.T + row * LD + c));
-  ST(ST_PASS);
-  SYNC();
-  minmax16(a.T, LD);
+  skip_minmax16(a.T, a.L, LD);
   ST(ST_PASS);
   SYNC();
 }
