@@ -89,9 +89,51 @@ class VectorizedReplayBuffer:
         t.max_steps = b["act"].shape[1]
         return t
 
+    # dtype of each trajectory field in the device ring / muz_traj (obs: int8 values 0..4)
+    TRAJ_DTYPES = {"obs": torch.int8, "act": torch.int32, "rew": torch.int32, "val": torch.float32,
+                   "pol": torch.float32, "mask": torch.float32, "player": torch.int32, "team": torch.int32,
+                   "discount": torch.int32, "idx": torch.int32}
+
+    def stage(self, all_buffers: dict) -> dict:
+        """Host trajectories (the reference's NumPy / jnp buffer dict, obs fp32) -> device tensors.
+
+        Each host field is converted to the ring's dtype on the host (observations to int8 after checking
+        that every value is an integer in [-128, 127], so the conversion is exact), copied into pinned
+        (page-locked) memory and sent with one asynchronous host->device copy on the current stream
+        (hipMemcpyAsync; the pinned block is released once its copy has completed).  Fields already on
+        the ring's device pass through untouched."""
+        out = {}
+        for k, v in all_buffers.items():
+            want = self.TRAJ_DTYPES.get(k, None)
+            if isinstance(v, torch.Tensor) and v.device == self.device:
+                out[k] = v if want is None or v.dtype == want or k == "obs" else v.to(want)
+                continue
+            a = v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+            if k == "obs" and a.dtype != np.int8:
+                i8 = a.astype(np.int8)
+                if not np.array_equal(i8.astype(a.dtype), a):
+                    raise ValueError("observations must hold small integers to be stored as int8")
+                a = i8
+            t = torch.from_numpy(np.ascontiguousarray(a))
+            if want is not None and t.dtype != want:
+                t = t.to(want)
+            out[k] = t.pin_memory().to(self.device, non_blocking=True)
+        if out["obs"].dtype != torch.int8:
+            # device fp32 observations (e.g. a torch re-implementation's buffers): exact int8 cast on device
+            o = out["obs"]
+            i8 = o.to(torch.int8)
+            if not torch.equal(i8.to(o.dtype), o):
+                raise ValueError("observations must hold small integers to be stored as int8")
+            out["obs"] = i8
+        return out
+
     def save_games_from_buffers(self, all_buffers: dict):
-        """vec_replay_buffer.py:36-61 on device."""
+        """vec_replay_buffer.py:36-61 on device.  Device buffers (SelfPlayEngine) are saved in place; host
+        buffers (NumPy, as the reference's callers hold them) go through pinned staging first (``stage``)."""
         b = all_buffers
+        if any(not (isinstance(v, torch.Tensor) and v.device == self.device) for v in b.values()) or \
+                b["obs"].dtype != torch.int8:
+            b = self.stage(b)
         n = b["idx"].shape[0]
         if b["obs"].dtype != torch.int8 or tuple(b["obs"].shape[2:]) != self.obs_shape:
             raise ValueError("expected int8 observations of shape [n, T, C, 56]")
@@ -198,6 +240,8 @@ class VectorizedReplayBufferStochastic(VectorizedReplayBuffer):
         r.won_if_positive = 1
         r.dice, r.dice_dist = self.dice_outcomes.data_ptr(), self.dice_distributions.data_ptr()
         return r
+
+    TRAJ_DTYPES = dict(VectorizedReplayBuffer.TRAJ_DTYPES, dice=torch.int32, dice_dist=torch.float32)
 
     def _chance(self, b: dict):
         ch = _L.MuzTrajChance()

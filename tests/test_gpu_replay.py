@@ -67,6 +67,29 @@ def test_ring_save_and_sample_synthetic(cuda, boot):
             assert_sample_equal(dev.sample_batch(), ora.sample_batch())
 
 
+def test_ring_from_host_buffers_pinned_staging(cuda):
+    """Reference-style host buffers (NumPy, fp32 observations, as play_n_games_v3's callers hold them) go
+    through pinned staging + async host->device copies into the device ring: same ring as the oracle fed
+    the same arrays; non-integral observations are refused (int8 storage would not be exact)."""
+    R = _R()
+    T, C, cap = 48, 18, 16
+    dev = R.VectorizedReplayBuffer(cap, 64, 10, 7, obs_shape=(C, 56), max_episode_length=T,
+                                   rng=np.random.RandomState(2))
+    ora = OracleRB(cap, 64, 10, 7, obs_shape=(C, 56), max_episode_length=T, rng=np.random.RandomState(2))
+    rng = np.random.default_rng(4)
+    for call in range(3):
+        b = make_buffers(rng.integers(0, T + 1, 11), T, C=C, seed=10 + call)
+        host = dict(b, obs=b["obs"].astype(np.float32))          # the reference's fp32 observations
+        dev.save_games_from_buffers(host)
+        ora.save_games_from_buffers(b)
+        assert_ring_equal(dev, ora)
+        assert_sample_equal(dev.sample_batch(), ora.sample_batch())
+    bad = make_buffers(np.array([5, 7]), T, C=C, seed=99)
+    bad["obs"] = bad["obs"].astype(np.float32) + 0.5
+    with pytest.raises(ValueError):
+        dev.save_games_from_buffers(bad)
+
+
 def test_ring_with_selfplay_buffers(cuda):
     from exploring_muzero_on_dog_amd import detmadn as E
     from exploring_muzero_on_dog_amd import game_agent as GA
