@@ -72,6 +72,41 @@ constexpr int NT64 = nt_for(64), NT128 = nt_for(128), NT256 = nt_for(256), NT384
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// ---- cross-lane helpers on the DPP / permlane network instead of ds_bpermute (which goes through the
+// LDS crossbar) ---------------------------------------------------------------------------------------
+template <class T>
+__device__ __forceinline__ unsigned as_u(T v) {
+  return __builtin_bit_cast(unsigned, v);
+}
+template <class T>
+__device__ __forceinline__ T from_u(unsigned u) {
+  return __builtin_bit_cast(T, u);
+}
+template <int CTRL, class T>
+__device__ __forceinline__ T dpp(T v) {
+  return from_u<T>((unsigned)__builtin_amdgcn_update_dpp(0, (int)as_u(v), CTRL, 0xF, 0xF, false));
+}
+enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140 };
+template <class T>
+struct LoHi {
+  T lo, hi;
+};
+// {value of the lower 16-lane row, value of the upper one} of each 32-lane group, in every lane.
+// (The two results are copied to plain scalars before the bit cast: bit-casting the vector element
+// directly loses the second result in this compiler.)
+template <class T>
+__device__ __forceinline__ LoHi<T> swap16(T v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(as_u(v), as_u(v), false, false);
+  const unsigned lo = p[0], hi = p[1];
+  return {from_u<T>(lo), from_u<T>(hi)};
+}
+template <class T>
+__device__ __forceinline__ LoHi<T> swap32(T v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(as_u(v), as_u(v), false, false);
+  const unsigned lo = p[0], hi = p[1];
+  return {from_u<T>(lo), from_u<T>(hi)};
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -102,10 +137,29 @@ __device__ __forceinline__ P tree_ld(const P* p) {
 #ifndef MUZ_A_PRELOAD
 #define MUZ_A_PRELOAD 1    // read the A fragment of k-block kb+1 from LDS before kb's MFMAs
 #endif
+#ifndef MUZ_DLN
+#define MUZ_DLN 0          // deferred LayerNorm (dense16_dp / dense16_la): 1 ResBlock LayerNorm_0, 2 + Dyn4 LayerNorm_1,
+                           // 3 + Pred4 head LayerNorms.  Measured on MI355X (B=4096 S=50 search): 1 -> +5 %,
+                           // 2 -> +6 %, 3 -> +8 % time: normalising every A fragment in all 8 waves costs more
+                           // than the row pass and barrier it saves
+#endif
+#ifndef MUZ_DLN_PK
+#define MUZ_DLN_PK 0       // deferred LayerNorm applied with packed fp32 math
+#endif
 
-template <int NT, bool AG>
+// Deferred LayerNorm + ReLU of the A operand (see dense16_dp): A[r][k] <- relu((A - mean_r) * (inv_r *
+// sc[k]) + sh[k]) as the fragments are read, with the row statistics of this lane's row and the
+// LayerNorm parameters staged in LDS by the producing layer.  Same arithmetic as ln16<.., LN_RELU>.
+struct LnA {
+  float mean, inv;
+  const float* sc;   // LDS, indexed by k
+  const float* sh;
+};
+
+template <int NT, bool AG, bool LNA = false>
 __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int KB, const float* A, int lda,
-                                               f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT]) {
+                                               f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT],
+                                               const LnA& ln = LnA{}) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(Wg)) + lane * NT;
@@ -115,8 +169,45 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
     if constexpr (AG) return *gp(reinterpret_cast<const f32x4*>(ap + kb * 16));
     else return *reinterpret_cast<const f32x4*>(ap + kb * 16);
   };
+  // LNA: the raw fragment and its LayerNorm parameters are read one step ahead (with the A preload) and
+  // normalised after the step's MFMAs are issued, so the VALU work co-issues with the other wave's MFMAs
+  struct ARaw {
+    f32x4 x, s, h;
+  };
+  const float* scp = ln.sc + 4 * g;
+  const float* shp = ln.sh + 4 * g;
+  auto ldr = [&](int kb) -> ARaw {
+    ARaw v;
+    v.x = lda4(kb);
+    v.s = *reinterpret_cast<const f32x4*>(scp + kb * 16);
+    v.h = *reinterpret_cast<const f32x4*>(shp + kb * 16);
+    return v;
+  };
+  auto fin = [&](const ARaw& v) -> f32x4 {
+    f32x4 y;
+#if MUZ_DLN_PK
+    // packed fp32 (v_pk_add / v_pk_mul / v_pk_fma): half the VALU issue slots next to the MFMAs
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 m2 = {ln.mean, ln.mean}, i2 = {ln.inv, ln.inv};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 x2 = {v.x[2 * h], v.x[2 * h + 1]}, s2 = {v.s[2 * h], v.s[2 * h + 1]},
+                  h2 = {v.h[2 * h], v.h[2 * h + 1]};
+      const f32x2 r2 = (x2 - m2) * (i2 * s2) + h2;
+      y[2 * h] = fmaxf(r2[0], 0.f);
+      y[2 * h + 1] = fmaxf(r2[1], 0.f);
+    }
+#else
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = fmaxf((v.x[q] - ln.mean) * (ln.inv * v.s[q]) + v.h[q], 0.f);
+#endif
+    return y;
+  };
   constexpr int D = MUZ_RING_DEPTH;
-  f32x4 a0 = lda4(0), a1 = a0;
+  f32x4 a0, a1;
+  if constexpr (LNA) a0 = fin(ldr(0));
+  else a0 = lda4(0);
+  a1 = a0;
   // step kb: issue k-block kb+D into `nxt` (the buffer consumed at step kb-1), read A of kb+1,
   // multiply `cur` (= kb) with A of kb
   auto step = [&](int kb, const f32x4 (&cur)[NT], f32x4 (&nxt)[NT], const f32x4& acur, f32x4& anxt) {
@@ -128,6 +219,17 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
     // first MFMA (one step of cover instead of D) once the loop is fully unrolled.
     __builtin_amdgcn_sched_barrier(0);
     f32x4 a;
+    if constexpr (LNA) {
+      ARaw rn;
+      if (kb + 1 < KB) rn = ldr(kb + 1);
+      a = acur;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma4(cur[t][j], a[j], acc[t]);
+      if (kb + 1 < KB) anxt = fin(rn);
+      return;
+    }
     if (MUZ_A_PRELOAD) {
       if (kb + 1 < KB) anxt = lda4(kb + 1);
       a = acur;
@@ -168,10 +270,13 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
   }
 }
 
-template <int NT>
+template <int NT, bool LNA = false>
 __device__ __forceinline__ void mfma_ring(const float* __restrict__ Wg, int KB, const float* A, int lda,
-                                          f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT], bool a_global) {
-  if (a_global)
+                                          f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT], bool a_global,
+                                          const LnA& ln = LnA{}) {
+  if constexpr (LNA)
+    mfma_ring_impl<NT, false, true>(Wg, KB, A, lda, acc, b0, b1, ln);
+  else if (a_global)
     mfma_ring_impl<NT, true>(Wg, KB, A, lda, acc, b0, b1);
   else
     mfma_ring_impl<NT, false>(Wg, KB, A, lda, acc, b0, b1);
@@ -217,18 +322,77 @@ __device__ __forceinline__ void pf_issue(Pf& pf, const AS4 muz_dense* L, int K, 
   }
 }
 
+// ---- deferred LayerNorm: statistics from the producer's epilogue, normalisation in the consumer ------
+// A LayerNorm + ReLU whose only reader is the next dense layer costs a row pass and a barrier when it
+// runs on its own (dense -> barrier -> ln16 -> barrier -> dense).  Deferred, the producer (dense16_dp)
+// stores its raw output together with per-(wave, row) partial sums of x and x^2 and the LayerNorm
+// parameters by column; after the one barrier the consumer (dense16_la with an LnA from dln_a) reduces
+// the partials of its row and normalises each A fragment as it reads it.  Two LDS buffers: a layer
+// that consumes buffer 0 can produce into buffer 1 while slower waves still read buffer 0.
+constexpr int kDlnCols = 384;
+struct Dln {
+  f32x4 part[kWaves][kRows];           // (sum, sum of squares) of column group 0 | group 1
+  float sc[kDlnCols], sh[kDlnCols];    // LayerNorm scale / bias by producer column
+};
+__device__ __forceinline__ Dln* dln_buf(int i) {
+  __shared__ Dln b[2];
+  return &b[i];
+}
+// producer waves that hold columns of an N-wide layer
+constexpr int nw_for(int N) { return (N + 16 * nt_for(N) - 1) / (16 * nt_for(N)); }
+
+// consumer side: mean / inverse deviation of this lane's MFMA row (lane & 15) over column group `grp`
+// (n columns) from the partials of the nw producer waves, and the parameters from producer column kcol0
+__device__ __forceinline__ LnA dln_a(const Dln* db, int grp, int kcol0, int n, int nw) {
+  const int r = threadIdx.x & 15;
+  f32x4 tot = db->part[0][r];
+  for (int w = 1; w < nw; ++w) tot += db->part[w][r];
+  const float s = grp ? tot[2] : tot[0];
+  const float s2 = grp ? tot[3] : tot[1];
+  const float mean = s / (float)n;
+  const float mean2 = s2 / (float)n;
+  const float var = fmaxf(0.f, mean2 - mean * mean);
+  LnA la;
+  la.mean = mean;
+  la.inv = 1.0f / sqrtf(var + 1e-6f);
+  la.sc = db->sc + kcol0;
+  la.sh = db->sh + kcol0;
+  return la;
+}
+
 // Dense layer over the tile: out[16][N] = A @ W + b, waves split N (NT tiles of 16 columns each).
 // `pf` holds this layer's first k-blocks on entry and the next layer's (Ln: K=Kn, N=Nn, NTN tiles)
 // on exit.  A may live in LDS or global memory.  Caller synchronises before/after.
-template <int NT, int NTN>
-__device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
-                                        int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
-                                        bool a_global = false) {
+// LNA: A is the raw output of a dense16_dp producer and `la` its deferred LayerNorm + ReLU.
+// DP (dense16_dp): also publish the deferred LayerNorm of this layer's output into `db` -- columns
+// [0, split) use P0, [split, N) use P1.
+template <int NT, int NTN, bool LNA = false, bool DP = false>
+__device__ __forceinline__ void dense16_core(const AS4 muz_dense& L, int K, int N, const float* A, int lda,
+                                             float* out, int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
+                                             bool a_global, const LnA& la, Dln* db, const AS4 muz_ln* P0,
+                                             const AS4 muz_ln* P1, int split) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int KB = (K + 15) >> 4;
   const int col0 = wv * NT * 16;
+  // DP: LayerNorm parameters of column threadIdx.x, loaded now and staged after the MFMA loop
+  float psc = 0.f, psh = 0.f;
+  const int pc = threadIdx.x;
+  if constexpr (DP) {
+    if (pc < N) {
+      const bool g1 = pc >= split;
+      const AS4 muz_ln* P = g1 ? P1 : P0;
+      psc = gp(P->scale)[g1 ? pc - split : pc];
+      psh = gp(P->bias)[g1 ? pc - split : pc];
+    }
+  }
   if (col0 >= N) {
     pf_issue<NTN>(pf, Ln, Kn, Nn);
+    if constexpr (DP) {
+      if (pc < N) {
+        db->sc[pc] = psc;
+        db->sh[pc] = psh;
+      }
+    }
     return;
   }
   const int r = lane & 15, g = lane >> 4;
@@ -243,58 +407,80 @@ __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, co
     b1[t] = pf.v1[t];
   }
   ST(ST_DENTRY);
-  mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global);
+  mfma_ring<NT, LNA>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global, la);
   ST(ST_MFMA);
   pf_issue<NTN>(pf, Ln, Kn, Nn);
   // The MFMA computes out^T (weights as the A operand), so lane (r, g) holds 4 CONSECUTIVE output
   // columns of row r: one 16-byte bias load and one ds_write_b128 per tile.
+  float st[4] = {0.f, 0.f, 0.f, 0.f};   // DP: sum, sum of squares of group 0, then group 1
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = col0 + t * 16 + 4 * g;
-    if (col < N) *reinterpret_cast<f32x4*>(out + r * ldo + col) = acc[t] + bb[t];
+    if (col < N) {
+      const f32x4 v = acc[t] + bb[t];
+      *reinterpret_cast<f32x4*>(out + r * ldo + col) = v;
+      if constexpr (DP) {
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          s += v[q];
+          s2 += v[q] * v[q];
+        }
+        if (col >= split) {
+          st[2] += s;
+          st[3] += s2;
+        } else {
+          st[0] += s;
+          st[1] += s2;
+        }
+      }
+    }
+  }
+  if constexpr (DP) {
+    // the 4 lanes of row r: (g0 + g1) | (g2 + g3) over permlane16, then the two halves over permlane32
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const LoHi<float> p = swap16(st[c]);
+      const LoHi<float> p2 = swap32(p.lo + p.hi);
+      st[c] = p2.lo + p2.hi;
+    }
+    if (g == 0) db->part[wv][r] = f32x4{st[0], st[1], st[2], st[3]};
+    if (pc < N) {
+      db->sc[pc] = psc;
+      db->sh[pc] = psh;
+    }
   }
   ST(ST_EPI);
+}
+
+template <int NT, int NTN>
+__device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
+                                        int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
+                                        bool a_global = false) {
+  dense16_core<NT, NTN>(L, K, N, A, lda, out, ldo, pf, Ln, Kn, Nn, a_global, LnA{}, nullptr, nullptr, nullptr, 0);
+}
+// dense16 whose A is normalised on the fly (the deferred LayerNorm + ReLU `la` of the producing layer)
+template <int NT, int NTN>
+__device__ __forceinline__ void dense16_la(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
+                                           int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn, const LnA& la) {
+  dense16_core<NT, NTN, true>(L, K, N, A, lda, out, ldo, pf, Ln, Kn, Nn, false, la, nullptr, nullptr, nullptr, 0);
+}
+// dense16 producing a deferred LayerNorm (P0 on [0, split), P1 on [split, N)) into db; LNA as dense16_la
+template <int NT, int NTN, bool LNA = false>
+__device__ __forceinline__ void dense16_dp(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
+                                           int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn, Dln* db,
+                                           const AS4 muz_ln& P0, const AS4 muz_ln* P1 = nullptr,
+                                           int split = 1 << 30, const LnA& la = LnA{}) {
+  dense16_core<NT, NTN, LNA, true>(L, K, N, A, lda, out, ldo, pf, Ln, Kn, Nn, false, la, db, &P0, P1, split);
 }
 
 // ---- row-wise ops: thread t -> row t/32, lane-in-row t%32 (half a wave per row) ---------------------
 __device__ __forceinline__ int trow() { return threadIdx.x / kRowLanes; }
 __device__ __forceinline__ int tsub() { return threadIdx.x % kRowLanes; }
-// Row reductions on the DPP / permlane network instead of ds_bpermute (which goes through the LDS
-// crossbar): xor-1 and xor-2 as quad_perm, then half-row and row mirrors, then a permlane swap across
-// the two 16-lane rows of a 32-lane row (and across wave halves for 64-lane rows).  Every lane of a
-// row ends with the same bits: each step combines a commutative pair in both lanes.
-template <class T>
-__device__ __forceinline__ unsigned as_u(T v) {
-  return __builtin_bit_cast(unsigned, v);
-}
-template <class T>
-__device__ __forceinline__ T from_u(unsigned u) {
-  return __builtin_bit_cast(T, u);
-}
-template <int CTRL, class T>
-__device__ __forceinline__ T dpp(T v) {
-  return from_u<T>((unsigned)__builtin_amdgcn_update_dpp(0, (int)as_u(v), CTRL, 0xF, 0xF, false));
-}
-enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140 };
-template <class T>
-struct LoHi {
-  T lo, hi;
-};
-// {value of the lower 16-lane row, value of the upper one} of each 32-lane group, in every lane.
-// (The two results are copied to plain scalars before the bit cast: bit-casting the vector element
-// directly loses the second result in this compiler.)
-template <class T>
-__device__ __forceinline__ LoHi<T> swap16(T v) {
-  const auto p = __builtin_amdgcn_permlane16_swap(as_u(v), as_u(v), false, false);
-  const unsigned lo = p[0], hi = p[1];
-  return {from_u<T>(lo), from_u<T>(hi)};
-}
-template <class T>
-__device__ __forceinline__ LoHi<T> swap32(T v) {
-  const auto p = __builtin_amdgcn_permlane32_swap(as_u(v), as_u(v), false, false);
-  const unsigned lo = p[0], hi = p[1];
-  return {from_u<T>(lo), from_u<T>(hi)};
-}
+// Row reductions on the DPP / permlane network (helpers above): xor-1 and xor-2 as quad_perm, then
+// half-row and row mirrors, then a permlane swap across the two 16-lane rows of a 32-lane row (and
+// across wave halves for 64-lane rows).  Every lane of a row ends with the same bits: each step
+// combines a commutative pair in both lanes.
 template <class T, class F>
 __device__ __forceinline__ T row_reduce(T v, F f) {
   static_assert(kRowLanes == 32 || kRowLanes == 64, "row width");
@@ -660,6 +846,16 @@ __device__ __forceinline__ void resblock16(const AS4 muz_resblock& R, float* X, 
   SYNC();
   dense16_ln<NT256, NTN, LN_RESID_RELU>(R.d1, LAT, LAT, T, LD, X, LD, pf, Ln, Kn, Nn, R.ln1);
   SYNC();
+#elif MUZ_DLN
+  // LayerNorm_0 + ReLU deferred into Dense_1's A reads
+  Dln* db = dln_buf(0);
+  dense16_dp<NT256, NT256>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT, db, R.ln0);
+  SYNC();
+  const LnP<LAT> p1 = ln_load<LAT>(R.ln1);
+  dense16_la<NT256, NTN>(R.d1, LAT, LAT, T, LD, U, LD, pf, Ln, Kn, Nn, dln_a(db, 0, 0, LAT, nw_for(LAT)));
+  SYNC();
+  ln16<LAT, LN_RESID_RELU>(U, LD, X, LD, p1);
+  SYNC();
 #else
   const LnP<LAT> p0 = ln_load<LAT>(R.ln0);
   dense16<NT256, NT256>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT);
@@ -738,6 +934,30 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
   }
   resblock16<NT256>(P.rb[0], a.X, a.T, a.U, pf, &P.rb[1].d0, LAT, LAT);
   resblock16<NT384>(P.rb[1], a.X, a.T, a.U, pf, &P.d03, LAT, 384);
+#if MUZ_DLN >= 2
+  // LayerNorm_1 | LayerNorm_3 of [policy Dense_0 | value Dense_3] deferred into Dense_1 / Dense_4, and
+  // LayerNorm_2 of Dense_1 into Dense_2; the value hidden layer's ReLU is applied as the head reads it
+  Dln* b0 = dln_buf(0);
+  Dln* b1 = dln_buf(1);
+  dense16_dp<NT384, NT128>(P.d03, LAT, 384, a.X, LD, a.W, LDW, pf, &P.d1, LAT, 128, b0, P.ln1, &P.ln3, LAT);
+  SYNC();
+  const HeadW hv = head_load(P.d5, 1);
+  dense16_dp<NT128, NT64, true>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &P.d4, 128, 64, b1, P.ln2, nullptr,
+                                1 << 30, dln_a(b0, 0, 0, LAT, nw_for(384)));                 // policy Dense_1
+  dense16_la<NT64, NTA>(P.d4, 128, 64, a.W + LAT, LDW, a.X, LD, pf, &P.d2, 128, A,
+                        dln_a(b0, 1, LAT, 128, nw_for(384)));                                // value Dense_4
+  ST(ST_PASS);
+  SYNC();
+  dense16_la<NTA, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn,
+                       dln_a(b1, 0, 0, 128, nw_for(128)));                                   // policy logits
+  {
+    const float zero[HeadW::kPer] = {};
+    const float v = head_dot_relu(a.X, LD, zero, hv, 0);
+    if (tsub() == 0) a.v0[trow()] = tanhf(v);
+  }
+  ST(ST_PASS);
+  SYNC();
+#else
   const LnP<LAT> p1 = ln_load<LAT>(P.ln1);
   const LnP<128> p3 = ln_load<128>(P.ln3);
   dense16<NT384, NT128>(P.d03, LAT, 384, a.X, LD, a.W, LDW, pf, &P.d1, LAT, 128);   // [policy Dense_0 | value Dense_3]
@@ -761,6 +981,7 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
   }
   ST(ST_PASS);
   SYNC();
+#endif
 }
 
 __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) {
@@ -840,6 +1061,14 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
     ST(ST_ROW);
   }
   SYNC();
+#if MUZ_DLN >= 3
+  // LayerNorm_1 + ReLU deferred into Dense_4's A reads
+  dense16_dp<NT256, NT256>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT, dln_buf(0), D.ln1);
+  SYNC();
+  const LnP<LAT> p2 = ln_load<LAT>(D.ln2);
+  dense16_la<NT256, NT256>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT,
+                           dln_a(dln_buf(0), 0, 0, LAT, nw_for(LAT)));
+#else
   const LnP<LAT> p1 = ln_load<LAT>(D.ln1);
   dense16<NT256, NT256>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT);
   SYNC();
@@ -847,6 +1076,7 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
   SYNC();
   const LnP<LAT> p2 = ln_load<LAT>(D.ln2);
   dense16<NT256, NT256>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT);
+#endif
   SYNC();
   ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, p2);
   SYNC();
