@@ -108,7 +108,12 @@ __device__ __forceinline__ LoHi<T> swap32(T v) {
 }
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+#ifdef MUZ_EXPT_NOMFMA   // timing experiment only (wrong results): one VALU fma instead of each MFMA
+  c[0] = fmaf(a, b, c[0]);
+  return c;
+#else
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+#endif
 }
 
 // acc[t] += A[16 rows][K] @ Wgroup[K][NT*16]  (KB = K/16 k-blocks; Wg = packed weights of this group).
@@ -211,10 +216,12 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
   // step kb: issue k-block kb+D into `nxt` (the buffer consumed at step kb-1), read A of kb+1,
   // multiply `cur` (= kb) with A of kb
   auto step = [&](int kb, const f32x4 (&cur)[NT], f32x4 (&nxt)[NT], const f32x4& acur, f32x4& anxt) {
+#ifndef MUZ_EXPT_NOLOAD   // timing experiment only (wrong results): no weight stream inside the loop
     if (kb + D < KB) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) nxt[t] = wp[(kb + D) * wstep + t];
     }
+#endif
     // Pin the issue point: without this the machine scheduler sinks each weight load next to its
     // first MFMA (one step of cover instead of D) once the loop is fully unrolled.
     __builtin_amdgcn_sched_barrier(0);
@@ -690,9 +697,15 @@ __device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
 }
 
 // ---- LDS arena of a 16-row tile ---------------------------------------------------------------------
-constexpr int LD = LAT + 4;      // 260: row stride of 256-wide buffers (keeps b128 reads 16B aligned)
-constexpr int LDW = 512 + 4;     // wide buffer (FiLM scale|shift 512, pred heads 384, concat 320)
-constexpr int LDE = 64 + 4;      // small buffer (action embed, global features)
+// Row strides (floats).  MUZ_LD_PAD 8 (stride = 8 mod 64 dwords) makes the MFMA loops' A-fragment
+// ds_read_b128 (lane (r, g) -> row r, dword 4g) conflict-free in all four 16-lane groups; with 4 two
+// lanes of each group share a 4-bank slot.
+#ifndef MUZ_LD_PAD
+#define MUZ_LD_PAD 4
+#endif
+constexpr int LD = LAT + MUZ_LD_PAD;     // row stride of 256-wide buffers (keeps b128 reads 16B aligned)
+constexpr int LDW = 512 + MUZ_LD_PAD;    // wide buffer (FiLM scale|shift 512, pred heads 384, concat 320)
+constexpr int LDE = 64 + MUZ_LD_PAD;     // small buffer (action embed, global features)
 constexpr int kArenaFloats = 4 * kRows * LD + kRows * LDW + kRows * LDE + 4 * kRows;
 
 struct Arena {
