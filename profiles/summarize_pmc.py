@@ -4,9 +4,11 @@ profiles/<tag>_pmc.json: per-launch counter means and the derived MFMA / LDS / L
     python profiles/summarize_pmc.py <tag>
 
 Derived (MI355X_MICROARCH.md, 'Per-instruction cycle constants' and 'L2'):
-  mfma_busy_frac   = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 256 CUs x 4 SIMDs)   (cycles, per SIMD)
+  gui_active_cycles = GRBM_GUI_ACTIVE / 8: rocprofv3 sums the GRBM counters over the 8 XCDs (a 3.86-ms
+                      launch reads 70.9 M = 8 x 8.86 M cycles at ~2.3 GHz)
+  mfma_busy_frac   = SQ_VALU_MFMA_BUSY_CYCLES / (gui_active_cycles x 256 CUs x 4 SIMDs)   (cycles, per SIMD)
   mfma_insts       = SQ_INSTS_VALU_MFMA_F32 (v_mfma_f32_16x16x4_f32, 2048 FLOP each)
-  mfma_flop_frac   = mfma_insts x 2048 / (GRBM_GUI_ACTIVE x 256 x 256 FLOP/clk/CU)
+  mfma_flop_frac   = mfma_insts x 2048 / (gui_active_cycles x 256 x 256 FLOP/clk/CU)
   l2_hit           = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
   lds_conflict     = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE"""
 import csv
@@ -17,7 +19,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-CUS, SIMDS = 256, 4
+CUS, SIMDS, XCDS = 256, 4, 8
 
 
 def passes(src):
@@ -34,6 +36,7 @@ def main():
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_pmc")
     mean, n = passes(src)
     gui = mean.get("GRBM_GUI_ACTIVE")
+    gui = gui / XCDS if gui else gui
     out = {"kernel": "k_gumbel_search", "workload": "profiles/search_microbench.py 4096 50 (one full-batch search "
            "per launch)", "launches_per_pass": n, "per_launch_mean": mean}
     if gui:
