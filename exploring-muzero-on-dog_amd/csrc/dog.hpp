@@ -39,6 +39,7 @@ struct DogG {   // one game in LDS
   int8_t pool[kMaxPool];
   int8_t shuffled[kMaxPool];
   unsigned long long wb[7];     // base validity bits by checking slot (env_dog.hip: dog_check_of)
+  unsigned long long wj[7], wr[7];   // k_dog_play: legal joker / real-card copies by checking slot
   int need_deal;
 };
 

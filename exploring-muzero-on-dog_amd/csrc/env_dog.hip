@@ -141,8 +141,11 @@ __device__ __forceinline__ void dog_finish(const DetConsts& c, const DogG& s, in
   reward = s.done ? 0 : (invalid ? -1 : (int)((w >> cp) & 1u));
 }
 
-__device__ void dog_step_swap(const DetConsts& c, DogG& s, int cp, int pin, int pos, int& reward, int& done) {
-  const bool invalid = !dog_val_swap(c, s, cp, pin, pos);
+// `legal`: the caller drew the action from the legal mask of this very state, so the step function's own
+// validity check (the same predicate) is skipped.
+__device__ void dog_step_swap(const DetConsts& c, DogG& s, int cp, int pin, int pos, int& reward, int& done,
+                              bool legal = false) {
+  const bool invalid = !legal && !dog_val_swap(c, s, cp, pin, pos);
   if (!invalid) {
     const int sp = s.board[pos];
     const int pp = s.pins[cp * 4 + pin];
@@ -155,22 +158,33 @@ __device__ void dog_step_swap(const DetConsts& c, DogG& s, int cp, int pin, int 
   dog_finish(c, s, cp, invalid, reward, done);
 }
 
+// `legal` (k_dog_play): the board equals set_pins_on_board(pins) before the move (every transition ends
+// with a rebuild or the equivalent swap update), the mover is on the board or at home and npos is a cell,
+// so the rebuild reduces to clearing the mover's old cell and writing its new one: the captured pin sat
+// on npos, which the mover now takes.
 __device__ void dog_capture_move(const DetConsts& c, DogG& s, int cp, int pin, int npos, bool invalid, int& reward,
-                                 int& done) {
+                                 int& done, bool legal = false) {
   if (!invalid) {
     const int at = s.board[jidx(npos, kCells)];
     if (at != -1 && (at != cp || has(c.flags, R_FRIENDLY)))
       for (int k = 0; k < 4; ++k)
         if (s.pins[at * 4 + k] == npos) s.pins[at * 4 + k] = -1;
+    const int cur = s.pins[cp * 4 + pin];
     s.pins[cp * 4 + pin] = (int8_t)npos;
-    dog_rebuild(c, s);
+    if (legal && npos >= 0 && npos < kCells) {
+      if (cur >= 0 && cur < kCells) s.board[cur] = -1;
+      s.board[npos] = (int8_t)cp;
+    } else {
+      dog_rebuild(c, s);
+    }
   }
   dog_finish(c, s, cp, invalid, reward, done);
 }
 
-__device__ void dog_step_normal(const DetConsts& c, DogG& s, int cp, int pin, int move, int& reward, int& done) {
+__device__ void dog_step_normal(const DetConsts& c, DogG& s, int cp, int pin, int move, int& reward, int& done,
+                                bool legal = false) {
   const uint32_t F = c.flags;
-  const bool invalid = !dog_val_normal(c, s, cp, pin, move);
+  const bool invalid = !legal && !dog_val_normal(c, s, cp, pin, move);
   const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
   const int tgt = cst(c.target, cp);
   const int g0 = dgoal(c, cp, 0);
@@ -191,12 +205,13 @@ __device__ void dog_step_normal(const DetConsts& c, DogG& s, int cp, int pin, in
     npos = gx;
   else
     npos = fitted;
-  dog_capture_move(c, s, cp, pin, npos, invalid, reward, done);
+  dog_capture_move(c, s, cp, pin, npos, invalid, reward, done, legal);
 }
 
-__device__ void dog_step_neg(const DetConsts& c, DogG& s, int cp, int pin, int& reward, int& done, int move = -4) {
-  const bool invalid = !dog_val_neg(c, s, cp, pin, move);
-  dog_capture_move(c, s, cp, pin, fmodp(s.pins[cp * 4 + pin] + move, kTrack), invalid, reward, done);
+__device__ void dog_step_neg(const DetConsts& c, DogG& s, int cp, int pin, int& reward, int& done, int move = -4,
+                             bool legal = false) {
+  const bool invalid = !legal && !dog_val_neg(c, s, cp, pin, move);
+  dog_capture_move(c, s, cp, pin, fmodp(s.pins[cp * 4 + pin] + move, kTrack), invalid, reward, done, legal);
 }
 
 // path bits [si, ei] (wrap when si > ei) inside [0, N); empty for a pin at home or not moving
@@ -208,9 +223,10 @@ __device__ __forceinline__ unsigned long long path_bits(int si, int ei, int N, b
   return si <= ei ? (ge(si) & le(ei)) : (ge(si) | le(ei));
 }
 
-__device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d)[4], int& reward, int& done) {
+__device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d)[4], int& reward, int& done,
+                              bool legal = false) {
   const uint32_t F = c.flags;
-  const bool invalid = !dog_val7(c, s, cp, d);
+  const bool invalid = !legal && !dog_val7(c, s, cp, d);
   const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
   const int tgt = cst(c.target, cp);
   int cur[4], moved[4], npos[4];
@@ -277,26 +293,44 @@ __device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d
   dog_finish(c, s, cp, invalid, reward, done);
 }
 
+// Cards in each player's hand: the 56 hand bytes as 7 eight-byte LDS reads, summed 4 bytes at a time.
+// Counts can go negative (the swap phase decrements without a check, dog.py:1084), so each dword's byte
+// sum is v_sad_u8's unsigned sum minus 256 per byte with the sign bit set.  Player p owns bytes
+// [14p, 14p + 14).
+__device__ __forceinline__ void dog_hand_counts(const DogG& s, int (&h)[4]) {
+  static_assert(__builtin_offsetof(DogG, hands) % 8 == 0, "hands must be 8-byte aligned");
+  const uint2* q = reinterpret_cast<const uint2*>(&s.hands[0][0]);
+  uint32_t d[14];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const uint2 v = q[i];
+    d[2 * i] = v.x;
+    d[2 * i + 1] = v.y;
+  }
+  auto ssum = [](uint32_t x) { return (int)__builtin_amdgcn_sad_u8(x, 0u, 0u) - 256 * __popc(x & 0x80808080u); };
+  h[0] = ssum(d[0]) + ssum(d[1]) + ssum(d[2]) + ssum(d[3] & 0xFFFFu);
+  h[1] = ssum(d[3] >> 16) + ssum(d[4]) + ssum(d[5]) + ssum(d[6]);
+  h[2] = ssum(d[7]) + ssum(d[8]) + ssum(d[9]) + ssum(d[10] & 0xFFFFu);
+  h[3] = ssum(d[10] >> 16) + ssum(d[11]) + ssum(d[12]) + ssum(d[13]);
+}
+
 // next player holding cards after the UNSUBSTITUTED current player (fori_loop of dog.py:1042-1046)
 __device__ __forceinline__ int dog_next_with_cards(const DetConsts& c, const DogG& s, int& total) {
+  int h[4];
+  dog_hand_counts(s, h);
   int nxt = -1;
   total = 0;
-  for (int p = 0; p < c.P; ++p) {
-    int h = 0;
-    for (int k = 0; k < kDogCards; ++k) h += s.hands[p][k];
-    total += h;
-  }
+  for (int p = 0; p < c.P; ++p) total += h[p];
   for (int i = 0; i < c.P; ++i) {
     const int cand = (s.cp + i + 1) % c.P;
-    int h = 0;
-    for (int k = 0; k < kDogCards; ++k) h += s.hands[cand][k];
-    if (nxt == -1 && h > 0) nxt = cand;
+    const int hc = cand == 0 ? h[0] : cand == 1 ? h[1] : cand == 2 ? h[2] : h[3];
+    if (nxt == -1 && hc > 0) nxt = cand;
   }
   return nxt;
 }
 
 // env_step (dog.py:1117-1131) on lane 0; returns 1 when a deal must follow.
-__device__ int dog_env_step(const DetConsts& c, DogG& s, int action, int& reward, int& done) {
+__device__ int dog_env_step(const DetConsts& c, DogG& s, int action, int& reward, int& done, bool legal = false) {
   if (s.phase == 1) {   // env_step_swap_phase (1077-1114): no validity check
     const int card = action - kDogPlay;
     const int cp0 = s.cp;
@@ -329,18 +363,18 @@ __device__ int dog_env_step(const DetConsts& c, DogG& s, int action, int& reward
     reward = -1;
     done = s.done;
   } else if (act < kDogSwaps) {
-    dog_step_swap(c, s, cp, act / kCells, act % kCells, reward, done);
+    dog_step_swap(c, s, cp, act / kCells, act % kCells, reward, done, legal);
   } else if (act < kDogNormalBase) {
     int d[4];
     for (int k = 0; k < 4; ++k) d[k] = c_dists7[act - kDogSwaps][k];
-    dog_step_hot7(c, s, cp, d, reward, done);
+    dog_step_hot7(c, s, cp, d, reward, done, legal);
   } else if (act < kDogNegBase) {
     const int na = act - kDogNormalBase;
     int mv = na % 12 + 1;
     mv += mv >= 7 ? 1 : 0;
-    dog_step_normal(c, s, cp, na / 12, mv, reward, done);
+    dog_step_normal(c, s, cp, na / 12, mv, reward, done, legal);
   } else {
-    dog_step_neg(c, s, cp, act - kDogNegBase, reward, done);
+    dog_step_neg(c, s, cp, act - kDogNegBase, reward, done, -4, legal);
   }
   if (reward != -1) s.hands[cp][card] = (int8_t)(s.hands[cp][card] - 1);
   int total;
@@ -348,7 +382,8 @@ __device__ int dog_env_step(const DetConsts& c, DogG& s, int action, int& reward
   s.cp = done ? cp : nxt;
   s.reward = reward;
   s.done = done;
-  return ((total == 0 || nxt == -1) && !done) ? 1 : 0;
+  (void)total;   // all(hand_cards == 0) implies nxt == -1 (dog.py:1059); per-player, not summed
+  return (nxt == -1 && !done) ? 1 : 0;
 }
 
 // no_step (dog.py:713-752) on lane 0; returns 1 when a deal must follow.
@@ -356,7 +391,8 @@ __device__ int dog_no_step(const DetConsts& c, DogG& s) {
   for (int k = 0; k < kDogCards; ++k) s.hands[s.cp][k] = 0;
   int total;
   const int nxt = dog_next_with_cards(c, s, total);
-  if (total > 0 && nxt != -1) {
+  (void)total;   // any(hand_cards > 0) <=> nxt != -1 (dog.py:752)
+  if (nxt != -1) {
     s.cp = nxt;
     return 0;
   }
@@ -427,6 +463,75 @@ __device__ __forceinline__ void dog_checks_block(const DetConsts& c, DogG& s, in
     if ((tid & 63) == 0) s.wb[tid >> 6] = b;
   }
   __syncthreads();
+}
+
+// k_dog_play's checks: as dog_checks_block, but the joker and real-card copies of each base action are
+// gated by the hand right here (two ballots), so the legal set is 14 slot-ordered words (wj then wr) in
+// LDS instead of the 806-bit mask.  Slot order is base order, so the k-th set bit over wj[0..6], wr[0..6]
+// is the k-th legal action in action order (joker copies [0, 396) before real copies [396, 792)).
+__device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int tid) {
+  if (s.phase == 0) {
+    const int cp = dog_sub(c, s);
+    const int i = dog_check_of(tid);
+    const bool hj = s.hands[cp][0] > 0;
+    const bool hr = i >= 0 && s.hands[cp][dog_base_card(i)] > 0;
+    const bool v = i >= 0 && (hj || hr) && dog_base_valid(c, s, cp, i);
+    const unsigned long long bj = __ballot(v && hj), br = __ballot(v && hr);
+    if ((tid & 63) == 0) {
+      s.wj[tid >> 6] = bj;
+      s.wr[tid >> 6] = br;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int dog_base_of_slot(int sl) {
+  return sl < 256 ? sl : (sl < 384 ? kDogSwaps + sl - 256 : kDogNormalBase + sl - 384);
+}
+
+// The k-th legal action, k = floor(u * count) (kth_legal over dog_mask_words, same result), from the
+// slot words of dog_checks_play (play phase) or the current player's cards (swap phase); -1 when nothing
+// is legal.  One full wave; the bit inside the chosen word is found by a ballot over per-lane prefix counts.
+__device__ __forceinline__ int dog_pick(const DogG& s, float u, int lane) {
+  unsigned long long w[14];
+  if (s.phase == 0) {
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      w[r] = s.wj[r];
+      w[7 + r] = s.wr[r];
+    }
+  } else {
+    w[0] = __ballot(lane < kDogCards && s.hands[s.cp][lane < kDogCards ? lane : 0] > 0);
+#pragma unroll
+    for (int r = 1; r < 14; ++r) w[r] = 0ull;
+  }
+  int tot = 0;
+#pragma unroll
+  for (int r = 0; r < 14; ++r) tot += __popcll(w[r]);
+  if (tot == 0) return -1;
+  int k = (int)(u * (float)tot);
+  k = k >= tot ? tot - 1 : k;
+  int word = -1, kk = 0;
+  unsigned long long x = 0;
+#pragma unroll
+  for (int r = 0; r < 14; ++r) {   // the word holding the k-th bit, without indexing w[] dynamically
+    const int pc = __popcll(w[r]);
+    if (word < 0) {
+      if (k < pc) {
+        word = r;
+        x = w[r];
+        kk = k;
+      } else {
+        k -= pc;
+      }
+    }
+  }
+  const bool set = (x >> lane) & 1ull;
+  const int before = __popcll(x & ((1ull << lane) - 1ull));
+  const int b = __ffsll((long long)__ballot(set && before == kk)) - 1;
+  if (s.phase != 0) return kDogPlay + b;
+  const int base = dog_base_of_slot((word % 7) * 64 + b);
+  return word < 7 ? base : kDogBase + base;
 }
 
 // valid_actions (dog.py:693-711) from s.wb as 13 wave-uniform words (bit a of word a/64); one wave.
@@ -503,56 +608,106 @@ __device__ __forceinline__ int kth_legal(const unsigned long long (&m)[13], floa
   return word * 64 + __ffsll((long long)x) - 1;
 }
 
+// Diagnostic build only (EXTRA=-DMUZ_DOG_STAMPS): per-phase shader-clock totals of k_dog_play, thread 0.
+#ifdef MUZ_DOG_STAMPS
+__device__ unsigned long long g_dog_stamps[8];
+#define DOG_STAMP_INIT() \
+  unsigned long long ds_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ds_last = __builtin_amdgcn_s_memtime()
+#define DOG_STAMP(i)                                          \
+  do {                                                        \
+    if (tid == 0) {                                           \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+      ds_acc[i] += _t - ds_last;                              \
+      ds_last = _t;                                           \
+    }                                                         \
+  } while (0)
+#define DOG_STAMP_END() \
+  do {                  \
+    if (tid == 0)       \
+      for (int i = 0; i < 8; ++i) atomicAdd(&g_dog_stamps[i], ds_acc[i]); \
+  } while (0)
+#else
+#define DOG_STAMP_INIT() do {} while (0)
+#define DOG_STAMP(i) do {} while (0)
+#define DOG_STAMP_END() do {} while (0)
+#endif
+
 // Config (d)'s actor: `nturns` turns of one game per workgroup with the state resident in LDS --
 // valid_actions -> uniform random legal action (turn0 + t) -> env_step, or no_step when nothing is legal
 // -> deal if needed.  A finished game stops (action -2), or with `auto_reset` restarts in place
 // (dog_reset_lds, deal counter continued) and keeps playing.  env_steps[g] (optional) accumulates the
 // turns played and episodes[g] (optional) the games finished; action / reward / done (optional) are
 // those of the last turn.
-__global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_eu(MUZ_DOG_WPE))) void k_dog_play(DetConsts c, muz_dog_soa st, unsigned long long seed,
-                                                               int turn0, int nturns, int auto_reset,
-                                                               int32_t* action_out, int8_t* reward, uint8_t* done,
-                                                               uint32_t* env_steps, uint32_t* episodes) {
+struct DogPlayArgs {
+  DetConsts c;
+  muz_dog_soa st;
+  unsigned long long seed;
+  int turn0, nturns, auto_reset;
+  int32_t* action_out;   // optional outputs of the last turn
+  int8_t* reward;
+  uint8_t* done;
+  uint32_t* env_steps;   // optional accumulators
+  uint32_t* episodes;
+};
+
+// All arguments come in one struct that the kernel reads through the kernarg segment (kernarg0: scalar
+// loads, the pointer laundered at each use), so the rule constants and the SoA pointers are reloaded where
+// they are needed instead of being held live across the turn loop -- at the 64-VGPR budget that kept
+// state spilled SGPRs into VGPR lanes and VGPRs into scratch.
+__global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_eu(MUZ_DOG_WPE))) void k_dog_play(
+    DogPlayArgs args) {
+  (void)args;
   __shared__ DogG s;
   const int tid = threadIdx.x, g = blockIdx.x;
-  if (st.done[g] && !auto_reset) {
+  auto A = []() -> const DogPlayArgs& { return *(const DogPlayArgs*)kernarg0<DogPlayArgs>(); };
+  if (A().st.done[g] && !A().auto_reset) {
     if (tid == 0) {
-      if (action_out) action_out[g] = -2;
-      if (reward) reward[g] = 0;
-      if (done) done[g] = 1;
+      if (A().action_out) A().action_out[g] = -2;
+      if (A().reward) A().reward[g] = 0;
+      if (A().done) A().done[g] = 1;
     }
     return;
   }
-  dog_load<BlockSync>(c, st, g, s, tid);
+  dog_load<BlockSync>(A().c, A().st, g, s, tid);
+  const int nturns = A().nturns;
   int played = 0, finished = 0, a = -2, r = 0;
+  DOG_STAMP_INIT();
   for (int t = 0; t < nturns; ++t) {
+    const DogPlayArgs& P = A();
+    const DetConsts& c = P.c;
     if (s.done) {        // block-uniform: read after a barrier
-      if (!auto_reset) break;
-      dog_reset_lds<BlockSync>(c, s, seed, g, s.deal, tid);
+      if (!P.auto_reset) break;
+      dog_reset_lds<BlockSync>(c, s, P.seed, g, s.deal, tid);
     }
-    dog_checks_block(c, s, tid);
+    DOG_STAMP(0);   // reset
+    dog_checks_play(c, s, tid);
+    DOG_STAMP(1);   // base checks (+ barrier)
     if (tid < 64) {
-      unsigned long long m[13];
-      dog_mask_words(c, s, tid, m);
-      a = kth_legal(m, random_action_uniform(seed, g, turn0 + t));
+      a = dog_pick(s, random_action_uniform(P.seed, g, P.turn0 + t), tid);
+      DOG_STAMP(2);   // action choice
       if (tid == 0) {
         int d = s.done;
         r = 0;
-        s.need_deal = a < 0 ? dog_no_step(c, s) : dog_env_step(c, s, a, r, d);
+        s.need_deal = a < 0 ? dog_no_step(c, s) : dog_env_step(c, s, a, r, d, true);
       }
+      DOG_STAMP(3);   // env_step / no_step (lane 0)
     }
     ++played;
     __syncthreads();
-    if (s.need_deal) dog_deal<BlockSync>(c, s, seed, g, tid);
+    DOG_STAMP(4);   // barrier
+    if (s.need_deal) dog_deal<BlockSync>(c, s, P.seed, g, tid);
+    DOG_STAMP(5);   // deal
     finished += s.done;
   }
-  dog_store<BlockSync>(c, st, g, s, tid);
+  DOG_STAMP_END();
+  const DogPlayArgs& P = A();
+  dog_store<BlockSync>(P.c, P.st, g, s, tid);
   if (tid == 0) {
-    if (action_out) action_out[g] = a;
-    if (reward) reward[g] = (int8_t)r;
-    if (done) done[g] = (uint8_t)s.done;
-    if (env_steps) env_steps[g] += (uint32_t)played;
-    if (episodes) episodes[g] += (uint32_t)finished;
+    if (P.action_out) P.action_out[g] = a;
+    if (P.reward) P.reward[g] = (int8_t)r;
+    if (P.done) P.done[g] = (uint8_t)s.done;
+    if (P.env_steps) P.env_steps[g] += (uint32_t)played;
+    if (P.episodes) P.episodes[g] += (uint32_t)finished;
   }
 }
 
@@ -691,6 +846,18 @@ static inline unsigned dog_blocks(int n) { return (unsigned)((n + kDogGamesPerBl
 
 extern "C" {
 
+#ifdef MUZ_DOG_STAMPS
+int muz_diag_dog_stamps(unsigned long long* host_out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_dog_stamps), sizeof(unsigned long long) * 8);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_dog_stamps), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
+
 int muz_dog_reset(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int32_t n, void* stream) {
   DOG_PROLOGUE(true)
   k_dog_reset<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, seed, n);
@@ -727,8 +894,8 @@ int muz_dog_step_move(const muz_rules* rules, muz_dog_soa st, const int32_t* kin
 int muz_dog_random_turn(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int32_t turn, int32_t* action,
                         int8_t* reward, uint8_t* done, int32_t n, void* stream) {
   DOG_PROLOGUE(true)
-  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(c, st, seed, turn, 1, 0, action, reward, done, nullptr,
-                                                              nullptr);
+  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(
+      DogPlayArgs{c, st, seed, turn, 1, 0, action, reward, done, nullptr, nullptr});
   return muz_last_launch_error();
 }
 
@@ -736,8 +903,8 @@ int muz_dog_random_play(const muz_rules* rules, muz_dog_soa st, uint64_t seed, i
                         int32_t auto_reset, uint32_t* env_steps, uint32_t* episodes, int32_t n, void* stream) {
   DOG_PROLOGUE(nturns >= 0)
   if (nturns == 0) return MUZ_OK;
-  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(c, st, seed, turn0, nturns, auto_reset ? 1 : 0, nullptr,
-                                                              nullptr, nullptr, env_steps, episodes);
+  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(
+      DogPlayArgs{c, st, seed, turn0, nturns, auto_reset ? 1 : 0, nullptr, nullptr, nullptr, env_steps, episodes});
   return muz_last_launch_error();
 }
 
