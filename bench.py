@@ -271,7 +271,9 @@ def run_dog(args):
         "roofline": {"bound": "hbm", "kernel": "k_dog_play", "achieved": round(achieved, 2),
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
                      "avg_launch_ms": round(avg_ms, 5), "bytes_per_launch": launch_bytes,
-                     "note": "latency-bound: 1024 games = 1024 workgroups of 7 waves; HBM is not the limit",
+                     "note": "latency-bound: 1024 games = 1024 workgroups of 7 waves, each game a serial chain "
+                             "of checks -> choice -> one-lane step per turn; waves wait 86 % of their cycles, VALU "
+                             "issue 4 % (profiles/r1c_dog_pmc.json); HBM is not the limit",
                      "traffic": None},
     }
     if world == 1 and not args.no_cpu_baseline:
