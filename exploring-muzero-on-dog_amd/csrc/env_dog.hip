@@ -5,6 +5,9 @@
 
 namespace muz {
 
+#ifndef MUZ_DOG_INCR
+#define MUZ_DOG_INCR 1
+#endif
 constexpr int kDogGamesPerBlock = 4;   // wave-per-game kernels (reset, explicit-action step)
 #ifndef MUZ_DOG_WPE
 #define MUZ_DOG_WPE 8      // waves per SIMD the play kernel is budgeted for: 4 blocks of 7 waves per CU (measured best)
@@ -171,7 +174,7 @@ __device__ void dog_capture_move(const DetConsts& c, DogG& s, int cp, int pin, i
         if (s.pins[at * 4 + k] == npos) s.pins[at * 4 + k] = -1;
     const int cur = s.pins[cp * 4 + pin];
     s.pins[cp * 4 + pin] = (int8_t)npos;
-    if (legal && npos >= 0 && npos < kCells) {
+    if (MUZ_DOG_INCR && legal && npos >= 0 && npos < kCells) {
       if (cur >= 0 && cur < kCells) s.board[cur] = -1;
       s.board[npos] = (int8_t)cp;
     } else {
@@ -293,25 +296,18 @@ __device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d
   dog_finish(c, s, cp, invalid, reward, done);
 }
 
-// Cards in each player's hand: the 56 hand bytes as 7 eight-byte LDS reads, summed 4 bytes at a time.
-// Counts can go negative (the swap phase decrements without a check, dog.py:1084), so each dword's byte
-// sum is v_sad_u8's unsigned sum minus 256 per byte with the sign bit set.  Player p owns bytes
-// [14p, 14p + 14).
+// Cards in each player's hand (counts can be negative: the swap phase decrements without a check,
+// dog.py:1084).  A v_sad_u8 variant over 8-byte reads of the hand bytes made the multi-turn kernel's
+// results differ run to run (measured; tests/test_gpu_dog.py::test_dog_play_deterministic), so plain
+// byte sums.
 __device__ __forceinline__ void dog_hand_counts(const DogG& s, int (&h)[4]) {
-  static_assert(__builtin_offsetof(DogG, hands) % 8 == 0, "hands must be 8-byte aligned");
-  const uint2* q = reinterpret_cast<const uint2*>(&s.hands[0][0]);
-  uint32_t d[14];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const uint2 v = q[i];
-    d[2 * i] = v.x;
-    d[2 * i + 1] = v.y;
+  for (int p = 0; p < 4; ++p) {
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < kDogCards; ++k) t += s.hands[p][k];
+    h[p] = t;
   }
-  auto ssum = [](uint32_t x) { return (int)__builtin_amdgcn_sad_u8(x, 0u, 0u) - 256 * __popc(x & 0x80808080u); };
-  h[0] = ssum(d[0]) + ssum(d[1]) + ssum(d[2]) + ssum(d[3] & 0xFFFFu);
-  h[1] = ssum(d[3] >> 16) + ssum(d[4]) + ssum(d[5]) + ssum(d[6]);
-  h[2] = ssum(d[7]) + ssum(d[8]) + ssum(d[9]) + ssum(d[10] & 0xFFFFu);
-  h[3] = ssum(d[10] >> 16) + ssum(d[11]) + ssum(d[12]) + ssum(d[13]);
 }
 
 // next player holding cards after the UNSUBSTITUTED current player (fori_loop of dog.py:1042-1046)

@@ -261,3 +261,26 @@ def test_dog_auto_reset_followed_by_oracle(cuda):
     e_dev = eps.cpu().numpy()
     assert all(e_dev[g] == n_eps[g] for g in follow)
     assert e_dev.sum() > B // 2, "random DOG games end within ~1000 turns; restarts must have happened"
+
+
+def test_dog_play_deterministic_and_launch_split_invariant(cuda):
+    """Config (d)'s workload (1024 games, 16-turn launches with in-place restarts): two runs agree exactly,
+    and so does the same schedule cut into single-turn launches (the state carried in LDS across turns
+    of one launch must equal the state round-tripped through HBM every turn)."""
+    D = _D()
+    B, seed, launches = 1024, 4, 30
+
+    def run(turns_per_launch):
+        rp = D.RandomPlay(B, seed=seed)
+        steps = torch.zeros(B, dtype=torch.int32, device="cuda")
+        eps = torch.zeros(B, dtype=torch.int32, device="cuda")
+        for _ in range(launches * 16 // turns_per_launch):
+            rp.play(turns_per_launch, steps, auto_reset=True, episodes=eps)
+        return D.to_host(rp.env), steps.cpu().numpy(), eps.cpu().numpy()
+
+    a, b, c = run(16), run(16), run(1)
+    for other in (b, c):
+        for k in a[0]:
+            assert np.array_equal(a[0][k], other[0][k]), k
+        assert np.array_equal(a[1], other[1]) and np.array_equal(a[2], other[2])
+    assert a[2].sum() > 10          # some games finished and restarted inside a launch
