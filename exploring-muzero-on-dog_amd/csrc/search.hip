@@ -33,6 +33,9 @@ __device__ unsigned long long g_muz_stamps[8];
 
 // Two of the ~31 workgroup barriers per simulation are not needed for correctness (see the uses); removing
 // them measured within noise on MI355X (B=4096 S=50: +-1 %), so they stay.
+#ifndef MUZ_YOUNG_PRIO
+#define MUZ_YOUNG_PRIO 0   // s_setprio 1 for waves 4-7: measured within noise (profiles/r1e_prio_ab.log)
+#endif
 #ifndef MUZ_SEL_SYNC
 #define MUZ_SEL_SYNC 1   // workgroup barrier between the tree walk and Dyn4's first pass
 #endif
@@ -185,6 +188,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
 
   if (n_dev) n = *n_dev;
   if ((int)blockIdx.x * kRows >= n) return;
+#if MUZ_YOUNG_PRIO
+  // static priority for the second-dispatched half (waves 4-7): it otherwise loses VALU arbitration to its
+  // SIMD partner at the start of every phase (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= kThreads / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   const Arena ar = Arena::carve(smem);
   const int A = Wt.num_actions;
   const int row = trow(), a = tsub();      // this lane holds action `a` of game `row`

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(HERE)
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
-    for w in ("classic", "dog"):
+    for w in (sys.argv[2:] or ("classic", "dog")):
         src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{w}")
         bench = open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1]
         open(os.path.join(HERE, f"{tag}_{w}_bench.json"), "w").write(bench + "\n")
