@@ -2,7 +2,7 @@
 """Self-play throughput benchmark: det-MADN, B = 4096 games per GPU, 50-simulation Gumbel MuZero.
 
 Metric (BASELINE.json): self-play env-steps/s (+ MCTS sims/s), det-MADN batch 4096, 1/2/4/8 GPU.
-  * one bench "step" = 16 x 4096 complete games per rank with a 50-simulation search per move (SURVEY
+  * one bench "step" = 32 x 4096 complete games per rank with a 50-simulation search per move (SURVEY
     §8d b), played 4096 at a time: the self-play batch is 4096 concurrent games, and a game that ends
     hands its lane to the next game (muz_detmadn_selfplay_stream).  --games 0 times the reference's
     own unit instead, one play_n_games_v3 call of 4096 games whose batch shrinks as games finish;
@@ -25,13 +25,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BATCH = 4096
-# One det bench step streams 16 x 4096 games through the 4096 concurrently played games (lanes): a lane
+# One det bench step streams 32 x 4096 games through the 4096 concurrently played games (lanes): a lane
 # whose game ends starts the next game, so searches run on a full batch instead of shrinking with the
 # finished games as one play_n_games_v3 batch does (its tail averages ~54 % active games).  Each game's
 # record is identical to the batch call's (tests/test_gpu_selfplay.py::test_stream_equals_batch).  Only
-# the drain at the end of a step (the last games of the queue finishing) runs on a partial batch; 16
-# generations keep that drain to a few percent of the step (8: ~12 %).
-STREAM_GENERATIONS = 16
+# the drain at the end of a step (the last games of the queue finishing) runs on a partial batch: ~12 %
+# of a step with 8 generations, ~6 % with 16, ~3 % with 32 (a continuously running actor has none).
+# Records of 131072 games (T = 500) take ~75 GB of the GPU's 288 GB HBM.
+STREAM_GENERATIONS = 32
 S = 50
 D = 25
 MAX_STEPS = 500
@@ -66,7 +67,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--games", type=int, default=-1,
-                    help="det: games per step streamed through the --batch lanes (default 16 x batch; 0 = one "
+                    help="det: games per step streamed through the --batch lanes (default 32 x batch; 0 = one "
                          "batch of --batch games, the reference's play_n_games_v3 call)")
     ap.add_argument("--train-steps", type=int, default=2500, help="train workload: learner steps per iteration")
     ap.add_argument("--workload", choices=("det", "classic", "dog", "train"), default="det",
