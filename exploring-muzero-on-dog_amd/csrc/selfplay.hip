@@ -17,7 +17,10 @@
 
 namespace muz {
 
-constexpr int kSpBlock = 256;
+#ifndef MUZ_SP_BLOCK
+#define MUZ_SP_BLOCK 256
+#endif
+constexpr int kSpBlock = MUZ_SP_BLOCK;
 
 // lane_game (streaming driver only): game number of each lane, -1 = idle; a game whose record is full
 // (idx == T, the reference's max_steps) stops like a finished one.
