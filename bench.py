@@ -70,14 +70,49 @@ def parse():
                     help="det: games per step streamed through the --batch lanes (default 32 x batch; 0 = one "
                          "batch of --batch games, the reference's play_n_games_v3 call)")
     ap.add_argument("--train-steps", type=int, default=2500, help="train workload: learner steps per iteration")
-    ap.add_argument("--workload", choices=("det", "classic", "dog", "train"), default="det",
+    ap.add_argument("--workload", choices=("det", "classic", "dog", "train", "selftest"), default="det",
                     help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
+    ap.add_argument("--split", action="store_true",
+                    help="strong scaling (SURVEY §8e): --batch is the WHOLE job's batch, split evenly over the ranks "
+                         "(det 4096 -> 2048/1024/512 per GPU); default is weak scaling, --batch games per GPU")
     args = ap.parse_args()
     if args.workload == "dog" and args.batch == BATCH:
         args.batch = DOG_BATCH
+    args.job_batch = args.batch
+    if args.split:
+        world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+        if args.batch % world:
+            raise SystemExit(f"--split: batch {args.batch} is not divisible by {world} ranks")
+        args.batch //= world
     if args.games < 0:
         args.games = STREAM_GENERATIONS * args.batch
     return args
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher around it: start N fresh child processes of this script, one per
+    GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what torch.distributed.run
+    would set), wait for all of them and exit with the worst status.  This parent never touches the GPU; each
+    child initialises its own device and the process group.  Rank 0 prints the job's JSON line."""
+    import socket
+    import subprocess
+    backend = os.environ.get("MUZ_BENCH_BACKEND", "nccl")
+    if backend == "nccl":
+        import torch   # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if n > have:
+            raise SystemExit(f"bench.py --gpus {n}: only {have} GPU(s) visible")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
 
 
 def dist_env():
@@ -85,19 +120,6 @@ def dist_env():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     return rank, world, local
-
-
-def reduce_results(dist, device, steps_done, searches, elapsed, search_ms, launches):
-    """Sum work over ranks, max of wall time (the slowest rank bounds the job)."""
-    import torch
-    if dist is None:
-        return steps_done, searches, elapsed, search_ms, launches
-    t = torch.tensor([float(steps_done), float(searches), search_ms, float(launches)], dtype=torch.float64,
-                     device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    m = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    dist.all_reduce(m, op=dist.ReduceOp.MAX)
-    return t[0].item(), t[1].item(), m[0].item(), t[2].item(), t[3].item()
 
 
 def cpu_baseline(seconds, sims, depth, max_steps):
@@ -156,36 +178,55 @@ def measured_traffic():
 
 def setup(args):
     rank, world, local = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}")
     import torch
     import muzpkg
     muzpkg.load()
     dist = None
+    backend = os.environ.get("MUZ_BENCH_BACKEND", "nccl")
+    if backend == "gloo":      # CPU rehearsal of the launcher / reduction path (tests/test_bench_launcher.py)
+        device = torch.device("cpu")
+    else:
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", init_method="env://")
+        tdist.init_process_group(backend, init_method="env://")
         dist = tdist
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
     return rank, world, dist, device
+
+
+def parallelism(args, world):
+    if args.split:
+        return f"dp{world} strong: {args.job_batch} games split {args.batch}/GPU"
+    return f"dp{world} weak: {args.batch} games/GPU, independent games"
+
+
+def synchronize(device):
+    import torch
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
 
 
 def timed_region(dist, fn, steps):
     """barrier + synchronize, K steps, synchronize + barrier; returns the rank's elapsed seconds."""
     import torch
+    dev = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    synchronize(dev)
     t0 = time.perf_counter()
     for k in range(steps):
         fn(k)
-    torch.cuda.synchronize()
+    synchronize(dev)
     if dist is not None:
         dist.barrier()
     return time.perf_counter() - t0
 
 
 def sum_max(dist, device, sums, elapsed):
+    """Sum work over ranks, max of wall time (the slowest rank bounds the job)."""
     import torch
     if dist is None:
         return sums, elapsed
@@ -262,13 +303,13 @@ def run_dog(args):
         "metric": "self-play env steps/sec, DOG 2v2 random legal policy (config d)",
         "value": round(steps_done / elapsed, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "scaling": "strong" if args.split else "weak", "vs_baseline": None, "dtype": "int8",
         "data": "synthetic (seeded deals, counter-RNG random legal actions)", "games_finished": int(games),
         "config": {"workload": f"DOG 4p teams, {args.batch} games/GPU, uniform random legal action per turn, "
                                f"{T} turns per step in one launch (state resident in LDS), finished games "
                                f"restart in place", "games_per_gpu": args.batch,
                    "turns_per_step": T,
-                   "parallelism": f"independent games, {world} rank(s)"},
+                   "parallelism": parallelism(args, world)},
         "roofline": {"bound": "hbm", "kernel": "k_dog_play", "achieved": round(achieved, 2),
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
                      "avg_launch_ms": round(avg_ms, 5), "bytes_per_launch": launch_bytes,
@@ -323,14 +364,14 @@ def run_classic(args):
         "metric": "self-play env steps/sec + MCTS sims/sec, classic MADN 4p teams (config c)",
         "value": round(steps_done / elapsed, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "scaling": "strong" if args.split else "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (self-generated games, seeded random fp32 weights)",
         "config": {"workload": f"classic MADN {CLASSIC_PLAYERS}p teams self-play, {args.batch} games/GPU, "
                                f"Stochastic MuZero S={args.sims} D={args.depth}, max_steps={args.max_steps}"
                                + (f", {args.games} games per step streamed through the {args.batch} lanes"
                                   if args.games else ""), "games_per_step": args.games or args.batch,
                    "games_per_gpu": args.batch, "num_simulations": args.sims, "max_depth": args.depth,
-                   "parallelism": f"independent games, {world} rank(s)"},
+                   "parallelism": parallelism(args, world)},
         "sims_per_s": round(searches * args.sims / elapsed, 1),
         "env_steps": int(steps_done), "searches": int(searches),
         "search_kernel": {"kernel": "k_stochastic_search", "avg_launch_ms": round(search_ms / max(1, turns), 4)},
@@ -425,30 +466,37 @@ def run_train(args):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
-    if args.workload == "train":
-        return run_train(args)
-    if args.workload == "dog":
-        return run_dog(args)
-    if args.workload == "classic":
-        return run_classic(args)
-    rank, world, local = dist_env()
+def run_selftest(args):
+    """CPU rehearsal of the multi-rank plumbing (launcher, barrier + timed region, sum / max reduction,
+    rank-0 JSON) without a GPU: each rank 'processes' (rank + 1) x batch units per step.  Only for
+    tests/test_bench_launcher.py (MUZ_BENCH_BACKEND=gloo)."""
+    rank, world, dist, device = setup(args)
+    done = {"units": 0}
+
+    def step(k):
+        time.sleep(0.01 * (rank + 1))
+        done["units"] += (rank + 1) * args.batch
+
+    elapsed = timed_region(dist, step, args.steps)
+    (units,), elapsed = sum_max(dist, device, [done["units"]], elapsed)
+    if rank == 0:
+        print(json.dumps({"metric": "launcher selftest", "value": units / elapsed, "unit": "units/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "units": int(units),
+                          "elapsed": elapsed, "scaling": "strong" if args.split else "weak",
+                          "config": {"games_per_gpu": args.batch, "parallelism": parallelism(args, world)}}),
+              flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_det(args):
+    """Config (b), the BASELINE.json headline: det-MADN 2p self-play, 4096 concurrent games per GPU (or the
+    job's 4096 split over the ranks with --split), Gumbel MuZero S=50 D=25."""
     import torch
-    import muzpkg
-    muzpkg.load()
+    rank, world, dist, device = setup(args)
     from exploring_muzero_on_dog_amd import game_agent as GA
     from exploring_muzero_on_dog_amd import nets as N
     from exploring_muzero_on_dog_amd import detmadn as E
-
-    dist = None
-    if world > 1:
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", init_method="env://")
-        dist = tdist
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
 
     C = E.num_channels(PLAYERS)
     net = N.DeviceNet(N.init_muzero_params(0, C), C, device=device)
@@ -463,29 +511,19 @@ def main():
     for w in range(args.warmup):
         play(10_000 * rank + w)
     torch.cuda.synchronize()
+    acc = {"steps": 0, "searches": 0, "search_ms": 0.0, "launches": 0}
 
-    steps_done = 0
-    searches = 0
-    search_ms = 0.0
-    launches = 0
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
+    def step(k):
         buf = play(10_000 * rank + 1000 + k)
         st = eng.last_stats
-        steps_done += int(buf["idx"].sum().item())
-        searches += st["searches"]
-        search_ms += st["search_ms"]
-        launches += st["turns"]
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+        acc["steps"] += int(buf["idx"].sum().item())
+        acc["searches"] += st["searches"]
+        acc["search_ms"] += st["search_ms"]
+        acc["launches"] += st["turns"]
 
-    steps_done, searches, elapsed, search_ms, launches = reduce_results(dist, device, steps_done, searches, elapsed,
-                                                                         search_ms, launches)
+    elapsed = timed_region(dist, step, args.steps)
+    (steps_done, searches, search_ms, launches), elapsed = sum_max(
+        dist, device, [acc["steps"], acc["searches"], acc["search_ms"], acc["launches"]], elapsed)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -504,16 +542,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1000 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.split else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (self-generated games, seeded random fp32 weights)",
         "config": {"workload": f"det-MADN {PLAYERS}p self-play, {args.batch} games/GPU, Gumbel MuZero "
                                f"S={args.sims} D={args.depth}, max_steps={args.max_steps}, temp={TEMP}"
-                               + (f", {args.games} games per step streamed through the {args.batch} lanes"
+                               + (f", {args.games} games per step per GPU streamed through the {args.batch} lanes"
                                   if args.games else ""),
-                   "games_per_gpu": args.batch, "games_per_step": args.games or args.batch, "num_simulations": args.sims, "max_depth": args.depth,
-                   "parallelism": f"independent games, {world} rank(s)"},
+                   "games_per_gpu": args.batch, "job_batch": args.job_batch if args.split else args.batch * world,
+                   "games_per_step": (args.games or args.batch) * world,
+                   "num_simulations": args.sims, "max_depth": args.depth,
+                   "parallelism": parallelism(args, world)},
         "sims_per_s": round(searches * args.sims / elapsed, 1),
         "env_steps": int(steps_done),
         "searches": int(searches),
@@ -530,6 +570,14 @@ def main():
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    return {"train": run_train, "dog": run_dog, "classic": run_classic, "det": run_det,
+            "selftest": run_selftest}[args.workload](args)
 
 
 if __name__ == "__main__":

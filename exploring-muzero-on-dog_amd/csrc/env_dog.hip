@@ -296,18 +296,20 @@ __device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d
   dog_finish(c, s, cp, invalid, reward, done);
 }
 
-// Cards in each player's hand (counts can be negative: the swap phase decrements without a check,
-// dog.py:1084).  A v_sad_u8 variant over 8-byte reads of the hand bytes made the multi-turn kernel's
-// results differ run to run (measured; tests/test_gpu_dog.py::test_dog_play_deterministic), so plain
-// byte sums.
+// Cards in each player's hand: the 56 hand bytes as 7 eight-byte LDS reads (memcpy, no type pun), summed
+// 4 bytes at a time.  Counts can go negative (the swap phase decrements without a check, dog.py:1084), so
+// each dword's byte sum is v_sad_u8's unsigned sum minus 256 per byte with the sign bit set.  Player p owns
+// bytes [14p, 14p + 14).  (Round 1 blamed this function for k_dog_play's run-to-run differences; the cause
+// was the unordered s.done read in the turn loop, see k_dog_play.)
 __device__ __forceinline__ void dog_hand_counts(const DogG& s, int (&h)[4]) {
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    int t = 0;
-#pragma unroll
-    for (int k = 0; k < kDogCards; ++k) t += s.hands[p][k];
-    h[p] = t;
-  }
+  static_assert(__builtin_offsetof(DogG, hands) % 8 == 0, "hands must be 8-byte aligned");
+  uint32_t d[14];
+  __builtin_memcpy(d, &s.hands[0][0], sizeof(d));
+  auto ssum = [](uint32_t x) { return (int)__builtin_amdgcn_sad_u8(x, 0u, 0u) - 256 * __popc(x & 0x80808080u); };
+  h[0] = ssum(d[0]) + ssum(d[1]) + ssum(d[2]) + ssum(d[3] & 0xFFFFu);
+  h[1] = ssum(d[3] >> 16) + ssum(d[4]) + ssum(d[5]) + ssum(d[6]);
+  h[2] = ssum(d[7]) + ssum(d[8]) + ssum(d[9]) + ssum(d[10] & 0xFFFFu);
+  h[3] = ssum(d[10] >> 16) + ssum(d[11]) + ssum(d[12]) + ssum(d[13]);
 }
 
 // next player holding cards after the UNSUBSTITUTED current player (fori_loop of dog.py:1042-1046)
@@ -671,9 +673,16 @@ __global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_e
   for (int t = 0; t < nturns; ++t) {
     const DogPlayArgs& P = A();
     const DetConsts& c = P.c;
-    if (s.done) {        // block-uniform: read after a barrier
+    // s.done is block-uniform: its last writer (lane 0's env_step) is ordered before these reads by the
+    // turn-end barrier.  When the game ended, the barrier below keeps dog_reset_lds's s.done = 0 (tid 0,
+    // before its first barrier) from overtaking a wave that has not read s.done yet -- without it, such a
+    // wave read 0, skipped the reset, and its barriers paired with the wrong ones of the other waves
+    // (the run-to-run differences of round 1).
+    if (s.done) {
       if (!P.auto_reset) break;
-      dog_reset_lds<BlockSync>(c, s, P.seed, g, s.deal, tid);
+      const unsigned deal = s.deal;
+      __syncthreads();
+      dog_reset_lds<BlockSync>(c, s, P.seed, g, deal, tid);
     }
     DOG_STAMP(0);   // reset
     dog_checks_play(c, s, tid);

@@ -268,7 +268,9 @@ def test_dog_play_deterministic_and_launch_split_invariant(cuda):
     and so does the same schedule cut into single-turn launches (the state carried in LDS across turns
     of one launch must equal the state round-tripped through HBM every turn)."""
     D = _D()
-    B, seed, launches = 1024, 4, 30
+    # 100 launches = 1600 turns: most games end and restart at least once inside a launch, which is where
+    # round 1's unordered s.done read (fixed in k_dog_play) made runs differ
+    B, seed, launches = 1024, 4, 100
 
     def run(turns_per_launch):
         rp = D.RandomPlay(B, seed=seed)
@@ -278,9 +280,9 @@ def test_dog_play_deterministic_and_launch_split_invariant(cuda):
             rp.play(turns_per_launch, steps, auto_reset=True, episodes=eps)
         return D.to_host(rp.env), steps.cpu().numpy(), eps.cpu().numpy()
 
-    a, b, c = run(16), run(16), run(1)
-    for other in (b, c):
+    a, b, b2, c = run(16), run(16), run(16), run(1)
+    for other in (b, b2, c):
         for k in a[0]:
             assert np.array_equal(a[0][k], other[0][k]), k
         assert np.array_equal(a[1], other[1]) and np.array_equal(a[2], other[2])
-    assert a[2].sum() > 10          # some games finished and restarted inside a launch
+    assert a[2].sum() > B // 2      # most games finished and restarted inside a launch
