@@ -100,7 +100,7 @@ def play_vs_random(net: N.DeviceNet | None, num_games: int, num_players: int = 4
         if ag.numel():
             sub = _sub(env, ag)
             obs = E.encode_board(sub)
-            out, _ = M.run_muzero_mcts(net, obs, bits[ag], num_simulations, max_depth, 0.0, seed=seed, turn=turn,
+            out, _ = M.muzero_mcts(net, obs, bits[ag], num_simulations, max_depth, 0.0, seed=seed, turn=turn,
                                        workspace=ws)
             act[ag] = out.action
         if rd.numel():

@@ -110,8 +110,25 @@ class SelfPlayEngine:
         return self._sbuf
 
 
-def play_n_games_v3(net: N.DeviceNet, seed: int, num_envs: int, num_simulation: int, max_depth: int,
-                    max_steps: int, temp: float, num_players: int = 4, rules: dict | None = None) -> dict:
-    """play_n_games_v3 (game_agent.py:185-192) -> trajectory buffers (device tensors)."""
-    eng = SelfPlayEngine(net, num_envs, num_players, max_steps, num_simulation, max_depth, rules)
-    return eng.play(seed, temp)
+REFERENCE_DTYPES = {"obs": torch.float32, "act": torch.int32, "rew": torch.int32, "val": torch.float32,
+                    "pol": torch.float32, "mask": torch.float32, "player": torch.int32, "team": torch.int32,
+                    "discount": torch.int32, "idx": torch.int32}
+
+
+def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_depth, max_steps, temp,
+                    rules: dict | None = None, obs_dtype=torch.float32) -> dict:
+    """play_n_games_v3 (MuZero_det_MADN/game_agent.py:185-192), reference signature.
+
+    ``params``: init_muzero_params' nested Flax dict (or a flat dict / DeviceNet, nets.as_device_net);
+    ``rng_key``: int or uint32[2] key (nets.rng_key_to_seed; the engine's counter RNG, not threefry);
+    ``input_shape``: (C, 56) with C = 8P + 2, which fixes the player count (the reference's game_agent
+    plays P = 4, C = 34).  Returns the reference's buffer dict (game_agent.py:158-169): obs fp32
+    [num_envs, max_steps, C, 56] (``obs_dtype=torch.int8`` keeps the engine's exact int8 copy), act / rew /
+    player / team / discount int32, val / mask fp32, pol fp32 [.., 24], idx int32 -- device tensors."""
+    C = int(input_shape[0])
+    if (C - 2) % 8 or int(input_shape[-1]) != E.CELLS:
+        raise ValueError(f"input_shape {tuple(input_shape)} is not (8P + 2, 56)")
+    net = N.as_device_net(params, C)
+    eng = SelfPlayEngine(net, num_envs, (C - 2) // 8, max_steps, num_simulation, max_depth, rules)
+    buf = eng.play(N.rng_key_to_seed(rng_key), temp)
+    return {k: v.to(REFERENCE_DTYPES[k] if k != "obs" else obs_dtype) for k, v in buf.items()}

@@ -103,9 +103,20 @@ class StochasticSelfPlayEngine:
         return self._sbuf
 
 
-def play_n_games_v3(net: ST.DeviceClassicNet, seed: int, num_envs: int, num_simulation: int, max_depth: int,
-                    max_steps: int, temp: float) -> dict:
-    """game_agent_stochastic.py:234-257 (the reset seeds only feed jax's unused random start)."""
-    eng = StochasticSelfPlayEngine(net, num_envs, max_steps=max_steps, num_simulations=num_simulation,
-                                   max_depth=max_depth)
-    return eng.play(seed, temp)
+def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_depth, max_steps, temp,
+                    obs_dtype=torch.float32) -> dict:
+    """play_n_games_v3 (MuZero_Classic_MADN/game_agent_stochastic.py:220-244), reference signature: Flax
+    params dict (or flat dict / DeviceClassicNet), int / uint32[2] key (the engine's counter RNG), input_shape
+    (2P + 3, 56).  Returns the reference's buffers (obs fp32 unless ``obs_dtype``; dice int32, dice_dist fp32)
+    as device tensors.  The reference's reset seeds only feed jax's unused random start."""
+    from .game_agent import REFERENCE_DTYPES
+    from .nets import rng_key_to_seed
+    C = int(input_shape[0])
+    if (C - 3) % 2 or int(input_shape[-1]) != E.CELLS:
+        raise ValueError(f"input_shape {tuple(input_shape)} is not (2P + 3, 56)")
+    net = ST.as_device_classic_net(params, C)
+    eng = StochasticSelfPlayEngine(net, num_envs, num_players=(C - 3) // 2, max_steps=max_steps,
+                                   num_simulations=num_simulation, max_depth=max_depth)
+    buf = eng.play(rng_key_to_seed(rng_key), temp)
+    dt = dict(REFERENCE_DTYPES, obs=obs_dtype, dice=torch.int32, dice_dist=torch.float32)
+    return {k: v.to(dt[k]) for k, v in buf.items()}

@@ -320,7 +320,8 @@ class Learner:
         for k in self.KEYS:
             self._static[k].copy_(batch[k])
         self._g.replay()
-        return self._out
+        # the captured outputs are overwritten by the next replay: hand out copies so a caller may keep them
+        return {k: v.clone() for k, v in self._out.items()}
 
     def push_to(self, net: "N.DeviceNet"):
         """Pack the current parameters into the self-play engine's arena (same layout) in place."""

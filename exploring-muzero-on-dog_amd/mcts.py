@@ -7,6 +7,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from . import lib as _L
@@ -76,11 +77,36 @@ def gumbel_muzero_policy(net: _N.DeviceNet, root_logits, root_value, root_embedd
     return PolicyOutput(action, weights), value
 
 
-def run_muzero_mcts(net: _N.DeviceNet, observations, legal_bits, num_simulations, max_depth, temperature,
-                    gumbel=None, seed=0, turn=0, workspace: SearchWorkspace | None = None):
-    """run_muzero_mcts (lines 663-704): root inference + Gumbel search over a batch of observations.
-    The reference passes ``invalid_actions = ~valid_action``; here the 24-bit legal mask is passed."""
+def muzero_mcts(net: _N.DeviceNet, observations, legal_bits, num_simulations, max_depth, temperature,
+                gumbel=None, seed=0, turn=0, workspace: SearchWorkspace | None = None):
+    """Device-native form of run_muzero_mcts: a DeviceNet, device observations and the 24-bit legal mask
+    per game (what the self-play / evaluation loops hold); root inference + Gumbel search."""
     scratch = workspace.scratch if workspace is not None else None
     logits, value, emb = _N.root_inference_fn(net, observations, scratch)
     return gumbel_muzero_policy(net, logits, value, emb, legal_bits, num_simulations, max_depth, temperature,
                                 gumbel=gumbel, seed=seed, turn=turn, workspace=workspace)
+
+
+def invalid_to_bits(invalid_actions) -> torch.Tensor:
+    """bool [B, A] invalid mask (True = illegal, the reference's ``~valid_action``) -> int32 legal bits [B]."""
+    inv = invalid_actions if isinstance(invalid_actions, torch.Tensor) else torch.from_numpy(
+        np.asarray(invalid_actions, dtype=bool))
+    inv = inv.reshape(inv.shape[0], -1).to(torch.bool)
+    sh = torch.arange(inv.shape[1], device=inv.device, dtype=torch.int64)
+    return ((~inv).to(torch.int64) << sh).sum(1).to(torch.int32)
+
+
+def run_muzero_mcts(params, rng_key, observations, invalid_actions, num_simulations, max_depth, temperature):
+    """run_muzero_mcts (MuZero_det_MADN/muzero_deterministic_madn.py:663-704), reference signature.
+
+    ``params``: init_muzero_params' nested Flax dict (or a flat dict / DeviceNet, see nets.as_device_net);
+    ``rng_key``: int or uint32[2] key (selects the engine's Gumbel stream, nets.rng_key_to_seed);
+    ``observations``: [B, C, 56] (NumPy or torch, any device); ``invalid_actions``: bool [B, 24].
+    Returns (PolicyOutput(action, action_weights), root_value = search_tree.summary().value) as device
+    tensors on cuda."""
+    dev = torch.device("cuda")
+    net = _N.as_device_net(params, device=dev)
+    obs = observations if isinstance(observations, torch.Tensor) else torch.from_numpy(np.asarray(observations))
+    obs = obs.to(device=dev, dtype=torch.float32)
+    bits = invalid_to_bits(invalid_actions).to(dev)
+    return muzero_mcts(net, obs, bits, num_simulations, max_depth, temperature, seed=_N.rng_key_to_seed(rng_key))

@@ -256,3 +256,42 @@ def recurrent_inference_fn(net: DeviceNet, action: torch.Tensor, embedding: torc
                                     _L.ptr(logits), _L.ptr(value), _L.ptr(nxt), _L.stream_ptr()),
              "muz_nets_recurrent")
     return reward, discount, logits, value, nxt
+
+
+# ---------------------------------------------------------------------------------- reference params
+_NET_CACHE: dict = {}
+
+
+def rng_key_to_seed(rng_key) -> int:
+    """The reference's ``rng_key`` argument -> this engine's 64-bit counter-RNG seed.  Accepts an int or a
+    jax-style uint32[2] key (key data as a list / NumPy / torch array).  jax's threefry streams are not
+    reproduced: the key only selects the engine's own noise stream, deterministically."""
+    if isinstance(rng_key, (int, np.integer)):
+        return int(rng_key) & ((1 << 64) - 1)
+    k = np.asarray(rng_key.cpu() if isinstance(rng_key, torch.Tensor) else rng_key).astype(np.uint64).ravel()
+    if k.size != 2:
+        raise ValueError(f"rng_key must be an int or a uint32[2] key, got shape {k.shape}")
+    return int((int(k[0]) << 32) | int(k[1]))
+
+
+def as_device_net(params, obs_channels: int | None = None, device="cuda") -> DeviceNet:
+    """The reference's ``params`` argument -> a DeviceNet (packed once, cached per params object).
+
+    Accepts what the reference passes around -- init_muzero_params' nested Flax tree
+    (``{"representation": {"params": ...}, "dynamics": ..., "prediction": ...}``,
+    muzero_deterministic_madn.py:706-748), a flat ``"net/Layer/param"`` dict, or a DeviceNet.  The channel
+    count is read from the representation's Dense_1 kernel (C - 6 inputs) when not given."""
+    if isinstance(params, DeviceNet):
+        return params
+    hit = _NET_CACHE.get(id(params))
+    if hit is not None and hit[0] is params and str(hit[1].buffer.device) == str(torch.device(device)):
+        return hit[1]
+    from . import checkpoint as CK
+    flat = params if all(isinstance(k, str) and "/" in k for k in params) else CK.muzero_tree_to_flat(params)
+    flat = {k: np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v, np.float32) for k, v in flat.items()}
+    C = int(flat["representation/Dense_1/kernel"].shape[0]) + 6 if obs_channels is None else int(obs_channels)
+    A = int(flat["prediction/Dense_2/kernel"].shape[1])
+    net = DeviceNet(flat, C, A, device=device)
+    _NET_CACHE.clear()          # one live weight set per process is what the reference's loops use
+    _NET_CACHE[id(params)] = (params, net)
+    return net

@@ -101,12 +101,14 @@ class VectorizedReplayBuffer:
         that every value is an integer in [-128, 127], so the conversion is exact), copied into pinned
         (page-locked) memory and sent with one asynchronous host->device copy on the current stream
         (hipMemcpyAsync; the pinned block is released once its copy has completed).  Fields already on
-        the ring's device pass through untouched."""
+        the ring's device pass through (made contiguous if they are strided views)."""
         out = {}
         for k, v in all_buffers.items():
             want = self.TRAJ_DTYPES.get(k, None)
             if isinstance(v, torch.Tensor) and v.device == self.device:
-                out[k] = v if want is None or v.dtype == want or k == "obs" else v.to(want)
+                # the kernels read data_ptr() as a dense [n, T, ...] block: a strided view is made dense
+                v = v if want is None or v.dtype == want or k == "obs" else v.to(want)
+                out[k] = v.contiguous()
                 continue
             a = v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
             if k == "obs" and a.dtype != np.int8:

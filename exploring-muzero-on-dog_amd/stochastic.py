@@ -3,7 +3,8 @@
 * ``DeviceClassicNet`` packs a flat parameter dict (Flax paths, see oracle/classic_nets.py) into the
   ``muz_classic_net_w`` table and fills the FiLM tables (``muz_classic_net_prepare``);
 * ``root_inference_fn`` (453-462), ``decision_recurrent_fn`` (414-432), ``chance_recurrent_fn`` (434-451);
-* ``run_stochastic_muzero_mcts`` (464-517): ``mctx.stochastic_muzero_policy`` as one HIP launch.
+* ``run_stochastic_muzero_mcts`` (464-517, reference signature) / ``stochastic_muzero_mcts`` (device-native):
+  ``mctx.stochastic_muzero_policy`` as one HIP launch.
 """
 from __future__ import annotations
 
@@ -188,9 +189,48 @@ def stochastic_muzero_policy(net: DeviceClassicNet, root_logits, root_value, roo
     return action, weights, value
 
 
-def run_stochastic_muzero_mcts(net: DeviceClassicNet, observations, legal_bits, num_simulations, max_depth,
-                               temperature, seed=0, turn=0, **kw):
-    """run_stochastic_muzero_mcts (464-517): root inference + search."""
+def stochastic_muzero_mcts(net: DeviceClassicNet, observations, legal_bits, num_simulations, max_depth,
+                           temperature, seed=0, turn=0, **kw):
+    """Device-native form of run_stochastic_muzero_mcts: DeviceClassicNet, device observations, 4-bit legal
+    mask per game; root inference + search.  Returns (action, action_weights, clipped root value)."""
     logits, value, emb = root_inference_fn(net, observations)
     return stochastic_muzero_policy(net, logits, value, emb, legal_bits, num_simulations, max_depth, temperature,
                                     seed=seed, turn=turn, **kw)
+
+
+_NET_CACHE: dict = {}
+
+
+def as_device_classic_net(params, obs_channels: int | None = None, device="cuda") -> DeviceClassicNet:
+    """The reference's classic ``params`` (init_muzero_params' nested Flax tree, muzero_classic_madn.py, or a
+    flat dict, or a DeviceClassicNet) -> DeviceClassicNet, packed once per params object."""
+    if isinstance(params, DeviceClassicNet):
+        return params
+    hit = _NET_CACHE.get(id(params))
+    if hit is not None and hit[0] is params and str(hit[1].buffer.device) == str(torch.device(device)):
+        return hit[1]
+    from . import checkpoint as CK
+    flat = params if all(isinstance(k, str) and "/" in k for k in params) else CK.muzero_tree_to_flat(params)
+    flat = {k: np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v, np.float32) for k, v in flat.items()}
+    C = int(flat["representation/Dense_1/kernel"].shape[0]) + 6 if obs_channels is None else int(obs_channels)
+    net = DeviceClassicNet(flat, C, device=device)
+    _NET_CACHE.clear()
+    _NET_CACHE[id(params)] = (params, net)
+    return net
+
+
+def run_stochastic_muzero_mcts(params, rng_key, observations, invalid_actions, num_simulations, max_depth,
+                               temperature):
+    """run_stochastic_muzero_mcts (MuZero_Classic_MADN/muzero_classic_madn.py:464-517), reference signature:
+    Flax params dict, int / uint32[2] key (the engine's Dirichlet / Gumbel streams, nets.rng_key_to_seed),
+    observations [B, 2P + 3, 56], invalid_actions bool [B, 4].  Returns (PolicyOutput(action,
+    action_weights), root_value = node_values[0] clipped to [-1, 1]) as cuda tensors."""
+    from .mcts import PolicyOutput, invalid_to_bits
+    from .nets import rng_key_to_seed
+    dev = torch.device("cuda")
+    net = as_device_classic_net(params, device=dev)
+    obs = observations if isinstance(observations, torch.Tensor) else torch.from_numpy(np.asarray(observations))
+    bits = invalid_to_bits(invalid_actions).to(dev)
+    a, w, v = stochastic_muzero_mcts(net, obs.to(device=dev, dtype=torch.float32), bits, num_simulations, max_depth,
+                                     temperature, seed=rng_key_to_seed(rng_key))
+    return PolicyOutput(a, w), v

@@ -77,6 +77,35 @@ def masked_argmax(x, invalid):
     return np.argmax(x, -1).astype(np.int32)
 
 
+# Near-tie instrumentation for the parity tests (not part of mctx).  Two fp32 implementations of the same
+# tree arithmetic that sum in different orders agree on every value in [-1, 1] to a few ulps; the Q-value
+# rescale (q - lo) / (hi - lo) multiplies that by the gain K = visit_scale * value_scale / (hi - lo), which
+# is large when the children's values are nearly equal (and 0 when they are exactly equal: the rescale then
+# maps every entry to 0 on both sides).  A decision whose top-2 gap is below
+# TIE_REL * max(1, |top|) + DQ * K could legitimately go either way; margin = gap / that bound (<= 1: tie).
+TIE_REL = 1e-5
+DQ = 4.8e-7            # 4 fp32 ulps at 1
+
+
+def top2_margin(x, gain=0.0):
+    """Top-2 gap of each row's argmax decision over its uncertainty bound (see above); inf when only one
+    entry is finite."""
+    x = np.asarray(x, np.float64)
+    srt = np.sort(np.where(np.isfinite(x), x, -np.inf), -1)
+    with np.errstate(invalid="ignore"):
+        bound = TIE_REL * np.maximum(1.0, np.abs(srt[:, -1])) + DQ * np.asarray(gain, np.float64)
+        m = (srt[:, -1] - srt[:, -2]) / bound
+    return np.where(np.isfinite(m), m, np.inf)
+
+
+def _note(trace, mask, x, gain=0.0):
+    """Fold the decision margins of the rows in `mask` into trace['margin'] (per game minimum)."""
+    if trace is None:
+        return
+    m = top2_margin(x, gain)
+    trace["margin"] = np.where(mask, np.minimum(trace["margin"], m), trace["margin"])
+
+
 class Tree:
     def __init__(self, B, S, A, E):
         N = S + 1
@@ -111,7 +140,7 @@ def update_tree_node(t: Tree, node, prior_logits, value, embedding):
 
 # ---------------------------------------------------------------- qtransforms.py
 def qtransform_completed_by_mix_value(t: Tree, node, value_scale=0.5, maxvisit_init=50.0, rescale_values=True,
-                                      use_mixed_value=True, epsilon=1e-8):
+                                      use_mixed_value=True, epsilon=1e-8, with_gain=False):
     b = np.arange(t.B)
     q = t.qvalues(node)
     visits = t.children_visits[b, node]
@@ -128,41 +157,53 @@ def qtransform_completed_by_mix_value(t: Tree, node, value_scale=0.5, maxvisit_i
     else:
         value = raw
     cq = np.where(visits > 0, q, value[:, None]).astype(F32)
+    span = np.ones(t.B, F32)
     if rescale_values:
         lo = cq.min(-1, keepdims=True)
         hi = cq.max(-1, keepdims=True)
+        span = np.maximum(hi - lo, F32(epsilon))[:, 0]
         cq = ((cq - lo) / np.maximum(hi - lo, F32(epsilon))).astype(F32)
     maxvisit = visits.max(-1)
     visit_scale = (F32(maxvisit_init) + maxvisit.astype(F32)).astype(F32)
-    return (visit_scale[:, None] * F32(value_scale) * cq).astype(F32)
+    out = (visit_scale[:, None] * F32(value_scale) * cq).astype(F32)
+    if with_gain:      # d out / d q: how much the rescale amplifies rounding in q (near-tie instrumentation);
+        # an exactly flat row (hi == lo: every entry the same completed value) carries no amplified difference
+        flat = (cq.max(-1) == cq.min(-1)) if not rescale_values else (span <= F32(epsilon)) & (hi == lo)[:, 0]
+        return out, np.where(flat, 0.0, visit_scale.astype(np.float64) * value_scale / span)
+    return out
 
 
 # ---------------------------------------------------------------- action_selection.py
-def root_action_selection(t: Tree, node, root_invalid, gumbel, table, max_num_considered=16):
+def root_action_selection(t: Tree, node, root_invalid, gumbel, table, max_num_considered=16, trace=None,
+                          active=None):
     b = np.arange(t.B)
     visits = t.children_visits[b, node]
     prior = t.children_prior_logits[b, node]
-    cq = qtransform_completed_by_mix_value(t, node)
+    cq, gain = qtransform_completed_by_mix_value(t, node, with_gain=True)
     num_valid = (1 - root_invalid.astype(np.int32)).sum(-1)
     num_considered = np.minimum(max_num_considered, num_valid)
     sim_index = visits.sum(-1)
     considered_visit = table[num_considered, sim_index]
     score = score_considered(considered_visit[:, None], gumbel, prior, cq, visits)
+    if active is not None:
+        _note(trace, active, np.where(root_invalid, -np.inf, score), gain)
     return masked_argmax(score, root_invalid)
 
 
-def interior_action_selection(t: Tree, node):
+def interior_action_selection(t: Tree, node, trace=None, active=None):
     b = np.arange(t.B)
     visits = t.children_visits[b, node]
     prior = t.children_prior_logits[b, node]
-    cq = qtransform_completed_by_mix_value(t, node)
+    cq, gain = qtransform_completed_by_mix_value(t, node, with_gain=True)
     probs = softmax(prior + cq)
     to_argmax = probs - visits.astype(F32) / (1 + visits.sum(-1, keepdims=True)).astype(F32)
+    if active is not None:
+        _note(trace, active, to_argmax, gain)
     return np.argmax(to_argmax, -1).astype(np.int32)
 
 
 # ---------------------------------------------------------------- search.py
-def simulate(t: Tree, root_invalid, gumbel, table, max_depth):
+def simulate(t: Tree, root_invalid, gumbel, table, max_depth, trace=None):
     B = t.B
     b = np.arange(B)
     node_index = np.full(B, NO_PARENT, np.int32)
@@ -172,8 +213,9 @@ def simulate(t: Tree, root_invalid, gumbel, table, max_depth):
     cont = np.ones(B, bool)
     while cont.any():
         ni = np.where(cont, next_node, node_index)
-        root_a = root_action_selection(t, ni, root_invalid, gumbel, table)
-        int_a = interior_action_selection(t, ni)
+        root_a = root_action_selection(t, ni, root_invalid, gumbel, table, trace=trace,
+                                       active=cont & (depth == 0))
+        int_a = interior_action_selection(t, ni, trace=trace, active=cont & (depth != 0))
         a = np.where(depth == 0, root_a, int_a)
         nn = t.children_index[b, ni, a]
         d = depth + 1
@@ -224,10 +266,14 @@ def backward(t: Tree, leaf):
 
 
 def gumbel_muzero_policy(params, root_logits, root_value, root_embedding, recurrent_fn, num_simulations,
-                         invalid_actions, gumbel, max_depth=None, max_num_considered_actions=16):
+                         invalid_actions, gumbel, max_depth=None, max_num_considered_actions=16, trace=None):
     """mctx.gumbel_muzero_policy with explicit (already gumbel_scale-scaled) Gumbel noise.
 
-    Returns (action [B], action_weights [B, A], root_value [B] = summary().value, tree)."""
+    Returns (action [B], action_weights [B, A], root_value [B] = summary().value, tree).  With a dict `trace`,
+    trace['margin'][b] is the smallest normalised top-2 gap (top2_margin) of every argmax decision game b's
+    search took (root and interior selections of every simulation, and the final action), and
+    trace['gain'][b] the Q-rescale gain of the final action weights: a game whose margin is > 1 cannot
+    legitimately choose differently under another fp32 summation order."""
     B, A = root_logits.shape
     E = root_embedding.shape[-1]
     S = num_simulations
@@ -238,9 +284,11 @@ def gumbel_muzero_policy(params, root_logits, root_value, root_embedding, recurr
     gumbel = np.asarray(gumbel, F32)
     table = get_table_of_considered_visits(max_num_considered_actions, S)
     t = Tree(B, S, A, E)
+    if trace is not None:
+        trace["margin"] = np.full(B, np.inf)
     update_tree_node(t, np.zeros(B, np.int32), logits, root_value.astype(F32), root_embedding.astype(F32))
     for sim in range(S):
-        parent, action = simulate(t, invalid, gumbel, table, max_depth)
+        parent, action = simulate(t, invalid, gumbel, table, max_depth, trace)
         nn = t.children_index[np.arange(B), parent, action]
         nn = np.where(nn == UNVISITED, sim + 1, nn).astype(np.int32)
         expand(params, t, recurrent_fn, parent, action, nn)
@@ -248,8 +296,11 @@ def gumbel_muzero_policy(params, root_logits, root_value, root_embedding, recurr
     root = np.zeros(B, np.int32)
     visits = t.children_visits[:, 0].astype(F32)
     considered_visit = visits.max(-1, keepdims=True)
-    cq = qtransform_completed_by_mix_value(t, root)
+    cq, gain = qtransform_completed_by_mix_value(t, root, with_gain=True)
     to_argmax = score_considered(considered_visit, gumbel, logits, cq, visits)
+    _note(trace, np.ones(B, bool), np.where(invalid, -np.inf, to_argmax), gain)
+    if trace is not None:
+        trace["gain"] = gain    # the action weights softmax(logits + cq) inherit q's rounding times this
     action = masked_argmax(to_argmax, invalid)
     weights = softmax(mask_invalid_actions((logits + cq).astype(F32), invalid))
     return action, weights, t.node_values[:, 0].copy(), t

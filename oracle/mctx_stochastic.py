@@ -72,7 +72,7 @@ class _Tree:
         self.info[n] = info
 
 
-def qtransform_by_parent_and_siblings(t: _Tree, n, eps=1e-8):
+def qtransform_by_parent_and_siblings(t: _Tree, n, eps=1e-8, with_gain=False):
     q = t.qvalues(n)
     vis = t.c_visits[n]
     nv = t.value[n]
@@ -80,35 +80,51 @@ def qtransform_by_parent_and_siblings(t: _Tree, n, eps=1e-8):
     lo = min(nv, safe.min())
     hi = max(nv, safe.max())
     comp = np.where(vis > 0, q, lo)
-    return ((comp - lo) / max(F32(hi - lo), F32(eps))).astype(F32)
+    out = ((comp - lo) / max(F32(hi - lo), F32(eps))).astype(F32)
+    if with_gain:       # d out / d q (near-tie instrumentation, see mctx_gumbel.top2_margin)
+        return out, (0.0 if hi == lo else 1.0 / float(max(F32(hi - lo), F32(eps))))
+    return out
 
 
-def decision_select(t: _Tree, n, depth, root_invalid, tb):
+def _margin(x, gain=0.0):
+    """Normalised top-2 gap of one argmax decision (see mctx_gumbel.top2_margin); test instrumentation."""
+    from oracle.mctx_gumbel import top2_margin
+    return float(top2_margin(np.asarray(x)[None], gain)[0])
+
+
+def decision_select(t: _Tree, n, depth, root_invalid, tb, margins=None):
     """muzero_action_selection (action_selection.py) with the root mask at depth 0."""
     vc = t.c_visits[n]
     nvis = t.visits[n]
     pb_c = F32(1.25) + F32(np.log(F32((F32(nvis) + F32(19652.0) + F32(1.0)) / F32(19652.0))))
     probs = _softmax(t.c_prior[n])
     policy = (F32(np.sqrt(F32(nvis))) * pb_c * probs / (vc + 1).astype(F32)).astype(F32)
-    score = (qtransform_by_parent_and_siblings(t, n) + policy + F32(1e-7) * tb).astype(F32)
+    cq, gain = qtransform_by_parent_and_siblings(t, n, with_gain=True)
+    score = (cq + policy + F32(1e-7) * tb).astype(F32)
     if depth == 0:
         score = np.where(root_invalid, -np.inf, score)
+    if margins is not None:
+        margins.append(_margin(score, gain))
     return int(np.argmax(score))
 
 
-def chance_select(t: _Tree, n, A):
+def chance_select(t: _Tree, n, A, margins=None):
     p = _softmax(t.c_prior[n, A:])
-    return int(np.argmax(p / (t.c_visits[n, A:] + 1).astype(F32))) + A
+    x = p / (t.c_visits[n, A:] + 1).astype(F32)
+    if margins is not None:
+        margins.append(_margin(x))
+    return int(np.argmax(x)) + A
 
 
 def stochastic_muzero_policy(params, root_logits, root_value, root_emb, decision_fn, chance_fn, num_simulations,
                              invalid, dirichlet, gumbel, max_depth=None, temperature=1.0, seed=0, turn=0, gids=None,
-                             num_chance=6, dirichlet_fraction=0.25):
+                             num_chance=6, dirichlet_fraction=0.25, trace=None):
     """Batched over B games (per-game trees, batched network calls).
 
     decision_fn(params, action[b], emb[b,256]) -> (chance_logits, afterstate_value, afterstate, reward, discount)
     chance_fn(params, chance[b], afterstate[b,256]) -> (action_logits, value, next_state)
-    Returns (action [B], action_weights [B, A], root_value_clipped [B], trees)."""
+    Returns (action [B], action_weights [B, A], root_value_clipped [B], trees).  With a dict `trace`,
+    trace['margin'][b] is the smallest relative top-2 gap of every argmax decision of game b's search."""
     B, A = root_logits.shape
     C = num_chance
     Ap = A + C
@@ -125,6 +141,7 @@ def stochastic_muzero_policy(params, root_logits, root_value, root_emb, decision
     root_prior = np.concatenate([logits, np.full((B, C), -np.inf, F32)], -1)
     root_invalid = np.concatenate([invalid.astype(bool), np.ones((B, C), bool)], -1)
     trees = [_Tree(S + 1, Ap, L) for _ in range(B)]
+    margins = [[] if trace is not None else None for _ in range(B)]
     for b, t in enumerate(trees):
         t.update_node(0, root_prior[b], F32(root_value[b]), True, root_emb[b], (0.0, 0.0))
     for sim in range(S):
@@ -134,9 +151,9 @@ def stochastic_muzero_policy(params, root_logits, root_value, root_emb, decision
             while True:
                 if t.is_dec[node]:
                     tb = np.array([tiebreak_uniform(seed, int(gids[b]), turn, sim, depth, a) for a in range(Ap)], F32)
-                    a = decision_select(t, node, depth, root_invalid[b], tb)
+                    a = decision_select(t, node, depth, root_invalid[b], tb, margins[b])
                 else:
-                    a = chance_select(t, node, A)
+                    a = chance_select(t, node, A, margins[b])
                 nxt = t.c_index[node, a]
                 depth += 1
                 if nxt == -1 or depth >= D:
@@ -190,6 +207,10 @@ def stochastic_muzero_policy(params, root_logits, root_value, root_emb, decision
         with np.errstate(divide="ignore"):
             lw = np.log(w).astype(F32)
         lw = ((lw - lw.max()) / max(TINY, F32(temperature))).astype(F32)
+        if margins[b] is not None:
+            margins[b].append(_margin(lw + gumbel[b].astype(F32)))
         action[b] = int(np.argmax(lw + gumbel[b].astype(F32)))
         rv[b] = np.clip(t.value[0], -1.0, 1.0)
+    if trace is not None:
+        trace["margin"] = np.array([min(m) if m else np.inf for m in margins])
     return action, weights, rv, trees

@@ -48,6 +48,10 @@ def play_batch_of_games(params, root_fn, recurrent_fn, envs, num_simulations, ma
         "pol": np.zeros((n, T, 24), np.float32), "mask": np.zeros((n, T), np.float32),
         "player": np.zeros((n, T), np.int32), "team": np.full((n, T), -1, np.int32),
         "discount": np.zeros((n, T), np.int32), "idx": np.zeros(n, np.int32),
+        # test instrumentation: smallest relative top-2 gap of any argmax decision of the turn's search
+        # (inf on no-move turns), see mctx_gumbel.top2_margin
+        "margin": np.full((n, T), np.inf),
+        "gain": np.zeros((n, T)),          # Q-rescale gain of the turn's action weights (test instrumentation)
     }
     dones = np.zeros(n, bool)
     step = 0
@@ -63,11 +67,14 @@ def play_batch_of_games(params, root_fn, recurrent_fn, envs, num_simulations, ma
             invalid = np.stack([~va for _, va in search])
             gum = np.stack([gumbel_noise(seed, i, step, scale=temp) for i, _ in search])
             lg, v, e = root_fn(params, obs)
+            trace = {}
             act, w, rv, _ = G.gumbel_muzero_policy(params, lg, v, e, recurrent_fn, num_simulations, invalid, gum,
-                                                   max_depth=max_depth)
+                                                   max_depth=max_depth, trace=trace)
             for k, (i, _) in enumerate(search):
                 env = envs[i]
                 t = buf["idx"][i]
+                buf["margin"][i, t] = trace["margin"][k]
+                buf["gain"][i, t] = trace["gain"][k]
                 cpb = env.current_player
                 teamb = cpb % 2 if teams else -1
                 nxt, r, nd = dm.env_step(env, dm.map_action(int(act[k])))
@@ -130,6 +137,7 @@ def play_batch_of_games_stochastic(params, root_fn, decision_fn, chance_fn, envs
         "dice": np.zeros((n, T), np.int32), "dice_dist": np.zeros((n, T, 6), np.float32),
         "player": np.zeros((n, T), np.int32), "team": np.full((n, T), -1, np.int32),
         "discount": np.zeros((n, T), np.int32), "idx": np.zeros(n, np.int32),
+        "margin": np.full((n, T), np.inf),   # test instrumentation, as in play_batch_of_games
     }
     dones = np.zeros(n, bool)
     step = 0
@@ -147,13 +155,15 @@ def play_batch_of_games_stochastic(params, root_fn, decision_fn, chance_fn, envs
             gids = np.array([i for i, _ in search])
             gum = np.stack([gumbel_noise(seed ^ GUMBEL_STREAM, int(i), step, A=4) for i in gids])
             lg, v, e = root_fn(params, obs)
+            trace = {}
             act, w, rv, _ = MS.stochastic_muzero_policy(params, lg, v, e, decision_fn, chance_fn, num_simulations,
                                                         invalid, np.zeros((len(search), 4), np.float32), gum,
                                                         max_depth=max_depth, temperature=temp, seed=seed, turn=step,
-                                                        gids=gids, dirichlet_fraction=0.0)
+                                                        gids=gids, dirichlet_fraction=0.0, trace=trace)
             for k, (i, _) in enumerate(search):
                 env = envs[i]
                 t = buf["idx"][i]
+                buf["margin"][i, t] = trace["margin"][k]
                 cpb = env.current_player
                 teamb = cpb % 2 if teams else -1
                 nxt, r, nd = cm.env_step(env, int(act[k]))

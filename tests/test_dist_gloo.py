@@ -19,8 +19,9 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
-    res = bench.reduce_results(dist, torch.device("cpu"), steps_done=100 * (rank + 1), searches=10 * (rank + 1),
-                               elapsed=1.0 + rank, search_ms=5.0, launches=3)
+    sums, elapsed = bench.sum_max(dist, torch.device("cpu"), [100 * (rank + 1), 10 * (rank + 1), 5.0, 3],
+                                  elapsed=1.0 + rank)
+    res = (sums[0], sums[1], elapsed, sums[2], sums[3])
     q.put((rank, res))
     dist.destroy_process_group()
 

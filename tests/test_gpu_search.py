@@ -12,6 +12,7 @@ import torch
 from oracle import detmadn as dm
 from oracle import mctx_gumbel as G
 from oracle import nets as ON
+from tests._parity import search_parity
 from tests.test_gpu_nets import random_obs
 
 pytestmark = pytest.mark.gpu
@@ -53,16 +54,12 @@ def test_search_logic_matches_mctx_restatement(cuda, P, S, D, rule_set):
     gum = np.random.default_rng(3).gumbel(size=(B, 24)).astype(np.float32)
     pol, rv = M.gumbel_muzero_policy(net, lg, v, e, torch.from_numpy(bits), S, D, 1.0,
                                      gumbel=torch.from_numpy(gum))
+    trace = {}
     a, w, orv, tree = G.gumbel_muzero_policy(params, lg.cpu().numpy(), v.cpu().numpy(), e.cpu().numpy(),
-                                             gpu_recurrent_fn(N, net), S, ~valid, gum, max_depth=D)
+                                             gpu_recurrent_fn(N, net), S, ~valid, gum, max_depth=D, trace=trace)
     torch.cuda.synchronize()
     ga, gw, grv = pol.action.cpu().numpy(), pol.action_weights.cpu().numpy(), rv.cpu().numpy()
-    agree = (ga == a).mean()
-    print(f"P{P} S{S} D{D}: action agreement {agree:.3f}, |dw| {np.abs(gw - w).max():.2e}, |dv| {np.abs(grv - orv).max():.2e}")
-    assert agree >= 0.97
-    same = ga == a
-    assert np.abs(gw - w)[same].max() < 1e-4
-    assert np.abs(grv - orv)[same].max() < 1e-4
+    search_parity(f"search logic P{P} S{S} D{D}", ga, gw, grv, a, w, orv, trace["margin"], trace["gain"])
     assert valid[np.arange(B), ga].all(), "search picked an invalid root action"
 
 
@@ -70,22 +67,24 @@ def test_search_end_to_end_vs_numpy_networks(cuda):
     N, M, params, net, obs, valid, bits = setup(2, 32, 9, "selfplay_2p")
     B = obs.shape[0]
     gum = np.random.default_rng(4).gumbel(size=(B, 24)).astype(np.float32)
-    pol, rv = M.run_muzero_mcts(net, torch.from_numpy(obs).cuda(), torch.from_numpy(bits), 50, 25, 1.0,
+    pol, rv = M.muzero_mcts(net, torch.from_numpy(obs).cuda(), torch.from_numpy(bits), 50, 25, 1.0,
                                 gumbel=torch.from_numpy(gum))
     lg, v, e = ON.root_inference(params, obs)
-    a, w, orv, _ = G.gumbel_muzero_policy(params, lg, v, e, ON.recurrent_inference, 50, ~valid, gum, max_depth=25)
+    trace = {}
+    a, w, orv, _ = G.gumbel_muzero_policy(params, lg, v, e, ON.recurrent_inference, 50, ~valid, gum, max_depth=25,
+                                          trace=trace)
     torch.cuda.synchronize()
-    ga = pol.action.cpu().numpy()
-    agree = (ga == a).mean()
-    print(f"end-to-end: action agreement {agree:.3f}")
-    assert agree >= 0.9
+    # the NumPy networks sum in another order (|d logits|, |d values| ~3e-6 = ~6 DQ, tests/test_gpu_nets.py):
+    # decisions count as near-ties within 50x the tree-arithmetic bound, weights get 10x its gain term
+    search_parity("search end-to-end (NumPy nets)", pol.action.cpu().numpy(), pol.action_weights.cpu().numpy(),
+                  rv.cpu().numpy(), a, w, orv, trace["margin"], 10 * trace["gain"], tol=1e-4, tie=50.0)
 
 
 def test_device_noise_is_deterministic_and_valid(cuda):
     N, M, params, net, obs, valid, bits = setup(2, 40, 5, "selfplay_2p")
     t = torch.from_numpy(obs).cuda()
-    p1, v1 = M.run_muzero_mcts(net, t, torch.from_numpy(bits), 16, 8, 1.0, seed=123, turn=7)
-    p2, v2 = M.run_muzero_mcts(net, t, torch.from_numpy(bits), 16, 8, 1.0, seed=123, turn=7)
+    p1, v1 = M.muzero_mcts(net, t, torch.from_numpy(bits), 16, 8, 1.0, seed=123, turn=7)
+    p2, v2 = M.muzero_mcts(net, t, torch.from_numpy(bits), 16, 8, 1.0, seed=123, turn=7)
     assert torch.equal(p1.action, p2.action) and torch.equal(v1, v2)
     ga = p1.action.cpu().numpy()
     assert valid[np.arange(len(ga)), ga].all()
