@@ -5,9 +5,6 @@
 
 namespace muz {
 
-#ifndef MUZ_DOG_INCR
-#define MUZ_DOG_INCR 1
-#endif
 constexpr int kDogGamesPerBlock = 4;   // wave-per-game kernels (reset, explicit-action step)
 #ifndef MUZ_DOG_WPE
 #define MUZ_DOG_WPE 8      // waves per SIMD the play kernel is budgeted for: 4 blocks of 7 waves per CU (measured best)
@@ -174,7 +171,7 @@ __device__ void dog_capture_move(const DetConsts& c, DogG& s, int cp, int pin, i
         if (s.pins[at * 4 + k] == npos) s.pins[at * 4 + k] = -1;
     const int cur = s.pins[cp * 4 + pin];
     s.pins[cp * 4 + pin] = (int8_t)npos;
-    if (MUZ_DOG_INCR && legal && npos >= 0 && npos < kCells) {
+    if (legal && npos >= 0 && npos < kCells) {   // incremental board update (a validated move)
       if (cur >= 0 && cur < kCells) s.board[cur] = -1;
       s.board[npos] = (int8_t)cp;
     } else {

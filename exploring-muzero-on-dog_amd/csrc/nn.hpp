@@ -119,52 +119,24 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // acc[t] += A[16 rows][K] @ Wgroup[K][NT*16]  (KB = K/16 k-blocks; Wg = packed weights of this group).
 // b0 / b1 hold k-blocks 0 and 1 on entry.  Weights for k-blocks kb+1 and kb+2 are in flight while kb is
 // multiplied (3-deep register ring, written as a 3-way unrolled loop so every index is static).
-// Tree traffic (node embeddings, children arrays) is streamed with non-temporal hints so the weights
-// (3.8 MB, read by every simulation of every tile) keep the 4 MB L2 of each XCD (tuning knob).
-#ifndef MUZ_TREE_NT
-#define MUZ_TREE_NT 0   // measured: no gain on MI355X (the weights stay resident either way)
-#endif
+// Tree traffic (node embeddings, children arrays): plain loads / stores.  Non-temporal hints (to keep the
+// 3.8 MB of weights in each XCD's 4 MB L2) measured no gain on MI355X: the weights stay resident anyway.
 template <class P, class V>
 __device__ __forceinline__ void tree_st(P* p, V v) {
-  if constexpr (MUZ_TREE_NT) __builtin_nontemporal_store(v, p); else *p = v;
+  *p = v;
 }
 template <class P>
 __device__ __forceinline__ P tree_ld(const P* p) {
-  if constexpr (MUZ_TREE_NT) return __builtin_nontemporal_load(p); else return *p;
+  return *p;
 }
 
-#ifndef MUZ_EPI_LN
-#define MUZ_EPI_LN 0       // 1: LayerNorm statistics in the dense epilogue (dense16_ln); measured 2.7 % slower
-#endif
 #ifndef MUZ_RING_DEPTH
 #define MUZ_RING_DEPTH 2   // k-blocks of weights in flight ahead of the one being multiplied (2 or 3)
 #endif
-#ifndef MUZ_A_PRELOAD
-#define MUZ_A_PRELOAD 1    // read the A fragment of k-block kb+1 from LDS before kb's MFMAs
-#endif
-#ifndef MUZ_DLN
-#define MUZ_DLN 0          // deferred LayerNorm (dense16_dp / dense16_la): 1 ResBlock LayerNorm_0, 2 + Dyn4 LayerNorm_1,
-                           // 3 + Pred4 head LayerNorms.  Measured on MI355X (B=4096 S=50 search): 1 -> +5 %,
-                           // 2 -> +6 %, 3 -> +8 % time: normalising every A fragment in all 8 waves costs more
-                           // than the row pass and barrier it saves
-#endif
-#ifndef MUZ_DLN_PK
-#define MUZ_DLN_PK 0       // deferred LayerNorm applied with packed fp32 math
-#endif
 
-// Deferred LayerNorm + ReLU of the A operand (see dense16_dp): A[r][k] <- relu((A - mean_r) * (inv_r *
-// sc[k]) + sh[k]) as the fragments are read, with the row statistics of this lane's row and the
-// LayerNorm parameters staged in LDS by the producing layer.  Same arithmetic as ln16<.., LN_RELU>.
-struct LnA {
-  float mean, inv;
-  const float* sc;   // LDS, indexed by k
-  const float* sh;
-};
-
-template <int NT, bool AG, bool LNA = false>
+template <int NT, bool AG>
 __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int KB, const float* A, int lda,
-                                               f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT],
-                                               const LnA& ln = LnA{}) {
+                                               f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT]) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(Wg)) + lane * NT;
@@ -174,46 +146,9 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
     if constexpr (AG) return *gp(reinterpret_cast<const f32x4*>(ap + kb * 16));
     else return *reinterpret_cast<const f32x4*>(ap + kb * 16);
   };
-  // LNA: the raw fragment and its LayerNorm parameters are read one step ahead (with the A preload) and
-  // normalised after the step's MFMAs are issued, so the VALU work co-issues with the other wave's MFMAs
-  struct ARaw {
-    f32x4 x, s, h;
-  };
-  const float* scp = ln.sc + 4 * g;
-  const float* shp = ln.sh + 4 * g;
-  auto ldr = [&](int kb) -> ARaw {
-    ARaw v;
-    v.x = lda4(kb);
-    v.s = *reinterpret_cast<const f32x4*>(scp + kb * 16);
-    v.h = *reinterpret_cast<const f32x4*>(shp + kb * 16);
-    return v;
-  };
-  auto fin = [&](const ARaw& v) -> f32x4 {
-    f32x4 y;
-#if MUZ_DLN_PK
-    // packed fp32 (v_pk_add / v_pk_mul / v_pk_fma): half the VALU issue slots next to the MFMAs
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    const f32x2 m2 = {ln.mean, ln.mean}, i2 = {ln.inv, ln.inv};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x2 x2 = {v.x[2 * h], v.x[2 * h + 1]}, s2 = {v.s[2 * h], v.s[2 * h + 1]},
-                  h2 = {v.h[2 * h], v.h[2 * h + 1]};
-      const f32x2 r2 = (x2 - m2) * (i2 * s2) + h2;
-      y[2 * h] = fmaxf(r2[0], 0.f);
-      y[2 * h + 1] = fmaxf(r2[1], 0.f);
-    }
-#else
-#pragma unroll
-    for (int q = 0; q < 4; ++q) y[q] = fmaxf((v.x[q] - ln.mean) * (ln.inv * v.s[q]) + v.h[q], 0.f);
-#endif
-    return y;
-  };
   constexpr int D = MUZ_RING_DEPTH;
-  f32x4 a0, a1;
-  if constexpr (LNA) a0 = fin(ldr(0));
-  else a0 = lda4(0);
-  a1 = a0;
-  // step kb: issue k-block kb+D into `nxt` (the buffer consumed at step kb-1), read A of kb+1,
+  f32x4 a0 = lda4(0), a1 = a0;
+  // step kb: issue k-block kb+D into `nxt` (the buffer consumed at step kb-1), read A of kb+1 from LDS,
   // multiply `cur` (= kb) with A of kb
   auto step = [&](int kb, const f32x4 (&cur)[NT], f32x4 (&nxt)[NT], const f32x4& acur, f32x4& anxt) {
 #ifndef MUZ_EXPT_NOLOAD   // timing experiment only (wrong results): no weight stream inside the loop
@@ -225,24 +160,8 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
     // Pin the issue point: without this the machine scheduler sinks each weight load next to its
     // first MFMA (one step of cover instead of D) once the loop is fully unrolled.
     __builtin_amdgcn_sched_barrier(0);
-    f32x4 a;
-    if constexpr (LNA) {
-      ARaw rn;
-      if (kb + 1 < KB) rn = ldr(kb + 1);
-      a = acur;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma4(cur[t][j], a[j], acc[t]);
-      if (kb + 1 < KB) anxt = fin(rn);
-      return;
-    }
-    if (MUZ_A_PRELOAD) {
-      if (kb + 1 < KB) anxt = lda4(kb + 1);
-      a = acur;
-    } else {
-      a = lda4(kb);
-    }
+    if (kb + 1 < KB) anxt = lda4(kb + 1);
+    const f32x4 a = acur;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -277,13 +196,10 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
   }
 }
 
-template <int NT, bool LNA = false>
+template <int NT>
 __device__ __forceinline__ void mfma_ring(const float* __restrict__ Wg, int KB, const float* A, int lda,
-                                          f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT], bool a_global,
-                                          const LnA& ln = LnA{}) {
-  if constexpr (LNA)
-    mfma_ring_impl<NT, false, true>(Wg, KB, A, lda, acc, b0, b1, ln);
-  else if (a_global)
+                                          f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT], bool a_global) {
+  if (a_global)
     mfma_ring_impl<NT, true>(Wg, KB, A, lda, acc, b0, b1);
   else
     mfma_ring_impl<NT, false>(Wg, KB, A, lda, acc, b0, b1);
@@ -329,77 +245,18 @@ __device__ __forceinline__ void pf_issue(Pf& pf, const AS4 muz_dense* L, int K, 
   }
 }
 
-// ---- deferred LayerNorm: statistics from the producer's epilogue, normalisation in the consumer ------
-// A LayerNorm + ReLU whose only reader is the next dense layer costs a row pass and a barrier when it
-// runs on its own (dense -> barrier -> ln16 -> barrier -> dense).  Deferred, the producer (dense16_dp)
-// stores its raw output together with per-(wave, row) partial sums of x and x^2 and the LayerNorm
-// parameters by column; after the one barrier the consumer (dense16_la with an LnA from dln_a) reduces
-// the partials of its row and normalises each A fragment as it reads it.  Two LDS buffers: a layer
-// that consumes buffer 0 can produce into buffer 1 while slower waves still read buffer 0.
-constexpr int kDlnCols = 384;
-struct Dln {
-  f32x4 part[kWaves][kRows];           // (sum, sum of squares) of column group 0 | group 1
-  float sc[kDlnCols], sh[kDlnCols];    // LayerNorm scale / bias by producer column
-};
-__device__ __forceinline__ Dln* dln_buf(int i) {
-  __shared__ Dln b[2];
-  return &b[i];
-}
-// producer waves that hold columns of an N-wide layer
-constexpr int nw_for(int N) { return (N + 16 * nt_for(N) - 1) / (16 * nt_for(N)); }
-
-// consumer side: mean / inverse deviation of this lane's MFMA row (lane & 15) over column group `grp`
-// (n columns) from the partials of the nw producer waves, and the parameters from producer column kcol0
-__device__ __forceinline__ LnA dln_a(const Dln* db, int grp, int kcol0, int n, int nw) {
-  const int r = threadIdx.x & 15;
-  f32x4 tot = db->part[0][r];
-  for (int w = 1; w < nw; ++w) tot += db->part[w][r];
-  const float s = grp ? tot[2] : tot[0];
-  const float s2 = grp ? tot[3] : tot[1];
-  const float mean = s / (float)n;
-  const float mean2 = s2 / (float)n;
-  const float var = fmaxf(0.f, mean2 - mean * mean);
-  LnA la;
-  la.mean = mean;
-  la.inv = 1.0f / sqrtf(var + 1e-6f);
-  la.sc = db->sc + kcol0;
-  la.sh = db->sh + kcol0;
-  return la;
-}
-
 // Dense layer over the tile: out[16][N] = A @ W + b, waves split N (NT tiles of 16 columns each).
 // `pf` holds this layer's first k-blocks on entry and the next layer's (Ln: K=Kn, N=Nn, NTN tiles)
 // on exit.  A may live in LDS or global memory.  Caller synchronises before/after.
-// LNA: A is the raw output of a dense16_dp producer and `la` its deferred LayerNorm + ReLU.
-// DP (dense16_dp): also publish the deferred LayerNorm of this layer's output into `db` -- columns
-// [0, split) use P0, [split, N) use P1.
-template <int NT, int NTN, bool LNA = false, bool DP = false>
-__device__ __forceinline__ void dense16_core(const AS4 muz_dense& L, int K, int N, const float* A, int lda,
-                                             float* out, int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
-                                             bool a_global, const LnA& la, Dln* db, const AS4 muz_ln* P0,
-                                             const AS4 muz_ln* P1, int split) {
+template <int NT, int NTN>
+__device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
+                                        int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
+                                        bool a_global = false) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int KB = (K + 15) >> 4;
   const int col0 = wv * NT * 16;
-  // DP: LayerNorm parameters of column threadIdx.x, loaded now and staged after the MFMA loop
-  float psc = 0.f, psh = 0.f;
-  const int pc = threadIdx.x;
-  if constexpr (DP) {
-    if (pc < N) {
-      const bool g1 = pc >= split;
-      const AS4 muz_ln* P = g1 ? P1 : P0;
-      psc = gp(P->scale)[g1 ? pc - split : pc];
-      psh = gp(P->bias)[g1 ? pc - split : pc];
-    }
-  }
   if (col0 >= N) {
     pf_issue<NTN>(pf, Ln, Kn, Nn);
-    if constexpr (DP) {
-      if (pc < N) {
-        db->sc[pc] = psc;
-        db->sh[pc] = psh;
-      }
-    }
     return;
   }
   const int r = lane & 15, g = lane >> 4;
@@ -414,71 +271,17 @@ __device__ __forceinline__ void dense16_core(const AS4 muz_dense& L, int K, int 
     b1[t] = pf.v1[t];
   }
   ST(ST_DENTRY);
-  mfma_ring<NT, LNA>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global, la);
+  mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global);
   ST(ST_MFMA);
   pf_issue<NTN>(pf, Ln, Kn, Nn);
   // The MFMA computes out^T (weights as the A operand), so lane (r, g) holds 4 CONSECUTIVE output
   // columns of row r: one 16-byte bias load and one ds_write_b128 per tile.
-  float st[4] = {0.f, 0.f, 0.f, 0.f};   // DP: sum, sum of squares of group 0, then group 1
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = col0 + t * 16 + 4 * g;
-    if (col < N) {
-      const f32x4 v = acc[t] + bb[t];
-      *reinterpret_cast<f32x4*>(out + r * ldo + col) = v;
-      if constexpr (DP) {
-        float s = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          s += v[q];
-          s2 += v[q] * v[q];
-        }
-        if (col >= split) {
-          st[2] += s;
-          st[3] += s2;
-        } else {
-          st[0] += s;
-          st[1] += s2;
-        }
-      }
-    }
-  }
-  if constexpr (DP) {
-    // the 4 lanes of row r: (g0 + g1) | (g2 + g3) over permlane16, then the two halves over permlane32
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const LoHi<float> p = swap16(st[c]);
-      const LoHi<float> p2 = swap32(p.lo + p.hi);
-      st[c] = p2.lo + p2.hi;
-    }
-    if (g == 0) db->part[wv][r] = f32x4{st[0], st[1], st[2], st[3]};
-    if (pc < N) {
-      db->sc[pc] = psc;
-      db->sh[pc] = psh;
-    }
+    if (col < N) *reinterpret_cast<f32x4*>(out + r * ldo + col) = acc[t] + bb[t];
   }
   ST(ST_EPI);
-}
-
-template <int NT, int NTN>
-__device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
-                                        int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
-                                        bool a_global = false) {
-  dense16_core<NT, NTN>(L, K, N, A, lda, out, ldo, pf, Ln, Kn, Nn, a_global, LnA{}, nullptr, nullptr, nullptr, 0);
-}
-// dense16 whose A is normalised on the fly (the deferred LayerNorm + ReLU `la` of the producing layer)
-template <int NT, int NTN>
-__device__ __forceinline__ void dense16_la(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
-                                           int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn, const LnA& la) {
-  dense16_core<NT, NTN, true>(L, K, N, A, lda, out, ldo, pf, Ln, Kn, Nn, false, la, nullptr, nullptr, nullptr, 0);
-}
-// dense16 producing a deferred LayerNorm (P0 on [0, split), P1 on [split, N)) into db; LNA as dense16_la
-template <int NT, int NTN, bool LNA = false>
-__device__ __forceinline__ void dense16_dp(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
-                                           int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn, Dln* db,
-                                           const AS4 muz_ln& P0, const AS4 muz_ln* P1 = nullptr,
-                                           int split = 1 << 30, const LnA& la = LnA{}) {
-  dense16_core<NT, NTN, LNA, true>(L, K, N, A, lda, out, ldo, pf, Ln, Kn, Nn, false, la, db, &P0, P1, split);
 }
 
 // ---- row-wise ops: thread t -> row t/32, lane-in-row t%32 (half a wave per row) ---------------------
@@ -697,15 +500,14 @@ __device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
 }
 
 // ---- LDS arena of a 16-row tile ---------------------------------------------------------------------
-// Row strides (floats).  MUZ_LD_PAD 8 (stride = 8 mod 64 dwords) makes the MFMA loops' A-fragment
-// ds_read_b128 (lane (r, g) -> row r, dword 4g) conflict-free in all four 16-lane groups; with 4 two
-// lanes of each group share a 4-bank slot.
-#ifndef MUZ_LD_PAD
-#define MUZ_LD_PAD 4
-#endif
-constexpr int LD = LAT + MUZ_LD_PAD;     // row stride of 256-wide buffers (keeps b128 reads 16B aligned)
-constexpr int LDW = 512 + MUZ_LD_PAD;    // wide buffer (FiLM scale|shift 512, pred heads 384, concat 320)
-constexpr int LDE = 64 + MUZ_LD_PAD;     // small buffer (action embed, global features)
+// Row strides (floats): +4 keeps every row 16-byte aligned and spreads the 16 rows over the banks.  With
+// it the MFMA loops' A-fragment ds_read_b128 (lane (r, g) -> row r, dword 4g) has two lanes of each 16-lane
+// group sharing a 4-bank slot (the SQ_LDS_BANK_CONFLICT cycles of the search kernel); a stride of 8 mod 64
+// removes them and measured within noise (LDS is not on the critical path), so +4 stays.
+constexpr int kLdPad = 4;
+constexpr int LD = LAT + kLdPad;     // row stride of 256-wide buffers
+constexpr int LDW = 512 + kLdPad;    // wide buffer (FiLM scale|shift 512, pred heads 384, concat 320)
+constexpr int LDE = 64 + kLdPad;     // small buffer (action embed, global features)
 constexpr int kArenaFloats = 4 * kRows * LD + kRows * LDW + kRows * LDE + 4 * kRows;
 
 struct Arena {
@@ -735,141 +537,11 @@ struct Arena {
   }
 };
 
-// ---- dense layer + LayerNorm in the epilogue ----------------------------------------------------------
-// out = f(LN(A @ W + b)) with the LayerNorm statistics reduced across the waves through a small LDS
-// exchange instead of a separate row pass: each lane sums its 4*NT columns per row, the 4 lanes of a row
-// (g = 0..3) combine over the permlane network, one lane per (wave, row) publishes (sum, sum of squares),
-// and after one barrier every lane reads its row's partials (waves in order) and normalises the values it
-// still holds in registers.  Columns [0, split) use LayerNorm P0, [split, N) P1 (two LayerNorms over one
-// concatenated dense, Pred4's [policy Dense_0 | value Dense_3]); split is a multiple of 16 so every
-// 16-column tile belongs to one group.  MODE: LN_RELU -> out = relu(y);  LN_RESID_RELU -> out = relu(out + y).
-// Flax fast variance (E[x^2] - E[x]^2), eps 1e-6; only the summation order differs from ln16.
-// Contains one barrier (every wave of the workgroup must call it); the caller synchronises after it.
-__device__ __forceinline__ float4* ln_partials() {
-  __shared__ float4 part[kWaves * kRows];   // (sum0, sumsq0, sum1, sumsq1) per (wave, row)
-  return part;
-}
-
-template <int NT, int NTN, int MODE>
-__device__ __forceinline__ void dense16_ln(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
-                                           int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
-                                           const AS4 muz_ln& P0, const AS4 muz_ln* P1 = nullptr, int split = 1 << 30) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int KB = (K + 15) >> 4;
-  const int col0 = wv * NT * 16;
-  const int r = lane & 15, g = lane >> 4;
-  const bool work = col0 < N;
-  f32x4 acc[NT], sc[NT], sh[NT];
-  float4* part = ln_partials();
-  if (work) {
-    const AS1 f32x4* bias4 = gp(reinterpret_cast<const f32x4*>(L.b));
-    const AS1 f32x4* s0 = gp(reinterpret_cast<const f32x4*>(P0.scale));
-    const AS1 f32x4* h0 = gp(reinterpret_cast<const f32x4*>(P0.bias));
-    f32x4 b0[NT], b1[NT], bb[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = col0 + t * 16 + 4 * g;
-      const bool in = col < N;
-      bb[t] = in ? bias4[col >> 2] : f32x4{0.f, 0.f, 0.f, 0.f};   // these land under the MFMA loop
-      if (col < split) {
-        sc[t] = in ? s0[col >> 2] : f32x4{0.f, 0.f, 0.f, 0.f};
-        sh[t] = in ? h0[col >> 2] : f32x4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        sc[t] = in ? gp(reinterpret_cast<const f32x4*>(P1->scale))[(col - split) >> 2] : f32x4{0.f, 0.f, 0.f, 0.f};
-        sh[t] = in ? gp(reinterpret_cast<const f32x4*>(P1->bias))[(col - split) >> 2] : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      b0[t] = pf.v0[t];
-      b1[t] = pf.v1[t];
-    }
-    ST(ST_DENTRY);
-    mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, false);
-    ST(ST_MFMA);
-    pf_issue<NTN>(pf, Ln, Kn, Nn);
-    float s[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = col0 + t * 16 + 4 * g;
-      acc[t] += bb[t];
-      if (col < N) {
-        const int grp = col >= split;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          s[grp] += acc[t][q];
-          s2[grp] += acc[t][q] * acc[t][q];
-        }
-      }
-    }
-    // the 4 lanes of row r: (g0 + g1) | (g2 + g3) over permlane16, then the two halves over permlane32
-    float4 v = {s[0], s2[0], s[1], s2[1]};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float x = c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
-      const LoHi<float> p = swap16(x);
-      x = p.lo + p.hi;
-      const LoHi<float> p2 = swap32(x);
-      x = p2.lo + p2.hi;
-      if (c == 0) v.x = x; else if (c == 1) v.y = x; else if (c == 2) v.z = x; else v.w = x;
-    }
-    if (g == 0) part[wv * kRows + r] = v;
-  } else {
-    pf_issue<NTN>(pf, Ln, Kn, Nn);
-  }
-  ST(ST_EPI);
-  SYNC();
-  if (!work) return;
-  const int nw = (N + NT * 16 - 1) / (NT * 16);   // waves holding columns
-  float4 tot = part[r];
-  for (int w = 1; w < nw; ++w) {
-    const float4 p = part[w * kRows + r];
-    tot.x += p.x;
-    tot.y += p.y;
-    tot.z += p.z;
-    tot.w += p.w;
-  }
-  const float n0 = (float)min(N, split), n1 = (float)(N - min(N, split));
-  const float m0 = tot.x / n0, m1 = n1 > 0.f ? tot.z / n1 : 0.f;
-  const float i0 = 1.0f / sqrtf(fmaxf(0.f, tot.y / n0 - m0 * m0) + 1e-6f);
-  const float i1 = n1 > 0.f ? 1.0f / sqrtf(fmaxf(0.f, tot.w / n1 - m1 * m1) + 1e-6f) : 0.f;
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int col = col0 + t * 16 + 4 * g;
-    if (col < N) {
-      const bool g1 = col >= split;
-      const float mean = g1 ? m1 : m0, inv = g1 ? i1 : i0;
-      f32x4 y;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) y[q] = (acc[t][q] - mean) * (inv * sc[t][q]) + sh[t][q];
-      f32x4* o = reinterpret_cast<f32x4*>(out + r * ldo + col);
-      if (MODE == LN_RESID_RELU) y = *o + y;
-      *o = f32x4{fmaxf(y[0], 0.f), fmaxf(y[1], 0.f), fmaxf(y[2], 0.f), fmaxf(y[3], 0.f)};
-    }
-  }
-  ST(ST_ROW);
-}
-
 // ResBlock (muzero_deterministic_madn.py:12-24): X <- relu(X + LN1(D1(relu(LN0(D0(X))))))
 // pf: rb.d0 on entry, (Ln: Kn x Nn, NTN tiles) on exit.
 template <int NTN>
 __device__ __forceinline__ void resblock16(const AS4 muz_resblock& R, float* X, float* T, float* U, Pf& pf,
                                            const AS4 muz_dense* Ln, int Kn, int Nn) {
-#if MUZ_EPI_LN
-  (void)U;
-  dense16_ln<NT256, NT256, LN_RELU>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT, R.ln0);
-  SYNC();
-  dense16_ln<NT256, NTN, LN_RESID_RELU>(R.d1, LAT, LAT, T, LD, X, LD, pf, Ln, Kn, Nn, R.ln1);
-  SYNC();
-#elif MUZ_DLN
-  // LayerNorm_0 + ReLU deferred into Dense_1's A reads
-  Dln* db = dln_buf(0);
-  dense16_dp<NT256, NT256>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT, db, R.ln0);
-  SYNC();
-  const LnP<LAT> p1 = ln_load<LAT>(R.ln1);
-  dense16_la<NT256, NTN>(R.d1, LAT, LAT, T, LD, U, LD, pf, Ln, Kn, Nn, dln_a(db, 0, 0, LAT, nw_for(LAT)));
-  SYNC();
-  ln16<LAT, LN_RESID_RELU>(U, LD, X, LD, p1);
-  SYNC();
-#else
   const LnP<LAT> p0 = ln_load<LAT>(R.ln0);
   dense16<NT256, NT256>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT);
   SYNC();
@@ -880,7 +552,6 @@ __device__ __forceinline__ void resblock16(const AS4 muz_resblock& R, float* X, 
   SYNC();
   ln16<LAT, LN_RESID_RELU>(U, LD, X, LD, p1);
   SYNC();
-#endif
 }
 
 // 64-input heads: weights of this lane's inputs k = sub + i*kRowLanes, loaded early.
@@ -947,30 +618,6 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
   }
   resblock16<NT256>(P.rb[0], a.X, a.T, a.U, pf, &P.rb[1].d0, LAT, LAT);
   resblock16<NT384>(P.rb[1], a.X, a.T, a.U, pf, &P.d03, LAT, 384);
-#if MUZ_DLN >= 2
-  // LayerNorm_1 | LayerNorm_3 of [policy Dense_0 | value Dense_3] deferred into Dense_1 / Dense_4, and
-  // LayerNorm_2 of Dense_1 into Dense_2; the value hidden layer's ReLU is applied as the head reads it
-  Dln* b0 = dln_buf(0);
-  Dln* b1 = dln_buf(1);
-  dense16_dp<NT384, NT128>(P.d03, LAT, 384, a.X, LD, a.W, LDW, pf, &P.d1, LAT, 128, b0, P.ln1, &P.ln3, LAT);
-  SYNC();
-  const HeadW hv = head_load(P.d5, 1);
-  dense16_dp<NT128, NT64, true>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &P.d4, 128, 64, b1, P.ln2, nullptr,
-                                1 << 30, dln_a(b0, 0, 0, LAT, nw_for(384)));                 // policy Dense_1
-  dense16_la<NT64, NTA>(P.d4, 128, 64, a.W + LAT, LDW, a.X, LD, pf, &P.d2, 128, A,
-                        dln_a(b0, 1, LAT, 128, nw_for(384)));                                // value Dense_4
-  ST(ST_PASS);
-  SYNC();
-  dense16_la<NTA, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn,
-                       dln_a(b1, 0, 0, 128, nw_for(128)));                                   // policy logits
-  {
-    const float zero[HeadW::kPer] = {};
-    const float v = head_dot_relu(a.X, LD, zero, hv, 0);
-    if (tsub() == 0) a.v0[trow()] = tanhf(v);
-  }
-  ST(ST_PASS);
-  SYNC();
-#else
   const LnP<LAT> p1 = ln_load<LAT>(P.ln1);
   const LnP<128> p3 = ln_load<128>(P.ln3);
   dense16<NT384, NT128>(P.d03, LAT, 384, a.X, LD, a.W, LDW, pf, &P.d1, LAT, 128);   // [policy Dense_0 | value Dense_3]
@@ -994,7 +641,6 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
   }
   ST(ST_PASS);
   SYNC();
-#endif
 }
 
 __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) {
@@ -1074,14 +720,6 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
     ST(ST_ROW);
   }
   SYNC();
-#if MUZ_DLN >= 3
-  // LayerNorm_1 + ReLU deferred into Dense_4's A reads
-  dense16_dp<NT256, NT256>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT, dln_buf(0), D.ln1);
-  SYNC();
-  const LnP<LAT> p2 = ln_load<LAT>(D.ln2);
-  dense16_la<NT256, NT256>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT,
-                           dln_a(dln_buf(0), 0, 0, LAT, nw_for(LAT)));
-#else
   const LnP<LAT> p1 = ln_load<LAT>(D.ln1);
   dense16<NT256, NT256>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT);
   SYNC();
@@ -1089,7 +727,6 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
   SYNC();
   const LnP<LAT> p2 = ln_load<LAT>(D.ln2);
   dense16<NT256, NT256>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT);
-#endif
   SYNC();
   ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, p2);
   SYNC();

@@ -32,16 +32,8 @@ __device__ unsigned long long g_muz_stamps[8];
 #endif
 
 // Two of the ~31 workgroup barriers per simulation are not needed for correctness (see the uses); removing
-// them measured within noise on MI355X (B=4096 S=50: +-1 %), so they stay.
-#ifndef MUZ_YOUNG_PRIO
-#define MUZ_YOUNG_PRIO 0   // s_setprio 1 for waves 4-7: measured within noise (profiles/r1e_prio_ab.log)
-#endif
-#ifndef MUZ_SEL_SYNC
-#define MUZ_SEL_SYNC 1   // workgroup barrier between the tree walk and Dyn4's first pass
-#endif
-#ifndef MUZ_TREE_SYNC
-#define MUZ_TREE_SYNC 1  // workgroup barrier between expand/backup and the next walk
-#endif
+// them measured within noise on MI355X (B=4096 S=50: +-1 %), so they stay.  A static s_setprio 1 for
+// waves 4-7 also measured within noise (profiles/r1e_prio_ab.log).
 
 constexpr int kMaxSims = 100;              // S <= 100 (config (e) uses 100)
 constexpr int kMaxNodes = kMaxSims + 1;
@@ -188,11 +180,6 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
 
   if (n_dev) n = *n_dev;
   if ((int)blockIdx.x * kRows >= n) return;
-#if MUZ_YOUNG_PRIO
-  // static priority for the second-dispatched half (waves 4-7): it otherwise loses VALU arbitration to its
-  // SIMD partner at the start of every phase (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= kThreads / 2) __builtin_amdgcn_s_setprio(1);
-#endif
   const Arena ar = Arena::carve(smem);
   const int A = Wt.num_actions;
   const int row = trow(), a = tsub();      // this lane holds action `a` of game `row`
@@ -319,9 +306,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
       if (a == 0) s_act[row] = 0;
     }
     ST(ST_SEL);
-    // Dyn4's first pass (LayerNorm_0 + FiLM of the parent latent) only reads this row's own registers and
-    // writes this row of the arena, so it follows the walk without a workgroup barrier (MUZ_SEL_SYNC 0)
-    if (MUZ_SEL_SYNC) SYNC();
+    // (Dyn4's first pass -- LayerNorm_0 + FiLM of the parent latent -- only reads this row's own registers
+    // and writes this row of the arena: this barrier is not needed for correctness, see above)
+    SYNC();
     MUZ_STAMP(1);   // select
     // ---------------- expand (search.py expand): recurrent_fn on the 16 parents
     // the new node's embedding goes to the tree and Pred4's LayerNorm_0 into ar.X straight from Dyn4's
@@ -396,10 +383,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
       }
     }
     ST(ST_TREE);
-    // The next walk of row r reads only what row r's own lanes (one wave) wrote here: LDS in wave order,
-    // the tree arrays after this wave's stores completed (workgroup fence); the arena buffers the
-    // next phases overwrite are behind the barrier after Dyn4's first pass (MUZ_TREE_SYNC 0)
-    if (MUZ_TREE_SYNC) SYNC(); else __threadfence_block();
+    // (The next walk of row r reads only what row r's own lanes -- one wave -- wrote here: this barrier is
+    // not needed for correctness either)
+    SYNC();
     MUZ_STAMP(6);   // expand + backward
   }
 #ifdef MUZ_STAMPS

@@ -17,10 +17,8 @@
 
 namespace muz {
 
-#ifndef MUZ_SP_BLOCK
-#define MUZ_SP_BLOCK 256
-#endif
-constexpr int kSpBlock = MUZ_SP_BLOCK;
+// lane kernels' workgroup size; 64 / 128 measured within noise of 256 (profiles/r1g_sp_block_ab.log)
+constexpr int kSpBlock = 256;
 
 // lane_game (streaming driver only): game number of each lane, -1 = idle; a game whose record is full
 // (idx == T, the reference's max_steps) stops like a finished one.

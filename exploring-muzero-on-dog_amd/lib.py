@@ -277,6 +277,9 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
+    if os.environ.get("MUZ_LIB"):       # never silent: a diagnostic build gives different timings
+        import sys
+        print(f"libmuz: MUZ_LIB selects {LIB_PATH} instead of the in-tree libmuz.so", file=sys.stderr)
     if not os.path.exists(LIB_PATH):
         raise MuzError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     # torch must own the HIP runtime first so both share one libamdhip64.so.7 instance.
