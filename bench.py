@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--sims", type=int, default=S)
     ap.add_argument("--depth", type=int, default=D)
     ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample (1 core + all cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--games", type=int, default=-1,
                     help="det: games per step streamed through the --batch lanes (default 32 x batch; 0 = one "
@@ -122,47 +122,37 @@ def dist_env():
     return rank, world, local
 
 
-def cpu_baseline(seconds, sims, depth, max_steps):
-    """The NumPy restatement (oracle/) of the same workload on the host: a bounded sample of 16 games
-    played until the time budget is used; reports env-steps/s of that sample."""
-    import numpy as np
-    from threadpoolctl import threadpool_limits
-    from oracle import detmadn as dm
-    from oracle import mctx_gumbel as G
-    from oracle import nets as ON
-    from oracle import selfplay as OS
+def cpu_cores():
+    """Host cores for the all-core CPU baseline: the process's affinity set, capped by OMP_NUM_THREADS when
+    the environment sets it (the GPU box grants a 16-CPU share of a larger machine and sets it to 16)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (min(aff, int(omp)) if omp and omp.isdigit() else aff), aff
 
-    cores = min(16, len(os.sched_getaffinity(0)))
-    params = ON.init_params(dm.num_channels(PLAYERS), seed=0)
-    n = 16
-    envs = [dm.env_reset(num_players=PLAYERS, **dm.SELFPLAY_RULES) for _ in range(n)]
-    steps = 0
-    t0 = time.perf_counter()
-    turn = 0
-    with threadpool_limits(limits=cores):
-        while time.perf_counter() - t0 < seconds and turn < max_steps:
-            active = [i for i in range(n) if not envs[i].done]
-            if not active:
-                break
-            search = [i for i in active if dm.valid_action(envs[i]).any()]
-            if search:
-                obs = np.stack([dm.encode_board(envs[i]) for i in search]).astype(np.float32)
-                inv = np.stack([~dm.valid_action(envs[i]).flatten() for i in search])
-                gum = np.stack([OS.gumbel_noise(0, i, turn) for i in search])
-                lg, v, e = ON.root_inference(params, obs)
-                act, _, _, _ = G.gumbel_muzero_policy(params, lg, v, e, ON.recurrent_inference, sims, inv, gum,
-                                                      max_depth=depth)
-                for k, i in enumerate(search):
-                    envs[i] = dm.env_step(envs[i], dm.map_action(int(act[k])))[0]
-            for i in active:
-                if i not in search:
-                    envs[i] = dm.no_step(envs[i])[0]
-            steps += len(active)
-            turn += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(steps / dt, 2), "unit": "env_steps/s", "cores": cores, "kind": "port",
-            "sample": f"NumPy oracle self-play, {n} games x {turn} turns ({steps} env-steps, S={sims}, D={depth}) "
-                      f"in {dt:.1f}s, BLAS threads={cores}"}
+
+def cpu_baseline(seconds, sims, depth, max_steps, lanes=16):
+    """SURVEY §8(d)'s CPU timing: the C++ restatement of the reference algorithm (oracle/cpu_selfplay.cpp:
+    det-MADN env + Repr2/Dyn4/Pred4 fp32 + Gumbel MuZero, OpenMP over game lanes; checked against the NumPy
+    oracle by tests/test_cpu_baseline.py) plays streamed 2p games on the host for `seconds` at 1 thread and
+    again at all cores.  The reference's own JAX-CPU path cannot run here (no jax in the image)."""
+    from oracle import cpu_selfplay as CS
+    from oracle import detmadn as dm
+    from oracle import nets as ON
+    C = dm.num_channels(PLAYERS)
+    net = CS.CpuNet(ON.init_params(C, seed=0), C)
+    cores, aff = cpu_cores()
+    half = seconds / 2
+    one = net.bench(PLAYERS, dm.SELFPLAY_RULES, lanes, sims, depth, max_steps, TEMP, 0, 1, half)
+    allc = net.bench(PLAYERS, dm.SELFPLAY_RULES, lanes, sims, depth, max_steps, TEMP, 0, cores, half)
+    v1 = one["env_steps"] / one["elapsed"]
+    vn = allc["env_steps"] / allc["elapsed"]
+    return {"value": round(vn, 2), "unit": "env_steps/s", "cores": cores, "kind": "port",
+            "value_1core": round(v1, 2), "value_allcores": round(vn, 2), "cores_affinity": aff,
+            "sims_per_s_allcores": round(allc["searches"] * sims / allc["elapsed"], 1),
+            "sample": f"C++ restatement of the reference algorithm (oracle/cpu_selfplay.cpp, fp32 AVX2/FMA, OpenMP): "
+                      f"det-MADN {PLAYERS}p streamed self-play, {lanes} game lanes per thread, S={sims} D={depth}, "
+                      f"{half:.0f} s at 1 thread ({one['env_steps']} env-steps) and {half:.0f} s at {cores} threads "
+                      f"({allc['env_steps']} env-steps); affinity shows {aff} CPUs"}
 
 
 def measured_traffic():

@@ -1,0 +1,943 @@
+// CPU restatement of det-MADN MuZero self-play in C++ with OpenMP over games.
+//
+// TEST INFRASTRUCTURE / CPU BASELINE ONLY: this is the "port" CPU baseline of SURVEY.md §8(d) -- the
+// reference algorithm (MADN/deterministic_madn.py env, MuZero_det_MADN/muzero_deterministic_madn.py
+// networks, mctx 0.0.6 gumbel_muzero_policy, MuZero_det_MADN/game_agent.py:50-183 self-play loop) restated
+// as plain fp32 C++ so bench.py can time it on the GPU box's host cores beside the HIP engine.  It follows
+// the NumPy oracle line by line (oracle/detmadn.py, oracle/nets.py, oracle/mctx_gumbel.py,
+// oracle/selfplay.py) and is checked against it by tests/test_cpu_baseline.py (golden step vectors, network
+// outputs, a short self-play trace).  Only tests/, smoke() and bench.py's cpu_baseline leg load it; the
+// product path never does.
+//
+// Parallelism mirrors the reference's vmap over games: each OpenMP thread owns a batch of game lanes,
+// searches them together (batched network calls, per-game trees) and refills a lane with the next game
+// when its game ends.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include <immintrin.h>
+#include <omp.h>
+
+namespace {
+
+constexpr int kCells = 56;
+constexpr int kA = 24;
+constexpr int kLat = 256;
+constexpr float kTiny = std::numeric_limits<float>::min();
+constexpr float kFMin = -std::numeric_limits<float>::max();
+constexpr float kInf = std::numeric_limits<float>::infinity();
+
+enum : uint32_t {
+  R_TEAMS = 1, R_FREE_PIN = 2, R_CIRCULAR = 4, R_START_BLOCK = 8, R_JUMP_GOAL = 16, R_FRIENDLY = 32,
+  R_START_ON_1 = 64, R_BONUS_6 = 128, R_MUST_TRAVERSE = 256
+};
+
+}  // namespace
+
+extern "C" {
+
+// one deterministic_MADN state (deterministic_madn.py:24-40); pins / action_set / goal rows = players
+typedef struct {
+  int8_t board[kCells];
+  int8_t pins[16];
+  int8_t action_set[24];
+  int8_t start[4], target[4], goal[16];
+  int32_t current_player, reward, done, num_players, board_size, total, rules;
+} muzcpu_det;
+
+}  // extern "C"
+
+namespace {
+
+inline long long pymod(long long a, long long n) { long long r = a % n; return r < 0 ? r + n : r; }
+inline long long floordiv(long long a, long long n) { long long q = a / n; return (a % n != 0 && ((a < 0) != (n < 0))) ? q - 1 : q; }
+// jax gather: normalise a negative index once, then clamp into [0, n)
+inline long long gidx(long long i, long long n) { if (i < 0) i += n; return i < 0 ? 0 : (i >= n ? n - 1 : i); }
+inline bool has(const muzcpu_det& e, uint32_t f) { return (e.rules & f) != 0; }
+
+void set_pins_on_board(int8_t* board, const int8_t* pins, int P, int total) {   // 259-271
+  for (int i = 0; i < total; ++i) board[i] = -1;
+  for (int p = 0; p < P; ++p)
+    for (int k = 0; k < 4; ++k) {
+      const int pos = pins[p * 4 + k];
+      if (pos >= 0 && pos < total) board[pos] = (int8_t)p;
+    }
+}
+
+bool is_player_done(const muzcpu_det& e, const int8_t* board, int p) {   // 122-137
+  if (p >= e.num_players) return false;
+  for (int k = 0; k < 4; ++k)
+    if (board[e.goal[p * 4 + k]] < 0) return false;
+  return true;
+}
+
+void get_winner(const muzcpu_det& e, const int8_t* board, bool w[4]) {   // 139-168
+  bool d[4];
+  for (int p = 0; p < 4; ++p) d[p] = is_player_done(e, board, p);
+  if (!has(e, R_TEAMS)) {
+    for (int p = 0; p < 4; ++p) w[p] = d[p];
+    return;
+  }
+  const bool t0 = d[0] && d[2], t1 = d[1] && d[3];
+  for (int p = 0; p < 4; ++p) w[p] = false;
+  if ((t0 && t1) || !(t0 || t1)) return;
+  if (t0) w[0] = w[2] = true; else w[1] = w[3] = true;
+}
+
+int sub_player(const muzcpu_det& e) {   // 184 / 310
+  const int p = e.current_player;
+  return (has(e, R_TEAMS) && is_player_done(e, e.board, p)) ? (p + 2) % 4 : p;
+}
+
+// utils/utility_funcs.py:142-184: all(board[goal[ga]] != cp for start < ga < x)
+bool goal_path_free(long long start, long long x, const int8_t* goal, const int8_t* board, int cp) {
+  for (int ga = 0; ga < 4; ++ga)
+    if (start < ga && ga < x && board[goal[ga]] == cp) return false;
+  return true;
+}
+
+void valid_action(const muzcpu_det& e, bool va[4][6]) {   // 299-393
+  const int cp0 = e.current_player, cp = sub_player(e), P = e.num_players, bs = e.board_size;
+  const int8_t* board = e.board;
+  const int8_t* goal = e.goal + cp * 4;
+  const long long target = e.target[cp];
+  const long long mt = has(e, R_MUST_TRAVERSE) ? 1 : 0;
+  bool pos_[4];
+  for (int p = 0; p < P; ++p) pos_[p] = board[e.start[p]] == p;
+  const long long dist = bs / 4;
+  for (int i = 0; i < 4; ++i) {
+    const long long cur = e.pins[cp * 4 + i];
+    for (int m = 1; m <= 6; ++m) {
+      const long long moved = cur + m;
+      const long long fitted = pymod(moved, bs);
+      long long x = moved - target - mt;
+      bool res = (board[fitted] != cp) || has(e, R_FRIENDLY);
+      const long long nsb = pymod(floordiv(cur, dist) + 1, P);
+      const long long nsa = floordiv(fitted, dist);
+      const bool trav = e.start[gidx(nsb, P)] == e.start[gidx(nsa, P)];
+      const bool pos_nsa = pos_[gidx(nsa, P)];
+      if (has(e, R_START_BLOCK) && trav) res = (!pos_nsa || cur == e.start[cp]) && res;
+      if (has(e, R_MUST_TRAVERSE) && has(e, R_START_BLOCK) && trav && pos_nsa) x = 0;
+      if (!has(e, R_CIRCULAR) && cur <= target && (x > 4 || (x == 0 && has(e, R_MUST_TRAVERSE)))) res = false;
+      const bool A = has(e, R_CIRCULAR) && res;
+      const bool B = board[goal[gidx(x - 1, 4)]] != cp;
+      const bool C = has(e, R_JUMP_GOAL) || goal_path_free(-1, x, goal, board, cp);
+      if (4 >= x && x > 0 && cur <= target) res = A || (B && C);
+      const bool D = has(e, R_JUMP_GOAL) || goal_path_free(cur - goal[0], moved - goal[0] + 1, goal, board, cp);
+      bool in_goal = false;
+      for (int k = 0; k < 4; ++k) in_goal = in_goal || cur == goal[k];
+      if (in_goal) res = (moved <= goal[3]) && (board[gidx(moved, e.total)] != cp) && D;
+      const bool start_move = m == 6 || (m == 1 && has(e, R_START_ON_1));
+      if (cur == -1) res = start_move && (board[e.start[cp]] != cp0);
+      va[i][m - 1] = res && e.action_set[cp * 6 + m - 1] > 0;
+    }
+  }
+}
+
+void env_reset(muzcpu_det& e, int P, const int* layout, int distance, int starting_player, int rules) {   // 42-120
+  std::memset(&e, 0, sizeof(e));
+  e.rules = rules;
+  if (P != 4) e.rules &= ~R_TEAMS;
+  e.num_players = P;
+  e.board_size = 4 * distance;
+  e.total = e.board_size + 16;
+  bool lay[4];
+  int cnt = 0;
+  for (int i = 0; i < 4; ++i) cnt += (lay[i] = layout[i] != 0);
+  if (cnt != P || (cnt == 4 && P < 4))
+    for (int i = 0; i < 4; ++i) lay[i] = i < P;
+  int k = 0;
+  for (int s = 0; s < 4; ++s) {
+    if (!lay[s]) continue;
+    e.start[k] = (int8_t)(s * distance);
+    e.target[k] = (int8_t)pymod(s * distance - 1, e.board_size);
+    for (int j = 0; j < 4; ++j) e.goal[k * 4 + j] = (int8_t)(e.board_size + 4 * s + j);
+    ++k;
+  }
+  for (int i = 0; i < 16; ++i) e.pins[i] = -1;
+  if (e.rules & R_FREE_PIN)
+    for (int p = 0; p < P; ++p) e.pins[p * 4] = e.start[p];
+  set_pins_on_board(e.board, e.pins, P, e.total);
+  for (int i = 0; i < 24; ++i) e.action_set[i] = i < 6 * P ? 4 : 0;
+  e.current_player = starting_player;
+}
+
+void env_step(muzcpu_det& e, int pin, int move, int& reward_out, int& done_out) {   // 170-257
+  const int player_id = e.current_player, cp = sub_player(e);
+  bool va[4][6];
+  valid_action(e, va);
+  const int mi = (int)pymod(move - 1, 6);
+  const bool invalid = !va[pin][mi];
+  const long long cur = e.pins[cp * 4 + pin];
+  const long long moved = cur + move;
+  const long long fitted = pymod(moved, e.board_size);
+  const long long x = moved - e.target[cp] - (has(e, R_MUST_TRAVERSE) ? 1 : 0);
+  const int8_t* goal = e.goal + cp * 4;
+  const int8_t* board = e.board;
+  bool in_goal = false;
+  for (int k = 0; k < 4; ++k) in_goal = in_goal || cur == goal[k];
+  const bool a = in_goal ? goal_path_free(cur - goal[0], moved - goal[0] + 1, goal, board, cp)
+                         : goal_path_free(-1, x, goal, board, cp);
+  const bool A = (board[goal[gidx(x - 1, 4)]] != cp) && (has(e, R_JUMP_GOAL) || a);
+  long long new_pos;
+  if (cur == -1) new_pos = e.start[cp];
+  else if (in_goal) new_pos = moved;
+  else if (4 >= x && x > 0 && A && cur <= e.target[cp]) new_pos = goal[gidx(x - 1, 4)];
+  else new_pos = fitted;
+  const int pin_at = board[gidx(new_pos, e.total)];
+  int8_t pins[16];
+  std::memcpy(pins, e.pins, 16);
+  if (pin_at != -1 && (pin_at != cp || has(e, R_FRIENDLY)) && !invalid)
+    for (int k = 0; k < 4; ++k)
+      if (pins[pin_at * 4 + k] == new_pos) pins[pin_at * 4 + k] = -1;
+  if (!invalid) pins[cp * 4 + pin] = (int8_t)new_pos;
+  int8_t nb[kCells];
+  if (invalid) std::memcpy(nb, e.board, kCells);
+  else set_pins_on_board(nb, pins, e.num_players, e.total);
+  const int cs = e.action_set[cp * 6 + mi];
+  int8_t aset[24];
+  std::memcpy(aset, e.action_set, 24);
+  aset[cp * 6 + mi] = (int8_t)((invalid || cs == 0) ? cs : cs - 1);
+  bool empty = true;
+  for (int j = 0; j < 6; ++j) empty = empty && aset[cp * 6 + j] == 0;
+  if (empty) {   // refill restores the PRE-step set with the current player's row full (quirk, 235-240)
+    std::memcpy(aset, e.action_set, 24);
+    for (int j = 0; j < 6; ++j) aset[player_id * 6 + j] = 4;
+  }
+  bool w[4];
+  get_winner(e, nb, w);
+  const int reward = e.done ? 0 : (invalid ? -1 : (w[cp] ? 1 : 0));
+  const bool done = e.done || w[0] || w[1] || w[2] || w[3];
+  const int nxt = (done || (has(e, R_BONUS_6) && move == 6)) ? player_id : (player_id + 1) % e.num_players;
+  std::memcpy(e.board, nb, kCells);
+  std::memcpy(e.pins, pins, 16);
+  std::memcpy(e.action_set, aset, 24);
+  e.current_player = nxt;
+  e.done = done;
+  e.reward = reward;
+  reward_out = reward;
+  done_out = done;
+}
+
+void no_step(muzcpu_det& e) {   // 283-297
+  for (int j = 0; j < 6; ++j) e.action_set[e.current_player * 6 + j] = 4;
+  e.current_player = (e.current_player + 1) % e.num_players;
+}
+
+void encode_board(const muzcpu_det& e, float* out) {   // 395-438 -> [8P+2][56]
+  const int P = e.num_players, bs = e.board_size, dist = bs / 4, cp = e.current_player, W = e.total;
+  int8_t b[kCells];
+  for (int i = 0; i < bs; ++i) b[i] = e.board[(i + dist * cp) % bs];
+  for (int i = 0; i < 16; ++i) b[bs + i] = e.board[bs + (i + 4 * cp) % 16];
+  int rolled[4];
+  for (int k = 0; k < P; ++k) rolled[k] = (k + cp) % P;
+  const int C = 8 * P + 2;
+  std::memset(out, 0, sizeof(float) * C * W);
+  for (int k = 0; k < P; ++k)
+    for (int w = 0; w < W; ++w) out[k * W + w] = b[w] == rolled[k] ? 1.f : 0.f;
+  for (int w = 0; w < W; ++w) {
+    float t = 0.f, o = 0.f;
+    for (int k = 0; k < P; ++k) {
+      const bool team = has(e, R_TEAMS) ? (k % 2 == 0) : (k == 0);
+      (team ? t : o) += out[k * W + w];
+    }
+    out[P * W + w] = t;
+    out[(P + 1) * W + w] = o;
+  }
+  for (int k = 0; k < P; ++k) {
+    int home = 0;
+    for (int j = 0; j < 4; ++j) home += e.pins[rolled[k] * 4 + j] == -1;
+    for (int w = 0; w < W; ++w) out[(P + 2 + k) * W + w] = (float)home;
+  }
+  for (int k = 0; k < P; ++k)
+    for (int m = 0; m < 6; ++m)
+      for (int w = 0; w < W; ++w) out[(2 * P + 2 + k * 6 + m) * W + w] = (float)e.action_set[rolled[k] * 6 + m];
+}
+
+// ------------------------------------------------------------------------------------------- networks
+struct Net {
+  std::map<std::string, std::vector<float>> p;
+  int C = 0;
+  const float* w(const std::string& k) const {
+    auto it = p.find(k);
+    if (it == p.end()) return nullptr;
+    return it->second.data();
+  }
+  size_t n(const std::string& k) const { return p.at(k).size(); }
+};
+
+// out[R rows][N] = in[R][K] @ W[K][N] + b with the accumulators in AVX2 registers: 4 rows x 16 columns per
+// block, k innermost (each output is the k-ordered fma chain starting from its bias).
+template <int R>
+void dense_rows(const float* in, int K, int N, const float* W, const float* b, float* out) {
+  int j = 0;
+  for (; j + 16 <= N; j += 16) {
+    __m256 acc[R][2];
+    for (int r = 0; r < R; ++r) {
+      acc[r][0] = _mm256_loadu_ps(b + j);
+      acc[r][1] = _mm256_loadu_ps(b + j + 8);
+    }
+    for (int k = 0; k < K; ++k) {
+      const __m256 w0 = _mm256_loadu_ps(W + (size_t)k * N + j), w1 = _mm256_loadu_ps(W + (size_t)k * N + j + 8);
+      for (int r = 0; r < R; ++r) {
+        const __m256 a = _mm256_broadcast_ss(in + (size_t)r * K + k);
+        acc[r][0] = _mm256_fmadd_ps(a, w0, acc[r][0]);
+        acc[r][1] = _mm256_fmadd_ps(a, w1, acc[r][1]);
+      }
+    }
+    for (int r = 0; r < R; ++r) {
+      _mm256_storeu_ps(out + (size_t)r * N + j, acc[r][0]);
+      _mm256_storeu_ps(out + (size_t)r * N + j + 8, acc[r][1]);
+    }
+  }
+  for (; j + 8 <= N; j += 8) {
+    __m256 acc[R];
+    for (int r = 0; r < R; ++r) acc[r] = _mm256_loadu_ps(b + j);
+    for (int k = 0; k < K; ++k) {
+      const __m256 w0 = _mm256_loadu_ps(W + (size_t)k * N + j);
+      for (int r = 0; r < R; ++r) acc[r] = _mm256_fmadd_ps(_mm256_broadcast_ss(in + (size_t)r * K + k), w0, acc[r]);
+    }
+    for (int r = 0; r < R; ++r) _mm256_storeu_ps(out + (size_t)r * N + j, acc[r]);
+  }
+  for (; j < N; ++j)
+    for (int r = 0; r < R; ++r) {
+      float a = b[j];
+      for (int k = 0; k < K; ++k) a = std::fma(in[(size_t)r * K + k], W[(size_t)k * N + j], a);
+      out[(size_t)r * N + j] = a;
+    }
+}
+
+void dense_raw(const float* W, const float* b, const float* in, int B, int K, int N, float* out) {
+  int r = 0;
+  for (; r + 8 <= B; r += 8) dense_rows<8>(in + (size_t)r * K, K, N, W, b, out + (size_t)r * N);
+  for (; r + 4 <= B; r += 4) dense_rows<4>(in + (size_t)r * K, K, N, W, b, out + (size_t)r * N);
+  for (; r < B; ++r) dense_rows<1>(in + (size_t)r * K, K, N, W, b, out + (size_t)r * N);
+}
+
+void dense(const Net& net, const std::string& name, const float* in, int B, int K, int N, float* out) {
+  dense_raw(net.w(name + "/kernel"), net.w(name + "/bias"), in, B, K, N, out);
+}
+
+void layer_norm(const Net& net, const std::string& name, float* x, int B, int N, bool relu) {
+  const float* sc = net.w(name + "/scale");
+  const float* sh = net.w(name + "/bias");
+  for (int r = 0; r < B; ++r) {
+    float* v = x + (size_t)r * N;
+    float s = 0.f, s2 = 0.f;
+    for (int j = 0; j < N; ++j) {
+      s += v[j];
+      s2 += v[j] * v[j];
+    }
+    const float mean = s / (float)N, mean2 = s2 / (float)N;
+    const float var = std::max(0.f, mean2 - mean * mean);
+    const float inv = 1.0f / std::sqrt(var + 1e-6f);
+    for (int j = 0; j < N; ++j) {
+      const float y = (v[j] - mean) * (inv * sc[j]) + sh[j];
+      v[j] = relu ? std::max(y, 0.f) : y;
+    }
+  }
+}
+
+void relu_(float* x, size_t n) { for (size_t i = 0; i < n; ++i) x[i] = std::max(x[i], 0.f); }
+
+void minmax(float* x, int B, int N) {
+  for (int r = 0; r < B; ++r) {
+    float* v = x + (size_t)r * N;
+    float lo = kInf, hi = -kInf;
+    for (int j = 0; j < N; ++j) {
+      lo = std::min(lo, v[j]);
+      hi = std::max(hi, v[j]);
+    }
+    const float den = hi - lo + 1e-8f;
+    for (int j = 0; j < N; ++j) v[j] = (v[j] - lo) / den;
+  }
+}
+
+// ResBlock (12-24) in place on x [B][256]
+void resblock(const Net& net, const std::string& pre, float* x, int B, std::vector<float>& t1, std::vector<float>& t2) {
+  t1.resize((size_t)B * kLat);
+  t2.resize((size_t)B * kLat);
+  dense(net, pre + "/Dense_0", x, B, kLat, kLat, t1.data());
+  layer_norm(net, pre + "/LayerNorm_0", t1.data(), B, kLat, true);
+  dense(net, pre + "/Dense_1", t1.data(), B, kLat, kLat, t2.data());
+  layer_norm(net, pre + "/LayerNorm_1", t2.data(), B, kLat, false);
+  for (size_t i = 0; i < (size_t)B * kLat; ++i) x[i] = std::max(x[i] + t2[i], 0.f);
+}
+
+struct Scratch {
+  std::vector<float> a, b, c, d, t1, t2;
+};
+
+// Conv 1-D 'SAME' (Flax), as im2col + dense: in [B][56][Cin] -> out [B][56][Cout]
+void conv1d(const Net& net, const std::string& name, const float* in, int B, int Cin, int Cout, int K, float* out) {
+  const int pl = (K - 1) / 2;
+  std::vector<float> cols((size_t)B * kCells * K * Cin, 0.f);
+  for (int r = 0; r < B; ++r)
+    for (int w = 0; w < kCells; ++w)
+      for (int d = 0; d < K; ++d) {
+        const int src = w + d - pl;
+        if (src < 0 || src >= kCells) continue;
+        std::memcpy(&cols[(((size_t)r * kCells + w) * K + d) * Cin], in + ((size_t)r * kCells + src) * Cin,
+                    sizeof(float) * Cin);
+      }
+  dense(net, name, cols.data(), B * kCells, K * Cin, Cout, out);   // kernel [K][Cin][Cout] = [K*Cin][Cout]
+}
+
+// RepresentationNetwork2 (75-141): obs [B][C][56] -> latent [B][256]
+void representation(const Net& net, const float* obs, int B, float* lat, Scratch& s) {
+  const int C = net.C;
+  const std::string r = "representation/";
+  s.a.assign((size_t)B * kCells * 6, 0.f);
+  for (int b = 0; b < B; ++b)
+    for (int w = 0; w < kCells; ++w)
+      for (int c = 0; c < 6; ++c) s.a[((size_t)b * kCells + w) * 6 + c] = obs[((size_t)b * C + c) * kCells + w];
+  s.b.resize((size_t)B * kCells * 64);
+  s.c.resize((size_t)B * kCells * 64);
+  conv1d(net, r + "Conv_0", s.a.data(), B, 6, 32, 3, s.b.data());
+  layer_norm(net, r + "LayerNorm_0", s.b.data(), B * kCells, 32, true);
+  conv1d(net, r + "Conv_1", s.b.data(), B, 32, 64, 3, s.c.data());
+  layer_norm(net, r + "LayerNorm_1", s.c.data(), B * kCells, 64, true);
+  conv1d(net, r + "Conv_2", s.c.data(), B, 64, 64, 5, s.b.data());
+  layer_norm(net, r + "LayerNorm_2", s.b.data(), B * kCells, 64, true);
+  std::vector<float> cat((size_t)B * 320);
+  std::vector<float> flat((size_t)B * kLat);
+  dense(net, r + "Dense_0", s.b.data(), B, kCells * 64, kLat, flat.data());
+  layer_norm(net, r + "LayerNorm_3", flat.data(), B, kLat, true);
+  std::vector<float> g((size_t)B * (C - 6)), g1((size_t)B * 64), g2((size_t)B * 64);
+  for (int b = 0; b < B; ++b)
+    for (int c = 6; c < C; ++c) g[(size_t)b * (C - 6) + c - 6] = obs[((size_t)b * C + c) * kCells];
+  dense(net, r + "Dense_1", g.data(), B, C - 6, 64, g1.data());
+  layer_norm(net, r + "LayerNorm_4", g1.data(), B, 64, true);
+  dense(net, r + "Dense_2", g1.data(), B, 64, 64, g2.data());
+  layer_norm(net, r + "LayerNorm_5", g2.data(), B, 64, true);
+  for (int b = 0; b < B; ++b) {
+    std::memcpy(&cat[(size_t)b * 320], &flat[(size_t)b * kLat], sizeof(float) * kLat);
+    std::memcpy(&cat[(size_t)b * 320 + kLat], &g2[(size_t)b * 64], sizeof(float) * 64);
+  }
+  std::vector<float> h((size_t)B * kLat);
+  dense(net, r + "Dense_3", cat.data(), B, 320, kLat, h.data());
+  layer_norm(net, r + "LayerNorm_6", h.data(), B, kLat, true);
+  for (int i = 0; i < 6; ++i) resblock(net, r + "ResBlock_" + std::to_string(i), h.data(), B, s.t1, s.t2);
+  dense(net, r + "Dense_4", h.data(), B, kLat, kLat, lat);
+  minmax(lat, B, kLat);
+}
+
+// PredictionNetwork4 (549-583): latent [B][256] -> logits [B][A], value [B]
+void prediction(const Net& net, const float* lat, int B, float* logits, float* value, Scratch& s) {
+  const std::string p = "prediction/";
+  std::vector<float> x(lat, lat + (size_t)B * kLat);
+  layer_norm(net, p + "LayerNorm_0", x.data(), B, kLat, false);
+  for (int i = 0; i < 2; ++i) resblock(net, p + "ResBlock_" + std::to_string(i), x.data(), B, s.t1, s.t2);
+  std::vector<float> h0((size_t)B * kLat), h1((size_t)B * 128), v0((size_t)B * 128), v1((size_t)B * 64);
+  dense(net, p + "Dense_0", x.data(), B, kLat, kLat, h0.data());
+  layer_norm(net, p + "LayerNorm_1", h0.data(), B, kLat, true);
+  dense(net, p + "Dense_1", h0.data(), B, kLat, 128, h1.data());
+  layer_norm(net, p + "LayerNorm_2", h1.data(), B, 128, true);
+  dense(net, p + "Dense_2", h1.data(), B, 128, kA, logits);
+  dense(net, p + "Dense_3", x.data(), B, kLat, 128, v0.data());
+  layer_norm(net, p + "LayerNorm_3", v0.data(), B, 128, true);
+  dense(net, p + "Dense_4", v0.data(), B, 128, 64, v1.data());
+  relu_(v1.data(), v1.size());
+  std::vector<float> v2(B);
+  dense(net, p + "Dense_5", v1.data(), B, 64, 1, v2.data());
+  for (int b = 0; b < B; ++b) value[b] = std::tanh(v2[b]);
+}
+
+float support3(const float* l) {   // sum(softmax(l) * [-1, 0, 1])
+  const float m = std::max(std::max(l[0], l[1]), l[2]);
+  const float e0 = std::exp(l[0] - m), e1 = std::exp(l[1] - m), e2 = std::exp(l[2] - m);
+  const float z = e0 + e1 + e2;
+  return (e0 / z) * -1.0f + (e1 / z) * 0.0f + (e2 / z) * 1.0f;
+}
+
+// recurrent_inference_fn (632-661) with DynamicsNetwork4 (391-457)
+void recurrent(const Net& net, const int* action, const float* emb, int B, float* reward, float* discount,
+               float* logits, float* value, float* nxt, Scratch& s) {
+  const std::string d = "dynamics/";
+  std::vector<float> oh((size_t)B * kA, 0.f);
+  for (int b = 0; b < B; ++b)
+    if (action[b] >= 0 && action[b] < kA) oh[(size_t)b * kA + action[b]] = 1.f;
+  std::vector<float> e((size_t)B * 64), sc((size_t)B * kLat), shf((size_t)B * kLat);
+  dense(net, d + "Dense_0", oh.data(), B, kA, 64, e.data());
+  relu_(e.data(), e.size());
+  std::vector<float> x(emb, emb + (size_t)B * kLat);
+  layer_norm(net, d + "LayerNorm_0", x.data(), B, kLat, false);
+  dense(net, d + "Dense_1", e.data(), B, 64, kLat, sc.data());
+  dense(net, d + "Dense_2", e.data(), B, 64, kLat, shf.data());
+  for (size_t i = 0; i < x.size(); ++i) x[i] = x[i] * (1.0f + sc[i]) + shf[i];
+  std::vector<float> y((size_t)B * kLat);
+  dense(net, d + "Dense_3", x.data(), B, kLat, kLat, y.data());
+  layer_norm(net, d + "LayerNorm_1", y.data(), B, kLat, true);
+  dense(net, d + "Dense_4", y.data(), B, kLat, kLat, x.data());
+  layer_norm(net, d + "LayerNorm_2", x.data(), B, kLat, true);
+  for (int i = 0; i < 2; ++i) resblock(net, d + "ResBlock_" + std::to_string(i), x.data(), B, s.t1, s.t2);
+  dense(net, d + "Dense_5", x.data(), B, kLat, kLat, y.data());
+  for (size_t i = 0; i < y.size(); ++i) nxt[i] = emb[i] + y[i];
+  minmax(nxt, B, kLat);
+  std::vector<float> ri((size_t)B * (kLat + kA)), h((size_t)B * 64), l3((size_t)B * 3);
+  for (int b = 0; b < B; ++b) {
+    std::memcpy(&ri[(size_t)b * (kLat + kA)], nxt + (size_t)b * kLat, sizeof(float) * kLat);
+    std::memcpy(&ri[(size_t)b * (kLat + kA) + kLat], &oh[(size_t)b * kA], sizeof(float) * kA);
+  }
+  dense(net, d + "Dense_6", ri.data(), B, kLat + kA, 64, h.data());
+  relu_(h.data(), h.size());
+  dense(net, d + "reward_head", h.data(), B, 64, 3, l3.data());
+  for (int b = 0; b < B; ++b) reward[b] = support3(&l3[(size_t)b * 3]);
+  dense(net, d + "Dense_7", ri.data(), B, kLat + kA, 64, h.data());
+  relu_(h.data(), h.size());
+  dense(net, d + "discount_head", h.data(), B, 64, 3, l3.data());
+  for (int b = 0; b < B; ++b) discount[b] = support3(&l3[(size_t)b * 3]);
+  prediction(net, nxt, B, logits, value, s);
+}
+
+// ------------------------------------------------------------------------------ mctx gumbel_muzero_policy
+std::vector<int> considered_sequence(int m, int S) {   // seq_halving.get_sequence_of_considered_visits
+  std::vector<int> seq;
+  if (m <= 1) {
+    for (int i = 0; i < S; ++i) seq.push_back(i);
+    return seq;
+  }
+  const int log2max = (int)std::ceil(std::log2((double)m));
+  std::vector<int> visits(m, 0);
+  int k = m;
+  while ((int)seq.size() < S) {
+    const int extra = std::max(1, (int)(S / (log2max * k)));
+    for (int e = 0; e < extra; ++e) {
+      for (int i = 0; i < k; ++i) seq.push_back(visits[i]);
+      for (int i = 0; i < k; ++i) visits[i] += 1;
+    }
+    k = std::max(2, k / 2);
+  }
+  seq.resize(S);
+  return seq;
+}
+
+struct Tree {
+  int N;
+  std::vector<int> visits, parent, afp, c_index, c_visits;
+  std::vector<float> raw, value, c_prior, c_value, c_reward, c_disc, emb;
+  void init(int n) {
+    N = n;
+    visits.assign(n, 0);
+    parent.assign(n, -1);
+    afp.assign(n, -1);
+    raw.assign(n, 0.f);
+    value.assign(n, 0.f);
+    c_index.assign((size_t)n * kA, -1);
+    c_visits.assign((size_t)n * kA, 0);
+    c_prior.assign((size_t)n * kA, 0.f);
+    c_value.assign((size_t)n * kA, 0.f);
+    c_reward.assign((size_t)n * kA, 0.f);
+    c_disc.assign((size_t)n * kA, 0.f);
+    emb.assign((size_t)n * kLat, 0.f);
+  }
+  void update(int node, const float* prior, float v, const float* e) {
+    std::memcpy(&c_prior[(size_t)node * kA], prior, sizeof(float) * kA);
+    raw[node] = v;
+    value[node] = v;
+    visits[node] += 1;
+    std::memcpy(&emb[(size_t)node * kLat], e, sizeof(float) * kLat);
+  }
+};
+
+void softmax(const float* x, float* out, int n) {
+  float m = -kInf;
+  for (int i = 0; i < n; ++i) m = std::max(m, x[i]);
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += (out[i] = std::exp(x[i] - m));
+  for (int i = 0; i < n; ++i) out[i] /= s;
+}
+
+// qtransform_completed_by_mix_value(value_scale 0.5, maxvisit_init 50, rescale, mixed value, eps 1e-8)
+void completed_q(const Tree& t, int node, float* cq) {
+  const int* vis = &t.c_visits[(size_t)node * kA];
+  float q[kA], pp[kA];
+  softmax(&t.c_prior[(size_t)node * kA], pp, kA);
+  int sumv = 0, maxv = 0;
+  float sp = 0.f;
+  for (int a = 0; a < kA; ++a) {
+    q[a] = t.c_reward[(size_t)node * kA + a] + t.c_disc[(size_t)node * kA + a] * t.c_value[(size_t)node * kA + a];
+    pp[a] = std::max(kTiny, pp[a]);
+    sumv += vis[a];
+    maxv = std::max(maxv, vis[a]);
+    if (vis[a] > 0) sp += pp[a];
+  }
+  float wq = 0.f;
+  for (int a = 0; a < kA; ++a)
+    if (vis[a] > 0) wq += pp[a] * q[a] / sp;
+  const float mixed = (t.raw[node] + (float)sumv * wq) / (float)(sumv + 1);
+  float lo = kInf, hi = -kInf;
+  for (int a = 0; a < kA; ++a) {
+    cq[a] = vis[a] > 0 ? q[a] : mixed;
+    lo = std::min(lo, cq[a]);
+    hi = std::max(hi, cq[a]);
+  }
+  const float den = std::max(hi - lo, 1e-8f);
+  const float scale = (50.0f + (float)maxv) * 0.5f;
+  for (int a = 0; a < kA; ++a) cq[a] = scale * ((cq[a] - lo) / den);
+}
+
+int argmax(const float* x, int n) {
+  int bi = 0;
+  for (int i = 1; i < n; ++i)
+    if (x[i] > x[bi]) bi = i;
+  return bi;
+}
+
+struct Search {
+  int S, D;
+  std::vector<std::vector<int>> table;   // [m][sim]
+  void init(int s, int d) {
+    S = s;
+    D = d;
+    table.clear();
+    for (int m = 0; m <= 16; ++m) table.push_back(considered_sequence(m, S));
+  }
+};
+
+// score_considered + masked argmax (root) / softmax(prior + cq) - N / (1 + sum N) (interior)
+int select_child(const Tree& t, int node, int depth, const bool* invalid, const float* gumbel, const Search& sr,
+                 int ncons) {
+  float cq[kA], sc[kA];
+  completed_q(t, node, cq);
+  const int* vis = &t.c_visits[(size_t)node * kA];
+  const float* prior = &t.c_prior[(size_t)node * kA];
+  int sumv = 0;
+  for (int a = 0; a < kA; ++a) sumv += vis[a];
+  if (depth == 0) {
+    const int cv = sr.table[ncons][std::min(sumv, sr.S - 1)];
+    float pm = -kInf;
+    for (int a = 0; a < kA; ++a) pm = std::max(pm, prior[a]);
+    for (int a = 0; a < kA; ++a) {
+      const float s = std::max(-1e9f, gumbel[a] + (prior[a] - pm) + cq[a]) + (vis[a] == cv ? 0.f : -kInf);
+      sc[a] = invalid[a] ? -kInf : s;
+    }
+  } else {
+    float z[kA], p[kA];
+    for (int a = 0; a < kA; ++a) z[a] = prior[a] + cq[a];
+    softmax(z, p, kA);
+    for (int a = 0; a < kA; ++a) sc[a] = p[a] - (float)vis[a] / (float)(1 + sumv);
+  }
+  return argmax(sc, kA);
+}
+
+// one batched gumbel_muzero_policy over `B` games (root inference outputs given)
+void gumbel_search(const Net& net, const Search& sr, int B, const float* logits, const float* rvalue,
+                   const float* remb, const bool* invalid, const float* gumbel, std::vector<Tree>& trees,
+                   int* action_out, float* weights_out, float* value_out, Scratch& s) {
+  const int S = sr.S;
+  std::vector<int> ncons(B), parent(B), act(B), nxt(B);
+  std::vector<float> rew(B), disc(B), lg((size_t)B * kA), val(B), ne((size_t)B * kLat), pe((size_t)B * kLat);
+  for (int b = 0; b < B; ++b) {
+    Tree& t = trees[b];
+    t.init(S + 1);
+    float pr[kA];
+    float m = -kInf;
+    for (int a = 0; a < kA; ++a) m = std::max(m, logits[(size_t)b * kA + a]);
+    int nv = 0;
+    for (int a = 0; a < kA; ++a) {
+      pr[a] = invalid[(size_t)b * kA + a] ? kFMin : logits[(size_t)b * kA + a] - m;
+      nv += !invalid[(size_t)b * kA + a];
+    }
+    ncons[b] = std::min(16, nv);
+    t.update(0, pr, rvalue[b], remb + (size_t)b * kLat);
+  }
+  for (int sim = 0; sim < S; ++sim) {
+    for (int b = 0; b < B; ++b) {   // simulate
+      const Tree& t = trees[b];
+      int node = 0, depth = 0, a = 0;
+      while (true) {
+        a = select_child(t, node, depth, invalid + (size_t)b * kA, gumbel + (size_t)b * kA, sr, ncons[b]);
+        const int child = t.c_index[(size_t)node * kA + a];
+        ++depth;
+        if (child == -1 || depth >= sr.D) break;
+        node = child;
+      }
+      parent[b] = node;
+      act[b] = a;
+      const int c = t.c_index[(size_t)node * kA + a];
+      nxt[b] = c == -1 ? sim + 1 : c;
+      std::memcpy(&pe[(size_t)b * kLat], &t.emb[(size_t)node * kLat], sizeof(float) * kLat);
+    }
+    recurrent(net, act.data(), pe.data(), B, rew.data(), disc.data(), lg.data(), val.data(), ne.data(), s);
+    for (int b = 0; b < B; ++b) {   // expand + backward
+      Tree& t = trees[b];
+      const int p = parent[b], a = act[b], nn = nxt[b];
+      t.update(nn, &lg[(size_t)b * kA], val[b], &ne[(size_t)b * kLat]);
+      t.c_index[(size_t)p * kA + a] = nn;
+      t.c_reward[(size_t)p * kA + a] = rew[b];
+      t.c_disc[(size_t)p * kA + a] = disc[b];
+      t.parent[nn] = p;
+      t.afp[nn] = a;
+      float leaf = t.value[nn];
+      int idx = nn;
+      while (idx != 0) {
+        const int pr = t.parent[idx], pa = t.afp[idx];
+        const int cnt = t.visits[pr];
+        const size_t e = (size_t)pr * kA + pa;
+        leaf = t.c_reward[e] + t.c_disc[e] * leaf;
+        t.value[pr] = (t.value[pr] * (float)cnt + leaf) / ((float)cnt + 1.0f);
+        t.visits[pr] = cnt + 1;
+        t.c_value[e] = t.value[idx];
+        t.c_visits[e] += 1;
+        idx = pr;
+      }
+    }
+  }
+  for (int b = 0; b < B; ++b) {   // final action + action_weights (policies.py tail)
+    const Tree& t = trees[b];
+    float cq[kA], sc[kA], z[kA];
+    completed_q(t, 0, cq);
+    int cv = 0;
+    for (int a = 0; a < kA; ++a) cv = std::max(cv, t.c_visits[a]);
+    const float* prior = &t.c_prior[0];
+    float pm = -kInf;
+    for (int a = 0; a < kA; ++a) pm = std::max(pm, prior[a]);
+    const bool* inv = invalid + (size_t)b * kA;
+    for (int a = 0; a < kA; ++a) {
+      const float sv = std::max(-1e9f, gumbel[(size_t)b * kA + a] + (prior[a] - pm) + cq[a]) +
+                       (t.c_visits[a] == cv ? 0.f : -kInf);
+      sc[a] = inv[a] ? -kInf : sv;
+      z[a] = prior[a] + cq[a];
+    }
+    action_out[b] = argmax(sc, kA);
+    float zm = -kInf;
+    for (int a = 0; a < kA; ++a) zm = std::max(zm, z[a]);
+    for (int a = 0; a < kA; ++a) z[a] = inv[a] ? kFMin : z[a] - zm;
+    softmax(z, weights_out + (size_t)b * kA, kA);
+    value_out[b] = t.value[0];
+  }
+}
+
+// counter-based Gumbel noise of the engine (csrc/rng.hpp, oracle/selfplay.py:gumbel_noise)
+inline uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+void gumbel_noise(uint64_t seed, int gid, int turn, float scale, float* out) {
+  for (int a = 0; a < kA; ++a) {
+    const uint64_t h = mix64(seed ^ mix64(((uint64_t)(uint32_t)gid << 32) | (uint32_t)turn) ^
+                             ((uint64_t)(a + 1) * 0xD6E8FEB86659FD93ull));
+    float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    u = std::max(u, kTiny);
+    out[a] = scale * (-std::log(-std::log(u)));
+  }
+}
+
+struct Lane {
+  muzcpu_det env;
+  int game = -1, t = 0;
+};
+
+}  // namespace
+
+extern "C" {
+
+typedef struct {   // optional trajectory records of muzcpu_selfplay (game_agent.py:158-169), [n][T]
+  int32_t* act;
+  float* val;
+  float* pol;      // [n][T][24]
+  float* mask;
+  int32_t* idx;    // [n]
+} muzcpu_traj;
+
+void* muzcpu_net_create(const char** names, const float** data, const int64_t* sizes, int count, int obs_channels) {
+  Net* n = new Net;
+  n->C = obs_channels;
+  for (int i = 0; i < count; ++i) n->p[names[i]] = std::vector<float>(data[i], data[i] + sizes[i]);
+  return n;
+}
+void muzcpu_net_destroy(void* n) { delete (Net*)n; }
+
+void muzcpu_env_reset(muzcpu_det* e, int P, const int* layout, int distance, int starting_player, int rules) {
+  env_reset(*e, P, layout, distance, starting_player, rules);
+}
+void muzcpu_valid_action(const muzcpu_det* e, uint8_t* out24) {
+  bool va[4][6];
+  valid_action(*e, va);
+  for (int i = 0; i < 24; ++i) out24[i] = va[i / 6][i % 6];
+}
+void muzcpu_env_step(muzcpu_det* e, int pin, int move, int* reward, int* done) { env_step(*e, pin, move, *reward, *done); }
+void muzcpu_no_step(muzcpu_det* e) { no_step(*e); }
+void muzcpu_encode(const muzcpu_det* e, float* out) { encode_board(*e, out); }
+
+void muzcpu_root(void* net, const float* obs, int B, float* logits, float* value, float* emb) {
+  Scratch s;
+  representation(*(Net*)net, obs, B, emb, s);
+  prediction(*(Net*)net, emb, B, logits, value, s);
+}
+void muzcpu_recurrent(void* net, const int* action, const float* emb, int B, float* reward, float* discount,
+                      float* logits, float* value, float* nxt) {
+  Scratch s;
+  recurrent(*(Net*)net, action, emb, B, reward, discount, logits, value, nxt, s);
+}
+
+// play_batch_of_games (game_agent.py:50-183) of n games on one thread, the oracle's loop exactly: returns the
+// number of batched turns; records into tr (if non-null).
+int muzcpu_selfplay(void* netp, int P, int rules, int n, int S, int D, int T, float temp, uint64_t seed,
+                    const muzcpu_traj* tr) {
+  const Net& net = *(Net*)netp;
+  const int C = 8 * P + 2;
+  const int layout[4] = {1, 1, 1, 1};
+  std::vector<muzcpu_det> envs(n);
+  for (auto& e : envs) env_reset(e, P, layout, 10, 0, rules);
+  Search sr;
+  sr.init(S, D);
+  Scratch s;
+  std::vector<Tree> trees(n);
+  std::vector<int> idx(n, 0);
+  int step = 0;
+  while (step < T) {
+    std::vector<int> search, nomove;
+    std::vector<uint8_t> inv;
+    for (int i = 0; i < n; ++i) {
+      if (envs[i].done) continue;
+      bool va[4][6];
+      valid_action(envs[i], va);
+      bool any = false;
+      for (int k = 0; k < 24; ++k) any = any || va[k / 6][k % 6];
+      if (any) {
+        search.push_back(i);
+        for (int k = 0; k < 24; ++k) inv.push_back(!va[k / 6][k % 6]);
+      } else {
+        nomove.push_back(i);
+      }
+    }
+    if (search.empty() && nomove.empty()) break;
+    const int B = (int)search.size();
+    if (B) {
+      std::vector<float> obs((size_t)B * C * kCells), lg((size_t)B * kA), v(B), e((size_t)B * kLat),
+          gum((size_t)B * kA), w((size_t)B * kA), rv(B);
+      std::vector<int> act(B);
+      for (int k = 0; k < B; ++k) {
+        encode_board(envs[search[k]], &obs[(size_t)k * C * kCells]);
+        gumbel_noise(seed, search[k], step, temp, &gum[(size_t)k * kA]);
+      }
+      representation(net, obs.data(), B, e.data(), s);
+      prediction(net, e.data(), B, lg.data(), v.data(), s);
+      std::vector<bool> invb(inv.begin(), inv.end());
+      std::unique_ptr<bool[]> ib(new bool[invb.size()]);
+      for (size_t q = 0; q < invb.size(); ++q) ib[q] = invb[q];
+      gumbel_search(net, sr, B, lg.data(), v.data(), e.data(), ib.get(), gum.data(), trees, act.data(), w.data(),
+                    rv.data(), s);
+      for (int k = 0; k < B; ++k) {
+        const int i = search[k], t = idx[i];
+        if (tr) {
+          tr->act[(size_t)i * T + t] = act[k];
+          tr->val[(size_t)i * T + t] = rv[k];
+          std::memcpy(&tr->pol[((size_t)i * T + t) * kA], &w[(size_t)k * kA], sizeof(float) * kA);
+          tr->mask[(size_t)i * T + t] = 1.f;
+        }
+        int r, d;
+        env_step(envs[i], act[k] / 6, act[k] % 6 + 1, r, d);
+        idx[i] = t + 1;
+      }
+    }
+    for (int i : nomove) {
+      const int t = idx[i];
+      if (tr) {
+        tr->act[(size_t)i * T + t] = -1;
+        tr->mask[(size_t)i * T + t] = 0.f;
+      }
+      no_step(envs[i]);
+      idx[i] = t + 1;
+    }
+    ++step;
+  }
+  if (tr)
+    for (int i = 0; i < n; ++i) tr->idx[i] = idx[i];
+  return step;
+}
+
+// The CPU baseline: `threads` OpenMP threads, each playing `lanes` concurrent games (refilled with the next
+// game when one ends or reaches max_steps) until `seconds` have passed.  Returns env-steps (turns of
+// unfinished games, game_agent.py:140), and the searches / finished games / elapsed seconds through the
+// pointers.
+int64_t muzcpu_bench(void* netp, int P, int rules, int lanes, int S, int D, int T, float temp, uint64_t seed,
+                     int threads, double seconds, int64_t* searches_out, int64_t* games_out, double* elapsed_out) {
+  const Net& net = *(Net*)netp;
+  const int C = 8 * P + 2;
+  const int layout[4] = {1, 1, 1, 1};
+  std::atomic<int> next_game{0};
+  std::atomic<int64_t> steps{0}, searches{0}, games{0};
+  const auto t0 = std::chrono::steady_clock::now();
+  auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+#pragma omp parallel num_threads(threads)
+  {
+    Search sr;
+    sr.init(S, D);
+    Scratch s;
+    std::vector<Tree> trees(lanes);
+    std::vector<Lane> L(lanes);
+    auto fresh = [&](Lane& l) {
+      env_reset(l.env, P, layout, 10, 0, rules);
+      l.game = next_game.fetch_add(1);
+      l.t = 0;
+    };
+    for (auto& l : L) fresh(l);
+    int64_t my_steps = 0, my_searches = 0, my_games = 0;
+    std::vector<float> obs((size_t)lanes * C * kCells), lg((size_t)lanes * kA), v(lanes), e((size_t)lanes * kLat),
+        gum((size_t)lanes * kA), w((size_t)lanes * kA), rv(lanes);
+    std::vector<int> act(lanes), search;
+    std::unique_ptr<bool[]> inv(new bool[(size_t)lanes * kA]);
+    while (elapsed() < seconds) {
+      search.clear();
+      for (int i = 0; i < lanes; ++i) {
+        Lane& l = L[i];
+        bool va[4][6];
+        valid_action(l.env, va);
+        bool any = false;
+        for (int k = 0; k < 24; ++k) any = any || va[k / 6][k % 6];
+        if (any) {
+          const int k = (int)search.size();
+          for (int q = 0; q < 24; ++q) inv[(size_t)k * kA + q] = !va[q / 6][q % 6];
+          encode_board(l.env, &obs[(size_t)k * C * kCells]);
+          gumbel_noise(seed, l.game, l.t, temp, &gum[(size_t)k * kA]);
+          search.push_back(i);
+        } else {
+          no_step(l.env);
+        }
+      }
+      const int B = (int)search.size();
+      if (B) {
+        representation(net, obs.data(), B, e.data(), s);
+        prediction(net, e.data(), B, lg.data(), v.data(), s);
+        gumbel_search(net, sr, B, lg.data(), v.data(), e.data(), inv.get(), gum.data(), trees, act.data(), w.data(),
+                      rv.data(), s);
+        for (int k = 0; k < B; ++k) {
+          int r, d;
+          env_step(L[search[k]].env, act[k] / 6, act[k] % 6 + 1, r, d);
+        }
+      }
+      my_searches += B;
+      my_steps += lanes;
+      for (auto& l : L) {
+        l.t += 1;
+        if (l.env.done || l.t >= T) {
+          ++my_games;
+          fresh(l);
+        }
+      }
+    }
+    steps += my_steps;
+    searches += my_searches;
+    games += my_games;
+  }
+  if (searches_out) *searches_out = searches.load();
+  if (games_out) *games_out = games.load();
+  if (elapsed_out) *elapsed_out = elapsed();
+  return steps.load();
+}
+
+}  // extern "C"

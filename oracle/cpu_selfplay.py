@@ -1,0 +1,172 @@
+"""ctypes binding of the C++ CPU restatement (oracle/cpu_selfplay.cpp -> oracle/libmuzcpu.so).
+
+TEST INFRASTRUCTURE / CPU BASELINE ONLY: used by tests/test_cpu_baseline.py (checked against the NumPy
+oracle) and by bench.py's cpu_baseline leg (the reference algorithm timed on the host cores,
+at 1 core and at all cores).  The product path never loads it."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmuzcpu.so")
+
+R_TEAMS, R_FREE_PIN, R_CIRCULAR, R_START_BLOCK, R_JUMP_GOAL, R_FRIENDLY, R_START_ON_1, R_BONUS_6, \
+    R_MUST_TRAVERSE = (1 << i for i in range(9))
+_FLAGS = dict(enable_teams=R_TEAMS, enable_initial_free_pin=R_FREE_PIN, enable_circular_board=R_CIRCULAR,
+              enable_start_blocking=R_START_BLOCK, enable_jump_in_goal_area=R_JUMP_GOAL,
+              enable_friendly_fire=R_FRIENDLY, enable_start_on_1=R_START_ON_1, enable_bonus_turn_on_6=R_BONUS_6,
+              must_traverse_start=R_MUST_TRAVERSE)
+
+
+class Det(ctypes.Structure):
+    _fields_ = [("board", ctypes.c_int8 * 56), ("pins", ctypes.c_int8 * 16), ("action_set", ctypes.c_int8 * 24),
+                ("start", ctypes.c_int8 * 4), ("target", ctypes.c_int8 * 4), ("goal", ctypes.c_int8 * 16),
+                ("current_player", ctypes.c_int32), ("reward", ctypes.c_int32), ("done", ctypes.c_int32),
+                ("num_players", ctypes.c_int32), ("board_size", ctypes.c_int32), ("total", ctypes.c_int32),
+                ("rules", ctypes.c_int32)]
+
+
+class Traj(ctypes.Structure):
+    _fields_ = [("act", ctypes.c_void_p), ("val", ctypes.c_void_p), ("pol", ctypes.c_void_p),
+                ("mask", ctypes.c_void_p), ("idx", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: make -C oracle")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, ip, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.muzcpu_net_create.restype = vp
+        L.muzcpu_net_create.argtypes = [vp, vp, vp, ip, ip]
+        L.muzcpu_net_destroy.argtypes = [vp]
+        L.muzcpu_env_reset.argtypes = [vp, ip, vp, ip, ip, ip]
+        L.muzcpu_valid_action.argtypes = [vp, vp]
+        L.muzcpu_env_step.argtypes = [vp, ip, ip, vp, vp]
+        L.muzcpu_no_step.argtypes = [vp]
+        L.muzcpu_encode.argtypes = [vp, vp]
+        L.muzcpu_root.argtypes = [vp, vp, ip, vp, vp, vp]
+        L.muzcpu_recurrent.argtypes = [vp, vp, vp, ip, vp, vp, vp, vp, vp]
+        L.muzcpu_selfplay.restype = ip
+        L.muzcpu_selfplay.argtypes = [vp, ip, ip, ip, ip, ip, ip, fp, ctypes.c_uint64, vp]
+        L.muzcpu_bench.restype = ctypes.c_int64
+        L.muzcpu_bench.argtypes = [vp, ip, ip, ip, ip, ip, ip, fp, ctypes.c_uint64, ip, ctypes.c_double, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def rule_bits(**rules) -> int:
+    from oracle import detmadn as dm
+    r = dict(dm.DEFAULT_RULES)
+    r.update(rules)
+    return sum(bit for k, bit in _FLAGS.items() if r[k])
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class CpuNet:
+    """Flat Flax-path parameter dict -> the C++ network (copied once)."""
+
+    def __init__(self, params: dict, obs_channels: int):
+        L = load()
+        self._keep = {k: np.ascontiguousarray(v, np.float32) for k, v in params.items()}
+        names = [k.encode() for k in self._keep]
+        n = len(names)
+        cn = (ctypes.c_char_p * n)(*names)
+        ptrs = (ctypes.c_void_p * n)(*[v.ctypes.data for v in self._keep.values()])
+        sizes = (ctypes.c_int64 * n)(*[v.size for v in self._keep.values()])
+        self.h = L.muzcpu_net_create(cn, ptrs, sizes, n, obs_channels)
+        self.C = obs_channels
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.muzcpu_net_destroy(self.h)
+            self.h = None
+
+    def root(self, obs):
+        obs = np.ascontiguousarray(obs, np.float32)
+        B = obs.shape[0]
+        lg, v, e = np.empty((B, 24), np.float32), np.empty(B, np.float32), np.empty((B, 256), np.float32)
+        load().muzcpu_root(self.h, _p(obs), B, _p(lg), _p(v), _p(e))
+        return lg, v, e
+
+    def recurrent(self, action, emb):
+        a = np.ascontiguousarray(action, np.int32)
+        emb = np.ascontiguousarray(emb, np.float32)
+        B = emb.shape[0]
+        r, d, v = (np.empty(B, np.float32) for _ in range(3))
+        lg, nx = np.empty((B, 24), np.float32), np.empty((B, 256), np.float32)
+        load().muzcpu_recurrent(self.h, _p(a), _p(emb), B, _p(r), _p(d), _p(lg), _p(v), _p(nx))
+        return r, d, lg, v, nx
+
+    def selfplay(self, P, rules, n, S, D, T, temp, seed):
+        """play_batch_of_games of n games (one thread): (buffers act / val / pol / mask / idx, turns)."""
+        buf = {"act": np.zeros((n, T), np.int32), "val": np.zeros((n, T), np.float32),
+               "pol": np.zeros((n, T, 24), np.float32), "mask": np.zeros((n, T), np.float32),
+               "idx": np.zeros(n, np.int32)}
+        tr = Traj(*[buf[k].ctypes.data for k in ("act", "val", "pol", "mask", "idx")])
+        turns = load().muzcpu_selfplay(self.h, P, rule_bits(**rules), n, S, D, T, temp, seed, ctypes.byref(tr))
+        return buf, turns
+
+    def bench(self, P, rules, lanes, S, D, T, temp, seed, threads, seconds):
+        """Streamed self-play on `threads` cores for `seconds`: dict(env_steps, searches, games, elapsed)."""
+        s, g, t = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+        steps = load().muzcpu_bench(self.h, P, rule_bits(**rules), lanes, S, D, T, temp, seed, threads, seconds,
+                                    ctypes.byref(s), ctypes.byref(g), ctypes.byref(t))
+        return dict(env_steps=int(steps), searches=int(s.value), games=int(g.value), elapsed=float(t.value))
+
+
+def env_from_oracle(e) -> Det:
+    """oracle/detmadn.State -> the C++ state struct."""
+    d = Det()
+    P = e.num_players
+    d.board[:] = [int(x) for x in e.board]
+    pins = -np.ones(16, np.int8)
+    pins[:P * 4] = np.asarray(e.pins, np.int8).ravel()
+    d.pins[:] = [int(x) for x in pins]
+    aset = np.zeros(24, np.int8)
+    aset[:P * 6] = np.asarray(e.action_set, np.int8).ravel()
+    d.action_set[:] = [int(x) for x in aset]
+    st, tg, gl = np.zeros(4, np.int8), np.zeros(4, np.int8), np.zeros(16, np.int8)
+    st[:P], tg[:P], gl[:P * 4] = e.start, e.target, np.asarray(e.goal).ravel()
+    d.start[:], d.target[:], d.goal[:] = [int(x) for x in st], [int(x) for x in tg], [int(x) for x in gl]
+    d.current_player, d.reward, d.done = int(e.current_player), int(e.reward), int(e.done)
+    d.num_players, d.board_size, d.total = P, e.board_size, e.total_board_size
+    d.rules = rule_bits(**e.rules)
+    return d
+
+
+def valid_action(d: Det) -> np.ndarray:
+    out = np.zeros(24, np.uint8)
+    load().muzcpu_valid_action(ctypes.byref(d), _p(out))
+    return out.astype(bool).reshape(4, 6)
+
+
+def env_step(d: Det, pin, move):
+    r, dn = ctypes.c_int(), ctypes.c_int()
+    load().muzcpu_env_step(ctypes.byref(d), int(pin), int(move), ctypes.byref(r), ctypes.byref(dn))
+    return r.value, bool(dn.value)
+
+
+def no_step(d: Det):
+    load().muzcpu_no_step(ctypes.byref(d))
+
+
+def encode(d: Det) -> np.ndarray:
+    C = 8 * d.num_players + 2
+    out = np.zeros((C, 56), np.float32)
+    load().muzcpu_encode(ctypes.byref(d), _p(out))
+    return out
+
+
+def pins(d: Det) -> np.ndarray:
+    return np.array(d.pins[:d.num_players * 4], np.int8).reshape(d.num_players, 4)
