@@ -70,7 +70,7 @@ def parse():
                     help="det: games per step streamed through the --batch lanes (default 32 x batch; 0 = one "
                          "batch of --batch games, the reference's play_n_games_v3 call)")
     ap.add_argument("--train-steps", type=int, default=2500, help="train workload: learner steps per iteration")
-    ap.add_argument("--workload", choices=("det", "classic", "dog", "train", "selftest"), default="det",
+    ap.add_argument("--workload", choices=("det", "classic", "dog", "train", "env", "selftest"), default="det",
                     help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
     ap.add_argument("--split", action="store_true",
                     help="strong scaling (SURVEY §8e): --batch is the WHOLE job's batch, split evenly over the ranks "
@@ -456,6 +456,90 @@ def run_train(args):
         dist.destroy_process_group()
 
 
+ENV_ROUNDS_PER_STEP = 100      # --workload env: one bench step = 100 random-play env rounds (one launch each)
+ENV_PREROLL = 300              # rounds played before warm-up: games spread over 0..300 plies (SURVEY §8(d)(b'))
+
+
+def env_bytes_per_step(P):
+    """Algorithmic HBM bytes of one env-step of muz_detmadn_random_round: the SoA state read and
+    written (board 56 + pins 4P + current player, reward, done + action set 6P), the legal mask read and
+    written, reward and done written, and the int8 observation (8P+2) x 56 written.  2p: 1176 B."""
+    state = 56 + 4 * P + 3 + 6 * P
+    return 2 * state + 2 * 4 + 2 + (8 * P + 2) * 56
+
+
+def run_env(args):
+    """SURVEY §8(d)(b'): the env kernels alone -- step + legal + encode of det-MADN 2p over the batch -- as the
+    fused random-play round (muz_detmadn_random_round), on a mid-game state distribution (ENV_PREROLL rounds
+    of seeded random legal play first; finished games restart in place).  One bench step = 100 rounds."""
+    import torch
+    rank, world, dist, device = setup(args)
+    from exploring_muzero_on_dog_amd import detmadn as E
+    B, R = args.batch, ENV_ROUNDS_PER_STEP
+    env = E.env_reset(B, num_players=PLAYERS, device=device, **E.SELFPLAY_RULES)
+    legal = E.legal_bits(env)
+    C = E.num_channels(PLAYERS)
+    obs = torch.empty((B, C, E.CELLS), dtype=torch.int8, device=device)
+    reward = torch.empty(B, dtype=torch.int8, device=device)
+    done = torch.empty(B, dtype=torch.uint8, device=device)
+    seed = 77 + 1000 * rank
+    turn = [0]
+
+    def rounds(k, ev=None):
+        for i in range(R):
+            if ev is not None:
+                ev[2 * (k * R + i)].record()
+            E.random_round(env, legal, seed, turn[0], obs=obs, reward=reward, done=done)
+            if ev is not None:
+                ev[2 * (k * R + i) + 1].record()
+            turn[0] += 1
+
+    for _ in range(ENV_PREROLL // R):
+        rounds(0)
+    for _ in range(args.warmup):
+        rounds(0)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * R * args.steps)]
+    elapsed = timed_region(dist, lambda k: rounds(k, ev), args.steps)
+    launch_ms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(R * args.steps))
+    (steps_done, lms), elapsed = sum_max(dist, device, [B * R * args.steps, launch_ms], elapsed)
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    avg_ms = lms / (R * args.steps * world)
+    per = env_bytes_per_step(PLAYERS)
+    achieved = B * per / (avg_ms * 1e-3) / 1e9
+    out = {
+        "metric": "env-only steps/sec (step + legal + encode), det-MADN 2p random legal play (SURVEY 8(d)(b'))",
+        "value": round(steps_done / elapsed, 1), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
+        "scaling": "strong" if args.split else "weak", "vs_baseline": None, "dtype": "int8",
+        "data": "synthetic (seeded random legal play, counter RNG)",
+        "config": {"workload": f"det-MADN {PLAYERS}p env rounds: {B} games/GPU, {R} rounds per step, each one "
+                               f"muz_detmadn_random_round launch (legal -> random legal action -> env_step / no_step "
+                               f"-> reset finished -> next legal + int8 obs), after {ENV_PREROLL} pre-roll rounds",
+                   "games_per_gpu": B, "rounds_per_step": R, "parallelism": parallelism(args, world)},
+        "roofline": {"bound": "hbm", "kernel": "k_det_round", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "avg_launch_ms": round(avg_ms, 5),
+                     "bytes_per_env_step": per, "bytes_per_launch": B * per, "traffic": None},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_selfplay as CS
+        cores, aff = cpu_cores()
+        half = min(args.cpu_seconds, 20.0) / 2
+        s1, t1 = CS.env_bench(PLAYERS, E.SELFPLAY_RULES, 1024, 1, 1, half)
+        sn, tn = CS.env_bench(PLAYERS, E.SELFPLAY_RULES, 1024, 1, cores, half)
+        out["cpu_baseline"] = {"value": round(sn / tn, 1), "unit": "env_steps/s", "cores": cores, "kind": "port",
+                               "value_1core": round(s1 / t1, 1), "value_allcores": round(sn / tn, 1),
+                               "cores_affinity": aff,
+                               "sample": f"C++ restatement (oracle/cpu_selfplay.cpp muzcpu_env_bench): 1024 games per "
+                                         f"thread of random-play rounds incl. fp32 encode, {half:.0f} s at 1 thread "
+                                         f"and {half:.0f} s at {cores} threads"}
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def run_selftest(args):
     """CPU rehearsal of the multi-rank plumbing (launcher, barrier + timed region, sum / max reduction,
     rank-0 JSON) without a GPU: each rank 'processes' (rank + 1) x batch units per step.  Only for
@@ -566,7 +650,7 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
-    return {"train": run_train, "dog": run_dog, "classic": run_classic, "det": run_det,
+    return {"train": run_train, "dog": run_dog, "classic": run_classic, "det": run_det, "env": run_env,
             "selftest": run_selftest}[args.workload](args)
 
 

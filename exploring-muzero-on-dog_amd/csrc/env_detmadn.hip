@@ -2,6 +2,7 @@
 // One board per lane; 256-lane workgroups; the lane's board is staged in LDS.
 #include "detmadn.hpp"
 #include "host_consts.hpp"
+#include "rng.hpp"
 
 namespace muz {
 
@@ -96,6 +97,117 @@ __global__ __launch_bounds__(64) void k_det_encode(DetConsts c, muz_detmadn_soa 
   for (int ch = 0; ch < C; ++ch) out[ch * kCells + w] = (T)det_encode_value(c, s, ch, w, owner);
 }
 
+
+// ---- random-play env round (SURVEY §8(d)(b'): the env-only micro-benchmark, and a random-play actor) -----
+// One env-step per game: the k-th legal action of the mask left by the previous round (k = floor(u * count),
+// u from the counter RNG of (seed ^ kDetRandomStream, game, turn)), env_step -- or no_step when nothing is
+// legal --, an in-place env_reset of a game that finished, the next legal mask, and the int8 observation of
+// the state the next round acts on (encode_board, deterministic_madn.py:395-438).
+// Phase 1 is lane per game (256 games per workgroup; SoA loads / stores coalesced) and stages per game, in
+// LDS, each rolled cell's owner relative to the current player (rel = (owner - cp) mod P, 0xFF empty) and
+// the constant channels (home counts, action sets).  Phase 2 writes the workgroup's 256 x C x 56
+// contiguous observation bytes as 8-byte chunks -- 56 = 7 x 8, so a chunk never straddles two channels --
+// with consecutive threads on consecutive chunks (fully coalesced 512-byte wave stores).
+constexpr int kRoundBlock = 256;
+constexpr unsigned long long kDetRandomStream = 0xD37A11D0ull;
+constexpr int kEncStride = 96;   // per game: rel[56] + constant channel values at [56 + ch]
+
+__global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detmadn_soa st, uint32_t* legal,
+                                                           unsigned long long seed, int turn, int8_t* obs,
+                                                           int8_t* reward, uint8_t* done, int n) {
+  __shared__ int8_t sboard[kCells * kRoundBlock];
+  __shared__ __attribute__((aligned(16))) uint8_t senc[kRoundBlock * kEncStride];
+  const int g = blockIdx.x * kRoundBlock + threadIdx.x;
+  const int P = c.P, C = 8 * P + 2;
+  if (g < n) {
+    BoardView b{sboard + threadIdx.x, kRoundBlock};
+    DetLane s;
+    det_load(c, st, g, s, b);
+    const uint32_t lb = legal[g];
+    const int cnt = __popc(lb);
+    int r = 0;
+    if (cnt == 0) {
+      det_nostep(c, s);
+    } else {
+      const float u = u24(mix64(game_key(seed ^ kDetRandomStream, g, turn)));
+      int k = (int)(u * (float)cnt);
+      k = k >= cnt ? cnt - 1 : k;
+      uint32_t x = lb;
+      for (int j = 0; j < k; ++j) x &= x - 1;   // drop the k lowest set bits
+      const int a = __ffs(x) - 1;
+      r = det_step(c, s, b, a / 6, a % 6 + 1);
+    }
+    const int fin = s.done;
+    if (fin) {   // env_reset in place with the batch's rules (deterministic_madn.py:42-120)
+      const bool fp = has(c.flags, R_FREE_PIN);
+      for (int cell = 0; cell < kCells; ++cell) b.set(cell, -1);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s.pins[j] = (fp && (j & 3) == 0 && (j >> 2) < P) ? c.start[j >> 2] : -1;
+#pragma unroll
+      for (int j = 0; j < 24; ++j) s.aset[j] = j < 6 * P ? 4 : 0;
+      if (fp)
+        for (int p = 0; p < P; ++p) b.set(c.start[p], p);
+      s.cp = c.starting_player;
+      s.done = 0;
+      s.reward = 0;
+    }
+    det_store(c, st, g, s, b, true);
+    legal[g] = det_legal(c, s, b);
+    if (reward) reward[g] = (int8_t)r;
+    if (done) done[g] = (uint8_t)fin;
+    if (obs) {   // stage this game's encode inputs
+      uint8_t* e = senc + threadIdx.x * kEncStride;
+      uint32_t wv = 0;
+      for (int w = 0; w < kCells; ++w) {
+        const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
+        const int v = b.at(src);
+        const uint32_t rel = v < 0 ? 0xFFu : (uint32_t)((v - s.cp + P) % P);
+        wv |= rel << (8 * (w & 3));
+        if ((w & 3) == 3) {
+          *reinterpret_cast<uint32_t*>(e + (w & ~3)) = wv;
+          wv = 0;
+        }
+      }
+      auto none = [](int) { return 0; };
+      for (int ch = P + 2; ch < C; ++ch) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
+    }
+  }
+  if (!obs) return;
+  __syncthreads();
+  const int g0 = blockIdx.x * kRoundBlock;
+  const int games = min(kRoundBlock, n - g0);
+  const int per = 7 * C;
+  const bool teams = has(c.flags, R_TEAMS);
+  uint2* out = reinterpret_cast<uint2*>(obs + (size_t)g0 * C * kCells);
+  for (int q = threadIdx.x; q < games * per; q += kRoundBlock) {
+    const int gl = q / per, rem = q - gl * per;
+    const int ch = rem / 7, w0 = (rem - ch * 7) * 8;
+    const uint8_t* e = senc + gl * kEncStride;
+    uint32_t word[2];
+    if (ch < P + 2) {
+      const uint2 rw = *reinterpret_cast<const uint2*>(e + w0);
+      const uint32_t rr[2] = {rw.x, rw.y};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t rel = (rr[h] >> (8 * j)) & 0xFFu;
+          bool on;
+          if (ch < P) on = rel == (uint32_t)ch;                                            // one-hot player
+          else if (ch == P) on = teams ? (rel == 0u || rel == 2u) : rel == 0u;              // own team
+          else on = teams ? (rel == 1u || rel == 3u) : (rel >= 1u && rel < (uint32_t)P);   // opponents
+          o |= (uint32_t)on << (8 * j);
+        }
+        word[h] = o;
+      }
+    } else {
+      word[0] = word[1] = (uint32_t)e[kCells + ch] * 0x01010101u;
+    }
+    out[q] = make_uint2(word[0], word[1]);
+  }
+}
+
 }  // namespace muz
 
 using namespace muz;
@@ -176,6 +288,18 @@ int muz_detmadn_encode_i8(const muz_rules* rules, muz_detmadn_soa st, int8_t* ob
   MUZ_HOST_CHECK(n >= 0 && st.stride >= n && obs);
   if (n == 0) return MUZ_OK;
   k_det_encode<int8_t><<<n, 64, 0, (hipStream_t)stream>>>(c, st, obs, n);
+  return muz_last_launch_error();
+}
+
+int muz_detmadn_random_round(const muz_rules* rules, muz_detmadn_soa st, uint32_t* legal_bits, uint64_t seed,
+                             int32_t turn, int8_t* obs, int8_t* reward, uint8_t* done, int32_t n, void* stream) {
+  DetConsts c;
+  int rc = make_det_consts(rules, &c);
+  if (rc) return rc;
+  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && legal_bits);
+  if (n == 0) return MUZ_OK;
+  k_det_round<<<nblocks(n, kRoundBlock), kRoundBlock, 0, (hipStream_t)stream>>>(c, st, legal_bits, seed, turn, obs,
+                                                                                reward, done, n);
   return muz_last_launch_error();
 }
 

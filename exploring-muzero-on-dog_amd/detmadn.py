@@ -13,6 +13,7 @@ Reference entry points mirrored (file:line in the reference):
   no_step              MADN/deterministic_madn.py:283-297
   encode_board         MADN/deterministic_madn.py:395-438
   map_action           MADN/deterministic_madn.py:469-479
+  random_round         game_agent.py:84-119's per-turn env work with a uniform random legal policy
   set_pins_on_board    MADN/deterministic_madn.py:259-271
 """
 from __future__ import annotations
@@ -233,6 +234,17 @@ def encode_board(env: DetMADNState, dtype=torch.float32) -> torch.Tensor:
         raise TypeError(dtype)
     _L.check(rc, "muz_detmadn_encode")
     return out
+
+
+def random_round(env: DetMADNState, legal: torch.Tensor, seed: int, turn: int, obs: torch.Tensor | None = None,
+                 reward: torch.Tensor | None = None, done: torch.Tensor | None = None):
+    """One env-step of uniform random legal play for every game (muz_detmadn_random_round): the k-th legal
+    action of ``legal`` (int32 [B], updated in place to the next mask), env_step / no_step, in-place reset of
+    finished games, and encode_board of the next state into ``obs`` (int8 [B, 8P+2, 56]) when given."""
+    _L.check(_L.load().muz_detmadn_random_round(env.rules, env.soa(), _L.ptr(legal), int(seed) & ((1 << 64) - 1),
+                                                int(turn), _L.ptr(obs), _L.ptr(reward), _L.ptr(done), env.batch,
+                                                _L.stream_ptr()), "muz_detmadn_random_round")
+    return env
 
 
 def map_action(idx):

@@ -189,6 +189,8 @@ SIGNATURES = {
     "muz_detmadn_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
+    "muz_detmadn_random_round": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_uint64, ctypes.c_int32,
+                                                vp, vp, vp, ctypes.c_int32, vp]),
     "muz_dog_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, ctypes.c_int32, vp]),
     "muz_dog_legal": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_int32, vp]),
     "muz_dog_step": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_uint64, vp, vp, ctypes.c_int32,

@@ -112,6 +112,16 @@ int muz_detmadn_nostep(const muz_rules* rules, muz_detmadn_soa state, int8_t* re
 int muz_detmadn_encode_f32(const muz_rules* rules, muz_detmadn_soa state, float* obs, int32_t n, void* stream);
 int muz_detmadn_encode_i8(const muz_rules* rules, muz_detmadn_soa state, int8_t* obs, int32_t n, void* stream);
 
+/* One env-step of uniform random legal play for every game (the env-only micro-benchmark of SURVEY §8(d)(b'),
+ * and a random-play actor): legal_bits holds each game's mask on entry (muz_detmadn_legal before the first
+ * round) and the next round's mask on exit; the action is the k-th legal one, k = floor(u * count), u =
+ * (mix64(game_key(seed ^ 0xD37A11D0, g, turn)) >> 40) / 2^24; no_step when nothing is legal; a game that
+ * finishes is reset in place (done[g] = 1 for that round).  obs (nullable) receives encode_board of the state
+ * the next round acts on, int8 [n][8P+2][56].  Replaces the vmapped valid_action -> env_step / no_step ->
+ * encode_board sequence of MuZero_det_MADN/game_agent.py:84-119 (MADN/deterministic_madn.py:170-438). */
+int muz_detmadn_random_round(const muz_rules* rules, muz_detmadn_soa state, uint32_t* legal_bits, uint64_t seed,
+                             int32_t turn, int8_t* obs, int8_t* reward, uint8_t* done, int32_t n, void* stream);
+
 
 /* ---- classic MADN environment (MADN/classic_madn.py) -------------------------------------- */
 

@@ -940,4 +940,48 @@ int64_t muzcpu_bench(void* netp, int P, int rules, int lanes, int S, int D, int 
   return steps.load();
 }
 
+// The env-only CPU baseline (SURVEY §8(d)(b')): `threads` threads each advance `lanes` games by rounds of
+// uniform random legal play (valid_action -> k-th legal action -> env_step / no_step -> reset of finished
+// games -> encode_board) for `seconds`; returns env-steps.
+int64_t muzcpu_env_bench(int P, int rules, int lanes, uint64_t seed, int threads, double seconds, double* elapsed_out) {
+  const int layout[4] = {1, 1, 1, 1};
+  const int C = 8 * P + 2;
+  std::atomic<int64_t> steps{0};
+  const auto t0 = std::chrono::steady_clock::now();
+  auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+#pragma omp parallel num_threads(threads)
+  {
+    const int tid = omp_get_thread_num();
+    std::vector<muzcpu_det> envs(lanes);
+    for (auto& e : envs) env_reset(e, P, layout, 10, 0, rules);
+    std::vector<float> obs((size_t)C * kCells);
+    int64_t mine = 0;
+    for (int turn = 0; elapsed() < seconds; ++turn) {
+      for (int i = 0; i < lanes; ++i) {
+        muzcpu_det& e = envs[i];
+        bool va[4][6];
+        valid_action(e, va);
+        int legal[24], cnt = 0;
+        for (int k = 0; k < 24; ++k)
+          if (va[k / 6][k % 6]) legal[cnt++] = k;
+        if (cnt == 0) {
+          no_step(e);
+        } else {
+          const uint64_t h = mix64((seed ^ 0xD37A11D0ull) ^ mix64(((uint64_t)(uint32_t)(tid * lanes + i) << 32) | (uint32_t)turn));
+          const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+          const int k = std::min((int)(u * (float)cnt), cnt - 1);
+          int r, d;
+          env_step(e, legal[k] / 6, legal[k] % 6 + 1, r, d);
+        }
+        if (e.done) env_reset(e, P, layout, 10, 0, rules);
+        encode_board(e, obs.data());
+      }
+      mine += lanes;
+    }
+    steps += mine;
+  }
+  if (elapsed_out) *elapsed_out = elapsed();
+  return steps.load();
+}
+
 }  // extern "C"

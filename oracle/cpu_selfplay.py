@@ -58,6 +58,8 @@ def load():
         L.muzcpu_selfplay.argtypes = [vp, ip, ip, ip, ip, ip, ip, fp, ctypes.c_uint64, vp]
         L.muzcpu_bench.restype = ctypes.c_int64
         L.muzcpu_bench.argtypes = [vp, ip, ip, ip, ip, ip, ip, fp, ctypes.c_uint64, ip, ctypes.c_double, vp, vp, vp]
+        L.muzcpu_env_bench.restype = ctypes.c_int64
+        L.muzcpu_env_bench.argtypes = [ip, ip, ip, ctypes.c_uint64, ip, ctypes.c_double, vp]
         _lib = L
     return _lib
 
@@ -123,6 +125,13 @@ class CpuNet:
         steps = load().muzcpu_bench(self.h, P, rule_bits(**rules), lanes, S, D, T, temp, seed, threads, seconds,
                                     ctypes.byref(s), ctypes.byref(g), ctypes.byref(t))
         return dict(env_steps=int(steps), searches=int(s.value), games=int(g.value), elapsed=float(t.value))
+
+
+def env_bench(P, rules, lanes, seed, threads, seconds):
+    """Random-play env rounds on `threads` host cores for `seconds`: (env_steps, elapsed)."""
+    t = ctypes.c_double()
+    steps = load().muzcpu_env_bench(P, rule_bits(**rules), lanes, seed, threads, seconds, ctypes.byref(t))
+    return int(steps), float(t.value)
 
 
 def env_from_oracle(e) -> Det:
