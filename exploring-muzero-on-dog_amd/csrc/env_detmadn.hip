@@ -208,6 +208,109 @@ __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detm
   }
 }
 
+// ---- evaluation agents (MuZero_det_MADN/evaluate_agent.py) --------------------------------------------
+// mode 0: the random agent (do_random, 770-775: jax.random.categorical over 0 / -1e9 logits of the legal
+// actions); mode 1: the rule-based agent (do_rule_based, 777-864): per action pin*6 + m a score
+//   base  = abundance[a // 4]   (jnp.repeat(counts / max(sum counts, 1), 4): indexed by a // 4, as written)
+//   + goal_bonus  if the pin (not yet in the goal area) lands on one of the player's goal cells
+//   + out_many / out_few (>= 2 / < 2 pins at home) if a home pin moves to the start
+//   + hit_bonus   if the pin moves onto an opponent pin (teams: the partner is no opponent)
+// with landing cells from cur + m, m = 0..5 (jnp.arange(6), as written) and the UNSUBSTITUTED current
+// player; illegal actions -inf; action = argmax(score / temperature + gumbel) -- jax.random.categorical,
+// the Gumbel draw from the engine's counter RNG (seed ^ kPolicyStream, game, turn, action).  -1 when
+// nothing is legal.
+constexpr unsigned long long kPolicyStream = 0x9011C7A6E47ull;
+
+__global__ __launch_bounds__(256) void k_det_policy(DetConsts c, muz_detmadn_soa st, const uint32_t* legal, int mode,
+                                                    muz_rule_agent ag, unsigned long long seed, int turn,
+                                                    const int32_t* game_id, int32_t* action, int n) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= n) return;
+  const int S = st.stride;
+  const uint32_t lb = legal[g];
+  if (lb == 0u) {
+    action[g] = -1;
+    return;
+  }
+  const int gid = game_id ? game_id[g] : g;
+  const unsigned long long key = game_key(seed ^ kPolicyStream, gid, turn);
+  auto gum = [&](int a) {
+    const float u = fmaxf(u24(mix64(key ^ (unsigned long long)(a + 1) * 0xD6E8FEB86659FD93ull)), kTinyF);
+    return -logf(-logf(u));
+  };
+  int best = -1;
+  float bv = -INFINITY;
+  if (mode == 0) {
+    for (int a = 0; a < 24; ++a) {
+      const float l = ((lb >> a) & 1u) ? 0.0f : -1e9f;
+      const float v = l + gum(a);
+      if (v > bv) {
+        bv = v;
+        best = a;
+      }
+    }
+    action[g] = best;
+    return;
+  }
+  const int P = c.P, cp = st.current_player[g];
+  const int mt = has(c.flags, R_MUST_TRAVERSE) ? 1 : 0;
+  const int tgt = cst(c.target, cp), start = cst(c.start, cp);
+  int pins[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) pins[j] = j < P * 4 ? st.pins[min(j, P * 4 - 1) * S + g] : -1;
+  int home = 0;
+  for (int k = 0; k < 4; ++k) home += rsel(pins, cp * 4 + k) < 0 ? 1 : 0;
+  int counts[6];
+  int total = 0;
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    counts[m] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) counts[m] += (lb >> (i * 6 + m)) & 1u;
+    total += counts[m];
+  }
+  const float denom = fmaxf((float)total, 1.0f);
+  const int partner = has(c.flags, R_TEAMS) ? (cp + 2) % 4 : -1;
+  for (int i = 0; i < 4; ++i) {
+    const int cur = rsel(pins, cp * 4 + i);
+    for (int m = 0; m < 6; ++m) {
+      const int a = i * 6 + m;
+      if (((lb >> a) & 1u) == 0u) continue;
+      const int moved = cur + m;
+      const int x = moved - tgt - mt;
+      int np;
+      if (cur < 0) np = start;
+      else if (cur >= kTrack) np = moved;
+      else if (4 >= x && x > 0 && cur <= tgt) np = goal_of(c, cp, jidx(x - 1, 4));
+      else np = fmodp(moved, kTrack);
+      const int ab = a >> 2;   // jnp.repeat(action_abundance, 4)[a]
+      int cab = 0;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) cab = q == ab ? counts[q] : cab;
+      const float base = (float)cab / denom;
+      bool in_goal = false;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) in_goal |= np == goal_of(c, cp, h);
+      const float gb = (in_goal && cur < kTrack) ? ag.goal_bonus : 0.0f;
+      const float ob = (cur < 0 && np == start) ? (home >= 2 ? ag.out_many : ag.out_few) : 0.0f;
+      bool hit = false;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int p = j >> 2;
+        hit |= p < P && p != cp && p != partner && pins[j] == np;
+      }
+      const float hb = (np != cur && hit) ? ag.hit_bonus : 0.0f;
+      const float score = ((base + gb) + ob) + hb;
+      const float v = score / ag.temperature + gum(a);
+      if (v > bv) {
+        bv = v;
+        best = a;
+      }
+    }
+  }
+  action[g] = best;
+}
+
 }  // namespace muz
 
 using namespace muz;
@@ -300,6 +403,21 @@ int muz_detmadn_random_round(const muz_rules* rules, muz_detmadn_soa st, uint32_
   if (n == 0) return MUZ_OK;
   k_det_round<<<nblocks(n, kRoundBlock), kRoundBlock, 0, (hipStream_t)stream>>>(c, st, legal_bits, seed, turn, obs,
                                                                                 reward, done, n);
+  return muz_last_launch_error();
+}
+
+int muz_detmadn_policy_action(const muz_rules* rules, muz_detmadn_soa st, const uint32_t* legal_bits, int32_t mode,
+                              const muz_rule_agent* agent, uint64_t seed, int32_t turn, const int32_t* game_id,
+                              int32_t* action, int32_t n, void* stream) {
+  DetConsts c;
+  int rc = make_det_consts(rules, &c);
+  if (rc) return rc;
+  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && legal_bits && action && (mode == 0 || mode == 1));
+  MUZ_HOST_CHECK(mode == 0 || (agent && agent->temperature > 0.f));
+  if (n == 0) return MUZ_OK;
+  const muz_rule_agent ag = agent ? *agent : muz_rule_agent{1.f, 0.f, 0.f, 0.f, 0.f};
+  k_det_policy<<<nblocks(n, 256), 256, 0, (hipStream_t)stream>>>(c, st, legal_bits, mode, ag, seed, turn, game_id,
+                                                                 action, n);
   return muz_last_launch_error();
 }
 

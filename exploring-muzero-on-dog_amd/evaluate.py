@@ -6,6 +6,12 @@
                                 474-646); no-move turns apply no_step; wins are counted at seat 0
                                 (manual_get_winner 16-45); at most 2000 turns.
   compare_agents_statistically  648-713: both agents against random opponents, two-proportion z-test.
+  evaluate_agent_parallel       253-311 + play_n_games_for_eval_jitted / play_eval_loop_jitted 715-960: four
+                                seats, each a MuZero agent (a DeviceNet, or None = randomly initialised
+                                params), 'rule_based_agent' or 'random_agent'; batch_size games per starting
+                                player; winners and calculate_progress (129-195) per starting player.
+  policy_action                 the random agent (770-775) and the rule-based agent (777-864) as one device
+                                kernel (muz_detmadn_policy_action), sampling by Gumbel-max on the counter RNG.
 
 Everything runs batched on the GPU: one legal-mask launch per turn, the agent's games go through
 encode -> root inference -> muz_gumbel_search as one sub-batch, the random seats draw from the legal
@@ -20,8 +26,12 @@ import math
 import torch
 
 from . import detmadn as E
+from . import lib as _L
 from . import mcts as M
 from . import nets as N
+
+# evaluate_agent.py:777-864 (the variant evaluate_agent_parallel runs); 509-603 uses 0.5 / 5 / 3 / 1.5 / 2.5
+RULE_AGENT = dict(temperature=0.25, goal_bonus=5.0, out_many=3.0, out_few=2.0, hit_bonus=2.0)
 
 # MuZero_det_MADN/evaluate_agent.py uses the game_agent.py rules
 RULES = dict(E.SELFPLAY_RULES)
@@ -151,3 +161,126 @@ def compare_agents_statistically(net1, net2, num_games: int = 1000, batch_size: 
     w1, _ = test_agent_vs_random(net1, num_games, batch_size, seed, **kw)
     w2, _ = test_agent_vs_random(net2, num_games, batch_size, seed, **kw)
     return z_test(w1, w2, num_games)
+
+
+# ---- four seats: evaluate_agent_parallel (evaluate_agent.py:253-311, 715-960) ----------------------------
+def policy_action(env: E.DetMADNState, legal: torch.Tensor, mode: str, seed: int, turn: int, agent: dict | None = None,
+                  game_id: torch.Tensor | None = None) -> torch.Tensor:
+    """The random ('random_agent') or rule-based ('rule_based_agent') action of every game (int32 [B], -1
+    without a legal action), one launch over the batch (muz_detmadn_policy_action)."""
+    m = {"random_agent": 0, "rule_based_agent": 1}[mode]
+    a = dict(RULE_AGENT if agent is None else agent)
+    ag = _L.MuzRuleAgent(a["temperature"], a["goal_bonus"], a["out_many"], a["out_few"], a["hit_bonus"])
+    out = torch.empty((env.batch,), dtype=torch.int32, device=env.board.device)
+    gid = None if game_id is None else game_id.to(device=out.device, dtype=torch.int32).contiguous()
+    _L.check(_L.load().muz_detmadn_policy_action(env.rules, env.soa(), _L.ptr(legal.contiguous()), m, ag,
+                                                 int(seed) & ((1 << 64) - 1), int(turn), _L.ptr(gid), _L.ptr(out),
+                                                 env.batch, _L.stream_ptr()), "muz_detmadn_policy_action")
+    return out
+
+
+def _seats(rules, P):
+    """Seat (start cell / 10) of each player after env_reset's layout fix-up (deterministic_madn.py:70-74)."""
+    lay = [bool(rules.layout[i]) for i in range(4)]
+    if sum(lay) != P or (all(lay) and P < 4):
+        lay = [i < P for i in range(4)]
+    return [i for i in range(4) if lay[i]]
+
+
+def calculate_progress(env: E.DetMADNState, must_traverse_start: bool = False) -> torch.Tensor:
+    """calculate_progress (evaluate_agent.py:129-195) for every game and player -> float32 [B, P]: pins rotated
+    to the player's view (home -> pin - 5, track -> (pin - (40 // P) * p) % 40 - traverse, goal -> 40 + offset),
+    sorted, and greedily matched to the goal cells 40..43 (repeated masked argmin of |pin - goal|, first index
+    on ties).  Note the reference's distance = board_size // num_players (20 at two players, as written)."""
+    P = env.num_players
+    pins = env.pins_bp().long()                                           # [B, P, 4]
+    seats = torch.tensor(_seats(env.rules, P), device=pins.device)
+    p_idx = torch.arange(P, device=pins.device)[None, :, None]
+    g0 = (40 + 4 * seats)[None, :, None]
+    rot = torch.where(pins < 0, pins - 5,
+                      torch.where(pins < 40, torch.remainder(pins - (40 // P) * p_idx, 40) - int(must_traverse_start),
+                                  40 + (pins - g0)))
+    sp = torch.sort(rot, dim=2).values
+    dmat = (sp[..., :, None] - (40 + torch.arange(4, device=pins.device))).abs().double()   # [B, P, 4, 4]
+    mask = torch.ones_like(dmat, dtype=torch.bool)
+    total = torch.zeros(dmat.shape[:2], dtype=torch.float64, device=pins.device)
+    inf = torch.full_like(dmat, float("inf"))
+    for _ in range(4):
+        flat = torch.where(mask, dmat, inf).flatten(2).argmin(dim=2)     # first minimum
+        r, c = flat // 4, flat % 4
+        total += dmat.flatten(2).gather(2, flat[..., None])[..., 0]
+        rows = torch.arange(4, device=pins.device)
+        mask &= ~(rows[None, None, :, None] == r[..., None, None])
+        mask &= ~(rows[None, None, None, :] == c[..., None, None])
+    return total.float()
+
+
+@torch.no_grad()
+def evaluate_agent_parallel(agents, batch_size: int = 20, num_simulations: int = 100, max_depth: int = 50,
+                            temperature: float = 0.0, seed: int = 0, rules: dict | None = None, max_turns: int = 2000,
+                            rule_agent: dict | None = None, device="cuda") -> dict:
+    """evaluate_agent_parallel (evaluate_agent.py:253-311): `agents` = the four seats (player indices 0-3),
+    each a DeviceNet, None (a MuZero agent with randomly initialised params), 'rule_based_agent' or
+    'random_agent'.  4 x batch_size games, block i started by player i (jnp.repeat(arange(4), batch_size)),
+    at most 2000 turns; MuZero seats search with S / D / temperature (evaluate_agent.py:938-940 defaults).
+    Returns winners[start][player] and average_progress[start][player] as the reference prints them, plus
+    their totals (wins per player, progress per player = column sum / 4)."""
+    r = dict(RULES if rules is None else rules)
+    P = 4
+    C = E.num_channels(P)
+    nets = []
+    for i, a in enumerate(agents):
+        if a is None:
+            nets.append(N.DeviceNet(N.init_muzero_params(1_000_003 * (seed + 1) + i, C), C, device=device))
+        elif isinstance(a, str):
+            if a not in ("rule_based_agent", "random_agent"):
+                raise ValueError(f"unknown agent {a!r}")
+            nets.append(a)
+        else:
+            nets.append(N.as_device_net(a, C, device=device))
+    n = 4 * batch_size
+    env = E.env_reset(n, num_players=P, device=device, **r)
+    for sp in range(1, 4):
+        idx = torch.arange(sp * batch_size, (sp + 1) * batch_size, device=device)
+        _put(env, idx, E.env_reset(batch_size, num_players=P, starting_player=sp, device=device, **r))
+    gid = torch.arange(n, device=device, dtype=torch.int32)
+    ws = M.SearchWorkspace(n, num_simulations, device) if any(not isinstance(x, str) for x in nets) else None
+    for turn in range(max_turns):
+        active = env.done == 0
+        if not bool(active.any()):
+            break
+        bits = E.legal_bits(env)
+        cp = env.current_player.long()
+        has = bits != 0
+        mover = active & has
+        act = torch.full((n,), -1, dtype=torch.int32, device=device)
+        for s, a in enumerate(nets):
+            sel = mover & (cp == s)
+            if not bool(sel.any()):
+                continue
+            if isinstance(a, str):
+                pa = policy_action(env, bits, a, seed, turn, rule_agent, gid)
+                act = torch.where(sel, pa, act)
+            else:
+                idx = sel.nonzero().flatten()
+                sub = _sub(env, idx)
+                out, _ = M.muzero_mcts(a, E.encode_board(sub), bits[idx], num_simulations, max_depth, temperature,
+                                       seed=seed, turn=turn, workspace=ws)
+                act[idx] = out.action
+        step = mover.nonzero().flatten()
+        if step.numel():
+            sub = _sub(env, step)
+            E.env_step(sub, act[step])
+            _put(env, step, sub)
+        nos = (active & ~has).nonzero().flatten()
+        if nos.numel():
+            sub = _sub(env, nos)
+            E.no_step(sub)
+            _put(env, nos, sub)
+    w = winners(env, bool(r.get("enable_teams", False))) & (env.done != 0)[:, None]
+    prog = calculate_progress(env, bool(r.get("must_traverse_start", False)))
+    win_tab = w.long().reshape(4, batch_size, P).sum(dim=1)
+    prog_tab = prog.reshape(4, batch_size, P).mean(dim=1)
+    return {"games": n, "winners": win_tab.tolist(), "average_progress": prog_tab.tolist(),
+            "wins_per_player": win_tab.sum(dim=0).tolist(), "progress_per_player": (prog_tab.sum(dim=0) / 4).tolist(),
+            "finished": int((env.done != 0).sum()), "final_state": env}

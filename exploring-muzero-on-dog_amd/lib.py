@@ -21,6 +21,11 @@ MUZ_E_INVALID = MUZ_E_BASE + 1
 MUZ_E_UNSUPPORTED = MUZ_E_BASE + 2
 
 
+class MuzRuleAgent(ctypes.Structure):
+    _fields_ = [("temperature", ctypes.c_float), ("goal_bonus", ctypes.c_float), ("out_many", ctypes.c_float),
+                ("out_few", ctypes.c_float), ("hit_bonus", ctypes.c_float)]
+
+
 class MuzRules(ctypes.Structure):
     _fields_ = [
         ("num_players", ctypes.c_int32),
@@ -191,6 +196,9 @@ SIGNATURES = {
     "muz_detmadn_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_random_round": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_uint64, ctypes.c_int32,
                                                 vp, vp, vp, ctypes.c_int32, vp]),
+    "muz_detmadn_policy_action": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32,
+                                                 ctypes.POINTER(MuzRuleAgent), ctypes.c_uint64, ctypes.c_int32, vp, vp,
+                                                 ctypes.c_int32, vp]),
     "muz_dog_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, ctypes.c_int32, vp]),
     "muz_dog_legal": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_int32, vp]),
     "muz_dog_step": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_uint64, vp, vp, ctypes.c_int32,

@@ -122,6 +122,22 @@ int muz_detmadn_encode_i8(const muz_rules* rules, muz_detmadn_soa state, int8_t*
 int muz_detmadn_random_round(const muz_rules* rules, muz_detmadn_soa state, uint32_t* legal_bits, uint64_t seed,
                              int32_t turn, int8_t* obs, int8_t* reward, uint8_t* done, int32_t n, void* stream);
 
+/* Evaluation agents of MuZero_det_MADN/evaluate_agent.py: mode 0 = the random agent (do_random, 770-775),
+ * mode 1 = the rule-based agent (do_rule_based, 777-864; weights in `agent`, the reference's
+ * {0.25, 5.0, 3.0, 2.0, 2.0}; the multiactor_step variant 509-603 uses {0.5, 5.0, 3.0, 1.5, 2.5}).  Both
+ * sample jax.random.categorical as argmax(logits + Gumbel) with the Gumbel draw of the counter RNG
+ * (seed ^ 0x9011C7A6E47, game_id[g] (or g), turn, action).  action[g] = -1 when legal_bits[g] == 0. */
+typedef struct muz_rule_agent {
+  float temperature;   /* softmax temperature of the scores */
+  float goal_bonus;    /* landing on an own goal cell from outside the goal area */
+  float out_many;      /* leaving home with >= 2 pins at home */
+  float out_few;       /* leaving home with < 2 pins at home */
+  float hit_bonus;     /* moving onto an opponent pin */
+} muz_rule_agent;
+int muz_detmadn_policy_action(const muz_rules* rules, muz_detmadn_soa state, const uint32_t* legal_bits, int32_t mode,
+                              const muz_rule_agent* agent /*host, mode 1*/, uint64_t seed, int32_t turn,
+                              const int32_t* game_id, int32_t* action, int32_t n, void* stream);
+
 
 /* ---- classic MADN environment (MADN/classic_madn.py) -------------------------------------- */
 

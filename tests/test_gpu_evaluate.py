@@ -1,7 +1,10 @@
 """Evaluation harness (evaluate_agent.py) on the GPU: the random baseline is fair, the MuZero seat plays
 legal games to the end, and results are reproducible."""
+import numpy as np
 import pytest
+import torch
 
+from oracle import detmadn as dm
 from oracle import nets as ON
 
 pytestmark = pytest.mark.gpu
@@ -27,3 +30,84 @@ def test_muzero_seat_vs_random(cuda):
     assert a == b and a["finished"] == 128 and sum(a["seat_wins"]) > 0
     z = EV.compare_agents_statistically(net, None, 128, batch_size=128, num_simulations=8, max_depth=6)
     assert 0.0 <= z["p"] <= 1.0
+
+
+# ---- four seats: rule-based / random agents, evaluate_agent_parallel, calculate_progress -----------------
+def _states(rule_set, n, seed):
+    from tests._detmadn_util import random_play_transitions
+    envs = []
+    for _, batch in random_play_transitions(rule_set, 16, seed, max_plies=500, p_illegal=0.0):
+        envs.extend(e for _, e, _, _ in batch)
+    rng = np.random.default_rng(seed)
+    return [envs[i] for i in rng.choice(len(envs), size=min(n, len(envs)), replace=False)]
+
+
+@pytest.mark.parametrize("rule_set", ["selfplay_4p_teams", "exotic_4p"])
+def test_policy_kernel_matches_oracle(cuda, rule_set):
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import evaluate as EV
+    from oracle import evaluate as OE
+    from tests._detmadn_util import RULE_SETS
+    envs = _states(rule_set, 256, 7)
+    kw = RULE_SETS[rule_set]
+    rules = E.make_rules(kw["num_players"], **{k: v for k, v in kw.items() if k != "num_players"})
+    st = E.state_from_host(np.stack([e.pins for e in envs]), [e.current_player for e in envs], rules,
+                           action_set=np.stack([e.action_set for e in envs]), board=np.stack([e.board for e in envs]))
+    bits = E.legal_bits(st)
+    gid = torch.arange(len(envs), dtype=torch.int32, device="cuda") + 1000
+    for turn in (0, 5):
+        ra = EV.policy_action(st, bits, "random_agent", 11, turn, game_id=gid).cpu().numpy()
+        rb = EV.policy_action(st, bits, "rule_based_agent", 11, turn, game_id=gid).cpu().numpy()
+        want_r = [OE.random_action(e, 11, 1000 + i, turn) for i, e in enumerate(envs)]
+        want_b = [OE.rule_based_action(e, 11, 1000 + i, turn) for i, e in enumerate(envs)]
+        assert ra.tolist() == want_r
+        assert rb.tolist() == want_b
+        va = np.stack([dm.valid_action(e).flatten() for e in envs])
+        assert all(va[i, a] for i, a in enumerate(rb) if a >= 0)
+
+
+def test_rule_based_beats_random_and_random_is_fair(cuda):
+    from exploring_muzero_on_dog_amd import evaluate as EV
+    n = 4 * 128
+    rr = EV.evaluate_agent_parallel(["random_agent"] * 4, batch_size=128, seed=1)
+    assert rr["finished"] == n
+    w = rr["wins_per_player"]
+    assert w[0] == w[2] and w[1] == w[3] and w[0] + w[1] == n      # teams: one team wins every finished game
+    assert abs(w[0] / n - 0.5) < 4 * (0.25 / n) ** 0.5, w          # fair within 4 sigma of the binomial
+    # The reference's rule-based agent as written (landing cells from cur + arange(6), i.e. one short of the
+    # real move, and the base score indexed by a // 4) plays WORSE than random: its seats win far less than
+    # half, in either seating -- consistent with eval_results.md, where MuZero beats it more often (99.6 %)
+    # than it beats the random agent (97.8 %).  The margin is asserted both ways round (seat mapping check).
+    rb = EV.evaluate_agent_parallel(["rule_based_agent", "random_agent", "rule_based_agent", "random_agent"],
+                                    batch_size=128, seed=2)
+    rb2 = EV.evaluate_agent_parallel(["random_agent", "rule_based_agent", "random_agent", "rule_based_agent"],
+                                     batch_size=128, seed=3)
+    frac = rb["wins_per_player"][0] / n
+    frac2 = rb2["wins_per_player"][1] / n
+    from tests._parity import log
+    log(f"4-seat evaluation, {n} games each: random vs random team 0&2 {w[0] / n:.3f}; rule-based team 0&2 vs "
+        f"random {frac:.3f}; rule-based team 1&3 vs random {frac2:.3f}; progress {rb['progress_per_player']}")
+    sig = 4 * (0.25 / n) ** 0.5
+    assert frac < 0.5 - sig and frac2 < 0.5 - sig, (rb["wins_per_player"], rb2["wins_per_player"])
+    # calculate_progress of the final states equals the oracle restatement
+    from oracle import evaluate as OE
+    st = rb["final_state"]
+    prog = EV.calculate_progress(st).cpu().numpy()
+    pins = st.pins_bp().cpu().numpy()
+    for g in range(0, n, 17):
+        e = dm.env_reset(num_players=4, **dm.SELFPLAY_RULES).replace(pins=pins[g])
+        for p in range(4):
+            assert prog[g, p] == OE.calculate_progress(e, p), (g, p)
+
+
+def test_four_seat_with_muzero_seats_is_reproducible(cuda):
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import evaluate as EV
+    from exploring_muzero_on_dog_amd import nets as N
+    C = E.num_channels(4)
+    net = N.DeviceNet(ON.init_params(C, seed=3), C)
+    agents = [net, "random_agent", None, "rule_based_agent"]
+    a = EV.evaluate_agent_parallel(agents, batch_size=8, num_simulations=4, max_depth=4, seed=4, max_turns=300)
+    b = EV.evaluate_agent_parallel(agents, batch_size=8, num_simulations=4, max_depth=4, seed=4, max_turns=300)
+    assert a["winners"] == b["winners"] and a["average_progress"] == b["average_progress"]
+    assert len(a["winners"]) == 4 and all(len(r) == 4 for r in a["winners"])
