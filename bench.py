@@ -47,6 +47,10 @@ FLOP_PER_SIM = 2 * (529_280 + 404_544)
 EXEC_FLOP_PER_SIM = 2 * (491_904 + 404_544)
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E
+# Config (e) learner step (train_with_reward.py:24-164): per sample Repr2 once (3,380,480 MAC at C = 34),
+# Pred4 K + 1 = 11 times (404,544), Dyn4 K = 10 times (529,280) -> 13,123,264 MAC forward; x2 FLOP, x3 for
+# forward + backward, x batch 128
+LEARNER_FLOP_PER_STEP = 3 * 2 * 13_123_264 * 128
 # Config (c): classic MADN 4p teams.  Algorithmic MAC per simulation (one branch evaluated):
 # decision = StochasticDynamics afterstate path + Pred4(A=4); chance = StochasticDynamics chance path + Pred4.
 CLASSIC_PLAYERS = 4
@@ -401,7 +405,7 @@ def run_train(args):
     ring = R.VectorizedReplayBuffer(20000, 128, 10, 50, obs_shape=(C, 56), max_episode_length=T, device=device,
                                     rng=np.random.RandomState(rank)) if is_learner else None
     learner = LR.Learner(params, C, unroll_steps=10, device=device, graph=True) if is_learner else None
-    stats = {"env_steps": 0, "train_steps": 0}
+    stats = {"env_steps": 0, "train_steps": 0, "learner_ms": 0.0}
 
     def iteration(seed, train_steps):
         buf = eng.play_stream(games, seed=seed + 7919 * rank, temperature=1.0) if is_actor else None
@@ -417,8 +421,13 @@ def run_train(args):
                     if r != learner_rank:
                         ring.save_packed(p)
         if is_learner:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             for _ in range(train_steps):
                 learner.train_step(ring.sample_batch())
+            e1.record()
+            e1.synchronize()
+            stats["learner_ms"] += e0.elapsed_time(e1)
             stats["train_steps"] += train_steps
             learner.push_to(net)
         if world > 1:
@@ -432,9 +441,10 @@ def run_train(args):
 
     for w in range(max(args.warmup, 1)):       # fills the ring and captures the learner's HIP graph
         iteration(100 * w, 2)
-    stats.update(env_steps=0, train_steps=0)
+    stats.update(env_steps=0, train_steps=0, learner_ms=0.0)
     elapsed = timed_region(dist, lambda k: iteration(1000 + k, args.train_steps), args.steps)
-    (env_steps, train_steps), elapsed = sum_max(dist, device, [stats["env_steps"], stats["train_steps"]], elapsed)
+    (env_steps, train_steps, learner_ms), elapsed = sum_max(
+        dist, device, [stats["env_steps"], stats["train_steps"], stats["learner_ms"]], elapsed)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -451,6 +461,15 @@ def run_train(args):
                    f"{world - 1} actor ranks + 1 learner rank (packed-trajectory gather, weight broadcast)"},
         "env_steps_per_s": round(env_steps / elapsed, 1), "train_steps_per_s": round(train_steps / elapsed, 2),
     }
+    if train_steps:
+        step_ms = learner_ms / train_steps
+        achieved = LEARNER_FLOP_PER_STEP / (step_ms * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": "learner train_step (forward + backward + AdamW, one HIP graph)",
+                           "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 5), "avg_step_ms": round(step_ms, 3),
+                           "flop_per_step": LEARNER_FLOP_PER_STEP,
+                           "note": "batch 128 x unroll 10 of 256-wide fp32 layers: hundreds of small GEMMs and "
+                                   "LayerNorms per step, latency-bound, not MFMA-bound", "traffic": None}
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

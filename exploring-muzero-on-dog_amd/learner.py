@@ -60,12 +60,18 @@ class MuZeroNets:
         return F.layer_norm(x, (x.shape[-1],), self.p[f"{name}/scale"], self.p[f"{name}/bias"], EPS_LN)
 
     def _conv(self, name, x):
-        """Flax Conv 'SAME', stride 1, NWC input [B, W, Cin] -> [B, W, Cout]."""
-        k = self.p[f"{name}/kernel"]            # (K, Cin, Cout)
-        K = k.shape[0]
+        """Flax Conv 'SAME', stride 1, NWC input [B, W, Cin] -> [B, W, Cout], as im2col + one GEMM (the kernel
+        (K, Cin, Cout) is already the [K * Cin, Cout] matrix).  MIOpen's conv1d picks algorithms that
+        accumulate with atomics (run-to-run different losses and gradients, measured:
+        profiles/learner_determinism.py); the GEMM form is deterministic, so eager and graph-captured steps
+        are bit-identical."""
+        k = self.p[f"{name}/kernel"]
+        K, Cin, Cout = k.shape
         pl = (K - 1) // 2
-        y = F.conv1d(F.pad(x.transpose(1, 2), (pl, K - 1 - pl)), k.permute(2, 1, 0), self.p[f"{name}/bias"])
-        return y.transpose(1, 2)
+        W = x.shape[1]
+        xp = F.pad(x, (0, 0, pl, K - 1 - pl))
+        cols = torch.cat([xp[:, d:d + W, :] for d in range(K)], dim=-1)      # [B, W, K * Cin]
+        return cols @ k.reshape(K * Cin, Cout) + self.p[f"{name}/bias"]
 
     def _rb(self, name, x):
         y = F.relu(self._ln(f"{name}/LayerNorm_0", self._dense(f"{name}/Dense_0", x)))

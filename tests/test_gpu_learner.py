@@ -76,20 +76,15 @@ def test_graph_captured_step_equals_eager(cuda):
     for i, b in enumerate(batches):
         le = eager.train_step(b)
         lg = graph.train_step(b)
-        # step 0 starts from identical parameters; later steps start from parameters that already differ by
-        # the Adam rounding noise described below, so their losses agree less tightly
-        tol = 1e-5 if i == 0 else 1e-4
-        assert abs(float(le["total_loss"]) - float(lg["total_loss"])) <= tol * abs(float(le["total_loss"])), i
-    # Adam normalises each update to ~lr (0.005): an element whose gradient is ~0 moves by +-lr on rounding
-    # noise alone (the captured and eager runs may pick different GEMM / convolution algorithms), so the
-    # check is on the bulk of the parameters, not the maximum
-    n = bad = 0
-    for k in eager.nets.p:
-        d = (eager.nets.p[k] - graph.nets.p[k]).abs()
-        n += d.numel()
-        bad += int((d > 1e-4).sum())
-    assert bad <= 1e-2 * n, (bad, n)      # measured ~0.12 %
-    print("parameters off by > 1e-4 after 4 steps:", bad, "of", n)
+        assert torch.equal(le["total_loss"], lg["total_loss"]), i
+    # The losses are bit-identical at every step.  Round 1's drift (1.7e-5 relative in the loss) was MIOpen's
+    # conv1d, whose algorithms accumulate with atomics (two EAGER runs differed; profiles/learner_determinism.py);
+    # the convolutions now run as im2col GEMMs.  What remains: from the third step on, the captured and eager
+    # weight-gradient GEMMs of the convolutions (reduction length 128 x 56 = 7168) round differently in the
+    # last bits (Adam's first moment differs there), measured <= 2.3e-7 on the parameters after 4 steps.
+    worst = max((eager.nets.p[k] - graph.nets.p[k]).abs().max().item() for k in eager.nets.p)
+    print("max |parameter difference| after 4 steps:", worst)
+    assert worst <= 1e-6, worst
 
 
 def test_stochastic_learner_on_classic_ring(cuda):
@@ -124,3 +119,44 @@ def test_stochastic_learner_on_classic_ring(cuda):
     assert (v - tv[:, 0]).abs().max().item() < 2e-5
     buf = eng.play_stream(20, seed=4)
     assert int(buf["idx"].min()) > 0
+
+
+def test_config_e_iteration_at_its_shape(cuda):
+    """Config (e) at train_with_reward.py:311-352's shape on one GPU: 4 players in teams, 1500 games at S=100 /
+    D=50 / max_len 550 streamed into a 20000 x 550 device ring, learner steps at batch 128 / unroll 10 /
+    td 50 (graph-captured), weights pushed back: ring lengths equal the games' lengths, losses finite, and
+    the pushed arena reproduces the torch forward within 1e-5 on the ring's own observations."""
+    E, GA, L, N, R = _mods()
+    P, GAMES, T, S, D = 4, 1500, 550, 100, 50
+    C = E.num_channels(P)
+    params = N.init_muzero_params(42, C)
+    net = N.DeviceNet(params, C)
+    eng = GA.SelfPlayEngine(net, GAMES, num_players=P, max_steps=T, num_simulations=S, max_depth=D)
+    ring = R.VectorizedReplayBuffer(20000, 128, 10, 50, obs_shape=(C, 56), max_episode_length=T,
+                                    rng=np.random.RandomState(0))
+    learner = L.Learner(params, C, unroll_steps=10, graph=True)
+    buf = eng.play_stream(GAMES, seed=1, temperature=1.0)
+    idx = buf["idx"].clone()
+    ring.save_games_from_buffers(buf)
+    assert ring.size == GAMES
+    assert torch.equal(ring.episode_lengths[:GAMES], idx)
+    assert int(idx.min()) > 0 and int(idx.max()) <= T
+    losses = [learner.train_step(ring.sample_batch()) for _ in range(6)]
+    assert all(np.isfinite(float(x["total_loss"])) for x in losses)
+    learner.push_to(net)
+    obs = ring.observations[:64, 7].float()                      # real game observations from the ring
+    lg, v, e = N.root_inference_fn(net, obs)
+    act = ring.actions[:64, 7].clamp(min=0)
+    r, d, rl, rv, ne = N.recurrent_inference_fn(net, act, e)
+    with torch.no_grad():
+        te = learner.nets.representation(obs)
+        tl, tv = learner.nets.prediction(te)
+        tn, trl, tdl = learner.nets.dynamics(te, act.long())
+        tpl, tpv = learner.nets.prediction(tn)
+    err = max((e - te).abs().max().item(), (lg - tl).abs().max().item(), (v - tv[:, 0]).abs().max().item(),
+              (ne - tn).abs().max().item(), (rl - tpl).abs().max().item(), (rv - tpv[:, 0]).abs().max().item())
+    from tests._parity import log
+    log(f"config (e) shape: {GAMES} games 4p S={S} D={D}, {int(idx.sum())} env-steps into the 20000 x {T} ring, "
+        f"6 learner steps at batch 128 / unroll 10 (losses {[round(float(x['total_loss']), 4) for x in losses]}), "
+        f"pushed arena vs torch forward max |d| {err:.2e}")
+    assert err <= 1e-5, err
