@@ -54,6 +54,11 @@ LEARNER_FLOP_PER_STEP = 3 * 2 * 13_123_264 * 128
 # Config (c): classic MADN 4p teams.  Algorithmic MAC per simulation (one branch evaluated):
 # decision = StochasticDynamics afterstate path + Pred4(A=4); chance = StochasticDynamics chance path + Pred4.
 CLASSIC_PLAYERS = 4
+# Algorithmic MAC per simulation of the stochastic search: each simulation expands ONE node -- a decision
+# node's child (action dynamics 518,432 + PredictionNetwork4(A=4) on the afterstate 401,984 = 920,416) or a
+# chance node's child (chance dynamics 491,904 + 401,984 = 893,888); paths alternate decision / chance
+# levels, so the mean of the two, 907,152, is used (JAX evaluates both branches: 1,814,304).
+CLASSIC_FLOP_PER_SIM = 2 * 907_152
 # Config (d): DOG 2v2, 1024 games per GPU (8192 over 8 GPUs), uniform random legal policy.
 DOG_BATCH = 1024
 DOG_TURNS_PER_STEP = 16         # one bench step = one muz_dog_random_play launch of 16 turns over the batch
@@ -319,6 +324,30 @@ def run_dog(args):
         dist.destroy_process_group()
 
 
+def classic_cpu_baseline(seconds, sims, depth):
+    """The NumPy restatement of classic Stochastic MuZero self-play (oracle/selfplay.py
+    play_batch_of_games_stochastic with oracle/classic_nets.py, "port"): 8 games for `seconds` on the host."""
+    from threadpoolctl import threadpool_limits
+    from oracle import classic_madn as cm
+    from oracle import classic_nets as CN
+    from oracle import selfplay as OS
+    cores, _ = cpu_cores()
+    C = cm.num_channels(CLASSIC_PLAYERS)
+    params = CN.init_params(C, seed=0)
+    n = 8
+    envs = [cm.env_reset(num_players=CLASSIC_PLAYERS, **cm.SELFPLAY_RULES) for _ in range(n)]
+    t0 = time.perf_counter()
+    with threadpool_limits(limits=cores):
+        buf, turns = OS.play_batch_of_games_stochastic(
+            params, CN.root_inference, lambda p, a, e: CN.decision_recurrent(p, a, e),
+            lambda p, c, a: CN.chance_recurrent(p, c, a), envs, sims, depth, 10_000, TEMP, 0, time_budget=seconds)
+    dt = time.perf_counter() - t0
+    steps = int(buf["idx"].sum())
+    return {"value": round(steps / dt, 2), "unit": "env_steps/s", "cores": cores, "kind": "port",
+            "sample": f"NumPy oracle classic Stochastic MuZero self-play, {n} games x {turns} turns ({steps} env-steps, "
+                      f"S={sims}, D={depth}) in {dt:.1f}s, BLAS threads={cores}"}
+
+
 def run_classic(args):
     """Config (c): classic MADN 4p teams (game_agent_stochastic.py:13-24 rules), B games per GPU played to
     the end with a 50-simulation Stochastic MuZero search per move (muz_classic_selfplay)."""
@@ -368,8 +397,14 @@ def run_classic(args):
                    "parallelism": parallelism(args, world)},
         "sims_per_s": round(searches * args.sims / elapsed, 1),
         "env_steps": int(steps_done), "searches": int(searches),
-        "search_kernel": {"kernel": "k_stochastic_search", "avg_launch_ms": round(search_ms / max(1, turns), 4)},
     }
+    achieved = searches * args.sims * CLASSIC_FLOP_PER_SIM / (search_ms * 1e-3) / 1e12 if search_ms > 0 else 0.0
+    out["roofline"] = {"bound": "mfma", "kernel": "k_stochastic_search", "achieved": round(achieved, 3),
+                       "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                       "avg_launch_ms": round(search_ms / max(1, turns), 4), "flop_per_sim": CLASSIC_FLOP_PER_SIM,
+                       "traffic": None}
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = classic_cpu_baseline(min(args.cpu_seconds, 20.0), args.sims, args.depth)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -487,7 +487,7 @@ __device__ __forceinline__ int dog_base_of_slot(int sl) {
 // The k-th legal action, k = floor(u * count) (kth_legal over dog_mask_words, same result), from the
 // slot words of dog_checks_play (play phase) or the current player's cards (swap phase); -1 when nothing
 // is legal.  One full wave; the bit inside the chosen word is found by a ballot over per-lane prefix counts.
-__device__ __forceinline__ int dog_pick(const DogG& s, float u, int lane) {
+__device__ __forceinline__ int dog_pick(const DogG& s, float u, int lane, int* count = nullptr) {
   unsigned long long w[14];
   if (s.phase == 0) {
 #pragma unroll
@@ -503,6 +503,7 @@ __device__ __forceinline__ int dog_pick(const DogG& s, float u, int lane) {
   int tot = 0;
 #pragma unroll
   for (int r = 0; r < 14; ++r) tot += __popcll(w[r]);
+  if (count) *count = tot;
   if (tot == 0) return -1;
   int k = (int)(u * (float)tot);
   k = k >= tot ? tot - 1 : k;
@@ -643,6 +644,7 @@ struct DogPlayArgs {
   uint8_t* done;
   uint32_t* env_steps;   // optional accumulators
   uint32_t* episodes;
+  muz_dog_traj rec;      // optional per-turn records (rec.act == null: none)
 };
 
 // All arguments come in one struct that the kernel reads through the kernarg segment (kernarg0: scalar
@@ -685,12 +687,25 @@ __global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_e
     dog_checks_play(c, s, tid);
     DOG_STAMP(1);   // base checks (+ barrier)
     if (tid < 64) {
-      a = dog_pick(s, random_action_uniform(P.seed, g, P.turn0 + t), tid);
+      int nleg = 0;
+      a = dog_pick(s, random_action_uniform(P.seed, g, P.turn0 + t), tid, &nleg);
       DOG_STAMP(2);   // action choice
       if (tid == 0) {
+        const int mover = s.cp;
         int d = s.done;
         r = 0;
         s.need_deal = a < 0 ? dog_no_step(c, s) : dog_env_step(c, s, a, r, d, true);
+        if (P.rec.act) {   // the turn's record row (game lane g, row idx[g] + turns recorded this launch)
+          const int row = P.rec.idx[g] + played;
+          if (row < P.rec.max_steps) {
+            const size_t o = (size_t)g * P.rec.max_steps + row;
+            P.rec.act[o] = a;
+            P.rec.player[o] = mover;
+            P.rec.reward[o] = r;
+            P.rec.legal[o] = nleg;
+            P.rec.done[o] = (uint8_t)s.done;
+          }
+        }
       }
       DOG_STAMP(3);   // env_step / no_step (lane 0)
     }
@@ -710,6 +725,7 @@ __global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_e
     if (P.done) P.done[g] = (uint8_t)s.done;
     if (P.env_steps) P.env_steps[g] += (uint32_t)played;
     if (P.episodes) P.episodes[g] += (uint32_t)finished;
+    if (P.rec.act) P.rec.idx[g] = min(P.rec.max_steps, P.rec.idx[g] + played);
   }
 }
 
@@ -906,7 +922,19 @@ int muz_dog_random_play(const muz_rules* rules, muz_dog_soa st, uint64_t seed, i
   DOG_PROLOGUE(nturns >= 0)
   if (nturns == 0) return MUZ_OK;
   k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(
-      DogPlayArgs{c, st, seed, turn0, nturns, auto_reset ? 1 : 0, nullptr, nullptr, nullptr, env_steps, episodes});
+      DogPlayArgs{c, st, seed, turn0, nturns, auto_reset ? 1 : 0, nullptr, nullptr, nullptr, env_steps, episodes,
+                  muz_dog_traj{}});
+  return muz_last_launch_error();
+}
+
+int muz_dog_random_play_record(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int32_t turn0, int32_t nturns,
+                               int32_t auto_reset, uint32_t* env_steps, uint32_t* episodes, muz_dog_traj rec, int32_t n,
+                               void* stream) {
+  DOG_PROLOGUE(nturns >= 0)
+  MUZ_HOST_CHECK(rec.act && rec.player && rec.reward && rec.legal && rec.done && rec.idx && rec.max_steps > 0);
+  if (nturns == 0) return MUZ_OK;
+  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(
+      DogPlayArgs{c, st, seed, turn0, nturns, auto_reset ? 1 : 0, nullptr, nullptr, nullptr, env_steps, episodes, rec});
   return muz_last_launch_error();
 }
 

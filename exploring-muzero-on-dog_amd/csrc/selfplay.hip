@@ -11,6 +11,7 @@
 #include "detmadn.hpp"
 #include "host_consts.hpp"
 #include "launch.hpp"
+#include "turn_ledger.hpp"
 #include "compact.hpp"
 
 #include <algorithm>
@@ -271,80 +272,34 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
   sa.key_turn = tr.idx;   // the game's own step count (== the turn for every game of a batch)
   sa.key_game = lane_game;
 
-  constexpr int kLag = 2, kRing = 4;
-  // host_counts[turn][0] = games searching this turn, [1] = games active at the start of this turn
-  int32_t* host_counts = nullptr;
-  MUZ_HIP_RET(hipHostMalloc((void**)&host_counts, (size_t)max_turns * 2 * sizeof(int32_t), hipHostMallocDefault));
-  hipEvent_t ev[kRing];
-  for (int i = 0; i < kRing; ++i) (void)hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
-  // optional per-turn timing of the search launch (stats != null)
-  hipEvent_t* tev = nullptr;
-  if (stats) {
-    tev = new hipEvent_t[2 * (size_t)max_turns];
-    for (int i = 0; i < 2 * max_turns; ++i) (void)hipEventCreate(&tev[i]);
-  }
-  hipEvent_t t0, t1;
-  (void)hipEventCreate(&t0);
-  (void)hipEventCreate(&t1);
-  (void)hipEventRecord(t0, s);
+  TurnLedger led(s, stats != nullptr);
+  if ((rc = led.begin())) return rc;
   int turns = 0;
   rc = MUZ_OK;
   for (int turn = 0; turn < max_turns; ++turn) {
-    if (turn >= kLag) {
-      const int k = (turn - kLag) % kRing;
-      (void)hipEventSynchronize(ev[k]);
-      if (host_counts[2 * (turn - kLag) + 1] == 0) break;
-    }
+    if (!led.proceed(turn)) break;
     if (lane_game)
       k_ss_refill<<<1, kScanThreads, 0, s>>>(c, st, ws.lane_game, tr.idx, T, ws.next_game, num_games, n);
     k_sp_flags<<<(n + kSpBlock - 1) / kSpBlock, kSpBlock, 0, s>>>(c, st, ws.legal, ws.flag, n, lane_game, tr.idx, T);
     k_sp_compact<<<1, kScanThreads, 0, s>>>(ws.flag, n, ws.list, ws.slot, ws.counts);
-    (void)hipMemcpyAsync(&host_counts[2 * turn], ws.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s);
-    (void)hipEventRecord(ev[turn % kRing], s);
+    led.counts(turn, ws.counts);
     k_sp_encode<<<n, 64, 0, s>>>(c, st, ws.list, ws.counts, ws.legal, ws.legal_c, ws.obs, tr.obs, tr.idx, T, lane_game);
     if ((rc = muz_last_launch_error())) break;
     if ((rc = launch_root_inference(*w, ws.obs, n, ws.counts, ws.conv, ws.root_logits, ws.root_value, ws.root_emb,
                                     s)))
       break;
     sa.turn = turn;
-    if (tev) (void)hipEventRecord(tev[2 * turn], s);
+    led.search_begin(turn);
     if ((rc = launch_gumbel_search(*w, sa, ws.root_logits, ws.root_value, ws.root_emb, ws.legal_c, nullptr, ws.list, n, ws.counts, ws.tree, ws.action, ws.weights,
                                    ws.value, s)))
       break;
-    if (tev) (void)hipEventRecord(tev[2 * turn + 1], s);
+    led.search_end(turn);
     k_sp_apply<<<(n + kSpBlock - 1) / kSpBlock, kSpBlock, 0, s>>>(c, st, ws.flag, ws.slot, ws.action, ws.weights,
                                                                    ws.value, tr, n, lane_game);
     if ((rc = muz_last_launch_error())) break;
     ++turns;
   }
-  (void)hipEventRecord(t1, s);
-  (void)hipStreamSynchronize(s);
-  if (stats) {
-    // turns whose start found no active game recorded nothing: count the turns the reference would run
-    int active_turns = 0;
-    long long searches = 0;
-    double search_ms = 0.0;
-    for (int t = 0; t < turns; ++t) {
-      if (host_counts[2 * t + 1] == 0) break;
-      ++active_turns;
-      searches += host_counts[2 * t];
-      float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, tev[2 * t], tev[2 * t + 1]);
-      search_ms += ms;
-    }
-    float tot = 0.f;
-    (void)hipEventElapsedTime(&tot, t0, t1);
-    stats->turns = active_turns;
-    stats->searches = searches;
-    stats->search_ms = search_ms;
-    stats->total_ms = tot;
-    for (int i = 0; i < 2 * max_turns; ++i) (void)hipEventDestroy(tev[i]);
-    delete[] tev;
-  }
-  (void)hipEventDestroy(t0);
-  (void)hipEventDestroy(t1);
-  for (int i = 0; i < kRing; ++i) (void)hipEventDestroy(ev[i]);
-  (void)hipHostFree(host_counts);
+  led.finish(turns, stats);
   return rc;
 }
 

@@ -326,12 +326,59 @@ class RandomPlay:
         self.t += 1
 
     def play(self, nturns: int, env_steps: torch.Tensor | None = None, auto_reset: bool = False,
-             episodes: torch.Tensor | None = None):
+             episodes: torch.Tensor | None = None, record: "DogTrajectory | None" = None):
         """``nturns`` fused turns in ONE launch (muz_dog_random_play: every game stays in LDS for all of
         them).  ``env_steps`` / ``episodes`` (int32 [B]) accumulate turns played / games finished; with
-        ``auto_reset`` a finished game restarts in place and keeps playing."""
+        ``auto_reset`` a finished game restarts in place and keeps playing.  ``record`` (a DogTrajectory)
+        receives one row per turn and game (muz_dog_random_play_record)."""
         e = self.env
-        _L.check(self._lib.muz_dog_random_play(e.rules, self._soa, ctypes_u64(self.seed), self.t, int(nturns),
-                                               int(bool(auto_reset)), _L.ptr(env_steps), _L.ptr(episodes), e.batch,
-                                               _L.stream_ptr()), "muz_dog_random_play")
+        if record is None:
+            _L.check(self._lib.muz_dog_random_play(e.rules, self._soa, ctypes_u64(self.seed), self.t, int(nturns),
+                                                   int(bool(auto_reset)), _L.ptr(env_steps), _L.ptr(episodes),
+                                                   e.batch, _L.stream_ptr()), "muz_dog_random_play")
+        else:
+            if record.batch != e.batch:
+                raise ValueError("record batch differs from the actor's")
+            _L.check(self._lib.muz_dog_random_play_record(e.rules, self._soa, ctypes_u64(self.seed), self.t,
+                                                          int(nturns), int(bool(auto_reset)), _L.ptr(env_steps),
+                                                          _L.ptr(episodes), record.struct(), e.batch,
+                                                          _L.stream_ptr()), "muz_dog_random_play_record")
         self.t += int(nturns)
+
+
+# ---- DOG actor trajectories (config (d): actors -> learner over RCCL) -----------------------------------
+DOG_TRAJ_FIELDS = (("act", torch.int32), ("player", torch.int32), ("reward", torch.int32), ("legal", torch.int32),
+                   ("done", torch.uint8))
+
+
+class DogTrajectory:
+    """Per-turn records of the DOG actor (muz_dog_traj in include/muz.h): [B, T] action (-1 = no_step),
+    player who moved, reward, number of legal actions, game-finished flag, and idx [B] rows recorded.  The
+    reference's DOG agent is a stub (MuZero_DOG/game_agent.py:52-57), so this record is the engine's own
+    (parity-unpinned); transfer.gather_packed moves packed records to a learner rank like det games."""
+
+    def __init__(self, batch: int, max_steps: int, device="cuda"):
+        self.batch, self.T = int(batch), int(max_steps)
+        self.buf = {k: torch.zeros((self.batch, self.T), dtype=dt, device=device) for k, dt in DOG_TRAJ_FIELDS}
+        self.buf["idx"] = torch.zeros((self.batch,), dtype=torch.int32, device=device)
+
+    def struct(self) -> _L.MuzDogTraj:
+        t = _L.MuzDogTraj()
+        for k, _ in DOG_TRAJ_FIELDS:
+            setattr(t, k, self.buf[k].data_ptr())
+        t.idx = self.buf["idx"].data_ptr()
+        t.max_steps = self.T
+        return t
+
+    def reset(self):
+        self.buf["idx"].zero_()
+
+    def pack(self) -> dict:
+        """Rows [0, idx) of every lane, contiguous per lane in lane order (the packed layout of
+        transfer.pack): every field [R] with R = sum(idx), plus idx [B] and row_offset [B] (int64)."""
+        idx = self.buf["idx"]
+        keep = torch.arange(self.T, device=idx.device)[None, :] < idx[:, None]
+        out = {k: self.buf[k][keep] for k, _ in DOG_TRAJ_FIELDS}
+        out["idx"] = idx.clone()
+        out["row_offset"] = torch.cumsum(idx.to(torch.int64), 0) - idx.to(torch.int64)
+        return out

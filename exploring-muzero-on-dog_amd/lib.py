@@ -26,6 +26,12 @@ class MuzRuleAgent(ctypes.Structure):
                 ("out_few", ctypes.c_float), ("hit_bonus", ctypes.c_float)]
 
 
+class MuzDogTraj(ctypes.Structure):
+    _fields_ = [("act", ctypes.c_void_p), ("player", ctypes.c_void_p), ("reward", ctypes.c_void_p),
+                ("legal", ctypes.c_void_p), ("done", ctypes.c_void_p), ("idx", ctypes.c_void_p),
+                ("max_steps", ctypes.c_int32)]
+
+
 class MuzRules(ctypes.Structure):
     _fields_ = [
         ("num_players", ctypes.c_int32),
@@ -210,6 +216,9 @@ SIGNATURES = {
                                            vp, vp, ctypes.c_int32, vp]),
     "muz_dog_random_play": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, ctypes.c_int32,
                                            ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp]),
+    "muz_dog_random_play_record": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64,
+                                                  ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, MuzDogTraj,
+                                                  ctypes.c_int32, vp]),
     "muz_dog_random_action": (ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_int32, vp, ctypes.c_int32, vp]),
     "muz_classic_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, ctypes.c_int32, vp]),
     "muz_classic_set_die": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),

@@ -79,16 +79,23 @@ def pack(buffers: dict) -> dict:
     return out
 
 
-def gather_packed(packed: dict, obs_channels: int, num_actions: int, chance: bool = False, dst: int = 0,
-                  group=None) -> list | None:
+def dog_fields():
+    """(name, dtype, per-row shape) of packed DOG actor records (dog.DogTrajectory), in transfer order."""
+    return [("act", torch.int32, ()), ("player", torch.int32, ()), ("reward", torch.int32, ()),
+            ("legal", torch.int32, ()), ("done", torch.uint8, ())]
+
+
+def gather_packed(packed: dict, obs_channels: int = 0, num_actions: int = 0, chance: bool = False, dst: int = 0,
+                  group=None, spec: list | None = None) -> list | None:
     """Every rank's packed games -> rank ``dst`` (a list indexed by source rank, its own included);
-    None on the other ranks.  Tensors stay on their device (RCCL) or CPU (gloo)."""
+    None on the other ranks.  Tensors stay on their device (RCCL) or CPU (gloo).  ``spec`` overrides the
+    field list (dog_fields() for DOG actor records); by default the det / classic trajectory fields."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = packed["idx"].device
     meta = torch.tensor([packed["idx"].shape[0], packed["act"].shape[0]], dtype=torch.int64, device=dev)
     metas = [torch.empty_like(meta) for _ in range(world)]
     dist.all_gather(metas, meta, group=group)
-    spec = fields(obs_channels, num_actions, chance)
+    spec = fields(obs_channels, num_actions, chance) if spec is None else spec
     order = [("idx", torch.int32, None), ("row_offset", torch.int64, None)] + spec
     ops, result = [], None
     if rank == dst:

@@ -226,6 +226,26 @@ int muz_dog_random_turn(const muz_rules* rules, muz_dog_soa state, uint64_t seed
 int muz_dog_random_play(const muz_rules* rules, muz_dog_soa state, uint64_t seed, int32_t turn0, int32_t nturns,
                         int32_t auto_reset, uint32_t* env_steps, uint32_t* episodes, int32_t n, void* stream);
 
+/* Per-turn records of the DOG actor (config (d)'s "trajectories"; the reference's DOG agent is a stub,
+ * MuZero_DOG/game_agent.py:52-57, so this minimal record is this engine's own and parity-unpinned): row
+ * idx[b] + t of game lane b holds the turn's action (-1 = no legal action, no_step), the player who moved
+ * (current player before the move), the reward, the number of legal actions and whether the game finished
+ * on it (with auto_reset the next row starts the new game).  idx[b] advances by the turns played, capped at
+ * max_steps (rows past it are dropped). */
+typedef struct muz_dog_traj {
+  int32_t* act;      /* [n][max_steps] */
+  int32_t* player;   /* [n][max_steps] */
+  int32_t* reward;   /* [n][max_steps] */
+  int32_t* legal;    /* [n][max_steps] */
+  uint8_t* done;     /* [n][max_steps] */
+  int32_t* idx;      /* [n] rows recorded (in / out) */
+  int32_t max_steps;
+} muz_dog_traj;
+/* muz_dog_random_play that also writes the per-turn records into `rec` (all pointers non-null). */
+int muz_dog_random_play_record(const muz_rules* rules, muz_dog_soa state, uint64_t seed, int32_t turn0, int32_t nturns,
+                               int32_t auto_reset, uint32_t* env_steps, uint32_t* episodes, muz_dog_traj rec, int32_t n,
+                               void* stream);
+
 /* One step function on its own, the form DOG/test.py calls (dog.py:754-984): kind[b] 0 step_swap(pin, pos),
  * 1 step_normal_move(pin, move), 2 step_neg_move(pin, move), 3 step_hot_7(dist); args[b][4] = (pin, pos|move,
  * -, -) or dist[4].  Writes board and pins; reward / done (may be null) are the function's results. */

@@ -120,9 +120,12 @@ def die_uniform(seed, g, turn):
 
 
 def play_batch_of_games_stochastic(params, root_fn, decision_fn, chance_fn, envs, num_simulations, max_depth,
-                                   max_steps, temp, seed, dirichlet_fraction=0.0):
+                                   max_steps, temp, seed, dirichlet_fraction=0.0, time_budget=None):
     """game_agent_stochastic.py:52-218 over a list of oracle classic envs.  The root Dirichlet noise is
-    only supported with dirichlet_fraction 0 here (the engine's Gamma sampler is not restated)."""
+    only supported with dirichlet_fraction 0 here (the engine's Gamma sampler is not restated).  With
+    `time_budget` (seconds) the loop also stops once that much wall time has passed (bench.py's CPU sample)."""
+    import time as _time
+    _t0 = _time.perf_counter()
     from oracle import classic_madn as cm
     from oracle import mctx_stochastic as MS
     assert dirichlet_fraction == 0.0
@@ -142,6 +145,8 @@ def play_batch_of_games_stochastic(params, root_fn, decision_fn, chance_fn, envs
     dones = np.zeros(n, bool)
     step = 0
     while (~dones).any() and step < max_steps:
+        if time_budget is not None and _time.perf_counter() - _t0 > time_budget:
+            break
         search, nomove = [], []
         for i in range(n):
             if dones[i]:

@@ -119,3 +119,56 @@ def test_gather_packed_two_ranks():
 
 def test_gather_packed_three_ranks_learner_last_with_dice():
     _run(3, dst=2, chance=True)
+
+
+# ---- DOG actor records (config (d): 1024 games per GPU actor, records gathered to one learner rank) ------
+def _dog_packed(rank):
+    """Packed DOG records of one actor rank, built through DogTrajectory.pack on CPU tensors."""
+    import muzpkg
+    muzpkg.load()
+    from exploring_muzero_on_dog_amd import dog as D
+    g = torch.Generator().manual_seed(7 + rank)
+    tr = D.DogTrajectory(4 + rank, 12, device="cpu")
+    for k, _ in D.DOG_TRAJ_FIELDS:
+        tr.buf[k].copy_(torch.randint(-1, 50, tr.buf[k].shape, generator=g).to(tr.buf[k].dtype))
+    tr.buf["idx"].copy_(torch.randint(0, 13, (tr.batch,), generator=g, dtype=torch.int32))
+    return tr.pack(), tr
+
+
+def _dog_gather_worker(rank, world, port, q, dst):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import muzpkg
+    muzpkg.load()
+    from exploring_muzero_on_dog_amd import transfer as T
+    packed, _ = _dog_packed(rank)
+    got = T.gather_packed(packed, dst=dst, spec=T.dog_fields())
+    ok = True
+    if rank == dst:
+        ok = len(got) == world
+        for r in range(world):
+            want, tr = _dog_packed(r)
+            ok &= all(torch.equal(got[r][k], want[k]) for k in want)
+            # row_offset / idx locate every game's rows: they equal the lane's record prefix
+            for b in range(tr.batch):
+                o, n = int(got[r]["row_offset"][b]), int(got[r]["idx"][b])
+                ok &= torch.equal(got[r]["act"][o:o + n], tr.buf["act"][b, :n])
+    else:
+        ok = got is None
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_dog_records_gather_three_ranks():
+    world, dst = 3, 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dog_gather_worker, args=(r, world, port, q, dst)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(out[r] for r in range(world)), out

@@ -286,3 +286,48 @@ def test_dog_play_deterministic_and_launch_split_invariant(cuda):
             assert np.array_equal(a[0][k], other[0][k]), k
         assert np.array_equal(a[1], other[1]) and np.array_equal(a[2], other[2])
     assert a[2].sum() > B // 2      # most games finished and restarted inside a launch
+
+
+def test_dog_records_follow_the_oracle(cuda):
+    """muz_dog_random_play_record: every recorded row (action, mover, reward, legal count, finished flag)
+    of the followed games equals the oracle's turn, across launches and in-place restarts; the packed
+    records locate each game's rows."""
+    D = _D()
+    B, seed, T, chunk, launches = 64, 6, 900, 100, 9
+    rp = D.RandomPlay(B, seed=seed)
+    rec = D.DogTrajectory(B, T)
+    follow = list(range(0, B, 8))
+    envs = {g: reset(RULE_SETS["selfplay_4p_teams"], seed, g) for g in follow}
+    keys = {g: dg.engine_shuffle_keys(seed, g) for g in follow}
+    rows = {g: [] for g in follow}
+    for li in range(launches):
+        rp.play(chunk, auto_reset=True, record=rec)
+        for t in range(li * chunk, (li + 1) * chunk):
+            for g in follow:
+                e = envs[g]
+                if e.done:
+                    base = e.deal
+                    e = dg.env_reset(num_players=4, shuffle_keys=lambda x, b=base, k=keys[g]: k(x.replace(deal=x.deal + b)),
+                                     **dg.SELFPLAY_RULES)
+                    e = e.replace(deal=e.deal + base)
+                mask = dg.valid_actions(e)
+                a = dg.engine_random_action(mask, seed, g, t)
+                mover = e.current_player
+                if a < 0:
+                    e2, r, d = dg.no_step(e, keys[g])
+                else:
+                    e2, r, d = dg.env_step(e, a, keys[g])
+                rows[g].append((a, mover, int(r), int(np.asarray(mask).sum()), int(bool(d))))
+                envs[g] = e2
+    buf = {k: v.cpu().numpy() for k, v in rec.buf.items()}
+    n = launches * chunk
+    assert (buf["idx"] == n).all()
+    for g in follow:
+        got = list(zip(buf["act"][g, :n], buf["player"][g, :n], buf["reward"][g, :n], buf["legal"][g, :n],
+                       buf["done"][g, :n]))
+        assert [tuple(int(x) for x in r) for r in got] == rows[g], g
+    assert sum(sum(r[4] for r in rows[g]) for g in follow) > 0, "games must finish within the records"
+    packed = rec.pack()
+    off, idx = packed["row_offset"].cpu().numpy(), packed["idx"].cpu().numpy()
+    for g in follow:
+        assert np.array_equal(packed["act"].cpu().numpy()[off[g]:off[g] + idx[g]], buf["act"][g, :idx[g]])
