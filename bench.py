@@ -208,6 +208,11 @@ def synchronize(device):
         torch.cuda.synchronize(device)
 
 
+def beat(msg):
+    """Progress line on stderr (long steps would otherwise look hung to a watchdog)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def timed_region(dist, fn, steps):
     """barrier + synchronize, K steps, synchronize + barrier; returns the rank's elapsed seconds."""
     import torch
@@ -218,6 +223,7 @@ def timed_region(dist, fn, steps):
     t0 = time.perf_counter()
     for k in range(steps):
         fn(k)
+        beat(f"step {k + 1}/{steps} issued")
     synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -262,6 +268,29 @@ def dog_cpu_baseline(seconds):
     dt = time.perf_counter() - t0
     return {"value": round(steps / dt, 2), "unit": "env_steps/s", "cores": 1, "kind": "port",
             "sample": f"NumPy oracle DOG random play, {n} concurrent games, {steps} env-steps in {dt:.1f}s"}
+
+
+# k_dog_play's per-turn critical path, measured with the stamp build (profiles/diag_dog_stamps.py,
+# profiles/r2_dog_stamps.log): thread 0 of each game's workgroup, cycles per game-turn by phase.
+DOG_PHASES = {"reset check / restart": 4478, "base checks + barrier": 9640, "mask words + choice": 3860,
+              "env_step (lane 0)": 8708, "barrier": 277, "deal": 1623}
+
+
+def dog_latency_model(avg_ms, games, turns, launch_bytes):
+    """Config (d)'s roofline is a latency model, not a bandwidth fraction: each game is one workgroup whose
+    turn is a serial chain (checks -> barrier -> choice -> one-lane env_step -> barrier -> deal); all games
+    are resident at once (4 workgroups of 7 waves per CU), so a launch takes about one chain per turn.
+    `frac` = the share of the chain that is single-lane serial work (env_step), the part a faster kernel
+    would have to parallelise; HBM traffic is negligible (bytes_per_launch / launch time)."""
+    tot = sum(DOG_PHASES.values())
+    us_per_turn = avg_ms * 1e3 / turns
+    return {"bound": "latency", "kernel": "k_dog_play", "unit": "us/game-turn", "achieved": round(us_per_turn, 3),
+            "peak": None, "frac": round(DOG_PHASES["env_step (lane 0)"] / tot, 4),
+            "phase_share": {k: round(v / tot, 4) for k, v in DOG_PHASES.items()},
+            "phase_cycles_per_turn_stamp_build": DOG_PHASES, "games_resident": games, "avg_launch_ms": round(avg_ms, 5),
+            "hbm_gbs": round(launch_bytes / (avg_ms * 1e-3) / 1e9, 2), "traffic": None,
+            "note": "per-phase cycles from the stamp build (profiles/r2_dog_stamps.log; stamps add ~11 %); "
+                    "PMC of r1c: waves wait 86 % of their cycles, VALU issue 4 %"}
 
 
 def run_dog(args):
@@ -309,13 +338,7 @@ def run_dog(args):
                                f"restart in place", "games_per_gpu": args.batch,
                    "turns_per_step": T,
                    "parallelism": parallelism(args, world)},
-        "roofline": {"bound": "hbm", "kernel": "k_dog_play", "achieved": round(achieved, 2),
-                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
-                     "avg_launch_ms": round(avg_ms, 5), "bytes_per_launch": launch_bytes,
-                     "note": "latency-bound: 1024 games = 1024 workgroups of 7 waves, each game a serial chain "
-                             "of checks -> choice -> one-lane step per turn; waves wait 86 % of their cycles, VALU "
-                             "issue 4 % (profiles/r1c_dog_pmc.json); HBM is not the limit",
-                     "traffic": None},
+        "roofline": dog_latency_model(avg_ms, args.batch, T, launch_bytes),
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = dog_cpu_baseline(min(args.cpu_seconds, 15.0))
@@ -366,6 +389,7 @@ def run_classic(args):
 
     for w in range(args.warmup):
         play(10_000 * rank + w)
+        beat(f"warm-up {w + 1}/{args.warmup}")
     acc = {"steps": 0, "searches": 0, "search_ms": 0.0, "turns": 0}
 
     def step(k):
@@ -476,6 +500,7 @@ def run_train(args):
 
     for w in range(max(args.warmup, 1)):       # fills the ring and captures the learner's HIP graph
         iteration(100 * w, 2)
+        beat(f"warm-up {w + 1}")
     stats.update(env_steps=0, train_steps=0, learner_ms=0.0)
     elapsed = timed_region(dist, lambda k: iteration(1000 + k, args.train_steps), args.steps)
     (env_steps, train_steps, learner_ms), elapsed = sum_max(
@@ -638,6 +663,7 @@ def run_det(args):
 
     for w in range(args.warmup):
         play(10_000 * rank + w)
+        beat(f"warm-up {w + 1}/{args.warmup}")
     torch.cuda.synchronize()
     acc = {"steps": 0, "searches": 0, "search_ms": 0.0, "launches": 0}
 
