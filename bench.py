@@ -175,6 +175,21 @@ def measured_traffic():
     return t.get("bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+L2_SERVED_TBS = 18.8   # MI355X_MICROARCH.md, rows shared by every workgroup, served by the XCD's L2 (16.8-18.8)
+
+
+def measured_l2_reads():
+    """L1 -> L2 read bytes per k_gumbel_search launch from the newest committed PMC summary that has
+    TCP_TCC_READ_REQ_sum (128-byte requests): the per-simulation weight stream (3.6 MB per 16-game tile)
+    plus the tree reads.  Returns (bytes, source) or (None, None)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        per = json.load(open(f)).get("per_launch_mean", {})
+        if "TCP_TCC_READ_REQ_sum" in per:
+            return per["TCP_TCC_READ_REQ_sum"] * 128, os.path.relpath(f, ROOT)
+    return None, None
+
+
 def setup(args):
     rank, world, local = dist_env()
     if world != args.gpus:
@@ -719,6 +734,16 @@ def run_det(args):
                      "executed_frac": round(achieved * EXEC_FLOP_PER_SIM / FLOP_PER_SIM / PEAK_FP32_MFMA_TFLOPS, 4),
                      "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src},
     }
+    l2, l2_src = measured_l2_reads()
+    if l2 and launches:
+        avg_s = search_ms / launches * 1e-3
+        # second ceiling: the weights stream from L2 every simulation (a 16-row tile reuses each weight byte
+        # for 8 FLOP); at the L2-served rate the launch could not be shorter than l2 / 18.8 TB/s
+        out["roofline"]["l2_stream"] = {"bytes_per_launch": round(l2), "achieved_TBs": round(l2 / avg_s / 1e12, 2),
+                                        "ceiling_TBs": L2_SERVED_TBS, "frac": round(l2 / avg_s / 1e12 / L2_SERVED_TBS, 4),
+                                        "mfma_frac_at_l2_ceiling": round(achieved / PEAK_FP32_MFMA_TFLOPS * avg_s /
+                                                                         (l2 / (L2_SERVED_TBS * 1e12)), 4),
+                                        "source": l2_src}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.sims, args.depth, args.max_steps)
     print(json.dumps(out), flush=True)
