@@ -58,7 +58,67 @@ __device__ __forceinline__ void st_end() {
     __syncthreads();   \
     ST(ST_BAR);        \
   } while (0)
+__device__ __forceinline__ void st_sim(int) {}
+#elif defined(MUZ_TIMELINE)
+// ---- diagnostic per-wave timeline (make EXTRA=-DMUZ_TIMELINE): lane 0 of every wave of workgroup
+// MUZ_TL_WG records (s_memtime << 8 | category) at each segment end of simulation MUZ_TL_SIM.
+#ifndef MUZ_TL_WG
+#define MUZ_TL_WG 0
+#endif
+#ifndef MUZ_TL_SIM
+#define MUZ_TL_SIM 20
+#endif
+constexpr int kTlMax = 1024;
+__device__ unsigned long long g_tl[kWaves][kTlMax];
+__device__ unsigned int g_tl_n[kWaves];
+// per-wave record index in LDS (-1: not recording), so a stamp costs one LDS read, a vector store and an
+// LDS write (no global read)
+__device__ __forceinline__ int* tl_idx() {
+  __shared__ int idx[kWaves];
+  return idx;
+}
+__device__ __forceinline__ void st_begin() {
+  if ((threadIdx.x & 63) == 0) tl_idx()[threadIdx.x >> 6] = -1;
+}
+__device__ __forceinline__ void ST(int cat) {
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    const int i = tl_idx()[w];
+    if (i >= 0 && i < kTlMax) {
+      g_tl[w][i] = (__builtin_amdgcn_s_memtime() << 8) | (unsigned)cat;
+      tl_idx()[w] = i + 1;
+      g_tl_n[w] = i + 1;
+    }
+  }
+}
+// called at the top of every simulation by every wave
+__device__ __forceinline__ void st_sim(int sim) {
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    const bool on = blockIdx.x == MUZ_TL_WG && sim == MUZ_TL_SIM;
+    const int i = tl_idx()[w];
+    if (i > 0 && i + 1 < kTlMax) {   // end of the recorded simulation: shader clock and 100 MHz clock
+      g_tl[w][i] = (__builtin_amdgcn_s_memtime() << 8) | (unsigned)(ST_N - 1);
+      g_tl[w][i + 1] = (__builtin_amdgcn_s_memrealtime() << 8) | (unsigned)(ST_N - 2);
+      g_tl_n[w] = i + 2;
+    }
+    tl_idx()[w] = on ? 0 : -1;
+    if (on) {
+      g_tl[w][0] = (__builtin_amdgcn_s_memrealtime() << 8) | (unsigned)(ST_N - 2);
+      tl_idx()[w] = 1;
+    }
+  }
+  ST(ST_N - 1);
+}
+__device__ __forceinline__ void st_end() {}
+#define SYNC()         \
+  do {                 \
+    ST(ST_OTHER);      \
+    __syncthreads();   \
+    ST(ST_BAR);        \
+  } while (0)
 #else
+__device__ __forceinline__ void st_sim(int) {}
 __device__ __forceinline__ void st_begin() {}
 __device__ __forceinline__ void ST(int) {}
 __device__ __forceinline__ void st_end() {}
@@ -293,12 +353,12 @@ __device__ __forceinline__ int tsub() { return threadIdx.x % kRowLanes; }
 // combines a commutative pair in both lanes.
 template <class T, class F>
 __device__ __forceinline__ T row_reduce(T v, F f) {
-  static_assert(kRowLanes == 32 || kRowLanes == 64, "row width");
+  static_assert(kRowLanes == 16 || kRowLanes == 32 || kRowLanes == 64, "row width");
   v = f(v, dpp<DPP_XOR1>(v));
   v = f(v, dpp<DPP_XOR2>(v));
   v = f(v, dpp<DPP_HALF_MIRROR>(v));
   v = f(v, dpp<DPP_MIRROR>(v));
-  {
+  if constexpr (kRowLanes >= 32) {
     const LoHi<T> p = swap16(v);
     v = f(p.lo, p.hi);
   }

@@ -248,6 +248,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
 #pragma unroll 1
   for (int sim = 0; sim < sa.S; ++sim) {
     MUZ_STAMP(0);
+    st_sim(sim);
     // Weight table = kernel argument 0, read through the kernarg segment and laundered once per
     // simulation so the compiler re-derives the layer addresses inside the loop.
     const AS4 muz_net_w* wl = kernarg0<muz_net_w>();
@@ -480,6 +481,19 @@ int muz_diag_stamps2(unsigned long long* host_out, int reset) {
   if (reset) {
     unsigned long long z[ST_N] = {};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_st2), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
+
+#ifdef MUZ_TIMELINE
+// out: kWaves x kTlMax records then kWaves counts (reset: zero the counts after the copy)
+int muz_diag_timeline(unsigned long long* host_out, unsigned int* host_n, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl), sizeof(unsigned long long) * kWaves * kTlMax);
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(host_n, HIP_SYMBOL(g_tl_n), sizeof(unsigned int) * kWaves);
+  if (e == hipSuccess && reset) {
+    unsigned int z[kWaves] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_tl_n), z, sizeof(z));
   }
   return (int)e;
 }
