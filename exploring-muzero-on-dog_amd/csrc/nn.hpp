@@ -146,7 +146,8 @@ template <int CTRL, class T>
 __device__ __forceinline__ T dpp(T v) {
   return from_u<T>((unsigned)__builtin_amdgcn_update_dpp(0, (int)as_u(v), CTRL, 0xF, 0xF, false));
 }
-enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140 };
+// (DPP_WAVE_SHL1: lane i reads lane i + 1 across the whole wave; a GFX9 DPP control)
+enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140, DPP_WAVE_SHL1 = 0x130 };
 template <class T>
 struct LoHi {
   T lo, hi;

@@ -40,6 +40,13 @@ constexpr int kMaxNodes = kMaxSims + 1;
 constexpr int kMaxDepth = 64;
 constexpr int kAPad = 32;                  // children arrays padded to 32 actions
 constexpr float kFMin = -3.4028234663852886e38f;   // jnp.finfo(float32).min
+// levels per backup chunk (one per lane); a smaller value only in the test build that exercises the chunked
+// path of max_depth > 32 at ordinary depths (tests/test_gpu_search.py)
+#ifndef MUZ_BACKUP_CHUNK
+#define MUZ_BACKUP_CHUNK kRowLanes
+#endif
+constexpr int kBackupChunk = MUZ_BACKUP_CHUNK;
+static_assert(kBackupChunk >= 1 && kBackupChunk <= kRowLanes, "backup chunk");
 
 struct TreeWs {
   int32_t* c_index;
@@ -340,8 +347,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
         rk.reward = ar.v1[row];
         rk.disc = ar.v2[row];
       }
+      const float v = ar.v0[row], rw = ar.v1[row], dc = ar.v2[row];
       if (a == 0) {
-        const float v = ar.v0[row], rw = ar.v1[row], dc = ar.v2[row];
         if (par != 0) {
           const size_t eb = T.ca(g, par, pa);
           tree_st(T.index() + eb, nx);
@@ -351,29 +358,55 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
         s_raw[row][nx] = v;
         s_val[row][nx] = v;
         s_visits[row][nx] = fresh ? 1 : s_visits[row][nx] + 1;
-        // ---------------- backward (search.py backward) along the recorded path
-        float leaf = v;
-        int idx = nx;
-        const int d = s_depth[row];
-        for (int lvl = d - 1; lvl >= 0; --lvl) {
-          const int parent = p_node[row][lvl];
-          const int pact = p_act[row][lvl];
-          const int cnt = s_visits[row][parent];
-          const float r = (lvl == d - 1) ? rw : p_rew[row][lvl];
-          const float dsc = (lvl == d - 1) ? dc : p_disc[row][lvl];
-          leaf = r + dsc * leaf;
-          const float pv = (s_val[row][parent] * (float)cnt + leaf) / ((float)cnt + 1.0f);
-          if (lvl > 0) {
+      }
+      // ---------------- backward (search.py backward) along the recorded path, one level per lane: lane a
+      // holds level base + a (chunks of kRowLanes levels from the top when max_depth > kRowLanes).  Path nodes
+      // are distinct, so every level's parent statistics are read at once; only the discounted leaf value is a
+      // chain, evaluated level by level in the original order (leaf = r + discount * leaf, bit-identical to a
+      // sequential walk) with the level above's value moved down one lane per step.
+      const int d = s_depth[row];
+      float carry = v;      // leaf value entering the chunk from the level above it
+      float carry_v = v;    // new value of the node below the chunk's top level (its tree edge's value)
+      for (int base = ((d - 1) / kBackupChunk) * kBackupChunk; base >= 0; base -= kBackupChunk) {
+        const int l = base + a;
+        const int top = min(d, base + kBackupChunk) - 1 - base;   // highest lane of this row's chunk
+        const bool on = a <= top;
+        int parent = 0, pact = 0, cvis = 0, cnt = 0;
+        float r = 0.f, dsc = 0.f, pval = 0.f;
+        if (on) {
+          parent = p_node[row][l];
+          pact = p_act[row][l];
+          cvis = p_cvis[row][l];
+          r = (l == d - 1) ? rw : p_rew[row][l];
+          dsc = (l == d - 1) ? dc : p_disc[row][l];
+          cnt = s_visits[row][parent];
+          pval = s_val[row][parent];
+        }
+        // highest chunk lane over the wave's two rows (wave-uniform loop bound)
+        const unsigned long long tb = __ballot(a == top);
+        const int k0 = max(tb & 0xFFFFFFFFull ? 31 - __builtin_clz((unsigned)tb) : -1,
+                           tb >> 32 ? 31 - __builtin_clz((unsigned)(tb >> 32)) : -1);
+        float leaf = 0.f;
+        for (int k = k0; k >= 0; --k) {
+          const float up = dpp<DPP_WAVE_SHL1>(leaf);   // lane a + 1's value
+          if (a == k && on) leaf = r + dsc * (a == top ? carry : up);
+        }
+        const float pv = (pval * (float)cnt + leaf) / ((float)cnt + 1.0f);
+        const float pv_up = dpp<DPP_WAVE_SHL1>(pv);
+        const float child_v = (a == top) ? carry_v : pv_up;
+        if (on) {
+          if (l > 0) {
             const size_t ei = T.ca(g, parent, pact);
-            tree_st(T.value() + ei, s_val[row][idx]);
-            tree_st(T.visits() + ei, p_cvis[row][lvl] + 1);
+            tree_st(T.value() + ei, child_v);
+            tree_st(T.visits() + ei, cvis + 1);
           } else {
-            s_rootv[row] = s_val[row][idx];
+            s_rootv[row] = child_v;
           }
           s_val[row][parent] = pv;
           s_visits[row][parent] = cnt + 1;
-          idx = parent;
         }
+        carry = __shfl(leaf, 0, kRowLanes);
+        carry_v = __shfl(pv, 0, kRowLanes);
       }
       // the root edge of this path (level 0): its lane takes the value lane 0 just backed up
       // (same wave: LDS operations of one wave complete in order)
