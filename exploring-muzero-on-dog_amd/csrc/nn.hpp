@@ -561,11 +561,11 @@ __device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
 }
 
 // ---- LDS arena of a 16-row tile ---------------------------------------------------------------------
-// Row strides (floats): +4 keeps every row 16-byte aligned and spreads the 16 rows over the banks.  With
-// it the MFMA loops' A-fragment ds_read_b128 (lane (r, g) -> row r, dword 4g) has two lanes of each 16-lane
-// group sharing a 4-bank slot (the SQ_LDS_BANK_CONFLICT cycles of the search kernel); a stride of 8 mod 64
-// removes them and measured within noise (LDS is not on the critical path), so +4 stays.
-constexpr int kLdPad = 4;
+// Row strides (floats): +8 keeps every row 16-byte aligned and makes the MFMA loops' A-fragment
+// ds_read_b128 (lane (r, g) -> row r, dword 4g) conflict-free.  With +4 each of those reads cost 4 bank-conflict
+// cycles -- all of the search kernel's SQ_LDS_BANK_CONFLICT (profiles/r2_lds_conflicts.log) -- without slowing
+// the loop (the read is issued a k-block ahead; profiles/r2_loop_bench.log).
+constexpr int kLdPad = 8;
 constexpr int LD = LAT + kLdPad;     // row stride of 256-wide buffers
 constexpr int LDW = 512 + kLdPad;    // wide buffer (FiLM scale|shift 512, pred heads 384, concat 320)
 constexpr int LDE = 64 + kLdPad;     // small buffer (action embed, global features)

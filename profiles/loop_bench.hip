@@ -4,7 +4,7 @@
 // Reports the fraction of each SIMD's cycles the MFMA pipe was busy (s_memtime), and the shader clock.
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 [-DMUZ_TILE_WAVES=4 -DLB_NT=4] [-DMUZ_RING_DEPTH=3]
-//         [-DLB_SYNC=0] profiles/loop_bench.hip -o loop_bench && ./loop_bench
+//         [-DLB_SYNC=0] [-DLB_PAD=8] profiles/loop_bench.hip -o loop_bench && ./loop_bench
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -19,13 +19,17 @@ using namespace muz;
 #ifndef LB_SYNC
 #define LB_SYNC 1   // workgroup barrier after every layer (as between the search kernel's layers)
 #endif
+#ifndef LB_PAD
+#define LB_PAD kLdPad   // LDS row padding of the 16-row tile (floats)
+#endif
+constexpr int LDA = LAT + LB_PAD;
 constexpr int LAYERS = 14;
 constexpr int KB = 16;
 static_assert(kWaves * LB_NT * 16 == 256, "waves x NT x 16 must cover the 256 outputs");
 
 __global__ __launch_bounds__(kThreads, 1) void k_loop(const float* W, int reps, float* out, unsigned long long* cyc) {
-  __shared__ __attribute__((aligned(16))) float A[kRows * LD];
-  for (int i = threadIdx.x; i < kRows * LD; i += kThreads) A[i] = 0.001f * (float)(i % 97);
+  __shared__ __attribute__((aligned(16))) float A[kRows * LDA];
+  for (int i = threadIdx.x; i < kRows * LDA; i += kThreads) A[i] = 0.001f * (float)(i % 97);
   __syncthreads();
   constexpr int NT = LB_NT;
   const int lane = threadIdx.x & 63;
@@ -48,7 +52,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_loop(const float* W, int reps, 
     for (int l = 0; l < LAYERS; ++l) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_ring_impl<NT, false>(group(l), KB, A, LD, acc, b0, b1);
+      mfma_ring_impl<NT, false>(group(l), KB, A, LDA, acc, b0, b1);
       pf(l + 1 < LAYERS ? l + 1 : 0);
 #pragma unroll
       for (int t = 0; t < NT; ++t) keep[t] += acc[t];
@@ -110,8 +114,8 @@ int main(int argc, char** argv) {
   // per SIMD: (kWaves / 4) waves x NT tiles x KB k-blocks x 4 MFMAs x 32 cycles per layer
   const double mfma_cyc = (double)reps * LAYERS * (kWaves / 4) * LB_NT * KB * 4 * 32;
   const double flop = (double)grid * reps * LAYERS * 2.0 * 16 * 256 * 256 * launches;
-  printf("waves=%d NT=%d depth=%d sync=%d: MFMA busy %.3f of SIMD cycles, clock %.2f GHz, %.1f TFLOP/s "
+  printf("waves=%d NT=%d depth=%d sync=%d pad=%d: MFMA busy %.3f of SIMD cycles, clock %.2f GHz, %.1f TFLOP/s "
          "(%.1f us per layer)\n",
-         kWaves, LB_NT, MUZ_RING_DEPTH, LB_SYNC, mfma_cyc / cs, cs / rs * 0.1, flop / (ms * 1e-3) / 1e12, ms * 1e3 / launches / reps / LAYERS);
+         kWaves, LB_NT, MUZ_RING_DEPTH, LB_SYNC, LB_PAD, mfma_cyc / cs, cs / rs * 0.1, flop / (ms * 1e-3) / 1e12, ms * 1e3 / launches / reps / LAYERS);
   return 0;
 }
