@@ -190,6 +190,24 @@ def measured_l2_reads():
     return None, None
 
 
+def measured_loop_ceiling():
+    """The search kernel's weight-stream MFMA loop alone (profiles/loop_bench.hip: 14 resident 256x256 fp32
+    layers on a 16-row LDS tile, a barrier per layer, every CU busy) from the newest committed loop-bench
+    log: its TFLOP/s / the fp32 MFMA peak is the fraction the kernel could reach if its serial phases (tree
+    walk, LayerNorm passes, epilogues, heads, backup) cost nothing.  Returns a dict or None."""
+    import glob
+    import re
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_loop_bench.log")), reverse=True):
+        for line in open(f):
+            m = re.match(r"grid 256 lb_base: .*MFMA busy ([0-9.]+) of SIMD cycles, clock ([0-9.]+) GHz, ([0-9.]+) TFLOP/s",
+                         line)
+            if m:
+                busy, clk, tf = (float(x) for x in m.groups())
+                return {"frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4), "tflops": tf, "mfma_busy": busy, "clock_GHz": clk,
+                        "source": os.path.relpath(f, ROOT)}
+    return None
+
+
 def setup(args):
     rank, world, local = dist_env()
     if world != args.gpus:
@@ -744,6 +762,9 @@ def run_det(args):
                                         "mfma_frac_at_l2_ceiling": round(achieved / PEAK_FP32_MFMA_TFLOPS * avg_s /
                                                                          (l2 / (L2_SERVED_TBS * 1e12)), 4),
                                         "source": l2_src}
+    loop = measured_loop_ceiling()
+    if loop:
+        out["roofline"]["loop_ceiling"] = dict(loop, frac_of_ceiling=round(achieved / PEAK_FP32_MFMA_TFLOPS / loop["frac"], 4))
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.sims, args.depth, args.max_steps)
     print(json.dumps(out), flush=True)
