@@ -145,16 +145,6 @@ class MuZeroNets:
         return logits, torch.tanh(self._dense(f"{p}/Dense_5", v))
 
 
-def _balanced_ce(logits, labels, mask, special, w_special, w_other):
-    """Per-class balanced cross-entropy (train_with_reward.py:54-86)."""
-    ce = F.cross_entropy(logits, labels.long(), reduction="none")
-    is_s = labels == special
-    n_s = torch.clamp((mask * is_s).sum(), min=1.0)
-    n_o = torch.clamp((mask * ~is_s).sum(), min=1.0)
-    return (w_special * (mask * torch.where(is_s, ce, torch.zeros_like(ce))).sum() / n_s +
-            w_other * (mask * torch.where(~is_s, ce, torch.zeros_like(ce))).sum() / n_o)
-
-
 def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: float = 0.5):
     """train_with_reward.py:24-141 -> (total_loss, (value_loss, policy_loss, discount_loss, reward_loss)).
     grad_scale: the gradient share carried through the unrolled latent (0.5 in the reference, line 106;
@@ -177,25 +167,33 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
         latents.append((nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale)   # gradient scaling (fwd identity)
     logits_all, v_all = nets.prediction(torch.cat(latents, 0))
     rl_all, dl_all = nets.dynamics_heads(torch.cat(latents[1:], 0), oh) if K else (None, None)
-    total = torch.zeros((), dtype=obs.dtype, device=dev)
-    sums = [torch.zeros((), dtype=obs.dtype, device=dev) for _ in range(4)]
-    for k in range(K + 1):
-        mask = batch["masks"][:, k].to(obs.dtype)
-        logits, v = logits_all[k * B:(k + 1) * B], v_all[k * B:(k + 1) * B]
-        l_value = torch.mean(mask * (batch["target_values"][:, k].to(obs.dtype) - v[:, 0]) ** 2)
-        l_policy = torch.mean(mask * -(batch["policies"][:, k].to(obs.dtype) * F.log_softmax(logits, -1)).sum(-1))
-        step = (1.0 / unroll_steps) * (VALUE_SCALING * l_value + POLICY_SCALING * l_policy)
-        if k < K:
-            rl, dl = rl_all[k * B:(k + 1) * B], dl_all[k * B:(k + 1) * B]
-            l_rew = _balanced_ce(rl, rew_t[:, k], mask, 1, 0.1, 1.0)        # neutral 0.1, win/lose 1.0
-            l_disc = _balanced_ce(dl, disc_t[:, k], mask, 1, 1.0, 0.1)      # terminal 1.0, other 0.1
-        else:
-            l_rew, l_disc = torch.zeros((), dtype=obs.dtype, device=dev), torch.zeros((), dtype=obs.dtype, device=dev)
-        total = total + step + (1.0 / unroll_steps) * DISCOUNT_SCALING * l_disc + \
-            (1.0 / unroll_steps) * REWARD_SCALING * l_rew
-        for i, x in enumerate((l_value, l_policy, l_disc, l_rew)):
-            sums[i] = sums[i] + x
-    return total, tuple(sums)
+    # The per-step losses, all K (+1) steps at once ([K+1, B] views; row k = unroll step k).
+    m = batch["masks"][:, :K + 1].transpose(0, 1).to(obs.dtype)
+    v = v_all[:, 0].reshape(K + 1, B)
+    l_value = torch.mean(m * (batch["target_values"][:, :K + 1].transpose(0, 1).to(obs.dtype) - v) ** 2, 1)
+    logp = F.log_softmax(logits_all, -1).reshape(K + 1, B, -1)
+    l_policy = torch.mean(m * -(batch["policies"][:, :K + 1].transpose(0, 1).to(obs.dtype) * logp).sum(-1), 1)
+    zero = torch.zeros((), dtype=obs.dtype, device=dev)
+    if K:
+        l_rew = _balanced_ce_steps(rl_all, rew_t[:, :K].transpose(0, 1), m[:K], 1, 0.1, 1.0)    # neutral 0.1, win/lose 1.0
+        l_disc = _balanced_ce_steps(dl_all, disc_t[:, :K].transpose(0, 1), m[:K], 1, 1.0, 0.1)  # terminal 1.0, other 0.1
+    else:
+        l_rew = l_disc = zero[None]
+    total = ((1.0 / unroll_steps) * (VALUE_SCALING * l_value + POLICY_SCALING * l_policy)).sum() + \
+        (1.0 / unroll_steps) * (DISCOUNT_SCALING * l_disc.sum() + REWARD_SCALING * l_rew.sum())
+    return total, (l_value.sum(), l_policy.sum(), l_disc.sum(), l_rew.sum())
+
+
+def _balanced_ce_steps(logits, labels, mask, special, w_special, w_other):
+    """Per-class balanced cross-entropy (train_with_reward.py:54-86) of every unroll step at once:
+    logits [K*B, n] (step-major), labels / mask [K, B] -> [K]."""
+    Kk, B = labels.shape
+    ce = F.cross_entropy(logits, labels.reshape(-1).long(), reduction="none").reshape(Kk, B)
+    is_s = labels == special
+    n_s = torch.clamp((mask * is_s).sum(1), min=1.0)
+    n_o = torch.clamp((mask * ~is_s).sum(1), min=1.0)
+    return (w_special * (mask * torch.where(is_s, ce, torch.zeros_like(ce))).sum(1) / n_s +
+            w_other * (mask * torch.where(~is_s, ce, torch.zeros_like(ce))).sum(1) / n_o)
 
 
 def lr_schedule(step: int, lr0: float = 0.005, steps_per_iteration: int = 2500) -> float:
@@ -266,6 +264,15 @@ class AdamW:
         return g_norm
 
 
+def prefer_rocblas():
+    """The learner's GEMMs are small (M = 128 or 1408 rows, N and K <= 512).  hipBLASLt (torch's default on
+    ROCm) runs them on 256x256 / 256x128 macro-tiles at ~33 us each; rocBLAS picks tiles that fit and the
+    graph-captured det step drops from 17.4 to 12.4 ms on MI355X (profiles/r2_learner_profile.log).
+    Process-wide torch setting; the self-play path does not use torch GEMMs."""
+    if torch.cuda.is_available():
+        torch.backends.cuda.preferred_blas_library("cublas")   # = rocBLAS on ROCm
+
+
 class Learner:
     """train_step (train_with_reward.py:148-162) on batches sampled from the device ring.
 
@@ -277,6 +284,7 @@ class Learner:
 
     def __init__(self, params: dict, obs_channels: int, num_actions: int = 24, unroll_steps: int = 10,
                  device="cuda", graph: bool = False, **opt):
+        prefer_rocblas()
         self.nets = MuZeroNets(params, obs_channels, num_actions, device)
         self.opt = AdamW(self.nets.parameters(), **opt)
         self.unroll_steps = int(unroll_steps)
@@ -389,14 +397,6 @@ class ClassicMuZeroNets(MuZeroNets):
         return self._film_trunk("chance", 2, afterstate, self.chance_embed(chance))
 
 
-def balanced_loss(ce, is_rare, mask, n_valid, w_rare=1.0, w_common=0.1):
-    """train_stochastic.py:25-32 (n_common counts against the clamped n_rare, as the reference does)."""
-    masked_rare = mask * is_rare
-    n_rare = torch.clamp(masked_rare.sum(), min=1.0)
-    n_common = torch.clamp(n_valid - n_rare, min=1.0)
-    return w_rare * (masked_rare * ce).sum() / n_rare + w_common * ((mask - masked_rare) * ce).sum() / n_common
-
-
 def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: float = 0.5):
     """train_stochastic.py:34-180 -> (total, (value, policy, chance, discount, reward) losses)."""
     dt = nets.p["prediction/Dense_5/bias"].dtype
@@ -424,35 +424,40 @@ def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int =
     logits_all, v_all = nets.prediction(torch.cat(latents, 0))
     if K:
         rl_all, cl_all, dl_all = nets.action_heads(torch.cat(latents[:K], 0), torch.cat(afters, 0), oh_all)
-    total = torch.zeros((), dtype=dt, device=dev)
-    sums = [torch.zeros((), dtype=dt, device=dev) for _ in range(5)]
-    for k in range(K + 1):
-        mask = batch["masks"][:, k].to(dt)
-        sl = slice(k * B, (k + 1) * B)
-        logits, v = logits_all[sl], v_all[sl]
-        l_policy = torch.mean(mask * -(batch["policies"][:, k].to(dt) * F.log_softmax(logits, -1)).sum(-1))
-        l_value = torch.mean(mask * (batch["target_values"][:, k].to(dt) - v[:, 0]) ** 2)
-        zero = torch.zeros((), dtype=dt, device=dev)
-        if k < K:
-            n_valid = mask.sum()
-            rl, cl, dl = rl_all[sl], cl_all[sl], dl_all[sl]
-            rc, dc = rew_t[:, k], disc_t[:, k]
-            tp = probs[:, k]
-            reward_ce = F.cross_entropy(rl, rc.long(), reduction="none")
-            discount_ce = F.cross_entropy(dl, dc.long(), reduction="none")
-            chance_ce = -(tp * F.log_softmax(cl, -1)).sum(-1)
-            non_uniform = ((tp - 1.0 / 6.0) ** 2).sum(-1) > 1e-6
-            l_reward = balanced_loss(reward_ce, (rc != 1).to(dt), mask, n_valid)
-            l_discount = balanced_loss(discount_ce, (dc == 1).to(dt), mask, n_valid)
-            l_chance = balanced_loss(chance_ce, non_uniform.to(dt), mask, n_valid)
-        else:
-            l_chance, l_discount, l_reward = zero, zero, zero
-        total = total + (1.0 / unroll_steps) * (sc["value"] * l_value + sc["policy"] * l_policy +
-                                                sc["chance"] * l_chance + sc["discount"] * l_discount +
-                                                sc["reward"] * l_reward)
-        for i, x in enumerate((l_value, l_policy, l_chance, l_discount, l_reward)):
-            sums[i] = sums[i] + x
-    return total, tuple(sums)
+    # all K (+1) steps at once, as in loss_fn
+    m = batch["masks"][:, :K + 1].transpose(0, 1).to(dt)
+    v = v_all[:, 0].reshape(K + 1, B)
+    logp = F.log_softmax(logits_all, -1).reshape(K + 1, B, -1)
+    l_policy = torch.mean(m * -(batch["policies"][:, :K + 1].transpose(0, 1).to(dt) * logp).sum(-1), 1)
+    l_value = torch.mean(m * (batch["target_values"][:, :K + 1].transpose(0, 1).to(dt) - v) ** 2, 1)
+    zero = torch.zeros((1,), dtype=dt, device=dev)
+    if K:
+        mk = m[:K]
+        n_valid = mk.sum(1)
+        rc, dc = rew_t[:, :K].transpose(0, 1), disc_t[:, :K].transpose(0, 1)
+        tp = probs[:, :K].transpose(0, 1)                                          # [K, B, 6]
+        reward_ce = F.cross_entropy(rl_all, rc.reshape(-1).long(), reduction="none").reshape(K, B)
+        discount_ce = F.cross_entropy(dl_all, dc.reshape(-1).long(), reduction="none").reshape(K, B)
+        chance_ce = -(tp * F.log_softmax(cl_all, -1).reshape(K, B, -1)).sum(-1)
+        non_uniform = ((tp - 1.0 / 6.0) ** 2).sum(-1) > 1e-6
+        l_reward = balanced_loss_steps(reward_ce, (rc != 1).to(dt), mk, n_valid)
+        l_discount = balanced_loss_steps(discount_ce, (dc == 1).to(dt), mk, n_valid)
+        l_chance = balanced_loss_steps(chance_ce, non_uniform.to(dt), mk, n_valid)
+    else:
+        l_chance = l_discount = l_reward = zero
+    total = (1.0 / unroll_steps) * (sc["value"] * l_value.sum() + sc["policy"] * l_policy.sum() +
+                                    sc["chance"] * l_chance.sum() + sc["discount"] * l_discount.sum() +
+                                    sc["reward"] * l_reward.sum())
+    return total, (l_value.sum(), l_policy.sum(), l_chance.sum(), l_discount.sum(), l_reward.sum())
+
+
+def balanced_loss_steps(ce, is_rare, mask, n_valid, w_rare=1.0, w_common=0.1):
+    """train_stochastic.py:25-32 for every unroll step at once ([K, B] -> [K]; n_common counts against the
+    clamped n_rare, as the reference does)."""
+    masked_rare = mask * is_rare
+    n_rare = torch.clamp(masked_rare.sum(1), min=1.0)
+    n_common = torch.clamp(n_valid - n_rare, min=1.0)
+    return w_rare * (masked_rare * ce).sum(1) / n_rare + w_common * ((mask - masked_rare) * ce).sum(1) / n_common
 
 
 class StochasticLearner(Learner):
@@ -464,6 +469,7 @@ class StochasticLearner(Learner):
     def __init__(self, params: dict, obs_channels: int, unroll_steps: int = 10, device="cuda", graph: bool = False,
                  **opt):
         opt.setdefault("boundaries", CLASSIC_LR_BOUNDARIES)
+        prefer_rocblas()
         self.nets = ClassicMuZeroNets(params, obs_channels, device)
         self.opt = AdamW(self.nets.parameters(), **opt)
         self.unroll_steps = int(unroll_steps)
