@@ -50,8 +50,8 @@ class MuZeroNets:
 
     # ---- layers (oracle/nets.py restates the same Flax semantics) ----------------------------------
     def _dense(self, name, x):
-        if x.dim() == 2:
-            return torch.addmm(self.p[f"{name}/bias"], x, self.p[f"{name}/kernel"])
+        # (not addmm: torch routes a GEMM with a bias epilogue to hipBLASLt whatever the preferred BLAS, and
+        # hipBLASLt's macro-tiles make these small GEMMs ~33 us each; see prefer_rocblas)
         return x @ self.p[f"{name}/kernel"] + self.p[f"{name}/bias"]
 
     def _ln(self, name, x):
@@ -267,7 +267,8 @@ class AdamW:
 def prefer_rocblas():
     """The learner's GEMMs are small (M = 128 or 1408 rows, N and K <= 512).  hipBLASLt (torch's default on
     ROCm) runs them on 256x256 / 256x128 macro-tiles at ~33 us each; rocBLAS picks tiles that fit and the
-    graph-captured det step drops from 17.4 to 12.4 ms on MI355X (profiles/r2_learner_profile.log).
+    graph-captured det step drops from 17.4 to 12.4 ms on MI355X (8.4 ms with the losses vectorised and no
+    addmm; profiles/r2_learner_profile.log).
     Process-wide torch setting; the self-play path does not use torch GEMMs."""
     if torch.cuda.is_available():
         torch.backends.cuda.preferred_blas_library("cublas")   # = rocBLAS on ROCm
