@@ -1,0 +1,199 @@
+// Fused Dense epilogue for the learner (train_with_reward.py / train_stochastic.py: Flax Dense -> LayerNorm
+// -> ReLU, and the ResBlock tail relu(x + LayerNorm(Dense(.))).  The GEMM stays a library GEMM; these kernels
+// replace the bias add, LayerNorm, ReLU and residual add of the forward pass (one kernel instead of 3-5) and
+// the ReLU / LayerNorm / bias backward (two kernels instead of ~5), which is what a batch-128 training step
+// is made of: hundreds of tiny launches.
+//
+// Forward, per row m of y [M][N] (one wave per row, N in {32, 64, 128, 256}):
+//   z = y + bias;  Flax LayerNorm (eps 1e-6, fast variance E[z^2] - E[z]^2, as nn.hpp's ln16);
+//   o = (z - mean) * (rstd * gamma) + beta;  out = o (PLAIN) | relu(o) (RELU) | relu(res + o) (RESID_RELU).
+// Saved for the backward: z, mean, rstd and out (the ReLU mask).
+// Backward: do = dout (PLAIN) or dout * (out > 0); dres = do (RESID_RELU);
+//   xhat = (z - mean) * rstd, g = do * gamma,
+//   dz = rstd * (g - mean_n(g) - xhat * mean_n(g * xhat))       (= dy, and its column sum is dbias),
+//   dgamma = sum_m do * xhat, dbeta = sum_m do, dbias = sum_m dz
+// with the column sums as per-block partials reduced in a fixed order (deterministic: graph-captured and
+// eager steps stay bit-identical).
+#include "launch.hpp"
+
+namespace muz {
+
+enum { LN_MODE_PLAIN = 0, LN_MODE_RELU = 1, LN_MODE_RESID_RELU = 2 };
+constexpr int kLnRowsPerBlock = 16;   // backward: rows per workgroup (4 waves x 4 rows)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ y, const float* __restrict__ bias,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                const float* __restrict__ res, int M, int mode, float* __restrict__ out,
+                                                float* __restrict__ z, float* __restrict__ mean_out,
+                                                float* __restrict__ rstd_out) {
+  constexpr int E = (N + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const size_t row = (size_t)m * N;
+  float v[E];
+  float s = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < N ? y[row + c] + bias[c] : 0.f;
+    s += v[i];
+    s2 += v[i] * v[i];
+  }
+  s = wave_sum(s);
+  s2 = wave_sum(s2);
+  const float mean = s / (float)N;
+  const float rstd = 1.0f / sqrtf(fmaxf(0.f, s2 / (float)N - mean * mean) + 1e-6f);
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int c = lane + 64 * i;
+    if (c >= N) continue;
+    float o = (v[i] - mean) * (rstd * gamma[c]) + beta[c];
+    if (mode == LN_MODE_RELU) o = fmaxf(o, 0.f);
+    if (mode == LN_MODE_RESID_RELU) o = fmaxf(res[row + c] + o, 0.f);
+    out[row + c] = o;
+    z[row + c] = v[i];
+  }
+  if (lane == 0) {
+    mean_out[m] = mean;
+    rstd_out[m] = rstd;
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dout, const float* __restrict__ out,
+                                                const float* __restrict__ z, const float* __restrict__ mean_in,
+                                                const float* __restrict__ rstd_in, const float* __restrict__ gamma,
+                                                int M, int mode, float* __restrict__ dz, float* __restrict__ dres,
+                                                float* __restrict__ part) {
+  constexpr int E = (N + 63) / 64;
+  __shared__ float red[4][3][N];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float pg[E], pb[E], pd[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) pg[i] = pb[i] = pd[i] = 0.f;
+  for (int k = 0; k < kLnRowsPerBlock / 4; ++k) {
+    const int m = blockIdx.x * kLnRowsPerBlock + wv * (kLnRowsPerBlock / 4) + k;
+    if (m >= M) break;
+    const size_t row = (size_t)m * N;
+    const float mean = mean_in[m], rstd = rstd_in[m];
+    float d[E], xh[E], g[E];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const int c = lane + 64 * i;
+      d[i] = xh[i] = g[i] = 0.f;
+      if (c >= N) continue;
+      float t = dout[row + c];
+      if (mode != LN_MODE_PLAIN && !(out[row + c] > 0.f)) t = 0.f;
+      if (mode == LN_MODE_RESID_RELU) dres[row + c] = t;
+      d[i] = t;
+      xh[i] = (z[row + c] - mean) * rstd;
+      g[i] = t * gamma[c];
+      a += g[i];
+      b += g[i] * xh[i];
+    }
+    a = wave_sum(a) / (float)N;
+    b = wave_sum(b) / (float)N;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const int c = lane + 64 * i;
+      if (c >= N) continue;
+      const float dzi = rstd * (g[i] - a - xh[i] * b);
+      dz[row + c] = dzi;
+      pg[i] += d[i] * xh[i];
+      pb[i] += d[i];
+      pd[i] += dzi;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int c = lane + 64 * i;
+    if (c >= N) continue;
+    red[wv][0][c] = pg[i];
+    red[wv][1][c] = pb[i];
+    red[wv][2][c] = pd[i];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 3 * N; t += 256) {
+    const int q = t / N, c = t % N;
+    part[((size_t)blockIdx.x * 3 + q) * N + c] = ((red[0][q][c] + red[1][q][c]) + red[2][q][c]) + red[3][q][c];
+  }
+}
+
+// column sums of the per-block partials, blocks in order
+__global__ __launch_bounds__(256) void k_ln_colsum(const float* __restrict__ part, int nblk, int N,
+                                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                   float* __restrict__ dbias) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= 3 * N) return;
+  const int q = t / N, c = t % N;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[((size_t)b * 3 + q) * N + c];
+  (q == 0 ? dgamma : q == 1 ? dbeta : dbias)[c] = s;
+}
+
+static bool ln_width_ok(int N) { return N == 32 || N == 64 || N == 128 || N == 256; }
+
+}  // namespace muz
+
+using namespace muz;
+
+extern "C" {
+
+int muz_ln_fwd(const float* y, const float* bias, const float* gamma, const float* beta, const float* res, int32_t M,
+               int32_t N, int32_t mode, float* out, float* z, float* mean, float* rstd, void* stream) {
+  if (!ln_width_ok(N) || mode < 0 || mode > 2) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(M >= 0 && y && bias && gamma && beta && out && z && mean && rstd);
+  MUZ_HOST_CHECK((mode == LN_MODE_RESID_RELU) == (res != nullptr));
+  if (M == 0) return MUZ_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (M + 3) / 4;
+#define MUZ_LN_FWD(n) k_ln_fwd<n><<<grid, 256, 0, s>>>(y, bias, gamma, beta, res, M, mode, out, z, mean, rstd)
+  switch (N) {
+    case 32: MUZ_LN_FWD(32); break;
+    case 64: MUZ_LN_FWD(64); break;
+    case 128: MUZ_LN_FWD(128); break;
+    default: MUZ_LN_FWD(256); break;
+  }
+#undef MUZ_LN_FWD
+  return muz_last_launch_error();
+}
+
+int64_t muz_ln_bwd_scratch_floats(int32_t M, int32_t N) {
+  if (M < 0 || !ln_width_ok(N)) return -1;
+  return (int64_t)((M + kLnRowsPerBlock - 1) / kLnRowsPerBlock) * 3 * N;
+}
+
+int muz_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
+               const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
+               float* dgamma, float* dbeta, float* dbias, void* stream) {
+  if (!ln_width_ok(N) || mode < 0 || mode > 2) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(M >= 0 && dout && out && z && mean && rstd && gamma && dz && scratch && dgamma && dbeta && dbias);
+  MUZ_HOST_CHECK((mode == LN_MODE_RESID_RELU) == (dres != nullptr));
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = (M + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
+  if (M > 0) {
+#define MUZ_LN_BWD(n) k_ln_bwd<n><<<nblk, 256, 0, s>>>(dout, out, z, mean, rstd, gamma, M, mode, dz, dres, scratch)
+    switch (N) {
+      case 32: MUZ_LN_BWD(32); break;
+      case 64: MUZ_LN_BWD(64); break;
+      case 128: MUZ_LN_BWD(128); break;
+      default: MUZ_LN_BWD(256); break;
+    }
+#undef MUZ_LN_BWD
+    int rc = muz_last_launch_error();
+    if (rc) return rc;
+  }
+  k_ln_colsum<<<(3 * N + 255) / 256, 256, 0, s>>>(scratch, nblk, N, dgamma, dbeta, dbias);
+  return muz_last_launch_error();
+}
+
+}  // extern "C"

@@ -24,10 +24,51 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import lib as _L
 from . import nets as N
 
 EPS_LN = 1e-6
 VALUE_SCALING, POLICY_SCALING, DISCOUNT_SCALING, REWARD_SCALING = 4.0, 1.0, 1.0, 1.0
+
+
+LN_PLAIN, LN_RELU, LN_RESID_RELU = 0, 1, 2
+
+
+class _DenseLN(torch.autograd.Function):
+    """act(LayerNorm(x @ W + b)) with the GEMMs on the BLAS library and the bias / LayerNorm / ReLU / residual
+    epilogue and its backward as the fused kernels of csrc/learner_ln.hip (one launch forward, two backward,
+    instead of ~8 small ones).  mode LN_RELU: relu(LN(.)); LN_RESID_RELU: relu(res + LN(.)); LN_PLAIN: LN(.)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, gamma, beta, res, mode):
+        lib = _L.load()
+        y = x @ W
+        M, Nn = y.shape
+        out, z = torch.empty_like(y), torch.empty_like(y)
+        mean = torch.empty((M,), dtype=y.dtype, device=y.device)
+        rstd = torch.empty_like(mean)
+        _L.check(lib.muz_ln_fwd(_L.ptr(y), _L.ptr(b), _L.ptr(gamma), _L.ptr(beta), _L.ptr(res), M, Nn, mode,
+                                _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.stream_ptr()), "muz_ln_fwd")
+        ctx.save_for_backward(x, W, gamma, out, z, mean, rstd)
+        ctx.mode = mode
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _L.load()
+        x, W, gamma, out, z, mean, rstd = ctx.saved_tensors
+        dout = dout.contiguous()
+        M, Nn = out.shape
+        dz = torch.empty_like(out)
+        dres = torch.empty_like(out) if ctx.mode == LN_RESID_RELU else None
+        scratch = torch.empty((lib.muz_ln_bwd_scratch_floats(M, Nn),), dtype=out.dtype, device=out.device)
+        dgamma, dbeta, db = (torch.empty((Nn,), dtype=out.dtype, device=out.device) for _ in range(3))
+        _L.check(lib.muz_ln_bwd(_L.ptr(dout), _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.ptr(gamma), M, Nn,
+                                ctx.mode, _L.ptr(dz), _L.ptr(dres), _L.ptr(scratch), _L.ptr(dgamma), _L.ptr(dbeta),
+                                _L.ptr(db), _L.stream_ptr()), "muz_ln_bwd")
+        dx = dz @ W.t() if ctx.needs_input_grad[0] else None
+        dW = x.t() @ dz if ctx.needs_input_grad[1] else None
+        return dx, dW, db, dgamma, dbeta, dres, None
 
 
 class MuZeroNets:
@@ -59,10 +100,23 @@ class MuZeroNets:
         # ~1e-7 relative on these activations (tests/test_learner.py holds the forward to 1e-5)
         return F.layer_norm(x, (x.shape[-1],), self.p[f"{name}/scale"], self.p[f"{name}/bias"], EPS_LN)
 
-    def _conv(self, name, x):
-        """Flax Conv 'SAME', stride 1, NWC input [B, W, Cin] -> [B, W, Cout], as im2col + one GEMM (the kernel
-        (K, Cin, Cout) is already the [K * Cin, Cout] matrix).  MIOpen's conv1d picks algorithms that
-        accumulate with atomics (run-to-run different losses and gradients, measured:
+    def _dense_ln(self, dense, ln, x, mode=LN_RELU, res=None, W=None):
+        """act(LayerNorm(Dense(x))) (mode: LN_RELU, LN_RESID_RELU = relu(res + .), LN_PLAIN).  On the GPU the
+        fused epilogue of csrc/learner_ln.hip; on the CPU (the host tests) the same layers as torch ops."""
+        W = self.p[f"{dense}/kernel"] if W is None else W
+        if x.is_cuda:
+            lead, Nn = x.shape[:-1], W.shape[-1]
+            r = None if res is None else res.reshape(-1, Nn).contiguous()
+            out = _DenseLN.apply(x.reshape(-1, x.shape[-1]).contiguous(), W, self.p[f"{dense}/bias"],
+                                 self.p[f"{ln}/scale"], self.p[f"{ln}/bias"], r, mode)
+            return out.reshape(*lead, Nn)
+        y = self._ln(ln, x @ W + self.p[f"{dense}/bias"])
+        return F.relu(y) if mode == LN_RELU else (F.relu(res + y) if mode == LN_RESID_RELU else y)
+
+    def _conv_cols(self, name, x):
+        """Flax Conv 'SAME', stride 1, NWC input [B, W, Cin]: the im2col matrix [B, W, K * Cin] and the kernel
+        (K, Cin, Cout) as the [K * Cin, Cout] matrix, so the conv is one GEMM.  MIOpen's conv1d picks
+        algorithms that accumulate with atomics (run-to-run different losses and gradients, measured:
         profiles/learner_determinism.py); the GEMM form is deterministic, so eager and graph-captured steps
         are bit-identical."""
         k = self.p[f"{name}/kernel"]
@@ -70,13 +124,11 @@ class MuZeroNets:
         pl = (K - 1) // 2
         W = x.shape[1]
         xp = F.pad(x, (0, 0, pl, K - 1 - pl))
-        cols = torch.cat([xp[:, d:d + W, :] for d in range(K)], dim=-1)      # [B, W, K * Cin]
-        return cols @ k.reshape(K * Cin, Cout) + self.p[f"{name}/bias"]
+        return torch.cat([xp[:, d:d + W, :] for d in range(K)], dim=-1), k.reshape(K * Cin, Cout)
 
     def _rb(self, name, x):
-        y = F.relu(self._ln(f"{name}/LayerNorm_0", self._dense(f"{name}/Dense_0", x)))
-        y = self._ln(f"{name}/LayerNorm_1", self._dense(f"{name}/Dense_1", y))
-        return F.relu(x + y)
+        y = self._dense_ln(f"{name}/Dense_0", f"{name}/LayerNorm_0", x, LN_RELU)
+        return self._dense_ln(f"{name}/Dense_1", f"{name}/LayerNorm_1", y, LN_RESID_RELU, res=x)
 
     @staticmethod
     def _minmax(x):
@@ -90,11 +142,12 @@ class MuZeroNets:
         sp = obs[:, :6, :].transpose(1, 2)
         g = obs[:, 6:, 0]
         for i in range(3):
-            sp = F.relu(self._ln(f"{r}/LayerNorm_{i}", self._conv(f"{r}/Conv_{i}", sp)))
-        flat = F.relu(self._ln(f"{r}/LayerNorm_3", self._dense(f"{r}/Dense_0", sp.reshape(sp.shape[0], -1))))
-        g = F.relu(self._ln(f"{r}/LayerNorm_4", self._dense(f"{r}/Dense_1", g)))
-        g = F.relu(self._ln(f"{r}/LayerNorm_5", self._dense(f"{r}/Dense_2", g)))
-        h = F.relu(self._ln(f"{r}/LayerNorm_6", self._dense(f"{r}/Dense_3", torch.cat([flat, g], -1))))
+            cols, k = self._conv_cols(f"{r}/Conv_{i}", sp)
+            sp = self._dense_ln(f"{r}/Conv_{i}", f"{r}/LayerNorm_{i}", cols, LN_RELU, W=k)
+        flat = self._dense_ln(f"{r}/Dense_0", f"{r}/LayerNorm_3", sp.reshape(sp.shape[0], -1))
+        g = self._dense_ln(f"{r}/Dense_1", f"{r}/LayerNorm_4", g)
+        g = self._dense_ln(f"{r}/Dense_2", f"{r}/LayerNorm_5", g)
+        h = self._dense_ln(f"{r}/Dense_3", f"{r}/LayerNorm_6", torch.cat([flat, g], -1))
         for b in range(6):
             h = self._rb(f"{r}/ResBlock_{b}", h)
         return self._minmax(self._dense(f"{r}/Dense_4", h))
@@ -112,8 +165,8 @@ class MuZeroNets:
         """latent -> next latent (the sequential part of the unroll)."""
         d = "dynamics"
         x = self._ln(f"{d}/LayerNorm_0", latent) * (1.0 + scale) + shift
-        x = F.relu(self._ln(f"{d}/LayerNorm_1", self._dense(f"{d}/Dense_3", x)))
-        x = F.relu(self._ln(f"{d}/LayerNorm_2", self._dense(f"{d}/Dense_4", x)))
+        x = self._dense_ln(f"{d}/Dense_3", f"{d}/LayerNorm_1", x)
+        x = self._dense_ln(f"{d}/Dense_4", f"{d}/LayerNorm_2", x)
         for b in range(2):
             x = self._rb(f"{d}/ResBlock_{b}", x)
         return self._minmax(latent + self._dense(f"{d}/Dense_5", x))
@@ -137,10 +190,10 @@ class MuZeroNets:
         x = self._ln(f"{p}/LayerNorm_0", latent)
         for b in range(2):
             x = self._rb(f"{p}/ResBlock_{b}", x)
-        pol = F.relu(self._ln(f"{p}/LayerNorm_1", self._dense(f"{p}/Dense_0", x)))
-        pol = F.relu(self._ln(f"{p}/LayerNorm_2", self._dense(f"{p}/Dense_1", pol)))
+        pol = self._dense_ln(f"{p}/Dense_0", f"{p}/LayerNorm_1", x)
+        pol = self._dense_ln(f"{p}/Dense_1", f"{p}/LayerNorm_2", pol)
         logits = self._dense(f"{p}/Dense_2", pol)
-        v = F.relu(self._ln(f"{p}/LayerNorm_3", self._dense(f"{p}/Dense_3", x)))
+        v = self._dense_ln(f"{p}/Dense_3", f"{p}/LayerNorm_3", x)
         v = F.relu(self._dense(f"{p}/Dense_4", v))
         return logits, torch.tanh(self._dense(f"{p}/Dense_5", v))
 
@@ -361,8 +414,8 @@ class ClassicMuZeroNets(MuZeroNets):
         d = "dynamics"
         ln = self._ln(f"{d}/{pre}_input_ln", x_in)
         x = ln * (1.0 + self._dense(f"{d}/{pre}_film_scale", e)) + self._dense(f"{d}/{pre}_film_shift", e)
-        x = F.relu(self._ln(f"{d}/{pre}_ln1", self._dense(f"{d}/{pre}_dense1", x)))
-        x = F.relu(self._ln(f"{d}/{pre}_ln2", self._dense(f"{d}/{pre}_dense2", x)))
+        x = self._dense_ln(f"{d}/{pre}_dense1", f"{d}/{pre}_ln1", x)
+        x = self._dense_ln(f"{d}/{pre}_dense2", f"{d}/{pre}_ln2", x)
         for r in range(rb0, rb0 + 2):
             x = self._rb(f"{d}/ResBlock_{r}", x)
         return self._minmax(x_in + self._dense(f"{d}/{pre}_proj", x))
@@ -381,8 +434,7 @@ class ClassicMuZeroNets(MuZeroNets):
         """(reward, chance, discount) logits of action_dynamics; row-wise, batchable over unroll steps."""
         d = "dynamics"
         rl = self._dense(f"{d}/reward_head", F.relu(self._dense(f"{d}/reward_dense", torch.cat([after, oh], -1))))
-        dl = self._dense(f"{d}/discount_head",
-                         F.relu(self._ln(f"{d}/discount_ln", self._dense(f"{d}/discount_dense", latent))))
+        dl = self._dense(f"{d}/discount_head", self._dense_ln(f"{d}/discount_dense", f"{d}/discount_ln", latent))
         cl = self._dense(f"{d}/chance_head", after)
         return rl, cl, dl
 

@@ -278,6 +278,11 @@ SIGNATURES = {
     "muz_detmadn_selfplay": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzNetW),
                                             ctypes.POINTER(MuzSearchCfg), MuzDetSoA, MuzTraj, ctypes.c_int32, vp,
                                             ctypes.c_int64, ctypes.POINTER(MuzSpStats), vp]),
+    "muz_ln_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp,
+                                  vp]),
+    "muz_ln_bwd_scratch_floats": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    "muz_ln_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
+                                  vp, vp, vp, vp]),
     "muz_detmadn_selfplay_stream": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzNetW),
                                                    ctypes.POINTER(MuzSearchCfg), MuzDetSoA, MuzTraj, ctypes.c_int32,
                                                    ctypes.c_int32, vp, ctypes.c_int64, ctypes.POINTER(MuzSpStats),

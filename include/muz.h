@@ -651,6 +651,22 @@ int muz_ring_save_packed(muz_ring ring, muz_traj packed, const muz_traj_chance* 
                          int32_t n, int32_t max_len, int32_t position, int32_t* slot_out, int32_t* count_out,
                          void* stream);
 
+/* ---- learner support (config (e); not a reference FFI entry point) --------------------------------
+ * The Dense -> LayerNorm -> ReLU blocks of the unrolled MuZero loss (train_with_reward.py:24-141,
+ * train_stochastic.py:34-181; Flax LayerNorm eps 1e-6, fast variance) as one fused epilogue after a
+ * library GEMM, and its backward (csrc/learner_ln.hip).  y, res, out, z, dout, dz, dres: device float
+ * [M][N] row-major; bias, gamma, beta, dgamma, dbeta, dbias: [N]; mean, rstd: [M]; N in {32, 64, 128, 256}.
+ * mode 0: out = LN(y + bias); 1: relu(LN(y + bias)); 2: relu(res + LN(y + bias)) (res required exactly for
+ * mode 2, and dres for its backward).  z, mean, rstd, out are the forward's saved values. */
+int muz_ln_fwd(const float* y, const float* bias, const float* gamma, const float* beta, const float* res, int32_t M,
+               int32_t N, int32_t mode, float* out, float* z, float* mean, float* rstd, void* stream);
+/* device float scratch muz_ln_bwd needs for M rows of width N (-1 for an unsupported N). */
+int64_t muz_ln_bwd_scratch_floats(int32_t M, int32_t N);
+/* dz = d(y) (= the GEMM output's gradient); dgamma / dbeta / dbias: column sums (deterministic order). */
+int muz_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
+               const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
+               float* dgamma, float* dbeta, float* dbias, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -160,3 +160,41 @@ def test_config_e_iteration_at_its_shape(cuda):
         f"6 learner steps at batch 128 / unroll 10 (losses {[round(float(x['total_loss']), 4) for x in losses]}), "
         f"pushed arena vs torch forward max |d| {err:.2e}")
     assert err <= 1e-5, err
+
+
+@pytest.mark.parametrize("N,mode", [(32, 1), (64, 1), (128, 0), (256, 1), (256, 2)])
+def test_fused_dense_layernorm_matches_float64_autograd(cuda, N, mode):
+    """csrc/learner_ln.hip (bias + Flax LayerNorm + ReLU / residual ReLU, forward and backward) against float64
+    autograd of the same expression; M = 300 rows (a partial backward block) and K = 96."""
+    _, _, L, _, _ = _mods()
+    g = torch.Generator().manual_seed(10 * N + mode)
+    M, K = 300, 96
+    x = torch.randn(M, K, generator=g, dtype=torch.float64)
+    W = torch.randn(K, N, generator=g, dtype=torch.float64) * 0.2
+    b, gam, bet = (torch.randn(N, generator=g, dtype=torch.float64) * s for s in (0.3, 1.0, 0.3))
+    res = torch.randn(M, N, generator=g, dtype=torch.float64) if mode == 2 else None
+    dout = torch.randn(M, N, generator=g, dtype=torch.float64)
+
+    def ref(x, W, b, gam, bet, res):
+        z = x @ W + b
+        mean = z.mean(-1, keepdim=True)
+        var = (z * z).mean(-1, keepdim=True) - mean * mean          # Flax's fast variance
+        y = (z - mean) / torch.sqrt(var + 1e-6) * gam + bet
+        return y if mode == 0 else (torch.relu(y) if mode == 1 else torch.relu(res + y))
+
+    leaves = [t.clone().requires_grad_(True) for t in (x, W, b, gam, bet)] + ([res.clone().requires_grad_(True)]
+                                                                               if res is not None else [])
+    out_ref = ref(*leaves[:5], leaves[5] if res is not None else None)
+    grads_ref = torch.autograd.grad(out_ref, leaves, dout)
+    dev = [t.detach().float().cuda().requires_grad_(True) for t in leaves]
+    out = L._DenseLN.apply(dev[0], dev[1], dev[2], dev[3], dev[4], dev[5] if res is not None else None, mode)
+    grads = torch.autograd.grad(out, dev, dout.float().cuda())
+    torch.cuda.synchronize()
+
+    def close(a, r, what):
+        a, r = a.detach().double().cpu(), r.detach()
+        err = (a - r).abs().max().item() / max(1.0, r.abs().max().item())
+        assert err < 2e-5, f"{what}: relative error {err:.2e}"
+    close(out, out_ref, "out")
+    for name, gg, gr in zip(("dx", "dW", "dbias", "dgamma", "dbeta", "dres"), grads, grads_ref):
+        close(gg, gr, name)
