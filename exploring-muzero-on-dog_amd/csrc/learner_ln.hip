@@ -19,7 +19,7 @@
 namespace muz {
 
 enum { LN_MODE_PLAIN = 0, LN_MODE_RELU = 1, LN_MODE_RESID_RELU = 2 };
-constexpr int kLnRowsPerBlock = 16;   // backward: rows per workgroup (4 waves x 4 rows)
+constexpr int kLnRowsPerBlock = 4;    // backward: rows per workgroup (one per wave: these launches are latency-bound)
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -128,16 +128,23 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dout, 
   }
 }
 
-// column sums of the per-block partials, blocks in order
+// column sums of the per-block partials: workgroup (q, 64-column chunk); thread (j, c) sums blocks j, j + 4,
+// j + 8, ... in order, then the 4 partial sums are added in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void k_ln_colsum(const float* __restrict__ part, int nblk, int N,
                                                    float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                    float* __restrict__ dbias) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= 3 * N) return;
-  const int q = t / N, c = t % N;
+  __shared__ float red[4][64];
+  const int chunks = (N + 63) / 64;
+  const int q = blockIdx.x / chunks, c = (blockIdx.x % chunks) * 64 + (threadIdx.x & 63), j = threadIdx.x >> 6;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[((size_t)b * 3 + q) * N + c];
-  (q == 0 ? dgamma : q == 1 ? dbeta : dbias)[c] = s;
+  if (c < N)
+    for (int b = j; b < nblk; b += 4) s += part[((size_t)b * 3 + q) * N + c];
+  red[j][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (j == 0 && c < N) {
+    const int t = threadIdx.x & 63;
+    (q == 0 ? dgamma : q == 1 ? dbeta : dbias)[c] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+  }
 }
 
 static bool ln_width_ok(int N) { return N == 32 || N == 64 || N == 128 || N == 256; }
@@ -192,7 +199,7 @@ int muz_ln_bwd(const float* dout, const float* out, const float* z, const float*
     int rc = muz_last_launch_error();
     if (rc) return rc;
   }
-  k_ln_colsum<<<(3 * N + 255) / 256, 256, 0, s>>>(scratch, nblk, N, dgamma, dbeta, dbias);
+  k_ln_colsum<<<3 * ((N + 63) / 64), 256, 0, s>>>(scratch, nblk, N, dgamma, dbeta, dbias);
   return muz_last_launch_error();
 }
 

@@ -291,7 +291,8 @@ class AdamW:
     @torch.no_grad()
     def step(self):
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
-        g_norm = torch.sqrt(torch.stack([torch.sum(g * g) for g in grads]).sum())
+        # per-tensor norms in one multi-tensor kernel (a sum(g * g) per tensor was ~200 launches per step)
+        g_norm = torch.sqrt(torch.stack(torch._foreach_norm(grads)).square().sum())
         trigger = g_norm < self.max_norm
         denom = torch.where(trigger, torch.ones_like(g_norm), g_norm)
         mult = torch.where(trigger, torch.ones_like(g_norm), torch.full_like(g_norm, self.max_norm))
