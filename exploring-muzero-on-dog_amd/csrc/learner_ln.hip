@@ -179,11 +179,11 @@ int64_t muz_ln_bwd_scratch_floats(int32_t M, int32_t N) {
   return (int64_t)((M + kLnRowsPerBlock - 1) / kLnRowsPerBlock) * 3 * N;
 }
 
-int muz_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
-               const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
-               float* dgamma, float* dbeta, float* dbias, void* stream) {
+int muz_ln_bwd_rows(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
+                    const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
+                    void* stream) {
   if (!ln_width_ok(N) || mode < 0 || mode > 2) return MUZ_E_UNSUPPORTED;
-  MUZ_HOST_CHECK(M >= 0 && dout && out && z && mean && rstd && gamma && dz && scratch && dgamma && dbeta && dbias);
+  MUZ_HOST_CHECK(M >= 0 && dout && out && z && mean && rstd && gamma && dz && scratch);
   MUZ_HOST_CHECK((mode == LN_MODE_RESID_RELU) == (dres != nullptr));
   hipStream_t s = (hipStream_t)stream;
   const int nblk = (M + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
@@ -196,11 +196,26 @@ int muz_ln_bwd(const float* dout, const float* out, const float* z, const float*
       default: MUZ_LN_BWD(256); break;
     }
 #undef MUZ_LN_BWD
-    int rc = muz_last_launch_error();
-    if (rc) return rc;
+    return muz_last_launch_error();
   }
-  k_ln_colsum<<<3 * ((N + 63) / 64), 256, 0, s>>>(scratch, nblk, N, dgamma, dbeta, dbias);
+  return MUZ_OK;
+}
+
+int muz_ln_colsum(const float* scratch, int64_t nblk, int32_t N, float* dgamma, float* dbeta, float* dbias,
+                  void* stream) {
+  if (!ln_width_ok(N)) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(nblk >= 0 && nblk <= INT32_MAX && scratch && dgamma && dbeta && dbias);
+  k_ln_colsum<<<3 * ((N + 63) / 64), 256, 0, (hipStream_t)stream>>>(scratch, (int)nblk, N, dgamma, dbeta, dbias);
   return muz_last_launch_error();
+}
+
+int muz_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
+               const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
+               float* dgamma, float* dbeta, float* dbias, void* stream) {
+  MUZ_HOST_CHECK(dgamma && dbeta && dbias);
+  const int rc = muz_ln_bwd_rows(dout, out, z, mean, rstd, gamma, M, N, mode, dz, dres, scratch, stream);
+  if (rc) return rc;
+  return muz_ln_colsum(scratch, muz_ln_bwd_scratch_floats(M, N) / (3 * N), N, dgamma, dbeta, dbias, stream);
 }
 
 }  // extern "C"

@@ -71,6 +71,147 @@ class _DenseLN(torch.autograd.Function):
         return dx, dW, db, dgamma, dbeta, dres, None
 
 
+def _ln_fwd(y, bias, gamma, beta, res, mode):
+    """Fused bias + LayerNorm (+ ReLU / residual ReLU) forward: -> (out, z, mean, rstd) (no autograd)."""
+    M, Nn = y.shape
+    out, z = torch.empty_like(y), torch.empty_like(y)
+    mean = torch.empty((M,), dtype=y.dtype, device=y.device)
+    rstd = torch.empty_like(mean)
+    _L.check(_L.load().muz_ln_fwd(_L.ptr(y), _L.ptr(bias), _L.ptr(gamma), _L.ptr(beta), _L.ptr(res), M, Nn, mode,
+                                  _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.stream_ptr()), "muz_ln_fwd")
+    return out, z, mean, rstd
+
+
+def _ln_bwd_rows(dout, fwd, gamma, mode, scratch):
+    """Row half of the fused backward: -> (dz, dres or None); column partials into scratch."""
+    out, z, mean, rstd = fwd
+    M, Nn = out.shape
+    dout = dout.contiguous()
+    dz = torch.empty_like(out)
+    dres = torch.empty_like(out) if mode == LN_RESID_RELU else None
+    _L.check(_L.load().muz_ln_bwd_rows(_L.ptr(dout), _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.ptr(gamma),
+                                       M, Nn, mode, _L.ptr(dz), _L.ptr(dres), _L.ptr(scratch), _L.stream_ptr()),
+             "muz_ln_bwd_rows")
+    return dz, dres
+
+
+def _ln_colsum(scratch, Nn):
+    """-> (dgamma, dbeta, dbias) from the column partials of any number of row-half calls."""
+    dg, db_, dbias = (torch.empty((Nn,), dtype=scratch.dtype, device=scratch.device) for _ in range(3))
+    _L.check(_L.load().muz_ln_colsum(_L.ptr(scratch), scratch.numel() // (3 * Nn), Nn, _L.ptr(dg), _L.ptr(db_),
+                                     _L.ptr(dbias), _L.stream_ptr()), "muz_ln_colsum")
+    return dg, db_, dbias
+
+
+DYN_TRUNK_PARAMS = (["dynamics/LayerNorm_0/scale", "dynamics/LayerNorm_0/bias"] +
+                    [f"dynamics/{n}" for n in ("Dense_3/kernel", "Dense_3/bias", "LayerNorm_1/scale", "LayerNorm_1/bias",
+                                               "Dense_4/kernel", "Dense_4/bias", "LayerNorm_2/scale", "LayerNorm_2/bias")] +
+                    [f"dynamics/ResBlock_{r}/{n}" for r in range(2)
+                     for n in ("Dense_0/kernel", "Dense_0/bias", "LayerNorm_0/scale", "LayerNorm_0/bias",
+                               "Dense_1/kernel", "Dense_1/bias", "LayerNorm_1/scale", "LayerNorm_1/bias")] +
+                    ["dynamics/Dense_5/kernel", "dynamics/Dense_5/bias"])
+
+
+class _DynChain(torch.autograd.Function):
+    """The K sequential DynamicsNetwork4 trunk steps of the unrolled loss (loss_fn: latent_{k+1} =
+    trunk(latent_k, FiLM_k) with the gradient through each new latent scaled by grad_scale) as ONE autograd
+    node.  Forward = the fused kernels of csrc/learner_ln.hip + library GEMMs; the hand-written backward walks
+    the steps in reverse and, because every step uses the same weights, forms each weight gradient with ONE
+    GEMM over all K steps and each LayerNorm / bias gradient with ONE column sum (per-step autograd made ten
+    GEMMs, ten column sums and nine accumulation adds per parameter).  min / max follow torch's backward (the
+    gradient goes to the returned index).  Inputs: latent_0 [B, 256], FiLM scale / shift [K, B, 256], params in
+    DYN_TRUNK_PARAMS order.  Output: latents 1..K as [K, B, 256]."""
+
+    @staticmethod
+    def forward(ctx, latent0, scale, shift, grad_scale, *P):
+        g0, be0, W3, b3, g1, be1, W4, b4, g2, be2 = P[:10]
+        W5, b5 = P[26], P[27]
+        K, B, Nn = scale.shape
+        zero = torch.zeros((Nn,), dtype=latent0.dtype, device=latent0.device)
+        outs = torch.empty((K, B, Nn), dtype=latent0.dtype, device=latent0.device)
+        st = []
+        lat = latent0.contiguous()
+        for k in range(K):
+            f0 = _ln_fwd(lat, zero, g0, be0, None, LN_PLAIN)
+            x0 = f0[0] * (1.0 + scale[k]) + shift[k]
+            f3 = _ln_fwd(x0 @ W3, b3, g1, be1, None, LN_RELU)
+            f4 = _ln_fwd(f3[0] @ W4, b4, g2, be2, None, LN_RELU)
+            x, rbs = f4[0], []
+            for r in range(2):
+                Wa, ba, ga, bea, Wb, bb, gb, beb = P[10 + 8 * r:18 + 8 * r]
+                fa = _ln_fwd(x @ Wa, ba, ga, bea, None, LN_RELU)
+                fb = _ln_fwd(fa[0] @ Wb, bb, gb, beb, x, LN_RESID_RELU)
+                rbs.append((x, fa, fb))
+                x = fb[0]
+            q = lat + (x @ W5 + b5)
+            lo, ilo = q.min(-1, keepdim=True)
+            hi, ihi = q.max(-1, keepdim=True)
+            nxt = (q - lo) / (hi - lo + 1e-8)
+            outs[k] = nxt
+            st.append((f0, x0, f3, f4, rbs, x, q, lo, hi, ilo, ihi))
+            lat = nxt
+        ctx.st, ctx.P, ctx.grad_scale = st, P, float(grad_scale)
+        ctx.save_for_backward(scale)
+        return outs
+
+    @staticmethod
+    def backward(ctx, G):
+        (scale,) = ctx.saved_tensors
+        P, st, s = ctx.P, ctx.st, ctx.grad_scale
+        g0, g1, g2 = P[0], P[4], P[8]
+        W3, W4, W5 = P[2], P[6], P[26]
+        K, B, Nn = scale.shape
+        G = G.contiguous()
+        dev, dt = G.device, G.dtype
+        nf = _L.load().muz_ln_bwd_scratch_floats(B, Nn)
+        scr = {n: torch.empty((K, nf), dtype=dt, device=dev) for n in ("0", "3", "4", "a0", "b0", "a1", "b1")}
+        cols = {n: ([], []) for n in ("3", "4", "a0", "b0", "a1", "b1", "5")}      # (layer inputs, output grads)
+        dscale, dshift = torch.empty_like(scale), torch.empty_like(scale)
+        carry = None
+        for k in range(K - 1, -1, -1):
+            f0, x0, f3, f4, rbs, x5, q, lo, hi, ilo, ihi = st[k]
+            dnxt = (G[k] if carry is None else G[k] + carry) * s
+            den = hi - lo + 1e-8
+            dq = dnxt / den
+            t = (dnxt * (q - lo)).sum(-1, keepdim=True) / (den * den)
+            dq.scatter_add_(-1, ilo, -dnxt.sum(-1, keepdim=True) / den + t)
+            dq.scatter_add_(-1, ihi, -t)
+            cols["5"][0].append(x5)
+            cols["5"][1].append(dq)
+            dx = dq @ W5.t()
+            for r in (1, 0):
+                xin, fa, fb = rbs[r]
+                Wa, Wb, ga, gb = P[10 + 8 * r], P[14 + 8 * r], P[12 + 8 * r], P[16 + 8 * r]
+                dzb, dres = _ln_bwd_rows(dx, fb, gb, LN_RESID_RELU, scr[f"b{r}"][k])
+                cols[f"b{r}"][0].append(fa[0])
+                cols[f"b{r}"][1].append(dzb)
+                dza, _ = _ln_bwd_rows(dzb @ Wb.t(), fa, ga, LN_RELU, scr[f"a{r}"][k])
+                cols[f"a{r}"][0].append(xin)
+                cols[f"a{r}"][1].append(dza)
+                dx = dres + dza @ Wa.t()
+            dz4, _ = _ln_bwd_rows(dx, f4, g2, LN_RELU, scr["4"][k])
+            cols["4"][0].append(f3[0])
+            cols["4"][1].append(dz4)
+            dz3, _ = _ln_bwd_rows(dz4 @ W4.t(), f3, g1, LN_RELU, scr["3"][k])
+            cols["3"][0].append(x0)
+            cols["3"][1].append(dz3)
+            dx0 = dz3 @ W3.t()
+            dscale[k] = dx0 * f0[0]
+            dshift[k] = dx0
+            dz0, _ = _ln_bwd_rows(dx0 * (1.0 + scale[k]), f0, g0, LN_PLAIN, scr["0"][k])
+            carry = dz0 + dq
+        grads = [None] * len(P)
+        grads[0], grads[1], _ = _ln_colsum(scr["0"], Nn)
+        for n, (iw, ib, ig, ibe) in (("3", (2, 3, 4, 5)), ("4", (6, 7, 8, 9)), ("a0", (10, 11, 12, 13)),
+                                     ("b0", (14, 15, 16, 17)), ("a1", (18, 19, 20, 21)), ("b1", (22, 23, 24, 25))):
+            X, DZ = (torch.cat(c, 0) for c in cols[n])
+            grads[iw] = X.t() @ DZ
+            grads[ig], grads[ibe], grads[ib] = _ln_colsum(scr[n], Nn)
+        X, DZ = (torch.cat(c, 0) for c in cols["5"])
+        grads[26], grads[27] = X.t() @ DZ, DZ.sum(0)
+        return (carry, dscale, dshift, None, *grads)
+
+
 class MuZeroNets:
     """Flax-named fp32 parameters of (RepresentationNetwork2, DynamicsNetwork4, PredictionNetwork4)."""
 
@@ -215,9 +356,14 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     # (same per-row arithmetic as the step-by-step loop of the reference; far fewer kernel launches).
     oh, scale, shift = nets.dynamics_film(acts[:, :K].transpose(0, 1).reshape(-1))
     latents = [latent]
-    for k in range(K):
-        nxt = nets.dynamics_trunk(latents[-1], scale[k * B:(k + 1) * B], shift[k * B:(k + 1) * B])
-        latents.append((nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale)   # gradient scaling (fwd identity)
+    if K and latent.is_cuda:     # the whole latent chain as one autograd node (fused kernels, batched weight grads)
+        chain = _DynChain.apply(latent, scale.reshape(K, B, -1), shift.reshape(K, B, -1), grad_scale,
+                                *(nets.p[n] for n in DYN_TRUNK_PARAMS))
+        latents += list(chain.unbind(0))
+    else:
+        for k in range(K):
+            nxt = nets.dynamics_trunk(latents[-1], scale[k * B:(k + 1) * B], shift[k * B:(k + 1) * B])
+            latents.append((nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale)   # gradient scaling (fwd identity)
     logits_all, v_all = nets.prediction(torch.cat(latents, 0))
     rl_all, dl_all = nets.dynamics_heads(torch.cat(latents[1:], 0), oh) if K else (None, None)
     # The per-step losses, all K (+1) steps at once ([K+1, B] views; row k = unroll step k).

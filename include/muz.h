@@ -662,6 +662,14 @@ int muz_ln_fwd(const float* y, const float* bias, const float* gamma, const floa
                int32_t N, int32_t mode, float* out, float* z, float* mean, float* rstd, void* stream);
 /* device float scratch muz_ln_bwd needs for M rows of width N (-1 for an unsupported N). */
 int64_t muz_ln_bwd_scratch_floats(int32_t M, int32_t N);
+/* The backward's two halves: muz_ln_bwd_rows writes dz (and dres) and the per-block column partials into
+ * scratch (muz_ln_bwd_scratch_floats(M, N) floats = nblk x 3 x N); muz_ln_colsum reduces nblk partial blocks
+ * (several calls' scratch laid end to end, e.g. one layer applied at every unroll step) in a fixed order. */
+int muz_ln_bwd_rows(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
+                    const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
+                    void* stream);
+int muz_ln_colsum(const float* scratch, int64_t nblk, int32_t N, float* dgamma, float* dbeta, float* dbias,
+                  void* stream);
 /* dz = d(y) (= the GEMM output's gradient); dgamma / dbeta / dbias: column sums (deterministic order). */
 int muz_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
                const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,

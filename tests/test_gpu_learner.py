@@ -198,3 +198,35 @@ def test_fused_dense_layernorm_matches_float64_autograd(cuda, N, mode):
     close(out, out_ref, "out")
     for name, gg, gr in zip(("dx", "dW", "dbias", "dgamma", "dbeta", "dres"), grads, grads_ref):
         close(gg, gr, name)
+
+
+def test_dynamics_chain_node_matches_per_step_autograd(cuda):
+    """learner._DynChain (the K-step latent chain as one autograd node, batched weight gradients) against the
+    per-step graph of the same layers (loss_fn's CPU-style loop run on the GPU): forward within 1e-5, gradients
+    of every input and parameter within 1e-5 relative (summation orders differ)."""
+    _, _, L, _, _ = _mods()
+    C, B, K = 18, 64, 6
+    nets = L.MuZeroNets(ON.init_params(C, seed=4, randomize_affine=True), C, 24, "cuda")
+    g = torch.Generator().manual_seed(3)
+    lat0 = torch.rand(B, 256, generator=g).cuda().requires_grad_(True)
+    scale = (0.3 * torch.randn(K, B, 256, generator=g)).cuda().requires_grad_(True)
+    shift = (0.3 * torch.randn(K, B, 256, generator=g)).cuda().requires_grad_(True)
+    w = torch.randn(K, B, 256, generator=g).cuda()
+    params = [nets.p[n] for n in L.DYN_TRUNK_PARAMS]
+    inputs = [lat0, scale, shift] + params
+
+    out = L._DynChain.apply(lat0, scale, shift, 0.5, *params)
+    g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs)
+    lats = [lat0]
+    for k in range(K):
+        nxt = nets.dynamics_trunk(lats[-1], scale[k], shift[k])
+        lats.append((nxt * 0.5).detach() + nxt * 0.5)
+    ref = torch.stack(lats[1:])
+    g2 = torch.autograd.grad((ref * w).sum() + ref[-1].square().sum(), inputs)
+    torch.cuda.synchronize()
+    # (the per-step graph's first LayerNorm is torch's two-pass one, the node's the fused Flax fast-variance one)
+    assert (out - ref).abs().max().item() < 1e-5, "forward differs"
+    names = ["latent0", "scale", "shift"] + list(L.DYN_TRUNK_PARAMS)
+    for n, a, b in zip(names, g1, g2):
+        err = (a - b).abs().max().item() / max(1e-3, b.abs().max().item())
+        assert err < 1e-5, f"{n}: relative gradient difference {err:.2e}"
