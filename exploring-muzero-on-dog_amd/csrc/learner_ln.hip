@@ -129,16 +129,23 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dout, 
 }
 
 // column sums of the per-block partials: workgroup (q, 64-column chunk); thread (j, c) sums blocks j, j + 4,
-// j + 8, ... in order, then the 4 partial sums are added in a fixed order (deterministic)
+// j + 8, ..., then the 4 partial sums are added in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void k_ln_colsum(const float* __restrict__ part, int nblk, int N,
                                                    float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                    float* __restrict__ dbias) {
   __shared__ float red[4][64];
   const int chunks = (N + 63) / 64;
   const int q = blockIdx.x / chunks, c = (blockIdx.x % chunks) * 64 + (threadIdx.x & 63), j = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < N)
-    for (int b = j; b < nblk; b += 4) s += part[((size_t)b * 3 + q) * N + c];
+  // 8 independent accumulators (blocks j + 4 * (8 i + u)), so the loads of a thread overlap; combined in order
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    int b = j;
+    for (; b + 28 < nblk; b += 32)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += part[((size_t)(b + 4 * u) * 3 + q) * N + c];
+    for (; b < nblk; b += 4) acc[0] += part[((size_t)b * 3 + q) * N + c];
+  }
+  const float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   red[j][threadIdx.x & 63] = s;
   __syncthreads();
   if (j == 0 && c < N) {

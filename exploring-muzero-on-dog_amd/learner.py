@@ -146,8 +146,7 @@ class _DynChain(torch.autograd.Function):
             q = lat + (x @ W5 + b5)
             lo, ilo = q.min(-1, keepdim=True)
             hi, ihi = q.max(-1, keepdim=True)
-            nxt = (q - lo) / (hi - lo + 1e-8)
-            outs[k] = nxt
+            nxt = torch.div(q - lo, hi - lo + 1e-8, out=outs[k])
             st.append((f0, x0, f3, f4, rbs, x, q, lo, hi, ilo, ihi))
             lat = nxt
         ctx.st, ctx.P, ctx.grad_scale = st, P, float(grad_scale)
@@ -195,9 +194,8 @@ class _DynChain(torch.autograd.Function):
             dz3, _ = _ln_bwd_rows(dz4 @ W4.t(), f3, g1, LN_RELU, scr["3"][k])
             cols["3"][0].append(x0)
             cols["3"][1].append(dz3)
-            dx0 = dz3 @ W3.t()
-            dscale[k] = dx0 * f0[0]
-            dshift[k] = dx0
+            dx0 = torch.mm(dz3, W3.t(), out=dshift[k])
+            torch.mul(dx0, f0[0], out=dscale[k])
             dz0, _ = _ln_bwd_rows(dx0 * (1.0 + scale[k]), f0, g0, LN_PLAIN, scr["0"][k])
             carry = dz0 + dq
         grads = [None] * len(P)
