@@ -81,6 +81,10 @@ def parse():
     ap.add_argument("--train-steps", type=int, default=2500, help="train workload: learner steps per iteration")
     ap.add_argument("--workload", choices=("det", "classic", "dog", "train", "env", "selftest"), default="det",
                     help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
+    ap.add_argument("--records", action="store_true",
+                    help="dog: record every turn (muz_dog_random_play_record), pack the records each step and gather "
+                         "them to rank 0 (RCCL point-to-point at N > 1) inside the timed region -- config (d) as "
+                         "BASELINE.json names it")
     ap.add_argument("--split", action="store_true",
                     help="strong scaling (SURVEY §8e): --batch is the WHOLE job's batch, split evenly over the ranks "
                          "(det 4096 -> 2048/1024/512 per GPU); default is weak scaling, --batch games per GPU")
@@ -336,16 +340,37 @@ def run_dog(args):
     T = DOG_TURNS_PER_STEP
     rp = DG.RandomPlay(args.batch, seed=4 + 1000 * rank, fused=True)
     warm = torch.zeros(args.batch, dtype=torch.int32, device=device)
-    for _ in range(args.warmup):
-        rp.play(T, warm, auto_reset=True)
     env_steps = torch.zeros(args.batch, dtype=torch.int32, device=device)
     episodes = torch.zeros(args.batch, dtype=torch.int32, device=device)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    traj = DG.DogTrajectory(args.batch, T, device=device) if args.records else None
+    gathered = [0]
 
     def step(k):
         ev[k][0].record()
-        rp.play(T, env_steps, auto_reset=True, episodes=episodes)
+        if traj is not None:
+            traj.reset()
+        rp.play(T, env_steps, auto_reset=True, episodes=episodes, record=traj)
         ev[k][1].record()
+        if traj is not None:            # actor -> learner rank: pack the step's rows, gather them to rank 0
+            packed = traj.pack()
+            if dist is not None:
+                from exploring_muzero_on_dog_amd import transfer as TR
+                got = TR.gather_packed(packed, dst=0, spec=TR.dog_fields())
+                if got is not None:
+                    gathered[0] += sum(int(g["act"].shape[0]) for g in got)
+            else:
+                gathered[0] += int(packed["act"].shape[0])
+
+    for _ in range(args.warmup):        # the same calls as a timed step (record, pack and gather included)
+        if traj is not None:
+            traj.reset()
+        rp.play(T, warm, auto_reset=True, record=traj)
+        if traj is not None:
+            packed = traj.pack()
+            if dist is not None:
+                from exploring_muzero_on_dog_amd import transfer as TR
+                TR.gather_packed(packed, dst=0, spec=TR.dog_fields())
 
     elapsed = timed_region(dist, step, args.steps)
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev)
@@ -368,11 +393,15 @@ def run_dog(args):
         "data": "synthetic (seeded deals, counter-RNG random legal actions)", "games_finished": int(games),
         "config": {"workload": f"DOG 4p teams, {args.batch} games/GPU, uniform random legal action per turn, "
                                f"{T} turns per step in one launch (state resident in LDS), finished games "
-                               f"restart in place", "games_per_gpu": args.batch,
+                               f"restart in place" + (", every turn recorded, packed and gathered to rank 0"
+                                                      if args.records else ""), "games_per_gpu": args.batch,
+                   "records": bool(args.records),
                    "turns_per_step": T,
                    "parallelism": parallelism(args, world)},
         "roofline": dog_latency_model(avg_ms, args.batch, T, launch_bytes),
     }
+    if args.records:
+        out["records_gathered"] = int(gathered[0])
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = dog_cpu_baseline(min(args.cpu_seconds, 15.0))
     print(json.dumps(out), flush=True)

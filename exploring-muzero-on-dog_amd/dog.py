@@ -377,8 +377,14 @@ class DogTrajectory:
         """Rows [0, idx) of every lane, contiguous per lane in lane order (the packed layout of
         transfer.pack): every field [R] with R = sum(idx), plus idx [B] and row_offset [B] (int64)."""
         idx = self.buf["idx"]
-        keep = torch.arange(self.T, device=idx.device)[None, :] < idx[:, None]
-        out = {k: self.buf[k][keep] for k, _ in DOG_TRAJ_FIELDS}
+        full = int(idx.sum().item()) == self.batch * self.T      # one host sync
+        if full:        # every lane recorded T rows (e.g. auto-reset play): the [B, T] buffers are the packed rows
+            out = {k: self.buf[k].reshape(-1).clone() for k, _ in DOG_TRAJ_FIELDS}
+            out["row_offset"] = torch.arange(self.batch, dtype=torch.int64, device=idx.device) * self.T
+        else:
+            keep = torch.arange(self.T, device=idx.device)[None, :] < idx[:, None]
+            flat = keep.reshape(-1).nonzero().squeeze(1)
+            out = {k: self.buf[k].reshape(-1).index_select(0, flat) for k, _ in DOG_TRAJ_FIELDS}
+            out["row_offset"] = torch.cumsum(idx.to(torch.int64), 0) - idx.to(torch.int64)
         out["idx"] = idx.clone()
-        out["row_offset"] = torch.cumsum(idx.to(torch.int64), 0) - idx.to(torch.int64)
         return out
