@@ -46,7 +46,8 @@ def gpu_recurrent_fn(N, net):
 
 
 @pytest.mark.parametrize("P,S,D,rule_set", [(2, 50, 25, "selfplay_2p"), (4, 16, 4, "selfplay_4p_teams"),
-                                            (2, 8, 50, "selfplay_2p")])
+                                            (2, 8, 50, "selfplay_2p"),
+                                            (4, 100, 50, "selfplay_4p_teams")])   # config (e)'s search shape
 def test_search_logic_matches_mctx_restatement(cuda, P, S, D, rule_set):
     N, M, params, net, obs, valid, bits = setup(P, 48, 7, rule_set)
     B = obs.shape[0]
