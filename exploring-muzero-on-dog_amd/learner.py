@@ -103,111 +103,152 @@ def _ln_colsum(scratch, Nn):
     return dg, db_, dbias
 
 
-DYN_TRUNK_PARAMS = (["dynamics/LayerNorm_0/scale", "dynamics/LayerNorm_0/bias"] +
-                    [f"dynamics/{n}" for n in ("Dense_3/kernel", "Dense_3/bias", "LayerNorm_1/scale", "LayerNorm_1/bias",
-                                               "Dense_4/kernel", "Dense_4/bias", "LayerNorm_2/scale", "LayerNorm_2/bias")] +
-                    [f"dynamics/ResBlock_{r}/{n}" for r in range(2)
-                     for n in ("Dense_0/kernel", "Dense_0/bias", "LayerNorm_0/scale", "LayerNorm_0/bias",
-                               "Dense_1/kernel", "Dense_1/bias", "LayerNorm_1/scale", "LayerNorm_1/bias")] +
-                    ["dynamics/Dense_5/kernel", "dynamics/Dense_5/bias"])
+_RB_PARAMS = ("Dense_0/kernel", "Dense_0/bias", "LayerNorm_0/scale", "LayerNorm_0/bias",
+              "Dense_1/kernel", "Dense_1/bias", "LayerNorm_1/scale", "LayerNorm_1/bias")
 
 
-class _DynChain(torch.autograd.Function):
-    """The K sequential DynamicsNetwork4 trunk steps of the unrolled loss (loss_fn: latent_{k+1} =
-    trunk(latent_k, FiLM_k) with the gradient through each new latent scaled by grad_scale) as ONE autograd
-    node.  Forward = the fused kernels of csrc/learner_ln.hip + library GEMMs; the hand-written backward walks
-    the steps in reverse and, because every step uses the same weights, forms each weight gradient with ONE
-    GEMM over all K steps and each LayerNorm / bias gradient with ONE column sum (per-step autograd made ten
-    GEMMs, ten column sums and nine accumulation adds per parameter).  min / max follow torch's backward (the
-    gradient goes to the returned index).  Inputs: latent_0 [B, 256], FiLM scale / shift [K, B, 256], params in
-    DYN_TRUNK_PARAMS order.  Output: latents 1..K as [K, B, 256]."""
+def trunk_param_names(kind: str = "det") -> list:
+    """The 28 parameters of one FiLM trunk, in _TrunkChain's order: input LayerNorm, two Dense + LayerNorm
+    layers, two ResBlocks, the projection.  kind "det": DynamicsNetwork4 (muzero_deterministic_madn.py:
+    391-457); "act" / "chance": the afterstate / chance trunks of StochasticDynamicsNetwork4
+    (muzero_classic_madn.py:329-408; ResBlocks 0-1 / 2-3)."""
+    d = "dynamics"
+    if kind == "det":
+        head = ["LayerNorm_0/scale", "LayerNorm_0/bias", "Dense_3/kernel", "Dense_3/bias", "LayerNorm_1/scale",
+                "LayerNorm_1/bias", "Dense_4/kernel", "Dense_4/bias", "LayerNorm_2/scale", "LayerNorm_2/bias"]
+        rbs, tail = (0, 1), ["Dense_5/kernel", "Dense_5/bias"]
+    elif kind in ("act", "chance"):
+        head = [f"{kind}_{n}" for n in ("input_ln/scale", "input_ln/bias", "dense1/kernel", "dense1/bias",
+                                        "ln1/scale", "ln1/bias", "dense2/kernel", "dense2/bias", "ln2/scale",
+                                        "ln2/bias")]
+        rbs, tail = ((0, 1) if kind == "act" else (2, 3)), [f"{kind}_proj/kernel", f"{kind}_proj/bias"]
+    else:
+        raise ValueError(f"unknown trunk kind {kind!r}")
+    return [f"{d}/{n}" for n in head] + [f"{d}/ResBlock_{r}/{n}" for r in rbs for n in _RB_PARAMS] + \
+        [f"{d}/{n}" for n in tail]
+
+
+DYN_TRUNK_PARAMS = tuple(trunk_param_names("det"))
+CHAIN = True                     # False: the losses build the per-step autograd graph instead (A/B timing)
+_NP = len(DYN_TRUNK_PARAMS)      # 28 per trunk
+
+
+class _TrunkChain(torch.autograd.Function):
+    """The sequential FiLM-trunk applications of an unrolled loss as ONE autograd node.  Application i maps
+    x_i -> x_{i+1} = minmax(x_i + proj(trunk(LN(x_i) * (1 + scale_i) + shift_i))) with trunk group apps[i]'s
+    weights; the gradient reaching x_{i+1} is scaled by grad_scale where scaled[i].  det loss_fn: one group,
+    apps = (0,) * K, all scaled (train_with_reward.py:98-107); classic loss_fn_stochastic: groups (act, chance),
+    apps = (0, 1) * K, only the chance outputs (the new states) scaled (train_stochastic.py:95-121).
+
+    Forward = the fused kernels of csrc/learner_ln.hip + library GEMMs; the hand-written backward walks the
+    applications in reverse and, because a group's weights are shared by all its applications, forms each
+    weight gradient with ONE GEMM and each LayerNorm / bias gradient with ONE column sum per group (per-step
+    autograd made K GEMMs, K column sums and K - 1 accumulation adds per parameter).  min / max follow torch's
+    backward (the gradient goes to the returned index).  Inputs: x_0 [B, 256], FiLM scale / shift [T, B, 256],
+    the groups' parameters concatenated, each in trunk_param_names order.  Output: x_1..x_T as [T, B, 256]."""
 
     @staticmethod
-    def forward(ctx, latent0, scale, shift, grad_scale, *P):
-        g0, be0, W3, b3, g1, be1, W4, b4, g2, be2 = P[:10]
-        W5, b5 = P[26], P[27]
-        K, B, Nn = scale.shape
+    def forward(ctx, latent0, scale, shift, grad_scale, apps, scaled, *P):
+        T, B, Nn = scale.shape
+        if len(apps) != T or len(scaled) != T or len(P) != _NP * (max(apps) + 1):
+            raise ValueError("apps / scaled / parameters do not match the FiLM rows")
         zero = torch.zeros((Nn,), dtype=latent0.dtype, device=latent0.device)
-        outs = torch.empty((K, B, Nn), dtype=latent0.dtype, device=latent0.device)
+        outs = torch.empty((T, B, Nn), dtype=latent0.dtype, device=latent0.device)
         st = []
         lat = latent0.contiguous()
-        for k in range(K):
+        for i in range(T):
+            Q = P[_NP * apps[i]:_NP * (apps[i] + 1)]
+            g0, be0, W3, b3, g1, be1, W4, b4, g2, be2 = Q[:10]
             f0 = _ln_fwd(lat, zero, g0, be0, None, LN_PLAIN)
-            x0 = f0[0] * (1.0 + scale[k]) + shift[k]
+            x0 = f0[0] * (1.0 + scale[i]) + shift[i]
             f3 = _ln_fwd(x0 @ W3, b3, g1, be1, None, LN_RELU)
             f4 = _ln_fwd(f3[0] @ W4, b4, g2, be2, None, LN_RELU)
             x, rbs = f4[0], []
             for r in range(2):
-                Wa, ba, ga, bea, Wb, bb, gb, beb = P[10 + 8 * r:18 + 8 * r]
+                Wa, ba, ga, bea, Wb, bb, gb, beb = Q[10 + 8 * r:18 + 8 * r]
                 fa = _ln_fwd(x @ Wa, ba, ga, bea, None, LN_RELU)
                 fb = _ln_fwd(fa[0] @ Wb, bb, gb, beb, x, LN_RESID_RELU)
                 rbs.append((x, fa, fb))
                 x = fb[0]
-            q = lat + (x @ W5 + b5)
+            q = lat + (x @ Q[26] + Q[27])
             lo, ilo = q.min(-1, keepdim=True)
             hi, ihi = q.max(-1, keepdim=True)
-            nxt = torch.div(q - lo, hi - lo + 1e-8, out=outs[k])
+            nxt = torch.div(q - lo, hi - lo + 1e-8, out=outs[i])
             st.append((f0, x0, f3, f4, rbs, x, q, lo, hi, ilo, ihi))
             lat = nxt
         ctx.st, ctx.P, ctx.grad_scale = st, P, float(grad_scale)
+        ctx.apps, ctx.scaled = tuple(apps), tuple(scaled)
         ctx.save_for_backward(scale)
         return outs
 
     @staticmethod
     def backward(ctx, G):
         (scale,) = ctx.saved_tensors
-        P, st, s = ctx.P, ctx.st, ctx.grad_scale
-        g0, g1, g2 = P[0], P[4], P[8]
-        W3, W4, W5 = P[2], P[6], P[26]
-        K, B, Nn = scale.shape
+        P, st, s, apps = ctx.P, ctx.st, ctx.grad_scale, ctx.apps
+        T, B, Nn = scale.shape
         G = G.contiguous()
         dev, dt = G.device, G.dtype
         nf = _L.load().muz_ln_bwd_scratch_floats(B, Nn)
-        scr = {n: torch.empty((K, nf), dtype=dt, device=dev) for n in ("0", "3", "4", "a0", "b0", "a1", "b1")}
-        cols = {n: ([], []) for n in ("3", "4", "a0", "b0", "a1", "b1", "5")}      # (layer inputs, output grads)
+        ngroups = len(P) // _NP
+        slot, seen = [], [0] * ngroups           # application i's row in its group's column-partial buffers
+        for g in apps:
+            slot.append(seen[g])
+            seen[g] += 1
+        layers = ("0", "3", "4", "a0", "b0", "a1", "b1")
+        scr = {(g, n): torch.empty((max(seen[g], 1), nf), dtype=dt, device=dev) for g in range(ngroups) for n in layers}
+        cols = {(g, n): ([], []) for g in range(ngroups) for n in layers[1:] + ("5",)}   # (layer inputs, output grads)
         dscale, dshift = torch.empty_like(scale), torch.empty_like(scale)
         carry = None
-        for k in range(K - 1, -1, -1):
-            f0, x0, f3, f4, rbs, x5, q, lo, hi, ilo, ihi = st[k]
-            dnxt = (G[k] if carry is None else G[k] + carry) * s
+        for i in range(T - 1, -1, -1):
+            g, j = apps[i], slot[i]
+            Q = P[_NP * g:_NP * (g + 1)]
+            f0, x0, f3, f4, rbs, x5, q, lo, hi, ilo, ihi = st[i]
+            dnxt = G[i] if carry is None else G[i] + carry
+            if ctx.scaled[i]:
+                dnxt = dnxt * s
             den = hi - lo + 1e-8
             dq = dnxt / den
             t = (dnxt * (q - lo)).sum(-1, keepdim=True) / (den * den)
             dq.scatter_add_(-1, ilo, -dnxt.sum(-1, keepdim=True) / den + t)
             dq.scatter_add_(-1, ihi, -t)
-            cols["5"][0].append(x5)
-            cols["5"][1].append(dq)
-            dx = dq @ W5.t()
+            cols[(g, "5")][0].append(x5)
+            cols[(g, "5")][1].append(dq)
+            dx = dq @ Q[26].t()
             for r in (1, 0):
                 xin, fa, fb = rbs[r]
-                Wa, Wb, ga, gb = P[10 + 8 * r], P[14 + 8 * r], P[12 + 8 * r], P[16 + 8 * r]
-                dzb, dres = _ln_bwd_rows(dx, fb, gb, LN_RESID_RELU, scr[f"b{r}"][k])
-                cols[f"b{r}"][0].append(fa[0])
-                cols[f"b{r}"][1].append(dzb)
-                dza, _ = _ln_bwd_rows(dzb @ Wb.t(), fa, ga, LN_RELU, scr[f"a{r}"][k])
-                cols[f"a{r}"][0].append(xin)
-                cols[f"a{r}"][1].append(dza)
+                Wa, ga, Wb, gb = Q[10 + 8 * r], Q[12 + 8 * r], Q[14 + 8 * r], Q[16 + 8 * r]
+                dzb, dres = _ln_bwd_rows(dx, fb, gb, LN_RESID_RELU, scr[(g, f"b{r}")][j])
+                cols[(g, f"b{r}")][0].append(fa[0])
+                cols[(g, f"b{r}")][1].append(dzb)
+                dza, _ = _ln_bwd_rows(dzb @ Wb.t(), fa, ga, LN_RELU, scr[(g, f"a{r}")][j])
+                cols[(g, f"a{r}")][0].append(xin)
+                cols[(g, f"a{r}")][1].append(dza)
                 dx = dres + dza @ Wa.t()
-            dz4, _ = _ln_bwd_rows(dx, f4, g2, LN_RELU, scr["4"][k])
-            cols["4"][0].append(f3[0])
-            cols["4"][1].append(dz4)
-            dz3, _ = _ln_bwd_rows(dz4 @ W4.t(), f3, g1, LN_RELU, scr["3"][k])
-            cols["3"][0].append(x0)
-            cols["3"][1].append(dz3)
-            dx0 = torch.mm(dz3, W3.t(), out=dshift[k])
-            torch.mul(dx0, f0[0], out=dscale[k])
-            dz0, _ = _ln_bwd_rows(dx0 * (1.0 + scale[k]), f0, g0, LN_PLAIN, scr["0"][k])
+            dz4, _ = _ln_bwd_rows(dx, f4, Q[8], LN_RELU, scr[(g, "4")][j])
+            cols[(g, "4")][0].append(f3[0])
+            cols[(g, "4")][1].append(dz4)
+            dz3, _ = _ln_bwd_rows(dz4 @ Q[6].t(), f3, Q[4], LN_RELU, scr[(g, "3")][j])
+            cols[(g, "3")][0].append(x0)
+            cols[(g, "3")][1].append(dz3)
+            dx0 = torch.mm(dz3, Q[2].t(), out=dshift[i])
+            torch.mul(dx0, f0[0], out=dscale[i])
+            dz0, _ = _ln_bwd_rows(dx0 * (1.0 + scale[i]), f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
             carry = dz0 + dq
         grads = [None] * len(P)
-        grads[0], grads[1], _ = _ln_colsum(scr["0"], Nn)
-        for n, (iw, ib, ig, ibe) in (("3", (2, 3, 4, 5)), ("4", (6, 7, 8, 9)), ("a0", (10, 11, 12, 13)),
-                                     ("b0", (14, 15, 16, 17)), ("a1", (18, 19, 20, 21)), ("b1", (22, 23, 24, 25))):
-            X, DZ = (torch.cat(c, 0) for c in cols[n])
-            grads[iw] = X.t() @ DZ
-            grads[ig], grads[ibe], grads[ib] = _ln_colsum(scr[n], Nn)
-        X, DZ = (torch.cat(c, 0) for c in cols["5"])
-        grads[26], grads[27] = X.t() @ DZ, DZ.sum(0)
-        return (carry, dscale, dshift, None, *grads)
+        for g in range(ngroups):
+            if not seen[g]:
+                grads[_NP * g:_NP * (g + 1)] = [torch.zeros_like(p) for p in P[_NP * g:_NP * (g + 1)]]
+                continue
+            o = _NP * g
+            grads[o], grads[o + 1], _ = _ln_colsum(scr[(g, "0")], Nn)
+            for n, (iw, ib, ig, ibe) in (("3", (2, 3, 4, 5)), ("4", (6, 7, 8, 9)), ("a0", (10, 11, 12, 13)),
+                                         ("b0", (14, 15, 16, 17)), ("a1", (18, 19, 20, 21)), ("b1", (22, 23, 24, 25))):
+                X, DZ = (torch.cat(c, 0) for c in cols[(g, n)])
+                grads[o + iw] = X.t() @ DZ
+                grads[o + ig], grads[o + ibe], grads[o + ib] = _ln_colsum(scr[(g, n)], Nn)
+            X, DZ = (torch.cat(c, 0) for c in cols[(g, "5")])
+            grads[o + 26], grads[o + 27] = X.t() @ DZ, DZ.sum(0)
+        return (carry, dscale, dshift, None, None, None, *grads)
 
 
 class MuZeroNets:
@@ -354,9 +395,9 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     # (same per-row arithmetic as the step-by-step loop of the reference; far fewer kernel launches).
     oh, scale, shift = nets.dynamics_film(acts[:, :K].transpose(0, 1).reshape(-1))
     latents = [latent]
-    if K and latent.is_cuda:     # the whole latent chain as one autograd node (fused kernels, batched weight grads)
-        chain = _DynChain.apply(latent, scale.reshape(K, B, -1), shift.reshape(K, B, -1), grad_scale,
-                                *(nets.p[n] for n in DYN_TRUNK_PARAMS))
+    if K and latent.is_cuda and CHAIN:     # the whole latent chain as one autograd node (fused kernels, batched weight grads)
+        chain = _TrunkChain.apply(latent, scale.reshape(K, B, -1), shift.reshape(K, B, -1), grad_scale,
+                                  (0,) * K, (True,) * K, *(nets.p[n] for n in DYN_TRUNK_PARAMS))
         latents += list(chain.unbind(0))
     else:
         for k in range(K):
@@ -614,7 +655,16 @@ def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int =
     oh_all, ea_all = nets.action_embed(acts[:, :K].transpose(0, 1).reshape(-1))
     ec_all = nets.chance_embed(dice[:, :K].transpose(0, 1).reshape(-1))
     latents, afters = [latent], []
-    for k in range(K):
+    if K and latent.is_cuda and CHAIN:     # the afterstate / state chain as one autograd node (as loss_fn's latent chain)
+        d = "dynamics"
+        film = [torch.stack([nets._dense(f"{d}/{pre}_film_{w}", e).reshape(K, B, -1) for pre, e in
+                             (("act", ea_all), ("chance", ec_all))], 1).reshape(2 * K, B, -1)
+                for w in ("scale", "shift")]                       # rows interleaved: act_0, chance_0, act_1, ...
+        chain = _TrunkChain.apply(latent, film[0], film[1], grad_scale, (0, 1) * K, (False, True) * K,
+                                  *(nets.p[n] for kind in ("act", "chance") for n in trunk_param_names(kind)))
+        afters = list(chain[0::2].unbind(0))
+        latents += list(chain[1::2].unbind(0))
+    for k in range(len(afters), K):
         after = nets._film_trunk("act", 0, latents[-1], ea_all[k * B:(k + 1) * B])
         afters.append(after)
         nxt = nets._film_trunk("chance", 2, after, ec_all[k * B:(k + 1) * B])

@@ -49,6 +49,25 @@ timed("sample_batch", ring.sample_batch)
 timed("train_step (graph replay, fixed batch)", lambda: lr.train_step(batch))
 timed("sample_batch + train_step", lambda: lr.train_step(ring.sample_batch()))
 
+# classic (train_stochastic.py) step at the same batch / unroll / td, chain node on and off
+from exploring_muzero_on_dog_amd import classic as CL, game_agent_stochastic as GS, stochastic as S  # noqa: E402
+Cc = CL.num_channels(4)
+cparams = S.init_classic_params(Cc, 0)
+ceng = GS.StochasticSelfPlayEngine(S.DeviceClassicNet(cparams, Cc), 256, max_steps=550, num_simulations=8, max_depth=8)
+cring = R.VectorizedReplayBufferStochastic(20000, 128, 10, 50, obs_shape=(Cc, 56), max_episode_length=550,
+                                           rng=np.random.RandomState(0))
+cring.save_games_from_buffers(ceng.play_stream(512, seed=1))
+cbatch = cring.sample_batch()
+for chain in (True, False):
+    L.CHAIN = chain
+    for graph in (True, False):
+        clr = L.StochasticLearner(cparams, Cc, unroll_steps=10, graph=graph)
+        timed(f"classic train_step ({'graph replay' if graph else 'eager'}, chain node {'on' if chain else 'off'})",
+              lambda: clr.train_step(cbatch))
+    lr_d = L.Learner(params, C, unroll_steps=10, graph=True)
+    timed(f"det train_step (graph replay, chain node {'on' if chain else 'off'})", lambda: lr_d.train_step(batch))
+L.CHAIN = True
+
 if len(sys.argv) > 2:   # also time with the other BLAS backend (rocBLAS vs hipBLASLt)
     torch.backends.cuda.preferred_blas_library(sys.argv[2])
     lr2 = L.Learner(params, C, unroll_steps=10, graph=True)

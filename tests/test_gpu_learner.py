@@ -201,7 +201,7 @@ def test_fused_dense_layernorm_matches_float64_autograd(cuda, N, mode):
 
 
 def test_dynamics_chain_node_matches_per_step_autograd(cuda):
-    """learner._DynChain (the K-step latent chain as one autograd node, batched weight gradients) against the
+    """learner._TrunkChain (the K-step latent chain as one autograd node, batched weight gradients) against the
     per-step graph of the same layers (loss_fn's CPU-style loop run on the GPU): forward within 1e-5, gradients
     of every input and parameter within 1e-5 relative (summation orders differ)."""
     _, _, L, _, _ = _mods()
@@ -215,7 +215,7 @@ def test_dynamics_chain_node_matches_per_step_autograd(cuda):
     params = [nets.p[n] for n in L.DYN_TRUNK_PARAMS]
     inputs = [lat0, scale, shift] + params
 
-    out = L._DynChain.apply(lat0, scale, shift, 0.5, *params)
+    out = L._TrunkChain.apply(lat0, scale, shift, 0.5, (0,) * K, (True,) * K, *params)
     g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs)
     lats = [lat0]
     for k in range(K):
@@ -228,5 +228,46 @@ def test_dynamics_chain_node_matches_per_step_autograd(cuda):
     assert (out - ref).abs().max().item() < 1e-5, "forward differs"
     names = ["latent0", "scale", "shift"] + list(L.DYN_TRUNK_PARAMS)
     for n, a, b in zip(names, g1, g2):
+        err = (a - b).abs().max().item() / max(1e-3, b.abs().max().item())
+        assert err < 1e-5, f"{n}: relative gradient difference {err:.2e}"
+
+
+def test_classic_chain_node_matches_per_step_autograd(cuda):
+    """The classic afterstate / state chain (act and chance trunks alternating, only the new states'
+    gradient scaled) as one _TrunkChain node against loss_fn_stochastic's per-step graph on the GPU."""
+    _, _, L, _, _ = _mods()
+    from exploring_muzero_on_dog_amd import stochastic as ST
+    C, B, K = 20, 64, 5
+    params = ST.init_classic_params(C, seed=6)
+    rng = np.random.default_rng(8)
+    params = {k: (v + 0.1 * rng.standard_normal(v.shape).astype(np.float32)) if not k.endswith("kernel") else v
+              for k, v in params.items()}
+    nets = L.ClassicMuZeroNets(params, C, "cuda")
+    g = torch.Generator().manual_seed(5)
+    lat0 = torch.rand(B, 256, generator=g).cuda().requires_grad_(True)
+    ea = torch.relu(torch.randn(K * B, 64, generator=g)).cuda().requires_grad_(True)
+    ec = torch.relu(torch.randn(K * B, 64, generator=g)).cuda().requires_grad_(True)
+    w = torch.randn(2 * K, B, 256, generator=g).cuda()
+    names = [n for kind in ("act", "chance") for n in L.trunk_param_names(kind)]
+    names += [f"dynamics/{pre}_film_{x}/{y}" for pre in ("act", "chance") for x in ("scale", "shift")
+              for y in ("kernel", "bias")]
+    inputs = [lat0, ea, ec] + [nets.p[n] for n in names]
+
+    film = [torch.stack([nets._dense(f"dynamics/{pre}_film_{x}", e).reshape(K, B, -1)
+                         for pre, e in (("act", ea), ("chance", ec))], 1).reshape(2 * K, B, -1) for x in ("scale", "shift")]
+    out = L._TrunkChain.apply(lat0, film[0], film[1], 0.5, (0, 1) * K, (False, True) * K,
+                              *(nets.p[n] for n in names[:2 * L._NP]))
+    g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs)
+    seq, lat = [], lat0
+    for k in range(K):
+        after = nets._film_trunk("act", 0, lat, ea[k * B:(k + 1) * B])
+        nxt = nets._film_trunk("chance", 2, after, ec[k * B:(k + 1) * B])
+        lat = (nxt * 0.5).detach() + nxt * 0.5
+        seq += [after, lat]
+    ref = torch.stack(seq)
+    g2 = torch.autograd.grad((ref * w).sum() + ref[-1].square().sum(), inputs)
+    torch.cuda.synchronize()
+    assert (out - ref).abs().max().item() < 1e-5, "forward differs"
+    for n, a, b in zip(["latent0", "act_embed", "chance_embed"] + names, g1, g2):
         err = (a - b).abs().max().item() / max(1e-3, b.abs().max().item())
         assert err < 1e-5, f"{n}: relative gradient difference {err:.2e}"
