@@ -473,8 +473,38 @@ class AdamW:
         self.lr0, self.spi, self.boundaries = lr0, steps_per_iteration, boundaries
         self.dt = dt
 
+        self._fused = None
+        if dev.type == "cuda":
+            import ctypes
+            n = len(params)
+            if dt != torch.float32 or any(not p.is_contiguous() for p in params) or len(boundaries) > 4:
+                raise ValueError("AdamW on the GPU takes contiguous float32 parameters and <= 4 lr boundaries")
+            numel = (ctypes.c_int64 * n)(*[p.numel() for p in params])
+            nbytes = _L.load().muz_adamw_scratch_bytes(n, numel)
+            self._fused = dict(
+                n=n, numel=numel, scratch=torch.empty((nbytes,), dtype=torch.uint8, device=dev),
+                gnorm=torch.zeros((), dtype=torch.float32, device=dev),
+                p=(ctypes.c_void_p * n)(*[q.data_ptr() for q in params]),
+                m=(ctypes.c_void_p * n)(*[q.data_ptr() for q in self.mu]),
+                v=(ctypes.c_void_p * n)(*[q.data_ptr() for q in self.nu]),
+                bounds=(ctypes.c_double * max(1, 2 * len(boundaries)))(*[float(x) for b in boundaries for x in b]),
+                gtype=ctypes.c_void_p * n)
+
     @torch.no_grad()
     def step(self):
+        if self._fused is not None:
+            # csrc/learner_opt.hip: norm + clip + AdamW over all tensors in two passes (the foreach form
+            # below is the same arithmetic; it stays for the CPU host tests)
+            f = self._fused
+            grads = f["gtype"](*[q.grad.data_ptr() if q.grad is not None else None for q in self.params])
+            if any(q.grad is not None and (q.grad.dtype != torch.float32 or not q.grad.is_contiguous())
+                   for q in self.params):
+                raise ValueError("AdamW on the GPU takes contiguous float32 gradients")
+            _L.check(_L.load().muz_adamw_step(f["p"], grads, f["m"], f["v"], f["numel"], f["n"], _L.ptr(self.count),
+                                              _L.ptr(f["scratch"]), _L.ptr(f["gnorm"]), self.max_norm, self.b1, self.b2,
+                                              self.eps, self.wd, self.lr0, float(self.spi), f["bounds"],
+                                              len(self.boundaries), _L.stream_ptr()), "muz_adamw_step")
+            return f["gnorm"]
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
         # per-tensor norms in one multi-tensor kernel (a sum(g * g) per tensor was ~200 launches per step)
         g_norm = torch.sqrt(torch.stack(torch._foreach_norm(grads)).square().sum())

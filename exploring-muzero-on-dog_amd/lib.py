@@ -286,6 +286,10 @@ SIGNATURES = {
     "muz_ln_colsum": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp, vp]),
     "muz_ln_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
                                   vp, vp, vp, vp]),
+    "muz_adamw_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32, vp]),
+    "muz_adamw_step": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_double,
+                                      ctypes.c_double, ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double,
+                                      vp, ctypes.c_int32, vp]),
     "muz_detmadn_selfplay_stream": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzNetW),
                                                    ctypes.POINTER(MuzSearchCfg), MuzDetSoA, MuzTraj, ctypes.c_int32,
                                                    ctypes.c_int32, vp, ctypes.c_int64, ctypes.POINTER(MuzSpStats),

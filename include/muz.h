@@ -675,6 +675,19 @@ int muz_ln_bwd(const float* dout, const float* out, const float* z, const float*
                const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
                float* dgamma, float* dbeta, float* dbias, void* stream);
 
+/* One optimizer step over ntensors parameter tensors (csrc/learner_opt.hip): optax.chain(
+ * clip_by_global_norm(max_norm), adamw(lr, b1, b2, eps, weight_decay)) with the piecewise-constant lr
+ * lr0 x prod{factor_j : step - 1 >= iteration_j x steps_per_iteration} (train_with_reward.py:361-372,
+ * train_stochastic.py:415-426).  params / grads / mu / nu: host arrays of device float pointers (a null
+ * grad is a zero gradient), numel: host array; count: device double step counter (incremented); gnorm:
+ * device float, receives the pre-clip global norm; scratch: muz_adamw_scratch_bytes(ntensors, numel) device
+ * bytes; boundaries: host [nb][2] (iteration, factor), nb <= 4.  Deterministic (fixed-order reduction). */
+int64_t muz_adamw_scratch_bytes(int32_t ntensors, const int64_t* numel);
+int muz_adamw_step(float* const* params, const float* const* grads, float* const* mu, float* const* nu,
+                   const int64_t* numel, int32_t ntensors, double* count, void* scratch, float* gnorm,
+                   float max_norm, double b1, double b2, float eps, float weight_decay, double lr0,
+                   double steps_per_iteration, const double* boundaries, int32_t nb, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -49,6 +49,9 @@ timed("sample_batch", ring.sample_batch)
 timed("train_step (graph replay, fixed batch)", lambda: lr.train_step(batch))
 timed("sample_batch + train_step", lambda: lr.train_step(ring.sample_batch()))
 
+if os.environ.get("MUZ_PROFILE_DET_ONLY"):      # (for a kernel trace of the det step alone)
+    sys.exit(0)
+
 # classic (train_stochastic.py) step at the same batch / unroll / td, chain node on and off
 from exploring_muzero_on_dog_amd import classic as CL, game_agent_stochastic as GS, stochastic as S  # noqa: E402
 Cc = CL.num_channels(4)

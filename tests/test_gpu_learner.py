@@ -271,3 +271,35 @@ def test_classic_chain_node_matches_per_step_autograd(cuda):
     for n, a, b in zip(["latent0", "act_embed", "chance_embed"] + names, g1, g2):
         err = (a - b).abs().max().item() / max(1e-3, b.abs().max().item())
         assert err < 1e-5, f"{n}: relative gradient difference {err:.2e}"
+
+
+def test_fused_adamw_matches_foreach_form(cuda):
+    """csrc/learner_opt.hip (global-norm clip + AdamW + lr schedule in two passes over all tensors) against the
+    torch._foreach form of the same step (learner.AdamW on the CPU path, here run on the GPU): 45 tensors (two
+    kernel-argument tables), sizes across the 4096-element chunk edges, an empty tensor and one without a
+    gradient; clipped and unclipped steps across two lr boundaries."""
+    _, _, L, _, _ = _mods()
+    rng = np.random.default_rng(12)
+    sizes = [1, 3, 4095, 4096, 4097, 9000, 0, 256 * 256] + list(rng.integers(1, 3000, 37))
+    base = [rng.standard_normal(int(n)).astype(np.float32) for n in sizes]
+    p1 = [torch.from_numpy(b).cuda().requires_grad_(True) for b in base]
+    p2 = [torch.from_numpy(b).cuda().requires_grad_(True) for b in base]
+    kw = dict(steps_per_iteration=1, boundaries=((2, 0.2), (4, 0.5)))
+    fused, ref = L.AdamW(p1, **kw), L.AdamW(p2, **kw)
+    assert fused._fused is not None
+    ref._fused = None
+    for step in range(7):
+        scale = 3.0 if step in (1, 4) else 0.01                 # global norm above / below max_norm 5
+        for i, (a, b) in enumerate(zip(p1, p2)):
+            if i == 5:
+                a.grad = b.grad = None
+                continue
+            g = torch.from_numpy((rng.standard_normal(a.numel()) * scale).astype(np.float32)).cuda()
+            a.grad, b.grad = g.clone(), g.clone()
+        n1, n2 = fused.step(), ref.step()
+        torch.cuda.synchronize()
+        assert abs(float(n1) - float(n2)) <= 1e-6 * float(n2), (step, float(n1), float(n2))
+        for name, xs, ys in (("param", p1, p2), ("mu", fused.mu, ref.mu), ("nu", fused.nu, ref.nu)):
+            for i, (a, b) in enumerate(zip(xs, ys)):
+                assert torch.allclose(a, b, rtol=2e-6, atol=1e-8), (step, name, i, (a - b).abs().max().item())
+    assert float(fused.count) == float(ref.count) == 7.0
