@@ -154,6 +154,88 @@ __global__ __launch_bounds__(256) void k_ln_colsum(const float* __restrict__ par
   }
 }
 
+// Min-max latent scaling at the end of a dynamics trunk (muzero_deterministic_madn.py:449-457,
+// muzero_classic_madn.py:365-371): q = x + (y + bias), out = (q - min q) / (max q - min q + 1e-8) per row
+// (one wave per row; ties go to the lowest column, as torch's min / max).  Saved: q, (lo, hi), their columns.
+// Backward, with the incoming gradient d = (g + (a + b)) * scale (a, b: optional extra terms):
+//   dq = d / den;  dq[argmin] += -sum(d) / den + t;  dq[argmax] += -t,  t = sum(d (q - lo)) / den^2.
+__device__ __forceinline__ void wave_argext(float& v, int& i, bool is_max) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if ((is_max ? ov > v : ov < v) || (ov == v && oi < i)) v = ov, i = oi;
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_minmax_fwd(const float* __restrict__ x, const float* __restrict__ y,
+                                                    const float* __restrict__ bias, int M, float* __restrict__ out,
+                                                    float* __restrict__ q, float* __restrict__ lohi,
+                                                    int* __restrict__ idx) {
+  constexpr int E = N / 64;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const size_t row = (size_t)m * N;
+  float v[E];
+  float lo = INFINITY, hi = -INFINITY;
+  int ilo = N, ihi = N;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int c = lane + 64 * e;
+    v[e] = x[row + c] + (y[row + c] + bias[c]);
+    q[row + c] = v[e];
+    if (v[e] < lo) lo = v[e], ilo = c;
+    if (v[e] > hi) hi = v[e], ihi = c;
+  }
+  wave_argext(lo, ilo, false);
+  wave_argext(hi, ihi, true);
+  const float den = (hi - lo) + 1e-8f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) out[row + lane + 64 * e] = (v[e] - lo) / den;
+  if (lane == 0) {
+    lohi[2 * m] = lo, lohi[2 * m + 1] = hi;
+    idx[2 * m] = ilo, idx[2 * m + 1] = ihi;
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_minmax_bwd(const float* __restrict__ g, const float* __restrict__ a,
+                                                    const float* __restrict__ b, float scale, int scaled,
+                                                    const float* __restrict__ q, const float* __restrict__ lohi,
+                                                    const int* __restrict__ idx, int M, float* __restrict__ dq) {
+  constexpr int E = N / 64;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const size_t row = (size_t)m * N;
+  const float lo = lohi[2 * m], hi = lohi[2 * m + 1];
+  const float den = (hi - lo) + 1e-8f;
+  float d[E], sd = 0.f, st = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const size_t k = row + lane + 64 * e;
+    float t = g[k];
+    if (a) t = t + (a[k] + b[k]);
+    if (scaled) t = t * scale;
+    d[e] = t;
+    sd += t;
+    st += t * (q[k] - lo);
+  }
+  sd = wave_sum(sd);
+  st = wave_sum(st) / (den * den);
+  const int ilo = idx[2 * m], ihi = idx[2 * m + 1];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int c = lane + 64 * e;
+    float r = d[e] / den;
+    if (c == ilo) r = r + (-sd / den + st);
+    if (c == ihi) r = r + (-st);
+    dq[row + c] = r;
+  }
+}
+
 static bool ln_width_ok(int N) { return N == 32 || N == 64 || N == 128 || N == 256; }
 
 }  // namespace muz
@@ -223,6 +305,24 @@ int muz_ln_bwd(const float* dout, const float* out, const float* z, const float*
   const int rc = muz_ln_bwd_rows(dout, out, z, mean, rstd, gamma, M, N, mode, dz, dres, scratch, stream);
   if (rc) return rc;
   return muz_ln_colsum(scratch, muz_ln_bwd_scratch_floats(M, N) / (3 * N), N, dgamma, dbeta, dbias, stream);
+}
+
+int muz_minmax_fwd(const float* x, const float* y, const float* bias, int32_t M, int32_t N, float* out, float* q,
+                   float* lohi, int32_t* idx, void* stream) {
+  if (N != 256) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(M >= 0 && x && y && bias && out && q && lohi && idx);
+  if (M == 0) return MUZ_OK;
+  k_minmax_fwd<256><<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(x, y, bias, M, out, q, lohi, idx);
+  return muz_last_launch_error();
+}
+
+int muz_minmax_bwd(const float* g, const float* a, const float* b, float scale, int32_t scaled, const float* q,
+                   const float* lohi, const int32_t* idx, int32_t M, int32_t N, float* dq, void* stream) {
+  if (N != 256) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(M >= 0 && g && q && lohi && idx && dq && (a == nullptr) == (b == nullptr));
+  if (M == 0) return MUZ_OK;
+  k_minmax_bwd<256><<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(g, a, b, scale, scaled, q, lohi, idx, M, dq);
+  return muz_last_launch_error();
 }
 
 }  // extern "C"

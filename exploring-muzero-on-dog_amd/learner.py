@@ -152,15 +152,21 @@ class _TrunkChain(torch.autograd.Function):
         T, B, Nn = scale.shape
         if len(apps) != T or len(scaled) != T or len(P) != _NP * (max(apps) + 1):
             raise ValueError("apps / scaled / parameters do not match the FiLM rows")
-        zero = torch.zeros((Nn,), dtype=latent0.dtype, device=latent0.device)
-        outs = torch.empty((T, B, Nn), dtype=latent0.dtype, device=latent0.device)
+        dev, dt = latent0.device, latent0.dtype
+        zero = torch.zeros((Nn,), dtype=dt, device=dev)
+        outs = torch.empty((T, B, Nn), dtype=dt, device=dev)
+        qs = torch.empty((T, B, Nn), dtype=dt, device=dev)                  # min-max inputs and their extrema
+        lohi = torch.empty((T, B, 2), dtype=dt, device=dev)
+        idx = torch.empty((T, B, 2), dtype=torch.int32, device=dev)
+        scale1 = 1.0 + scale
+        lib = _L.load()
         st = []
         lat = latent0.contiguous()
         for i in range(T):
             Q = P[_NP * apps[i]:_NP * (apps[i] + 1)]
             g0, be0, W3, b3, g1, be1, W4, b4, g2, be2 = Q[:10]
             f0 = _ln_fwd(lat, zero, g0, be0, None, LN_PLAIN)
-            x0 = f0[0] * (1.0 + scale[i]) + shift[i]
+            x0 = torch.addcmul(shift[i], f0[0], scale1[i])
             f3 = _ln_fwd(x0 @ W3, b3, g1, be1, None, LN_RELU)
             f4 = _ln_fwd(f3[0] @ W4, b4, g2, be2, None, LN_RELU)
             x, rbs = f4[0], []
@@ -170,25 +176,24 @@ class _TrunkChain(torch.autograd.Function):
                 fb = _ln_fwd(fa[0] @ Wb, bb, gb, beb, x, LN_RESID_RELU)
                 rbs.append((x, fa, fb))
                 x = fb[0]
-            q = lat + (x @ Q[26] + Q[27])
-            lo, ilo = q.min(-1, keepdim=True)
-            hi, ihi = q.max(-1, keepdim=True)
-            nxt = torch.div(q - lo, hi - lo + 1e-8, out=outs[i])
-            st.append((f0, x0, f3, f4, rbs, x, q, lo, hi, ilo, ihi))
-            lat = nxt
+            _L.check(lib.muz_minmax_fwd(_L.ptr(lat), _L.ptr(x @ Q[26]), _L.ptr(Q[27]), B, Nn, _L.ptr(outs[i]),
+                                        _L.ptr(qs[i]), _L.ptr(lohi[i]), _L.ptr(idx[i]), _L.stream_ptr()), "muz_minmax_fwd")
+            st.append((f0, x0, f3, f4, rbs, x))
+            lat = outs[i]
         ctx.st, ctx.P, ctx.grad_scale = st, P, float(grad_scale)
         ctx.apps, ctx.scaled = tuple(apps), tuple(scaled)
-        ctx.save_for_backward(scale)
+        ctx.save_for_backward(scale1, qs, lohi, idx)
         return outs
 
     @staticmethod
     def backward(ctx, G):
-        (scale,) = ctx.saved_tensors
+        scale1, qs, lohi, idx = ctx.saved_tensors
         P, st, s, apps = ctx.P, ctx.st, ctx.grad_scale, ctx.apps
-        T, B, Nn = scale.shape
+        T, B, Nn = scale1.shape
         G = G.contiguous()
         dev, dt = G.device, G.dtype
-        nf = _L.load().muz_ln_bwd_scratch_floats(B, Nn)
+        lib = _L.load()
+        nf = lib.muz_ln_bwd_scratch_floats(B, Nn)
         ngroups = len(P) // _NP
         slot, seen = [], [0] * ngroups           # application i's row in its group's column-partial buffers
         for g in apps:
@@ -197,20 +202,16 @@ class _TrunkChain(torch.autograd.Function):
         layers = ("0", "3", "4", "a0", "b0", "a1", "b1")
         scr = {(g, n): torch.empty((max(seen[g], 1), nf), dtype=dt, device=dev) for g in range(ngroups) for n in layers}
         cols = {(g, n): ([], []) for g in range(ngroups) for n in layers[1:] + ("5",)}   # (layer inputs, output grads)
-        dscale, dshift = torch.empty_like(scale), torch.empty_like(scale)
-        carry = None
+        dscale, dshift = torch.empty_like(scale1), torch.empty_like(scale1)
+        ca = cb = None                            # the carried gradient of x_{i+1}: ca + cb
         for i in range(T - 1, -1, -1):
             g, j = apps[i], slot[i]
             Q = P[_NP * g:_NP * (g + 1)]
-            f0, x0, f3, f4, rbs, x5, q, lo, hi, ilo, ihi = st[i]
-            dnxt = G[i] if carry is None else G[i] + carry
-            if ctx.scaled[i]:
-                dnxt = dnxt * s
-            den = hi - lo + 1e-8
-            dq = dnxt / den
-            t = (dnxt * (q - lo)).sum(-1, keepdim=True) / (den * den)
-            dq.scatter_add_(-1, ilo, -dnxt.sum(-1, keepdim=True) / den + t)
-            dq.scatter_add_(-1, ihi, -t)
+            f0, x0, f3, f4, rbs, x5 = st[i]
+            dq = torch.empty((B, Nn), dtype=dt, device=dev)
+            _L.check(lib.muz_minmax_bwd(_L.ptr(G[i]), _L.ptr(ca), _L.ptr(cb), s, int(ctx.scaled[i]), _L.ptr(qs[i]),
+                                        _L.ptr(lohi[i]), _L.ptr(idx[i]), B, Nn, _L.ptr(dq), _L.stream_ptr()),
+                     "muz_minmax_bwd")
             cols[(g, "5")][0].append(x5)
             cols[(g, "5")][1].append(dq)
             dx = dq @ Q[26].t()
@@ -232,8 +233,8 @@ class _TrunkChain(torch.autograd.Function):
             cols[(g, "3")][1].append(dz3)
             dx0 = torch.mm(dz3, Q[2].t(), out=dshift[i])
             torch.mul(dx0, f0[0], out=dscale[i])
-            dz0, _ = _ln_bwd_rows(dx0 * (1.0 + scale[i]), f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
-            carry = dz0 + dq
+            dz0, _ = _ln_bwd_rows(dx0 * scale1[i], f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
+            ca, cb = dz0, dq
         grads = [None] * len(P)
         for g in range(ngroups):
             if not seen[g]:
@@ -248,7 +249,7 @@ class _TrunkChain(torch.autograd.Function):
                 grads[o + ig], grads[o + ibe], grads[o + ib] = _ln_colsum(scr[(g, n)], Nn)
             X, DZ = (torch.cat(c, 0) for c in cols[(g, "5")])
             grads[o + 26], grads[o + 27] = X.t() @ DZ, DZ.sum(0)
-        return (carry, dscale, dshift, None, None, None, *grads)
+        return (ca + cb, dscale, dshift, None, None, None, *grads)
 
 
 class MuZeroNets:

@@ -674,6 +674,13 @@ int muz_ln_colsum(const float* scratch, int64_t nblk, int32_t N, float* dgamma, 
 int muz_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
                const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
                float* dgamma, float* dbeta, float* dbias, void* stream);
+/* Min-max latent scaling closing a dynamics trunk, N = 256: q = x + (y + bias), out = (q - min) /
+ * (max - min + 1e-8) per row; saves q [M][N], lohi [M][2] (min, max) and idx [M][2] (their columns, lowest on
+ * ties).  Backward: dq from d = (g + (a + b)) x (scale if scaled) (a, b both null or both given). */
+int muz_minmax_fwd(const float* x, const float* y, const float* bias, int32_t M, int32_t N, float* out, float* q,
+                   float* lohi, int32_t* idx, void* stream);
+int muz_minmax_bwd(const float* g, const float* a, const float* b, float scale, int32_t scaled, const float* q,
+                   const float* lohi, const int32_t* idx, int32_t M, int32_t N, float* dq, void* stream);
 
 /* One optimizer step over ntensors parameter tensors (csrc/learner_opt.hip): optax.chain(
  * clip_by_global_norm(max_norm), adamw(lr, b1, b2, eps, weight_decay)) with the piecewise-constant lr
