@@ -236,6 +236,37 @@ __global__ __launch_bounds__(256) void k_minmax_bwd(const float* __restrict__ g,
   }
 }
 
+// 'SAME' Conv1D as one GEMM (learner.MuZeroNets._conv_cols): the im2col matrix of x [B][W][Cin] is
+// cols [B][W][K * Cin], cols[b][w][d * Cin + c] = x[b][w + d - (K - 1) / 2][c] (0 outside the row), and its
+// backward dx[b][w][c] = sum_d dcols[b][w - d + (K - 1) / 2][d * Cin + c] (d ascending: deterministic).
+__global__ __launch_bounds__(256) void k_im2col_fwd(const float* __restrict__ x, int B, int W, int Cin, int K,
+                                                    float* __restrict__ cols) {
+  const int64_t n = (int64_t)B * W * K * Cin;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % Cin);
+  const int d = (int)((i / Cin) % K);
+  const int64_t bw = i / ((int64_t)K * Cin);
+  const int w = (int)(bw % W), src = w + d - (K - 1) / 2;
+  cols[i] = (src >= 0 && src < W) ? x[(bw - w + src) * Cin + c] : 0.f;
+}
+
+__global__ __launch_bounds__(256) void k_im2col_bwd(const float* __restrict__ dcols, int B, int W, int Cin, int K,
+                                                    float* __restrict__ dx) {
+  const int64_t n = (int64_t)B * W * Cin;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % Cin);
+  const int64_t bw = i / Cin;
+  const int w = (int)(bw % W);
+  float s = 0.f;
+  for (int d = 0; d < K; ++d) {
+    const int dst = w - d + (K - 1) / 2;
+    if (dst >= 0 && dst < W) s += dcols[((bw - w + dst) * K + d) * Cin + c];
+  }
+  dx[i] = s;
+}
+
 static bool ln_width_ok(int N) { return N == 32 || N == 64 || N == 128 || N == 256; }
 
 }  // namespace muz
@@ -322,6 +353,22 @@ int muz_minmax_bwd(const float* g, const float* a, const float* b, float scale, 
   MUZ_HOST_CHECK(M >= 0 && g && q && lohi && idx && dq && (a == nullptr) == (b == nullptr));
   if (M == 0) return MUZ_OK;
   k_minmax_bwd<256><<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(g, a, b, scale, scaled, q, lohi, idx, M, dq);
+  return muz_last_launch_error();
+}
+
+int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream) {
+  MUZ_HOST_CHECK(B >= 0 && W > 0 && Cin > 0 && K > 0 && x && cols);
+  const int64_t n = (int64_t)B * W * K * Cin;
+  if (n == 0) return MUZ_OK;
+  k_im2col_fwd<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, B, W, Cin, K, cols);
+  return muz_last_launch_error();
+}
+
+int muz_im2col_bwd(const float* dcols, int32_t B, int32_t W, int32_t Cin, int32_t K, float* dx, void* stream) {
+  MUZ_HOST_CHECK(B >= 0 && W > 0 && Cin > 0 && K > 0 && dcols && dx);
+  const int64_t n = (int64_t)B * W * Cin;
+  if (n == 0) return MUZ_OK;
+  k_im2col_bwd<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(dcols, B, W, Cin, K, dx);
   return muz_last_launch_error();
 }
 

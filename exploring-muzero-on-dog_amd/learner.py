@@ -71,6 +71,29 @@ class _DenseLN(torch.autograd.Function):
         return dx, dW, db, dgamma, dbeta, dres, None
 
 
+class _Im2col(torch.autograd.Function):
+    """The im2col matrix of a 'SAME' Conv1D (MuZeroNets._conv_cols) in one kernel each way
+    (csrc/learner_ln.hip; torch's pad + slices + cat made ~25 kernels per convolution's backward)."""
+
+    @staticmethod
+    def forward(ctx, x, K):
+        B, W, Cin = x.shape
+        x = x.contiguous()
+        cols = torch.empty((B, W, K * Cin), dtype=x.dtype, device=x.device)
+        _L.check(_L.load().muz_im2col_fwd(_L.ptr(x), B, W, Cin, K, _L.ptr(cols), _L.stream_ptr()), "muz_im2col_fwd")
+        ctx.K, ctx.shape = K, (B, W, Cin)
+        return cols
+
+    @staticmethod
+    def backward(ctx, dcols):
+        B, W, Cin = ctx.shape
+        dcols = dcols.contiguous()
+        dx = torch.empty((B, W, Cin), dtype=dcols.dtype, device=dcols.device)
+        _L.check(_L.load().muz_im2col_bwd(_L.ptr(dcols), B, W, Cin, ctx.K, _L.ptr(dx), _L.stream_ptr()),
+                 "muz_im2col_bwd")
+        return dx, None
+
+
 def _ln_fwd(y, bias, gamma, beta, res, mode):
     """Fused bias + LayerNorm (+ ReLU / residual ReLU) forward: -> (out, z, mean, rstd) (no autograd)."""
     M, Nn = y.shape
@@ -224,7 +247,7 @@ class _TrunkChain(torch.autograd.Function):
                 dza, _ = _ln_bwd_rows(dzb @ Wb.t(), fa, ga, LN_RELU, scr[(g, f"a{r}")][j])
                 cols[(g, f"a{r}")][0].append(xin)
                 cols[(g, f"a{r}")][1].append(dza)
-                dx = dres + dza @ Wa.t()
+                dx = dres.addmm_(dza, Wa.t())          # dres + dza Wa^T, the GEMM accumulating in place
             dz4, _ = _ln_bwd_rows(dx, f4, Q[8], LN_RELU, scr[(g, "4")][j])
             cols[(g, "4")][0].append(f3[0])
             cols[(g, "4")][1].append(dz4)
@@ -302,6 +325,8 @@ class MuZeroNets:
         are bit-identical."""
         k = self.p[f"{name}/kernel"]
         K, Cin, Cout = k.shape
+        if x.is_cuda:
+            return _Im2col.apply(x, K), k.reshape(K * Cin, Cout)
         pl = (K - 1) // 2
         W = x.shape[1]
         xp = F.pad(x, (0, 0, pl, K - 1 - pl))

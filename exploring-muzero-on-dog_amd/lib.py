@@ -289,6 +289,8 @@ SIGNATURES = {
     "muz_minmax_fwd": (ctypes.c_int, [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
     "muz_minmax_bwd": (ctypes.c_int, [vp, vp, vp, ctypes.c_float, ctypes.c_int32, vp, vp, vp, ctypes.c_int32,
                                       ctypes.c_int32, vp, vp]),
+    "muz_im2col_fwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),
+    "muz_im2col_bwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),
     "muz_adamw_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32, vp]),
     "muz_adamw_step": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_double,
                                       ctypes.c_double, ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double,

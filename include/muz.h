@@ -681,6 +681,10 @@ int muz_minmax_fwd(const float* x, const float* y, const float* bias, int32_t M,
                    float* lohi, int32_t* idx, void* stream);
 int muz_minmax_bwd(const float* g, const float* a, const float* b, float scale, int32_t scaled, const float* q,
                    const float* lohi, const int32_t* idx, int32_t M, int32_t N, float* dq, void* stream);
+/* 'SAME' Conv1D as a GEMM: the im2col matrix cols [B][W][K x Cin] of x [B][W][Cin] (zero outside each row;
+ * tap d reads column w + d - (K - 1) / 2) and its backward dx = sum over taps (fixed order). */
+int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream);
+int muz_im2col_bwd(const float* dcols, int32_t B, int32_t W, int32_t Cin, int32_t K, float* dx, void* stream);
 
 /* One optimizer step over ntensors parameter tensors (csrc/learner_opt.hip): optax.chain(
  * clip_by_global_norm(max_norm), adamw(lr, b1, b2, eps, weight_decay)) with the piecewise-constant lr

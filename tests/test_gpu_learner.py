@@ -303,3 +303,22 @@ def test_fused_adamw_matches_foreach_form(cuda):
             for i, (a, b) in enumerate(zip(xs, ys)):
                 assert torch.allclose(a, b, rtol=2e-6, atol=1e-8), (step, name, i, (a - b).abs().max().item())
     assert float(fused.count) == float(ref.count) == 7.0
+
+
+@pytest.mark.parametrize("K,Cin", [(3, 6), (3, 32), (5, 64)])
+def test_im2col_matches_pad_and_cat(cuda, K, Cin):
+    """learner._Im2col (one kernel each way) against the pad / slice / cat form of the same 'SAME' Conv1D
+    im2col matrix (MuZeroNets._conv_cols on the CPU path): forward identical, backward within float rounding."""
+    _, _, L, _, _ = _mods()
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(K * 100 + Cin)
+    x = torch.randn(7, 56, Cin, generator=g).cuda().requires_grad_(True)
+    dc = torch.randn(7, 56, K * Cin, generator=g).cuda()
+    cols = L._Im2col.apply(x, K)
+    (dx,) = torch.autograd.grad(cols, x, dc)
+    pl = (K - 1) // 2
+    xp = F.pad(x, (0, 0, pl, K - 1 - pl))
+    ref = torch.cat([xp[:, d:d + 56, :] for d in range(K)], dim=-1)
+    (dref,) = torch.autograd.grad(ref, x, dc)
+    assert torch.equal(cols, ref)
+    assert torch.allclose(dx, dref, rtol=1e-6, atol=1e-6)
