@@ -118,14 +118,13 @@ __device__ __forceinline__ int cls_step(const DetConsts& c, ClsLane& s, const Bo
   if (!invalid) {
     if (pin_at != -1 && (pin_at != cp || has(F, R_FRIENDLY))) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (q == pin_at && s.pins[q * 4 + k] == new_pos) s.pins[q * 4 + k] = -1;
+      for (int j = 0; j < 16; ++j) {   // (selects + asm guard: a folded a[i] store demotes pins to scratch)
+        int x = ((j >> 2) == pin_at && s.pins[j] == new_pos) ? -1 : s.pins[j];
+        asm volatile("" : "+v"(x));
+        s.pins[j] = x;
+      }
     }
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (j == cp * 4 + pi) s.pins[j] = new_pos;
+    rset(s.pins, cp * 4 + pi, new_pos);
     cls_rebuild_board(c, s, b);
   }
   const uint32_t w = winners(c, b);

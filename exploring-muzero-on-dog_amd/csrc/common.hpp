@@ -62,11 +62,27 @@ __device__ __forceinline__ const AS4 T* kernarg0() {
   return p;
 }
 
-// Dynamic index into a small register array without a scratch round trip.
+// Dynamic index into a small register array without a scratch round trip.  The empty asm after each select
+// keeps LLVM from folding the chain back into a[i] -- which demotes the whole array to scratch memory (it did:
+// 176 B/lane of scratch in k_det_round, round 2).
 template <int N>
 __device__ __forceinline__ int rsel(const int (&a)[N], int i) {
   int r = a[0];
 #pragma unroll
-  for (int j = 1; j < N; ++j) r = (i == j) ? a[j] : r;
+  for (int j = 1; j < N; ++j) {
+    r = (i == j) ? a[j] : r;
+    asm volatile("" : "+v"(r));
+  }
   return r;
+}
+
+// a[i] = v for a dynamic i, by selects over the register array (same folding guard as rsel).
+template <int N>
+__device__ __forceinline__ void rset(int (&a)[N], int i, int v) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    int x = (i == j) ? v : a[j];
+    asm volatile("" : "+v"(x));
+    a[j] = x;
+  }
 }

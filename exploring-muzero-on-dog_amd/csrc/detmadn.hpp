@@ -66,7 +66,10 @@ __device__ __forceinline__ int goal_of(const DetConsts& c, int p, int g) {
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int h = 0; h < 4; ++h) r = (p == q && g == h) ? c.goal[q][h] : r;
+    for (int h = 0; h < 4; ++h) {
+      r = (p == q && g == h) ? c.goal[q][h] : r;
+      asm volatile("" : "+v"(r));   // (see rsel: keeps the consts out of scratch)
+    }
   return r;
 }
 
@@ -215,14 +218,13 @@ __device__ __forceinline__ int det_step(const DetConsts& c, DetLane& s, const Bo
   if (!invalid) {
     if (pin_at != -1 && (pin_at != cp || has(F, R_FRIENDLY))) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (q == pin_at && s.pins[q * 4 + k] == new_pos) s.pins[q * 4 + k] = -1;
+      for (int j = 0; j < 16; ++j) {
+        int x = ((j >> 2) == pin_at && s.pins[j] == new_pos) ? -1 : s.pins[j];
+        asm volatile("" : "+v"(x));
+        s.pins[j] = x;
+      }
     }
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (j == cp * 4 + pi) s.pins[j] = new_pos;
+    rset(s.pins, cp * 4 + pi, new_pos);
     rebuild_board(c, s, b);
   }
   // action set: decrement [cp, move-1]; if the row empties, refill row current_player of the
@@ -234,12 +236,13 @@ __device__ __forceinline__ int det_step(const DetConsts& c, DetLane& s, const Bo
   for (int m = 0; m < 6; ++m) row_empty &= ((m == mi) ? nv : aset_of(s, cp, m)) == 0;
   if (row_empty) {
 #pragma unroll
-    for (int j = 0; j < 24; ++j)
-      if (j / 6 == player_id) s.aset[j] = 4;
+    for (int j = 0; j < 24; ++j) {
+      int x = (j / 6 == player_id) ? 4 : s.aset[j];
+      asm volatile("" : "+v"(x));
+      s.aset[j] = x;
+    }
   } else {
-#pragma unroll
-    for (int j = 0; j < 24; ++j)
-      if (j == cp * 6 + mi) s.aset[j] = nv;
+    rset(s.aset, cp * 6 + mi, nv);
   }
   const uint32_t w = winners(c, b);
   const int reward = s.done ? 0 : (invalid ? -1 : (int)((w >> cp) & 1u));
@@ -253,8 +256,11 @@ __device__ __forceinline__ int det_step(const DetConsts& c, DetLane& s, const Bo
 // no_step (deterministic_madn.py:283-297).
 __device__ __forceinline__ void det_nostep(const DetConsts& c, DetLane& s) {
 #pragma unroll
-  for (int j = 0; j < 24; ++j)
-    if (j / 6 == s.cp) s.aset[j] = 4;
+  for (int j = 0; j < 24; ++j) {
+    int x = (j / 6 == s.cp) ? 4 : s.aset[j];
+    asm volatile("" : "+v"(x));
+    s.aset[j] = x;
+  }
   s.cp = (s.cp + 1) % c.P;
 }
 

@@ -43,7 +43,23 @@ struct DogG {   // one game in LDS
   int need_deal;
 };
 
-__device__ __forceinline__ int dgoal(const DetConsts& c, int p, int g) { return goal_of(c, p, g); }
+// (DOG keeps the plain select chains: k_dog_play runs at 64 VGPRs, where rsel / goal_of's VGPR guards add
+// spills -- its lane-0 transitions index wave-uniform values)
+__device__ __forceinline__ int dgoal(const DetConsts& c, int p, int g) {
+  int r = c.goal[0][0];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int h = 0; h < 4; ++h) r = (p == q && g == h) ? c.goal[q][h] : r;
+  return r;
+}
+
+__device__ __forceinline__ int dcst(const int (&a)[4], int i) {
+  int r = a[0];
+#pragma unroll
+  for (int j = 1; j < 4; ++j) r = (i == j) ? a[j] : r;
+  return r;
+}
 
 __device__ __forceinline__ bool dog_player_done(const DetConsts& c, const int8_t* board, int p) {
   if (p >= c.P) return false;
@@ -83,7 +99,7 @@ __device__ __forceinline__ bool dog_goal_free(const DetConsts& c, const int8_t* 
 }
 
 __device__ __forceinline__ bool pos_on_start(const DetConsts& c, const int8_t* board, int q) {
-  return q < c.P && board[cst(c.start, q)] == q;
+  return q < c.P && board[dcst(c.start, q)] == q;
 }
 
 // ---- val_swap (dog.py:317-348): bit [pin, pos] -------------------------------------------------
@@ -93,7 +109,7 @@ __device__ __forceinline__ bool dog_val_swap(const DetConsts& c, const DogG& s, 
   bool ok = !(b == -1 || b == cp);                       // cond_a
   bool is_start = false;
   for (int q = 0; q < c.P; ++q)
-    if (cst(c.start, q) == pos) {                        // cond_b (start columns)
+    if (dcst(c.start, q) == pos) {                        // cond_b (start columns)
       is_start = true;
       ok = !((s.board[pos] == q) && has(F, R_START_BLOCK)) && (s.board[pos] != -1);
     }
@@ -105,7 +121,7 @@ __device__ __forceinline__ bool dog_val_swap(const DetConsts& c, const DogG& s, 
   for (int q = 0; q < c.P; ++q)                           // condA: every goal column
     if (in_goal_p(c, q, pos)) ok = false;
   const int cur = dpin(s, cp, pin);                       // condB: disallowed pin positions
-  const bool dis = cur == -1 || (has(F, R_START_BLOCK) && cur == cst(c.start, cp)) || in_goal_p(c, cp, cur);
+  const bool dis = cur == -1 || (has(F, R_START_BLOCK) && cur == dcst(c.start, cp)) || in_goal_p(c, cp, cur);
   return ok && !dis;
 }
 
@@ -113,7 +129,7 @@ __device__ __forceinline__ bool dog_val_swap(const DetConsts& c, const DogG& s, 
 __device__ __forceinline__ bool dog_val_normal(const DetConsts& c, const DogG& s, int cp, int pin, int move) {
   const uint32_t F = c.flags;
   const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
-  const int tgt = cst(c.target, cp);
+  const int tgt = dcst(c.target, cp);
   const int g0 = dgoal(c, cp, 0), g3 = dgoal(c, cp, 3);
   const int cur = dpin(s, cp, pin);
   if (cur == -1) return (move == 1 || move == 11 || move == 13) && !pos_on_start(c, s.board, cp) && move > 0;
@@ -123,9 +139,9 @@ __device__ __forceinline__ bool dog_val_normal(const DetConsts& c, const DogG& s
   bool res = (s.board[fitted] != cp) || has(F, R_FRIENDLY);
   const int nsb_j = jidx(fmodp(fdiv(cur, kDist) + 1, c.P), c.P);
   const int nsa_j = jidx(fdiv(fitted, kDist), c.P);
-  const bool trav = cst(c.start, nsb_j) == cst(c.start, nsa_j);
+  const bool trav = dcst(c.start, nsb_j) == dcst(c.start, nsa_j);
   const bool pa = pos_on_start(c, s.board, nsa_j);
-  if (has(F, R_START_BLOCK) && trav) res = (!pa || cur == cst(c.start, cp)) && res;
+  if (has(F, R_START_BLOCK) && trav) res = (!pa || cur == dcst(c.start, cp)) && res;
   if (mt && has(F, R_START_BLOCK) && trav && pa) x = 0;
   if (!has(F, R_CIRCULAR) && cur <= tgt && (x > 4 || (x == 0 && mt))) res = false;
   if (4 >= x && x > 0 && cur <= tgt) {
@@ -151,16 +167,16 @@ __device__ __forceinline__ bool dog_val_neg(const DetConsts& c, const DogG& s, i
   bool res = (s.board[fitted] != cp) || has(F, R_FRIENDLY);
   const int nsb_j = jidx(fdiv(cur, kDist), c.P);
   const int nsa_j = jidx(fmodp(fdiv(fitted, kDist) + 1, c.P), c.P);
-  const bool cond = cst(c.start, nsb_j) == cst(c.start, nsa_j);
-  if (has(F, R_START_BLOCK) && cond) res = (!pos_on_start(c, s.board, nsa_j) || cur == cst(c.start, cp)) && res;
-  return res && (has(F, R_CIRCULAR) || moved >= cst(c.start, cp));
+  const bool cond = dcst(c.start, nsb_j) == dcst(c.start, nsa_j);
+  if (has(F, R_START_BLOCK) && cond) res = (!pos_on_start(c, s.board, nsa_j) || cur == dcst(c.start, cp)) && res;
+  return res && (has(F, R_CIRCULAR) || moved >= dcst(c.start, cp));
 }
 
 // ---- val_action_7 (dog.py:350-481) for one distribution ------------------------------------------
 __device__ __forceinline__ bool dog_val7(const DetConsts& c, const DogG& s, int cp, const int (&d)[4]) {
   const uint32_t F = c.flags;
   const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
-  const int tgt = cst(c.target, cp);
+  const int tgt = dcst(c.target, cp);
   const int g3 = dgoal(c, cp, 3);
   int cur[4], moved[4];
   bool ing[4];
@@ -170,7 +186,7 @@ __device__ __forceinline__ bool dog_val7(const DetConsts& c, const DogG& s, int 
     cur[k] = dpin(s, cp, k);
     moved[k] = cur[k] + d[k];
     ing[k] = in_goal_p(c, cp, cur[k]);
-    pos_cp |= (cur[k] == cst(c.start, cp)) && (moved[k] == cst(c.start, cp));
+    pos_cp |= (cur[k] == dcst(c.start, cp)) && (moved[k] == dcst(c.start, cp));
   }
   // goal cells of cp occupied by cp after the in-goal pins moved (tmp_board)
   bool occ[4];
@@ -189,7 +205,7 @@ __device__ __forceinline__ bool dog_val7(const DetConsts& c, const DogG& s, int 
     bool res = has(F, R_CIRCULAR) ? true : !((cur[k] <= tgt) && ((moved[k] > tgt + 4) || (x == 0 && mt)));
     const int nsb_j = jidx(fmodp(fdiv(cur[k], kDist) + 1, c.P), c.P);
     const int nsa_j = jidx(fdiv(fitted, kDist), c.P);
-    const bool trav = cst(c.start, nsb_j) == cst(c.start, nsa_j);
+    const bool trav = dcst(c.start, nsb_j) == dcst(c.start, nsa_j);
     const bool pa = (nsa_j == cp) ? pos_cp : pos_on_start(c, s.board, nsa_j);
     if (has(F, R_START_BLOCK) && trav) res = !pa && res;
     if (mt && has(F, R_START_BLOCK) && trav && pa) x = 0;

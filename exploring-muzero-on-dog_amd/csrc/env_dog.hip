@@ -186,7 +186,7 @@ __device__ void dog_step_normal(const DetConsts& c, DogG& s, int cp, int pin, in
   const uint32_t F = c.flags;
   const bool invalid = !legal && !dog_val_normal(c, s, cp, pin, move);
   const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
-  const int tgt = cst(c.target, cp);
+  const int tgt = dcst(c.target, cp);
   const int g0 = dgoal(c, cp, 0);
   const int cur = s.pins[cp * 4 + pin];
   const int moved = cur + move;
@@ -198,7 +198,7 @@ __device__ void dog_step_normal(const DetConsts& c, DogG& s, int cp, int pin, in
   const bool A = (s.board[gx] != cp) && (has(F, R_JUMP_GOAL) || a);
   int npos;
   if (cur == -1)
-    npos = cst(c.start, cp);
+    npos = dcst(c.start, cp);
   else if (ing)
     npos = moved;
   else if (4 >= x && x > 0 && A && cur <= tgt)
@@ -228,7 +228,7 @@ __device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d
   const uint32_t F = c.flags;
   const bool invalid = !legal && !dog_val7(c, s, cp, d);
   const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
-  const int tgt = cst(c.target, cp);
+  const int tgt = dcst(c.target, cp);
   int cur[4], moved[4], npos[4];
   bool ing[4];
   for (int k = 0; k < 4; ++k) {
@@ -269,7 +269,7 @@ __device__ void dog_step_hot7(const DetConsts& c, DogG& s, int cp, const int (&d
                         : (path_bits(cur[k], tgt, kTrack, false) | path_bits(g0, npos[k], kCells, false));
   }
   if (cross)
-    for (int k = 0; k < 4; ++k) row[k] |= 1ull << cst(c.start, cp);
+    for (int k = 0; k < 4; ++k) row[k] |= 1ull << dcst(c.start, cp);
   const unsigned long long anyp = row[0] | row[1] | row[2] | row[3];
   if (!invalid) {
     uint32_t hit = 0;   // bit p*4+k

@@ -1,0 +1,23 @@
+"""Per-launch means of the counters in <dir>/p*/**/*counter_collection.csv (profiles/pmc_env.sh), plus the
+derived utilisations (SQ_* quad-cycle units per MI355X_MICROARCH.md; FETCH/WRITE_SIZE in KB)."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+d = sys.argv[1]
+per = collections.defaultdict(lambda: collections.defaultdict(float))
+for f in glob.glob(f"{d}/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        per[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+m = {k: sum(v.values()) / len(v) for k, v in per.items()}
+out = {"counters_per_launch": m, "launches": {k: len(v) for k, v in per.items()}}
+if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+    out["hbm_bytes_per_launch"] = (m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
+if "SQ_ACTIVE_INST_VALU" in m and "SQ_WAVE_CYCLES" in m:
+    out["valu_active_per_wave_cycle"] = m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"]
+    out["wait_any_per_wave_cycle"] = m.get("SQ_WAIT_ANY", 0) / m["SQ_WAVE_CYCLES"]
+if "SQ_LDS_BANK_CONFLICT" in m and "SQ_LDS_IDX_ACTIVE" in m:
+    out["lds_conflict_share"] = m["SQ_LDS_BANK_CONFLICT"] / max(1.0, m["SQ_LDS_IDX_ACTIVE"])
+print(json.dumps(out, indent=1))
