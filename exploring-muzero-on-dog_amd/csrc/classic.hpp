@@ -86,13 +86,15 @@ __device__ __forceinline__ void cls_rebuild_board(const DetConsts& c, const ClsL
       }
 }
 
-// env_step (classic_madn.py:257-337): move pin `pin` of the substituted player by s.die.
-__device__ __forceinline__ int cls_step(const DetConsts& c, ClsLane& s, const BoardView& b, int pin) {
+// env_step (classic_madn.py:257-337): move pin `pin` of the substituted player by s.die, given the state's
+// legal mask (valid_action of the same state and die; cls_step computes it).
+__device__ __forceinline__ int cls_step_masked(const DetConsts& c, ClsLane& s, const BoardView& b, int pin,
+                                               const uint32_t legal) {
   const uint32_t F = c.flags;
   const int player_id = s.cp;
   const int cp = sub_player(c, b, player_id);
   const int pi = jidx((int)(int8_t)pin, 4);
-  const bool invalid = ((cls_legal(c, s, b) >> pi) & 1u) == 0u;
+  const bool invalid = ((legal >> pi) & 1u) == 0u;
   const int move = s.die;
   const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
   const int tgt = cst(c.target, cp);
@@ -134,6 +136,10 @@ __device__ __forceinline__ int cls_step(const DetConsts& c, ClsLane& s, const Bo
   s.done = done;
   s.reward = reward;
   return reward;
+}
+
+__device__ __forceinline__ int cls_step(const DetConsts& c, ClsLane& s, const BoardView& b, int pin) {
+  return cls_step_masked(c, s, b, pin, cls_legal(c, s, b));
 }
 
 // is_soft_locked (classic_madn.py:180-206): the UNSUBSTITUTED current player's pins out of the house

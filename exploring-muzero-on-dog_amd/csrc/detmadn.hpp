@@ -183,13 +183,14 @@ __device__ __forceinline__ void rebuild_board(const DetConsts& c, const DetLane&
       }
 }
 
-// env_step (deterministic_madn.py:170-257) with (pin, move).  Updates s and the LDS board.
+// env_step (deterministic_madn.py:170-257) with (pin, move), given the state's legal mask (valid_action of
+// the same state; callers that already hold it skip the second legality pass).  Updates s and the LDS board.
 // Returns the reward; s.done / s.reward / s.cp updated like the reference.
-__device__ __forceinline__ int det_step(const DetConsts& c, DetLane& s, const BoardView& b, int pin, int move) {
+__device__ __forceinline__ int det_step_masked(const DetConsts& c, DetLane& s, const BoardView& b, int pin, int move,
+                                               const uint32_t legal) {
   const uint32_t F = c.flags;
   const int player_id = s.cp;
   const int cp = sub_player(c, b, player_id);
-  const uint32_t legal = det_legal(c, s, b);
   const int mi = jidx(move - 1, 6);
   const int pi = jidx(pin, 4);
   const bool invalid = ((legal >> (pi * 6 + mi)) & 1u) == 0u;
@@ -251,6 +252,10 @@ __device__ __forceinline__ int det_step(const DetConsts& c, DetLane& s, const Bo
   s.done = done;
   s.reward = reward;
   return reward;
+}
+
+__device__ __forceinline__ int det_step(const DetConsts& c, DetLane& s, const BoardView& b, int pin, int move) {
+  return det_step_masked(c, s, b, pin, move, det_legal(c, s, b));
 }
 
 // no_step (deterministic_madn.py:283-297).

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detm
       uint32_t x = lb;
       for (int j = 0; j < k; ++j) x &= x - 1;   // drop the k lowest set bits
       const int a = __ffs(x) - 1;
-      r = det_step(c, s, b, a / 6, a % 6 + 1);
+      r = det_step_masked(c, s, b, a / 6, a % 6 + 1, lb);   // lb: this state's mask (the round contract)
     }
     const int fin = s.done;
     if (fin) {   // env_reset in place with the batch's rules (deterministic_madn.py:42-120)

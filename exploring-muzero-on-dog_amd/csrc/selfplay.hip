@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64) void k_sp_encode(DetConsts c, muz_detmadn_soa s
 __global__ __launch_bounds__(kSpBlock) void k_sp_apply(DetConsts c, muz_detmadn_soa st, const int32_t* flag,
                                                        const int32_t* slot, const int32_t* s_action,
                                                        const float* s_weights, const float* s_value, muz_traj tr,
-                                                       int n, const int32_t* lane_game) {
+                                                       int n, const int32_t* lane_game, const uint32_t* legal) {
   __shared__ int8_t sboard[kCells * kSpBlock];
   const int g = blockIdx.x * kSpBlock + threadIdx.x;
   if (g >= n) return;
@@ -103,7 +103,8 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_apply(DetConsts c, muz_detmadn_
   if (f == 1) {
     const int sl = slot[g];
     act = s_action[sl];
-    const int r = det_step(c, s, b, fdiv(act, 6), fmodp(act, 6) + 1);
+    // legal[g]: this state's mask from k_sp_flags (the state is unchanged since), so no second legality pass
+    const int r = det_step_masked(c, s, b, fdiv(act, 6), fmodp(act, 6) + 1, legal[g]);
     const bool nd = s.done != 0;
     const int next_player = s.cp;
     const int next_team = teams ? next_player % 2 : -1;
@@ -295,7 +296,7 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
       break;
     led.search_end(turn);
     k_sp_apply<<<(n + kSpBlock - 1) / kSpBlock, kSpBlock, 0, s>>>(c, st, ws.flag, ws.slot, ws.action, ws.weights,
-                                                                   ws.value, tr, n, lane_game);
+                                                                   ws.value, tr, n, lane_game, ws.legal);
     if ((rc = muz_last_launch_error())) break;
     ++turns;
   }

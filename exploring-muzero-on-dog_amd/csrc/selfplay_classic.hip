@@ -86,7 +86,8 @@ __global__ __launch_bounds__(64) void k_cs_encode(DetConsts c, muz_classic_soa s
 __global__ __launch_bounds__(kCsBlock) void k_cs_apply(DetConsts c, muz_classic_soa st, const int32_t* flag,
                                                        const int32_t* slot, const int32_t* s_action,
                                                        const float* s_weights, const float* s_value, muz_traj tr,
-                                                       muz_traj_chance ch, int n, const int32_t* lane_game) {
+                                                       muz_traj_chance ch, int n, const int32_t* lane_game,
+                                                       const uint32_t* legal) {
   __shared__ int8_t sboard[kCells * kCsBlock];
   const int g = blockIdx.x * kCsBlock + threadIdx.x;
   if (g >= n) return;
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(kCsBlock) void k_cs_apply(DetConsts c, muz_classic_
   if (f == 1) {
     const int sl = slot[g];
     act = s_action[sl];
-    const int r = cls_step(c, s, b, act);
+    const int r = cls_step_masked(c, s, b, act, legal[g]);   // legal[g]: this state's mask (k_cs_flags)
     const bool nd = s.done != 0;
     const int next_team = teams ? s.cp % 2 : -1;
     rew_cls = (nd && r > 0) ? 2 : ((nd && r < 0) ? 0 : 1);
@@ -292,7 +293,7 @@ static int cs_turns(const DetConsts& c, const muz_classic_net_w* w, const muz_st
       break;
     led.search_end(turn);
     k_cs_apply<<<(n + kCsBlock - 1) / kCsBlock, kCsBlock, 0, s>>>(c, st, ws.flag, ws.slot, ws.action, ws.weights,
-                                                                   ws.value, tr, ch, n, lane_game);
+                                                                   ws.value, tr, ch, n, lane_game, ws.legal);
     if ((rc = muz_last_launch_error())) break;
     ++turns;
   }
