@@ -545,7 +545,7 @@ def run_train(args):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(train_steps):
-                learner.train_step(ring.sample_batch())
+                learner.train_step_from(ring)
             e1.record()
             e1.synchronize()
             stats["learner_ms"] += e0.elapsed_time(e1)

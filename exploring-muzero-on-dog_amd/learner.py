@@ -71,6 +71,37 @@ class _DenseLN(torch.autograd.Function):
         return dx, dW, db, dgamma, dbeta, dres, None
 
 
+_ONES = {}
+
+
+def _ones(M, like):
+    """A cached ones vector of length M (filled on the eager warm-up step, so a captured graph reuses it)."""
+    key = (M, like.device, like.dtype)
+    v = _ONES.get(key)
+    if v is None:
+        v = _ONES[key] = torch.ones((M,), dtype=like.dtype, device=like.device)
+    return v
+
+
+class _Dense(torch.autograd.Function):
+    """x @ W + b whose bias gradient is a BLAS GEMV (dy^T @ 1) instead of torch's column-sum reduction
+    (~12 us per call at the learner's 1280-1408 rows, against ~5 us)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        return (x @ W).add_(b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dy @ W.t() if ctx.needs_input_grad[0] else None
+        dW = x.reshape(-1, x.shape[-1]).t() @ dy2 if ctx.needs_input_grad[1] else None
+        db = torch.mv(dy2.t(), _ones(dy2.shape[0], dy2)) if ctx.needs_input_grad[2] else None
+        return dx, dW, db
+
+
 class _Im2col(torch.autograd.Function):
     """The im2col matrix of a 'SAME' Conv1D (MuZeroNets._conv_cols) in one kernel each way
     (csrc/learner_ln.hip; torch's pad + slices + cat made ~25 kernels per convolution's backward)."""
@@ -94,10 +125,12 @@ class _Im2col(torch.autograd.Function):
         return dx, None
 
 
-def _ln_fwd(y, bias, gamma, beta, res, mode):
-    """Fused bias + LayerNorm (+ ReLU / residual ReLU) forward: -> (out, z, mean, rstd) (no autograd)."""
+def _ln_fwd(y, bias, gamma, beta, res, mode, out=None):
+    """Fused bias + LayerNorm (+ ReLU / residual ReLU) forward: -> (out, z, mean, rstd) (no autograd).
+    `out`: a preallocated contiguous [M, N] destination (a row block of a stacked buffer)."""
     M, Nn = y.shape
-    out, z = torch.empty_like(y), torch.empty_like(y)
+    out = torch.empty_like(y) if out is None else out
+    z = torch.empty_like(y)
     mean = torch.empty((M,), dtype=y.dtype, device=y.device)
     rstd = torch.empty_like(mean)
     _L.check(_L.load().muz_ln_fwd(_L.ptr(y), _L.ptr(bias), _L.ptr(gamma), _L.ptr(beta), _L.ptr(res), M, Nn, mode,
@@ -105,12 +138,13 @@ def _ln_fwd(y, bias, gamma, beta, res, mode):
     return out, z, mean, rstd
 
 
-def _ln_bwd_rows(dout, fwd, gamma, mode, scratch):
-    """Row half of the fused backward: -> (dz, dres or None); column partials into scratch."""
+def _ln_bwd_rows(dout, fwd, gamma, mode, scratch, dz=None):
+    """Row half of the fused backward: -> (dz, dres or None); column partials into scratch.  `dz`: a
+    preallocated contiguous destination."""
     out, z, mean, rstd = fwd
     M, Nn = out.shape
     dout = dout.contiguous()
-    dz = torch.empty_like(out)
+    dz = torch.empty_like(out) if dz is None else dz
     dres = torch.empty_like(out) if mode == LN_RESID_RELU else None
     _L.check(_L.load().muz_ln_bwd_rows(_L.ptr(dout), _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.ptr(gamma),
                                        M, Nn, mode, _L.ptr(dz), _L.ptr(dres), _L.ptr(scratch), _L.stream_ptr()),
@@ -156,6 +190,18 @@ CHAIN = True                     # False: the losses build the per-step autograd
 _NP = len(DYN_TRUNK_PARAMS)      # 28 per trunk
 
 
+_GEMM_LAYERS = ("3", "4", "a0", "b0", "a1", "b1", "5")   # the trunk's weight layers, named by their input
+
+
+def _slots(apps, ngroups):
+    """-> (slot, seen): application i's index among its group's applications, and each group's count."""
+    slot, seen = [], [0] * ngroups
+    for g in apps:
+        slot.append(seen[g])
+        seen[g] += 1
+    return slot, seen
+
+
 class _TrunkChain(torch.autograd.Function):
     """The sequential FiLM-trunk applications of an unrolled loss as ONE autograd node.  Application i maps
     x_i -> x_{i+1} = minmax(x_i + proj(trunk(LN(x_i) * (1 + scale_i) + shift_i))) with trunk group apps[i]'s
@@ -184,26 +230,33 @@ class _TrunkChain(torch.autograd.Function):
         scale1 = 1.0 + scale
         lib = _L.load()
         st = []
+        slot, seen = _slots(apps, len(P) // _NP)
+        # every weight layer's inputs of all applications of a group, stacked [apps, B, N]: each layer writes
+        # its output straight into the next layer's block, so the backward's weight gradient is one GEMM
+        # over the stack without concatenating anything
+        X = {(g, n): torch.empty((max(seen[g], 1), B, Nn), dtype=dt, device=dev)
+             for g in range(len(seen)) for n in _GEMM_LAYERS}
         lat = latent0.contiguous()
         for i in range(T):
-            Q = P[_NP * apps[i]:_NP * (apps[i] + 1)]
+            g, j = apps[i], slot[i]
+            Q = P[_NP * g:_NP * (g + 1)]
             g0, be0, W3, b3, g1, be1, W4, b4, g2, be2 = Q[:10]
             f0 = _ln_fwd(lat, zero, g0, be0, None, LN_PLAIN)
-            x0 = torch.addcmul(shift[i], f0[0], scale1[i])
-            f3 = _ln_fwd(x0 @ W3, b3, g1, be1, None, LN_RELU)
-            f4 = _ln_fwd(f3[0] @ W4, b4, g2, be2, None, LN_RELU)
+            x0 = torch.addcmul(shift[i], f0[0], scale1[i], out=X[(g, "3")][j])
+            f3 = _ln_fwd(x0 @ W3, b3, g1, be1, None, LN_RELU, out=X[(g, "4")][j])
+            f4 = _ln_fwd(f3[0] @ W4, b4, g2, be2, None, LN_RELU, out=X[(g, "a0")][j])
             x, rbs = f4[0], []
             for r in range(2):
                 Wa, ba, ga, bea, Wb, bb, gb, beb = Q[10 + 8 * r:18 + 8 * r]
-                fa = _ln_fwd(x @ Wa, ba, ga, bea, None, LN_RELU)
-                fb = _ln_fwd(fa[0] @ Wb, bb, gb, beb, x, LN_RESID_RELU)
+                fa = _ln_fwd(x @ Wa, ba, ga, bea, None, LN_RELU, out=X[(g, f"b{r}")][j])
+                fb = _ln_fwd(fa[0] @ Wb, bb, gb, beb, x, LN_RESID_RELU, out=X[(g, "a1" if r == 0 else "5")][j])
                 rbs.append((x, fa, fb))
                 x = fb[0]
             _L.check(lib.muz_minmax_fwd(_L.ptr(lat), _L.ptr(x @ Q[26]), _L.ptr(Q[27]), B, Nn, _L.ptr(outs[i]),
                                         _L.ptr(qs[i]), _L.ptr(lohi[i]), _L.ptr(idx[i]), _L.stream_ptr()), "muz_minmax_fwd")
             st.append((f0, x0, f3, f4, rbs, x))
             lat = outs[i]
-        ctx.st, ctx.P, ctx.grad_scale = st, P, float(grad_scale)
+        ctx.st, ctx.X, ctx.P, ctx.grad_scale = st, X, P, float(grad_scale)
         ctx.apps, ctx.scaled = tuple(apps), tuple(scaled)
         ctx.save_for_backward(scale1, qs, lohi, idx)
         return outs
@@ -218,42 +271,31 @@ class _TrunkChain(torch.autograd.Function):
         lib = _L.load()
         nf = lib.muz_ln_bwd_scratch_floats(B, Nn)
         ngroups = len(P) // _NP
-        slot, seen = [], [0] * ngroups           # application i's row in its group's column-partial buffers
-        for g in apps:
-            slot.append(seen[g])
-            seen[g] += 1
+        slot, seen = _slots(apps, ngroups)       # application i's row in its group's stacked buffers
         layers = ("0", "3", "4", "a0", "b0", "a1", "b1")
         scr = {(g, n): torch.empty((max(seen[g], 1), nf), dtype=dt, device=dev) for g in range(ngroups) for n in layers}
-        cols = {(g, n): ([], []) for g in range(ngroups) for n in layers[1:] + ("5",)}   # (layer inputs, output grads)
+        # output gradients of the weight layers, stacked like the forward's inputs (ctx.X)
+        DZ = {(g, n): torch.empty((max(seen[g], 1), B, Nn), dtype=dt, device=dev)
+              for g in range(ngroups) for n in _GEMM_LAYERS}
         dscale, dshift = torch.empty_like(scale1), torch.empty_like(scale1)
         ca = cb = None                            # the carried gradient of x_{i+1}: ca + cb
         for i in range(T - 1, -1, -1):
             g, j = apps[i], slot[i]
             Q = P[_NP * g:_NP * (g + 1)]
             f0, x0, f3, f4, rbs, x5 = st[i]
-            dq = torch.empty((B, Nn), dtype=dt, device=dev)
+            dq = DZ[(g, "5")][j]
             _L.check(lib.muz_minmax_bwd(_L.ptr(G[i]), _L.ptr(ca), _L.ptr(cb), s, int(ctx.scaled[i]), _L.ptr(qs[i]),
                                         _L.ptr(lohi[i]), _L.ptr(idx[i]), B, Nn, _L.ptr(dq), _L.stream_ptr()),
                      "muz_minmax_bwd")
-            cols[(g, "5")][0].append(x5)
-            cols[(g, "5")][1].append(dq)
             dx = dq @ Q[26].t()
             for r in (1, 0):
                 xin, fa, fb = rbs[r]
                 Wa, ga, Wb, gb = Q[10 + 8 * r], Q[12 + 8 * r], Q[14 + 8 * r], Q[16 + 8 * r]
-                dzb, dres = _ln_bwd_rows(dx, fb, gb, LN_RESID_RELU, scr[(g, f"b{r}")][j])
-                cols[(g, f"b{r}")][0].append(fa[0])
-                cols[(g, f"b{r}")][1].append(dzb)
-                dza, _ = _ln_bwd_rows(dzb @ Wb.t(), fa, ga, LN_RELU, scr[(g, f"a{r}")][j])
-                cols[(g, f"a{r}")][0].append(xin)
-                cols[(g, f"a{r}")][1].append(dza)
+                dzb, dres = _ln_bwd_rows(dx, fb, gb, LN_RESID_RELU, scr[(g, f"b{r}")][j], DZ[(g, f"b{r}")][j])
+                dza, _ = _ln_bwd_rows(dzb @ Wb.t(), fa, ga, LN_RELU, scr[(g, f"a{r}")][j], DZ[(g, f"a{r}")][j])
                 dx = dres.addmm_(dza, Wa.t())          # dres + dza Wa^T, the GEMM accumulating in place
-            dz4, _ = _ln_bwd_rows(dx, f4, Q[8], LN_RELU, scr[(g, "4")][j])
-            cols[(g, "4")][0].append(f3[0])
-            cols[(g, "4")][1].append(dz4)
-            dz3, _ = _ln_bwd_rows(dz4 @ Q[6].t(), f3, Q[4], LN_RELU, scr[(g, "3")][j])
-            cols[(g, "3")][0].append(x0)
-            cols[(g, "3")][1].append(dz3)
+            dz4, _ = _ln_bwd_rows(dx, f4, Q[8], LN_RELU, scr[(g, "4")][j], DZ[(g, "4")][j])
+            dz3, _ = _ln_bwd_rows(dz4 @ Q[6].t(), f3, Q[4], LN_RELU, scr[(g, "3")][j], DZ[(g, "3")][j])
             dx0 = torch.mm(dz3, Q[2].t(), out=dshift[i])
             torch.mul(dx0, f0[0], out=dscale[i])
             dz0, _ = _ln_bwd_rows(dx0 * scale1[i], f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
@@ -267,11 +309,11 @@ class _TrunkChain(torch.autograd.Function):
             grads[o], grads[o + 1], _ = _ln_colsum(scr[(g, "0")], Nn)
             for n, (iw, ib, ig, ibe) in (("3", (2, 3, 4, 5)), ("4", (6, 7, 8, 9)), ("a0", (10, 11, 12, 13)),
                                          ("b0", (14, 15, 16, 17)), ("a1", (18, 19, 20, 21)), ("b1", (22, 23, 24, 25))):
-                X, DZ = (torch.cat(c, 0) for c in cols[(g, n)])
-                grads[o + iw] = X.t() @ DZ
+                Xs, Ds = (t[(g, n)][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
+                grads[o + iw] = Xs.t() @ Ds
                 grads[o + ig], grads[o + ibe], grads[o + ib] = _ln_colsum(scr[(g, n)], Nn)
-            X, DZ = (torch.cat(c, 0) for c in cols[(g, "5")])
-            grads[o + 26], grads[o + 27] = X.t() @ DZ, DZ.sum(0)
+            Xs, Ds = (t[(g, "5")][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
+            grads[o + 26], grads[o + 27] = Xs.t() @ Ds, torch.mv(Ds.t(), _ones(Ds.shape[0], Ds))
         return (ca + cb, dscale, dshift, None, None, None, *grads)
 
 
@@ -297,6 +339,8 @@ class MuZeroNets:
     def _dense(self, name, x):
         # (not addmm: torch routes a GEMM with a bias epilogue to hipBLASLt whatever the preferred BLAS, and
         # hipBLASLt's macro-tiles make these small GEMMs ~33 us each; see prefer_rocblas)
+        if x.is_cuda:
+            return _Dense.apply(x, self.p[f"{name}/kernel"], self.p[f"{name}/bias"])
         return x @ self.p[f"{name}/kernel"] + self.p[f"{name}/bias"]
 
     def _ln(self, name, x):
@@ -633,6 +677,22 @@ class Learner:
         # the captured outputs are overwritten by the next replay: hand out copies so a caller may keep them
         return {k: v.clone() for k, v in self._out.items()}
 
+    def train_step_from(self, ring) -> dict:
+        """train_step on the next batch of a device ring (``ring.sample_batch()``).  Once the step is captured,
+        the ring writes the batch straight into the graph's static inputs (no per-key copy)."""
+        if self.graph and self._g is not None:
+            ep, t = ring.draw_indices()
+            if not getattr(self, "_static_full", False):    # the batch fields the step does not read
+                B, K = len(ep), ring.unroll_steps + 1
+                fresh = ring._new_batch(B, K, ring.obs_shape[0], ring.action_dim, dict(device=ring.device))
+                for k, v in fresh.items():
+                    self._static.setdefault(k, v)
+                self._static_full = True
+            ring.sample_at(ep, t, out=self._static)
+            self._g.replay()
+            return {k: v.clone() for k, v in self._out.items()}
+        return self.train_step(ring.sample_batch())
+
     def push_to(self, net: "N.DeviceNet"):
         """Pack the current parameters into the self-play engine's arena (same layout) in place."""
         fresh = self._device_net(net)
@@ -806,7 +866,7 @@ def train_loop(learner: Learner, engine, ring, iterations: int, train_steps: int
     for it in range(iterations):
         ring.save_games_from_buffers(engine.play_stream(games_per_iteration, seed + it ** 3, temp(it)))
         for _ in range(train_steps):
-            losses = learner.train_step(ring.sample_batch())
+            losses = learner.train_step_from(ring)
         learner.push_to(engine.net)
         history.append({k: float(v) for k, v in losses.items()})
     return history

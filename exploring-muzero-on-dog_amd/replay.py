@@ -190,12 +190,67 @@ class VectorizedReplayBuffer:
         t_t = np.maximum(len_t - 1 - term_k, 0)
         return np.concatenate([ep_n, ep_t]).astype(np.int32), np.concatenate([t_n, t_t]).astype(np.int32)
 
-    def sample_at(self, ep_indices, t_starts) -> dict:
-        """The deterministic part of sample_batch (vec_replay_buffer.py:101-264), on device."""
+    def sample_at(self, ep_indices, t_starts, out: dict | None = None) -> dict:
+        """The deterministic part of sample_batch (vec_replay_buffer.py:101-264), on device.  `out`: the
+        batch tensors to fill (same keys, shapes and dtypes as a returned batch, contiguous, on the ring's
+        device) -- a learner's static graph inputs, so no copy follows."""
         B = len(ep_indices)
         K = self.unroll_steps + 1
         C, A = self.obs_shape[0], self.action_dim
         z = dict(device=self.device)
+        if out is not None:
+            ref = self._batch_spec(B, K, C, A)
+            for k, (shape, dt) in ref.items():
+                t = out.get(k)
+                if t is None or tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous() \
+                        or t.device.type != self.device.type or \
+                        (self.device.index is not None and t.device.index != self.device.index):
+                    raise ValueError(f"sample_at(out=): '{k}' must be a contiguous {dt} {shape} tensor on {self.device}")
+        else:
+            out = self._new_batch(B, K, C, A, z)
+        s = _L.MuzSample()
+        for k in self._batch_spec(B, K, C, A):
+            setattr(s, k, out[k].data_ptr())
+        ep, ts = self._stage_indices(ep_indices, t_starts)
+        _L.check(_L.load().muz_ring_sample(self.ring(), _L.ptr(ep), _L.ptr(ts), B, self.unroll_steps, self.td_steps,
+                                           int(self.bootstrap_value_target), _L.ptr(self.gamma_pow), s,
+                                           _L.stream_ptr()), "muz_ring_sample")
+        return out
+
+    def _batch_spec(self, B, K, C, A) -> dict:
+        spec = getattr(self, "_spec", None)
+        if spec is None or spec[0] != B:
+            spec = self._spec = (B, {k: (tuple(v.shape), v.dtype)
+                                     for k, v in self._new_batch(B, K, C, A, dict(device="meta")).items()})
+        return spec[1]
+
+    def _stage_indices(self, ep_indices, t_starts):
+        """Episode / start indices to the device through a pinned double buffer (an async copy; a pageable
+        source would make the copy wait for the stream to drain, serialising the host's next index draw with
+        the previous learner step).  Slot k is reused only after its copy from two calls ago completed."""
+        B = len(ep_indices)
+        if self.device.type != "cuda":
+            return (torch.as_tensor(np.asarray(ep_indices, np.int32)).to(self.device),
+                    torch.as_tensor(np.asarray(t_starts, np.int32)).to(self.device))
+        st = getattr(self, "_idx_stage", None)
+        if st is None or st["host"].shape[1] != 2 * B:
+            st = self._idx_stage = {"host": torch.empty((2, 2 * B), dtype=torch.int32, pin_memory=True),
+                                    "dev": torch.empty((2, 2 * B), dtype=torch.int32, device=self.device),
+                                    "ev": [None, None], "k": 0}
+        k = st["k"]
+        st["k"] ^= 1
+        if st["ev"][k] is not None:
+            st["ev"][k].synchronize()
+        h = st["host"][k].numpy()
+        h[:B] = np.asarray(ep_indices, np.int32)
+        h[B:] = np.asarray(t_starts, np.int32)
+        d = st["dev"][k]
+        d.copy_(st["host"][k], non_blocking=True)
+        ev = st["ev"][k] = torch.cuda.Event()
+        ev.record()
+        return d[:B], d[B:]
+
+    def _new_batch(self, B, K, C, A, z) -> dict:
         out = {
             "observations": torch.empty((B, C, CELLS), dtype=torch.float32, **z),
             "actions": torch.empty((B, K - 1), dtype=torch.int32, **z),
@@ -207,14 +262,6 @@ class VectorizedReplayBuffer:
             "discount_targets": torch.empty((B, K - 1), dtype=torch.int32, **z),
         }
         out.update(self._extra_outputs(B, K, z))
-        s = _L.MuzSample()
-        for k in out:
-            setattr(s, k, out[k].data_ptr())
-        ep = torch.as_tensor(np.asarray(ep_indices, np.int32)).to(self.device)
-        ts = torch.as_tensor(np.asarray(t_starts, np.int32)).to(self.device)
-        _L.check(_L.load().muz_ring_sample(self.ring(), _L.ptr(ep), _L.ptr(ts), B, self.unroll_steps, self.td_steps,
-                                           int(self.bootstrap_value_target), _L.ptr(self.gamma_pow), s,
-                                           _L.stream_ptr()), "muz_ring_sample")
         return out
 
     def sample_batch(self) -> dict:

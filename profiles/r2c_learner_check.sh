@@ -8,3 +8,5 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 
 tail -3 $O/tests.log
 timeout -k 10 200 python3 profiles/learner_profile.py 100 > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
 grep "ms$" $O/profile.log
+timeout -k 10 400 python bench.py --workload train --steps 1 --warmup 1 > $O/train.json 2> $O/train.err || { tail -20 $O/train.err; exit 1; }
+cat $O/train.json

@@ -322,3 +322,27 @@ def test_im2col_matches_pad_and_cat(cuda, K, Cin):
     (dref,) = torch.autograd.grad(ref, x, dc)
     assert torch.equal(cols, ref)
     assert torch.allclose(dx, dref, rtol=1e-6, atol=1e-6)
+
+
+def test_train_step_from_ring_equals_sampled_batches(cuda):
+    """Learner.train_step_from(ring) (the ring writes each batch into the captured graph's inputs through the
+    pinned index stage) gives the same losses and parameters as train_step(ring.sample_batch()) on an
+    identically seeded ring."""
+    E, GA, L, N, R = _mods()
+    C = E.num_channels(2)
+    params = ON.init_params(C, seed=11)
+    net = N.DeviceNet(params, C)
+    eng = GA.SelfPlayEngine(net, 32, num_players=2, max_steps=80, num_simulations=4, max_depth=4)
+    buf = eng.play(seed=5)
+    rings = [R.VectorizedReplayBuffer(64, 32, 5, 10, obs_shape=(C, 56), max_episode_length=80,
+                                      rng=np.random.RandomState(7)) for _ in range(2)]
+    for r in rings:
+        r.save_games_from_buffers(buf)
+    a = L.Learner(params, C, unroll_steps=5, graph=True)
+    b = L.Learner(params, C, unroll_steps=5, graph=True)
+    for i in range(5):
+        la = a.train_step(rings[0].sample_batch())
+        lb = b.train_step_from(rings[1])
+        assert torch.equal(la["total_loss"], lb["total_loss"]), i
+    for k in a.nets.p:
+        assert torch.equal(a.nets.p[k], b.nets.p[k]), k
