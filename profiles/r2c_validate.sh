@@ -1,7 +1,7 @@
 #!/bin/bash
 # Re-entry check of HEAD on a fresh box: full GPU suite, smoke(), headline bench.
 set -o pipefail
-O=gpurun_out/r2c
+O=gpurun_out/${R2C_OUT:-r2c}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
