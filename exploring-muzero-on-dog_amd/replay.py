@@ -215,6 +215,11 @@ class VectorizedReplayBuffer:
         _L.check(_L.load().muz_ring_sample(self.ring(), _L.ptr(ep), _L.ptr(ts), B, self.unroll_steps, self.td_steps,
                                            int(self.bootstrap_value_target), _L.ptr(self.gamma_pow), s,
                                            _L.stream_ptr()), "muz_ring_sample")
+        st = getattr(self, "_idx_stage", None)
+        if st is not None and self.device.type == "cuda":
+            # the slot is free again once this sample has read it (covers the pinned source and the device copy)
+            ev = st["ev"][st["k"] ^ 1] = torch.cuda.Event()
+            ev.record()
         return out
 
     def _batch_spec(self, B, K, C, A) -> dict:
@@ -227,7 +232,8 @@ class VectorizedReplayBuffer:
     def _stage_indices(self, ep_indices, t_starts):
         """Episode / start indices to the device through a pinned double buffer (an async copy; a pageable
         source would make the copy wait for the stream to drain, serialising the host's next index draw with
-        the previous learner step).  Slot k is reused only after its copy from two calls ago completed."""
+        the previous learner step).  Slot k is reused only after the sample that read it two calls ago completed
+        (the event sample_at records after its launch)."""
         B = len(ep_indices)
         if self.device.type != "cuda":
             return (torch.as_tensor(np.asarray(ep_indices, np.int32)).to(self.device),
@@ -246,8 +252,6 @@ class VectorizedReplayBuffer:
         h[B:] = np.asarray(t_starts, np.int32)
         d = st["dev"][k]
         d.copy_(st["host"][k], non_blocking=True)
-        ev = st["ev"][k] = torch.cuda.Event()
-        ev.record()
         return d[:B], d[B:]
 
     def _new_batch(self, B, K, C, A, z) -> dict:
