@@ -123,9 +123,32 @@ def launch_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+    # poll every child: the first one that fails ends the job (the others would wait forever in the
+    # process-group rendezvous or an RCCL collective), and MUZ_BENCH_TIMEOUT (seconds) bounds the whole job
+    import time
+    limit = float(os.environ.get("MUZ_BENCH_TIMEOUT", "0") or 0)
+    t0, code = time.monotonic(), 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad or all(c == 0 for c in codes):
+            code = bad[0] if bad else 0
+            break
+        if limit and time.monotonic() - t0 > limit:
+            print(f"bench.py: ranks still running after {limit:.0f} s, terminating", file=sys.stderr)
+            code = 124
+            break
+        time.sleep(0.2)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return code
 
 
 def dist_env():

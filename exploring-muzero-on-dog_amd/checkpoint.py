@@ -50,6 +50,9 @@ def load_flax_msgpack(src) -> dict:
     return msgpack.unpackb(data, ext_hook=_ext_hook, raw=False, strict_map_key=False)
 
 
+loads_flax_msgpack = load_flax_msgpack
+
+
 def dumps_flax_msgpack(tree: dict) -> bytes:
     """flax.serialization.msgpack_serialize of a nested dict of arrays."""
     return msgpack.packb(tree, default=_default, strict_types=True)
@@ -89,6 +92,16 @@ def muzero_tree_to_flat(tree: dict) -> dict:
         sub = tree[net]["params"] if "params" in tree[net] else tree[net]
         for k, v in flatten(sub, net).items():
             flat[k] = np.asarray(v, np.float32)
+    return flat
+
+
+def muzero_tree_to_flat_any(tree: dict) -> dict:
+    """muzero_tree_to_flat keeping the leaves as they are (torch tensors, e.g. a learner's live parameters,
+    stay torch tensors)."""
+    flat = {}
+    for net in NETS:
+        sub = tree[net]["params"] if "params" in tree[net] else tree[net]
+        flat.update(flatten(sub, net))
     return flat
 
 

@@ -156,9 +156,13 @@ __global__ __launch_bounds__(256) void k_ln_colsum(const float* __restrict__ par
 
 // Min-max latent scaling at the end of a dynamics trunk (muzero_deterministic_madn.py:449-457,
 // muzero_classic_madn.py:365-371): q = x + (y + bias), out = (q - min q) / (max q - min q + 1e-8) per row
-// (one wave per row; ties go to the lowest column, as torch's min / max).  Saved: q, (lo, hi), their columns.
-// Backward, with the incoming gradient d = (g + (a + b)) * scale (a, b: optional extra terms):
-//   dq = d / den;  dq[argmin] += -sum(d) / den + t;  dq[argmax] += -t,  t = sum(d (q - lo)) / den^2.
+// (one wave per row).  Saved: q, (lo, hi) and the first column of each extremum.
+// Backward, with the incoming gradient d = (g + (a + b)) * scale + h (a, b: the carried gradient of the next
+// application; h: a gradient that bypasses the 0.5 latent scaling, e.g. the det reward / discount heads which
+// read the unscaled next latent, train_with_reward.py:49-105):
+//   dq = d / den;  dq[c] += (-sum(d) / den + t) / n_lo for every c with q[c] == lo;  dq[c] += -t / n_hi for
+//   every c with q[c] == hi,  t = sum(d (q - lo)) / den^2 -- the extremum's gradient split evenly over tied
+//   columns, as JAX's reduce_min / reduce_max JVP does (jnp.min / jnp.max in the Flax modules).
 __device__ __forceinline__ void wave_argext(float& v, int& i, bool is_max) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -202,9 +206,9 @@ __global__ __launch_bounds__(256) void k_minmax_fwd(const float* __restrict__ x,
 
 template <int N>
 __global__ __launch_bounds__(256) void k_minmax_bwd(const float* __restrict__ g, const float* __restrict__ a,
-                                                    const float* __restrict__ b, float scale, int scaled,
-                                                    const float* __restrict__ q, const float* __restrict__ lohi,
-                                                    const int* __restrict__ idx, int M, float* __restrict__ dq) {
+                                                    const float* __restrict__ b, const float* __restrict__ h,
+                                                    float scale, int scaled, const float* __restrict__ q,
+                                                    const float* __restrict__ lohi, int M, float* __restrict__ dq) {
   constexpr int E = N / 64;
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -212,27 +216,31 @@ __global__ __launch_bounds__(256) void k_minmax_bwd(const float* __restrict__ g,
   const size_t row = (size_t)m * N;
   const float lo = lohi[2 * m], hi = lohi[2 * m + 1];
   const float den = (hi - lo) + 1e-8f;
-  float d[E], sd = 0.f, st = 0.f;
+  float d[E], qv[E], sd = 0.f, st = 0.f;
+  int nlo = 0, nhi = 0;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const size_t k = row + lane + 64 * e;
     float t = g[k];
     if (a) t = t + (a[k] + b[k]);
     if (scaled) t = t * scale;
+    if (h) t = t + h[k];
     d[e] = t;
+    qv[e] = q[k];
     sd += t;
-    st += t * (q[k] - lo);
+    st += t * (qv[e] - lo);
+    nlo += __popcll(__ballot(qv[e] == lo));
+    nhi += __popcll(__ballot(qv[e] == hi));
   }
   sd = wave_sum(sd);
   st = wave_sum(st) / (den * den);
-  const int ilo = idx[2 * m], ihi = idx[2 * m + 1];
+  const float glo = (-sd / den + st) / (float)nlo, ghi = (-st) / (float)nhi;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const int c = lane + 64 * e;
     float r = d[e] / den;
-    if (c == ilo) r = r + (-sd / den + st);
-    if (c == ihi) r = r + (-st);
-    dq[row + c] = r;
+    if (qv[e] == lo) r = r + glo;
+    if (qv[e] == hi) r = r + ghi;
+    dq[row + lane + 64 * e] = r;
   }
 }
 
@@ -347,12 +355,12 @@ int muz_minmax_fwd(const float* x, const float* y, const float* bias, int32_t M,
   return muz_last_launch_error();
 }
 
-int muz_minmax_bwd(const float* g, const float* a, const float* b, float scale, int32_t scaled, const float* q,
-                   const float* lohi, const int32_t* idx, int32_t M, int32_t N, float* dq, void* stream) {
+int muz_minmax_bwd(const float* g, const float* a, const float* b, const float* h, float scale, int32_t scaled,
+                   const float* q, const float* lohi, int32_t M, int32_t N, float* dq, void* stream) {
   if (N != 256) return MUZ_E_UNSUPPORTED;
-  MUZ_HOST_CHECK(M >= 0 && g && q && lohi && idx && dq && (a == nullptr) == (b == nullptr));
+  MUZ_HOST_CHECK(M >= 0 && g && q && lohi && dq && (a == nullptr) == (b == nullptr));
   if (M == 0) return MUZ_OK;
-  k_minmax_bwd<256><<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(g, a, b, scale, scaled, q, lohi, idx, M, dq);
+  k_minmax_bwd<256><<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(g, a, b, h, scale, scaled, q, lohi, M, dq);
   return muz_last_launch_error();
 }
 

@@ -20,31 +20,30 @@ class TurnLedger {
 
   TurnLedger(hipStream_t s, bool timing) : s_(s), timing_(timing) {}
   ~TurnLedger() {
-    if (!ok_) return;
     for (int i = 0; i < kRing; ++i) {
-      (void)hipEventDestroy(ev_[i]);
-      if (timing_) {
-        (void)hipEventDestroy(tev_[i][0]);
-        (void)hipEventDestroy(tev_[i][1]);
-      }
+      if (ev_[i]) (void)hipEventDestroy(ev_[i]);
+      if (tev_[i][0]) (void)hipEventDestroy(tev_[i][0]);
+      if (tev_[i][1]) (void)hipEventDestroy(tev_[i][1]);
     }
-    (void)hipEventDestroy(t0_);
-    (void)hipEventDestroy(t1_);
-    (void)hipHostFree(host_);
+    if (t0_) (void)hipEventDestroy(t0_);
+    if (t1_) (void)hipEventDestroy(t1_);
+    if (host_) (void)hipHostFree(host_);
   }
   int begin() {
     hipError_t e = hipHostMalloc((void**)&host_, (size_t)kRing * 2 * sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) return (int)e;
+    // every create is checked; on a failure the events made so far (and the pinned ring) are released by the
+    // destructor, which only touches handles that were created (nullptr-initialised members)
     for (int i = 0; i < kRing; ++i) {
-      (void)hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming);
+      if ((e = hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming)) != hipSuccess) return (int)e;
       if (timing_) {
-        (void)hipEventCreate(&tev_[i][0]);
-        (void)hipEventCreate(&tev_[i][1]);
+        if ((e = hipEventCreate(&tev_[i][0])) != hipSuccess) return (int)e;
+        if ((e = hipEventCreate(&tev_[i][1])) != hipSuccess) return (int)e;
       }
     }
-    (void)hipEventCreate(&t0_);
-    (void)hipEventCreate(&t1_);
-    (void)hipEventRecord(t0_, s_);
+    if ((e = hipEventCreate(&t0_)) != hipSuccess) return (int)e;
+    if ((e = hipEventCreate(&t1_)) != hipSuccess) return (int)e;
+    if ((e = hipEventRecord(t0_, s_)) != hipSuccess) return (int)e;
     ok_ = true;
     return MUZ_OK;
   }
@@ -106,7 +105,7 @@ class TurnLedger {
   hipStream_t s_;
   bool timing_, ok_ = false, stopped_ = false;
   int32_t* host_ = nullptr;
-  hipEvent_t ev_[kRing], tev_[kRing][2], t0_, t1_;
+  hipEvent_t ev_[kRing] = {}, tev_[kRing][2] = {}, t0_ = nullptr, t1_ = nullptr;
   int retired_ = 0, timed_ = 0, active_ = 0;
   long long searches_ = 0;
   double search_ms_ = 0.0;

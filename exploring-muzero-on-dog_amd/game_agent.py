@@ -110,6 +110,24 @@ class SelfPlayEngine:
         return self._sbuf
 
 
+_ENGINE_CACHE = {}
+
+
+def cached_engine(net: N.DeviceNet, num_envs, num_players, max_steps, num_simulation, max_depth, rules) -> SelfPlayEngine:
+    """The engine of the last reference-signature call, reused when the call's shape, rules and weight set are
+    the same: a test_training-style loop calls play_n_games_v3 once per iteration, and a fresh engine would
+    reallocate its state, workspace and [num_envs, max_steps] buffers (GBs at config (e)) every time.  One live
+    engine per process (the reference's loops play one configuration at a time)."""
+    key = (id(net), int(num_envs), int(num_players), int(max_steps), int(num_simulation), int(max_depth),
+           tuple(sorted((dict(RULES if rules is None else rules)).items())))
+    hit = _ENGINE_CACHE.get(key)
+    if hit is not None and hit.net is net:
+        return hit
+    _ENGINE_CACHE.clear()
+    eng = _ENGINE_CACHE[key] = SelfPlayEngine(net, num_envs, num_players, max_steps, num_simulation, max_depth, rules)
+    return eng
+
+
 REFERENCE_DTYPES = {"obs": torch.float32, "act": torch.int32, "rew": torch.int32, "val": torch.float32,
                     "pol": torch.float32, "mask": torch.float32, "player": torch.int32, "team": torch.int32,
                     "discount": torch.int32, "idx": torch.int32}
@@ -129,6 +147,6 @@ def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_
     if (C - 2) % 8 or int(input_shape[-1]) != E.CELLS:
         raise ValueError(f"input_shape {tuple(input_shape)} is not (8P + 2, 56)")
     net = N.as_device_net(params, C)
-    eng = SelfPlayEngine(net, num_envs, (C - 2) // 8, max_steps, num_simulation, max_depth, rules)
+    eng = cached_engine(net, num_envs, (C - 2) // 8, max_steps, num_simulation, max_depth, rules)
     buf = eng.play(N.rng_key_to_seed(rng_key), temp)
     return {k: v.to(REFERENCE_DTYPES[k] if k != "obs" else obs_dtype) for k, v in buf.items()}

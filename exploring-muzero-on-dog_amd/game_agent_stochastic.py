@@ -103,6 +103,9 @@ class StochasticSelfPlayEngine:
         return self._sbuf
 
 
+_ENGINE_CACHE = {}
+
+
 def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_depth, max_steps, temp,
                     obs_dtype=torch.float32) -> dict:
     """play_n_games_v3 (MuZero_Classic_MADN/game_agent_stochastic.py:220-244), reference signature: Flax
@@ -115,8 +118,14 @@ def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_
     if (C - 3) % 2 or int(input_shape[-1]) != E.CELLS:
         raise ValueError(f"input_shape {tuple(input_shape)} is not (2P + 3, 56)")
     net = ST.as_device_classic_net(params, C)
-    eng = StochasticSelfPlayEngine(net, num_envs, num_players=(C - 3) // 2, max_steps=max_steps,
-                                   num_simulations=num_simulation, max_depth=max_depth)
+    key = (id(net), int(num_envs), (C - 3) // 2, int(max_steps), int(num_simulation), int(max_depth))
+    hit = _ENGINE_CACHE.get(key)
+    if hit is None or hit.net is not net:          # one live engine, reused by a test_training-style loop
+        _ENGINE_CACHE.clear()
+        hit = _ENGINE_CACHE[key] = StochasticSelfPlayEngine(net, num_envs, num_players=(C - 3) // 2,
+                                                            max_steps=max_steps, num_simulations=num_simulation,
+                                                            max_depth=max_depth)
+    eng = hit
     buf = eng.play(rng_key_to_seed(rng_key), temp)
     dt = dict(REFERENCE_DTYPES, obs=obs_dtype, dice=torch.int32, dice_dist=torch.float32)
     return {k: v.to(dt[k]) for k, v in buf.items()}

@@ -208,16 +208,19 @@ class _TrunkChain(torch.autograd.Function):
     weights; the gradient reaching x_{i+1} is scaled by grad_scale where scaled[i].  det loss_fn: one group,
     apps = (0,) * K, all scaled (train_with_reward.py:98-107); classic loss_fn_stochastic: groups (act, chance),
     apps = (0, 1) * K, only the chance outputs (the new states) scaled (train_stochastic.py:95-121).
+    heads=True adds a second output with the same values whose gradient is NOT scaled: the det reward /
+    discount heads read the next latent inside dynamics_net, before the scaling (train_with_reward.py:49-105).
 
     Forward = the fused kernels of csrc/learner_ln.hip + library GEMMs; the hand-written backward walks the
     applications in reverse and, because a group's weights are shared by all its applications, forms each
     weight gradient with ONE GEMM and each LayerNorm / bias gradient with ONE column sum per group (per-step
-    autograd made K GEMMs, K column sums and K - 1 accumulation adds per parameter).  min / max follow torch's
-    backward (the gradient goes to the returned index).  Inputs: x_0 [B, 256], FiLM scale / shift [T, B, 256],
-    the groups' parameters concatenated, each in trunk_param_names order.  Output: x_1..x_T as [T, B, 256]."""
+    autograd made K GEMMs, K column sums and K - 1 accumulation adds per parameter).  min / max split their
+    gradient evenly over tied columns (JAX's reduce_min / reduce_max rule).  Inputs: x_0 [B, 256], FiLM scale / shift [T, B, 256],
+    the groups' parameters concatenated, each in trunk_param_names order.  Output: x_1..x_T as [T, B, 256]
+    (and its unscaled-gradient twin when heads)."""
 
     @staticmethod
-    def forward(ctx, latent0, scale, shift, grad_scale, apps, scaled, *P):
+    def forward(ctx, latent0, scale, shift, grad_scale, apps, scaled, heads, *P):
         T, B, Nn = scale.shape
         if len(apps) != T or len(scaled) != T or len(P) != _NP * (max(apps) + 1):
             raise ValueError("apps / scaled / parameters do not match the FiLM rows")
@@ -258,15 +261,16 @@ class _TrunkChain(torch.autograd.Function):
             lat = outs[i]
         ctx.st, ctx.X, ctx.P, ctx.grad_scale = st, X, P, float(grad_scale)
         ctx.apps, ctx.scaled = tuple(apps), tuple(scaled)
-        ctx.save_for_backward(scale1, qs, lohi, idx)
-        return outs
+        ctx.save_for_backward(scale1, qs, lohi)
+        return (outs, outs.clone()) if heads else outs
 
     @staticmethod
-    def backward(ctx, G):
-        scale1, qs, lohi, idx = ctx.saved_tensors
+    def backward(ctx, G, H=None):
+        scale1, qs, lohi = ctx.saved_tensors
         P, st, s, apps = ctx.P, ctx.st, ctx.grad_scale, ctx.apps
         T, B, Nn = scale1.shape
         G = G.contiguous()
+        H = None if H is None else H.contiguous()
         dev, dt = G.device, G.dtype
         lib = _L.load()
         nf = lib.muz_ln_bwd_scratch_floats(B, Nn)
@@ -284,9 +288,9 @@ class _TrunkChain(torch.autograd.Function):
             Q = P[_NP * g:_NP * (g + 1)]
             f0, x0, f3, f4, rbs, x5 = st[i]
             dq = DZ[(g, "5")][j]
-            _L.check(lib.muz_minmax_bwd(_L.ptr(G[i]), _L.ptr(ca), _L.ptr(cb), s, int(ctx.scaled[i]), _L.ptr(qs[i]),
-                                        _L.ptr(lohi[i]), _L.ptr(idx[i]), B, Nn, _L.ptr(dq), _L.stream_ptr()),
-                     "muz_minmax_bwd")
+            _L.check(lib.muz_minmax_bwd(_L.ptr(G[i]), _L.ptr(ca), _L.ptr(cb), _L.ptr(None if H is None else H[i]), s,
+                                        int(ctx.scaled[i]), _L.ptr(qs[i]), _L.ptr(lohi[i]), B, Nn, _L.ptr(dq),
+                                        _L.stream_ptr()), "muz_minmax_bwd")
             dx = dq @ Q[26].t()
             for r in (1, 0):
                 xin, fa, fb = rbs[r]
@@ -314,7 +318,7 @@ class _TrunkChain(torch.autograd.Function):
                 grads[o + ig], grads[o + ibe], grads[o + ib] = _ln_colsum(scr[(g, n)], Nn)
             Xs, Ds = (t[(g, "5")][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
             grads[o + 26], grads[o + 27] = Xs.t() @ Ds, torch.mv(Ds.t(), _ones(Ds.shape[0], Ds))
-        return (ca + cb, dscale, dshift, None, None, None, *grads)
+        return (ca + cb, dscale, dshift, None, None, None, None, *grads)
 
 
 class MuZeroNets:
@@ -382,8 +386,9 @@ class MuZeroNets:
 
     @staticmethod
     def _minmax(x):
-        lo = x.min(-1, keepdim=True).values
-        hi = x.max(-1, keepdim=True).values
+        # amin / amax: the gradient of a tied extremum is split evenly, as jnp.min / jnp.max do
+        lo = torch.amin(x, -1, keepdim=True)
+        hi = torch.amax(x, -1, keepdim=True)
         return (x - lo) / (hi - lo + 1e-8)
 
     # ---- networks ------------------------------------------------------------------------------------
@@ -465,16 +470,23 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     # (same per-row arithmetic as the step-by-step loop of the reference; far fewer kernel launches).
     oh, scale, shift = nets.dynamics_film(acts[:, :K].transpose(0, 1).reshape(-1))
     latents = [latent]
+    # The reward / discount heads read the next latent inside dynamics_net (muzero_deterministic_madn.py:
+    # 437-455), BEFORE the loss scales the gradient of the latent it carries on (line 105): the heads take
+    # the unscaled outputs.
     if K and latent.is_cuda and CHAIN:     # the whole latent chain as one autograd node (fused kernels, batched weight grads)
-        chain = _TrunkChain.apply(latent, scale.reshape(K, B, -1), shift.reshape(K, B, -1), grad_scale,
-                                  (0,) * K, (True,) * K, *(nets.p[n] for n in DYN_TRUNK_PARAMS))
+        chain, raw = _TrunkChain.apply(latent, scale.reshape(K, B, -1), shift.reshape(K, B, -1), grad_scale,
+                                       (0,) * K, (True,) * K, True, *(nets.p[n] for n in DYN_TRUNK_PARAMS))
         latents += list(chain.unbind(0))
+        head_in = raw.reshape(K * B, -1)
     else:
+        raws = []
         for k in range(K):
             nxt = nets.dynamics_trunk(latents[-1], scale[k * B:(k + 1) * B], shift[k * B:(k + 1) * B])
+            raws.append(nxt)
             latents.append((nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale)   # gradient scaling (fwd identity)
+        head_in = torch.cat(raws, 0) if K else None
     logits_all, v_all = nets.prediction(torch.cat(latents, 0))
-    rl_all, dl_all = nets.dynamics_heads(torch.cat(latents[1:], 0), oh) if K else (None, None)
+    rl_all, dl_all = nets.dynamics_heads(head_in, oh) if K else (None, None)
     # The per-step losses, all K (+1) steps at once ([K+1, B] views; row k = unroll step k).
     m = batch["masks"][:, :K + 1].transpose(0, 1).to(obs.dtype)
     v = v_all[:, 0].reshape(K + 1, B)
@@ -776,7 +788,7 @@ def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int =
         film = [torch.stack([nets._dense(f"{d}/{pre}_film_{w}", e).reshape(K, B, -1) for pre, e in
                              (("act", ea_all), ("chance", ec_all))], 1).reshape(2 * K, B, -1)
                 for w in ("scale", "shift")]                       # rows interleaved: act_0, chance_0, act_1, ...
-        chain = _TrunkChain.apply(latent, film[0], film[1], grad_scale, (0, 1) * K, (False, True) * K,
+        chain = _TrunkChain.apply(latent, film[0], film[1], grad_scale, (0, 1) * K, (False, True) * K, False,
                                   *(nets.p[n] for kind in ("act", "chance") for n in trunk_param_names(kind)))
         afters = list(chain[0::2].unbind(0))
         latents += list(chain[1::2].unbind(0))

@@ -287,7 +287,7 @@ SIGNATURES = {
     "muz_ln_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
                                   vp, vp, vp, vp]),
     "muz_minmax_fwd": (ctypes.c_int, [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
-    "muz_minmax_bwd": (ctypes.c_int, [vp, vp, vp, ctypes.c_float, ctypes.c_int32, vp, vp, vp, ctypes.c_int32,
+    "muz_minmax_bwd": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, ctypes.c_int32, vp, vp, ctypes.c_int32,
                                       ctypes.c_int32, vp, vp]),
     "muz_im2col_fwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),
     "muz_im2col_bwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),

@@ -283,15 +283,42 @@ def as_device_net(params, obs_channels: int | None = None, device="cuda") -> Dev
     count is read from the representation's Dense_1 kernel (C - 6 inputs) when not given."""
     if isinstance(params, DeviceNet):
         return params
+    fp = params_fingerprint(params)
     hit = _NET_CACHE.get(id(params))
-    if hit is not None and hit[0] is params and str(hit[1].buffer.device) == str(torch.device(device)):
+    if hit is not None and hit[0] is params and hit[2] == fp and str(hit[1].buffer.device) == str(torch.device(device)):
         return hit[1]
     from . import checkpoint as CK
-    flat = params if all(isinstance(k, str) and "/" in k for k in params) else CK.muzero_tree_to_flat(params)
+    flat = params if all(isinstance(k, str) and "/" in k for k in params) else CK.muzero_tree_to_flat_any(params)
     flat = {k: np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v, np.float32) for k, v in flat.items()}
     C = int(flat["representation/Dense_1/kernel"].shape[0]) + 6 if obs_channels is None else int(obs_channels)
     A = int(flat["prediction/Dense_2/kernel"].shape[1])
     net = DeviceNet(flat, C, A, device=device)
     _NET_CACHE.clear()          # one live weight set per process is what the reference's loops use
-    _NET_CACHE[id(params)] = (params, net)
+    _NET_CACHE[id(params)] = (params, net, fp)
     return net
+
+
+def params_fingerprint(params) -> tuple:
+    """Content fingerprint of a parameter tree, so an in-place update of the same dict / arrays between
+    calls invalidates as_device_net's cache: per NumPy leaf a CRC32 of its bytes (~10 ms for the 11 MB det
+    tree); the torch leaves (e.g. a learner's live parameters, which the fused AdamW kernel updates through
+    raw pointers, so torch's version counters do not move) by their L2 norms, all in one multi-tensor kernel
+    and one device-to-host copy."""
+    import zlib
+    out, tens = [], []
+
+    def walk(t, pre):
+        if isinstance(t, dict):
+            for k in sorted(t):
+                walk(t[k], f"{pre}/{k}")
+        elif isinstance(t, torch.Tensor):
+            out.append((pre, tuple(t.shape), t.data_ptr()))
+            tens.append(t.detach())
+        else:
+            a = np.ascontiguousarray(np.asarray(t))
+            out.append((pre, zlib.crc32(a.view(np.uint8).reshape(-1)), a.shape))
+    walk(params, "")
+    if tens:
+        norms = torch.stack([n.double() for n in torch._foreach_norm(tens)]).cpu().numpy()
+        out.append(("norms", norms.tobytes()))
+    return tuple(out)

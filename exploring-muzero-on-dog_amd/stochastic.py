@@ -206,16 +206,18 @@ def as_device_classic_net(params, obs_channels: int | None = None, device="cuda"
     flat dict, or a DeviceClassicNet) -> DeviceClassicNet, packed once per params object."""
     if isinstance(params, DeviceClassicNet):
         return params
+    from .nets import params_fingerprint
+    fp = params_fingerprint(params)          # an in-place update of the same tree re-packs (nets.as_device_net)
     hit = _NET_CACHE.get(id(params))
-    if hit is not None and hit[0] is params and str(hit[1].buffer.device) == str(torch.device(device)):
+    if hit is not None and hit[0] is params and hit[2] == fp and str(hit[1].buffer.device) == str(torch.device(device)):
         return hit[1]
     from . import checkpoint as CK
-    flat = params if all(isinstance(k, str) and "/" in k for k in params) else CK.muzero_tree_to_flat(params)
+    flat = params if all(isinstance(k, str) and "/" in k for k in params) else CK.muzero_tree_to_flat_any(params)
     flat = {k: np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v, np.float32) for k, v in flat.items()}
     C = int(flat["representation/Dense_1/kernel"].shape[0]) + 6 if obs_channels is None else int(obs_channels)
     net = DeviceClassicNet(flat, C, device=device)
     _NET_CACHE.clear()
-    _NET_CACHE[id(params)] = (params, net)
+    _NET_CACHE[id(params)] = (params, net, fp)
     return net
 
 

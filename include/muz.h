@@ -676,11 +676,14 @@ int muz_ln_bwd(const float* dout, const float* out, const float* z, const float*
                float* dgamma, float* dbeta, float* dbias, void* stream);
 /* Min-max latent scaling closing a dynamics trunk, N = 256: q = x + (y + bias), out = (q - min) /
  * (max - min + 1e-8) per row; saves q [M][N], lohi [M][2] (min, max) and idx [M][2] (their columns, lowest on
- * ties).  Backward: dq from d = (g + (a + b)) x (scale if scaled) (a, b both null or both given). */
+ * ties).  Backward: dq from d = (g + (a + b)) x (scale if scaled) + h (a, b both null or both given; h
+ * optional: a gradient that bypasses the latent scaling, e.g. the det reward / discount heads reading the
+ * unscaled next latent, train_with_reward.py:49-105); the extremum gradient is split evenly over tied columns
+ * (JAX's reduce_min / reduce_max rule). */
 int muz_minmax_fwd(const float* x, const float* y, const float* bias, int32_t M, int32_t N, float* out, float* q,
                    float* lohi, int32_t* idx, void* stream);
-int muz_minmax_bwd(const float* g, const float* a, const float* b, float scale, int32_t scaled, const float* q,
-                   const float* lohi, const int32_t* idx, int32_t M, int32_t N, float* dq, void* stream);
+int muz_minmax_bwd(const float* g, const float* a, const float* b, const float* h, float scale, int32_t scaled,
+                   const float* q, const float* lohi, int32_t M, int32_t N, float* dq, void* stream);
 /* 'SAME' Conv1D as a GEMM: the im2col matrix cols [B][W][K x Cin] of x [B][W][Cin] (zero outside each row;
  * tap d reads column w + d - (K - 1) / 2) and its backward dx = sum over taps (fixed order). */
 int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream);

@@ -293,7 +293,7 @@ def check_relative_order_preserved(old, new, board_size):
 
 # ------------------------------------------------------------------------------------ legality
 def val_swap(env):
-    """dog.py:317-348 -> bool[4, 56]."""
+    """dog.py:361-391 -> bool[4, 56]."""
     R = env.rules
     cp = sub_player(env)
     pins = env.pins[cp].astype(np.int64)
@@ -325,7 +325,7 @@ def _common(env, move_vec):
 
 
 def val_action_7(env, dist) -> bool:
-    """dog.py:350-481 -> scalar bool for one hot-7 distribution."""
+    """dog.py:393-481 -> scalar bool for one hot-7 distribution."""
     R = env.rules
     cp, cur, start, P, pos, moved, fitted = _common(env, dist)
     board = env.board
@@ -432,7 +432,7 @@ def val_action_normal_move(env, move):
 
 
 def val_neg_move(env, move):
-    """dog.py:568-614 -> bool[4]."""
+    """dog.py:568-615 -> bool[4]."""
     R = env.rules
     cp, cur, start, P, pos, moved, fitted = _common(env, np.full(4, move))
     board = env.board
@@ -449,7 +449,7 @@ def val_neg_move(env, move):
 
 
 def valid_step_actions(env):
-    """dog.py:617-691 -> bool[792] = [joker copies (396), real cards (396)]."""
+    """dog.py:618-691 -> bool[792] = [joker copies (396), real cards (396)]."""
     cp = sub_player(env)
     hand = env.hands[cp]
     have = hand > 0
@@ -483,7 +483,7 @@ def _finish(env, cp, board, pins, invalid):
 
 
 def step_swap(env, pin_idx, swap_pos):
-    """dog.py:754-787 -> (board, pins, reward, done)."""
+    """dog.py:755-788 -> (board, pins, reward, done)."""
     cp = sub_player(env)
     N = env.total_board_size
     invalid = not bool(val_swap(env)[int(np.clip(pin_idx, 0, 3)), int(np.clip(swap_pos, 0, N - 1))])
@@ -502,7 +502,7 @@ def step_swap(env, pin_idx, swap_pos):
 
 
 def step_normal_move(env, pin, move):
-    """dog.py:789-858."""
+    """dog.py:790-859."""
     R = env.rules
     cp = sub_player(env)
     pin, move = int(pin), int(move)
@@ -544,7 +544,7 @@ def _capture_move(env, cp, pin, new, invalid):
 
 
 def step_neg_move(env, pin, move):
-    """dog.py:860-910."""
+    """dog.py:861-911."""
     cp = sub_player(env)
     pin, move = int(pin), int(move)
     invalid = not bool(val_neg_move(env, move)[pin])
@@ -587,7 +587,7 @@ def check_moving_pins_hit(i, start, end, matrix):
 
 
 def step_hot_7(env, dist):
-    """dog.py:912-984."""
+    """dog.py:913-985."""
     R = env.rules
     cp = sub_player(env)
     dist = np.asarray(dist, np.int64)
@@ -620,7 +620,7 @@ def step_hot_7(env, dist):
 
 
 def map_action_to_move(env, action):
-    """dog.py:1133-1196 -> [is_joker, is_swap, d0, d1, d2, d3]."""
+    """dog.py:1134-1197 -> [is_joker, is_swap, d0, d1, d2, d3]."""
     size = play_action_size(env)
     half = size // 2
     is_joker = (action - half) < 0
@@ -656,7 +656,7 @@ def map_action_to_card(mapped) -> int:
 
 
 def map_move_to_action(env, mapped) -> int:
-    """dog.py:1198-1239."""
+    """dog.py:1199-1239."""
     size = play_action_size(env)
     half = size // 2
     pxb = 4 * env.total_board_size
@@ -685,7 +685,7 @@ def _next_with_cards(env, hands):
 
 
 def env_step_play_phase(env, action, shuffle_keys=None):
-    """dog.py:986-1062."""
+    """dog.py:987-1063."""
     cp = sub_player(env)
     mapped = map_action_to_move(env, action)
     card = map_action_to_card(mapped)
@@ -713,7 +713,7 @@ def env_step_play_phase(env, action, shuffle_keys=None):
 
 
 def env_step_swap_phase(env, card):
-    """dog.py:1077-1114 (no validity check in the reference)."""
+    """dog.py:1078-1116 (no validity check in the reference)."""
     hands = env.hands.copy()
     ci = _si(env.num_cards, card)
     if ci is not None:                       # out-of-range scatter is dropped
@@ -735,14 +735,14 @@ def env_step_swap_phase(env, card):
 
 
 def env_step(env, action, shuffle_keys=None):
-    """dog.py:1117-1131."""
+    """dog.py:1118-1132."""
     if env.phase == 1:
         return env_step_swap_phase(env, int(action) - play_action_size(env))
     return env_step_play_phase(env, int(action), shuffle_keys)
 
 
 def no_step(env, shuffle_keys=None):
-    """dog.py:713-752."""
+    """dog.py:714-753."""
     hands = env.hands.copy()
     hands[env.current_player] = 0
     nxt, tot = _next_with_cards(env, hands)

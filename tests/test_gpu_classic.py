@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from oracle import classic_madn as cm
-from tests.test_oracle_golden import CLASSIC_CASES, classic_env_from_case
+from tests.test_oracle_golden import CLASSIC_CASES, DICE_CASES, classic_env_from_case, dice_env_from_case
 
 pytestmark = pytest.mark.gpu
 
@@ -57,6 +57,19 @@ def assert_same(gpu, envs, what):
         ok = (np.array_equal(pins[b], e.pins) and np.array_equal(board[b], e.board) and cp[b] == e.current_player
               and bool(done[b]) == e.done and die[b] == e.die)
         assert ok, (what, b, pins[b].tolist(), e.pins.tolist(), int(cp[b]), e.current_player, int(die[b]), e.die)
+
+
+def test_classic_dice_probs_notebook_outputs(cuda):
+    """muz_classic_dice_probs on the 8 positions of MADN/jupyter_code/test_functions.ipynb cells 3-4 against the
+    reference's recorded is_soft_locked / dice_probabilities outputs (classic_madn.py:180-228)."""
+    C = _C()
+    for case in DICE_CASES:
+        env = dice_env_from_case(case)
+        gpu = to_gpu([env], rules_of(env))
+        probs, soft = C.dice_probabilities(gpu, with_soft_lock=True)
+        torch.cuda.synchronize()
+        assert bool(soft.cpu()[0]) == case["soft_locked"], case
+        assert np.allclose(probs.cpu().numpy()[0], case["dice_probabilities"], rtol=0, atol=5e-9), case
 
 
 def test_classic_golden_step_vectors(cuda):

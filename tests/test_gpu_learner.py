@@ -203,7 +203,9 @@ def test_fused_dense_layernorm_matches_float64_autograd(cuda, N, mode):
 def test_dynamics_chain_node_matches_per_step_autograd(cuda):
     """learner._TrunkChain (the K-step latent chain as one autograd node, batched weight gradients) against the
     per-step graph of the same layers (loss_fn's CPU-style loop run on the GPU): forward within 1e-5, gradients
-    of every input and parameter within 1e-5 relative (summation orders differ)."""
+    of every input and parameter within 1e-5 relative (summation orders differ).  Both outputs carry a
+    gradient: the scaled latent (carried on, read by Pred4) and its unscaled twin (read by the reward /
+    discount heads, train_with_reward.py:49-105)."""
     _, _, L, _, _ = _mods()
     C, B, K = 18, 64, 6
     nets = L.MuZeroNets(ON.init_params(C, seed=4, randomize_affine=True), C, 24, "cuda")
@@ -212,24 +214,59 @@ def test_dynamics_chain_node_matches_per_step_autograd(cuda):
     scale = (0.3 * torch.randn(K, B, 256, generator=g)).cuda().requires_grad_(True)
     shift = (0.3 * torch.randn(K, B, 256, generator=g)).cuda().requires_grad_(True)
     w = torch.randn(K, B, 256, generator=g).cuda()
+    wh = torch.randn(K, B, 256, generator=g).cuda()
     params = [nets.p[n] for n in L.DYN_TRUNK_PARAMS]
     inputs = [lat0, scale, shift] + params
 
-    out = L._TrunkChain.apply(lat0, scale, shift, 0.5, (0,) * K, (True,) * K, *params)
-    g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs)
-    lats = [lat0]
+    out, raw = L._TrunkChain.apply(lat0, scale, shift, 0.5, (0,) * K, (True,) * K, True, *params)
+    g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum() + (raw * wh).sum(), inputs)
+    lats, raws = [lat0], []
     for k in range(K):
         nxt = nets.dynamics_trunk(lats[-1], scale[k], shift[k])
+        raws.append(nxt)
         lats.append((nxt * 0.5).detach() + nxt * 0.5)
     ref = torch.stack(lats[1:])
-    g2 = torch.autograd.grad((ref * w).sum() + ref[-1].square().sum(), inputs)
+    g2 = torch.autograd.grad((ref * w).sum() + ref[-1].square().sum() + (torch.stack(raws) * wh).sum(), inputs)
     torch.cuda.synchronize()
     # (the per-step graph's first LayerNorm is torch's two-pass one, the node's the fused Flax fast-variance one)
     assert (out - ref).abs().max().item() < 1e-5, "forward differs"
+    assert torch.equal(out, raw)
     names = ["latent0", "scale", "shift"] + list(L.DYN_TRUNK_PARAMS)
     for n, a, b in zip(names, g1, g2):
         err = (a - b).abs().max().item() / max(1e-3, b.abs().max().item())
         assert err < 1e-5, f"{n}: relative gradient difference {err:.2e}"
+
+
+def test_minmax_kernel_splits_tied_gradients(cuda):
+    """muz_minmax_fwd / _bwd on rows with tied extrema (quantised values): the extremum gradient is split over
+    the tied columns (JAX's reduce_min / reduce_max rule), against float64 amin / amax autograd; with both the
+    scaled carried gradient and the unscaled head term."""
+    _, _, L, _, _ = _mods()
+    from exploring_muzero_on_dog_amd import lib as _L
+    g = torch.Generator().manual_seed(17)
+    M, Nn = 37, 256
+    x = torch.round(torch.randn(M, Nn, generator=g) * 2) / 4          # few distinct values: many ties
+    y = torch.zeros(M, Nn)
+    bias = torch.zeros(Nn)
+    G, A, Bc, H = (torch.randn(M, Nn, generator=g) for _ in range(4))
+    xd = x.double().requires_grad_(True)
+    lo, hi = torch.amin(xd, -1, keepdim=True), torch.amax(xd, -1, keepdim=True)
+    o = (xd - lo) / (hi - lo + 1e-8)
+    (want,) = torch.autograd.grad(o, xd, ((G + (A + Bc)) * 0.5 + H).double())
+    dev = [t.cuda().contiguous() for t in (x, y, bias, G, A, Bc, H)]
+    out, q = torch.empty(M, Nn, device="cuda"), torch.empty(M, Nn, device="cuda")
+    lohi = torch.empty(M, 2, device="cuda")
+    idx = torch.empty(M, 2, dtype=torch.int32, device="cuda")
+    dq = torch.empty(M, Nn, device="cuda")
+    lib = _L.load()
+    _L.check(lib.muz_minmax_fwd(_L.ptr(dev[0]), _L.ptr(dev[1]), _L.ptr(dev[2]), M, Nn, _L.ptr(out), _L.ptr(q),
+                                _L.ptr(lohi), _L.ptr(idx), _L.stream_ptr()), "fwd")
+    _L.check(lib.muz_minmax_bwd(_L.ptr(dev[3]), _L.ptr(dev[4]), _L.ptr(dev[5]), _L.ptr(dev[6]), 0.5, 1, _L.ptr(q),
+                                _L.ptr(lohi), M, Nn, _L.ptr(dq), _L.stream_ptr()), "bwd")
+    torch.cuda.synchronize()
+    assert (out.double().cpu() - o.detach()).abs().max().item() < 1e-6
+    err = (dq.double().cpu() - want).abs().max().item() / want.abs().max().item()
+    assert err < 1e-6, err
 
 
 def test_classic_chain_node_matches_per_step_autograd(cuda):
@@ -255,7 +292,7 @@ def test_classic_chain_node_matches_per_step_autograd(cuda):
 
     film = [torch.stack([nets._dense(f"dynamics/{pre}_film_{x}", e).reshape(K, B, -1)
                          for pre, e in (("act", ea), ("chance", ec))], 1).reshape(2 * K, B, -1) for x in ("scale", "shift")]
-    out = L._TrunkChain.apply(lat0, film[0], film[1], 0.5, (0, 1) * K, (False, True) * K,
+    out = L._TrunkChain.apply(lat0, film[0], film[1], 0.5, (0, 1) * K, (False, True) * K, False,
                               *(nets.p[n] for n in names[:2 * L._NP]))
     g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs)
     seq, lat = [], lat0

@@ -95,6 +95,26 @@ def test_oracle_classic_golden(case):
     assert np.array_equal(env2.pins, np.array(case["expected_valid"]))
 
 
+DICE_CASES = _load("classic_dice_notebook_cases.json")
+
+
+def dice_env_from_case(c):
+    """MADN/jupyter_code/test_functions.ipynb cells 3-4: env_reset(0, num_players=2, distance=10, <rules>), pins
+    set by hand, board = set_pins_on_board(board, pins)."""
+    pins = np.array(c["pins"], dtype=np.int8)
+    env = cm.env_reset(num_players=c["num_players"], distance=c["distance"], **c["rules"])
+    return env.replace(pins=pins, board=cm.set_pins_on_board(env.board, pins), current_player=c["current_player"])
+
+
+@pytest.mark.parametrize("case", DICE_CASES, ids=[f"{c['source'][-6:]}-{i}" for i, c in enumerate(DICE_CASES)])
+def test_oracle_classic_dice_notebook_outputs(case):
+    """The reference's recorded is_soft_locked / dice_probabilities outputs (classic_madn.py:180-228; printed
+    to 8 decimals in the notebook)."""
+    env = dice_env_from_case(case)
+    assert cm.is_soft_locked(env) == case["soft_locked"]
+    assert np.allclose(cm.dice_probabilities(env), case["dice_probabilities"], rtol=0, atol=5e-9)
+
+
 def test_oracle_classic_dice():
     env = cm.env_reset(num_players=4, **cm.SELFPLAY_RULES)
     # initial free pin on start, 3 at home: not soft-locked (a pin is on the track)
