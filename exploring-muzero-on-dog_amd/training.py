@@ -20,7 +20,6 @@ from __future__ import annotations
 import os
 import time
 
-import msgpack
 import numpy as np
 import torch
 
@@ -150,7 +149,7 @@ def load_checkpoint(params_path: str, opt_path: str | None, optimizer: Optimizer
     if opt_path is not None:
         with open(opt_path, "rb") as f:
             raw = CK.loads_flax_msgpack(f.read())
-        st.load_state_dict({"count": int(np.asarray(raw["count"])), "mu": CK.muzero_tree_to_flat(raw["mu"]),
+        st.load_state_dict({"count": int(np.asarray(raw["count"]).reshape(-1)[0]), "mu": CK.muzero_tree_to_flat(raw["mu"]),
                             "nu": CK.muzero_tree_to_flat(raw["nu"])})
     return st.tree, st
 

@@ -56,7 +56,7 @@ def test_det_test_training_tiny(cuda, tmp_path):
     pp, op = TW._checkpoint_names(cfg, 2)
     p2, st2 = T.load_checkpoint(pp, op, TW.make_optimizer(cfg))
     assert st2.count == 2 * 3
-    got = T.CK.muzero_tree_to_flat(p2)
+    got = {k: v.detach().cpu().numpy() for k, v in T.CK.muzero_tree_to_flat_any(p2).items()}
     assert set(got) == set(saved) and all(np.array_equal(got[k], saved[k]) for k in saved)
 
 
