@@ -79,6 +79,9 @@ def parse():
                     help="det: games per step streamed through the --batch lanes (default 32 x batch; 0 = one "
                          "batch of --batch games, the reference's play_n_games_v3 call)")
     ap.add_argument("--train-steps", type=int, default=2500, help="train workload: learner steps per iteration")
+    ap.add_argument("--overlap", action="store_true",
+                    help="train workload: actors play iteration i+1 while the learner trains iteration i "
+                         "(pipeline.run_overlapped; weights one iteration staler than the reference's loop)")
     ap.add_argument("--workload", choices=("det", "classic", "dog", "train", "env", "selftest"), default="det",
                     help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
     ap.add_argument("--records", action="store_true",
@@ -519,6 +522,83 @@ def run_classic(args):
         dist.destroy_process_group()
 
 
+def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, games, stats, C, is_actor, is_learner,
+                      learner_rank, empty_packed):
+    """--workload train --overlap: pipeline.OverlappedIterations with this process's roles.  1 GPU: self-play in
+    a worker thread on its own stream while the learner's graph replays on another; N ranks: actors play while
+    the learner trains, then gather_packed + an async weight broadcast.  Returns the timed region's seconds."""
+    import torch
+    from exploring_muzero_on_dog_amd import pipeline as PL
+    from exploring_muzero_on_dog_amd import transfer as TR
+    s_play = torch.cuda.Stream(device=device) if is_actor else None
+    s_learn = torch.cuda.Stream(device=device) if is_learner else None
+    steps = {"n": 2}
+
+    def play(g):
+        with torch.cuda.stream(s_play):
+            buf = eng.play_stream(games, seed=5000 + g + 7919 * rank, temperature=1.0, stream=s_play)
+            stats["env_steps"] += int(buf["idx"].sum().item())
+            if world > 1:
+                buf = TR.pack(buf)
+                s_play.synchronize()
+            return buf
+
+    def train(i):
+        with torch.cuda.stream(s_learn):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(steps["n"]):
+                learner.train_step_from(ring)
+            e1.record()
+            e1.synchronize()
+            stats["learner_ms"] += e0.elapsed_time(e1)
+            stats["train_steps"] += steps["n"]
+
+    def deliver(g, got):
+        if world == 1:
+            with torch.cuda.stream(s_learn):
+                ring.save_games_from_buffers(got)
+            return
+        packed = got if is_actor else empty_packed(C, device)
+        recv = TR.gather_packed(packed, C, 24, dst=learner_rank)
+        if is_learner:
+            with torch.cuda.stream(s_learn):
+                for r, p in enumerate(recv):
+                    if r != learner_rank:
+                        ring.save_packed(p)
+            s_learn.synchronize()
+
+    def publish(i):
+        if is_learner:
+            with torch.cuda.stream(s_learn):
+                learner.push_to(net)
+            s_learn.synchronize()
+        if world == 1:
+            return PL._Done()
+        return TR.broadcast_weights_async(net, src=learner_rank)
+
+    loop = PL.OverlappedIterations(is_actor=is_actor, is_learner=is_learner, play=play, train=train, deliver=deliver,
+                                   publish=publish, concurrent=(world == 1))
+    loop.prologue()                               # generation 0; then warm-up iterations at 2 learner steps
+    if is_learner:
+        # capture the learner's HIP graph before any iteration runs self-play in another thread (a capture
+        # must not see the other thread's synchronising HIP calls)
+        with torch.cuda.stream(s_learn):
+            learner.train_step_from(ring)
+        s_learn.synchronize()
+    for w in range(max(args.warmup, 1)):
+        loop.step()
+        beat(f"overlap warm-up {w + 1}")
+    stats.update(env_steps=0, train_steps=0, learner_ms=0.0)
+    steps["n"] = args.train_steps
+
+    def timed(k):
+        loop.step()
+        if k == args.steps - 1:
+            loop.finish()
+    return timed_region(dist, timed, args.steps)
+
+
 def run_train(args):
     """Config (e): the det-MADN training loop (train_with_reward.py:167-311) at its hyper-parameters --
     4 players, 1500 games per iteration (S=100, D=50, max_len 550), replay ring 20000 x 550, batch 128,
@@ -583,11 +663,15 @@ def run_train(args):
         z["row_offset"] = torch.empty((0,), dtype=torch.int64, device=dev)
         return z
 
-    for w in range(max(args.warmup, 1)):       # fills the ring and captures the learner's HIP graph
-        iteration(100 * w, 2)
-        beat(f"warm-up {w + 1}")
-    stats.update(env_steps=0, train_steps=0, learner_ms=0.0)
-    elapsed = timed_region(dist, lambda k: iteration(1000 + k, args.train_steps), args.steps)
+    if args.overlap:
+        elapsed = _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, games, stats, C,
+                                    is_actor, is_learner, learner_rank, _empty_packed)
+    else:
+        for w in range(max(args.warmup, 1)):       # fills the ring and captures the learner's HIP graph
+            iteration(100 * w, 2)
+            beat(f"warm-up {w + 1}")
+        stats.update(env_steps=0, train_steps=0, learner_ms=0.0)
+        elapsed = timed_region(dist, lambda k: iteration(1000 + k, args.train_steps), args.steps)
     (env_steps, train_steps, learner_ms), elapsed = sum_max(
         dist, device, [stats["env_steps"], stats["train_steps"], stats["learner_ms"]], elapsed)
     if rank != 0:
@@ -602,8 +686,12 @@ def run_train(args):
         "data": "synthetic (self-generated games, seeded random fp32 weights)",
         "config": {"workload": f"train_with_reward.py config: {GAMES} games/iter (S={S}, D={D}, max_len {T}), "
                                f"ring 20000, batch 128, unroll 10, td 50, {args.train_steps} learner steps/iter",
-                   "parallelism": "1 GPU (actor + learner)" if world == 1 else
-                   f"{world - 1} actor ranks + 1 learner rank (packed-trajectory gather, weight broadcast)"},
+                   "parallelism": ("1 GPU (actor + learner)" if world == 1 else
+                                   f"{world - 1} actor ranks + 1 learner rank (packed-trajectory gather, weight "
+                                   f"broadcast)"),
+                   "schedule": ("overlapped: iteration i+1's self-play runs while iteration i trains; games played "
+                                "with weights one iteration staler than the reference's sequential loop"
+                                if args.overlap else "sequential, as train_with_reward.py:244-292")},
         "env_steps_per_s": round(env_steps / elapsed, 1), "train_steps_per_s": round(train_steps / elapsed, 2),
     }
     if train_steps:

@@ -129,3 +129,26 @@ def broadcast_weights(net, src: int = 0, group=None):
     dist.broadcast(net.buffer, src=src, group=group)
     if hasattr(net, "prepare"):
         net.prepare()
+
+
+class _WeightUpdate:
+    """Handle of an asynchronous weight broadcast: wait() completes it and, on a receiving rank, rebuilds the
+    derived FiLM tables (net.prepare) so the next self-play launch sees the new weights."""
+
+    def __init__(self, work, net, receiver):
+        self.work, self.net, self.receiver = work, net, receiver
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+            if self.receiver and hasattr(self.net, "prepare"):
+                self.net.prepare()
+
+
+def broadcast_weights_async(net, src: int = 0, group=None) -> _WeightUpdate:
+    """broadcast_weights with ``async_op=True`` (pipeline.run_overlapped): the learner goes on training while
+    the arena travels; an actor calls wait() before its next self-play call.  The source must not repack its
+    arena before its own handle's wait()."""
+    work = dist.broadcast(net.buffer, src=src, group=group, async_op=True)
+    return _WeightUpdate(work, net, dist.get_rank(group) != src)
