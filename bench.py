@@ -435,28 +435,31 @@ def run_dog(args):
         dist.destroy_process_group()
 
 
-def classic_cpu_baseline(seconds, sims, depth):
-    """The NumPy restatement of classic Stochastic MuZero self-play (oracle/selfplay.py
-    play_batch_of_games_stochastic with oracle/classic_nets.py, "port"): 8 games for `seconds` on the host."""
-    from threadpoolctl import threadpool_limits
+def classic_cpu_baseline(seconds, sims, depth, max_steps, lanes=16):
+    """SURVEY §8(d)'s CPU timing for config (c): the C++ restatement of classic Stochastic MuZero self-play
+    (oracle/cpu_classic.cpp: classic-MADN env with the die thrown per turn, Repr2 / StochasticDynamicsNetwork4 /
+    Pred4 fp32, mctx stochastic_muzero_policy with Dirichlet root noise, OpenMP over game lanes; checked against
+    the NumPy oracle by tests/test_cpu_baseline_classic.py) on the host for `seconds`, at 1 thread and at all
+    cores (game_agent_stochastic.py:52-218, muzero_classic_madn.py:464-517)."""
     from oracle import classic_madn as cm
     from oracle import classic_nets as CN
-    from oracle import selfplay as OS
-    cores, _ = cpu_cores()
+    from oracle import cpu_selfplay as CS
     C = cm.num_channels(CLASSIC_PLAYERS)
-    params = CN.init_params(C, seed=0)
-    n = 8
-    envs = [cm.env_reset(num_players=CLASSIC_PLAYERS, **cm.SELFPLAY_RULES) for _ in range(n)]
-    t0 = time.perf_counter()
-    with threadpool_limits(limits=cores):
-        buf, turns = OS.play_batch_of_games_stochastic(
-            params, CN.root_inference, lambda p, a, e: CN.decision_recurrent(p, a, e),
-            lambda p, c, a: CN.chance_recurrent(p, c, a), envs, sims, depth, 10_000, TEMP, 0, time_budget=seconds)
-    dt = time.perf_counter() - t0
-    steps = int(buf["idx"].sum())
-    return {"value": round(steps / dt, 2), "unit": "env_steps/s", "cores": cores, "kind": "port",
-            "sample": f"NumPy oracle classic Stochastic MuZero self-play, {n} games x {turns} turns ({steps} env-steps, "
-                      f"S={sims}, D={depth}) in {dt:.1f}s, BLAS threads={cores}"}
+    net = CS.CpuClassicNet(CN.init_params(C, seed=0), C)
+    cores, aff = cpu_cores()
+    half = seconds / 2
+    one = net.bench(CLASSIC_PLAYERS, cm.SELFPLAY_RULES, lanes, sims, depth, max_steps, TEMP, 0, 1, half)
+    allc = net.bench(CLASSIC_PLAYERS, cm.SELFPLAY_RULES, lanes, sims, depth, max_steps, TEMP, 0, cores, half)
+    v1 = one["env_steps"] / one["elapsed"]
+    vn = allc["env_steps"] / allc["elapsed"]
+    return {"value": round(vn, 2), "unit": "env_steps/s", "cores": cores, "kind": "port",
+            "value_1core": round(v1, 2), "value_allcores": round(vn, 2), "cores_affinity": aff,
+            "sims_per_s_allcores": round(allc["searches"] * sims / allc["elapsed"], 1),
+            "sample": f"C++ restatement of the reference algorithm (oracle/cpu_classic.cpp, fp32 AVX2/FMA, OpenMP): "
+                      f"classic-MADN {CLASSIC_PLAYERS}p teams streamed Stochastic MuZero self-play (Dirichlet 0.25 / "
+                      f"0.3 root noise), {lanes} game lanes per thread, S={sims} D={depth}, {half:.0f} s at 1 thread "
+                      f"({one['env_steps']} env-steps) and {half:.0f} s at {cores} threads ({allc['env_steps']} "
+                      f"env-steps); affinity shows {aff} CPUs"}
 
 
 def run_classic(args):
@@ -516,7 +519,7 @@ def run_classic(args):
                        "avg_launch_ms": round(search_ms / max(1, turns), 4), "flop_per_sim": CLASSIC_FLOP_PER_SIM,
                        "traffic": None}
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = classic_cpu_baseline(min(args.cpu_seconds, 20.0), args.sims, args.depth)
+        out["cpu_baseline"] = classic_cpu_baseline(min(args.cpu_seconds, 20.0), args.sims, args.depth, args.max_steps)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

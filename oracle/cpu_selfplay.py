@@ -179,3 +179,172 @@ def encode(d: Det) -> np.ndarray:
 
 def pins(d: Det) -> np.ndarray:
     return np.array(d.pins[:d.num_players * 4], np.int8).reshape(d.num_players, 4)
+
+
+# ---- classic MADN: Stochastic MuZero (oracle/cpu_classic.cpp) ---------------------------------------------
+R_DICE_RETHROW = 1 << 9
+
+
+class Classic(ctypes.Structure):
+    _fields_ = [("board", ctypes.c_int8 * 56), ("pins", ctypes.c_int8 * 16), ("start", ctypes.c_int8 * 4),
+                ("target", ctypes.c_int8 * 4), ("goal", ctypes.c_int8 * 16), ("current_player", ctypes.c_int32),
+                ("reward", ctypes.c_int32), ("done", ctypes.c_int32), ("num_players", ctypes.c_int32),
+                ("board_size", ctypes.c_int32), ("total", ctypes.c_int32), ("rules", ctypes.c_int32),
+                ("die", ctypes.c_int32)]
+
+
+class CTraj(ctypes.Structure):
+    _fields_ = [("act", ctypes.c_void_p), ("val", ctypes.c_void_p), ("pol", ctypes.c_void_p),
+                ("mask", ctypes.c_void_p), ("dice", ctypes.c_void_p), ("idx", ctypes.c_void_p)]
+
+
+_classic_bound = False
+
+
+def _classic_lib():
+    global _classic_bound
+    L = load()
+    if not _classic_bound:
+        vp, ip, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.muzcpu_classic_net_create.restype = vp
+        L.muzcpu_classic_net_create.argtypes = [vp, vp, vp, ip, ip]
+        L.muzcpu_classic_net_destroy.argtypes = [vp]
+        L.muzcpu_classic_reset.argtypes = [vp, ip, vp, ip, ip, ip]
+        L.muzcpu_classic_valid_action.argtypes = [vp, vp]
+        L.muzcpu_classic_step.argtypes = [vp, ip, vp, vp]
+        L.muzcpu_classic_no_step.argtypes = [vp]
+        L.muzcpu_classic_encode.argtypes = [vp, vp]
+        L.muzcpu_classic_soft_locked.argtypes = [vp]
+        L.muzcpu_classic_soft_locked.restype = ip
+        L.muzcpu_classic_dice_probs.argtypes = [vp, vp]
+        L.muzcpu_classic_throw_die.argtypes = [vp, fp]
+        L.muzcpu_classic_root.argtypes = [vp, vp, ip, vp, vp, vp]
+        L.muzcpu_classic_decision.argtypes = [vp, vp, vp, ip, vp, vp, vp, vp, vp]
+        L.muzcpu_classic_chance.argtypes = [vp, vp, vp, ip, vp, vp, vp]
+        L.muzcpu_classic_selfplay.restype = ip
+        L.muzcpu_classic_selfplay.argtypes = [vp, ip, ip, ip, ip, ip, ip, fp, ctypes.c_uint64, fp, vp]
+        L.muzcpu_classic_bench.restype = ctypes.c_int64
+        L.muzcpu_classic_bench.argtypes = [vp, ip, ip, ip, ip, ip, ip, fp, ctypes.c_uint64, fp, ip, ctypes.c_double,
+                                           vp, vp, vp]
+        _classic_bound = True
+    return L
+
+
+def classic_rule_bits(**rules) -> int:
+    from oracle import classic_madn as cm
+    r = dict(cm.DEFAULT_RULES)
+    r.update(rules)
+    bits = sum(bit for k, bit in _FLAGS.items() if r[k])
+    return bits | (R_DICE_RETHROW if r["enable_dice_rethrow"] else 0)
+
+
+def classic_from_oracle(e) -> Classic:
+    """oracle/classic_madn.State -> the C++ state struct."""
+    d = Classic()
+    P = e.num_players
+    d.board[:] = [int(x) for x in e.board]
+    pins = -np.ones(16, np.int8)
+    pins[:P * 4] = np.asarray(e.pins, np.int8).ravel()
+    d.pins[:] = [int(x) for x in pins]
+    st, tg, gl = np.zeros(4, np.int8), np.zeros(4, np.int8), np.zeros(16, np.int8)
+    st[:P], tg[:P], gl[:P * 4] = e.start, e.target, np.asarray(e.goal).ravel()
+    d.start[:], d.target[:], d.goal[:] = [int(x) for x in st], [int(x) for x in tg], [int(x) for x in gl]
+    d.current_player, d.reward, d.done, d.die = int(e.current_player), int(e.reward), int(e.done), int(e.die)
+    d.num_players, d.board_size, d.total = P, e.board_size, e.total_board_size
+    d.rules = classic_rule_bits(**e.rules)
+    return d
+
+
+def classic_valid_action(d: Classic) -> np.ndarray:
+    out = np.zeros(4, np.uint8)
+    _classic_lib().muzcpu_classic_valid_action(ctypes.byref(d), _p(out))
+    return out.astype(bool)
+
+
+def classic_step(d: Classic, pin):
+    r, dn = ctypes.c_int(), ctypes.c_int()
+    _classic_lib().muzcpu_classic_step(ctypes.byref(d), int(pin), ctypes.byref(r), ctypes.byref(dn))
+    return r.value, bool(dn.value)
+
+
+def classic_no_step(d: Classic):
+    _classic_lib().muzcpu_classic_no_step(ctypes.byref(d))
+
+
+def classic_encode(d: Classic) -> np.ndarray:
+    out = np.zeros((2 * d.num_players + 3, 56), np.float32)
+    _classic_lib().muzcpu_classic_encode(ctypes.byref(d), _p(out))
+    return out
+
+
+def classic_dice(d: Classic):
+    p = np.zeros(6, np.float32)
+    L = _classic_lib()
+    L.muzcpu_classic_dice_probs(ctypes.byref(d), _p(p))
+    return bool(L.muzcpu_classic_soft_locked(ctypes.byref(d))), p
+
+
+def classic_throw_die(d: Classic, u: float):
+    _classic_lib().muzcpu_classic_throw_die(ctypes.byref(d), float(u))
+
+
+class CpuClassicNet:
+    """Flat Flax-path classic parameter dict (Repr2 / StochasticDynamicsNetwork4 / Pred4, A = 4) -> C++ network."""
+
+    def __init__(self, params: dict, obs_channels: int):
+        L = _classic_lib()
+        self._keep = {k: np.ascontiguousarray(v, np.float32) for k, v in params.items()}
+        names = [k.encode() for k in self._keep]
+        n = len(names)
+        cn = (ctypes.c_char_p * n)(*names)
+        ptrs = (ctypes.c_void_p * n)(*[v.ctypes.data for v in self._keep.values()])
+        sizes = (ctypes.c_int64 * n)(*[v.size for v in self._keep.values()])
+        self.h = L.muzcpu_classic_net_create(cn, ptrs, sizes, n, obs_channels)
+        self.C = obs_channels
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.muzcpu_classic_net_destroy(self.h)
+            self.h = None
+
+    def root(self, obs):
+        obs = np.ascontiguousarray(obs, np.float32)
+        B = obs.shape[0]
+        lg, v, e = np.empty((B, 4), np.float32), np.empty(B, np.float32), np.empty((B, 256), np.float32)
+        _classic_lib().muzcpu_classic_root(self.h, _p(obs), B, _p(lg), _p(v), _p(e))
+        return lg, v, e
+
+    def decision(self, action, emb):
+        """-> (chance_logits, afterstate_value, afterstate, reward, discount) (oracle/classic_nets.decision_recurrent)."""
+        a = np.ascontiguousarray(action, np.int32)
+        emb = np.ascontiguousarray(emb, np.float32)
+        B = emb.shape[0]
+        cl, av, af = np.empty((B, 6), np.float32), np.empty(B, np.float32), np.empty((B, 256), np.float32)
+        r, d = np.empty(B, np.float32), np.empty(B, np.float32)
+        _classic_lib().muzcpu_classic_decision(self.h, _p(a), _p(emb), B, _p(cl), _p(av), _p(af), _p(r), _p(d))
+        return cl, av, af, r, d
+
+    def chance(self, outcome, after):
+        """-> (action_logits, value, next_state) (oracle/classic_nets.chance_recurrent)."""
+        c = np.ascontiguousarray(outcome, np.int32)
+        after = np.ascontiguousarray(after, np.float32)
+        B = after.shape[0]
+        lg, v, nx = np.empty((B, 4), np.float32), np.empty(B, np.float32), np.empty((B, 256), np.float32)
+        _classic_lib().muzcpu_classic_chance(self.h, _p(c), _p(after), B, _p(lg), _p(v), _p(nx))
+        return lg, v, nx
+
+    def selfplay(self, P, rules, n, S, D, T, temp, seed, dirichlet_fraction=0.0):
+        buf = {"act": np.zeros((n, T), np.int32), "val": np.zeros((n, T), np.float32),
+               "pol": np.zeros((n, T, 4), np.float32), "mask": np.zeros((n, T), np.float32),
+               "dice": np.zeros((n, T), np.int32), "idx": np.zeros(n, np.int32)}
+        tr = CTraj(*[buf[k].ctypes.data for k in ("act", "val", "pol", "mask", "dice", "idx")])
+        turns = _classic_lib().muzcpu_classic_selfplay(self.h, P, classic_rule_bits(**rules), n, S, D, T, temp, seed,
+                                                       dirichlet_fraction, ctypes.byref(tr))
+        return buf, turns
+
+    def bench(self, P, rules, lanes, S, D, T, temp, seed, threads, seconds, dirichlet_fraction=0.25):
+        s, g, t = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+        steps = _classic_lib().muzcpu_classic_bench(self.h, P, classic_rule_bits(**rules), lanes, S, D, T, temp, seed,
+                                                    dirichlet_fraction, threads, seconds, ctypes.byref(s),
+                                                    ctypes.byref(g), ctypes.byref(t))
+        return dict(env_steps=int(steps), searches=int(s.value), games=int(g.value), elapsed=float(t.value))
