@@ -61,7 +61,8 @@ CLASSIC_PLAYERS = 4
 CLASSIC_FLOP_PER_SIM = 2 * 907_152
 # Config (d): DOG 2v2, 1024 games per GPU (8192 over 8 GPUs), uniform random legal policy.
 DOG_BATCH = 1024
-DOG_TURNS_PER_STEP = 16         # one bench step = one muz_dog_random_play launch of 16 turns over the batch
+DOG_TURNS_PER_LAUNCH = 1024     # one muz_dog_random_play launch plays 1024 turns of every game (~10 ms)
+DOG_LAUNCHES_PER_STEP = 32      # one bench step = 32 launches (~0.3 s: the default 3 steps time ~1 s)
 
 
 def parse():
@@ -305,32 +306,25 @@ def sum_max(dist, device, sums, elapsed):
     return [x.item() for x in t], m[0].item()
 
 
-def dog_cpu_baseline(seconds):
-    """oracle/dog.py random legal play (the same engine streams) on one host core, bounded by `seconds`;
-    finished games are replaced by fresh ones so the sample keeps playing."""
+def dog_cpu_baseline(seconds, lanes=8):
+    """SURVEY §8(d)'s CPU timing for config (d): the C++ restatement of the DOG env (oracle/cpu_dog.cpp: dog.py's
+    806-action legality, transitions and deals with the engine's counter-RNG deal keys and random legal action,
+    finished games restarted; checked against the NumPy oracle by tests/test_cpu_baseline_dog.py) on the host for
+    `seconds`, at 1 thread and at all cores."""
+    from oracle import cpu_selfplay as CS
     from oracle import dog as dg
-    n, seed = 8, 5
-
-    def fresh(g):
-        return dg.env_reset(num_players=4, shuffle_keys=dg.engine_shuffle_keys(seed, g), **dg.SELFPLAY_RULES)
-
-    gids = list(range(n))
-    envs = [fresh(g) for g in gids]
-    steps, t, nxt = 0, 0, n
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        for i in range(n):
-            if envs[i].done:
-                gids[i], nxt = nxt, nxt + 1
-                envs[i] = fresh(gids[i])
-            g, keys = gids[i], dg.engine_shuffle_keys(seed, gids[i])
-            a = dg.engine_random_action(dg.valid_actions(envs[i]), seed, g, t)
-            envs[i] = (dg.no_step(envs[i], keys) if a < 0 else dg.env_step(envs[i], a, keys))[0]
-            steps += 1
-        t += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(steps / dt, 2), "unit": "env_steps/s", "cores": 1, "kind": "port",
-            "sample": f"NumPy oracle DOG random play, {n} concurrent games, {steps} env-steps in {dt:.1f}s"}
+    cores, aff = cpu_cores()
+    half = seconds / 2
+    one = CS.dog_bench(4, dg.SELFPLAY_RULES, lanes, 5, 1, half)
+    allc = CS.dog_bench(4, dg.SELFPLAY_RULES, lanes, 5, cores, half)
+    v1 = one["env_steps"] / one["elapsed"]
+    vn = allc["env_steps"] / allc["elapsed"]
+    return {"value": round(vn, 2), "unit": "env_steps/s", "cores": cores, "kind": "port",
+            "value_1core": round(v1, 2), "value_allcores": round(vn, 2), "cores_affinity": aff,
+            "sample": f"C++ restatement of the reference DOG env (oracle/cpu_dog.cpp, OpenMP): 4p teams uniform random "
+                      f"legal play, {lanes} games per thread restarted when finished, {half:.0f} s at 1 thread "
+                      f"({one['env_steps']} env-steps, {one['games']} games finished) and {half:.0f} s at {cores} "
+                      f"threads ({allc['env_steps']} env-steps); affinity shows {aff} CPUs"}
 
 
 # k_dog_play's per-turn critical path, measured with the stamp build (profiles/diag_dog_stamps.py,
@@ -363,7 +357,7 @@ def run_dog(args):
     import torch
     rank, world, dist, device = setup(args)
     from exploring_muzero_on_dog_amd import dog as DG
-    T = DOG_TURNS_PER_STEP
+    T, L = DOG_TURNS_PER_LAUNCH, DOG_LAUNCHES_PER_STEP
     rp = DG.RandomPlay(args.batch, seed=4 + 1000 * rank, fused=True)
     warm = torch.zeros(args.batch, dtype=torch.int32, device=device)
     env_steps = torch.zeros(args.batch, dtype=torch.int32, device=device)
@@ -372,31 +366,28 @@ def run_dog(args):
     traj = DG.DogTrajectory(args.batch, T, device=device) if args.records else None
     gathered = [0]
 
-    def step(k):
-        ev[k][0].record()
+    def launch(counter, ep):
         if traj is not None:
             traj.reset()
-        rp.play(T, env_steps, auto_reset=True, episodes=episodes, record=traj)
-        ev[k][1].record()
-        if traj is not None:            # actor -> learner rank: pack the step's rows, gather them to rank 0
+        rp.play(T, counter, auto_reset=True, episodes=ep, record=traj)
+        if traj is not None:            # actor -> learner rank: pack the launch's rows, gather them to rank 0
             packed = traj.pack()
             if dist is not None:
                 from exploring_muzero_on_dog_amd import transfer as TR
                 got = TR.gather_packed(packed, dst=0, spec=TR.dog_fields())
-                if got is not None:
+                if got is not None and ep is not None:
                     gathered[0] += sum(int(g["act"].shape[0]) for g in got)
-            else:
+            elif ep is not None:
                 gathered[0] += int(packed["act"].shape[0])
 
+    def step(k):
+        ev[k][0].record()
+        for _ in range(L):
+            launch(env_steps, episodes)
+        ev[k][1].record()
+
     for _ in range(args.warmup):        # the same calls as a timed step (record, pack and gather included)
-        if traj is not None:
-            traj.reset()
-        rp.play(T, warm, auto_reset=True, record=traj)
-        if traj is not None:
-            packed = traj.pack()
-            if dist is not None:
-                from exploring_muzero_on_dog_amd import transfer as TR
-                TR.gather_packed(packed, dst=0, spec=TR.dog_fields())
+        launch(warm, None)
 
     elapsed = timed_region(dist, step, args.steps)
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev)
@@ -406,7 +397,7 @@ def run_dog(args):
         if dist is not None:
             dist.destroy_process_group()
         return
-    avg_ms = kms / (args.steps * world)
+    avg_ms = kms / (args.steps * L * world)         # per launch
     # algorithmic bytes of one launch: the state is read and written once per launch (it stays in LDS
     # across the T turns), plus the per-game step counter
     launch_bytes = args.batch * (2 * 156 + 8)   # + env_steps / episodes counters (read + write)
@@ -418,11 +409,11 @@ def run_dog(args):
         "scaling": "strong" if args.split else "weak", "vs_baseline": None, "dtype": "int8",
         "data": "synthetic (seeded deals, counter-RNG random legal actions)", "games_finished": int(games),
         "config": {"workload": f"DOG 4p teams, {args.batch} games/GPU, uniform random legal action per turn, "
-                               f"{T} turns per step in one launch (state resident in LDS), finished games "
-                               f"restart in place" + (", every turn recorded, packed and gathered to rank 0"
-                                                      if args.records else ""), "games_per_gpu": args.batch,
+                               f"{L} launches of {T} turns per step (state resident in LDS within a launch), finished "
+                               f"games restart in place" + (", every turn recorded, packed and gathered to rank 0"
+                                                            if args.records else ""), "games_per_gpu": args.batch,
                    "records": bool(args.records),
-                   "turns_per_step": T,
+                   "turns_per_launch": T, "launches_per_step": L,
                    "parallelism": parallelism(args, world)},
         "roofline": dog_latency_model(avg_ms, args.batch, T, launch_bytes),
     }

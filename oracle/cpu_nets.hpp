@@ -3,6 +3,7 @@
 // TEST INFRASTRUCTURE / CPU BASELINE ONLY (see cpu_selfplay.cpp).  Everything is in an anonymous namespace:
 // each translation unit gets its own copy.
 #pragma once
+#pragma GCC diagnostic ignored "-Wunused-function"   // not every TU uses every shared piece
 #include <algorithm>
 #include <atomic>
 #include <chrono>

@@ -348,3 +348,107 @@ class CpuClassicNet:
                                                     dirichlet_fraction, threads, seconds, ctypes.byref(s),
                                                     ctypes.byref(g), ctypes.byref(t))
         return dict(env_steps=int(steps), searches=int(s.value), games=int(g.value), elapsed=float(t.value))
+
+
+# ---- DOG: random legal play (oracle/cpu_dog.cpp) -----------------------------------------------------------
+class Dog(ctypes.Structure):
+    _fields_ = [("board", ctypes.c_int8 * 56), ("deck", ctypes.c_int8 * 14), ("hands", ctypes.c_int8 * 56),
+                ("swap_choices", ctypes.c_int8 * 4), ("pins", ctypes.c_int32 * 16), ("start", ctypes.c_int32 * 4),
+                ("target", ctypes.c_int32 * 4), ("goal", ctypes.c_int32 * 16)] + \
+               [(n, ctypes.c_int32) for n in ("current_player", "reward", "done", "num_players", "round_starter", "phase",
+                                              "hand_size", "num_cards", "board_size", "total", "rules", "deal", "game")] + \
+               [("seed", ctypes.c_uint64)]
+
+
+_dog_bound = False
+
+
+def _dog_lib():
+    global _dog_bound
+    L = load()
+    if not _dog_bound:
+        vp, ip, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
+        L.muzcpu_dog_reset.argtypes = [vp, ip, ip, u64, ip]
+        L.muzcpu_dog_valid_actions.argtypes = [vp, vp]
+        L.muzcpu_dog_step.argtypes = [vp, ip, vp, vp]
+        L.muzcpu_dog_no_step.argtypes = [vp]
+        L.muzcpu_dog_step_kind.argtypes = [vp, ip, ip, ip, vp, vp, vp]
+        L.muzcpu_dog_play.restype = ctypes.c_int64
+        L.muzcpu_dog_play.argtypes = [ip, ip, ip, ip, u64, vp]
+        L.muzcpu_dog_bench.restype = ctypes.c_int64
+        L.muzcpu_dog_bench.argtypes = [ip, ip, ip, u64, ip, ctypes.c_double, vp, vp]
+        _dog_bound = True
+    return L
+
+
+def dog_rule_bits(**rules) -> int:
+    from oracle import dog as dg
+    r = dict(dg.DEFAULT_RULES)
+    r.update(rules)
+    if r["disable_swapping"] or r["disable_hot_seven"] or r["disable_joker"]:
+        raise ValueError("the C++ DOG restatement plays the full 14-card deck (the reference's DOG configs)")
+    return sum(bit for k, bit in _FLAGS.items() if k in r and r[k])
+
+
+def dog_from_oracle(e, seed=0, game=0) -> Dog:
+    """oracle/dog.State -> the C++ state struct (seed / game select the engine's deal keys)."""
+    d = Dog()
+    P = e.num_players
+    d.board[:] = [int(x) for x in e.board]
+    d.deck[:] = [int(x) for x in e.deck]
+    h = np.zeros((4, 14), np.int8)
+    h[:P] = e.hands
+    d.hands[:] = [int(x) for x in h.ravel()]
+    d.swap_choices[:] = [int(x) for x in e.swap_choices]
+    pins = -np.ones(16, np.int32)
+    pins[:P * 4] = np.asarray(e.pins).ravel()
+    d.pins[:] = [int(x) for x in pins]
+    st, tg, gl = np.zeros(4, np.int32), np.zeros(4, np.int32), np.zeros(16, np.int32)
+    st[:P], tg[:P], gl[:P * 4] = e.start, e.target, np.asarray(e.goal).ravel()
+    d.start[:], d.target[:], d.goal[:] = [int(x) for x in st], [int(x) for x in tg], [int(x) for x in gl]
+    for k in ("current_player", "reward", "round_starter", "phase", "hand_size", "num_cards", "deal"):
+        setattr(d, k, int(getattr(e, k)))
+    d.done, d.num_players, d.board_size, d.total = int(e.done), P, e.board_size, e.total_board_size
+    d.rules, d.game, d.seed = dog_rule_bits(**e.rules), int(game), int(seed)
+    return d
+
+
+def dog_valid_actions(d: Dog) -> np.ndarray:
+    out = np.zeros(806, np.uint8)
+    _dog_lib().muzcpu_dog_valid_actions(ctypes.byref(d), _p(out))
+    return out.astype(bool)
+
+
+def dog_step(d: Dog, action):
+    r, dn = ctypes.c_int(), ctypes.c_int()
+    _dog_lib().muzcpu_dog_step(ctypes.byref(d), int(action), ctypes.byref(r), ctypes.byref(dn))
+    return r.value, bool(dn.value)
+
+
+def dog_no_step(d: Dog):
+    _dog_lib().muzcpu_dog_no_step(ctypes.byref(d))
+
+
+def dog_step_kind(d: Dog, kind: str, case: dict):
+    """One DOG/test.py step_* call: kind normal_move / neg_move / swap_move / hot7_move -> (pins, reward, done)."""
+    k = {"normal_move": 0, "neg_move": 1, "swap_move": 2, "hot7_move": 3}[kind]
+    dist = np.ascontiguousarray(case.get("dist", [0, 0, 0, 0]), np.int32)
+    a = case.get("pin", 0)
+    b = case.get("pos", case.get("move", 0))
+    r, dn = ctypes.c_int(), ctypes.c_int()
+    _dog_lib().muzcpu_dog_step_kind(ctypes.byref(d), k, int(a), int(b), _p(dist), ctypes.byref(r), ctypes.byref(dn))
+    return np.array(d.pins[:d.num_players * 4], np.int32).reshape(d.num_players, 4), r.value, bool(dn.value)
+
+
+def dog_play(P, rules, n, turns, seed):
+    """bench.py's DOG CPU loop on one thread: (actions [turns, n], env-steps)."""
+    acts = np.zeros((turns, n), np.int32)
+    steps = _dog_lib().muzcpu_dog_play(P, dog_rule_bits(**rules), n, turns, seed, _p(acts))
+    return acts, int(steps)
+
+
+def dog_bench(P, rules, lanes, seed, threads, seconds):
+    g, t = ctypes.c_int64(), ctypes.c_double()
+    steps = _dog_lib().muzcpu_dog_bench(P, dog_rule_bits(**rules), lanes, seed, threads, seconds, ctypes.byref(g),
+                                        ctypes.byref(t))
+    return dict(env_steps=int(steps), games=int(g.value), elapsed=float(t.value))
