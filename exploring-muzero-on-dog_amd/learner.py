@@ -20,6 +20,8 @@ self-play kernels' arena (nets.DeviceNet).  Everything is fp32.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -35,40 +37,35 @@ LN_PLAIN, LN_RELU, LN_RESID_RELU = 0, 1, 2
 
 
 class _DenseLN(torch.autograd.Function):
-    """act(LayerNorm(x @ W + b)) with the GEMMs on the BLAS library and the bias / LayerNorm / ReLU / residual
-    epilogue and its backward as the fused kernels of csrc/learner_ln.hip (one launch forward, two backward,
-    instead of ~8 small ones).  mode LN_RELU: relu(LN(.)); LN_RESID_RELU: relu(res + LN(.)); LN_PLAIN: LN(.)."""
+    """act(LayerNorm(x @ W + b)): forward = the GEMM with its bias / LayerNorm / ReLU / residual epilogue in one
+    launch (csrc/learner_fused.hip), backward = the LayerNorm / ReLU backward with the input-gradient GEMM in
+    one launch, the weight / LayerNorm gradients through the GradSink (or a GEMM + column sum without one).  mode LN_RELU: relu(LN(.)); LN_RESID_RELU: relu(res + LN(.)); LN_PLAIN: LN(.).
+    ``owners`` = the leaf parameters (W, b, gamma, beta) for a GradSink (W may be a reshaped view of its leaf)."""
 
     @staticmethod
-    def forward(ctx, x, W, b, gamma, beta, res, mode):
-        lib = _L.load()
-        y = x @ W
-        M, Nn = y.shape
-        out, z = torch.empty_like(y), torch.empty_like(y)
-        mean = torch.empty((M,), dtype=y.dtype, device=y.device)
-        rstd = torch.empty_like(mean)
-        _L.check(lib.muz_ln_fwd(_L.ptr(y), _L.ptr(b), _L.ptr(gamma), _L.ptr(beta), _L.ptr(res), M, Nn, mode,
-                                _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.stream_ptr()), "muz_ln_fwd")
+    def forward(ctx, x, W, b, gamma, beta, res, mode, owners=None):
+        out, z, mean, rstd = _dense_ln_fwd(x, W, b, gamma, beta, res, mode)
         ctx.save_for_backward(x, W, gamma, out, z, mean, rstd)
-        ctx.mode = mode
+        ctx.mode, ctx.owners = mode, owners
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        lib = _L.load()
         x, W, gamma, out, z, mean, rstd = ctx.saved_tensors
-        dout = dout.contiguous()
         M, Nn = out.shape
-        dz = torch.empty_like(out)
-        dres = torch.empty_like(out) if ctx.mode == LN_RESID_RELU else None
-        scratch = torch.empty((lib.muz_ln_bwd_scratch_floats(M, Nn),), dtype=out.dtype, device=out.device)
-        dgamma, dbeta, db = (torch.empty((Nn,), dtype=out.dtype, device=out.device) for _ in range(3))
-        _L.check(lib.muz_ln_bwd(_L.ptr(dout), _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.ptr(gamma), M, Nn,
-                                ctx.mode, _L.ptr(dz), _L.ptr(dres), _L.ptr(scratch), _L.ptr(dgamma), _L.ptr(dbeta),
-                                _L.ptr(db), _L.stream_ptr()), "muz_ln_bwd")
-        dx = dz @ W.t() if ctx.needs_input_grad[0] else None
+        K = x.shape[1]
+        scratch = torch.empty((_ln_scratch_floats(M, Nn, K),), dtype=out.dtype, device=out.device)
+        dz, dres, dx = _dense_ln_bwd(dout, (out, z, mean, rstd), gamma, ctx.mode, W, scratch,
+                                     need_dx=ctx.needs_input_grad[0])
+        sink = _sink()
+        if sink is not None and ctx.owners is not None:
+            Wp, bp, gp, bep = ctx.owners
+            sink.ln_colsum(scratch, Nn, gp, bep, bp)
+            sink.wgrad(x, dz, Wp)
+            return dx, None, None, None, None, dres, None, None
+        dgamma, dbeta, db = _ln_colsum(scratch, Nn)
         dW = x.t() @ dz if ctx.needs_input_grad[1] else None
-        return dx, dW, db, dgamma, dbeta, dres, None
+        return dx, dW, db, dgamma, dbeta, dres, None, None
 
 
 _ONES = {}
@@ -85,11 +82,13 @@ def _ones(M, like):
 
 class _Dense(torch.autograd.Function):
     """x @ W + b whose bias gradient is a BLAS GEMV (dy^T @ 1) instead of torch's column-sum reduction
-    (~12 us per call at the learner's 1280-1408 rows, against ~5 us)."""
+    (~12 us per call at the learner's 1280-1408 rows, against ~5 us); with a GradSink active both parameter
+    gradients go to the grouped launches."""
 
     @staticmethod
     def forward(ctx, x, W, b):
         ctx.save_for_backward(x, W)
+        ctx.owners = (W, b) if W.is_leaf and b.is_leaf else None
         return (x @ W).add_(b)
 
     @staticmethod
@@ -97,6 +96,12 @@ class _Dense(torch.autograd.Function):
         x, W = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dy @ W.t() if ctx.needs_input_grad[0] else None
+        sink = _sink()
+        if sink is not None and ctx.owners is not None:
+            dy2 = dy2.contiguous()
+            sink.wgrad(x.reshape(-1, x.shape[-1]).contiguous(), dy2, ctx.owners[0])
+            sink.colsum(dy2, ctx.owners[1])
+            return dx, None, None
         dW = x.reshape(-1, x.shape[-1]).t() @ dy2 if ctx.needs_input_grad[1] else None
         db = torch.mv(dy2.t(), _ones(dy2.shape[0], dy2)) if ctx.needs_input_grad[2] else None
         return dx, dW, db
@@ -138,6 +143,116 @@ def _ln_fwd(y, bias, gamma, beta, res, mode, out=None):
     return out, z, mean, rstd
 
 
+# csrc/learner_fused.hip in the learner, measured per layer at the step's shapes (HIP-graph replay,
+# profiles/fused_layer_bench.py, r3): backward, LayerNorm backward + input gradient in one launch 7.4 / 8.0 us
+# (M = 128 / 1408 rows) against 8.0 / 10.0 us for muz_ln_bwd_rows + library GEMM -> on; forward, GEMM + LayerNorm
+# in one launch 10.0 / 10.6 us against 7.2 / 9.9 us for library GEMM + muz_ln_fwd -> off: a 16-row tile must own
+# whole rows for the LayerNorm, so one CU streams the full weight matrix and carries the tile's 1024 MFMAs
+# (>= 3.4 us at 32 cycles each), where the library spreads the columns over 2-4x more CUs.
+FUSED_FWD = False
+FUSED_BWD = True
+FUSED_DENSE = True   # False: neither (A/B timing)
+
+
+def _fusable(K, Nn, fwd=False):
+    """csrc/learner_fused.hip's shapes: K <= 512 inputs, N in {32, 64, 128, 256} outputs."""
+    return FUSED_DENSE and (FUSED_FWD if fwd else FUSED_BWD) and 0 < K <= 512 and Nn in (32, 64, 128, 256)
+
+
+def _ln_scratch_floats(M, Nn, K):
+    """Column-partial scratch of one layer's backward (_dense_ln_bwd)."""
+    lib = _L.load()
+    return lib.muz_dense_ln_bwd_scratch_floats(M, Nn) if _fusable(K, Nn) else lib.muz_ln_bwd_scratch_floats(M, Nn)
+
+
+class WeightTranspose:
+    """Zero-padded transposes W^T [N][K16] of every fused layer's weight, so that the forward kernel reads its
+    weight operand as one 16-byte load per lane (csrc/learner_fused.hip) instead of four column loads.
+    refresh() is one grouped launch (muz_transpose_grouped); the learner calls it at the start of every step
+    (inside the captured graph), so the copies always equal the parameters the step reads."""
+
+    def __init__(self, params: dict):
+        self.map, probs = {}, []
+        for name, p in params.items():
+            if not name.endswith("/kernel") or p.dim() < 2:
+                continue
+            K, Nn = int(np.prod(p.shape[:-1])), int(p.shape[-1])
+            if not _fusable(K, Nn, fwd=True):
+                continue
+            ldt = (K + 15) // 16 * 16
+            wt = torch.zeros((Nn, ldt), dtype=p.dtype, device=p.device)
+            self.map[p.data_ptr()] = (wt, ldt, K, Nn)
+            probs.append(_L.MuzTransposeProblem(p.data_ptr(), wt.data_ptr(), K, Nn, ldt))
+        self.probs = (_L.MuzTransposeProblem * max(len(probs), 1))(*probs)
+        self.count = len(probs)
+
+    def refresh(self):
+        _L.check(_L.load().muz_transpose_grouped(self.probs, self.count, _L.stream_ptr()), "muz_transpose_grouped")
+
+    def get(self, W):
+        e = self.map.get(W.data_ptr())
+        return e if e is not None and e[2:] == tuple(W.shape) else None
+
+    def __enter__(self):
+        global _WT
+        _WT = self
+        return self
+
+    def __exit__(self, *exc):
+        global _WT
+        _WT = None
+        return False
+
+
+_WT = None      # the active WeightTranspose (set around the learner's forward)
+
+
+def _dense_ln_fwd(x, W, bias, gamma, beta, res, mode, out=None):
+    """act(LayerNorm(x @ W + bias)) [+ residual] -> (out, z, mean, rstd) (no autograd): one launch
+    (muz_dense_ln_fwd, with the active WeightTranspose's W^T when it holds this weight) where fusable, else
+    the library GEMM + muz_ln_fwd."""
+    M, K = x.shape
+    Nn = W.shape[1]
+    if not _fusable(K, Nn, fwd=True):
+        return _ln_fwd(x @ W, bias, gamma, beta, res, mode, out=out)
+    x, W = x.contiguous(), W.contiguous()
+    wt = _WT.get(W) if _WT is not None else None
+    out = torch.empty((M, Nn), dtype=x.dtype, device=x.device) if out is None else out
+    z = torch.empty((M, Nn), dtype=x.dtype, device=x.device)
+    mean = torch.empty((M,), dtype=x.dtype, device=x.device)
+    rstd = torch.empty_like(mean)
+    _L.check(_L.load().muz_dense_ln_fwd(_L.ptr(x), M, K, _L.ptr(W), _L.ptr(None if wt is None else wt[0]),
+                                        0 if wt is None else wt[1], _L.ptr(bias), _L.ptr(gamma), _L.ptr(beta),
+                                        _L.ptr(res), Nn, mode, _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd),
+                                        _L.stream_ptr()), "muz_dense_ln_fwd")
+    return out, z, mean, rstd
+
+
+def _dense_ln_bwd(dout, fwd, gamma, mode, W, scratch, dz=None, acc=None, dx_out=None, need_dx=True):
+    """Backward of _dense_ln_fwd up to the layer input: -> (dz, dres or None, dx = dz @ W^T (+ acc) or None);
+    column partials into scratch (_ln_scratch_floats).  One launch (muz_dense_ln_bwd) where fusable."""
+    out = fwd[0]
+    M, Nn = out.shape
+    K = W.shape[0]
+    if not _fusable(K, Nn):
+        dz, dres = _ln_bwd_rows(dout, fwd, gamma, mode, scratch, dz)
+        if not need_dx:
+            return dz, dres, None
+        if acc is None:
+            return dz, dres, torch.mm(dz, W.t(), out=dx_out) if dx_out is not None else dz @ W.t()
+        return dz, dres, torch.addmm(acc, dz, W.t(), out=dx_out) if dx_out is not None else torch.addmm(acc, dz, W.t())
+    dout, W = dout.contiguous(), W.contiguous()
+    dz = torch.empty_like(out) if dz is None else dz
+    dres = torch.empty_like(out) if mode == LN_RESID_RELU else None
+    dx = None
+    if need_dx:
+        dx = torch.empty((M, K), dtype=out.dtype, device=out.device) if dx_out is None else dx_out
+    _L.check(_L.load().muz_dense_ln_bwd(_L.ptr(dout), *(_L.ptr(t) for t in fwd), _L.ptr(gamma), M, Nn, mode, _L.ptr(W),
+                                        K, _L.ptr(acc), _L.ptr(dz), _L.ptr(dres), _L.ptr(dx), _L.ptr(scratch),
+                                        _L.stream_ptr()), "muz_dense_ln_bwd")
+    return dz, dres, dx
+
+
 def _ln_bwd_rows(dout, fwd, gamma, mode, scratch, dz=None):
     """Row half of the fused backward: -> (dz, dres or None); column partials into scratch.  `dz`: a
     preallocated contiguous destination."""
@@ -158,6 +273,116 @@ def _ln_colsum(scratch, Nn):
     _L.check(_L.load().muz_ln_colsum(_L.ptr(scratch), scratch.numel() // (3 * Nn), Nn, _L.ptr(dg), _L.ptr(db_),
                                      _L.ptr(dbias), _L.stream_ptr()), "muz_ln_colsum")
     return dg, db_, dbias
+
+
+class GradSink:
+    """The weight / bias / LayerNorm parameter gradients of one backward as TWO grouped launches
+    (csrc/learner_grad.hip: muz_wgrad_grouped, muz_colsum_grouped) instead of one library GEMM / column sum
+    each (~130 launches per det step).  While a sink is active (``with sink:`` around ``loss.backward()``) the
+    dense / LayerNorm autograd nodes record (X, dZ) pairs and column-sum partials here and return no gradient for
+    those parameters; ``flush()`` computes them into per-parameter buffers (allocated once, stable pointers: a
+    captured HIP graph replays into them) and points each parameter's ``.grad`` at its buffer.  A parameter is
+    owned by exactly one node (recorded twice -> error).  Recorded tensors are kept alive until the flush."""
+
+    def __init__(self):
+        self.buf, self.wg, self.cs, self.keep, self.owned = {}, [], [], [], set()
+        self.scratch = None     # segment partials of the long weight-gradient reductions
+
+    def __enter__(self):
+        global _SINK
+        _SINK = self
+        return self
+
+    def __exit__(self, *exc):
+        global _SINK
+        _SINK = None
+        return False
+
+    def _grad(self, p):
+        if id(p) in self.owned:
+            raise RuntimeError("GradSink: a parameter's gradient was recorded twice")
+        self.owned.add(id(p))
+        g = self.buf.get(id(p))
+        if g is None:
+            g = self.buf[id(p)] = (p, torch.empty_like(p, memory_format=torch.contiguous_format))
+        return g[1]
+
+    def wgrad(self, x2d, dz2d, p):
+        """grad(p) = x2d^T @ dz2d (p viewed as [K, N])."""
+        M, K = x2d.shape
+        N = dz2d.shape[1]
+        g = self._grad(p)
+        if g.numel() != K * N or x2d.stride(1) != 1 or dz2d.stride(1) != 1 or dz2d.shape[0] != M:
+            raise ValueError("GradSink.wgrad: shapes / layouts do not match the parameter")
+        self.keep += [x2d, dz2d]
+        self.wg.append((x2d.data_ptr(), dz2d.data_ptr(), g.data_ptr(), M, K, N, x2d.stride(0), dz2d.stride(0)))
+
+    def ln_colsum(self, scratch, N, gamma=None, beta=None, bias=None):
+        """dgamma / dbeta / dbias from muz_ln_bwd_rows partials (any subset of the three)."""
+        outs = [0 if q is None else self._grad(q).data_ptr() for q in (gamma, beta, bias)]
+        self.keep.append(scratch)
+        self.cs.append((scratch.data_ptr(), *outs, 0, scratch.numel() // (3 * N), N, N))
+
+    def colsum(self, dz2d, p):
+        """grad(p) = column sums of dz2d (a bias)."""
+        g = self._grad(p)
+        if dz2d.stride(1) != 1 or g.numel() != dz2d.shape[1]:
+            raise ValueError("GradSink.colsum: layout")
+        self.keep.append(dz2d)
+        self.cs.append((dz2d.data_ptr(), g.data_ptr(), 0, 0, 1, dz2d.shape[0], dz2d.shape[1], dz2d.stride(0)))
+
+    def flush(self):
+        lib, st = _L.load(), _L.stream_ptr()
+        if self.wg:
+            arr = (_L.MuzWgradProblem * len(self.wg))(*[_L.MuzWgradProblem(*w) for w in self.wg])
+            need = lib.muz_wgrad_scratch_floats(arr, len(self.wg))
+            if self.scratch is None or self.scratch.numel() < need:    # kept: a captured graph replays into it
+                self.scratch = torch.empty((max(need, 1),), dtype=torch.float32, device=self.keep[0].device)
+            _L.check(lib.muz_wgrad_grouped(arr, len(self.wg), _L.ptr(self.scratch), self.scratch.numel(), st),
+                     "muz_wgrad_grouped")
+        if self.cs:
+            arr = (_L.MuzColsumProblem * len(self.cs))(*[_L.MuzColsumProblem(*c) for c in self.cs])
+            _L.check(lib.muz_colsum_grouped(arr, len(self.cs), st), "muz_colsum_grouped")
+        for p, g in self.buf.values():
+            if id(p) in self.owned:
+                p.grad = g
+        self.wg, self.cs, self.keep, self.owned = [], [], [], set()
+
+
+class _transposed:
+    """with _transposed(wt): refresh the W^T copies, then run the forward with them (no-op for None)."""
+
+    def __init__(self, wt):
+        self.wt = wt
+
+    def __enter__(self):
+        if self.wt is not None:
+            self.wt.refresh()
+            self.wt.__enter__()
+
+    def __exit__(self, *exc):
+        if self.wt is not None:
+            self.wt.__exit__()
+        return False
+
+
+def _backward(loss, sink):
+    """loss.backward() with the parameter gradients formed by `sink`'s grouped launches (None: by autograd)."""
+    if sink is None:
+        loss.backward()
+        return
+    with sink:
+        loss.backward()
+    sink.flush()
+
+
+FUSED_LOSS = True      # False: the losses as torch ops (A/B timing, and the fused kernel's test reference)
+GROUPED_GRADS = True   # False: every weight / bias / LayerNorm gradient as its own launch (A/B timing)
+_SINK = None     # the active GradSink (module-global: autograd runs GPU backward nodes on its own thread)
+
+
+def _sink():
+    return _SINK
 
 
 _RB_PARAMS = ("Dense_0/kernel", "Dense_0/bias", "LayerNorm_0/scale", "LayerNorm_0/bias",
@@ -191,6 +416,11 @@ _NP = len(DYN_TRUNK_PARAMS)      # 28 per trunk
 
 
 _GEMM_LAYERS = ("3", "4", "a0", "b0", "a1", "b1", "5")   # the trunk's weight layers, named by their input
+
+
+# weight layer (named by its input) -> indices of (kernel, bias, LN scale, LN bias) in trunk_param_names order
+_TRUNK_LAYER_PARAMS = (("3", (2, 3, 4, 5)), ("4", (6, 7, 8, 9)), ("a0", (10, 11, 12, 13)), ("b0", (14, 15, 16, 17)),
+                       ("a1", (18, 19, 20, 21)), ("b1", (22, 23, 24, 25)))
 
 
 def _slots(apps, ngroups):
@@ -246,13 +476,13 @@ class _TrunkChain(torch.autograd.Function):
             g0, be0, W3, b3, g1, be1, W4, b4, g2, be2 = Q[:10]
             f0 = _ln_fwd(lat, zero, g0, be0, None, LN_PLAIN)
             x0 = torch.addcmul(shift[i], f0[0], scale1[i], out=X[(g, "3")][j])
-            f3 = _ln_fwd(x0 @ W3, b3, g1, be1, None, LN_RELU, out=X[(g, "4")][j])
-            f4 = _ln_fwd(f3[0] @ W4, b4, g2, be2, None, LN_RELU, out=X[(g, "a0")][j])
+            f3 = _dense_ln_fwd(x0, W3, b3, g1, be1, None, LN_RELU, out=X[(g, "4")][j])
+            f4 = _dense_ln_fwd(f3[0], W4, b4, g2, be2, None, LN_RELU, out=X[(g, "a0")][j])
             x, rbs = f4[0], []
             for r in range(2):
                 Wa, ba, ga, bea, Wb, bb, gb, beb = Q[10 + 8 * r:18 + 8 * r]
-                fa = _ln_fwd(x @ Wa, ba, ga, bea, None, LN_RELU, out=X[(g, f"b{r}")][j])
-                fb = _ln_fwd(fa[0] @ Wb, bb, gb, beb, x, LN_RESID_RELU, out=X[(g, "a1" if r == 0 else "5")][j])
+                fa = _dense_ln_fwd(x, Wa, ba, ga, bea, None, LN_RELU, out=X[(g, f"b{r}")][j])
+                fb = _dense_ln_fwd(fa[0], Wb, bb, gb, beb, x, LN_RESID_RELU, out=X[(g, "a1" if r == 0 else "5")][j])
                 rbs.append((x, fa, fb))
                 x = fb[0]
             _L.check(lib.muz_minmax_fwd(_L.ptr(lat), _L.ptr(x @ Q[26]), _L.ptr(Q[27]), B, Nn, _L.ptr(outs[i]),
@@ -273,11 +503,12 @@ class _TrunkChain(torch.autograd.Function):
         H = None if H is None else H.contiguous()
         dev, dt = G.device, G.dtype
         lib = _L.load()
-        nf = lib.muz_ln_bwd_scratch_floats(B, Nn)
+        nf = {n: lib.muz_ln_bwd_scratch_floats(B, Nn) if n == "0" else _ln_scratch_floats(B, Nn, Nn)
+              for n in ("0", "3", "4", "a0", "b0", "a1", "b1")}
         ngroups = len(P) // _NP
         slot, seen = _slots(apps, ngroups)       # application i's row in its group's stacked buffers
         layers = ("0", "3", "4", "a0", "b0", "a1", "b1")
-        scr = {(g, n): torch.empty((max(seen[g], 1), nf), dtype=dt, device=dev) for g in range(ngroups) for n in layers}
+        scr = {(g, n): torch.empty((max(seen[g], 1), nf[n]), dtype=dt, device=dev) for g in range(ngroups) for n in layers}
         # output gradients of the weight layers, stacked like the forward's inputs (ctx.X)
         DZ = {(g, n): torch.empty((max(seen[g], 1), B, Nn), dtype=dt, device=dev)
               for g in range(ngroups) for n in _GEMM_LAYERS}
@@ -295,24 +526,34 @@ class _TrunkChain(torch.autograd.Function):
             for r in (1, 0):
                 xin, fa, fb = rbs[r]
                 Wa, ga, Wb, gb = Q[10 + 8 * r], Q[12 + 8 * r], Q[14 + 8 * r], Q[16 + 8 * r]
-                dzb, dres = _ln_bwd_rows(dx, fb, gb, LN_RESID_RELU, scr[(g, f"b{r}")][j], DZ[(g, f"b{r}")][j])
-                dza, _ = _ln_bwd_rows(dzb @ Wb.t(), fa, ga, LN_RELU, scr[(g, f"a{r}")][j], DZ[(g, f"a{r}")][j])
-                dx = dres.addmm_(dza, Wa.t())          # dres + dza Wa^T, the GEMM accumulating in place
-            dz4, _ = _ln_bwd_rows(dx, f4, Q[8], LN_RELU, scr[(g, "4")][j], DZ[(g, "4")][j])
-            dz3, _ = _ln_bwd_rows(dz4 @ Q[6].t(), f3, Q[4], LN_RELU, scr[(g, "3")][j], DZ[(g, "3")][j])
-            dx0 = torch.mm(dz3, Q[2].t(), out=dshift[i])
+                _, dres, t = _dense_ln_bwd(dx, fb, gb, LN_RESID_RELU, Wb, scr[(g, f"b{r}")][j], DZ[(g, f"b{r}")][j])
+                # dres + dza Wa^T, the residual accumulated inside the same launch
+                _, _, dx = _dense_ln_bwd(t, fa, ga, LN_RELU, Wa, scr[(g, f"a{r}")][j], DZ[(g, f"a{r}")][j], acc=dres)
+            _, _, t = _dense_ln_bwd(dx, f4, Q[8], LN_RELU, Q[6], scr[(g, "4")][j], DZ[(g, "4")][j])
+            _, _, dx0 = _dense_ln_bwd(t, f3, Q[4], LN_RELU, Q[2], scr[(g, "3")][j], DZ[(g, "3")][j], dx_out=dshift[i])
             torch.mul(dx0, f0[0], out=dscale[i])
             dz0, _ = _ln_bwd_rows(dx0 * scale1[i], f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
             ca, cb = dz0, dq
         grads = [None] * len(P)
+        sink = _sink()
         for g in range(ngroups):
             if not seen[g]:
                 grads[_NP * g:_NP * (g + 1)] = [torch.zeros_like(p) for p in P[_NP * g:_NP * (g + 1)]]
                 continue
             o = _NP * g
+            if sink is not None:       # the same gradients, formed by the sink's grouped launches after backward
+                Q = P[o:o + _NP]
+                sink.ln_colsum(scr[(g, "0")], Nn, Q[0], Q[1])
+                for n, (iw, ib, ig, ibe) in _TRUNK_LAYER_PARAMS:
+                    Xs, Ds = (t[(g, n)][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
+                    sink.wgrad(Xs, Ds, Q[iw])
+                    sink.ln_colsum(scr[(g, n)], Nn, Q[ig], Q[ibe], Q[ib])
+                Xs, Ds = (t[(g, "5")][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
+                sink.wgrad(Xs, Ds, Q[26])
+                sink.colsum(Ds, Q[27])
+                continue
             grads[o], grads[o + 1], _ = _ln_colsum(scr[(g, "0")], Nn)
-            for n, (iw, ib, ig, ibe) in (("3", (2, 3, 4, 5)), ("4", (6, 7, 8, 9)), ("a0", (10, 11, 12, 13)),
-                                         ("b0", (14, 15, 16, 17)), ("a1", (18, 19, 20, 21)), ("b1", (22, 23, 24, 25))):
+            for n, (iw, ib, ig, ibe) in _TRUNK_LAYER_PARAMS:
                 Xs, Ds = (t[(g, n)][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
                 grads[o + iw] = Xs.t() @ Ds
                 grads[o + ig], grads[o + ibe], grads[o + ib] = _ln_colsum(scr[(g, n)], Nn)
@@ -359,8 +600,8 @@ class MuZeroNets:
         if x.is_cuda:
             lead, Nn = x.shape[:-1], W.shape[-1]
             r = None if res is None else res.reshape(-1, Nn).contiguous()
-            out = _DenseLN.apply(x.reshape(-1, x.shape[-1]).contiguous(), W, self.p[f"{dense}/bias"],
-                                 self.p[f"{ln}/scale"], self.p[f"{ln}/bias"], r, mode)
+            own = (self.p[f"{dense}/kernel"], self.p[f"{dense}/bias"], self.p[f"{ln}/scale"], self.p[f"{ln}/bias"])
+            out = _DenseLN.apply(x.reshape(-1, x.shape[-1]).contiguous(), W, *own[1:], r, mode, own)
             return out.reshape(*lead, Nn)
         y = self._ln(ln, x @ W + self.p[f"{dense}/bias"])
         return F.relu(y) if mode == LN_RELU else (F.relu(res + y) if mode == LN_RESID_RELU else y)
@@ -461,14 +702,10 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     latent = nets.representation(obs)
     B, K = batch["actions"].shape
     dev = obs.device
-    acts = torch.cat([batch["actions"], torch.zeros((B, 1), dtype=batch["actions"].dtype, device=dev)], 1)
-    ones = torch.ones((B, 1), dtype=torch.int32, device=dev)
-    disc_t = torch.cat([batch["discount_targets"].int(), ones], 1)
-    rew_t = torch.cat([batch["rewards"].int(), ones], 1)
     # Only the latent chain is sequential: the action FiLM rows, Pred4 on every step's latent and the
     # reward / discount heads are row-wise, so each runs once over all K (+1) steps stacked along the batch
     # (same per-row arithmetic as the step-by-step loop of the reference; far fewer kernel launches).
-    oh, scale, shift = nets.dynamics_film(acts[:, :K].transpose(0, 1).reshape(-1))
+    oh, scale, shift = nets.dynamics_film(batch["actions"][:, :K].transpose(0, 1).reshape(-1))
     latents = [latent]
     # The reward / discount heads read the next latent inside dynamics_net (muzero_deterministic_madn.py:
     # 437-455), BEFORE the loss scales the gradient of the latent it carries on (line 105): the heads take
@@ -487,7 +724,15 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
         head_in = torch.cat(raws, 0) if K else None
     logits_all, v_all = nets.prediction(torch.cat(latents, 0))
     rl_all, dl_all = nets.dynamics_heads(head_in, oh) if K else (None, None)
+    if obs.is_cuda and FUSED_LOSS:
+        u = 1.0 / unroll_steps
+        spec = dict(batch=batch, K=K, scale_value=u * VALUE_SCALING, scale_policy=u * POLICY_SCALING, norm=0,
+                    terms=[(batch["discount_targets"], 0, 1.0, 0.1, u * DISCOUNT_SCALING),     # terminal 1.0, other 0.1
+                           (batch["rewards"], 0, 0.1, 1.0, u * REWARD_SCALING)])               # neutral 0.1, win/lose 1.0
+        total, parts = _LossHeads.apply(logits_all, v_all, dl_all, rl_all, None, spec)
+        return total, (parts[1], parts[2], parts[3], parts[4])
     # The per-step losses, all K (+1) steps at once ([K+1, B] views; row k = unroll step k).
+    disc_t, rew_t = batch["discount_targets"].int(), batch["rewards"].int()
     m = batch["masks"][:, :K + 1].transpose(0, 1).to(obs.dtype)
     v = v_all[:, 0].reshape(K + 1, B)
     l_value = torch.mean(m * (batch["target_values"][:, :K + 1].transpose(0, 1).to(obs.dtype) - v) ** 2, 1)
@@ -502,6 +747,67 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     total = ((1.0 / unroll_steps) * (VALUE_SCALING * l_value + POLICY_SCALING * l_policy)).sum() + \
         (1.0 / unroll_steps) * (DISCOUNT_SCALING * l_disc.sum() + REWARD_SCALING * l_rew.sum())
     return total, (l_value.sum(), l_policy.sum(), l_disc.sum(), l_rew.sum())
+
+
+class _LossHeads(torch.autograd.Function):
+    """All losses of one unrolled batch and their gradients w.r.t. the network outputs as ONE launch
+    (csrc/learner_loss.hip: muz_loss_heads; ~120 torch launches forward + backward before).  Forward computes
+    the gradients too; backward scales them by the incoming gradient of the total (one foreach launch).
+    spec: K, batch, scale_value, scale_policy, norm and terms = [(labels | probs, rare_not_one, w_rare, w_common,
+    scale)] matching the logits tensors t0..t2.  -> (total, parts [6] = total, value, policy, term 0..2)."""
+
+    @staticmethod
+    def forward(ctx, logits, value, t0, t1, t2, spec):
+        b, K = spec["batch"], spec["K"]
+        B, A = b["masks"].shape[0], logits.shape[-1]
+        dev, dt = logits.device, logits.dtype
+        logits, value = logits.contiguous(), value.contiguous()
+        a = _L.MuzLossArgs()
+        a.K, a.B, a.A, a.T = K, B, A, b["masks"].shape[1]
+        masks, tv, pol = (b[k].to(dt).contiguous() for k in ("masks", "target_values", "policies"))
+        if tv.shape[1] != a.T or pol.shape[1] != a.T or pol.shape[2] != A or logits.shape[0] != (K + 1) * B:
+            raise ValueError("_LossHeads: batch / output shapes disagree")
+        dlogits, dvalue = torch.empty_like(logits), torch.empty_like(value)
+        a.masks, a.target_values, a.policies = masks.data_ptr(), tv.data_ptr(), pol.data_ptr()
+        a.value, a.logits, a.dvalue, a.dlogits = value.data_ptr(), logits.data_ptr(), dvalue.data_ptr(), dlogits.data_ptr()
+        a.scale_value, a.scale_policy, a.norm = spec["scale_value"], spec["scale_policy"], spec["norm"]
+        keep, dts = [masks, tv, pol, logits, value], []
+        terms = [t for t in (t0, t1, t2) if t is not None]
+        a.nterms = len(terms)
+        for j, (t, (tgt, rare_not_one, w_rare, w_common, scale)) in enumerate(zip(terms, spec["terms"])):
+            t = t.contiguous()
+            # class labels as int32 [B, K] (reference-style batches may carry them as int64 / float);
+            # distributions as float [B, K, ncls]
+            tgt = (tgt.to(dt) if tgt.dim() == 3 else tgt.to(torch.int32)).contiguous()
+            d = torch.empty_like(t)
+            keep += [t, tgt]
+            dts.append(d)
+            q = a.term[j]
+            q.logits, q.dlogits, q.ncls, q.ld = t.data_ptr(), d.data_ptr(), t.shape[-1], tgt.shape[1]
+            if tgt.dtype == torch.int32:
+                q.labels = tgt.data_ptr()
+            else:
+                q.probs = tgt.data_ptr()
+                if tgt.shape[2] != t.shape[-1]:
+                    raise ValueError("_LossHeads: target width")
+            if t.shape[0] != K * B or tgt.shape[0] != B:
+                raise ValueError("_LossHeads: term shapes")
+            q.rare_not_one, q.w_rare, q.w_common, q.scale = int(rare_not_one), w_rare, w_common, scale
+        parts = torch.empty((6,), dtype=dt, device=dev)
+        total = torch.empty((), dtype=dt, device=dev)
+        a.parts, a.total = parts.data_ptr(), total.data_ptr()
+        _L.check(_L.load().muz_loss_heads(ctypes.byref(a), _L.stream_ptr()), "muz_loss_heads")
+        ctx.d = (dlogits, dvalue, *dts)
+        ctx.present = tuple(t is not None for t in (t0, t1, t2))
+        ctx.mark_non_differentiable(parts)
+        return total, parts
+
+    @staticmethod
+    def backward(ctx, g_total, g_parts):
+        d = list(ctx.d)
+        torch._foreach_mul_(d, g_total)
+        it = iter(d[2:])
+        return (d[0], d[1], *(next(it) if p else None for p in ctx.present), None)
 
 
 def _balanced_ce_steps(logits, labels, mask, special, w_special, w_other):
@@ -642,10 +948,14 @@ class Learner:
         self.unroll_steps = int(unroll_steps)
         self.graph = bool(graph)
         self._g = None
+        self.sink = GradSink() if GROUPED_GRADS and torch.device(device).type == "cuda" else None
+        self.wt = WeightTranspose(self.nets.p) if FUSED_DENSE and FUSED_FWD and torch.device(device).type == "cuda" \
+            else None
 
     def _step(self, batch):
-        loss, (v, pl, d, r) = loss_fn(self.nets, batch, self.unroll_steps)
-        loss.backward()
+        with _transposed(self.wt):
+            loss, (v, pl, d, r) = loss_fn(self.nets, batch, self.unroll_steps)
+        _backward(loss, self.sink)
         self.opt.step()
         return {"total_loss": loss.detach(), "v_loss": v.detach(), "p_loss": pl.detach(), "d_loss": d.detach(),
                 "r_loss": r.detach()}
@@ -724,10 +1034,14 @@ class ClassicMuZeroNets(MuZeroNets):
         super().__init__(params, obs_channels, 4, device, dtype, shapes=classic_param_shapes(obs_channels))
         self.NC = 6
 
-    def _film_trunk(self, pre, rb0, x_in, e):
+    def _film_trunk(self, pre, rb0, x_in, e, film=None):
+        """film: precomputed (scale, shift) rows of this step (e unused) -- loss_fn_stochastic evaluates the FiLM
+        projections for all steps at once."""
         d = "dynamics"
         ln = self._ln(f"{d}/{pre}_input_ln", x_in)
-        x = ln * (1.0 + self._dense(f"{d}/{pre}_film_scale", e)) + self._dense(f"{d}/{pre}_film_shift", e)
+        if film is None:
+            film = (self._dense(f"{d}/{pre}_film_scale", e), self._dense(f"{d}/{pre}_film_shift", e))
+        x = ln * (1.0 + film[0]) + film[1]
         x = self._dense_ln(f"{d}/{pre}_dense1", f"{d}/{pre}_ln1", x)
         x = self._dense_ln(f"{d}/{pre}_dense2", f"{d}/{pre}_ln2", x)
         for r in range(rb0, rb0 + 2):
@@ -771,12 +1085,8 @@ def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int =
     latent = nets.representation(obs)
     B, K = batch["actions"].shape
     dev = obs.device
-    acts = torch.cat([batch["actions"], torch.zeros((B, 1), dtype=batch["actions"].dtype, device=dev)], 1)
-    dice = torch.cat([batch["dice_outcomes"][:, 1:].long(), torch.zeros((B, 2), dtype=torch.long, device=dev)], 1)
-    probs = torch.cat([batch["dice_probs"].to(dt), torch.full((B, 1, 6), 1.0 / 6.0, dtype=dt, device=dev)], 1)
-    ones = torch.ones((B, 1), dtype=torch.int32, device=dev)
-    disc_t = torch.cat([batch["discount_targets"].int(), ones], 1)
-    rew_t = torch.cat([batch["rewards"].int(), ones], 1)
+    acts = batch["actions"]
+    dice = torch.cat([batch["dice_outcomes"][:, 1:].long(), torch.zeros((B, 1), dtype=torch.long, device=dev)], 1)
     sc = CLASSIC_SCALING
     # Only the afterstate / state chain is sequential; the embeddings, Pred4 and the action heads run once
     # over all steps stacked along the batch (same per-row arithmetic, far fewer launches).
@@ -800,7 +1110,16 @@ def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int =
     logits_all, v_all = nets.prediction(torch.cat(latents, 0))
     if K:
         rl_all, cl_all, dl_all = nets.action_heads(torch.cat(latents[:K], 0), torch.cat(afters, 0), oh_all)
+    if obs.is_cuda and FUSED_LOSS and K:
+        u = 1.0 / unroll_steps
+        spec = dict(batch=batch, K=K, scale_value=u * sc["value"], scale_policy=u * sc["policy"], norm=1,
+                    terms=[(batch["dice_probs"], 0, 1.0, 0.1, u * sc["chance"]),
+                           (batch["discount_targets"], 0, 1.0, 0.1, u * sc["discount"]),      # rare: terminal
+                           (batch["rewards"], 1, 1.0, 0.1, u * sc["reward"])])                 # rare: won / lost
+        total, parts = _LossHeads.apply(logits_all, v_all, cl_all, dl_all, rl_all, spec)
+        return total, (parts[1], parts[2], parts[3], parts[4], parts[5])
     # all K (+1) steps at once, as in loss_fn
+    probs, disc_t, rew_t = batch["dice_probs"].to(dt), batch["discount_targets"].int(), batch["rewards"].int()
     m = batch["masks"][:, :K + 1].transpose(0, 1).to(dt)
     v = v_all[:, 0].reshape(K + 1, B)
     logp = F.log_softmax(logits_all, -1).reshape(K + 1, B, -1)
@@ -851,10 +1170,14 @@ class StochasticLearner(Learner):
         self.unroll_steps = int(unroll_steps)
         self.graph = bool(graph)
         self._g = None
+        self.sink = GradSink() if GROUPED_GRADS and torch.device(device).type == "cuda" else None
+        self.wt = WeightTranspose(self.nets.p) if FUSED_DENSE and FUSED_FWD and torch.device(device).type == "cuda" \
+            else None
 
     def _step(self, batch):
-        loss, (v, pl, c, d, r) = loss_fn_stochastic(self.nets, batch, self.unroll_steps)
-        loss.backward()
+        with _transposed(self.wt):
+            loss, (v, pl, c, d, r) = loss_fn_stochastic(self.nets, batch, self.unroll_steps)
+        _backward(loss, self.sink)
         self.opt.step()
         return {"total_loss": loss.detach(), "v_loss": v.detach(), "p_loss": pl.detach(), "c_loss": c.detach(),
                 "d_loss": d.detach(), "r_loss": r.detach()}

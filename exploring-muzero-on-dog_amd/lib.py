@@ -32,6 +32,32 @@ class MuzDogTraj(ctypes.Structure):
                 ("max_steps", ctypes.c_int32)]
 
 
+class MuzWgradProblem(ctypes.Structure):
+    _fields_ = [("x", vp), ("dz", vp), ("out", vp)] + [(k, ctypes.c_int32) for k in ("M", "K", "N", "ldx", "lddz")]
+
+
+class MuzColsumProblem(ctypes.Structure):
+    _fields_ = [("src", vp), ("out0", vp), ("out1", vp), ("out2", vp)] + \
+        [(k, ctypes.c_int32) for k in ("kind", "rows", "N", "ld")]
+
+
+class MuzTransposeProblem(ctypes.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("K", ctypes.c_int32), ("N", ctypes.c_int32), ("ldt", ctypes.c_int32)]
+
+
+class MuzLossTerm(ctypes.Structure):
+    _fields_ = [("logits", vp), ("dlogits", vp), ("labels", vp), ("probs", vp), ("ncls", ctypes.c_int32),
+                ("ld", ctypes.c_int32), ("rare_not_one", ctypes.c_int32), ("w_rare", ctypes.c_float),
+                ("w_common", ctypes.c_float), ("scale", ctypes.c_float)]
+
+
+class MuzLossArgs(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int32) for k in ("K", "B", "A", "T", "nterms", "norm")] + \
+        [(k, vp) for k in ("masks", "target_values", "policies", "value", "logits", "dvalue", "dlogits")] + \
+        [("scale_value", ctypes.c_float), ("scale_policy", ctypes.c_float), ("term", MuzLossTerm * 3),
+         ("parts", vp), ("total", vp)]
+
+
 class MuzRules(ctypes.Structure):
     _fields_ = [
         ("num_players", ctypes.c_int32),
@@ -291,6 +317,16 @@ SIGNATURES = {
                                       ctypes.c_int32, vp, vp]),
     "muz_im2col_fwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),
     "muz_im2col_bwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),
+    "muz_wgrad_scratch_floats": (ctypes.c_int64, [vp, ctypes.c_int32]),
+    "muz_wgrad_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp, ctypes.c_int64, vp]),
+    "muz_colsum_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp]),
+    "muz_loss_heads": (ctypes.c_int, [vp, vp]),
+    "muz_dense_ln_fwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp, vp, vp,
+                                        ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
+    "muz_transpose_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp]),
+    "muz_dense_ln_bwd_scratch_floats": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    "muz_dense_ln_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp,
+                                        ctypes.c_int32, vp, vp, vp, vp, vp, vp]),
     "muz_adamw_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32, vp]),
     "muz_adamw_step": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_double,
                                       ctypes.c_double, ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double,

@@ -684,6 +684,88 @@ int muz_minmax_fwd(const float* x, const float* y, const float* bias, int32_t M,
                    float* lohi, int32_t* idx, void* stream);
 int muz_minmax_bwd(const float* g, const float* a, const float* b, const float* h, float scale, int32_t scaled,
                    const float* q, const float* lohi, int32_t M, int32_t N, float* dq, void* stream);
+/* Grouped learner gradients (csrc/learner_grad.hip): every weight gradient dW = X^T dZ of one backward, and every
+ * bias / LayerNorm column sum, in two launches instead of one library call each.  Deterministic (fixed
+ * reduction order).  muz_wgrad_grouped: out[K][N] = x[M][K]^T dz[M][N] (row strides ldx, lddz; overwrites out).
+ * muz_colsum_grouped: kind 0 reduces muz_ln_bwd_rows partials (src = scratch, rows = blocks) into out0 = dgamma,
+ * out1 = dbeta, out2 = dbias (any may be null); kind 1 sums the rows of src [rows][ld] into out0 [N]. */
+typedef struct {
+  const float* x;
+  const float* dz;
+  float* out;
+  int32_t M, K, N, ldx, lddz;
+} muz_wgrad_problem;
+typedef struct {
+  const float* src;
+  float* out0;
+  float* out1;
+  float* out2;
+  int32_t kind, rows, N, ld;
+} muz_colsum_problem;
+/* scratch: muz_wgrad_scratch_floats(problems, count) device floats (problems over 2048 rows are split into
+ * 2048-row segments whose partials are added in segment order). */
+int64_t muz_wgrad_scratch_floats(const muz_wgrad_problem* problems, int32_t count);
+int muz_wgrad_grouped(const muz_wgrad_problem* problems, int32_t count, float* scratch, int64_t scratch_floats,
+                      void* stream);
+int muz_colsum_grouped(const muz_colsum_problem* problems, int32_t count, void* stream);
+/* The learner's losses and their gradients w.r.t. the network outputs in ONE launch (csrc/learner_loss.hip):
+ * loss_fn (train_with_reward.py:24-141) and loss_fn_stochastic (train_stochastic.py:34-180) for all K + 1
+ * unroll steps at once.  Rows are step-major (row k B + b = unroll step k of sample b).
+ *   value:  l_v[k] = mean_b m[b][k] (tv[b][k] - value[row])^2                        (rows of K + 1 steps)
+ *   policy: l_p[k] = mean_b m[b][k] * -(pol[b][k] . log_softmax(logits[row]))       (rows of K + 1 steps)
+ *   term j (rows of the first K steps): ce = cross-entropy of logits_j against a class label labels[b][k]
+ *     or a distribution probs[b][k][:]; "rare" rows: label == 1 (rare_not_one = 0), label != 1 (= 1), or a
+ *     distribution not uniform (sum (p - 1/6)^2 > 1e-6); l_j[k] = w_rare S(m r ce) / n_r + w_common
+ *     S(m (1 - r) ce) / n_c with n_r = max(S(m r), 1) and n_c = max(S(m) - S(m r), 1) (norm 0, det's
+ *     _balanced_ce_steps) or max(S(m) - n_r, 1) (norm 1, train_stochastic.py:25-32).
+ * total = scale_value S_k l_v + scale_policy S_k l_p + S_j scale_j S_k l_j.  parts: [total, S l_v, S l_p,
+ * S l_0, S l_1, S l_2] (unused terms 0).  Every d* output receives d total / d input (overwritten).
+ * Deterministic; one workgroup. */
+typedef struct {
+  const float* logits;
+  float* dlogits;
+  const int32_t* labels;   /* [B][ld] (column k) -- or null with probs */
+  const float* probs;      /* [B][ld][ncls] */
+  int32_t ncls, ld, rare_not_one;
+  float w_rare, w_common, scale;
+} muz_loss_term;
+typedef struct {
+  int32_t K, B, A, T;      /* unroll steps, batch, policy width, time stride of masks / target_values / policies */
+  int32_t nterms, norm;    /* CE terms (<= 3), n_common form */
+  const float* masks;      /* [B][T] */
+  const float* target_values;
+  const float* policies;   /* [B][T][A] */
+  const float* value;      /* [(K + 1) B] */
+  const float* logits;     /* [(K + 1) B][A] */
+  float* dvalue;
+  float* dlogits;
+  float scale_value, scale_policy;
+  muz_loss_term term[3];
+  float* parts;            /* [6] */
+  float* total;            /* [1] (= parts[0]; a separate scalar for the autograd node's output) */
+} muz_loss_args;
+int muz_loss_heads(const muz_loss_args* args, void* stream);
+/* One launch per learner layer (csrc/learner_fused.hip): muz_dense_ln_fwd = muz_ln_fwd(x @ W, ...) with the GEMM
+ * fused in (x [M][K], W [K][N] row-major, K <= 512, N in {32, 64, 128, 256}; same outputs out / z / mean / rstd);
+ * muz_dense_ln_bwd = muz_ln_bwd_rows followed by dx = dz W^T (+ acc) (dx [M][K]; dx null: no input gradient),
+ * column partials into scratch [ceil(M / 16)][3][N] (muz_dense_ln_bwd_scratch_floats; any muz_ln_colsum-style
+ * reduction over its rows gives dgamma / dbeta / dbias). */
+int muz_dense_ln_fwd(const float* x, int32_t M, int32_t K, const float* W, const float* WT, int32_t ldt,
+                     const float* bias, const float* gamma, const float* beta, const float* res, int32_t N,
+                     int32_t mode, float* out, float* z, float* mean, float* rstd, void* stream);
+/* WT (optional, used instead of W when given): W^T as [N][ldt], ldt >= K rounded up to 16, a multiple of 4,
+ * columns K .. ldt - 1 zero -- kept per layer by the learner and refreshed by muz_transpose_grouped, which
+ * writes dst[n * ldt + k] = src[k * N + n] for k < K (one launch for all layers). */
+typedef struct {
+  const float* src;
+  float* dst;
+  int32_t K, N, ldt;
+} muz_transpose_problem;
+int muz_transpose_grouped(const muz_transpose_problem* problems, int32_t count, void* stream);
+int64_t muz_dense_ln_bwd_scratch_floats(int32_t M, int32_t N);
+int muz_dense_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
+                     const float* gamma, int32_t M, int32_t N, int32_t mode, const float* W, int32_t K,
+                     const float* acc, float* dz, float* dres, float* dx, float* scratch, void* stream);
 /* 'SAME' Conv1D as a GEMM: the im2col matrix cols [B][W][K x Cin] of x [B][W][Cin] (zero outside each row;
  * tap d reads column w + d - (K - 1) / 2) and its backward dx = sum over taps (fixed order). */
 int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream);

@@ -294,11 +294,14 @@ def test_classic_chain_node_matches_per_step_autograd(cuda):
                          for pre, e in (("act", ea), ("chance", ec))], 1).reshape(2 * K, B, -1) for x in ("scale", "shift")]
     out = L._TrunkChain.apply(lat0, film[0], film[1], 0.5, (0, 1) * K, (False, True) * K, False,
                               *(nets.p[n] for n in names[:2 * L._NP]))
-    g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs)
+    g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs, retain_graph=True)
+    # the per-step graph reads the same FiLM rows (row-wise GEMMs over all steps at once, as loss_fn_stochastic
+    # does): a library GEMM over one step's rows may round differently from the same rows inside K steps
+    # (rocBLAS picks its kernel by shape), and this test is about the chain node, not the FiLM projections
     seq, lat = [], lat0
     for k in range(K):
-        after = nets._film_trunk("act", 0, lat, ea[k * B:(k + 1) * B])
-        nxt = nets._film_trunk("chance", 2, after, ec[k * B:(k + 1) * B])
+        after = nets._film_trunk("act", 0, lat, None, film=(film[0][2 * k], film[1][2 * k]))
+        nxt = nets._film_trunk("chance", 2, after, None, film=(film[0][2 * k + 1], film[1][2 * k + 1]))
         lat = (nxt * 0.5).detach() + nxt * 0.5
         seq += [after, lat]
     ref = torch.stack(seq)
