@@ -3,18 +3,20 @@
 // discount) / loss_fn_stochastic (train_stochastic.py:34-180: chance, discount, reward), all K + 1 unroll
 // steps at once.  As torch ops the same arithmetic was ~120 launches of ~4.5 us (forward + autograd) per step.
 //
-// One workgroup of 16 waves.  A wave takes a 64-row chunk of one unroll step (lane = sample), so every
-// per-step sum is a wave reduction plus a fixed-order sum over the step's chunks (deterministic):
-//   phase 1: per-step mask / rare counts of the CE terms -> the balanced-loss normalisers n_rare, n_common;
-//   phase 2: per row, the losses and their gradients (softmax - target, scaled by the row's weight);
-//   phase 3: per-step sums -> parts and total.
+// One workgroup per unroll step k (256 threads, thread = sample row), so the per-step sums are block
+// reductions in a fixed order (deterministic):
+//   phase 1: step k's mask / rare counts of the CE terms -> the balanced-loss normalisers n_rare, n_common;
+//   phase 2: per row, the losses and their gradients (softmax - target, scaled by the row's weight), with every
+//            load of a row issued before its arithmetic;
+//   phase 3: the step's sums -> partials[k]; the last workgroup to finish (a ticket counter, reset by that
+//            workgroup for the next launch / graph replay) adds the K + 1 partials in step order into the parts.
+// (Round 3's first version ran all steps in one workgroup: 70 us of serial memory latency.)
 #include "launch.hpp"
 
 namespace muz {
 
-constexpr int kLossThreads = 1024;
+constexpr int kLossThreads = 256;
 constexpr int kLossWaves = kLossThreads / 64;
-constexpr int kLossMaxChunks = 1024;
 constexpr int kLossMaxK = 64;
 
 __device__ __forceinline__ float wave_sum_f(float v) {
@@ -78,96 +80,110 @@ __device__ __forceinline__ float loss_ce_row(const float* __restrict__ l, float*
   return ce;
 }
 
+// a load that sees other workgroups' stores after their fence (relaxed atomic: not served from a stale L1 line)
+__device__ __forceinline__ float ld_coherent(const float* p) {
+  return __builtin_bit_cast(float, __atomic_load_n(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED));
+}
+
+// fixed-order block sum of NV values (every thread passes its own; the result is valid in every thread)
+template <int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float (*red)[NV]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const float s = wave_sum_f(v[q]);
+    if (lane == 0) red[wv][q] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    float s = red[0][q];
+#pragma unroll
+    for (int w = 1; w < kLossWaves; ++w) s += red[w][q];
+    v[q] = s;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kLossThreads) void k_loss_heads(muz_loss_args g) {
-  __shared__ float part[kLossMaxChunks][5];
-  __shared__ float cnt[kLossMaxK][4];
-  __shared__ float sk[kLossMaxK + 1][5];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, tid = threadIdx.x;
-  const int K = g.K, B = g.B, nch = (B + 63) / 64, nt = g.nterms;
-  // phase 1: S(m), S(m r_j) per (step, chunk) of the first K steps
-  for (int i = wv; i < K * nch; i += kLossWaves) {
-    const int k = i / nch, b = (i % nch) * 64 + lane;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (b < B) {
+  __shared__ float red4[kLossWaves][4];
+  __shared__ float red5[kLossWaves][5];
+  __shared__ int last;
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const int K = g.K, B = g.B, nt = g.nterms;
+  // phase 1: S(m), S(m r_j) of step k (the CE terms cover the first K steps)
+  float cnt[4] = {0.f, 0.f, 0.f, 0.f};
+  if (k < K) {
+    for (int b = tid; b < B; b += kLossThreads) {
       const float m = g.masks[(size_t)b * g.T + k];
-      v[0] = m;
+      cnt[0] += m;
 #pragma unroll
       for (int j = 0; j < 3; ++j)      // (static term indices: the term fields stay in scalar registers)
-        if (j < nt) v[1 + j] = loss_rare(g.term[j], b, k) ? m : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float s = wave_sum_f(v[q]);
-      if (lane == 0) part[i][q] = s;
+        if (j < nt) cnt[1 + j] += loss_rare(g.term[j], b, k) ? m : 0.f;
     }
   }
-  __syncthreads();
-  if (tid < K * 4) {
-    const int k = tid / 4, q = tid % 4;
-    float s = 0.f;
-    for (int c = 0; c < nch; ++c) s += part[k * nch + c][q];
-    cnt[k][q] = s;
-  }
-  __syncthreads();
+  block_sum<4>(cnt, red4);
   // phase 2: per row, losses (weighted) and gradients
   const float invB = 1.0f / (float)B;
-  for (int i = wv; i < (K + 1) * nch; i += kLossWaves) {
-    const int k = i / nch, b = (i % nch) * 64 + lane;
-    float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    if (b < B) {
-      const size_t row = (size_t)k * B + b;
-      const float m = g.masks[(size_t)b * g.T + k];
-      const float d = g.value[row] - g.target_values[(size_t)b * g.T + k];
-      v[0] = m * d * d;
-      g.dvalue[row] = g.scale_value * invB * m * 2.0f * d;
-      v[1] = m * loss_ce_row<kLossMaxA>(g.logits + row * g.A, g.dlogits + row * g.A, g.A, -1,
-                             g.policies + ((size_t)b * g.T + k) * g.A, g.scale_policy * invB * m);
-      if (k < K) {
+  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int b = tid; b < B; b += kLossThreads) {
+    const size_t row = (size_t)k * B + b;
+    const float m = g.masks[(size_t)b * g.T + k];
+    const float val = g.value[row], tv = g.target_values[(size_t)b * g.T + k];
+    int lab[3] = {-1, -1, -1};
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          if (j >= nt) break;
-          const muz_loss_term& t = g.term[j];
-          const float nr = fmaxf(cnt[k][1 + j], 1.f);
-          const float nc = fmaxf(cnt[k][0] - (g.norm ? nr : cnt[k][1 + j]), 1.f);
-          const bool r = loss_rare(t, b, k);
-          const float w = m * (r ? t.w_rare / nr : t.w_common / nc);
-          const int lab = t.labels ? t.labels[(size_t)b * t.ld + k] : -1;
-          const float* tg = t.labels ? nullptr : t.probs + ((size_t)b * t.ld + k) * t.ncls;
-          v[2 + j] = w * loss_ce_row<kLossMaxCls>(t.logits + row * t.ncls, t.dlogits + row * t.ncls, t.ncls, lab, tg, t.scale * w);
-        }
+    for (int j = 0; j < 3; ++j)
+      if (j < nt && k < K && g.term[j].labels) lab[j] = g.term[j].labels[(size_t)b * g.term[j].ld + k];
+    const float d = val - tv;
+    v[0] = m * d * d;
+    g.dvalue[row] = g.scale_value * invB * m * 2.0f * d;
+    v[1] = m * loss_ce_row<kLossMaxA>(g.logits + row * g.A, g.dlogits + row * g.A, g.A, -1,
+                                      g.policies + ((size_t)b * g.T + k) * g.A, g.scale_policy * invB * m);
+    if (k < K) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if (j >= nt) break;
+        const muz_loss_term& t = g.term[j];
+        const float nr = fmaxf(cnt[1 + j], 1.f);
+        const float nc = fmaxf(cnt[0] - (g.norm ? nr : cnt[1 + j]), 1.f);
+        const bool r = t.labels ? (t.rare_not_one ? lab[j] != 1 : lab[j] == 1) : loss_rare(t, b, k);
+        const float w = m * (r ? t.w_rare / nr : t.w_common / nc);
+        const float* tg = t.labels ? nullptr : t.probs + ((size_t)b * t.ld + k) * t.ncls;
+        v[2 + j] += w * loss_ce_row<kLossMaxCls>(t.logits + row * t.ncls, t.dlogits + row * t.ncls, t.ncls, lab[j],
+                                                 tg, t.scale * w);
       }
     }
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      const float s = wave_sum_f(v[q]);
-      if (lane == 0) part[i][q] = s;
-    }
   }
-  __syncthreads();
-  // phase 3: per-step sums, then the parts in step order
-  if (tid < (K + 1) * 5) {
-    const int k = tid / 5, q = tid % 5;
-    float s = 0.f;
-    for (int c = 0; c < nch; ++c) s += part[k * nch + c][q];
-    sk[k][q] = s;
-  }
-  __syncthreads();
+  block_sum<5>(v, red5);
+  // phase 3: this step's sums; the last workgroup adds all steps in order
   if (tid == 0) {
-    float lv = 0.f, lp = 0.f, lt[3] = {0.f, 0.f, 0.f}, total = 0.f;
-    for (int k = 0; k <= K; ++k) {
-      const float v = sk[k][0] * invB, p = sk[k][1] * invB;
-      lv += v;
-      lp += p;
-      total += g.scale_value * v + g.scale_policy * p;
-    }
-    for (int j = 0; j < nt; ++j) {
-      for (int k = 0; k < K; ++k) lt[j] += sk[k][2 + j];
-      total += g.term[j].scale * lt[j];
-    }
-    float* o = g.parts;
-    *g.total = total;
-    o[0] = total, o[1] = lv, o[2] = lp, o[3] = lt[0], o[4] = lt[1], o[5] = lt[2];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) g.partials[5 * k + q] = v[q];
+    __threadfence();
+    last = atomicAdd(g.ticket, 1) == K;
   }
+  __syncthreads();
+  if (!last || tid != 0) return;
+  __threadfence();
+  float lv = 0.f, lp = 0.f, lt[3] = {0.f, 0.f, 0.f}, total = 0.f;
+  for (int kk = 0; kk <= K; ++kk) {
+    const float* pk = g.partials + 5 * kk;
+    const float a = ld_coherent(pk) * invB, p = ld_coherent(pk + 1) * invB;
+    lv += a;
+    lp += p;
+    total += g.scale_value * a + g.scale_policy * p;
+    if (kk < K) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) lt[j] += ld_coherent(pk + 2 + j);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    if (j < nt) total += g.term[j].scale * lt[j];
+  float* o = g.parts;
+  *g.total = total;
+  o[0] = total, o[1] = lv, o[2] = lp, o[3] = lt[0], o[4] = lt[1], o[5] = lt[2];
+  *g.ticket = 0;     // ready for the next launch (or graph replay)
 }
 
 }  // namespace muz
@@ -179,12 +195,13 @@ extern "C" int muz_loss_heads(const muz_loss_args* args, void* stream) {
   const muz_loss_args& a = *args;
   MUZ_HOST_CHECK(a.K >= 0 && a.B > 0 && a.A > 0 && a.T >= a.K + 1 && a.nterms >= 0 && a.nterms <= 3);
   MUZ_HOST_CHECK(a.masks && a.target_values && a.policies && a.value && a.logits && a.dvalue && a.dlogits && a.parts && a.total);
-  if (a.K > kLossMaxK || (a.K + 1) * ((a.B + 63) / 64) > kLossMaxChunks || a.A > kLossMaxA) return MUZ_E_UNSUPPORTED;
+  if (a.K > kLossMaxK || a.A > kLossMaxA) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(a.partials && a.ticket);
   for (int j = 0; j < a.nterms; ++j) {
     const muz_loss_term& t = a.term[j];
     if (t.ncls > kLossMaxCls) return MUZ_E_UNSUPPORTED;
     MUZ_HOST_CHECK(t.logits && t.dlogits && t.ncls > 0 && t.ld >= a.K && (t.labels != nullptr) != (t.probs != nullptr));
   }
-  k_loss_heads<<<1, kLossThreads, 0, (hipStream_t)stream>>>(a);
+  k_loss_heads<<<a.K + 1, kLossThreads, 0, (hipStream_t)stream>>>(a);
   return muz_last_launch_error();
 }

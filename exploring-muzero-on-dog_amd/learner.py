@@ -749,6 +749,19 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     return total, (l_value.sum(), l_policy.sum(), l_disc.sum(), l_rew.sum())
 
 
+_TICKETS = {}
+
+
+def _loss_ticket(dev):
+    """The loss kernel's last-workgroup counter: zero between launches (the kernel resets it), one per device and
+    stream (launches on one stream are ordered; kept alive, so a captured graph replays with the same one)."""
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    t = _TICKETS.get(key)
+    if t is None:
+        t = _TICKETS[key] = torch.zeros((1,), dtype=torch.int32, device=dev)
+    return t
+
+
 class _LossHeads(torch.autograd.Function):
     """All losses of one unrolled batch and their gradients w.r.t. the network outputs as ONE launch
     (csrc/learner_loss.hip: muz_loss_heads; ~120 torch launches forward + backward before).  Forward computes
@@ -795,7 +808,9 @@ class _LossHeads(torch.autograd.Function):
             q.rare_not_one, q.w_rare, q.w_common, q.scale = int(rare_not_one), w_rare, w_common, scale
         parts = torch.empty((6,), dtype=dt, device=dev)
         total = torch.empty((), dtype=dt, device=dev)
-        a.parts, a.total = parts.data_ptr(), total.data_ptr()
+        partials = torch.empty((5 * (K + 1),), dtype=dt, device=dev)
+        a.parts, a.total, a.partials, a.ticket = parts.data_ptr(), total.data_ptr(), partials.data_ptr(), \
+            _loss_ticket(dev).data_ptr()
         _L.check(_L.load().muz_loss_heads(ctypes.byref(a), _L.stream_ptr()), "muz_loss_heads")
         ctx.d = (dlogits, dvalue, *dts)
         ctx.present = tuple(t is not None for t in (t0, t1, t2))

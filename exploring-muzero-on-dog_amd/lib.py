@@ -55,7 +55,7 @@ class MuzLossArgs(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int32) for k in ("K", "B", "A", "T", "nterms", "norm")] + \
         [(k, vp) for k in ("masks", "target_values", "policies", "value", "logits", "dvalue", "dlogits")] + \
         [("scale_value", ctypes.c_float), ("scale_policy", ctypes.c_float), ("term", MuzLossTerm * 3),
-         ("parts", vp), ("total", vp)]
+         ("parts", vp), ("total", vp), ("partials", vp), ("ticket", vp)]
 
 
 class MuzRules(ctypes.Structure):

@@ -720,7 +720,7 @@ int muz_colsum_grouped(const muz_colsum_problem* problems, int32_t count, void* 
  *     _balanced_ce_steps) or max(S(m) - n_r, 1) (norm 1, train_stochastic.py:25-32).
  * total = scale_value S_k l_v + scale_policy S_k l_p + S_j scale_j S_k l_j.  parts: [total, S l_v, S l_p,
  * S l_0, S l_1, S l_2] (unused terms 0).  Every d* output receives d total / d input (overwritten).
- * Deterministic; one workgroup. */
+ * Deterministic; one workgroup per unroll step. */
 typedef struct {
   const float* logits;
   float* dlogits;
@@ -743,6 +743,8 @@ typedef struct {
   muz_loss_term term[3];
   float* parts;            /* [6] */
   float* total;            /* [1] (= parts[0]; a separate scalar for the autograd node's output) */
+  float* partials;         /* scratch [(K + 1) * 5] */
+  int32_t* ticket;         /* a device counter, 0 before the launch (the kernel leaves it 0 again) */
 } muz_loss_args;
 int muz_loss_heads(const muz_loss_args* args, void* stream);
 /* One launch per learner layer (csrc/learner_fused.hip): muz_dense_ln_fwd = muz_ln_fwd(x @ W, ...) with the GEMM
