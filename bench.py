@@ -328,26 +328,37 @@ def dog_cpu_baseline(seconds, lanes=8):
 
 
 # k_dog_play's per-turn critical path, measured with the stamp build (profiles/diag_dog_stamps.py,
-# profiles/r2_dog_stamps.log): thread 0 of each game's workgroup, cycles per game-turn by phase.
-DOG_PHASES = {"reset check / restart": 4478, "base checks + barrier": 9640, "mask words + choice": 3860,
-              "env_step (lane 0)": 8708, "barrier": 277, "deal": 1623}
+# profiles/r3_dog_stamps.log: 256-thread workgroup, wave priority on): thread 0 of each game's workgroup,
+# shader-clock ticks per game-turn by phase (relative shares; the stamps themselves add ~10 %).
+DOG_PHASES = {"reset check / restart": 408, "base checks + barrier": 6700, "mask words + choice": 1960,
+              "env_step (lane 0)": 4626, "barrier": 98, "deal": 1486}
+# the phases a fully parallel turn keeps: the 448-thread base checks and their barrier, the one-wave action
+# choice, the turn-end barrier and the (already wave-parallel) deal; lane 0's env_step and the reset check are
+# the serial remainder a faster kernel would remove
+DOG_IRREDUCIBLE = ("base checks + barrier", "mask words + choice", "barrier", "deal")
 
 
 def dog_latency_model(avg_ms, games, turns, launch_bytes):
-    """Config (d)'s roofline is a latency model, not a bandwidth fraction: each game is one workgroup whose
+    """Config (d)'s roofline is a latency bound, not a bandwidth fraction: each game is one workgroup whose
     turn is a serial chain (checks -> barrier -> choice -> one-lane env_step -> barrier -> deal); all games
     are resident at once (4 workgroups of 7 waves per CU), so a launch takes about one chain per turn.
-    `frac` = the share of the chain that is single-lane serial work (env_step), the part a faster kernel
-    would have to parallelise; HBM traffic is negligible (bytes_per_launch / launch time)."""
+    `achieved` = measured us per game-turn; `peak` = the lower bound of that chain once lane 0's env_step
+    and the reset check are fully parallelised (the irreducible phases' share of the stamp-build turn applied
+    to the measured turn); frac = peak / achieved (time-like: 1.0 = nothing left to parallelise).  HBM
+    traffic is negligible (bytes_per_launch / launch time)."""
     tot = sum(DOG_PHASES.values())
     us_per_turn = avg_ms * 1e3 / turns
+    share = sum(DOG_PHASES[k] for k in DOG_IRREDUCIBLE) / tot
+    floor_us = us_per_turn * share
     return {"bound": "latency", "kernel": "k_dog_play", "unit": "us/game-turn", "achieved": round(us_per_turn, 3),
-            "peak": None, "frac": round(DOG_PHASES["env_step (lane 0)"] / tot, 4),
+            "peak": round(floor_us, 3), "frac": round(share, 4),
+            "ceiling": "per-turn chain without its serial part: " + " + ".join(DOG_IRREDUCIBLE),
             "phase_share": {k: round(v / tot, 4) for k, v in DOG_PHASES.items()},
-            "phase_cycles_per_turn_stamp_build": DOG_PHASES, "games_resident": games, "avg_launch_ms": round(avg_ms, 5),
+            "phase_ticks_per_turn_stamp_build": DOG_PHASES, "games_resident": games, "avg_launch_ms": round(avg_ms, 5),
             "hbm_gbs": round(launch_bytes / (avg_ms * 1e-3) / 1e9, 2), "traffic": None,
-            "note": "per-phase cycles from the stamp build (profiles/r2_dog_stamps.log; stamps add ~11 %); "
-                    "PMC of r1c: waves wait 86 % of their cycles, VALU issue 4 %"}
+            "note": "per-phase shares from the stamp build (profiles/r3_dog_stamps.log); r3: 4-wave workgroups "
+                    "(no register spills; 6.81 -> 6.17 us/turn) and the turn's serial part at raised wave priority "
+                    "(6.95 -> 6.68 us/turn at 7 waves), profiles/r3_dog_prio_ab.log"}
 
 
 def run_dog(args):

@@ -6,10 +6,16 @@
 namespace muz {
 
 constexpr int kDogGamesPerBlock = 4;   // wave-per-game kernels (reset, explicit-action step)
-#ifndef MUZ_DOG_WPE
-#define MUZ_DOG_WPE 8      // waves per SIMD the play kernel is budgeted for: 4 blocks of 7 waves per CU (measured best)
-#endif
 constexpr int kDogBlockThreads = 448;  // block-per-game kernels: 7 waves = 4 swap, 2 hot-7, 1 normal/-4 checks
+// k_dog_play's workgroup: 4 waves, each running the checks of two of the 7 check waves above in turn.  At
+// 1024 games per GPU (4 workgroups per CU) that is 4 waves per SIMD with 128 VGPRs each; with 7 waves per game
+// the 8-wave budget left 64 VGPRs, and the kernel spilled 45 VGPRs (and 240 SGPRs through VGPR lanes) to
+// scratch, which the serial part of every turn (lane 0's env_step) paid in memory latency.
+#ifndef MUZ_DOG_PLAY_THREADS
+#define MUZ_DOG_PLAY_THREADS 256
+#endif
+constexpr int kDogPlayThreads = MUZ_DOG_PLAY_THREADS;
+constexpr int kDogPlayWPE = kDogPlayThreads == 448 ? 8 : 4;   // waves per SIMD the play kernel is budgeted for
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -23,6 +29,10 @@ struct WaveSync {   // one wavefront owns the game
 };
 struct BlockSync {  // a whole workgroup owns the game
   static constexpr int N = kDogBlockThreads;
+  __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+struct PlaySync {   // k_dog_play's workgroup owns the game
+  static constexpr int N = kDogPlayThreads;
   __device__ __forceinline__ void operator()() const { __syncthreads(); }
 };
 
@@ -464,17 +474,22 @@ __device__ __forceinline__ void dog_checks_block(const DetConsts& c, DogG& s, in
 // gated by the hand right here (two ballots), so the legal set is 14 slot-ordered words (wj then wr) in
 // LDS instead of the 806-bit mask.  Slot order is base order, so the k-th set bit over wj[0..6], wr[0..6]
 // is the k-th legal action in action order (joker copies [0, 396) before real copies [396, 792)).
+// (thread t of an NTH-thread workgroup takes check threads t, t + NTH, ... of the 448; NTH a multiple of 64, so
+// each pass is whole waves and the ballots stay per check wave)
+template <int NTH = kDogBlockThreads>
 __device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int tid) {
   if (s.phase == 0) {
     const int cp = dog_sub(c, s);
-    const int i = dog_check_of(tid);
     const bool hj = s.hands[cp][0] > 0;
-    const bool hr = i >= 0 && s.hands[cp][dog_base_card(i)] > 0;
-    const bool v = i >= 0 && (hj || hr) && dog_base_valid(c, s, cp, i);
-    const unsigned long long bj = __ballot(v && hj), br = __ballot(v && hr);
-    if ((tid & 63) == 0) {
-      s.wj[tid >> 6] = bj;
-      s.wr[tid >> 6] = br;
+    for (int vt = tid; vt < kDogBlockThreads; vt += NTH) {
+      const int i = dog_check_of(vt);
+      const bool hr = i >= 0 && s.hands[cp][dog_base_card(i)] > 0;
+      const bool v = i >= 0 && (hj || hr) && dog_base_valid(c, s, cp, i);
+      const unsigned long long bj = __ballot(v && hj), br = __ballot(v && hr);
+      if ((vt & 63) == 0) {
+        s.wj[vt >> 6] = bj;
+        s.wr[vt >> 6] = br;
+      }
     }
   }
   __syncthreads();
@@ -634,6 +649,10 @@ __device__ unsigned long long g_dog_stamps[8];
 // (dog_reset_lds, deal counter continued) and keeps playing.  env_steps[g] (optional) accumulates the
 // turns played and episodes[g] (optional) the games finished; action / reward / done (optional) are
 // those of the last turn.
+#ifndef MUZ_DOG_PRIO
+#define MUZ_DOG_PRIO 1
+#endif
+
 struct DogPlayArgs {
   DetConsts c;
   muz_dog_soa st;
@@ -651,7 +670,7 @@ struct DogPlayArgs {
 // loads, the pointer laundered at each use), so the rule constants and the SoA pointers are reloaded where
 // they are needed instead of being held live across the turn loop -- at the 64-VGPR budget that kept
 // state spilled SGPRs into VGPR lanes and VGPRs into scratch.
-__global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_eu(MUZ_DOG_WPE))) void k_dog_play(
+__global__ __launch_bounds__(kDogPlayThreads) __attribute__((amdgpu_waves_per_eu(kDogPlayWPE))) void k_dog_play(
     DogPlayArgs args) {
   (void)args;
   __shared__ DogG s;
@@ -665,7 +684,7 @@ __global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_e
     }
     return;
   }
-  dog_load<BlockSync>(A().c, A().st, g, s, tid);
+  dog_load<PlaySync>(A().c, A().st, g, s, tid);
   const int nturns = A().nturns;
   int played = 0, finished = 0, a = -2, r = 0;
   DOG_STAMP_INIT();
@@ -681,12 +700,16 @@ __global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_e
       if (!P.auto_reset) break;
       const unsigned deal = s.deal;
       __syncthreads();
-      dog_reset_lds<BlockSync>(c, s, P.seed, g, deal, tid);
+      dog_reset_lds<PlaySync>(c, s, P.seed, g, deal, tid);
     }
     DOG_STAMP(0);   // reset
-    dog_checks_play(c, s, tid);
+    dog_checks_play<kDogPlayThreads>(c, s, tid);
     DOG_STAMP(1);   // base checks (+ barrier)
     if (tid < 64) {
+      // the turn's serial part (choice, lane 0's env_step) runs at raised wave priority: the CU's other
+      // workgroups are in their VALU-heavy check phases meanwhile, and without it this wave got a small share
+      // of the SIMD's issue slots
+      if (MUZ_DOG_PRIO) __builtin_amdgcn_s_setprio(2);
       int nleg = 0;
       a = dog_pick(s, random_action_uniform(P.seed, g, P.turn0 + t), tid, &nleg);
       DOG_STAMP(2);   // action choice
@@ -708,17 +731,18 @@ __global__ __launch_bounds__(kDogBlockThreads) __attribute__((amdgpu_waves_per_e
         }
       }
       DOG_STAMP(3);   // env_step / no_step (lane 0)
+      if (MUZ_DOG_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     ++played;
     __syncthreads();
     DOG_STAMP(4);   // barrier
-    if (s.need_deal) dog_deal<BlockSync>(c, s, P.seed, g, tid);
+    if (s.need_deal) dog_deal<PlaySync>(c, s, P.seed, g, tid);
     DOG_STAMP(5);   // deal
     finished += s.done;
   }
   DOG_STAMP_END();
   const DogPlayArgs& P = A();
-  dog_store<BlockSync>(P.c, P.st, g, s, tid);
+  dog_store<PlaySync>(P.c, P.st, g, s, tid);
   if (tid == 0) {
     if (P.action_out) P.action_out[g] = a;
     if (P.reward) P.reward[g] = (int8_t)r;
@@ -912,7 +936,7 @@ int muz_dog_step_move(const muz_rules* rules, muz_dog_soa st, const int32_t* kin
 int muz_dog_random_turn(const muz_rules* rules, muz_dog_soa st, uint64_t seed, int32_t turn, int32_t* action,
                         int8_t* reward, uint8_t* done, int32_t n, void* stream) {
   DOG_PROLOGUE(true)
-  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(
+  k_dog_play<<<n, kDogPlayThreads, 0, (hipStream_t)stream>>>(
       DogPlayArgs{c, st, seed, turn, 1, 0, action, reward, done, nullptr, nullptr});
   return muz_last_launch_error();
 }
@@ -921,7 +945,7 @@ int muz_dog_random_play(const muz_rules* rules, muz_dog_soa st, uint64_t seed, i
                         int32_t auto_reset, uint32_t* env_steps, uint32_t* episodes, int32_t n, void* stream) {
   DOG_PROLOGUE(nturns >= 0)
   if (nturns == 0) return MUZ_OK;
-  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(
+  k_dog_play<<<n, kDogPlayThreads, 0, (hipStream_t)stream>>>(
       DogPlayArgs{c, st, seed, turn0, nturns, auto_reset ? 1 : 0, nullptr, nullptr, nullptr, env_steps, episodes,
                   muz_dog_traj{}});
   return muz_last_launch_error();
@@ -933,7 +957,7 @@ int muz_dog_random_play_record(const muz_rules* rules, muz_dog_soa st, uint64_t 
   DOG_PROLOGUE(nturns >= 0)
   MUZ_HOST_CHECK(rec.act && rec.player && rec.reward && rec.legal && rec.done && rec.idx && rec.max_steps > 0);
   if (nturns == 0) return MUZ_OK;
-  k_dog_play<<<n, kDogBlockThreads, 0, (hipStream_t)stream>>>(
+  k_dog_play<<<n, kDogPlayThreads, 0, (hipStream_t)stream>>>(
       DogPlayArgs{c, st, seed, turn0, nturns, auto_reset ? 1 : 0, nullptr, nullptr, nullptr, env_steps, episodes, rec});
   return muz_last_launch_error();
 }
