@@ -85,6 +85,8 @@ def parse():
                          "(pipeline.run_overlapped; weights one iteration staler than the reference's loop)")
     ap.add_argument("--workload", choices=("det", "classic", "dog", "train", "env", "selftest"), default="det",
                     help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
+    ap.add_argument("--env-variant", type=int, choices=(0, 1, 2), default=0,
+                    help="env workload: 0 = kernel by batch size, 1 = one game per lane, 2 = one game per 32 lanes")
     ap.add_argument("--records", action="store_true",
                     help="dog: record every turn (muz_dog_random_play_record), pack the records each step and gather "
                          "them to rank 0 (RCCL point-to-point at N > 1) inside the timed region -- config (d) as "
@@ -714,6 +716,7 @@ def run_train(args):
 
 
 ENV_ROUNDS_PER_STEP = 100      # --workload env: one bench step = 100 random-play env rounds (one launch each)
+ENV_WIDE_MAX_GAMES = 1 << 16   # csrc/env_detmadn.hip kWideMaxGames: up to here one game per 32 lanes
 ENV_PREROLL = 300              # rounds played before warm-up: games spread over 0..300 plies (SURVEY §8(d)(b'))
 
 
@@ -746,7 +749,7 @@ def run_env(args):
         for i in range(R):
             if ev is not None:
                 ev[2 * (k * R + i)].record()
-            E.random_round(env, legal, seed, turn[0], obs=obs, reward=reward, done=done)
+            E.random_round(env, legal, seed, turn[0], obs=obs, reward=reward, done=done, variant=args.env_variant)
             if ev is not None:
                 ev[2 * (k * R + i) + 1].record()
             turn[0] += 1
@@ -765,6 +768,8 @@ def run_env(args):
         return
     avg_ms = lms / (R * args.steps * world)
     per = env_bytes_per_step(PLAYERS)
+    wide = args.env_variant == 2 or (args.env_variant == 0 and B <= ENV_WIDE_MAX_GAMES)
+    kernel = "k_det_round_wide" if wide else "k_det_round"
     achieved = B * per / (avg_ms * 1e-3) / 1e9
     out = {
         "metric": "env-only steps/sec (step + legal + encode), det-MADN 2p random legal play (SURVEY 8(d)(b'))",
@@ -775,8 +780,8 @@ def run_env(args):
         "config": {"workload": f"det-MADN {PLAYERS}p env rounds: {B} games/GPU, {R} rounds per step, each one "
                                f"muz_detmadn_random_round launch (legal -> random legal action -> env_step / no_step "
                                f"-> reset finished -> next legal + int8 obs), after {ENV_PREROLL} pre-roll rounds",
-                   "games_per_gpu": B, "rounds_per_step": R, "parallelism": parallelism(args, world)},
-        "roofline": {"bound": "hbm", "kernel": "k_det_round", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                   "games_per_gpu": B, "rounds_per_step": R, "kernel": kernel, "parallelism": parallelism(args, world)},
+        "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "avg_launch_ms": round(avg_ms, 5),
                      "bytes_per_env_step": per, "bytes_per_launch": B * per, "traffic": None},
     }

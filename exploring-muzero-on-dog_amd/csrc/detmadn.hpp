@@ -108,65 +108,83 @@ __device__ __forceinline__ bool goal_path_free(const DetConsts& c, const BoardVi
   return ok;
 }
 
-// valid_action (deterministic_madn.py:299-393) -> 24-bit mask, bit pin*6 + (move-1).
-__device__ __forceinline__ uint32_t det_legal(const DetConsts& c, const DetLane& s, const BoardView& b) {
-  const uint32_t F = c.flags;
-  const int cp0 = s.cp;
-  const int cp = sub_player(c, b, cp0);
-  const int tgt = cst(c.target, cp);
-  const int g0 = goal_of(c, cp, 0), g3 = goal_of(c, cp, 3);
-  const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
-  const int start_cp = cst(c.start, cp);
-  const bool home_ok = b.at(start_cp) != cp0;   // compares the UNSUBSTITUTED player (line 390)
+// valid_action (deterministic_madn.py:299-393), split into the per-state prelude (LegalCtx) and the check of one
+// (pin i, move m) (legal_one): det_legal runs all 24 checks in one lane, k_det_round_wide one check per lane.
+struct LegalCtx {
+  int cp0, cp, tgt, g0, g3, mt, start_cp;
+  bool home_ok;
   bool pos[4];
+  uint32_t avail;   // moves m with action_set[cp][m-1] > 0, bit m-1
+};
+__device__ __forceinline__ LegalCtx legal_ctx(const DetConsts& c, const DetLane& s, const BoardView& b) {
+  LegalCtx x;
+  const uint32_t F = c.flags;
+  x.cp0 = s.cp;
+  x.cp = sub_player(c, b, x.cp0);
+  x.tgt = cst(c.target, x.cp);
+  x.g0 = goal_of(c, x.cp, 0);
+  x.g3 = goal_of(c, x.cp, 3);
+  x.mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
+  x.start_cp = cst(c.start, x.cp);
+  x.home_ok = b.at(x.start_cp) != x.cp0;   // compares the UNSUBSTITUTED player (line 390)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) pos[q] = (q < c.P) ? (b.at(cst(c.start, q)) == q) : false;
-  uint32_t avail = 0;
+  for (int q = 0; q < 4; ++q) x.pos[q] = (q < c.P) ? (b.at(cst(c.start, q)) == q) : false;
+  x.avail = 0;
 #pragma unroll
-  for (int m = 0; m < 6; ++m) avail |= (aset_of(s, cp, m) > 0) ? (1u << m) : 0u;
-
+  for (int m = 0; m < 6; ++m) x.avail |= (aset_of(s, x.cp, m) > 0) ? (1u << m) : 0u;
+  return x;
+}
+// the rule checks of pin i (current cell `cur`) with move m, before the action-set gate
+__device__ __forceinline__ bool legal_one(const DetConsts& c, const BoardView& b, const LegalCtx& x, int cur, int m) {
+  const uint32_t F = c.flags;
+  const int cp = x.cp, tgt = x.tgt, mt = x.mt;
+  const bool in_goal = (cur == goal_of(c, cp, 0)) | (cur == goal_of(c, cp, 1)) | (cur == goal_of(c, cp, 2)) |
+                       (cur == goal_of(c, cp, 3));
+  const int nsb = fmodp(fdiv(cur, kDist) + 1, c.P);
+  bool res;
+  if (cur == -1) {
+    res = (m == 6 || (m == 1 && has(F, R_START_ON_1))) && x.home_ok;
+  } else {
+    const int moved = cur + m;
+    const int fitted = fmodp(moved, kTrack);
+    int xx = moved - tgt - mt;
+    res = (b.at(fitted) != cp) || has(F, R_FRIENDLY);
+    const int nsa = fdiv(fitted, kDist);
+    const int nsa_j = jidx(nsa, c.P);
+    const bool trav = cst(c.start, jidx(nsb, c.P)) == cst(c.start, nsa_j);
+    const bool pos_a = x.pos[0] & (nsa_j == 0) | x.pos[1] & (nsa_j == 1) | x.pos[2] & (nsa_j == 2) |
+                       x.pos[3] & (nsa_j == 3);
+    if (has(F, R_START_BLOCK) && trav) res = (!pos_a || cur == x.start_cp) && res;
+    if (mt && has(F, R_START_BLOCK) && trav && pos_a) xx = 0;
+    if (!has(F, R_CIRCULAR) && cur <= tgt && (xx > 4 || (xx == 0 && mt))) res = false;
+    if (4 >= xx && xx > 0 && cur <= tgt) {
+      const bool A = has(F, R_CIRCULAR) && res;
+      const bool B = b.at(goal_of(c, cp, jidx(xx - 1, 4))) != cp;
+      const bool C = has(F, R_JUMP_GOAL) || goal_path_free(c, b, cp, -1, xx);
+      res = A || (B && C);
+    }
+    if (in_goal) {
+      const bool D = has(F, R_JUMP_GOAL) || goal_path_free(c, b, cp, cur - x.g0, moved - x.g0 + 1);
+      res = (moved <= x.g3) && (b.at(jidx(moved, kCells)) != cp) && D;
+    }
+  }
+  return res;
+}
+// -> 24-bit mask, bit pin*6 + (move-1)
+__device__ __forceinline__ uint32_t det_legal(const DetConsts& c, const DetLane& s, const BoardView& b) {
+  const LegalCtx x = legal_ctx(c, s, b);
   uint32_t mask = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int cur = pin_of(s, cp, i);
-    const bool in_goal = (cur == goal_of(c, cp, 0)) | (cur == goal_of(c, cp, 1)) | (cur == goal_of(c, cp, 2)) |
-                         (cur == goal_of(c, cp, 3));
-    const int nsb = fmodp(fdiv(cur, kDist) + 1, c.P);
+    const int cur = pin_of(s, x.cp, i);
 #pragma unroll
-    for (int m = 1; m <= 6; ++m) {
-      bool res;
-      if (cur == -1) {
-        res = (m == 6 || (m == 1 && has(F, R_START_ON_1))) && home_ok;
-      } else {
-        const int moved = cur + m;
-        const int fitted = fmodp(moved, kTrack);
-        int x = moved - tgt - mt;
-        res = (b.at(fitted) != cp) || has(F, R_FRIENDLY);
-        const int nsa = fdiv(fitted, kDist);
-        const int nsa_j = jidx(nsa, c.P);
-        const bool trav = cst(c.start, jidx(nsb, c.P)) == cst(c.start, nsa_j);
-        const bool pos_a = pos[0] & (nsa_j == 0) | pos[1] & (nsa_j == 1) | pos[2] & (nsa_j == 2) | pos[3] & (nsa_j == 3);
-        if (has(F, R_START_BLOCK) && trav) res = (!pos_a || cur == start_cp) && res;
-        if (mt && has(F, R_START_BLOCK) && trav && pos_a) x = 0;
-        if (!has(F, R_CIRCULAR) && cur <= tgt && (x > 4 || (x == 0 && mt))) res = false;
-        if (4 >= x && x > 0 && cur <= tgt) {
-          const bool A = has(F, R_CIRCULAR) && res;
-          const bool B = b.at(goal_of(c, cp, jidx(x - 1, 4))) != cp;
-          const bool C = has(F, R_JUMP_GOAL) || goal_path_free(c, b, cp, -1, x);
-          res = A || (B && C);
-        }
-        if (in_goal) {
-          const bool D = has(F, R_JUMP_GOAL) || goal_path_free(c, b, cp, cur - g0, moved - g0 + 1);
-          res = (moved <= g3) && (b.at(jidx(moved, kCells)) != cp) && D;
-        }
-      }
-      if (res) mask |= 1u << (i * 6 + (m - 1));
-    }
+    for (int m = 1; m <= 6; ++m)
+      if (legal_one(c, b, x, cur, m)) mask |= 1u << (i * 6 + (m - 1));
   }
   // & valid_actions (action_set > 0) per move column
   uint32_t col = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) col |= avail << (i * 6);
+  for (int i = 0; i < 4; ++i) col |= x.avail << (i * 6);
   return mask & col;
 }
 

@@ -208,6 +208,153 @@ __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detm
   }
 }
 
+// The same round with one game per 32 lanes (half a wave), for batches too small to fill the GPU one game per
+// lane (4096 games = 16 workgroups of k_det_round on 16 of 256 CUs): the lanes load and store the game's SoA
+// bytes together, lane 0 picks the action and applies env_step / no_step / env_reset (the same device functions
+// as k_det_round, on the game's LDS copy), lane a < 24 checks action a (legal_one, the body of det_legal) and a
+// ballot forms the mask, lane a stages cells a and a + 32 and constant channel P + 2 + a of the encode, and the
+// game's C x 56 observation bytes go out as 8-byte chunks over its 32 lanes.  Same results, bit for bit.
+constexpr int kWideBlock = 256;
+constexpr int kWideGames = kWideBlock / 32;
+
+__global__ __launch_bounds__(kWideBlock) void k_det_round_wide(DetConsts c, muz_detmadn_soa st, uint32_t* legal,
+                                                                unsigned long long seed, int turn, int8_t* obs,
+                                                                int8_t* reward, uint8_t* done, int n) {
+  __shared__ int8_t sboard[kWideGames][kCells];
+  __shared__ int8_t sstate[kWideGames][48];   // pins [0, 16), action set [16, 40), cp 40, done 41, reward 42
+  __shared__ __attribute__((aligned(16))) uint8_t senc[kWideGames][kEncStride];
+  const int lg = threadIdx.x >> 5, a = threadIdx.x & 31;
+  const int g = blockIdx.x * kWideGames + lg;
+  const bool valid = g < n;   // uniform over the game's 32 lanes
+  const int S = st.stride, P = c.P, C = 8 * P + 2;
+  int8_t* sp = sstate[lg];
+  const BoardView b{sboard[lg], 1};
+  uint32_t lb = 0;
+  if (valid) {
+    for (int cell = a; cell < kCells; cell += 32) sboard[lg][cell] = st.board[cell * S + g];
+    if (a < 16) sp[a] = a < 4 * P ? st.pins[a * S + g] : (int8_t)-1;
+    if (a < 24) sp[16 + a] = a < 6 * P ? st.action_set[a * S + g] : (int8_t)0;
+    if (a == 0) {
+      sp[40] = st.current_player[g];
+      sp[41] = st.done[g] ? 1 : 0;
+      sp[42] = st.reward[g];
+    }
+    lb = legal[g];
+  }
+  auto lane_state = [&](DetLane& s) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s.pins[j] = sp[j];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) s.aset[j] = sp[16 + j];
+    s.cp = sp[40];
+    s.done = sp[41];
+    s.reward = sp[42];
+  };
+  __syncthreads();
+  int fin = 0;
+  if (valid && a == 0) {
+    DetLane s;
+    lane_state(s);
+    const int cnt = __popc(lb);
+    int r = 0;
+    if (cnt == 0) {
+      det_nostep(c, s);
+    } else {
+      const float u = u24(mix64(game_key(seed ^ kDetRandomStream, g, turn)));
+      int k = (int)(u * (float)cnt);
+      k = k >= cnt ? cnt - 1 : k;
+      uint32_t x = lb;
+      for (int j = 0; j < k; ++j) x &= x - 1;
+      const int act = __ffs(x) - 1;
+      r = det_step_masked(c, s, b, act / 6, act % 6 + 1, lb);
+    }
+    fin = s.done;
+    if (fin) {   // env_reset in place (as k_det_round)
+      const bool fp = has(c.flags, R_FREE_PIN);
+      for (int cell = 0; cell < kCells; ++cell) b.set(cell, -1);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s.pins[j] = (fp && (j & 3) == 0 && (j >> 2) < P) ? c.start[j >> 2] : -1;
+#pragma unroll
+      for (int j = 0; j < 24; ++j) s.aset[j] = j < 6 * P ? 4 : 0;
+      if (fp)
+        for (int p = 0; p < P; ++p) b.set(c.start[p], p);
+      s.cp = c.starting_player;
+      s.done = 0;
+      s.reward = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sp[j] = (int8_t)s.pins[j];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) sp[16 + j] = (int8_t)s.aset[j];
+    sp[40] = (int8_t)s.cp;
+    sp[41] = (int8_t)s.done;
+    sp[42] = (int8_t)s.reward;
+    if (reward) reward[g] = (int8_t)r;
+    if (done) done[g] = (uint8_t)fin;
+  }
+  __syncthreads();
+  if (valid) {
+    DetLane s;
+    lane_state(s);
+    // next legal mask: lane a < 24 checks (pin a / 6, move a % 6 + 1)
+    const LegalCtx x = legal_ctx(c, s, b);
+    const int i = a / 6, m = a % 6 + 1;
+    const bool ok = a < 24 && legal_one(c, b, x, pin_of(s, x.cp, i < 4 ? i : 0), m) && ((x.avail >> (m - 1)) & 1u);
+    const unsigned long long bal = __ballot(ok);
+    if (a == 0) legal[g] = (uint32_t)(bal >> (32 * (lg & 1))) & 0xFFFFFFu;
+    // state back to the SoA
+    for (int cell = a; cell < kCells; cell += 32) st.board[cell * S + g] = (int8_t)b.at(cell);
+    if (a < 4 * P) st.pins[a * S + g] = sp[a];
+    if (a < 6 * P) st.action_set[a * S + g] = sp[16 + a];
+    if (a == 0) {
+      st.current_player[g] = sp[40];
+      st.done[g] = (uint8_t)sp[41];
+      st.reward[g] = sp[42];
+    }
+    // encode staging: rolled cells' owner relative to cp, constant channels
+    if (obs) {
+      uint8_t* e = senc[lg];
+      for (int w = a; w < kCells; w += 32) {
+        const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
+        const int v = b.at(src);
+        e[w] = v < 0 ? 0xFFu : (uint8_t)((v - s.cp + P) % P);
+      }
+      auto none = [](int) { return 0; };
+      const int ch = P + 2 + a;
+      if (ch < C) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
+    }
+  }
+  if (!obs) return;
+  __syncthreads();
+  if (!valid) return;
+  const bool teams = has(c.flags, R_TEAMS);
+  const uint8_t* e = senc[lg];
+  uint2* out = reinterpret_cast<uint2*>(obs + (size_t)g * C * kCells);
+  for (int q = a; q < 7 * C; q += 32) {
+    const int ch = q / 7, w0 = (q - ch * 7) * 8;
+    uint32_t word[2];
+    if (ch < P + 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t rel = e[w0 + 4 * h + j];
+          bool on;
+          if (ch < P) on = rel == (uint32_t)ch;                                            // one-hot player
+          else if (ch == P) on = teams ? (rel == 0u || rel == 2u) : rel == 0u;              // own team
+          else on = teams ? (rel == 1u || rel == 3u) : (rel >= 1u && rel < (uint32_t)P);   // opponents
+          o |= (uint32_t)on << (8 * j);
+        }
+        word[h] = o;
+      }
+    } else {
+      word[0] = word[1] = (uint32_t)e[kCells + ch] * 0x01010101u;
+    }
+    out[q] = make_uint2(word[0], word[1]);
+  }
+}
+
 // ---- evaluation agents (MuZero_det_MADN/evaluate_agent.py) --------------------------------------------
 // mode 0: the random agent (do_random, 770-775: jax.random.categorical over 0 / -1e9 logits of the legal
 // actions); mode 1: the rule-based agent (do_rule_based, 777-864): per action pin*6 + m a score
@@ -311,11 +458,25 @@ __global__ __launch_bounds__(256) void k_det_policy(DetConsts c, muz_detmadn_soa
   action[g] = best;
 }
 
+// variant 0 = by batch size, 1 = one game per lane (k_det_round), 2 = one game per 32 lanes (k_det_round_wide).
+// The lane kernel needs >= 256 workgroups of 256 games to fill 256 CUs; below kWideMaxGames the wide one
+// spreads the same games over 32x the lanes (crossover measured: profiles/r3_env_variants.log).
+constexpr int kWideMaxGames = 1 << 16;
+static inline unsigned nblocks(int n, int b) { return (unsigned)((n + b - 1) / b); }
+
+int launch_det_round(const DetConsts& c, const muz_detmadn_soa& st, uint32_t* legal, unsigned long long seed, int turn,
+                     int8_t* obs, int8_t* reward, uint8_t* done, int n, int variant, hipStream_t s) {
+  if (variant == 2 || (variant == 0 && n <= kWideMaxGames))
+    k_det_round_wide<<<nblocks(n, kWideGames), kWideBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
+  else
+    k_det_round<<<nblocks(n, kRoundBlock), kRoundBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
+  return muz_last_launch_error();
+}
+
 }  // namespace muz
 
 using namespace muz;
 
-static inline unsigned nblocks(int n, int b) { return (unsigned)((n + b - 1) / b); }
 
 extern "C" {
 
@@ -401,9 +562,18 @@ int muz_detmadn_random_round(const muz_rules* rules, muz_detmadn_soa st, uint32_
   if (rc) return rc;
   MUZ_HOST_CHECK(n >= 0 && st.stride >= n && legal_bits);
   if (n == 0) return MUZ_OK;
-  k_det_round<<<nblocks(n, kRoundBlock), kRoundBlock, 0, (hipStream_t)stream>>>(c, st, legal_bits, seed, turn, obs,
-                                                                                reward, done, n);
-  return muz_last_launch_error();
+  return launch_det_round(c, st, legal_bits, seed, turn, obs, reward, done, n, 0, (hipStream_t)stream);
+}
+
+int muz_detmadn_random_round_variant(const muz_rules* rules, muz_detmadn_soa st, uint32_t* legal_bits, uint64_t seed,
+                                     int32_t turn, int8_t* obs, int8_t* reward, uint8_t* done, int32_t n,
+                                     int32_t variant, void* stream) {
+  DetConsts c;
+  int rc = make_det_consts(rules, &c);
+  if (rc) return rc;
+  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && legal_bits && variant >= 0 && variant <= 2);
+  if (n == 0) return MUZ_OK;
+  return launch_det_round(c, st, legal_bits, seed, turn, obs, reward, done, n, variant, (hipStream_t)stream);
 }
 
 int muz_detmadn_policy_action(const muz_rules* rules, muz_detmadn_soa st, const uint32_t* legal_bits, int32_t mode,

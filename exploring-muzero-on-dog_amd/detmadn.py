@@ -237,13 +237,21 @@ def encode_board(env: DetMADNState, dtype=torch.float32) -> torch.Tensor:
 
 
 def random_round(env: DetMADNState, legal: torch.Tensor, seed: int, turn: int, obs: torch.Tensor | None = None,
-                 reward: torch.Tensor | None = None, done: torch.Tensor | None = None):
+                 reward: torch.Tensor | None = None, done: torch.Tensor | None = None, variant: int = 0):
     """One env-step of uniform random legal play for every game (muz_detmadn_random_round): the k-th legal
     action of ``legal`` (int32 [B], updated in place to the next mask), env_step / no_step, in-place reset of
-    finished games, and encode_board of the next state into ``obs`` (int8 [B, 8P+2, 56]) when given."""
-    _L.check(_L.load().muz_detmadn_random_round(env.rules, env.soa(), _L.ptr(legal), int(seed) & ((1 << 64) - 1),
-                                                int(turn), _L.ptr(obs), _L.ptr(reward), _L.ptr(done), env.batch,
-                                                _L.stream_ptr()), "muz_detmadn_random_round")
+    finished games, and encode_board of the next state into ``obs`` (int8 [B, 8P+2, 56]) when given.
+    ``variant``: 0 = the kernel chosen by batch size, 1 = one game per lane, 2 = one game per 32 lanes (same
+    results)."""
+    lib = _L.load()
+    if variant == 0:
+        rc = lib.muz_detmadn_random_round(env.rules, env.soa(), _L.ptr(legal), int(seed) & ((1 << 64) - 1), int(turn),
+                                          _L.ptr(obs), _L.ptr(reward), _L.ptr(done), env.batch, _L.stream_ptr())
+    else:
+        rc = lib.muz_detmadn_random_round_variant(env.rules, env.soa(), _L.ptr(legal), int(seed) & ((1 << 64) - 1),
+                                                  int(turn), _L.ptr(obs), _L.ptr(reward), _L.ptr(done), env.batch,
+                                                  int(variant), _L.stream_ptr())
+    _L.check(rc, "muz_detmadn_random_round")
     return env
 
 

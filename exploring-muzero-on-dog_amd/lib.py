@@ -228,6 +228,8 @@ SIGNATURES = {
     "muz_detmadn_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_random_round": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_uint64, ctypes.c_int32,
                                                 vp, vp, vp, ctypes.c_int32, vp]),
+    "muz_detmadn_random_round_variant": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_uint64,
+                                                        ctypes.c_int32, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp]),
     "muz_detmadn_policy_action": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32,
                                                  ctypes.POINTER(MuzRuleAgent), ctypes.c_uint64, ctypes.c_int32, vp, vp,
                                                  ctypes.c_int32, vp]),

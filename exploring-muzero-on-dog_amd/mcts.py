@@ -103,7 +103,11 @@ def run_muzero_mcts(params, rng_key, observations, invalid_actions, num_simulati
     ``rng_key``: int or uint32[2] key (selects the engine's Gumbel stream, nets.rng_key_to_seed);
     ``observations``: [B, C, 56] (NumPy or torch, any device); ``invalid_actions``: bool [B, 24].
     Returns (PolicyOutput(action, action_weights), root_value = search_tree.summary().value) as device
-    tensors on cuda."""
+    tensors on cuda.
+
+    Kernel limits (k_gumbel_search; every reference call site is inside them: S = 50 / 100, D = 25 / 50):
+    num_simulations 1..100, max_depth 1..64, 24 actions (det-MADN), max_num_considered_actions 16 (mctx's
+    default); outside them muz_gumbel_search returns MUZ_E_UNSUPPORTED and this raises MuzError."""
     dev = torch.device("cuda")
     net = _N.as_device_net(params, device=dev)
     obs = observations if isinstance(observations, torch.Tensor) else torch.from_numpy(np.asarray(observations))

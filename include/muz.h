@@ -121,6 +121,12 @@ int muz_detmadn_encode_i8(const muz_rules* rules, muz_detmadn_soa state, int8_t*
  * encode_board sequence of MuZero_det_MADN/game_agent.py:84-119 (MADN/deterministic_madn.py:170-438). */
 int muz_detmadn_random_round(const muz_rules* rules, muz_detmadn_soa state, uint32_t* legal_bits, uint64_t seed,
                              int32_t turn, int8_t* obs, int8_t* reward, uint8_t* done, int32_t n, void* stream);
+/* The same round with the kernel chosen explicitly: variant 1 = one game per lane (k_det_round, for batches that
+ * fill the GPU), 2 = one game per 32 lanes (k_det_round_wide, small batches), 0 = by batch size (as
+ * muz_detmadn_random_round).  Identical results. */
+int muz_detmadn_random_round_variant(const muz_rules* rules, muz_detmadn_soa state, uint32_t* legal_bits,
+                                     uint64_t seed, int32_t turn, int8_t* obs, int8_t* reward, uint8_t* done,
+                                     int32_t n, int32_t variant, void* stream);
 
 /* Evaluation agents of MuZero_det_MADN/evaluate_agent.py: mode 0 = the random agent (do_random, 770-775),
  * mode 1 = the rule-based agent (do_rule_based, 777-864; weights in `agent`, the reference's

@@ -32,8 +32,10 @@ def oracle_round(envs, seed, turn, kw):
     return out
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("rule_set", ["selfplay_2p", "selfplay_4p_teams", "exotic_4p"])
-def test_random_round_matches_oracle(cuda, rule_set):
+def test_random_round_matches_oracle(cuda, rule_set, variant):
+    """variant 1: one game per lane (k_det_round), 2: one game per 32 lanes (k_det_round_wide)."""
     from exploring_muzero_on_dog_amd import detmadn as E
     kw = RULE_SETS[rule_set]
     B, seed, rounds = 48, 9, 400
@@ -46,7 +48,7 @@ def test_random_round_matches_oracle(cuda, rule_set):
     envs = [dm.env_reset(**kw) for _ in range(B)]
     finished = 0
     for t in range(rounds):
-        E.random_round(env, legal, seed, t, obs=obs, done=done)
+        E.random_round(env, legal, seed, t, obs=obs, done=done, variant=variant)
         res = oracle_round(envs, seed, t, kw)
         envs = [e for e, _ in res]
         fin = np.array([f for _, f in res])
@@ -62,7 +64,8 @@ def test_random_round_matches_oracle(cuda, rule_set):
     assert finished > 0, "games must finish and restart within the rounds"
 
 
-def test_random_round_large_batch_properties(cuda):
+@pytest.mark.parametrize("variant", [1, 2])
+def test_random_round_large_batch_properties(cuda, variant):
     """B = 2^20 games (the micro-benchmark's HBM-sized batch): the observation written by the fused kernel
     equals encode_board of the stored state, and the returned mask equals valid_action of it."""
     from exploring_muzero_on_dog_amd import detmadn as E
@@ -72,6 +75,6 @@ def test_random_round_large_batch_properties(cuda):
     legal = E.legal_bits(env)
     obs = torch.empty((B, 18, 56), dtype=torch.int8, device="cuda")
     for t in range(40):
-        E.random_round(env, legal, 3, t, obs=obs)
+        E.random_round(env, legal, 3, t, obs=obs, variant=variant)
     assert torch.equal(obs, E.encode_board(env, dtype=torch.int8))
     assert torch.equal(legal, E.legal_bits(env))
