@@ -85,7 +85,7 @@ def parse():
                          "(pipeline.run_overlapped; weights one iteration staler than the reference's loop)")
     ap.add_argument("--workload", choices=("det", "classic", "dog", "train", "env", "selftest"), default="det",
                     help="det = the BASELINE.json headline (config b); classic = config (c); dog = config (d)")
-    ap.add_argument("--env-variant", type=int, choices=(0, 1, 2), default=0,
+    ap.add_argument("--env-variant", type=int, choices=(0, 1, 2, 3, 4, 5), default=0,
                     help="env workload: 0 = kernel by batch size, 1 = one game per lane, 2 = one game per 32 lanes")
     ap.add_argument("--records", action="store_true",
                     help="dog: record every turn (muz_dog_random_play_record), pack the records each step and gather "
@@ -716,7 +716,10 @@ def run_train(args):
 
 
 ENV_ROUNDS_PER_STEP = 100      # --workload env: one bench step = 100 random-play env rounds (one launch each)
-ENV_WIDE_MAX_GAMES = 1 << 16   # csrc/env_detmadn.hip kWideMaxGames: up to here one game per 32 lanes
+# csrc/env_detmadn.hip launch_det_round: the kernel variant 0 picks by batch size (one game per 32 lanes up to
+# 2^13 games, per 4 lanes up to 2^16, per lane above)
+def env_auto_variant(B):
+    return 2 if B <= (1 << 13) else 4 if B <= (1 << 16) else 1
 ENV_PREROLL = 300              # rounds played before warm-up: games spread over 0..300 plies (SURVEY §8(d)(b'))
 
 
@@ -768,8 +771,9 @@ def run_env(args):
         return
     avg_ms = lms / (R * args.steps * world)
     per = env_bytes_per_step(PLAYERS)
-    wide = args.env_variant == 2 or (args.env_variant == 0 and B <= ENV_WIDE_MAX_GAMES)
-    kernel = "k_det_round_wide" if wide else "k_det_round"
+    variant = args.env_variant or env_auto_variant(B)
+    kernel = {1: "k_det_round", 2: "k_det_round_g<32>", 3: "k_det_round_g<8>", 4: "k_det_round_g<4>",
+              5: "k_det_round_g<16>"}[variant]
     achieved = B * per / (avg_ms * 1e-3) / 1e9
     out = {
         "metric": "env-only steps/sec (step + legal + encode), det-MADN 2p random legal play (SURVEY 8(d)(b'))",

@@ -59,6 +59,29 @@ __device__ __forceinline__ bool has(uint32_t f, uint32_t bit) { return (f & bit)
 __device__ __forceinline__ int pin_of(const DetLane& s, int p, int k) { return rsel(s.pins, p * 4 + k); }
 __device__ __forceinline__ int aset_of(const DetLane& s, int p, int m) { return rsel(s.aset, p * 6 + m); }
 
+// A game's pins and action set kept in an LDS row (pins [0, 16), action set [16, 40)) instead of registers, read
+// and written by index: the G-lane env round (k_det_round_g) runs legal_ctx, the encode and env_step on it
+// without holding all 40 values in VGPRs.  The rule functions below take either lane type through these
+// accessors (static index j: lane_pin / lane_aset; dynamic index: pin_of / aset_of / set_pin / set_aset).
+struct LdsLane {
+  int8_t* row;
+  int cp, done, reward;
+};
+__device__ __forceinline__ int pin_of(const LdsLane& s, int p, int k) { return s.row[p * 4 + k]; }
+__device__ __forceinline__ int aset_of(const LdsLane& s, int p, int m) { return s.row[16 + p * 6 + m]; }
+__device__ __forceinline__ int lane_pin(const DetLane& s, int j) { return s.pins[j]; }
+__device__ __forceinline__ int lane_aset(const DetLane& s, int j) { return s.aset[j]; }
+__device__ __forceinline__ void lane_set_pin(DetLane& s, int j, int v) { s.pins[j] = v; }
+__device__ __forceinline__ void lane_set_aset(DetLane& s, int j, int v) { s.aset[j] = v; }
+__device__ __forceinline__ void set_pin(DetLane& s, int idx, int v) { rset(s.pins, idx, v); }
+__device__ __forceinline__ void set_aset(DetLane& s, int idx, int v) { rset(s.aset, idx, v); }
+__device__ __forceinline__ int lane_pin(const LdsLane& s, int j) { return s.row[j]; }
+__device__ __forceinline__ int lane_aset(const LdsLane& s, int j) { return s.row[16 + j]; }
+__device__ __forceinline__ void lane_set_pin(LdsLane& s, int j, int v) { s.row[j] = (int8_t)v; }
+__device__ __forceinline__ void lane_set_aset(LdsLane& s, int j, int v) { s.row[16 + j] = (int8_t)v; }
+__device__ __forceinline__ void set_pin(LdsLane& s, int idx, int v) { s.row[idx] = (int8_t)v; }
+__device__ __forceinline__ void set_aset(LdsLane& s, int idx, int v) { s.row[16 + idx] = (int8_t)v; }
+
 __device__ __forceinline__ int cst(const int (&a)[4], int i) { return rsel(a, i); }
 
 __device__ __forceinline__ int goal_of(const DetConsts& c, int p, int g) {
@@ -109,14 +132,15 @@ __device__ __forceinline__ bool goal_path_free(const DetConsts& c, const BoardVi
 }
 
 // valid_action (deterministic_madn.py:299-393), split into the per-state prelude (LegalCtx) and the check of one
-// (pin i, move m) (legal_one): det_legal runs all 24 checks in one lane, k_det_round_wide one check per lane.
+// (pin i, move m) (legal_one): det_legal runs all 24 checks in one lane, k_det_round_g 24 / G checks per lane.
 struct LegalCtx {
   int cp0, cp, tgt, g0, g3, mt, start_cp;
   bool home_ok;
   bool pos[4];
   uint32_t avail;   // moves m with action_set[cp][m-1] > 0, bit m-1
 };
-__device__ __forceinline__ LegalCtx legal_ctx(const DetConsts& c, const DetLane& s, const BoardView& b) {
+template <class Lane>
+__device__ __forceinline__ LegalCtx legal_ctx(const DetConsts& c, const Lane& s, const BoardView& b) {
   LegalCtx x;
   const uint32_t F = c.flags;
   x.cp0 = s.cp;
@@ -189,14 +213,15 @@ __device__ __forceinline__ uint32_t det_legal(const DetConsts& c, const DetLane&
 }
 
 // set_pins_on_board (deterministic_madn.py:259-271) into the lane's LDS board.
-__device__ __forceinline__ void rebuild_board(const DetConsts& c, const DetLane& s, const BoardView& b) {
+template <class Lane>
+__device__ __forceinline__ void rebuild_board(const DetConsts& c, const Lane& s, const BoardView& b) {
   for (int cell = 0; cell < kCells; ++cell) b.set(cell, -1);
 #pragma unroll
   for (int p = 0; p < 4; ++p)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (p < c.P) {
-        const int pos = s.pins[p * 4 + k];
+        const int pos = lane_pin(s, p * 4 + k);
         if (pos >= 0 && pos < kCells) b.set(pos, p);
       }
 }
@@ -204,7 +229,8 @@ __device__ __forceinline__ void rebuild_board(const DetConsts& c, const DetLane&
 // env_step (deterministic_madn.py:170-257) with (pin, move), given the state's legal mask (valid_action of
 // the same state; callers that already hold it skip the second legality pass).  Updates s and the LDS board.
 // Returns the reward; s.done / s.reward / s.cp updated like the reference.
-__device__ __forceinline__ int det_step_masked(const DetConsts& c, DetLane& s, const BoardView& b, int pin, int move,
+template <class Lane>
+__device__ __forceinline__ int det_step_masked(const DetConsts& c, Lane& s, const BoardView& b, int pin, int move,
                                                const uint32_t legal) {
   const uint32_t F = c.flags;
   const int player_id = s.cp;
@@ -238,12 +264,13 @@ __device__ __forceinline__ int det_step_masked(const DetConsts& c, DetLane& s, c
     if (pin_at != -1 && (pin_at != cp || has(F, R_FRIENDLY))) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        int x = ((j >> 2) == pin_at && s.pins[j] == new_pos) ? -1 : s.pins[j];
+        const int pj = lane_pin(s, j);
+        int x = ((j >> 2) == pin_at && pj == new_pos) ? -1 : pj;
         asm volatile("" : "+v"(x));
-        s.pins[j] = x;
+        lane_set_pin(s, j, x);
       }
     }
-    rset(s.pins, cp * 4 + pi, new_pos);
+    set_pin(s, cp * 4 + pi, new_pos);
     rebuild_board(c, s, b);
   }
   // action set: decrement [cp, move-1]; if the row empties, refill row current_player of the
@@ -256,12 +283,12 @@ __device__ __forceinline__ int det_step_masked(const DetConsts& c, DetLane& s, c
   if (row_empty) {
 #pragma unroll
     for (int j = 0; j < 24; ++j) {
-      int x = (j / 6 == player_id) ? 4 : s.aset[j];
+      int x = (j / 6 == player_id) ? 4 : lane_aset(s, j);
       asm volatile("" : "+v"(x));
-      s.aset[j] = x;
+      lane_set_aset(s, j, x);
     }
   } else {
-    rset(s.aset, cp * 6 + mi, nv);
+    set_aset(s, cp * 6 + mi, nv);
   }
   const uint32_t w = winners(c, b);
   const int reward = s.done ? 0 : (invalid ? -1 : (int)((w >> cp) & 1u));
@@ -277,12 +304,13 @@ __device__ __forceinline__ int det_step(const DetConsts& c, DetLane& s, const Bo
 }
 
 // no_step (deterministic_madn.py:283-297).
-__device__ __forceinline__ void det_nostep(const DetConsts& c, DetLane& s) {
+template <class Lane>
+__device__ __forceinline__ void det_nostep(const DetConsts& c, Lane& s) {
 #pragma unroll
   for (int j = 0; j < 24; ++j) {
-    int x = (j / 6 == s.cp) ? 4 : s.aset[j];
+    int x = (j / 6 == s.cp) ? 4 : lane_aset(s, j);
     asm volatile("" : "+v"(x));
-    s.aset[j] = x;
+    lane_set_aset(s, j, x);
   }
   s.cp = (s.cp + 1) % c.P;
 }
@@ -325,8 +353,8 @@ __device__ __forceinline__ void det_store(const DetConsts& c, const muz_detmadn_
 
 // encode_board value of channel ch at cell w (deterministic_madn.py:395-438).
 // C = P + 2 + P + 6P; board cell lookups go through `cell_owner(src)`.
-template <class CellFn>
-__device__ __forceinline__ int det_encode_value(const DetConsts& c, const DetLane& s, int ch, int w,
+template <class Lane, class CellFn>
+__device__ __forceinline__ int det_encode_value(const DetConsts& c, const Lane& s, int ch, int w,
                                                 CellFn cell_owner) {
   const int P = c.P, cp = s.cp;
   const int src = (w < kTrack) ? fmodp(w + kDist * cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * cp, 16);

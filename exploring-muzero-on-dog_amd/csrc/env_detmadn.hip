@@ -104,13 +104,54 @@ __global__ __launch_bounds__(64) void k_det_encode(DetConsts c, muz_detmadn_soa 
 // legal --, an in-place env_reset of a game that finished, the next legal mask, and the int8 observation of
 // the state the next round acts on (encode_board, deterministic_madn.py:395-438).
 // Phase 1 is lane per game (256 games per workgroup; SoA loads / stores coalesced) and stages per game, in
-// LDS, each rolled cell's owner relative to the current player (rel = (owner - cp) mod P, 0xFF empty) and
-// the constant channels (home counts, action sets).  Phase 2 writes the workgroup's 256 x C x 56
-// contiguous observation bytes as 8-byte chunks -- 56 = 7 x 8, so a chunk never straddles two channels --
-// with consecutive threads on consecutive chunks (fully coalesced 512-byte wave stores).
+// LDS, each rolled cell's owner relative to the current player (rel = (owner - cp) mod P, kRelEmpty empty)
+// and the constant channels (home counts, action sets).  Phase 2 (det_obs_write) writes the workgroup's
+// 256 x C x 56 contiguous observation bytes as 16-byte chunks, consecutive threads on consecutive chunks.
 constexpr int kRoundBlock = 256;
 constexpr unsigned long long kDetRandomStream = 0xD37A11D0ull;
 constexpr int kEncStride = 96;   // per game: rel[56] + constant channel values at [56 + ch]
+
+// Phase 2 of the env rounds: `games` consecutive games' int8 observations (C x 56 bytes each, contiguous in
+// `out`) from their staged encode inputs (per game at senc + gl * kEncStride: rel[56] = the rolled cell's owner
+// relative to the current player, kRelEmpty for an empty cell, then the constant channels' values at [56 + ch]).
+// One 16-byte store per thread and iteration, consecutive threads on consecutive 16-byte chunks (1 KB per
+// wave-instruction): a game's C x 56 = 16 (28P + 7) bytes split into halves of 8 cells of one channel (56 = 7 x 8),
+// two per chunk.  A board channel's 4 output bytes are ONE byte permute of the 4 staged rel bytes through the
+// channel's 4-entry table (byte r = 1 if relative owner r is on the channel); kRelEmpty = 12 is v_perm_b32's
+// constant-zero selector.  (Per-byte predicates compiled to ~700 divergent-branch instructions per chunk and
+// made this phase ~80 % of the launch: profiles/r3_env_breakdown.log.)
+constexpr uint32_t kRelEmpty = 12u;
+__device__ __forceinline__ uint32_t det_obs_table(int ch, int P, bool teams) {
+  const uint32_t player = 1u << (8 * (ch & 3));                                        // ch < P: one-hot
+  const uint32_t own = teams ? 0x00010001u : 0x00000001u;                              // ch == P
+  const uint32_t opp = teams ? 0x01000100u : (P == 2 ? 0x00000100u : P == 3 ? 0x00010100u : 0x01010100u);
+  return ch < P ? player : ch == P ? own : opp;
+}
+__device__ __forceinline__ uint2 det_obs_half(const uint8_t* e, int m, int P, bool teams) {
+  const int ch = m / 7, w0 = (m - ch * 7) * 8;
+  const uint2 rw = *reinterpret_cast<const uint2*>(e + w0);
+  const uint32_t tab = det_obs_table(ch, P, teams);
+  const uint32_t cv = (uint32_t)e[kCells + ch] * 0x01010101u;   // constant channel (ignored below P + 2)
+  const bool board = ch < P + 2;
+  return make_uint2(board ? __builtin_amdgcn_perm(0u, tab, rw.x) : cv, board ? __builtin_amdgcn_perm(0u, tab, rw.y) : cv);
+}
+__device__ __forceinline__ void det_obs_write(const DetConsts& c, const uint8_t* senc, int games, int8_t* out, int t,
+                                              int nthreads) {
+  const int P = c.P, C = 8 * P + 2;
+  const bool teams = has(c.flags, R_TEAMS);
+  const int per = C * 7 / 2;   // 16-byte chunks per game
+  const float inv = 1.0f / (float)per;
+  uint4* o = reinterpret_cast<uint4*>(out);
+  for (int q = t; q < games * per; q += nthreads) {
+    int gl = (int)(((float)q + 0.5f) * inv);
+    gl -= gl * per > q ? 1 : 0;
+    gl += (gl + 1) * per <= q ? 1 : 0;
+    const int m = 2 * (q - gl * per);
+    const uint8_t* e = senc + gl * kEncStride;
+    const uint2 lo = det_obs_half(e, m, P, teams), hi = det_obs_half(e, m + 1, P, teams);
+    o[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
 
 __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detmadn_soa st, uint32_t* legal,
                                                            unsigned long long seed, int turn, int8_t* obs,
@@ -161,7 +202,7 @@ __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detm
       for (int w = 0; w < kCells; ++w) {
         const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
         const int v = b.at(src);
-        const uint32_t rel = v < 0 ? 0xFFu : (uint32_t)((v - s.cp + P) % P);
+        const uint32_t rel = v < 0 ? kRelEmpty : (uint32_t)((v - s.cp + P) % P);
         wv |= rel << (8 * (w & 3));
         if ((w & 3) == 3) {
           *reinterpret_cast<uint32_t*>(e + (w & ~3)) = wv;
@@ -175,86 +216,58 @@ __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detm
   if (!obs) return;
   __syncthreads();
   const int g0 = blockIdx.x * kRoundBlock;
-  const int games = min(kRoundBlock, n - g0);
-  const int per = 7 * C;
-  const bool teams = has(c.flags, R_TEAMS);
-  uint2* out = reinterpret_cast<uint2*>(obs + (size_t)g0 * C * kCells);
-  for (int q = threadIdx.x; q < games * per; q += kRoundBlock) {
-    const int gl = q / per, rem = q - gl * per;
-    const int ch = rem / 7, w0 = (rem - ch * 7) * 8;
-    const uint8_t* e = senc + gl * kEncStride;
-    uint32_t word[2];
-    if (ch < P + 2) {
-      const uint2 rw = *reinterpret_cast<const uint2*>(e + w0);
-      const uint32_t rr[2] = {rw.x, rw.y};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        uint32_t o = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t rel = (rr[h] >> (8 * j)) & 0xFFu;
-          bool on;
-          if (ch < P) on = rel == (uint32_t)ch;                                            // one-hot player
-          else if (ch == P) on = teams ? (rel == 0u || rel == 2u) : rel == 0u;              // own team
-          else on = teams ? (rel == 1u || rel == 3u) : (rel >= 1u && rel < (uint32_t)P);   // opponents
-          o |= (uint32_t)on << (8 * j);
-        }
-        word[h] = o;
-      }
-    } else {
-      word[0] = word[1] = (uint32_t)e[kCells + ch] * 0x01010101u;
-    }
-    out[q] = make_uint2(word[0], word[1]);
-  }
+  det_obs_write(c, senc, min(kRoundBlock, n - g0), obs + (size_t)g0 * C * kCells, threadIdx.x, kRoundBlock);
 }
 
-// The same round with one game per 32 lanes (half a wave), for batches too small to fill the GPU one game per
-// lane (4096 games = 16 workgroups of k_det_round on 16 of 256 CUs): the lanes load and store the game's SoA
-// bytes together, lane 0 picks the action and applies env_step / no_step / env_reset (the same device functions
-// as k_det_round, on the game's LDS copy), lane a < 24 checks action a (legal_one, the body of det_legal) and a
-// ballot forms the mask, lane a stages cells a and a + 32 and constant channel P + 2 + a of the encode, and the
-// game's C x 56 observation bytes go out as 8-byte chunks over its 32 lanes.  Same results, bit for bit.
+// The same round with one game per G lanes (G = 4, 8, 16 or 32), for batches too small to fill the GPU one game per
+// lane (4096 games = 16 workgroups of k_det_round on 16 of 256 CUs) and to shorten each lane's serial chain: the
+// workgroup copies its NG = 256 / G games' SoA rows into LDS with coalesced, game-contiguous loads (transposed to a
+// per-game row), lane 0 of a game picks the action and applies env_step / no_step / env_reset (the same device
+// functions as k_det_round, on the game's LDS copy), lane a checks actions a, a + G, ... (legal_one, the body of
+// det_legal; one ballot per G actions forms the mask), stages cells a, a + G, ... and constant channels P + 2 + a,
+// ... of the encode, and the workgroup writes the state rows back and its NG x C x 56 contiguous observation bytes
+// as 8-byte chunks, both fully coalesced.  Same results, bit for bit.
 constexpr int kWideBlock = 256;
-constexpr int kWideGames = kWideBlock / 32;
+constexpr int kStateRow = 48;   // per game in LDS: pins [0, 16), action set [16, 40), cp 40, done 41, reward 42, r 43
 
-__global__ __launch_bounds__(kWideBlock) void k_det_round_wide(DetConsts c, muz_detmadn_soa st, uint32_t* legal,
-                                                                unsigned long long seed, int turn, int8_t* obs,
-                                                                int8_t* reward, uint8_t* done, int n) {
-  __shared__ int8_t sboard[kWideGames][kCells];
-  __shared__ int8_t sstate[kWideGames][48];   // pins [0, 16), action set [16, 40), cp 40, done 41, reward 42
-  __shared__ __attribute__((aligned(16))) uint8_t senc[kWideGames][kEncStride];
-  const int lg = threadIdx.x >> 5, a = threadIdx.x & 31;
-  const int g = blockIdx.x * kWideGames + lg;
-  const bool valid = g < n;   // uniform over the game's 32 lanes
+template <int G>
+__global__ __launch_bounds__(kWideBlock) void k_det_round_g(DetConsts c, muz_detmadn_soa st, uint32_t* legal,
+                                                            unsigned long long seed, int turn, int8_t* obs,
+                                                            int8_t* reward, uint8_t* done, int n) {
+  static_assert(G == 4 || G == 8 || G == 16 || G == 32, "lanes per game");
+  constexpr int NG = kWideBlock / G;
+  __shared__ int8_t sboard[NG][kCells];
+  __shared__ int8_t sstate[NG][kStateRow];
+  __shared__ __attribute__((aligned(16))) uint8_t senc[NG][kEncStride];
+  const int t = threadIdx.x;
+  const int lg = t / G, a = t % G;
+  const int g0 = blockIdx.x * NG;
+  const int games = min(NG, n - g0);
+  const int g = g0 + lg;
+  const bool valid = lg < games;   // uniform over the game's G lanes
   const int S = st.stride, P = c.P, C = 8 * P + 2;
+  // SoA rows -> LDS: consecutive threads on consecutive games of one row (coalesced), transposed per game
+  for (int i = t; i < kCells * NG; i += kWideBlock) {
+    const int row = i / NG, gi = i - row * NG;
+    if (gi < games) sboard[gi][row] = st.board[row * S + g0 + gi];
+  }
+  for (int i = t; i < kStateRow * NG; i += kWideBlock) {
+    const int row = i / NG, gi = i - row * NG;
+    if (gi >= games) continue;
+    int8_t v = 0;
+    if (row < 16) v = row < 4 * P ? st.pins[row * S + g0 + gi] : (int8_t)-1;
+    else if (row < 40) v = row - 16 < 6 * P ? st.action_set[(row - 16) * S + g0 + gi] : (int8_t)0;
+    else if (row == 40) v = st.current_player[g0 + gi];
+    else if (row == 41) v = st.done[g0 + gi] ? 1 : 0;
+    else if (row == 42) v = st.reward[g0 + gi];
+    sstate[gi][row] = v;
+  }
   int8_t* sp = sstate[lg];
   const BoardView b{sboard[lg], 1};
-  uint32_t lb = 0;
-  if (valid) {
-    for (int cell = a; cell < kCells; cell += 32) sboard[lg][cell] = st.board[cell * S + g];
-    if (a < 16) sp[a] = a < 4 * P ? st.pins[a * S + g] : (int8_t)-1;
-    if (a < 24) sp[16 + a] = a < 6 * P ? st.action_set[a * S + g] : (int8_t)0;
-    if (a == 0) {
-      sp[40] = st.current_player[g];
-      sp[41] = st.done[g] ? 1 : 0;
-      sp[42] = st.reward[g];
-    }
-    lb = legal[g];
-  }
-  auto lane_state = [&](DetLane& s) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) s.pins[j] = sp[j];
-#pragma unroll
-    for (int j = 0; j < 24; ++j) s.aset[j] = sp[16 + j];
-    s.cp = sp[40];
-    s.done = sp[41];
-    s.reward = sp[42];
-  };
+  const uint32_t lb = valid ? legal[g] : 0u;
   __syncthreads();
-  int fin = 0;
-  if (valid && a == 0) {
-    DetLane s;
-    lane_state(s);
+  if (valid && a == 0) {   // the game's step on its LDS rows (pins / action set by index, not in VGPRs)
+    LdsLane s{sp, sp[40], sp[41], sp[42]};
     const int cnt = __popc(lb);
     int r = 0;
     if (cnt == 0) {
@@ -268,24 +281,20 @@ __global__ __launch_bounds__(kWideBlock) void k_det_round_wide(DetConsts c, muz_
       const int act = __ffs(x) - 1;
       r = det_step_masked(c, s, b, act / 6, act % 6 + 1, lb);
     }
-    fin = s.done;
+    const int fin = s.done;
     if (fin) {   // env_reset in place (as k_det_round)
       const bool fp = has(c.flags, R_FREE_PIN);
       for (int cell = 0; cell < kCells; ++cell) b.set(cell, -1);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) s.pins[j] = (fp && (j & 3) == 0 && (j >> 2) < P) ? c.start[j >> 2] : -1;
+      for (int j = 0; j < 16; ++j) sp[j] = (int8_t)((fp && (j & 3) == 0 && (j >> 2) < P) ? c.start[j >> 2] : -1);
 #pragma unroll
-      for (int j = 0; j < 24; ++j) s.aset[j] = j < 6 * P ? 4 : 0;
+      for (int j = 0; j < 24; ++j) sp[16 + j] = (int8_t)(j < 6 * P ? 4 : 0);
       if (fp)
         for (int p = 0; p < P; ++p) b.set(c.start[p], p);
       s.cp = c.starting_player;
       s.done = 0;
       s.reward = 0;
     }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) sp[j] = (int8_t)s.pins[j];
-#pragma unroll
-    for (int j = 0; j < 24; ++j) sp[16 + j] = (int8_t)s.aset[j];
     sp[40] = (int8_t)s.cp;
     sp[41] = (int8_t)s.done;
     sp[42] = (int8_t)s.reward;
@@ -294,65 +303,57 @@ __global__ __launch_bounds__(kWideBlock) void k_det_round_wide(DetConsts c, muz_
   }
   __syncthreads();
   if (valid) {
-    DetLane s;
-    lane_state(s);
-    // next legal mask: lane a < 24 checks (pin a / 6, move a % 6 + 1)
+    const LdsLane s{sp, sp[40], 0, 0};
+    // next legal mask: lane a checks actions a + G * it = (pin / 6, move % 6 + 1); the game's G bits of each ballot
     const LegalCtx x = legal_ctx(c, s, b);
-    const int i = a / 6, m = a % 6 + 1;
-    const bool ok = a < 24 && legal_one(c, b, x, pin_of(s, x.cp, i < 4 ? i : 0), m) && ((x.avail >> (m - 1)) & 1u);
-    const unsigned long long bal = __ballot(ok);
-    if (a == 0) legal[g] = (uint32_t)(bal >> (32 * (lg & 1))) & 0xFFFFFFu;
-    // state back to the SoA
-    for (int cell = a; cell < kCells; cell += 32) st.board[cell * S + g] = (int8_t)b.at(cell);
-    if (a < 4 * P) st.pins[a * S + g] = sp[a];
-    if (a < 6 * P) st.action_set[a * S + g] = sp[16 + a];
-    if (a == 0) {
-      st.current_player[g] = sp[40];
-      st.done[g] = (uint8_t)sp[41];
-      st.reward[g] = sp[42];
+    const int gw = (t & 63) / G;   // this game's slot in the wave
+    uint32_t mask = 0;
+#pragma unroll
+    for (int it = 0; it < (24 + G - 1) / G; ++it) {
+      const int act = a + G * it;
+      const int i = act / 6, m = act % 6 + 1;
+      const bool ok = act < 24 && legal_one(c, b, x, pin_of(s, x.cp, i < 4 ? i : 0), m) && ((x.avail >> (m - 1)) & 1u);
+      const unsigned long long bal = __ballot(ok);
+      mask |= (uint32_t)((bal >> (G * gw)) & ((1ull << G) - 1ull)) << (G * it);
     }
+    if (a == 0) legal[g] = mask & 0xFFFFFFu;
     // encode staging: rolled cells' owner relative to cp, constant channels
     if (obs) {
       uint8_t* e = senc[lg];
-      for (int w = a; w < kCells; w += 32) {
+      for (int w = a; w < kCells; w += G) {
         const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
         const int v = b.at(src);
-        e[w] = v < 0 ? 0xFFu : (uint8_t)((v - s.cp + P) % P);
+        e[w] = v < 0 ? (uint8_t)kRelEmpty : (uint8_t)((v - s.cp + P) % P);
       }
       auto none = [](int) { return 0; };
-      const int ch = P + 2 + a;
-      if (ch < C) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
+      for (int ch = P + 2 + a; ch < C; ch += G) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
+    }
+  }
+  // (lanes of invalid games, last workgroup only, skip the ballots: inactive lanes contribute zero bits)
+  __syncthreads();
+  // LDS -> SoA rows, coalesced as on the way in
+  for (int i = t; i < kCells * NG; i += kWideBlock) {
+    const int row = i / NG, gi = i - row * NG;
+    if (gi < games) st.board[row * S + g0 + gi] = sboard[gi][row];
+  }
+  for (int i = t; i < kStateRow * NG; i += kWideBlock) {
+    const int row = i / NG, gi = i - row * NG;
+    if (gi >= games) continue;
+    const int8_t v = sstate[gi][row];
+    if (row < 16) {
+      if (row < 4 * P) st.pins[row * S + g0 + gi] = v;
+    } else if (row < 40) {
+      if (row - 16 < 6 * P) st.action_set[(row - 16) * S + g0 + gi] = v;
+    } else if (row == 40) {
+      st.current_player[g0 + gi] = v;
+    } else if (row == 41) {
+      st.done[g0 + gi] = (uint8_t)v;
+    } else if (row == 42) {
+      st.reward[g0 + gi] = v;
     }
   }
   if (!obs) return;
-  __syncthreads();
-  if (!valid) return;
-  const bool teams = has(c.flags, R_TEAMS);
-  const uint8_t* e = senc[lg];
-  uint2* out = reinterpret_cast<uint2*>(obs + (size_t)g * C * kCells);
-  for (int q = a; q < 7 * C; q += 32) {
-    const int ch = q / 7, w0 = (q - ch * 7) * 8;
-    uint32_t word[2];
-    if (ch < P + 2) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        uint32_t o = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t rel = e[w0 + 4 * h + j];
-          bool on;
-          if (ch < P) on = rel == (uint32_t)ch;                                            // one-hot player
-          else if (ch == P) on = teams ? (rel == 0u || rel == 2u) : rel == 0u;              // own team
-          else on = teams ? (rel == 1u || rel == 3u) : (rel >= 1u && rel < (uint32_t)P);   // opponents
-          o |= (uint32_t)on << (8 * j);
-        }
-        word[h] = o;
-      }
-    } else {
-      word[0] = word[1] = (uint32_t)e[kCells + ch] * 0x01010101u;
-    }
-    out[q] = make_uint2(word[0], word[1]);
-  }
+  det_obs_write(c, &senc[0][0], games, obs + (size_t)g0 * C * kCells, t, kWideBlock);
 }
 
 // ---- evaluation agents (MuZero_det_MADN/evaluate_agent.py) --------------------------------------------
@@ -458,18 +459,33 @@ __global__ __launch_bounds__(256) void k_det_policy(DetConsts c, muz_detmadn_soa
   action[g] = best;
 }
 
-// variant 0 = by batch size, 1 = one game per lane (k_det_round), 2 = one game per 32 lanes (k_det_round_wide).
-// The lane kernel needs >= 256 workgroups of 256 games to fill 256 CUs; below kWideMaxGames the wide one
-// spreads the same games over 32x the lanes (crossover measured: profiles/r3_env_variants.log).
+// variant 0 = by batch size, 1 = one game per lane (k_det_round), 2 / 3 / 4 / 5 = one game per 32 / 8 / 4 / 16
+// lanes (k_det_round_g).  The lane kernel needs >= 256 workgroups of 256 games to fill 256 CUs; below kWideMaxGames
+// the G-lane kernel spreads the same games over G x the lanes: G = 32 up to kWide32MaxGames, G = 4 above
+// (every variant at 4096 / 65 536 / 2^20 games: profiles/r3_env_variants.log).
+constexpr int kWide32MaxGames = 1 << 13;
 constexpr int kWideMaxGames = 1 << 16;
 static inline unsigned nblocks(int n, int b) { return (unsigned)((n + b - 1) / b); }
 
 int launch_det_round(const DetConsts& c, const muz_detmadn_soa& st, uint32_t* legal, unsigned long long seed, int turn,
                      int8_t* obs, int8_t* reward, uint8_t* done, int n, int variant, hipStream_t s) {
-  if (variant == 2 || (variant == 0 && n <= kWideMaxGames))
-    k_det_round_wide<<<nblocks(n, kWideGames), kWideBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
-  else
-    k_det_round<<<nblocks(n, kRoundBlock), kRoundBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
+  if (variant == 0) variant = n <= kWide32MaxGames ? 2 : n <= kWideMaxGames ? 4 : 1;
+  switch (variant) {
+    case 2:
+      k_det_round_g<32><<<nblocks(n, kWideBlock / 32), kWideBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
+      break;
+    case 3:
+      k_det_round_g<8><<<nblocks(n, kWideBlock / 8), kWideBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
+      break;
+    case 4:
+      k_det_round_g<4><<<nblocks(n, kWideBlock / 4), kWideBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
+      break;
+    case 5:
+      k_det_round_g<16><<<nblocks(n, kWideBlock / 16), kWideBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
+      break;
+    default:
+      k_det_round<<<nblocks(n, kRoundBlock), kRoundBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
+  }
   return muz_last_launch_error();
 }
 
@@ -560,7 +576,7 @@ int muz_detmadn_random_round(const muz_rules* rules, muz_detmadn_soa st, uint32_
   DetConsts c;
   int rc = make_det_consts(rules, &c);
   if (rc) return rc;
-  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && legal_bits);
+  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && legal_bits && ((uintptr_t)obs & 15u) == 0);
   if (n == 0) return MUZ_OK;
   return launch_det_round(c, st, legal_bits, seed, turn, obs, reward, done, n, 0, (hipStream_t)stream);
 }
@@ -571,7 +587,7 @@ int muz_detmadn_random_round_variant(const muz_rules* rules, muz_detmadn_soa st,
   DetConsts c;
   int rc = make_det_consts(rules, &c);
   if (rc) return rc;
-  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && legal_bits && variant >= 0 && variant <= 2);
+  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && legal_bits && ((uintptr_t)obs & 15u) == 0 && variant >= 0 && variant <= 5);
   if (n == 0) return MUZ_OK;
   return launch_det_round(c, st, legal_bits, seed, turn, obs, reward, done, n, variant, (hipStream_t)stream);
 }

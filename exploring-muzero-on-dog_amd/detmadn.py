@@ -241,8 +241,8 @@ def random_round(env: DetMADNState, legal: torch.Tensor, seed: int, turn: int, o
     """One env-step of uniform random legal play for every game (muz_detmadn_random_round): the k-th legal
     action of ``legal`` (int32 [B], updated in place to the next mask), env_step / no_step, in-place reset of
     finished games, and encode_board of the next state into ``obs`` (int8 [B, 8P+2, 56]) when given.
-    ``variant``: 0 = the kernel chosen by batch size, 1 = one game per lane, 2 = one game per 32 lanes (same
-    results)."""
+    ``variant``: 0 = the kernel chosen by batch size, 1 = one game per lane, 2 / 3 / 4 / 5 = one game per
+    32 / 8 / 4 / 16 lanes (same results)."""
     lib = _L.load()
     if variant == 0:
         rc = lib.muz_detmadn_random_round(env.rules, env.soa(), _L.ptr(legal), int(seed) & ((1 << 64) - 1), int(turn),

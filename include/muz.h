@@ -117,12 +117,12 @@ int muz_detmadn_encode_i8(const muz_rules* rules, muz_detmadn_soa state, int8_t*
  * round) and the next round's mask on exit; the action is the k-th legal one, k = floor(u * count), u =
  * (mix64(game_key(seed ^ 0xD37A11D0, g, turn)) >> 40) / 2^24; no_step when nothing is legal; a game that
  * finishes is reset in place (done[g] = 1 for that round).  obs (nullable) receives encode_board of the state
- * the next round acts on, int8 [n][8P+2][56].  Replaces the vmapped valid_action -> env_step / no_step ->
+ * the next round acts on, int8 [n][8P+2][56], 16-byte aligned (else MUZ_E_INVALID).  Replaces the vmapped valid_action -> env_step / no_step ->
  * encode_board sequence of MuZero_det_MADN/game_agent.py:84-119 (MADN/deterministic_madn.py:170-438). */
 int muz_detmadn_random_round(const muz_rules* rules, muz_detmadn_soa state, uint32_t* legal_bits, uint64_t seed,
                              int32_t turn, int8_t* obs, int8_t* reward, uint8_t* done, int32_t n, void* stream);
 /* The same round with the kernel chosen explicitly: variant 1 = one game per lane (k_det_round, for batches that
- * fill the GPU), 2 = one game per 32 lanes (k_det_round_wide, small batches), 0 = by batch size (as
+ * fill the GPU), 2 / 3 / 4 / 5 = one game per 32 / 8 / 4 / 16 lanes (k_det_round_g<G>), 0 = by batch size (as
  * muz_detmadn_random_round).  Identical results. */
 int muz_detmadn_random_round_variant(const muz_rules* rules, muz_detmadn_soa state, uint32_t* legal_bits,
                                      uint64_t seed, int32_t turn, int8_t* obs, int8_t* reward, uint8_t* done,

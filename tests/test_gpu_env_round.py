@@ -32,10 +32,11 @@ def oracle_round(envs, seed, turn, kw):
     return out
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("rule_set", ["selfplay_2p", "selfplay_4p_teams", "exotic_4p"])
 def test_random_round_matches_oracle(cuda, rule_set, variant):
-    """variant 1: one game per lane (k_det_round), 2: one game per 32 lanes (k_det_round_wide)."""
+    """variant 1: one game per lane (k_det_round), 2 / 3 / 4 / 5: one game per 32 / 8 / 4 / 16 lanes
+    (k_det_round_g)."""
     from exploring_muzero_on_dog_amd import detmadn as E
     kw = RULE_SETS[rule_set]
     B, seed, rounds = 48, 9, 400
@@ -64,7 +65,7 @@ def test_random_round_matches_oracle(cuda, rule_set, variant):
     assert finished > 0, "games must finish and restart within the rounds"
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
 def test_random_round_large_batch_properties(cuda, variant):
     """B = 2^20 games (the micro-benchmark's HBM-sized batch): the observation written by the fused kernel
     equals encode_board of the stored state, and the returned mask equals valid_action of it."""
@@ -78,3 +79,28 @@ def test_random_round_large_batch_properties(cuda, variant):
         E.random_round(env, legal, 3, t, obs=obs, variant=variant)
     assert torch.equal(obs, E.encode_board(env, dtype=torch.int8))
     assert torch.equal(legal, E.legal_bits(env))
+
+
+def test_random_round_variants_identical_ragged(cuda):
+    """Every kernel variant (one game per 1 / 32 / 8 / 4 / 16 lanes) leaves the same state, mask, observation,
+    rewards and done flags at a batch that fills no workgroup evenly (5001 games, 4p teams rules)."""
+    from exploring_muzero_on_dog_amd import detmadn as E
+    kw = RULE_SETS["selfplay_4p_teams"]
+    B = 5001
+    outs = []
+    for variant in (1, 2, 3, 4, 5):
+        env = E.env_reset(B, **kw)
+        legal = E.legal_bits(env)
+        C = E.num_channels(kw["num_players"])
+        obs = torch.empty((B, C, 56), dtype=torch.int8, device="cuda")
+        reward = torch.empty(B, dtype=torch.int8, device="cuda")
+        done = torch.empty(B, dtype=torch.uint8, device="cuda")
+        acc = torch.zeros(B, dtype=torch.int64, device="cuda")
+        for t in range(60):
+            E.random_round(env, legal, 11, t, obs=obs, reward=reward, done=done, variant=variant)
+            acc += reward.long() * (t + 1) + done.long() * 1000
+        outs.append((env.board.clone(), env.pins.clone(), env.action_set.clone(), env.current_player.clone(),
+                     legal.clone(), obs.clone(), acc))
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
