@@ -8,6 +8,10 @@
 //   z = y + bias;  Flax LayerNorm (eps 1e-6, fast variance E[z^2] - E[z]^2, as nn.hpp's ln16);
 //   o = (z - mean) * (rstd * gamma) + beta;  out = o (PLAIN) | relu(o) (RELU) | relu(res + o) (RESID_RELU).
 // Saved for the backward: z, mean, rstd and out (the ReLU mask).
+// FiLM variant (the first op of a dynamics trunk, muzero_deterministic_madn.py:421-427: LayerNorm_0 of the latent,
+// then x * (1 + scale) + shift): PLAIN LayerNorm without a bias, plus film = shift + out * scale1 (scale1 = 1 + scale);
+// its backward takes d(film) and writes dscale = d(film) * out beside the LayerNorm backward of d(film) * scale1
+// (one launch each way instead of LayerNorm + addcmul and two multiplies + LayerNorm backward).
 // Backward: do = dout (PLAIN) or dout * (out > 0); dres = do (RESID_RELU);
 //   xhat = (z - mean) * rstd, g = do * gamma,
 //   dz = rstd * (g - mean_n(g) - xhat * mean_n(g * xhat))       (= dy, and its column sum is dbias),
@@ -27,12 +31,14 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-template <int N>
+template <int N, bool FILM = false>
 __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ y, const float* __restrict__ bias,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 const float* __restrict__ res, int M, int mode, float* __restrict__ out,
                                                 float* __restrict__ z, float* __restrict__ mean_out,
-                                                float* __restrict__ rstd_out) {
+                                                float* __restrict__ rstd_out, const float* __restrict__ scale1 = nullptr,
+                                                const float* __restrict__ shift = nullptr,
+                                                float* __restrict__ film = nullptr) {
   constexpr int E = (N + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -43,7 +49,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ y, con
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const int c = lane + 64 * i;
-    v[i] = c < N ? y[row + c] + bias[c] : 0.f;
+    v[i] = c < N ? (FILM ? y[row + c] : y[row + c] + bias[c]) : 0.f;
     s += v[i];
     s2 += v[i] * v[i];
   }
@@ -60,6 +66,13 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ y, con
     if (mode == LN_MODE_RESID_RELU) o = fmaxf(res[row + c] + o, 0.f);
     out[row + c] = o;
     z[row + c] = v[i];
+    // rounded as torch's addcmul (a multiply, then an add; no fma), so the chain node and the per-step graph
+    // see the same bits: min-max's extremum columns (and where their gradient goes) depend on the last ulp
+    if constexpr (FILM) {
+      float p = o * scale1[row + c];
+      asm volatile("" : "+v"(p));   // keeps the multiply out of an fma with the add
+      film[row + c] = shift[row + c] + p;
+    }
   }
   if (lane == 0) {
     mean_out[m] = mean;
@@ -67,12 +80,13 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ y, con
   }
 }
 
-template <int N>
+template <int N, bool FILM = false>
 __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dout, const float* __restrict__ out,
                                                 const float* __restrict__ z, const float* __restrict__ mean_in,
                                                 const float* __restrict__ rstd_in, const float* __restrict__ gamma,
                                                 int M, int mode, float* __restrict__ dz, float* __restrict__ dres,
-                                                float* __restrict__ part) {
+                                                float* __restrict__ part, const float* __restrict__ scale1 = nullptr,
+                                                float* __restrict__ dscale = nullptr) {
   constexpr int E = (N + 63) / 64;
   __shared__ float red[4][3][N];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -92,6 +106,10 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dout, 
       d[i] = xh[i] = g[i] = 0.f;
       if (c >= N) continue;
       float t = dout[row + c];
+      if constexpr (FILM) {
+        dscale[row + c] = t * out[row + c];
+        t = t * scale1[row + c];
+      }
       if (mode != LN_MODE_PLAIN && !(out[row + c] > 0.f)) t = 0.f;
       if (mode == LN_MODE_RESID_RELU) dres[row + c] = t;
       d[i] = t;
@@ -344,6 +362,27 @@ int muz_ln_bwd(const float* dout, const float* out, const float* z, const float*
   const int rc = muz_ln_bwd_rows(dout, out, z, mean, rstd, gamma, M, N, mode, dz, dres, scratch, stream);
   if (rc) return rc;
   return muz_ln_colsum(scratch, muz_ln_bwd_scratch_floats(M, N) / (3 * N), N, dgamma, dbeta, dbias, stream);
+}
+
+int muz_ln_film_fwd(const float* x, const float* gamma, const float* beta, const float* scale1, const float* shift,
+                    int32_t M, int32_t N, float* out, float* z, float* mean, float* rstd, float* film, void* stream) {
+  if (N != 256) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(M >= 0 && x && gamma && beta && scale1 && shift && out && z && mean && rstd && film);
+  if (M == 0) return MUZ_OK;
+  k_ln_fwd<256, true><<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(x, nullptr, gamma, beta, nullptr, M, LN_MODE_PLAIN,
+                                                                    out, z, mean, rstd, scale1, shift, film);
+  return muz_last_launch_error();
+}
+
+int muz_ln_film_bwd_rows(const float* dfilm, const float* out, const float* z, const float* mean, const float* rstd,
+                         const float* gamma, const float* scale1, int32_t M, int32_t N, float* dz, float* dscale,
+                         float* scratch, void* stream) {
+  if (N != 256) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(M >= 0 && dfilm && out && z && mean && rstd && gamma && scale1 && dz && dscale && scratch);
+  if (M == 0) return MUZ_OK;
+  k_ln_bwd<256, true><<<(M + kLnRowsPerBlock - 1) / kLnRowsPerBlock, 256, 0, (hipStream_t)stream>>>(
+      dfilm, out, z, mean, rstd, gamma, M, LN_MODE_PLAIN, dz, nullptr, scratch, scale1, dscale);
+  return muz_last_launch_error();
 }
 
 int muz_minmax_fwd(const float* x, const float* y, const float* bias, int32_t M, int32_t N, float* out, float* q,

@@ -267,6 +267,31 @@ def _ln_bwd_rows(dout, fwd, gamma, mode, scratch, dz=None):
     return dz, dres
 
 
+def _ln_film_fwd(x, gamma, beta, scale1, shift, film):
+    """LayerNorm_0 + FiLM of a dynamics trunk in one launch (muz_ln_film_fwd): film <- shift + LN(x) * scale1;
+    -> (out = LN(x), z, mean, rstd) for the backward, like _ln_fwd."""
+    M, Nn = x.shape
+    out, z = torch.empty_like(x), torch.empty_like(x)
+    mean = torch.empty((M,), dtype=x.dtype, device=x.device)
+    rstd = torch.empty_like(mean)
+    _L.check(_L.load().muz_ln_film_fwd(_L.ptr(x), _L.ptr(gamma), _L.ptr(beta), _L.ptr(scale1.contiguous()),
+                                       _L.ptr(shift.contiguous()), M, Nn, _L.ptr(out), _L.ptr(z), _L.ptr(mean),
+                                       _L.ptr(rstd), _L.ptr(film), _L.stream_ptr()), "muz_ln_film_fwd")
+    return out, z, mean, rstd
+
+
+def _ln_film_bwd_rows(dfilm, fwd, gamma, scale1, scratch, dscale):
+    """Backward row half of _ln_film_fwd (muz_ln_film_bwd_rows): dscale <- d(film) * LN(x); -> dz of the
+    LayerNorm input; column partials into scratch."""
+    out, z, mean, rstd = fwd
+    M, Nn = out.shape
+    dz = torch.empty_like(out)
+    _L.check(_L.load().muz_ln_film_bwd_rows(_L.ptr(dfilm.contiguous()), _L.ptr(out), _L.ptr(z), _L.ptr(mean),
+                                            _L.ptr(rstd), _L.ptr(gamma), _L.ptr(scale1.contiguous()), M, Nn, _L.ptr(dz),
+                                            _L.ptr(dscale), _L.ptr(scratch), _L.stream_ptr()), "muz_ln_film_bwd_rows")
+    return dz
+
+
 def _ln_colsum(scratch, Nn):
     """-> (dgamma, dbeta, dbias) from the column partials of any number of row-half calls."""
     dg, db_, dbias = (torch.empty((Nn,), dtype=scratch.dtype, device=scratch.device) for _ in range(3))
@@ -412,6 +437,7 @@ def trunk_param_names(kind: str = "det") -> list:
 
 DYN_TRUNK_PARAMS = tuple(trunk_param_names("det"))
 CHAIN = True                     # False: the losses build the per-step autograd graph instead (A/B timing)
+FUSED_FILM = True                # False: a trunk's LayerNorm_0 + FiLM as LayerNorm + addcmul (A/B, diagnosis)
 _NP = len(DYN_TRUNK_PARAMS)      # 28 per trunk
 
 
@@ -455,7 +481,6 @@ class _TrunkChain(torch.autograd.Function):
         if len(apps) != T or len(scaled) != T or len(P) != _NP * (max(apps) + 1):
             raise ValueError("apps / scaled / parameters do not match the FiLM rows")
         dev, dt = latent0.device, latent0.dtype
-        zero = torch.zeros((Nn,), dtype=dt, device=dev)
         outs = torch.empty((T, B, Nn), dtype=dt, device=dev)
         qs = torch.empty((T, B, Nn), dtype=dt, device=dev)                  # min-max inputs and their extrema
         lohi = torch.empty((T, B, 2), dtype=dt, device=dev)
@@ -474,8 +499,12 @@ class _TrunkChain(torch.autograd.Function):
             g, j = apps[i], slot[i]
             Q = P[_NP * g:_NP * (g + 1)]
             g0, be0, W3, b3, g1, be1, W4, b4, g2, be2 = Q[:10]
-            f0 = _ln_fwd(lat, zero, g0, be0, None, LN_PLAIN)
-            x0 = torch.addcmul(shift[i], f0[0], scale1[i], out=X[(g, "3")][j])
+            x0 = X[(g, "3")][j]
+            if FUSED_FILM:    # LayerNorm_0 + FiLM, one launch
+                f0 = _ln_film_fwd(lat, g0, be0, scale1[i], shift[i], x0)
+            else:
+                f0 = _ln_fwd(lat, torch.zeros_like(g0), g0, be0, None, LN_PLAIN)
+                torch.addcmul(shift[i], f0[0], scale1[i], out=x0)
             f3 = _dense_ln_fwd(x0, W3, b3, g1, be1, None, LN_RELU, out=X[(g, "4")][j])
             f4 = _dense_ln_fwd(f3[0], W4, b4, g2, be2, None, LN_RELU, out=X[(g, "a0")][j])
             x, rbs = f4[0], []
@@ -531,8 +560,11 @@ class _TrunkChain(torch.autograd.Function):
                 _, _, dx = _dense_ln_bwd(t, fa, ga, LN_RELU, Wa, scr[(g, f"a{r}")][j], DZ[(g, f"a{r}")][j], acc=dres)
             _, _, t = _dense_ln_bwd(dx, f4, Q[8], LN_RELU, Q[6], scr[(g, "4")][j], DZ[(g, "4")][j])
             _, _, dx0 = _dense_ln_bwd(t, f3, Q[4], LN_RELU, Q[2], scr[(g, "3")][j], DZ[(g, "3")][j], dx_out=dshift[i])
-            torch.mul(dx0, f0[0], out=dscale[i])
-            dz0, _ = _ln_bwd_rows(dx0 * scale1[i], f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
+            if FUSED_FILM:
+                dz0 = _ln_film_bwd_rows(dx0, f0, Q[0], scale1[i], scr[(g, "0")][j], dscale[i])
+            else:
+                torch.mul(dx0, f0[0], out=dscale[i])
+                dz0, _ = _ln_bwd_rows(dx0 * scale1[i], f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
             ca, cb = dz0, dq
         grads = [None] * len(P)
         sink = _sink()
@@ -1008,11 +1040,18 @@ class Learner:
             self._g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g):
                 self._out = self._step(self._static)
+                # the losses packed into one buffer inside the graph, so a replay hands them out with one copy
+                self._packed = torch.stack(list(self._out.values()))
         for k in self.KEYS:
             self._static[k].copy_(batch[k])
         self._g.replay()
-        # the captured outputs are overwritten by the next replay: hand out copies so a caller may keep them
-        return {k: v.clone() for k, v in self._out.items()}
+        return self._outputs()
+
+    def _outputs(self) -> dict:
+        """The captured losses are overwritten by the next replay: one copy of the packed buffer, handed out as
+        per-key views so a caller may keep them."""
+        c = self._packed.clone()
+        return {k: c[i] for i, k in enumerate(self._out)}
 
     def train_step_from(self, ring) -> dict:
         """train_step on the next batch of a device ring (``ring.sample_batch()``).  Once the step is captured,
@@ -1027,7 +1066,7 @@ class Learner:
                 self._static_full = True
             ring.sample_at(ep, t, out=self._static)
             self._g.replay()
-            return {k: v.clone() for k, v in self._out.items()}
+            return self._outputs()
         return self.train_step(ring.sample_batch())
 
     def push_to(self, net: "N.DeviceNet"):

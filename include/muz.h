@@ -680,6 +680,15 @@ int muz_ln_colsum(const float* scratch, int64_t nblk, int32_t N, float* dgamma, 
 int muz_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
                const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
                float* dgamma, float* dbeta, float* dbias, void* stream);
+/* The FiLM input of a dynamics trunk (muzero_deterministic_madn.py:421-427; learner._TrunkChain): out = LayerNorm(x)
+ * (Flax, eps 1e-6, no bias), film = shift + out * scale1 (scale1 = 1 + FiLM scale), saving z / mean / rstd like
+ * muz_ln_fwd; and its backward half from d(film): dscale = d(film) * out and the LayerNorm row backward of
+ * d(film) * scale1 (dz, column partials into scratch as muz_ln_bwd_rows, LN_PLAIN).  N = 256. */
+int muz_ln_film_fwd(const float* x, const float* gamma, const float* beta, const float* scale1, const float* shift,
+                    int32_t M, int32_t N, float* out, float* z, float* mean, float* rstd, float* film, void* stream);
+int muz_ln_film_bwd_rows(const float* dfilm, const float* out, const float* z, const float* mean, const float* rstd,
+                         const float* gamma, const float* scale1, int32_t M, int32_t N, float* dz, float* dscale,
+                         float* scratch, void* stream);
 /* Min-max latent scaling closing a dynamics trunk, N = 256: q = x + (y + bias), out = (q - min) /
  * (max - min + 1e-8) per row; saves q [M][N], lohi [M][2] (min, max) and idx [M][2] (their columns, lowest on
  * ties).  Backward: dq from d = (g + (a + b)) x (scale if scaled) + h (a, b both null or both given; h

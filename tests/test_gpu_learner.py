@@ -200,6 +200,47 @@ def test_fused_dense_layernorm_matches_float64_autograd(cuda, N, mode):
         close(gg, gr, name)
 
 
+def test_ln_film_kernels_match_float64_autograd(cuda):
+    """muz_ln_film_fwd / muz_ln_film_bwd_rows (a dynamics trunk's LayerNorm_0 + FiLM in one launch each way,
+    muzero_deterministic_madn.py:421-427) against float64 autograd of LN(x) * (1 + scale) + shift; M = 301 rows
+    (a partial backward block)."""
+    _, _, L, _, _ = _mods()
+    g = torch.Generator().manual_seed(21)
+    M, N = 301, 256
+    x, scale, shift, dfilm = (torch.randn(M, N, generator=g, dtype=torch.float64) * s for s in (1.0, 0.3, 0.3, 1.0))
+    gam, bet = (torch.randn(N, generator=g, dtype=torch.float64) * s for s in (1.0, 0.3))
+    leaves = [t.clone().requires_grad_(True) for t in (x, scale, shift, gam, bet)]
+    xl, sl, hl, gl, bl = leaves
+    mean = xl.mean(-1, keepdim=True)
+    var = (xl * xl).mean(-1, keepdim=True) - mean * mean
+    y = (xl - mean) / torch.sqrt(var + 1e-6) * gl + bl
+    ref = y * (1.0 + sl) + hl
+    grads_ref = torch.autograd.grad(ref, leaves, dfilm)
+    d = {k: v.float().cuda() for k, v in dict(x=x, s1=1.0 + scale, sh=shift, gam=gam, bet=bet, df=dfilm).items()}
+    film = torch.empty(M, N, device="cuda")
+    fwd = L._ln_film_fwd(d["x"], d["gam"], d["bet"], d["s1"], d["sh"], film)
+    scratch = torch.empty((L._L.load().muz_ln_bwd_scratch_floats(M, N),), device="cuda")
+    dscale = torch.empty(M, N, device="cuda")
+    dz = L._ln_film_bwd_rows(d["df"], fwd, d["gam"], d["s1"], scratch, dscale)
+    dgam, dbet, _ = L._ln_colsum(scratch, N)
+    torch.cuda.synchronize()
+
+    def close(a, r, what):
+        a = a.detach().double().cpu()
+        err = (a - r).abs().max().item() / max(1.0, r.abs().max().item())
+        assert err < 2e-5, f"{what}: relative error {err:.2e}"
+    close(film, ref.detach(), "film")
+    close(fwd[0], y.detach(), "LayerNorm output")
+    # bit-identical to the unfused form (LayerNorm kernel + torch.addcmul, the per-step graph's rounding): the
+    # min-max extremum columns downstream depend on the last ulp
+    ref_fwd = L._ln_fwd(d["x"], torch.zeros_like(d["gam"]), d["gam"], d["bet"], None, L.LN_PLAIN)
+    assert all(torch.equal(a, b) for a, b in zip(fwd, ref_fwd))
+    assert torch.equal(film, torch.addcmul(d["sh"], ref_fwd[0], d["s1"]))
+    for name, a, r in (("dx", dz, grads_ref[0]), ("dscale", dscale, grads_ref[1]), ("dgamma", dgam, grads_ref[3]),
+                       ("dbeta", dbet, grads_ref[4])):
+        close(a, r, name)
+
+
 def test_dynamics_chain_node_matches_per_step_autograd(cuda):
     """learner._TrunkChain (the K-step latent chain as one autograd node, batched weight gradients) against the
     per-step graph of the same layers (loss_fn's CPU-style loop run on the GPU): forward within 1e-5, gradients
