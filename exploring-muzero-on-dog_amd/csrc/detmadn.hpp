@@ -212,6 +212,114 @@ __device__ __forceinline__ uint32_t det_legal(const DetConsts& c, const DetLane&
   return mask & col;
 }
 
+// The legality mask of a game held in LDS by G lanes (G = 4, 8, 16 or 32; lane a of the game, t = threadIdx.x):
+// lane a checks actions a, a + G, ... (legal_one) and each ballot delivers the game's G bits.  Every lane of the
+// game must call it; lanes of other games in the wave may be inactive (they contribute zero bits).
+template <int G>
+__device__ __forceinline__ uint32_t det_legal_g(const DetConsts& c, const LdsLane& s, const BoardView& b, int a, int t) {
+  static_assert(G == 4 || G == 8 || G == 16 || G == 32, "lanes per game");
+  const LegalCtx x = legal_ctx(c, s, b);
+  const int gw = (t & 63) / G;   // this game's slot in the wave
+  uint32_t mask = 0;
+#pragma unroll
+  for (int it = 0; it < (24 + G - 1) / G; ++it) {
+    const int act = a + G * it;
+    const int i = act / 6, m = act % 6 + 1;
+    const bool ok = act < 24 && legal_one(c, b, x, pin_of(s, x.cp, i < 4 ? i : 0), m) && ((x.avail >> (m - 1)) & 1u);
+    const unsigned long long bal = __ballot(ok);
+    mask |= (uint32_t)((bal >> (G * gw)) & ((1ull << G) - 1ull)) << (G * it);
+  }
+  return mask & 0xFFFFFFu;
+}
+
+// `games` consecutive games' SoA rows (from game g0) to LDS, transposed per game: board[gi][cell] and the
+// state row [gi][kStateRow] (pins [0, 16), action set [16, 40), cp 40, done 41, reward 42); consecutive threads
+// on consecutive games of one SoA row, so the global loads are coalesced.  det_rows_store is the way back.
+constexpr int kStateRow = 48;
+template <int NG>
+__device__ __forceinline__ void det_rows_load(const DetConsts& c, const muz_detmadn_soa& st, int g0, int games,
+                                              int8_t (*sboard)[kCells], int8_t (*sstate)[kStateRow], int t, int nt) {
+  const int S = st.stride, P = c.P;
+  for (int i = t; i < kCells * NG; i += nt) {
+    const int row = i / NG, gi = i - row * NG;
+    if (gi < games) sboard[gi][row] = st.board[row * S + g0 + gi];
+  }
+  for (int i = t; i < kStateRow * NG; i += nt) {
+    const int row = i / NG, gi = i - row * NG;
+    if (gi >= games) continue;
+    int8_t v = 0;
+    if (row < 16) v = row < 4 * P ? st.pins[row * S + g0 + gi] : (int8_t)-1;
+    else if (row < 40) v = row - 16 < 6 * P ? st.action_set[(row - 16) * S + g0 + gi] : (int8_t)0;
+    else if (row == 40) v = st.current_player[g0 + gi];
+    else if (row == 41) v = st.done[g0 + gi] ? 1 : 0;
+    else if (row == 42) v = st.reward[g0 + gi];
+    sstate[gi][row] = v;
+  }
+}
+template <int NG>
+__device__ __forceinline__ void det_rows_store(const DetConsts& c, const muz_detmadn_soa& st, int g0, int games,
+                                               const int8_t (*sboard)[kCells], const int8_t (*sstate)[kStateRow],
+                                               int t, int nt) {
+  const int S = st.stride, P = c.P;
+  for (int i = t; i < kCells * NG; i += nt) {
+    const int row = i / NG, gi = i - row * NG;
+    if (gi < games) st.board[row * S + g0 + gi] = sboard[gi][row];
+  }
+  for (int i = t; i < kStateRow * NG; i += nt) {
+    const int row = i / NG, gi = i - row * NG;
+    if (gi >= games) continue;
+    const int8_t v = sstate[gi][row];
+    if (row < 16) {
+      if (row < 4 * P) st.pins[row * S + g0 + gi] = v;
+    } else if (row < 40) {
+      if (row - 16 < 6 * P) st.action_set[(row - 16) * S + g0 + gi] = v;
+    } else if (row == 40) {
+      st.current_player[g0 + gi] = v;
+    } else if (row == 41) {
+      st.done[g0 + gi] = (uint8_t)v;
+    } else if (row == 42) {
+      st.reward[g0 + gi] = v;
+    }
+  }
+}
+
+constexpr int kEncStride = 96;   // per game: rel[56] + constant channel values at [56 + ch]
+// Observation bytes from a staged game (the env rounds' phase 2, the self-play encode): per game at
+// senc + gl * kEncStride, rel[56] = the rolled cell's owner relative to the current player (kRelEmpty for an empty
+// cell), then the constant channels' values at [56 + ch] (det_enc_stage).  A game's C x 56 = 16 (28P + 7) bytes
+// split into halves of 8 cells of one channel (56 = 7 x 8), two per 16-byte chunk.  A board channel's 4 output bytes are ONE byte permute of the 4 staged rel bytes through the
+// channel's 4-entry table (byte r = 1 if relative owner r is on the channel); kRelEmpty = 12 is v_perm_b32's
+// constant-zero selector.  (Per-byte predicates compiled to ~700 divergent-branch instructions per chunk and
+// made this phase ~80 % of the launch: profiles/r3_env_breakdown.log.)
+constexpr uint32_t kRelEmpty = 12u;
+__device__ __forceinline__ uint32_t det_obs_table(int ch, int P, bool teams) {
+  const uint32_t player = 1u << (8 * (ch & 3));                                        // ch < P: one-hot
+  const uint32_t own = teams ? 0x00010001u : 0x00000001u;                              // ch == P
+  const uint32_t opp = teams ? 0x01000100u : (P == 2 ? 0x00000100u : P == 3 ? 0x00010100u : 0x01010100u);
+  return ch < P ? player : ch == P ? own : opp;
+}
+__device__ __forceinline__ uint2 det_obs_half(const uint8_t* e, int m, int P, bool teams) {
+  const int ch = m / 7, w0 = (m - ch * 7) * 8;
+  const uint2 rw = *reinterpret_cast<const uint2*>(e + w0);
+  const uint32_t tab = det_obs_table(ch, P, teams);
+  const uint32_t cv = (uint32_t)e[kCells + ch] * 0x01010101u;   // constant channel (ignored below P + 2)
+  const bool board = ch < P + 2;
+  return make_uint2(board ? __builtin_amdgcn_perm(0u, tab, rw.x) : cv, board ? __builtin_amdgcn_perm(0u, tab, rw.y) : cv);
+}
+// Stage one game's encode inputs into e (kEncStride bytes) with G lanes (lane a: cells a, a + G, ... and constant
+// channels P + 2 + a, ...): encode_board (deterministic_madn.py:395-438) split into the board part and the rest.
+template <int G, class Lane>
+__device__ __forceinline__ void det_enc_stage(const DetConsts& c, const Lane& s, const BoardView& b, uint8_t* e, int a) {
+  const int P = c.P, C = 8 * P + 2;
+  for (int w = a; w < kCells; w += G) {
+    const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
+    const int v = b.at(src);
+    e[w] = v < 0 ? (uint8_t)kRelEmpty : (uint8_t)((v - s.cp + P) % P);
+  }
+  auto none = [](int) { return 0; };
+  for (int ch = P + 2 + a; ch < C; ch += G) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
+}
+
 // set_pins_on_board (deterministic_madn.py:259-271) into the lane's LDS board.
 template <class Lane>
 __device__ __forceinline__ void rebuild_board(const DetConsts& c, const Lane& s, const BoardView& b) {

@@ -109,32 +109,9 @@ __global__ __launch_bounds__(64) void k_det_encode(DetConsts c, muz_detmadn_soa 
 // 256 x C x 56 contiguous observation bytes as 16-byte chunks, consecutive threads on consecutive chunks.
 constexpr int kRoundBlock = 256;
 constexpr unsigned long long kDetRandomStream = 0xD37A11D0ull;
-constexpr int kEncStride = 96;   // per game: rel[56] + constant channel values at [56 + ch]
 
-// Phase 2 of the env rounds: `games` consecutive games' int8 observations (C x 56 bytes each, contiguous in
-// `out`) from their staged encode inputs (per game at senc + gl * kEncStride: rel[56] = the rolled cell's owner
-// relative to the current player, kRelEmpty for an empty cell, then the constant channels' values at [56 + ch]).
-// One 16-byte store per thread and iteration, consecutive threads on consecutive 16-byte chunks (1 KB per
-// wave-instruction): a game's C x 56 = 16 (28P + 7) bytes split into halves of 8 cells of one channel (56 = 7 x 8),
-// two per chunk.  A board channel's 4 output bytes are ONE byte permute of the 4 staged rel bytes through the
-// channel's 4-entry table (byte r = 1 if relative owner r is on the channel); kRelEmpty = 12 is v_perm_b32's
-// constant-zero selector.  (Per-byte predicates compiled to ~700 divergent-branch instructions per chunk and
-// made this phase ~80 % of the launch: profiles/r3_env_breakdown.log.)
-constexpr uint32_t kRelEmpty = 12u;
-__device__ __forceinline__ uint32_t det_obs_table(int ch, int P, bool teams) {
-  const uint32_t player = 1u << (8 * (ch & 3));                                        // ch < P: one-hot
-  const uint32_t own = teams ? 0x00010001u : 0x00000001u;                              // ch == P
-  const uint32_t opp = teams ? 0x01000100u : (P == 2 ? 0x00000100u : P == 3 ? 0x00010100u : 0x01010100u);
-  return ch < P ? player : ch == P ? own : opp;
-}
-__device__ __forceinline__ uint2 det_obs_half(const uint8_t* e, int m, int P, bool teams) {
-  const int ch = m / 7, w0 = (m - ch * 7) * 8;
-  const uint2 rw = *reinterpret_cast<const uint2*>(e + w0);
-  const uint32_t tab = det_obs_table(ch, P, teams);
-  const uint32_t cv = (uint32_t)e[kCells + ch] * 0x01010101u;   // constant channel (ignored below P + 2)
-  const bool board = ch < P + 2;
-  return make_uint2(board ? __builtin_amdgcn_perm(0u, tab, rw.x) : cv, board ? __builtin_amdgcn_perm(0u, tab, rw.y) : cv);
-}
+// Phase 2 of the env rounds (the staging and chunk helpers are in detmadn.hpp): `games` consecutive games'
+// int8 observations, contiguous in `out`, one 16-byte chunk per thread and iteration.
 __device__ __forceinline__ void det_obs_write(const DetConsts& c, const uint8_t* senc, int games, int8_t* out, int t,
                                               int nthreads) {
   const int P = c.P, C = 8 * P + 2;
@@ -228,7 +205,6 @@ __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detm
 // ... of the encode, and the workgroup writes the state rows back and its NG x C x 56 contiguous observation bytes
 // as 8-byte chunks, both fully coalesced.  Same results, bit for bit.
 constexpr int kWideBlock = 256;
-constexpr int kStateRow = 48;   // per game in LDS: pins [0, 16), action set [16, 40), cp 40, done 41, reward 42, r 43
 
 template <int G>
 __global__ __launch_bounds__(kWideBlock) void k_det_round_g(DetConsts c, muz_detmadn_soa st, uint32_t* legal,
@@ -245,23 +221,8 @@ __global__ __launch_bounds__(kWideBlock) void k_det_round_g(DetConsts c, muz_det
   const int games = min(NG, n - g0);
   const int g = g0 + lg;
   const bool valid = lg < games;   // uniform over the game's G lanes
-  const int S = st.stride, P = c.P, C = 8 * P + 2;
-  // SoA rows -> LDS: consecutive threads on consecutive games of one row (coalesced), transposed per game
-  for (int i = t; i < kCells * NG; i += kWideBlock) {
-    const int row = i / NG, gi = i - row * NG;
-    if (gi < games) sboard[gi][row] = st.board[row * S + g0 + gi];
-  }
-  for (int i = t; i < kStateRow * NG; i += kWideBlock) {
-    const int row = i / NG, gi = i - row * NG;
-    if (gi >= games) continue;
-    int8_t v = 0;
-    if (row < 16) v = row < 4 * P ? st.pins[row * S + g0 + gi] : (int8_t)-1;
-    else if (row < 40) v = row - 16 < 6 * P ? st.action_set[(row - 16) * S + g0 + gi] : (int8_t)0;
-    else if (row == 40) v = st.current_player[g0 + gi];
-    else if (row == 41) v = st.done[g0 + gi] ? 1 : 0;
-    else if (row == 42) v = st.reward[g0 + gi];
-    sstate[gi][row] = v;
-  }
+  const int P = c.P, C = 8 * P + 2;
+  det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kWideBlock);
   int8_t* sp = sstate[lg];
   const BoardView b{sboard[lg], 1};
   const uint32_t lb = valid ? legal[g] : 0u;
@@ -304,54 +265,15 @@ __global__ __launch_bounds__(kWideBlock) void k_det_round_g(DetConsts c, muz_det
   __syncthreads();
   if (valid) {
     const LdsLane s{sp, sp[40], 0, 0};
-    // next legal mask: lane a checks actions a + G * it = (pin / 6, move % 6 + 1); the game's G bits of each ballot
-    const LegalCtx x = legal_ctx(c, s, b);
-    const int gw = (t & 63) / G;   // this game's slot in the wave
-    uint32_t mask = 0;
-#pragma unroll
-    for (int it = 0; it < (24 + G - 1) / G; ++it) {
-      const int act = a + G * it;
-      const int i = act / 6, m = act % 6 + 1;
-      const bool ok = act < 24 && legal_one(c, b, x, pin_of(s, x.cp, i < 4 ? i : 0), m) && ((x.avail >> (m - 1)) & 1u);
-      const unsigned long long bal = __ballot(ok);
-      mask |= (uint32_t)((bal >> (G * gw)) & ((1ull << G) - 1ull)) << (G * it);
-    }
-    if (a == 0) legal[g] = mask & 0xFFFFFFu;
+    // next legal mask: lane a checks actions a, a + G, ...; the game's G bits of each ballot
+    const uint32_t mask = det_legal_g<G>(c, s, b, a, t);
+    if (a == 0) legal[g] = mask;
     // encode staging: rolled cells' owner relative to cp, constant channels
-    if (obs) {
-      uint8_t* e = senc[lg];
-      for (int w = a; w < kCells; w += G) {
-        const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
-        const int v = b.at(src);
-        e[w] = v < 0 ? (uint8_t)kRelEmpty : (uint8_t)((v - s.cp + P) % P);
-      }
-      auto none = [](int) { return 0; };
-      for (int ch = P + 2 + a; ch < C; ch += G) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
-    }
+    if (obs) det_enc_stage<G>(c, s, b, senc[lg], a);
   }
   // (lanes of invalid games, last workgroup only, skip the ballots: inactive lanes contribute zero bits)
   __syncthreads();
-  // LDS -> SoA rows, coalesced as on the way in
-  for (int i = t; i < kCells * NG; i += kWideBlock) {
-    const int row = i / NG, gi = i - row * NG;
-    if (gi < games) st.board[row * S + g0 + gi] = sboard[gi][row];
-  }
-  for (int i = t; i < kStateRow * NG; i += kWideBlock) {
-    const int row = i / NG, gi = i - row * NG;
-    if (gi >= games) continue;
-    const int8_t v = sstate[gi][row];
-    if (row < 16) {
-      if (row < 4 * P) st.pins[row * S + g0 + gi] = v;
-    } else if (row < 40) {
-      if (row - 16 < 6 * P) st.action_set[(row - 16) * S + g0 + gi] = v;
-    } else if (row == 40) {
-      st.current_player[g0 + gi] = v;
-    } else if (row == 41) {
-      st.done[g0 + gi] = (uint8_t)v;
-    } else if (row == 42) {
-      st.reward[g0 + gi] = v;
-    }
-  }
+  det_rows_store<NG>(c, st, g0, games, sboard, sstate, t, kWideBlock);   // LDS -> SoA rows, coalesced
   if (!obs) return;
   det_obs_write(c, &senc[0][0], games, obs + (size_t)g0 * C * kCells, t, kWideBlock);
 }

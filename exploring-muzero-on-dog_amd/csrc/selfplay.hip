@@ -21,117 +21,154 @@ namespace muz {
 // lane kernels' workgroup size; 64 / 128 measured within noise of 256 (profiles/r1g_sp_block_ab.log)
 constexpr int kSpBlock = 256;
 
+// Legal masks + flags of every lane, one game per kFlagLanes lanes (a lane per game would leave a 4096-game batch
+// on 16 of 256 CUs, its launch one lane's 24 serial legality checks): the workgroup copies its games' SoA rows into
+// LDS (coalesced), and each game's lanes run its checks in parallel (det_legal_g, one ballot per 32 actions).
 // lane_game (streaming driver only): game number of each lane, -1 = idle; a game whose record is full
 // (idx == T, the reference's max_steps) stops like a finished one.
-__global__ __launch_bounds__(kSpBlock) void k_sp_flags(DetConsts c, muz_detmadn_soa st, uint32_t* legal, int32_t* flag,
-                                                       int n, const int32_t* lane_game, const int32_t* idx, int T) {
-  __shared__ int8_t sboard[kCells * kSpBlock];
-  const int g = blockIdx.x * kSpBlock + threadIdx.x;
-  if (g >= n) return;
-  if (st.done[g] || (lane_game && (lane_game[g] < 0 || idx[lane_game[g]] >= T))) {
-    flag[g] = 0;
-    legal[g] = 0;
+constexpr int kFlagLanes = 32;
+__global__ __launch_bounds__(kSpBlock) void k_sp_flags_g(DetConsts c, muz_detmadn_soa st, uint32_t* legal,
+                                                         int32_t* flag, int n, const int32_t* lane_game,
+                                                         const int32_t* idx, int T) {
+  constexpr int G = kFlagLanes, NG = kSpBlock / G;
+  __shared__ int8_t sboard[NG][kCells];
+  __shared__ int8_t sstate[NG][kStateRow];
+  const int t = threadIdx.x, lg = t / G, a = t % G;
+  const int g0 = blockIdx.x * NG, games = min(NG, n - g0), g = g0 + lg;
+  det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
+  __syncthreads();
+  if (lg >= games) return;   // (uniform over a game's lanes)
+  if (sstate[lg][41] || (lane_game && (lane_game[g] < 0 || idx[lane_game[g]] >= T))) {
+    if (a == 0) {
+      flag[g] = 0;
+      legal[g] = 0;
+    }
     return;
   }
-  BoardView b{sboard + threadIdx.x, kSpBlock};
-  DetLane s;
-  det_load(c, st, g, s, b);
-  const uint32_t l = det_legal(c, s, b);
-  legal[g] = l;
-  flag[g] = l ? 1 : 2;   // 1: search + env_step, 2: no legal move -> no_step (game_agent.py:119)
-}
-
-// Observation of every searching game (compacted order) + its int8 trajectory record.
-__global__ __launch_bounds__(64) void k_sp_encode(DetConsts c, muz_detmadn_soa st, const int32_t* list,
-                                                  const int32_t* counts, const uint32_t* legal, uint32_t* legal_c,
-                                                  float* obs, int8_t* traj_obs, const int32_t* idx, int T,
-                                                  const int32_t* lane_game) {
-  const int sl = blockIdx.x;
-  if (sl >= counts[0]) return;
-  const int w = threadIdx.x;
-  if (w >= kCells) return;
-  const int g = list[sl];
-  if (w == 0) legal_c[sl] = legal[g];
-  const int S = st.stride;
-  DetLane s;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int v = st.pins[min(j, c.P * 4 - 1) * S + g];
-    s.pins[j] = (j < c.P * 4) ? v : -1;
-  }
-#pragma unroll
-  for (int j = 0; j < 24; ++j) {
-    const int v = st.action_set[min(j, c.P * 6 - 1) * S + g];
-    s.aset[j] = (j < c.P * 6) ? v : 0;
-  }
-  s.cp = st.current_player[g];
-  const int C = 8 * c.P + 2;
-  float* o = obs + (size_t)sl * C * kCells;
-  const int gn = lane_game ? lane_game[g] : g;   // trajectory row of this lane's game
-  int8_t* to = traj_obs + ((size_t)gn * T + idx[gn]) * C * kCells;
-  auto owner = [&](int cell) { return (int)st.board[cell * S + g]; };
-  for (int ch = 0; ch < C; ++ch) {
-    const int v = det_encode_value(c, s, ch, w, owner);
-    o[ch * kCells + w] = (float)v;
-    to[ch * kCells + w] = (int8_t)v;
+  const LdsLane s{sstate[lg], sstate[lg][40], 0, 0};
+  const uint32_t l = det_legal_g<G>(c, s, BoardView{sboard[lg], 1}, a, t);
+  if (a == 0) {
+    legal[g] = l;
+    flag[g] = l ? 1 : 2;
   }
 }
 
-// Apply the searched action (env_step) or no_step, and write the trajectory record
-// (game_agent.py:79-141).
-__global__ __launch_bounds__(kSpBlock) void k_sp_apply(DetConsts c, muz_detmadn_soa st, const int32_t* flag,
-                                                       const int32_t* slot, const int32_t* s_action,
-                                                       const float* s_weights, const float* s_value, muz_traj tr,
-                                                       int n, const int32_t* lane_game, const uint32_t* legal) {
-  __shared__ int8_t sboard[kCells * kSpBlock];
-  const int g = blockIdx.x * kSpBlock + threadIdx.x;
-  if (g >= n) return;
-  const int f = flag[g];
-  if (f == 0) return;
-  BoardView b{sboard + threadIdx.x, kSpBlock};
-  DetLane s;
-  det_load(c, st, g, s, b);
+// Observation of every searching game (compacted order: slot sl plays lane list[sl]) as fp32 for root inference +
+// its int8 trajectory record; one game per kFlagLanes lanes: the game's lanes gather its SoA bytes into LDS, stage
+// the encode (det_enc_stage: rel[56] + constant channels) and write both outputs from the staging -- fp32 as
+// float4 per 4 cells of a channel (56 = 14 x 4; 4 bytes = one v_perm_b32 through the channel table), int8 as
+// 16-byte chunks -- consecutive lanes on consecutive chunks of the game's contiguous block.
+__global__ __launch_bounds__(kSpBlock) void k_sp_encode_g(DetConsts c, muz_detmadn_soa st, const int32_t* list,
+                                                          const int32_t* counts, const uint32_t* legal,
+                                                          uint32_t* legal_c, float* obs, int8_t* traj_obs,
+                                                          const int32_t* idx, int T, const int32_t* lane_game) {
+  constexpr int G = kFlagLanes, NG = kSpBlock / G;
+  __shared__ int8_t sboard[NG][kCells];
+  __shared__ int8_t sstate[NG][kStateRow];
+  __shared__ __attribute__((aligned(16))) uint8_t senc[NG][kEncStride];
+  const int cnt = counts[0];
+  if ((int)blockIdx.x * NG >= cnt) return;   // (uniform over the workgroup)
+  const int t = threadIdx.x, lg = t / G, a = t % G;
+  const int sl = blockIdx.x * NG + lg;
+  const bool valid = sl < cnt;   // uniform over a game's lanes
+  const int S = st.stride, P = c.P, C = 8 * P + 2;
+  const int g = valid ? list[sl] : 0;
+  if (valid) {
+    for (int cell = a; cell < kCells; cell += G) sboard[lg][cell] = st.board[cell * S + g];
+    if (a < 16) sstate[lg][a] = a < 4 * P ? st.pins[a * S + g] : (int8_t)-1;
+    if (a < 24) sstate[lg][16 + a] = a < 6 * P ? st.action_set[a * S + g] : (int8_t)0;
+    if (a == 0) {
+      sstate[lg][40] = st.current_player[g];
+      legal_c[sl] = legal[g];
+    }
+  }
+  __syncthreads();
+  if (valid) det_enc_stage<G>(c, LdsLane{sstate[lg], sstate[lg][40], 0, 0}, BoardView{sboard[lg], 1}, senc[lg], a);
+  __syncthreads();
+  if (!valid) return;
   const bool teams = has(c.flags, R_TEAMS);
-  const int T = tr.max_steps;
-  const int gn = lane_game ? lane_game[g] : g;
-  const int t = tr.idx[gn];
-  const size_t rec = (size_t)gn * T + t;
-  const int cp_before = s.cp;
-  const int team_before = teams ? cp_before % 2 : -1;
-  int act, rew_cls, disc_cls;
-  float val, mask;
-  if (f == 1) {
-    const int sl = slot[g];
-    act = s_action[sl];
-    // legal[g]: this state's mask from k_sp_flags (the state is unchanged since), so no second legality pass
-    const int r = det_step_masked(c, s, b, fdiv(act, 6), fmodp(act, 6) + 1, legal[g]);
-    const bool nd = s.done != 0;
-    const int next_player = s.cp;
-    const int next_team = teams ? next_player % 2 : -1;
-    rew_cls = (nd && r > 0) ? 2 : ((nd && r < 0) ? 0 : 1);
-    disc_cls = nd ? 1 : (teams ? (team_before == next_team ? 2 : 0) : (cp_before == next_player ? 2 : 0));
-    val = s_value[sl];
-    mask = 1.f;
-    float* pol = tr.pol + rec * MUZ_DET_ACTIONS;
-    for (int a = 0; a < MUZ_DET_ACTIONS; ++a) pol[a] = s_weights[(size_t)sl * MUZ_DET_ACTIONS + a];
-    det_store(c, st, g, s, b, true);
-  } else {
-    det_nostep(c, s);   // obs / policy records stay zero (buffers are zeroed per call)
-    act = -1;
-    rew_cls = 1;
-    disc_cls = 1;
-    val = 0.f;
-    mask = 0.f;
-    det_store(c, st, g, s, b, false);
+  const uint8_t* e = senc[lg];
+  float4* o = reinterpret_cast<float4*>(obs + (size_t)sl * C * kCells);
+  for (int q = a; q < C * 14; q += G) {   // 4 cells of one channel per float4
+    const int ch = q / 14, w0 = (q - ch * 14) * 4;
+    const uint32_t rel4 = *reinterpret_cast<const uint32_t*>(e + w0);
+    const uint32_t v4 = ch < P + 2 ? __builtin_amdgcn_perm(0u, det_obs_table(ch, P, teams), rel4)
+                                   : (uint32_t)e[kCells + ch] * 0x01010101u;
+    o[q] = make_float4((float)(v4 & 0xFFu), (float)((v4 >> 8) & 0xFFu), (float)((v4 >> 16) & 0xFFu),
+                       (float)(v4 >> 24));
   }
-  tr.act[rec] = act;
-  tr.rew[rec] = rew_cls;
-  tr.val[rec] = val;
-  tr.mask[rec] = mask;
-  tr.player[rec] = cp_before;
-  tr.team[rec] = team_before;
-  tr.discount[rec] = disc_cls;
-  tr.idx[gn] = t + 1;
+  const int gn = lane_game ? lane_game[g] : g;   // trajectory row of this lane's game
+  uint4* to = reinterpret_cast<uint4*>(traj_obs + ((size_t)gn * T + idx[gn]) * C * kCells);
+  for (int q = a; q < C * 7 / 2; q += G) {
+    const uint2 lo = det_obs_half(e, 2 * q, P, teams), hi = det_obs_half(e, 2 * q + 1, P, teams);
+    to[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
+
+// Apply the searched action (env_step) or no_step, and write the trajectory record (game_agent.py:79-141): one
+// game per kFlagLanes lanes, like k_sp_flags_g -- the workgroup's SoA rows go through LDS both ways (coalesced),
+// lane 0 of a game steps it on its LDS rows (LdsLane), its lanes copy the 24 action weights into the record.
+__global__ __launch_bounds__(kSpBlock) void k_sp_apply_g(DetConsts c, muz_detmadn_soa st, const int32_t* flag,
+                                                         const int32_t* slot, const int32_t* s_action,
+                                                         const float* s_weights, const float* s_value, muz_traj tr,
+                                                         int n, const int32_t* lane_game, const uint32_t* legal) {
+  constexpr int G = kFlagLanes, NG = kSpBlock / G;
+  __shared__ int8_t sboard[NG][kCells];
+  __shared__ int8_t sstate[NG][kStateRow];
+  const int t = threadIdx.x, lg = t / G, a = t % G;
+  const int g0 = blockIdx.x * NG, games = min(NG, n - g0), g = g0 + lg;
+  det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
+  const int f = lg < games ? flag[g] : 0;
+  const int T = tr.max_steps;
+  const int gn = f ? (lane_game ? lane_game[g] : g) : 0;
+  const int tt = f ? tr.idx[gn] : 0;   // read by every lane of the game before lane 0 advances it
+  const size_t rec = (size_t)gn * T + tt;
+  __syncthreads();
+  if (f == 1 && a < MUZ_DET_ACTIONS)
+    tr.pol[rec * MUZ_DET_ACTIONS + a] = s_weights[(size_t)slot[g] * MUZ_DET_ACTIONS + a];
+  if (f != 0 && a == 0) {
+    int8_t* sp = sstate[lg];
+    LdsLane s{sp, sp[40], sp[41], sp[42]};
+    const BoardView b{sboard[lg], 1};
+    const bool teams = has(c.flags, R_TEAMS);
+    const int cp_before = s.cp;
+    const int team_before = teams ? cp_before % 2 : -1;
+    int act, rew_cls, disc_cls;
+    float val, mask;
+    if (f == 1) {
+      const int sl = slot[g];
+      act = s_action[sl];
+      // legal[g]: this state's mask from k_sp_flags_g (the state is unchanged since), so no second legality pass
+      const int r = det_step_masked(c, s, b, fdiv(act, 6), fmodp(act, 6) + 1, legal[g]);
+      const bool nd = s.done != 0;
+      const int next_player = s.cp;
+      const int next_team = teams ? next_player % 2 : -1;
+      rew_cls = (nd && r > 0) ? 2 : ((nd && r < 0) ? 0 : 1);
+      disc_cls = nd ? 1 : (teams ? (team_before == next_team ? 2 : 0) : (cp_before == next_player ? 2 : 0));
+      val = s_value[sl];
+      mask = 1.f;
+    } else {
+      det_nostep(c, s);   // obs / policy records stay zero (buffers are zeroed per call)
+      act = -1;
+      rew_cls = 1;
+      disc_cls = 1;
+      val = 0.f;
+      mask = 0.f;
+    }
+    sp[40] = (int8_t)s.cp;
+    sp[41] = (int8_t)s.done;
+    sp[42] = (int8_t)s.reward;
+    tr.act[rec] = act;
+    tr.rew[rec] = rew_cls;
+    tr.val[rec] = val;
+    tr.mask[rec] = mask;
+    tr.player[rec] = cp_before;
+    tr.team[rec] = team_before;
+    tr.discount[rec] = disc_cls;
+    tr.idx[gn] = tt + 1;
+  }
+  __syncthreads();
+  det_rows_store<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
 }
 
 __device__ void det_reset_lane(const DetConsts& c, const muz_detmadn_soa& st, int g) {
@@ -281,10 +318,12 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
     if (!led.proceed(turn)) break;
     if (lane_game)
       k_ss_refill<<<1, kScanThreads, 0, s>>>(c, st, ws.lane_game, tr.idx, T, ws.next_game, num_games, n);
-    k_sp_flags<<<(n + kSpBlock - 1) / kSpBlock, kSpBlock, 0, s>>>(c, st, ws.legal, ws.flag, n, lane_game, tr.idx, T);
+    k_sp_flags_g<<<(n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes), kSpBlock, 0, s>>>(
+        c, st, ws.legal, ws.flag, n, lane_game, tr.idx, T);
     k_sp_compact<<<1, kScanThreads, 0, s>>>(ws.flag, n, ws.list, ws.slot, ws.counts);
     led.counts(turn, ws.counts);
-    k_sp_encode<<<n, 64, 0, s>>>(c, st, ws.list, ws.counts, ws.legal, ws.legal_c, ws.obs, tr.obs, tr.idx, T, lane_game);
+    k_sp_encode_g<<<(n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes), kSpBlock, 0, s>>>(
+        c, st, ws.list, ws.counts, ws.legal, ws.legal_c, ws.obs, tr.obs, tr.idx, T, lane_game);
     if ((rc = muz_last_launch_error())) break;
     if ((rc = launch_root_inference(*w, ws.obs, n, ws.counts, ws.conv, ws.root_logits, ws.root_value, ws.root_emb,
                                     s)))
@@ -295,8 +334,8 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
                                    ws.value, s)))
       break;
     led.search_end(turn);
-    k_sp_apply<<<(n + kSpBlock - 1) / kSpBlock, kSpBlock, 0, s>>>(c, st, ws.flag, ws.slot, ws.action, ws.weights,
-                                                                   ws.value, tr, n, lane_game, ws.legal);
+    k_sp_apply_g<<<(n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes), kSpBlock, 0, s>>>(
+        c, st, ws.flag, ws.slot, ws.action, ws.weights, ws.value, tr, n, lane_game, ws.legal);
     if ((rc = muz_last_launch_error())) break;
     ++turns;
   }
@@ -325,6 +364,7 @@ int muz_detmadn_selfplay(const muz_rules* rules, const muz_net_w* w, const muz_s
   if (w->obs_channels != 8 * c.P + 2 || w->num_actions != MUZ_DET_ACTIONS) return MUZ_E_UNSUPPORTED;
   MUZ_HOST_CHECK(n >= 0 && st.stride >= n && workspace && tr.max_steps > 0 && tr.obs && tr.act && tr.rew &&
                  tr.val && tr.pol && tr.mask && tr.player && tr.team && tr.discount && tr.idx);
+  MUZ_HOST_CHECK(((uintptr_t)tr.obs & 15u) == 0 && ((uintptr_t)workspace & 15u) == 0);
   if (cfg->num_simulations < 1 || cfg->num_simulations > 100 || cfg->max_depth < 1 || cfg->max_depth > 64)
     return MUZ_E_UNSUPPORTED;
   if (stats) *stats = muz_sp_stats{};
@@ -364,6 +404,7 @@ int muz_detmadn_selfplay_stream(const muz_rules* rules, const muz_net_w* w, cons
   const int n = lanes;
   MUZ_HOST_CHECK(n >= 0 && num_games >= 0 && st.stride >= n && workspace && tr.max_steps > 0 && tr.obs && tr.act &&
                  tr.rew && tr.val && tr.pol && tr.mask && tr.player && tr.team && tr.discount && tr.idx);
+  MUZ_HOST_CHECK(((uintptr_t)tr.obs & 15u) == 0 && ((uintptr_t)workspace & 15u) == 0);
   if (cfg->num_simulations < 1 || cfg->num_simulations > 100 || cfg->max_depth < 1 || cfg->max_depth > 64)
     return MUZ_E_UNSUPPORTED;
   if (stats) *stats = muz_sp_stats{};

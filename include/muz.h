@@ -415,7 +415,8 @@ int64_t muz_selfplay_workspace_bytes(int32_t n, int32_t obs_channels, const muz_
 
 /* play_n_games_v3 + play_batch_of_games_jitted: reset n games (rules->starting_player), then play
  * until every game is done or max_steps turns ran.  Searches use cfg (S, D, temperature = gumbel_scale,
- * device Gumbel noise from cfg->seed).  stats (host, nullable) receives turns / searches / timings. */
+ * device Gumbel noise from cfg->seed).  stats (host, nullable) receives turns / searches / timings.  The
+ * workspace and traj.obs must be 16-byte aligned (else MUZ_E_INVALID; the same for the streaming form). */
 int muz_detmadn_selfplay(const muz_rules* rules /*host*/, const muz_net_w* w /*host*/,
                          const muz_search_cfg* cfg /*host*/, muz_detmadn_soa state, muz_traj traj, int32_t n,
                          void* workspace, int64_t workspace_bytes, muz_sp_stats* stats /*host*/, void* stream);
