@@ -194,20 +194,10 @@ __device__ __forceinline__ P tree_ld(const P* p) {
 #ifndef MUZ_RING_DEPTH
 #define MUZ_RING_DEPTH 2   // k-blocks of weights in flight ahead of the one being multiplied (2 or 3)
 #endif
-#ifndef MUZ_YOUNG_EARLY_PF
-#define MUZ_YOUNG_EARLY_PF 0
-#endif
 
-struct NoEarly {
-  __device__ __forceinline__ void operator()() const {}
-};
-
-// `early` runs right after the loads of the layer's last weight k-block are issued (step KB - D - 1, KB > D):
-// a hook for issuing the next layer's first k-blocks inside the loop.
-template <int NT, bool AG, class Early = NoEarly>
+template <int NT, bool AG>
 __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int KB, const float* A, int lda,
-                                               f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT],
-                                               const Early& early = Early()) {
+                                               f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT]) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(Wg)) + lane * NT;
@@ -228,7 +218,6 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
       for (int t = 0; t < NT; ++t) nxt[t] = wp[(kb + D) * wstep + t];
     }
 #endif
-    if (kb + D + 1 == KB) early();
     // Pin the issue point: without this the machine scheduler sinks each weight load next to its
     // first MFMA (one step of cover instead of D) once the loop is fully unrolled.
     __builtin_amdgcn_sched_barrier(0);
@@ -268,14 +257,13 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
   }
 }
 
-template <int NT, class Early = NoEarly>
+template <int NT>
 __device__ __forceinline__ void mfma_ring(const float* __restrict__ Wg, int KB, const float* A, int lda,
-                                          f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT], bool a_global,
-                                          const Early& early = Early()) {
+                                          f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT], bool a_global) {
   if (a_global)
-    mfma_ring_impl<NT, true>(Wg, KB, A, lda, acc, b0, b1, early);
+    mfma_ring_impl<NT, true>(Wg, KB, A, lda, acc, b0, b1);
   else
-    mfma_ring_impl<NT, false>(Wg, KB, A, lda, acc, b0, b1, early);
+    mfma_ring_impl<NT, false>(Wg, KB, A, lda, acc, b0, b1);
 }
 
 template <int NT>
@@ -344,20 +332,9 @@ __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, co
     b1[t] = pf.v1[t];
   }
   ST(ST_DENTRY);
-#if MUZ_YOUNG_EARLY_PF
-  // experiment: the young waves (4-7, last to finish a layer under oldest-first issue) start the next layer's
-  // weight prefetch inside their loop, right after their last k-block's loads
-  const bool early = wv >= kWaves / 2 && KB > MUZ_RING_DEPTH;
-  mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global, [&]() {
-    if (early) pf_issue<NTN>(pf, Ln, Kn, Nn);
-  });
-  ST(ST_MFMA);
-  if (!early) pf_issue<NTN>(pf, Ln, Kn, Nn);
-#else
   mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global);
   ST(ST_MFMA);
   pf_issue<NTN>(pf, Ln, Kn, Nn);
-#endif
   // The MFMA computes out^T (weights as the A operand), so lane (r, g) holds 4 CONSECUTIVE output
   // columns of row r: one 16-byte bias load and one ds_write_b128 per tile.
 #pragma unroll
