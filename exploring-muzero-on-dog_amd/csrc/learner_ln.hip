@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void k_minmax_fwd(const float* __restrict__ x,
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int c = lane + 64 * e;
-    v[e] = x[row + c] + (y[row + c] + bias[c]);
+    v[e] = x ? x[row + c] + (y[row + c] + bias[c]) : y[row + c] + bias[c];
     q[row + c] = v[e];
     if (v[e] < lo) lo = v[e], ilo = c;
     if (v[e] > hi) hi = v[e], ihi = c;
@@ -388,7 +388,7 @@ int muz_ln_film_bwd_rows(const float* dfilm, const float* out, const float* z, c
 int muz_minmax_fwd(const float* x, const float* y, const float* bias, int32_t M, int32_t N, float* out, float* q,
                    float* lohi, int32_t* idx, void* stream) {
   if (N != 256) return MUZ_E_UNSUPPORTED;
-  MUZ_HOST_CHECK(M >= 0 && x && y && bias && out && q && lohi && idx);
+  MUZ_HOST_CHECK(M >= 0 && y && bias && out && q && lohi && idx);
   if (M == 0) return MUZ_OK;
   k_minmax_fwd<256><<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(x, y, bias, M, out, q, lohi, idx);
   return muz_last_launch_error();

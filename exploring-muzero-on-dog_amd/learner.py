@@ -107,6 +107,44 @@ class _Dense(torch.autograd.Function):
         return dx, dW, db
 
 
+class _DenseMinmax(torch.autograd.Function):
+    """minmax(x @ W + b) per row of 256 (RepresentationNetwork2's last layer, muzero_deterministic_madn.py:
+    139-140): the library GEMM, then the bias add and the min-max scaling in one launch each way
+    (muz_minmax_fwd / _bwd with no skip input; torch's add / amin / amax / sub / div and their backward were
+    ~10 launches).  Same arithmetic order as the torch form; tied extrema split their gradient evenly."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        M, Nn = x.shape[0], W.shape[1]
+        y = x @ W
+        out, q = torch.empty_like(y), torch.empty_like(y)
+        lohi = torch.empty((M, 2), dtype=y.dtype, device=y.device)
+        idx = torch.empty((M, 2), dtype=torch.int32, device=y.device)
+        _L.check(_L.load().muz_minmax_fwd(None, _L.ptr(y), _L.ptr(b), M, Nn, _L.ptr(out), _L.ptr(q), _L.ptr(lohi),
+                                          _L.ptr(idx), _L.stream_ptr()), "muz_minmax_fwd")
+        ctx.save_for_backward(x, W, q, lohi)
+        ctx.owners = (W, b) if W.is_leaf and b.is_leaf else None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W, q, lohi = ctx.saved_tensors
+        M, Nn = q.shape
+        g = g.contiguous()
+        dq = torch.empty_like(q)
+        _L.check(_L.load().muz_minmax_bwd(_L.ptr(g), None, None, None, 1.0, 0, _L.ptr(q), _L.ptr(lohi), M, Nn,
+                                          _L.ptr(dq), _L.stream_ptr()), "muz_minmax_bwd")
+        dx = dq @ W.t() if ctx.needs_input_grad[0] else None
+        sink = _sink()
+        if sink is not None and ctx.owners is not None:
+            sink.wgrad(x.contiguous(), dq, ctx.owners[0])
+            sink.colsum(dq, ctx.owners[1])
+            return dx, None, None
+        dW = x.t() @ dq if ctx.needs_input_grad[1] else None
+        db = torch.mv(dq.t(), _ones(M, dq)) if ctx.needs_input_grad[2] else None
+        return dx, dW, db
+
+
 class _Im2col(torch.autograd.Function):
     """The im2col matrix of a 'SAME' Conv1D (MuZeroNets._conv_cols) in one kernel each way
     (csrc/learner_ln.hip; torch's pad + slices + cat made ~25 kernels per convolution's backward)."""
@@ -678,6 +716,8 @@ class MuZeroNets:
         h = self._dense_ln(f"{r}/Dense_3", f"{r}/LayerNorm_6", torch.cat([flat, g], -1))
         for b in range(6):
             h = self._rb(f"{r}/ResBlock_{b}", h)
+        if h.is_cuda and h.shape[-1] == 256 and self.p[f"{r}/Dense_4/kernel"].shape[1] == 256:
+            return _DenseMinmax.apply(h.contiguous(), self.p[f"{r}/Dense_4/kernel"], self.p[f"{r}/Dense_4/bias"])
         return self._minmax(self._dense(f"{r}/Dense_4", h))
 
     def dynamics_film(self, action):

@@ -690,7 +690,8 @@ int muz_ln_film_fwd(const float* x, const float* gamma, const float* beta, const
 int muz_ln_film_bwd_rows(const float* dfilm, const float* out, const float* z, const float* mean, const float* rstd,
                          const float* gamma, const float* scale1, int32_t M, int32_t N, float* dz, float* dscale,
                          float* scratch, void* stream);
-/* Min-max latent scaling closing a dynamics trunk, N = 256: q = x + (y + bias), out = (q - min) /
+/* Min-max latent scaling closing a dynamics trunk (x = the trunk input; x null: q = y + bias, the
+ * representation's last Dense, muzero_deterministic_madn.py:139-140), N = 256: q = x + (y + bias), out = (q - min) /
  * (max - min + 1e-8) per row; saves q [M][N], lohi [M][2] (min, max) and idx [M][2] (their columns, lowest on
  * ties).  Backward: dq from d = (g + (a + b)) x (scale if scaled) + h (a, b both null or both given; h
  * optional: a gradient that bypasses the latent scaling, e.g. the det reward / discount heads reading the

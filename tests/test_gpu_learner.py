@@ -241,6 +241,34 @@ def test_ln_film_kernels_match_float64_autograd(cuda):
         close(a, r, name)
 
 
+def test_dense_minmax_node_matches_torch_form(cuda):
+    """learner._DenseMinmax (RepresentationNetwork2's last Dense + min-max scaling: library GEMM, then bias + min-max
+    in one launch each way) against the torch form (x @ W + b, amin / amax): forward bit-identical, gradients of x,
+    W and b within 1e-5 relative; a row with tied extrema checks the even split."""
+    _, _, L, _, _ = _mods()
+    g = torch.Generator().manual_seed(31)
+    M = 130
+    x = torch.randn(M, 256, generator=g).cuda()
+    W = (0.1 * torch.randn(256, 256, generator=g)).cuda()
+    b = (0.1 * torch.randn(256, generator=g)).cuda()
+    x[3] = 0.0                                   # row 3: q = b, whose extrema we tie below
+    b[7] = b[9] = b.max() + 1.0
+    dout = torch.randn(M, 256, generator=g).cuda()
+    leaves = [t.clone().requires_grad_(True) for t in (x, W, b)]
+    out = L._DenseMinmax.apply(*leaves)
+    g1 = torch.autograd.grad(out, leaves, dout)
+    ref_leaves = [t.clone().requires_grad_(True) for t in (x, W, b)]
+    q = (ref_leaves[0] @ ref_leaves[1]).add(ref_leaves[2])
+    lo, hi = torch.amin(q, -1, keepdim=True), torch.amax(q, -1, keepdim=True)
+    ref = (q - lo) / (hi - lo + 1e-8)
+    g2 = torch.autograd.grad(ref, ref_leaves, dout)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    for n, a, r in zip(("dx", "dW", "db"), g1, g2):
+        err = (a - r).abs().max().item() / max(1e-3, r.abs().max().item())
+        assert err < 1e-5, f"{n}: relative difference {err:.2e}"
+
+
 def test_dynamics_chain_node_matches_per_step_autograd(cuda):
     """learner._TrunkChain (the K-step latent chain as one autograd node, batched weight gradients) against the
     per-step graph of the same layers (loss_fn's CPU-style loop run on the GPU): forward within 1e-5, gradients
