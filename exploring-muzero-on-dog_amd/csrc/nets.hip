@@ -30,7 +30,7 @@ __device__ __forceinline__ void ln_positions(const float* pre, float* out, int o
   s2 += dpp<DPP_XOR1>(s2);
   s2 += dpp<DPP_XOR2>(s2);
   const float mean = s / (float)N, mean2 = s2 / (float)N;
-  const float inv = 1.0f / sqrtf(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
+  const float inv = ln_rstd(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = q + 4 * i;

@@ -385,6 +385,30 @@ __device__ __forceinline__ int row_imax(int v) {
   return row_reduce(v, [](int x, int y) { return max(x, y); });
 }
 
+// Reciprocals of the networks' row ops (LayerNorm's 1 / sqrt(var + eps), min-max's 1 / (max - min + 1e-8), the
+// reward / discount supports' 1 / sum(exp)): the hardware v_rsq_f32 / v_rcp_f32 (<= 1 ulp) instead of the correctly
+// rounded IEEE sequences (a div_scale / div_fmas / div_fixup chain per divide): k_gumbel_search 2-3 % faster
+// (profiles/r2_search_experiments.log), the networks still within 1e-5 of the fp32 oracle (tests/test_gpu_nets.py).
+// The search's own tree arithmetic (mctx's completed Q, softmaxes, visit ratios) keeps IEEE division.
+// MUZ_FAST_ROWOPS=0 builds the IEEE form.
+#ifndef MUZ_FAST_ROWOPS
+#define MUZ_FAST_ROWOPS 1
+#endif
+__device__ __forceinline__ float ln_rstd(float var_eps) {
+#if MUZ_FAST_ROWOPS
+  return __builtin_amdgcn_rsqf(var_eps);
+#else
+  return 1.0f / sqrtf(var_eps);
+#endif
+}
+__device__ __forceinline__ float mm_scale(float x, float den) {
+#if MUZ_FAST_ROWOPS
+  return x * __builtin_amdgcn_rcpf(den);
+#else
+  return x / den;
+#endif
+}
+
 enum LnMode { LN_PLAIN = 0, LN_RELU = 1, LN_RESID_RELU = 2 };
 
 // Flax LayerNorm (eps 1e-6, fast variance) of in[16][N] -> out.
@@ -449,7 +473,7 @@ __device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int l
   const float mean = s / (float)N;
   const float mean2 = s2 / (float)N;
   const float var = fmaxf(0.f, mean2 - mean * mean);
-  const float inv = 1.0f / sqrtf(var + 1e-6f);
+  const float inv = ln_rstd(var + 1e-6f);
   if (act) {
 #pragma unroll
     for (int i = 0; i < RV::V; ++i) {
@@ -492,7 +516,7 @@ __device__ __forceinline__ void minmax16(float* buf, int ld) {
   for (int i = 0; i < RV::V; ++i) {
     f32x4 y;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) y[q] = (v[i][q] - lo) / den;
+    for (int q = 0; q < 4; ++q) y[q] = mm_scale(v[i][q] - lo, den);
     sts4(buf + row * ld + RV::col(sub, i), y);
   }
 }
@@ -523,7 +547,7 @@ __device__ __forceinline__ void skip_minmax16(float* buf, const float* skip, int
   for (int i = 0; i < RV::V; ++i) {
     f32x4 y;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) y[q] = (v[i][q] - lo) / den;
+    for (int q = 0; q < 4; ++q) y[q] = mm_scale(v[i][q] - lo, den);
     sts4(buf + row * ld + RV::col(sub, i), y);
     v[i] = y;
   }
@@ -545,7 +569,7 @@ __device__ __forceinline__ void skip_minmax16(float* buf, const float* skip, int
   const float mean = s / (float)LAT;
   const float mean2 = s2 / (float)LAT;
   const float var = fmaxf(0.f, mean2 - mean * mean);
-  const float inv = 1.0f / sqrtf(var + 1e-6f);
+  const float inv = ln_rstd(var + 1e-6f);
 #pragma unroll
   for (int i = 0; i < RV::V; ++i) {
     f32x4 y;
@@ -709,7 +733,7 @@ __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) 
   const float m = fmaxf(fmaxf(l0, l1), l2);
   const float e0 = expf(l0 - m), e1 = expf(l1 - m), e2 = expf(l2 - m);
   const float z = e0 + e1 + e2;
-  return (e0 / z) * -1.0f + (e1 / z) * 0.0f + (e2 / z) * 1.0f;
+  return mm_scale(e0, z) * -1.0f + mm_scale(e1, z) * 0.0f + mm_scale(e2, z) * 1.0f;
 }
 
 // Dyn4 inputs of this thread's row, loaded as soon as the parent node and action are known (end of the
@@ -765,7 +789,7 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
     s2 = row_sum(s2);
     const float mean = s / (float)LAT;
     const float mean2 = s2 / (float)LAT;
-    const float inv = 1.0f / sqrtf(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
+    const float inv = ln_rstd(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
 #pragma unroll
     for (int i = 0; i < RV::V; ++i) {
       const int c = RV::col(sub, i);

@@ -67,7 +67,7 @@ __device__ __forceinline__ void film_trunk16(const TrunkW& W, const FilmIn& in, 
     s2 = row_sum(s2);
     const float mean = s / (float)LAT;
     const float mean2 = s2 / (float)LAT;
-    const float inv = 1.0f / sqrtf(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
+    const float inv = ln_rstd(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
 #pragma unroll
     for (int i = 0; i < RV::V; ++i) {
       const int c = RV::col(sub, i);
