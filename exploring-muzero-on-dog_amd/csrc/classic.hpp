@@ -51,7 +51,7 @@ __device__ __forceinline__ uint32_t cls_legal(const DetConsts& c, const ClsLane&
       const int fitted = fmodp(moved, kTrack);
       int x = moved - tgt - mt;
       res = (b.at(fitted) != cp) || has(F, R_FRIENDLY);
-      const int nsb = fmodp(fdiv(cur, kDist) + 1, c.P);
+      const int nsb = mod_small(fdiv(cur, kDist) + 1, c.P);   // fdiv(cur, 10) + 1 in [0, 6]
       const int nsa_j = jidx(fdiv(fitted, kDist), c.P);
       const bool trav = cst(c.start, jidx(nsb, c.P)) == cst(c.start, nsa_j);
       const bool pos_a = pos[0] & (nsa_j == 0) | pos[1] & (nsa_j == 1) | pos[2] & (nsa_j == 2) | pos[3] & (nsa_j == 3);
@@ -132,7 +132,7 @@ __device__ __forceinline__ int cls_step_masked(const DetConsts& c, ClsLane& s, c
   const uint32_t w = winners(c, b);
   const int reward = s.done ? 0 : (invalid ? -1 : (int)((w >> cp) & 1u));
   const int done = (s.done || w != 0u) ? 1 : 0;
-  s.cp = (done || (has(F, R_BONUS_6) && move == 6)) ? player_id : (player_id + 1) % c.P;
+  s.cp = (done || (has(F, R_BONUS_6) && move == 6)) ? player_id : mod_small(player_id + 1, c.P);
   s.done = done;
   s.reward = reward;
   return reward;
@@ -224,7 +224,7 @@ __device__ __forceinline__ int cls_encode_value(const DetConsts& c, const ClsLan
   const int P = c.P, cp = s.cp;
   const int src = (w < kTrack) ? fmodp(w + kDist * cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * cp, 16);
   const int v = cell_owner(src);
-  auto rolled = [&](int i) { return (i + cp) % P; };
+  auto rolled = [&](int i) { return mod_small(i + cp, P); };
   if (ch < P) return v == rolled(ch) ? 1 : 0;
   if (ch == P) {
     if (has(c.flags, R_TEAMS)) return (v == rolled(0) ? 1 : 0) + (v == rolled(2) ? 1 : 0);

@@ -34,6 +34,16 @@ __device__ __forceinline__ int fmodp(int a, int b) {
   return r;
 }
 // jnp gather index: a negative index is normalised ONCE (i + n), then clamped to [0, n-1].
+// a mod n (floor convention, result in [0, n)) for the player-count moduli of the rules (n = P in [2, 4],
+// -n <= a < 4n): conditional adds / subtracts instead of a runtime integer division (~25 instructions each),
+// which the legality checks and the encode ran once per action / cell.
+__device__ __forceinline__ int mod_small(int a, int n) {
+  a += a < 0 ? n : 0;
+  a -= a >= n ? n : 0;
+  a -= a >= n ? n : 0;
+  a -= a >= n ? n : 0;
+  return a;
+}
 __device__ __forceinline__ int jidx(int i, int n) {
   i = (i < 0) ? i + n : i;
   return i < 0 ? 0 : (i > n - 1 ? n - 1 : i);

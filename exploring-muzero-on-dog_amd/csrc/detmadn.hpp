@@ -164,7 +164,7 @@ __device__ __forceinline__ bool legal_one(const DetConsts& c, const BoardView& b
   const int cp = x.cp, tgt = x.tgt, mt = x.mt;
   const bool in_goal = (cur == goal_of(c, cp, 0)) | (cur == goal_of(c, cp, 1)) | (cur == goal_of(c, cp, 2)) |
                        (cur == goal_of(c, cp, 3));
-  const int nsb = fmodp(fdiv(cur, kDist) + 1, c.P);
+  const int nsb = mod_small(fdiv(cur, kDist) + 1, c.P);   // fdiv(cur, 10) + 1 in [0, 6]
   bool res;
   if (cur == -1) {
     res = (m == 6 || (m == 1 && has(F, R_START_ON_1))) && x.home_ok;
@@ -314,7 +314,7 @@ __device__ __forceinline__ void det_enc_stage(const DetConsts& c, const Lane& s,
   for (int w = a; w < kCells; w += G) {
     const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
     const int v = b.at(src);
-    e[w] = v < 0 ? (uint8_t)kRelEmpty : (uint8_t)((v - s.cp + P) % P);
+    e[w] = v < 0 ? (uint8_t)kRelEmpty : (uint8_t)mod_small(v - s.cp, P);
   }
   auto none = [](int) { return 0; };
   for (int ch = P + 2 + a; ch < C; ch += G) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
@@ -401,7 +401,7 @@ __device__ __forceinline__ int det_step_masked(const DetConsts& c, Lane& s, cons
   const uint32_t w = winners(c, b);
   const int reward = s.done ? 0 : (invalid ? -1 : (int)((w >> cp) & 1u));
   const int done = (s.done || w != 0u) ? 1 : 0;
-  s.cp = (done || (has(F, R_BONUS_6) && move == 6)) ? player_id : (player_id + 1) % c.P;
+  s.cp = (done || (has(F, R_BONUS_6) && move == 6)) ? player_id : mod_small(player_id + 1, c.P);
   s.done = done;
   s.reward = reward;
   return reward;
@@ -420,7 +420,7 @@ __device__ __forceinline__ void det_nostep(const DetConsts& c, Lane& s) {
     asm volatile("" : "+v"(x));
     lane_set_aset(s, j, x);
   }
-  s.cp = (s.cp + 1) % c.P;
+  s.cp = mod_small(s.cp + 1, c.P);
 }
 
 // ---- SoA load / store -----------------------------------------------------------------
@@ -467,7 +467,7 @@ __device__ __forceinline__ int det_encode_value(const DetConsts& c, const Lane& 
   const int P = c.P, cp = s.cp;
   const int src = (w < kTrack) ? fmodp(w + kDist * cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * cp, 16);
   const int v = cell_owner(src);
-  auto rolled = [&](int i) { return (i + cp) % P; };
+  auto rolled = [&](int i) { return mod_small(i + cp, P); };
   if (ch < P) return v == rolled(ch) ? 1 : 0;
   if (ch == P) {  // team channel
     if (has(c.flags, R_TEAMS)) return (v == rolled(0) ? 1 : 0) + (v == rolled(2) ? 1 : 0);

@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detm
       for (int w = 0; w < kCells; ++w) {
         const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
         const int v = b.at(src);
-        const uint32_t rel = v < 0 ? kRelEmpty : (uint32_t)((v - s.cp + P) % P);
+        const uint32_t rel = v < 0 ? kRelEmpty : (uint32_t)mod_small(v - s.cp, P);
         wv |= rel << (8 * (w & 3));
         if ((w & 3) == 3) {
           *reinterpret_cast<uint32_t*>(e + (w & ~3)) = wv;
