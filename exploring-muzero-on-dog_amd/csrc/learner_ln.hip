@@ -39,6 +39,8 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ y, con
                                                 float* __restrict__ rstd_out, const float* __restrict__ scale1 = nullptr,
                                                 const float* __restrict__ shift = nullptr,
                                                 float* __restrict__ film = nullptr) {
+  // no fma contraction: the row kernels and their fused boundary forms round identically
+#pragma clang fp contract(off)
   constexpr int E = (N + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -87,6 +89,8 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dout, 
                                                 int M, int mode, float* __restrict__ dz, float* __restrict__ dres,
                                                 float* __restrict__ part, const float* __restrict__ scale1 = nullptr,
                                                 float* __restrict__ dscale = nullptr) {
+  // no fma contraction: the row kernels and their fused boundary forms round identically
+#pragma clang fp contract(off)
   constexpr int E = (N + 63) / 64;
   __shared__ float red[4][3][N];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -195,6 +199,8 @@ __global__ __launch_bounds__(256) void k_minmax_fwd(const float* __restrict__ x,
                                                     const float* __restrict__ bias, int M, float* __restrict__ out,
                                                     float* __restrict__ q, float* __restrict__ lohi,
                                                     int* __restrict__ idx) {
+  // no fma contraction: the row kernels and their fused boundary forms round identically
+#pragma clang fp contract(off)
   constexpr int E = N / 64;
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -227,6 +233,8 @@ __global__ __launch_bounds__(256) void k_minmax_bwd(const float* __restrict__ g,
                                                     const float* __restrict__ b, const float* __restrict__ h,
                                                     float scale, int scaled, const float* __restrict__ q,
                                                     const float* __restrict__ lohi, int M, float* __restrict__ dq) {
+  // no fma contraction: the row kernels and their fused boundary forms round identically
+#pragma clang fp contract(off)
   constexpr int E = N / 64;
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -259,6 +267,167 @@ __global__ __launch_bounds__(256) void k_minmax_bwd(const float* __restrict__ g,
     if (qv[e] == lo) r = r + glo;
     if (qv[e] == hi) r = r + ghi;
     dq[row + lane + 64 * e] = r;
+  }
+}
+
+// The boundary between two applications of a dynamics trunk as one launch each way (learner._TrunkChain):
+// forward = k_minmax_fwd of application i followed by k_ln_fwd<256, FILM> of application i + 1 on the same row
+// (its input is the min-max output, still in registers); backward = k_ln_bwd<256, FILM> of application i + 1
+// followed by k_minmax_bwd of application i, whose carried gradient a is the LayerNorm input gradient just formed
+// (never stored).  Same expressions in the same order as the separate kernels: bit-identical results.
+__global__ __launch_bounds__(256) void k_minmax_film_fwd(const float* __restrict__ x, const float* __restrict__ y,
+                                                         const float* __restrict__ bias, int M, float* __restrict__ out,
+                                                         float* __restrict__ q, float* __restrict__ lohi,
+                                                         int* __restrict__ idx, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta,
+                                                         const float* __restrict__ scale1,
+                                                         const float* __restrict__ shift, float* __restrict__ ln_out,
+                                                         float* __restrict__ ln_z, float* __restrict__ ln_mean,
+                                                         float* __restrict__ ln_rstd, float* __restrict__ film) {
+  // no fma contraction: the row kernels and their fused boundary forms round identically
+#pragma clang fp contract(off)
+  constexpr int N = 256, E = N / 64;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const size_t row = (size_t)m * N;
+  float v[E];
+  float lo = INFINITY, hi = -INFINITY;
+  int ilo = N, ihi = N;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int c = lane + 64 * e;
+    v[e] = x[row + c] + (y[row + c] + bias[c]);
+    q[row + c] = v[e];
+    if (v[e] < lo) lo = v[e], ilo = c;
+    if (v[e] > hi) hi = v[e], ihi = c;
+  }
+  wave_argext(lo, ilo, false);
+  wave_argext(hi, ihi, true);
+  const float den = (hi - lo) + 1e-8f;
+  float w[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    w[e] = (v[e] - lo) / den;
+    out[row + lane + 64 * e] = w[e];
+  }
+  if (lane == 0) {
+    lohi[2 * m] = lo, lohi[2 * m + 1] = hi;
+    idx[2 * m] = ilo, idx[2 * m + 1] = ihi;
+  }
+  // the next application's LayerNorm_0 + FiLM of this row (k_ln_fwd<256, true>)
+  float s = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    s += w[e];
+    s2 += w[e] * w[e];
+  }
+  s = wave_sum(s);
+  s2 = wave_sum(s2);
+  const float mean = s / (float)N;
+  const float rstd = 1.0f / sqrtf(fmaxf(0.f, s2 / (float)N - mean * mean) + 1e-6f);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int c = lane + 64 * e;
+    const float o = (w[e] - mean) * (rstd * gamma[c]) + beta[c];
+    ln_out[row + c] = o;
+    ln_z[row + c] = w[e];
+    float p = o * scale1[row + c];
+    asm volatile("" : "+v"(p));
+    film[row + c] = shift[row + c] + p;
+  }
+  if (lane == 0) {
+    ln_mean[m] = mean;
+    ln_rstd[m] = rstd;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_film_minmax_bwd(const float* __restrict__ dfilm, const float* __restrict__ out,
+                                                         const float* __restrict__ z, const float* __restrict__ mean_in,
+                                                         const float* __restrict__ rstd_in,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ scale1, int M,
+                                                         float* __restrict__ dscale, float* __restrict__ part,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         const float* __restrict__ h, float scale, int scaled,
+                                                         const float* __restrict__ q, const float* __restrict__ lohi,
+                                                         float* __restrict__ dq) {
+  // no fma contraction: the row kernels and their fused boundary forms round identically
+#pragma clang fp contract(off)
+  constexpr int N = 256, E = N / 64;
+  __shared__ float red[4][3][N];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float pg[E], pb[E], pd[E], dzr[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) pg[i] = pb[i] = pd[i] = dzr[i] = 0.f;
+  const int m = blockIdx.x * kLnRowsPerBlock + wv;   // kLnRowsPerBlock == 4: one row per wave
+  if (m < M) {
+    const size_t row = (size_t)m * N;
+    const float mean = mean_in[m], rstd = rstd_in[m];
+    float d[E], xh[E], gg[E];
+    float a = 0.f, bb = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const int c = lane + 64 * i;
+      float t = dfilm[row + c];
+      dscale[row + c] = t * out[row + c];
+      t = t * scale1[row + c];
+      d[i] = t;
+      xh[i] = (z[row + c] - mean) * rstd;
+      gg[i] = t * gamma[c];
+      a += gg[i];
+      bb += gg[i] * xh[i];
+    }
+    a = wave_sum(a) / (float)N;
+    bb = wave_sum(bb) / (float)N;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      dzr[i] = rstd * (gg[i] - a - xh[i] * bb);
+      pg[i] += d[i] * xh[i];
+      pb[i] += d[i];
+      pd[i] += dzr[i];
+    }
+    // the previous application's min-max backward (k_minmax_bwd) with a = dzr
+    const float lo = lohi[2 * m], hi = lohi[2 * m + 1];
+    const float den = (hi - lo) + 1e-8f;
+    float dd[E], qv[E], sd = 0.f, st = 0.f;
+    int nlo = 0, nhi = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const size_t k = row + lane + 64 * e;
+      float t = g[k];
+      t = t + (dzr[e] + b[k]);
+      if (scaled) t = t * scale;
+      if (h) t = t + h[k];
+      dd[e] = t;
+      qv[e] = q[k];
+      sd += t;
+      st += t * (qv[e] - lo);
+      nlo += __popcll(__ballot(qv[e] == lo));
+      nhi += __popcll(__ballot(qv[e] == hi));
+    }
+    sd = wave_sum(sd);
+    st = wave_sum(st) / (den * den);
+    const float glo = (-sd / den + st) / (float)nlo, ghi = (-st) / (float)nhi;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float r = dd[e] / den;
+      if (qv[e] == lo) r = r + glo;
+      if (qv[e] == hi) r = r + ghi;
+      dq[row + lane + 64 * e] = r;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int c = lane + 64 * i;
+    red[wv][0][c] = pg[i];
+    red[wv][1][c] = pb[i];
+    red[wv][2][c] = pd[i];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 3 * N; t += 256) {
+    const int qq = t / N, c = t % N;
+    part[((size_t)blockIdx.x * 3 + qq) * N + c] = ((red[0][qq][c] + red[1][qq][c]) + red[2][qq][c]) + red[3][qq][c];
   }
 }
 
@@ -400,6 +569,32 @@ int muz_minmax_bwd(const float* g, const float* a, const float* b, const float* 
   MUZ_HOST_CHECK(M >= 0 && g && q && lohi && dq && (a == nullptr) == (b == nullptr));
   if (M == 0) return MUZ_OK;
   k_minmax_bwd<256><<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(g, a, b, h, scale, scaled, q, lohi, M, dq);
+  return muz_last_launch_error();
+}
+
+int muz_minmax_film_fwd(const float* x, const float* y, const float* bias, int32_t M, int32_t N, float* out, float* q,
+                        float* lohi, int32_t* idx, const float* gamma, const float* beta, const float* scale1,
+                        const float* shift, float* ln_out, float* ln_z, float* ln_mean, float* ln_rstd, float* film,
+                        void* stream) {
+  if (N != 256) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(M >= 0 && x && y && bias && out && q && lohi && idx && gamma && beta && scale1 && shift && ln_out &&
+                 ln_z && ln_mean && ln_rstd && film);
+  if (M == 0) return MUZ_OK;
+  k_minmax_film_fwd<<<(M + 3) / 4, 256, 0, (hipStream_t)stream>>>(x, y, bias, M, out, q, lohi, idx, gamma, beta, scale1,
+                                                                  shift, ln_out, ln_z, ln_mean, ln_rstd, film);
+  return muz_last_launch_error();
+}
+
+int muz_film_minmax_bwd(const float* dfilm, const float* out, const float* z, const float* mean, const float* rstd,
+                        const float* gamma, const float* scale1, int32_t M, int32_t N, float* dscale, float* scratch,
+                        const float* g, const float* b, const float* h, float scale, int32_t scaled, const float* q,
+                        const float* lohi, float* dq, void* stream) {
+  if (N != 256) return MUZ_E_UNSUPPORTED;
+  MUZ_HOST_CHECK(M >= 0 && dfilm && out && z && mean && rstd && gamma && scale1 && dscale && scratch && g && b && q &&
+                 lohi && dq);
+  if (M == 0) return MUZ_OK;
+  k_film_minmax_bwd<<<(M + kLnRowsPerBlock - 1) / kLnRowsPerBlock, 256, 0, (hipStream_t)stream>>>(
+      dfilm, out, z, mean, rstd, gamma, scale1, M, dscale, scratch, g, b, h, scale, scaled, q, lohi, dq);
   return muz_last_launch_error();
 }
 

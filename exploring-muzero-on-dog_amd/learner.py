@@ -476,6 +476,7 @@ def trunk_param_names(kind: str = "det") -> list:
 DYN_TRUNK_PARAMS = tuple(trunk_param_names("det"))
 CHAIN = True                     # False: the losses build the per-step autograd graph instead (A/B timing)
 FUSED_FILM = True                # False: a trunk's LayerNorm_0 + FiLM as LayerNorm + addcmul (A/B, diagnosis)
+FUSED_BOUNDARY = True            # False: min-max of application i and LayerNorm_0 + FiLM of i + 1 as separate launches
 _NP = len(DYN_TRUNK_PARAMS)      # 28 per trunk
 
 
@@ -533,12 +534,15 @@ class _TrunkChain(torch.autograd.Function):
         X = {(g, n): torch.empty((max(seen[g], 1), B, Nn), dtype=dt, device=dev)
              for g in range(len(seen)) for n in _GEMM_LAYERS}
         lat = latent0.contiguous()
+        f0_next = None    # LayerNorm_0 + FiLM of the next application, formed by the boundary launch
         for i in range(T):
             g, j = apps[i], slot[i]
             Q = P[_NP * g:_NP * (g + 1)]
             g0, be0, W3, b3, g1, be1, W4, b4, g2, be2 = Q[:10]
             x0 = X[(g, "3")][j]
-            if FUSED_FILM:    # LayerNorm_0 + FiLM, one launch
+            if f0_next is not None:
+                f0 = f0_next
+            elif FUSED_FILM:    # LayerNorm_0 + FiLM, one launch
                 f0 = _ln_film_fwd(lat, g0, be0, scale1[i], shift[i], x0)
             else:
                 f0 = _ln_fwd(lat, torch.zeros_like(g0), g0, be0, None, LN_PLAIN)
@@ -552,11 +556,25 @@ class _TrunkChain(torch.autograd.Function):
                 fb = _dense_ln_fwd(fa[0], Wb, bb, gb, beb, x, LN_RESID_RELU, out=X[(g, "a1" if r == 0 else "5")][j])
                 rbs.append((x, fa, fb))
                 x = fb[0]
-            _L.check(lib.muz_minmax_fwd(_L.ptr(lat), _L.ptr(x @ Q[26]), _L.ptr(Q[27]), B, Nn, _L.ptr(outs[i]),
-                                        _L.ptr(qs[i]), _L.ptr(lohi[i]), _L.ptr(idx[i]), _L.stream_ptr()), "muz_minmax_fwd")
+            y5 = x @ Q[26]
+            if FUSED_BOUNDARY and FUSED_FILM and i + 1 < T:   # min-max of i + LayerNorm_0 / FiLM of i + 1
+                gn, jn = apps[i + 1], slot[i + 1]
+                Qn = P[_NP * gn:_NP * (gn + 1)]
+                f0_next = (torch.empty_like(lat), torch.empty_like(lat), torch.empty((B,), dtype=dt, device=dev),
+                           torch.empty((B,), dtype=dt, device=dev))
+                _L.check(lib.muz_minmax_film_fwd(
+                    _L.ptr(lat), _L.ptr(y5), _L.ptr(Q[27]), B, Nn, _L.ptr(outs[i]), _L.ptr(qs[i]), _L.ptr(lohi[i]),
+                    _L.ptr(idx[i]), _L.ptr(Qn[0]), _L.ptr(Qn[1]), _L.ptr(scale1[i + 1]), _L.ptr(shift[i + 1].contiguous()),
+                    *(_L.ptr(t) for t in f0_next), _L.ptr(X[(gn, "3")][jn]), _L.stream_ptr()), "muz_minmax_film_fwd")
+            else:
+                f0_next = None
+                _L.check(lib.muz_minmax_fwd(_L.ptr(lat), _L.ptr(y5), _L.ptr(Q[27]), B, Nn, _L.ptr(outs[i]),
+                                            _L.ptr(qs[i]), _L.ptr(lohi[i]), _L.ptr(idx[i]), _L.stream_ptr()),
+                         "muz_minmax_fwd")
             st.append((f0, x0, f3, f4, rbs, x))
             lat = outs[i]
         ctx.st, ctx.X, ctx.P, ctx.grad_scale = st, X, P, float(grad_scale)
+        ctx.boundary = FUSED_BOUNDARY and FUSED_FILM
         ctx.apps, ctx.scaled = tuple(apps), tuple(scaled)
         ctx.save_for_backward(scale1, qs, lohi)
         return (outs, outs.clone()) if heads else outs
@@ -586,9 +604,10 @@ class _TrunkChain(torch.autograd.Function):
             Q = P[_NP * g:_NP * (g + 1)]
             f0, x0, f3, f4, rbs, x5 = st[i]
             dq = DZ[(g, "5")][j]
-            _L.check(lib.muz_minmax_bwd(_L.ptr(G[i]), _L.ptr(ca), _L.ptr(cb), _L.ptr(None if H is None else H[i]), s,
-                                        int(ctx.scaled[i]), _L.ptr(qs[i]), _L.ptr(lohi[i]), B, Nn, _L.ptr(dq),
-                                        _L.stream_ptr()), "muz_minmax_bwd")
+            if not (ctx.boundary and i + 1 < T):   # (else formed by application i + 1's boundary launch)
+                _L.check(lib.muz_minmax_bwd(_L.ptr(G[i]), _L.ptr(ca), _L.ptr(cb), _L.ptr(None if H is None else H[i]),
+                                            s, int(ctx.scaled[i]), _L.ptr(qs[i]), _L.ptr(lohi[i]), B, Nn, _L.ptr(dq),
+                                            _L.stream_ptr()), "muz_minmax_bwd")
             dx = dq @ Q[26].t()
             for r in (1, 0):
                 xin, fa, fb = rbs[r]
@@ -598,6 +617,15 @@ class _TrunkChain(torch.autograd.Function):
                 _, _, dx = _dense_ln_bwd(t, fa, ga, LN_RELU, Wa, scr[(g, f"a{r}")][j], DZ[(g, f"a{r}")][j], acc=dres)
             _, _, t = _dense_ln_bwd(dx, f4, Q[8], LN_RELU, Q[6], scr[(g, "4")][j], DZ[(g, "4")][j])
             _, _, dx0 = _dense_ln_bwd(t, f3, Q[4], LN_RELU, Q[2], scr[(g, "3")][j], DZ[(g, "3")][j], dx_out=dshift[i])
+            if ctx.boundary and i >= 1:   # LayerNorm_0 / FiLM backward of i + min-max backward of i - 1
+                gp, jp = apps[i - 1], slot[i - 1]
+                _L.check(lib.muz_film_minmax_bwd(
+                    _L.ptr(dx0.contiguous()), *(_L.ptr(t) for t in f0), _L.ptr(Q[0]), _L.ptr(scale1[i]), B, Nn,
+                    _L.ptr(dscale[i]), _L.ptr(scr[(g, "0")][j]), _L.ptr(G[i - 1]), _L.ptr(dq),
+                    _L.ptr(None if H is None else H[i - 1]), s, int(ctx.scaled[i - 1]), _L.ptr(qs[i - 1]),
+                    _L.ptr(lohi[i - 1]), _L.ptr(DZ[(gp, "5")][jp]), _L.stream_ptr()), "muz_film_minmax_bwd")
+                ca = cb = None
+                continue
             if FUSED_FILM:
                 dz0 = _ln_film_bwd_rows(dx0, f0, Q[0], scale1[i], scr[(g, "0")][j], dscale[i])
             else:

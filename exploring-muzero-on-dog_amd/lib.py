@@ -317,6 +317,10 @@ SIGNATURES = {
     "muz_ln_film_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp]),
     "muz_ln_film_bwd_rows": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
                                             vp]),
+    "muz_minmax_film_fwd": (ctypes.c_int, [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp,
+                                           vp, vp, vp, vp, vp, vp]),
+    "muz_film_minmax_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
+                                           vp, vp, ctypes.c_float, ctypes.c_int32, vp, vp, vp, vp]),
     "muz_minmax_fwd": (ctypes.c_int, [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
     "muz_minmax_bwd": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, ctypes.c_int32, vp, vp, ctypes.c_int32,
                                       ctypes.c_int32, vp, vp]),

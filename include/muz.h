@@ -690,6 +690,20 @@ int muz_ln_film_fwd(const float* x, const float* gamma, const float* beta, const
 int muz_ln_film_bwd_rows(const float* dfilm, const float* out, const float* z, const float* mean, const float* rstd,
                          const float* gamma, const float* scale1, int32_t M, int32_t N, float* dz, float* dscale,
                          float* scratch, void* stream);
+/* The boundary of two dynamics-trunk applications (learner._TrunkChain) as one launch each way, N = 256:
+ * muz_minmax_film_fwd = muz_minmax_fwd of application i (out, q, lohi, idx) followed by muz_ln_film_fwd of
+ * application i + 1 on its output (ln_out, ln_z, ln_mean, ln_rstd, film); muz_film_minmax_bwd =
+ * muz_ln_film_bwd_rows of application i + 1 (dscale, column partials into scratch) followed by muz_minmax_bwd of
+ * application i with a = that LayerNorm input gradient (g, b, h, scale, scaled, q, lohi -> dq).  Bit-identical
+ * to the separate calls. */
+int muz_minmax_film_fwd(const float* x, const float* y, const float* bias, int32_t M, int32_t N, float* out, float* q,
+                        float* lohi, int32_t* idx, const float* gamma, const float* beta, const float* scale1,
+                        const float* shift, float* ln_out, float* ln_z, float* ln_mean, float* ln_rstd, float* film,
+                        void* stream);
+int muz_film_minmax_bwd(const float* dfilm, const float* out, const float* z, const float* mean, const float* rstd,
+                        const float* gamma, const float* scale1, int32_t M, int32_t N, float* dscale, float* scratch,
+                        const float* g, const float* b, const float* h, float scale, int32_t scaled, const float* q,
+                        const float* lohi, float* dq, void* stream);
 /* Min-max latent scaling closing a dynamics trunk (x = the trunk input; x null: q = y + bias, the
  * representation's last Dense, muzero_deterministic_madn.py:139-140), N = 256: q = x + (y + bias), out = (q - min) /
  * (max - min + 1e-8) per row; saves q [M][N], lohi [M][2] (min, max) and idx [M][2] (their columns, lowest on

@@ -269,6 +269,44 @@ def test_dense_minmax_node_matches_torch_form(cuda):
         assert err < 1e-5, f"{n}: relative difference {err:.2e}"
 
 
+@pytest.mark.parametrize("kind", ["det", "classic"])
+def test_chain_boundary_launches_bit_identical(cuda, kind):
+    """learner.FUSED_BOUNDARY (the min-max of application i and the LayerNorm_0 + FiLM of i + 1 as one launch each
+    way: muz_minmax_film_fwd / muz_film_minmax_bwd) leaves the chain node's outputs and every gradient bit-identical
+    to the separate launches; det (one weight group, heads twin) and classic (act / chance groups alternating)."""
+    _, _, L, _, _ = _mods()
+    g = torch.Generator().manual_seed(41)
+    B, K = 96, 4
+    if kind == "det":
+        nets = L.MuZeroNets(ON.init_params(18, seed=4, randomize_affine=True), 18, 24, "cuda")
+        names, apps, scaled, heads, T = list(L.DYN_TRUNK_PARAMS), (0,) * K, (True,) * K, True, K
+    else:
+        from exploring_muzero_on_dog_amd import stochastic as ST
+        nets = L.ClassicMuZeroNets(ST.init_classic_params(20, seed=6), 20, "cuda")
+        names = [n for k in ("act", "chance") for n in L.trunk_param_names(k)]
+        apps, scaled, heads, T = (0, 1) * K, (False, True) * K, False, 2 * K
+    lat0 = torch.rand(B, 256, generator=g).cuda().requires_grad_(True)
+    scale = (0.3 * torch.randn(T, B, 256, generator=g)).cuda().requires_grad_(True)
+    shift = (0.3 * torch.randn(T, B, 256, generator=g)).cuda().requires_grad_(True)
+    w, wh = (torch.randn(T, B, 256, generator=g).cuda() for _ in range(2))
+    params = [nets.p[n] for n in names]
+    inputs = [lat0, scale, shift] + params
+    res = []
+    for fused in (True, False):
+        L.FUSED_BOUNDARY = fused
+        try:
+            o = L._TrunkChain.apply(lat0, scale, shift, 0.5, apps, scaled, heads, *params)
+            out, raw = o if heads else (o, None)
+            loss = (out * w).sum() + out[-1].square().sum() + ((raw * wh).sum() if heads else 0.0)
+            res.append((out.detach().clone(), torch.autograd.grad(loss, inputs)))
+        finally:
+            L.FUSED_BOUNDARY = True
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0])
+    for n, a, b in zip(["latent0", "scale", "shift"] + names, res[0][1], res[1][1]):
+        assert torch.equal(a, b), n
+
+
 def test_dynamics_chain_node_matches_per_step_autograd(cuda):
     """learner._TrunkChain (the K-step latent chain as one autograd node, batched weight gradients) against the
     per-step graph of the same layers (loss_fn's CPU-style loop run on the GPU): forward within 1e-5, gradients
