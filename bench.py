@@ -865,6 +865,17 @@ def run_det(args):
     elapsed = timed_region(dist, step, args.steps)
     (steps_done, searches, search_ms, launches), elapsed = sum_max(
         dist, device, [acc["steps"], acc["searches"], acc["search_ms"], acc["launches"]], elapsed)
+    # Secondary figure in the reference's own loop shape (game_agent.py:185-192): ONE play_n_games_v3 batch of
+    # --batch games per rank played to completion (the batch shrinks as games finish), timed on its own after
+    # the K streamed steps; `value` stays the streamed rate.
+    single = {"steps": 0}
+
+    def single_batch(_):
+        single["steps"] += int(eng.play(seed=10_000 * rank + 999, temperature=TEMP)["idx"].sum().item())
+
+    single_elapsed = timed_region(dist, single_batch, 1) if args.games else None
+    if single_elapsed is not None:
+        (single_steps,), single_elapsed = sum_max(dist, device, [single["steps"]], single_elapsed)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -896,11 +907,20 @@ def run_det(args):
                    "num_simulations": args.sims, "max_depth": args.depth,
                    "parallelism": parallelism(args, world)},
         "sims_per_s": round(searches * args.sims / elapsed, 1),
+        "value_single_batch": (round(single_steps / single_elapsed, 2) if single_elapsed else round(value, 2)),
+        "single_batch": ({"games_per_gpu": args.batch, "env_steps": int(single_steps),
+                          "seconds": round(single_elapsed, 4), "unit": "env_steps/s",
+                          "what": "one play_n_games_v3 batch per rank to completion (game_agent.py:185-192), "
+                                  "timed after the streamed steps"} if single_elapsed else
+                         {"what": "--games 0: value itself is the single-batch rate"}),
         "env_steps": int(steps_done),
         "searches": int(searches),
         "roofline": {"bound": "mfma", "kernel": "k_gumbel_search", "achieved": round(achieved, 3),
                      "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                     # the same algorithmic FLOP over the whole wall clock (root inference, env kernels, host gaps)
+                     "end_to_end_frac": round(searches * args.sims * FLOP_PER_SIM / elapsed / 1e12
+                                              / PEAK_FP32_MFMA_TFLOPS / world, 4),
                      "avg_launch_ms": round(search_ms / max(1, launches), 4),
                      "flop_per_sim": FLOP_PER_SIM, "executed_flop_per_sim": EXEC_FLOP_PER_SIM,
                      "executed_frac": round(achieved * EXEC_FLOP_PER_SIM / FLOP_PER_SIM / PEAK_FP32_MFMA_TFLOPS, 4),

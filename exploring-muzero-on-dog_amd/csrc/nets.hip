@@ -1,5 +1,7 @@
 // MuZero network kernels: root_inference_fn and recurrent_inference_fn
 // (MuZero_det_MADN/muzero_deterministic_madn.py:621-661) as fused fp32 MFMA kernels.
+#include <type_traits>
+
 #include "launch.hpp"
 #include "nn.hpp"
 
@@ -23,18 +25,18 @@ __device__ __forceinline__ void ln_positions(const float* pre, float* out, int o
   for (int i = 0; i < PER; ++i) {
     v[i] = pre[pos * kPreLd + q + 4 * i];
     s += v[i];
-    s2 += v[i] * v[i];
+    s2 = fmaf(v[i], v[i], s2);
   }
   s += dpp<DPP_XOR1>(s);
   s += dpp<DPP_XOR2>(s);
   s2 += dpp<DPP_XOR1>(s2);
   s2 += dpp<DPP_XOR2>(s2);
   const float mean = s / (float)N, mean2 = s2 / (float)N;
-  const float inv = ln_rstd(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
+  const float inv = ln_rstd(fmaxf(0.f, fmaf(-mean, mean, mean2)) + 1e-6f);
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = q + 4 * i;
-    out[(out_row0 + pos) * N + c] = fmaxf((v[i] - mean) * (inv * gp(P.scale)[c]) + gp(P.bias)[c], 0.f);
+    out[(out_row0 + pos) * N + c] = fmaxf(fmaf(v[i] - mean, inv * gp(P.scale)[c], gp(P.bias)[c]), 0.f);
   }
 }
 
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
 #pragma unroll
     for (int dk = 0; dk < 3; ++dk)
 #pragma unroll
-      for (int ci = 0; ci < 6; ++ci) s += in0[(w + dk) * 6 + ci] * gp(R.conv0.w)[(dk * 6 + ci) * 32 + co];
+      for (int ci = 0; ci < 6; ++ci) s = fmaf(in0[(w + dk) * 6 + ci], gp(R.conv0.w)[(dk * 6 + ci) * 32 + co], s);
     pre[w * kPreLd + co] = s + gp(R.conv0.b)[co];
   }
   __syncthreads();
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(kThreads) void k_root_dense(NW Wt, const float* __r
   if (valid)
     for (int c = sub; c < LAT; c += kRowLanes) embedding[(size_t)gr * LAT + c] = a.T[row * LD + c];
   __syncthreads();
-  pred16<1>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
+  pred16<1, false, false, kSplitkLogits && std::is_same<NW, muz_net_w>::value>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
   if (valid) {
     for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
     if (sub == 0) value[gr] = a.v0[row];
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
     }
   }
   // no barrier: pred16 reads a.T in its first pass and overwrites it only after its first SYNC
-  pred16<1>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
+  pred16<1, false, false, kSplitkLogits>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
   if (valid) {
     for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
     if (sub == 0) value[gr] = a.v0[row];

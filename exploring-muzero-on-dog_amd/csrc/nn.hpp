@@ -11,11 +11,30 @@
 #pragma once
 #include "common.hpp"
 
+// Rounding pinned: no fma contraction anywhere after this point (the networks here, and the search kernels' tree
+// arithmetic that includes this header); the products that should fuse are written as fmaf.  The compiler used to
+// contract differently per inlined context -- e.g. the fused Pred4 LayerNorm_0 of skip_minmax16 folded the min-max
+// multiply into the LayerNorm sums, which the separate ln16 pass cannot -- so the search kernel's networks and the
+// root / recurrent kernels (the parity tests' oracle side) differed in the last bit.  Now every kernel built on
+// these functions rounds identically.
+#ifndef MUZ_PINNED_ROUNDING
+#define MUZ_PINNED_ROUNDING 1
+#endif
+#if MUZ_PINNED_ROUNDING
+#pragma clang fp contract(off)
+#endif
+
 namespace muz {
 
 #ifndef MUZ_TILE_WAVES
 #define MUZ_TILE_WAVES 8   // waves per 16-row tile workgroup: 8 (2 per SIMD) or 16 (4 per SIMD)
 #endif
+// det networks' policy logits split over k (pred16 SPLITK_LOGITS; search, root and recurrent kernels alike, so
+// their outputs stay bit-identical to each other)
+#ifndef MUZ_SPLITK_LOGITS
+#define MUZ_SPLITK_LOGITS 0
+#endif
+constexpr bool kSplitkLogits = MUZ_SPLITK_LOGITS != 0;
 constexpr int kRows = 16;
 constexpr int kWaves = MUZ_TILE_WAVES;
 constexpr int kThreads = kWaves * 64;          // 512 / 1024
@@ -309,15 +328,28 @@ __device__ __forceinline__ void pf_issue(Pf& pf, const AS4 muz_dense* L, int K, 
 // Dense layer over the tile: out[16][N] = A @ W + b, waves split N (NT tiles of 16 columns each).
 // `pf` holds this layer's first k-blocks on entry and the next layer's (Ln: K=Kn, N=Nn, NTN tiles)
 // on exit.  A may live in LDS or global memory.  Caller synchronises before/after.
+// split-K prefetch of a <= 32-column layer (logits16_splitk): wave w takes k-block w of column tiles 0 and 1
+__device__ __forceinline__ void pf_issue_splitk(Pf& pf, const AS4 muz_dense* L, int K) {
+  const int KB = (K + 15) >> 4, w = threadIdx.x >> 6;
+  if (w >= KB) return;
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(L->w)) + (threadIdx.x & 63);
+  pf.v0[0] = wp[(0 * KB + w) * 64];   // packed [group][kb][lane][t = 0][4], groups = 16-column tiles
+  pf.v1[0] = wp[(1 * KB + w) * 64];
+}
+
 template <int NT, int NTN>
 __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
                                         int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
-                                        bool a_global = false) {
+                                        bool a_global = false, bool next_splitk = false) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int KB = (K + 15) >> 4;
   const int col0 = wv * NT * 16;
+  auto pf_next = [&]() {
+    if (next_splitk) pf_issue_splitk(pf, Ln, Kn);
+    else pf_issue<NTN>(pf, Ln, Kn, Nn);
+  };
   if (col0 >= N) {
-    pf_issue<NTN>(pf, Ln, Kn, Nn);
+    pf_next();
     return;
   }
   const int r = lane & 15, g = lane >> 4;
@@ -334,7 +366,7 @@ __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, co
   ST(ST_DENTRY);
   mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, a_global);
   ST(ST_MFMA);
-  pf_issue<NTN>(pf, Ln, Kn, Nn);
+  pf_next();
   // The MFMA computes out^T (weights as the A operand), so lane (r, g) holds 4 CONSECUTIVE output
   // columns of row r: one 16-byte bias load and one ds_write_b128 per tile.
 #pragma unroll
@@ -464,7 +496,7 @@ __device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int l
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         s += v[i][q];
-        s2 += v[i][q] * v[i][q];
+        s2 = fmaf(v[i][q], v[i][q], s2);
       }
     }
   }
@@ -472,7 +504,7 @@ __device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int l
   s2 = row_sum(s2);
   const float mean = s / (float)N;
   const float mean2 = s2 / (float)N;
-  const float var = fmaxf(0.f, mean2 - mean * mean);
+  const float var = fmaxf(0.f, fmaf(-mean, mean, mean2));
   const float inv = ln_rstd(var + 1e-6f);
   if (act) {
 #pragma unroll
@@ -480,7 +512,7 @@ __device__ __forceinline__ void ln16(const float* in, int ldi, float* out, int l
       const int c = RV::col(sub, i);
       f32x4 y;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) y[q] = (v[i][q] - mean) * (inv * p.sc[i][q]) + p.sh[i][q];
+      for (int q = 0; q < 4; ++q) y[q] = fmaf(v[i][q] - mean, inv * p.sc[i][q], p.sh[i][q]);
       if (MODE == LN_RELU) y = relu4(y);
       if (MODE == LN_RESID_RELU) y = relu4(lds4(out + row * ldo + c) + y);
       sts4(out + row * ldo + c, y);
@@ -526,7 +558,7 @@ __device__ __forceinline__ void minmax16(float* buf, int ld) {
 // in the tree, when non-null) and PredictionNetwork4's LayerNorm_0 of it to `lnout`, so pred16 can start with
 // its first ResBlock (same arithmetic, in the same order, as ln16<LAT, LN_PLAIN>).
 __device__ __forceinline__ void skip_minmax16(float* buf, const float* skip, int ld, const LnP<LAT>* ln = nullptr,
-                                              AS1 float* emb = nullptr, float* lnout = nullptr) {
+                                              AS1 float* emb = nullptr, float* lnout = nullptr, float* dst = nullptr) {
   using RV = RowVec<LAT>;
   const int row = trow(), sub = tsub();
   f32x4 v[RV::V];
@@ -548,7 +580,7 @@ __device__ __forceinline__ void skip_minmax16(float* buf, const float* skip, int
     f32x4 y;
 #pragma unroll
     for (int q = 0; q < 4; ++q) y[q] = mm_scale(v[i][q] - lo, den);
-    sts4(buf + row * ld + RV::col(sub, i), y);
+    sts4((dst ? dst : buf) + row * ld + RV::col(sub, i), y);   // (each lane reads its own skip / buf first)
     v[i] = y;
   }
   if (!ln) return;
@@ -562,19 +594,19 @@ __device__ __forceinline__ void skip_minmax16(float* buf, const float* skip, int
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       s += v[i][q];
-      s2 += v[i][q] * v[i][q];
+      s2 = fmaf(v[i][q], v[i][q], s2);
     }
   s = row_sum(s);
   s2 = row_sum(s2);
   const float mean = s / (float)LAT;
   const float mean2 = s2 / (float)LAT;
-  const float var = fmaxf(0.f, mean2 - mean * mean);
+  const float var = fmaxf(0.f, fmaf(-mean, mean, mean2));
   const float inv = ln_rstd(var + 1e-6f);
 #pragma unroll
   for (int i = 0; i < RV::V; ++i) {
     f32x4 y;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) y[q] = (v[i][q] - mean) * (inv * ln->sc[i][q]) + ln->sh[i][q];
+    for (int q = 0; q < 4; ++q) y[q] = fmaf(v[i][q] - mean, inv * ln->sc[i][q], ln->sh[i][q]);
     sts4(lnout + row * ld + RV::col(sub, i), y);
   }
 }
@@ -582,6 +614,41 @@ __device__ __forceinline__ void skip_minmax16(float* buf, const float* skip, int
 __device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
   const int row = trow(), sub = tsub();
   for (int c = sub * 4; c < n; c += 4 * kRowLanes) sts4(buf + row * ld + col0 + c, relu4(lds4(buf + row * ld + col0 + c)));
+}
+
+// Policy logits (Dense_2: K = 128 -> A <= 32) split over the k dimension instead of the columns: wave w multiplies
+// k-block w of both 16-column tiles (8 MFMAs, operands from pf_issue_splitk) and leaves its partial products in
+// part[w][16][32]; logits16_splitk_sum adds the K / 16 partials and the bias per (row, column) after the next
+// barrier.  The column split kept 6 of the 8 waves idle behind a 32-MFMA chain on two of them.
+template <int NTN>
+__device__ __forceinline__ void logits16_splitk(int K, const float* A, int lda, float* part, Pf& pf,
+                                                const AS4 muz_dense* Ln, int Kn, int Nn) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int KB = (K + 15) >> 4;
+  if (w >= KB) {
+    pf_issue<NTN>(pf, Ln, Kn, Nn);
+    return;
+  }
+  const int r = lane & 15, g = lane >> 4;
+  const f32x4 a = *reinterpret_cast<const f32x4*>(A + r * lda + w * 16 + 4 * g);
+  const f32x4 b0 = pf.v0[0], b1 = pf.v1[0];
+  f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    acc0 = mfma4(b0[j], a[j], acc0);
+    acc1 = mfma4(b1[j], a[j], acc1);
+  }
+  pf_issue<NTN>(pf, Ln, Kn, Nn);
+  float* pw = part + (w * 16 + r) * 32 + 4 * g;
+  *reinterpret_cast<f32x4*>(pw) = acc0;
+  *reinterpret_cast<f32x4*>(pw + 16) = acc1;
+}
+// logit (row trow(), column tsub() < N) = bias + sum of the K / 16 partials (k-block order); this lane only
+__device__ __forceinline__ float logits16_splitk_sum(const AS4 muz_dense& L, int K, const float* part) {
+  const int KB = (K + 15) >> 4, row = trow(), c = tsub();
+  float s = part[row * 32 + c];
+  for (int w = 1; w < KB; ++w) s += part[(w * 16 + row) * 32 + c];
+  return s + gp(L.b)[c];
 }
 
 // ---- LDS arena of a 16-row tile ---------------------------------------------------------------------
@@ -674,7 +741,7 @@ __device__ __forceinline__ float head_dot_relu(const float* in, int ld, const fl
 #pragma unroll
   for (int i = 0; i < HeadK<K>::kPer; ++i) {
     const int k = tsub() + i * kRowLanes;
-    if (k < K) s += fmaxf(in[trow() * ld + k] + add[i], 0.f) * h.w[j][i];
+    if (k < K) s = fmaf(fmaxf(in[trow() * ld + k] + add[i], 0.f), h.w[j][i], s);
   }
   return row_sum(s) + h.b[j];
 }
@@ -684,9 +751,17 @@ __device__ __forceinline__ float head_dot(const float* in, int ld, const HeadK<K
 #pragma unroll
   for (int i = 0; i < HeadK<K>::kPer; ++i) {
     const int k = tsub() + i * kRowLanes;
-    if (k < K) s += in[trow() * ld + k] * h.w[j][i];
+    if (k < K) s = fmaf(in[trow() * ld + k], h.w[j][i], s);
   }
   return row_sum(s) + h.b[j];
+}
+
+__device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) {
+  // sum(softmax(l) * [-1, 0, 1])  (recurrent_inference_fn 648-653)
+  const float m = fmaxf(fmaxf(l0, l1), l2);
+  const float e0 = expf(l0 - m), e1 = expf(l1 - m), e2 = expf(l2 - m);
+  const float z = e0 + e1 + e2;
+  return mm_scale(e0, z) * -1.0f + mm_scale(e1, z) * 0.0f + mm_scale(e2, z) * 1.0f;
 }
 
 // PredictionNetwork4 (muzero_deterministic_madn.py:549-583) on the latent in `lat` ([16][LD]).
@@ -694,9 +769,17 @@ __device__ __forceinline__ float head_dot(const float* in, int ld, const HeadK<K
 // pf: rb[0].d0 on entry, (Ln, NTN tiles) on exit.
 // LN0_DONE: the caller already left LayerNorm_0(lat) in a.X (dyn16<.., true>), so the pass and its barrier
 // are skipped.
-template <int NTN, bool LN0_DONE = false>
+// LATE_HEADS (search kernel, with dyn16<.., true, true>): Dyn4's reward / discount trunk -- Dense_6 | Dense_7 over
+// the new latent (left in a.L by dyn16) and the two 64 -> 3 support heads -- runs here, its MFMA loop in the same
+// barrier interval as policy Dense_1 / value Dense_4 and its head dots in the following row pass, instead of a
+// dense phase and a row phase of its own.  `D` / `ar`: Dyn4's weights and the row's action.  Leaves the reward /
+// discount support values in a.v1 / a.v2 like dyn16.
+// SPLITK_LOGITS: the policy logits by logits16_splitk (partials in a.W, summed per lane at the end into a.U; a
+// caller reads a.U[row][c] only from lane (row, c), as all of them do).
+template <int NTN, bool LN0_DONE = false, bool LATE_HEADS = false, bool SPLITK_LOGITS = false>
 __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const float* lat, const Arena& a, Pf& pf,
-                                       const AS4 muz_dense* Ln, int Kn, int Nn) {
+                                       const AS4 muz_dense* Ln, int Kn, int Nn, const AS4 muz_dyn_w* D = nullptr,
+                                       int ar = 0) {
   if constexpr (!LN0_DONE) {
     ln16<LAT, LN_PLAIN>(lat, LD, a.X, LD, P.ln0);
     SYNC();
@@ -712,28 +795,62 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
   SYNC();
   const LnP<128> p2 = ln_load<128>(P.ln2);
   const HeadW hv = head_load(P.d5, 1);
-  dense16<NT128, NT64>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &P.d4, 128, 64);     // policy Dense_1
-  dense16<NT64, NTA>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, A);  // value Dense_4 (X is free)
-  SYNC();
-  ln16<128, LN_RELU>(a.T, LD, a.T, LD, p2);
-  relu16(a.X, LD, 0, 64);
+  if constexpr (LATE_HEADS) {
+    dense16<NT128, NT128>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &D->d67, LAT, 128);   // policy Dense_1
+    // reward / discount heads and Dense_6 | Dense_7's one-hot rows at this lane's head inputs: issued here, they
+    // land under the two MFMA loops below
+    const HeadW hr = head_load(D->reward_head, 3);
+    const HeadW hd = head_load(D->discount_head, 3);
+    const bool oh = ar >= 0 && ar < A;
+    float add_r[HeadW::kPer], add_d[HeadW::kPer];
+    {
+      const AS1 float* w67 = gp(D->d67_onehot) + (oh ? ar : 0) * 128;
+#pragma unroll
+      for (int i = 0; i < HeadW::kPer; ++i) {
+        const int k = tsub() + i * kRowLanes;
+        add_r[i] = (oh && k < 64) ? w67[k] : 0.f;
+        add_d[i] = (oh && k < 64) ? w67[64 + k] : 0.f;
+      }
+    }
+    dense16<NT128, NT64>(D->d67, LAT, 128, a.L, LD, a.U, LD, pf, &P.d4, 128, 64);   // [reward | discount] hidden
+    dense16<NT64, NTA>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, A, false,
+                       SPLITK_LOGITS);                                              // value Dense_4 (X is free)
+    SYNC();
+    ln16<128, LN_RELU>(a.T, LD, a.T, LD, p2);
+    relu16(a.X, LD, 0, 64);
+    float rl[3], dl[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      rl[j] = head_dot_relu(a.U, LD, add_r, hr, j);
+      dl[j] = head_dot_relu(a.U + 64, LD, add_d, hd, j);
+    }
+    if (tsub() == 0) {
+      a.v1[trow()] = softmax3_support(rl[0], rl[1], rl[2]);
+      a.v2[trow()] = softmax3_support(dl[0], dl[1], dl[2]);
+    }
+  } else {
+    dense16<NT128, NT64>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &P.d4, 128, 64);     // policy Dense_1
+    dense16<NT64, NTA>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, A, false,
+                       SPLITK_LOGITS);                                              // value Dense_4 (X is free)
+    SYNC();
+    ln16<128, LN_RELU>(a.T, LD, a.T, LD, p2);
+    relu16(a.X, LD, 0, 64);
+  }
   ST(ST_PASS);
   SYNC();
-  dense16<NTA, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn);         // policy logits
+  if constexpr (SPLITK_LOGITS)
+    logits16_splitk<NTN>(128, a.T, LD, a.W, pf, Ln, Kn, Nn);                  // policy logits, split over k
+  else
+    dense16<NTA, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn);         // policy logits
   {
     const float v = head_dot(a.X, LD, hv, 0);
     if (tsub() == 0) a.v0[trow()] = tanhf(v);
   }
   ST(ST_PASS);
   SYNC();
-}
-
-__device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) {
-  // sum(softmax(l) * [-1, 0, 1])  (recurrent_inference_fn 648-653)
-  const float m = fmaxf(fmaxf(l0, l1), l2);
-  const float e0 = expf(l0 - m), e1 = expf(l1 - m), e2 = expf(l2 - m);
-  const float z = e0 + e1 + e2;
-  return mm_scale(e0, z) * -1.0f + mm_scale(e1, z) * 0.0f + mm_scale(e2, z) * 1.0f;
+  if constexpr (SPLITK_LOGITS) {
+    if (tsub() < A) a.U[trow() * LD + tsub()] = logits16_splitk_sum(P.d2, 128, a.W);
+  }
 }
 
 // Dyn4 inputs of this thread's row, loaded as soon as the parent node and action are known (end of the
@@ -768,10 +885,13 @@ __device__ __forceinline__ DynIn dyn_load(const AS4 muz_dyn_w& D, int A, const A
 // PRED_LN0: fuse the following pred16's LayerNorm_0 (params `pln0`) into the latent's min-max pass, store the
 // latent to the tree at `emb` there (null: no store), and end without the final barrier; the caller then runs
 // pred16<.., true>, whose first writes (ResBlock_0's Dense_0 into a.T) come after d67 has consumed a.T.
-template <int NTN, bool PRED_LN0 = false>
+// LATE_HEADS (with PRED_LN0): stop after the min-max pass, which leaves the new latent in a.L (and a.T is free),
+// and let pred16<.., true, true> run Dense_6 | Dense_7 and the reward / discount heads; ends with a barrier.
+template <int NTN, bool PRED_LN0 = false, bool LATE_HEADS = false>
 __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn& in, int ar, const Arena& a, Pf& pf,
                                       const AS4 muz_dense* Ln, int Kn, int Nn, const AS4 muz_ln* pln0 = nullptr,
                                       AS1 float* emb = nullptr) {
+  static_assert(!LATE_HEADS || PRED_LN0, "late heads need the fused Pred4 LayerNorm_0");
   using RV = RowVec<LAT>;
   const int row = trow(), sub = tsub();
   const bool oh = ar >= 0 && ar < A;   // jax.nn.one_hot: out-of-range -> zero row
@@ -783,21 +903,21 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         s += in.lat[i][q];
-        s2 += in.lat[i][q] * in.lat[i][q];
+        s2 = fmaf(in.lat[i][q], in.lat[i][q], s2);
       }
     s = row_sum(s);
     s2 = row_sum(s2);
     const float mean = s / (float)LAT;
     const float mean2 = s2 / (float)LAT;
-    const float inv = ln_rstd(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
+    const float inv = ln_rstd(fmaxf(0.f, fmaf(-mean, mean, mean2)) + 1e-6f);
 #pragma unroll
     for (int i = 0; i < RV::V; ++i) {
       const int c = RV::col(sub, i);
       f32x4 x;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float y = (in.lat[i][q] - mean) * (inv * in.ln0.sc[i][q]) + in.ln0.sh[i][q];
-        x[q] = y * (1.0f + in.sc[i][q]) + in.sh[i][q];
+        const float y = fmaf(in.lat[i][q] - mean, inv * in.ln0.sc[i][q], in.ln0.sh[i][q]);
+        x[q] = fmaf(y, 1.0f + in.sc[i][q], in.sh[i][q]);
       }
       sts4(a.X + row * LD + c, x);
       sts4(a.L + row * LD + c, in.lat[i]);
@@ -817,6 +937,15 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
   SYNC();
   resblock16<NT256>(D.rb[0], a.X, a.T, a.U, pf, &D.rb[1].d0, LAT, LAT);
   resblock16<NT256>(D.rb[1], a.X, a.T, a.U, pf, &D.d5, LAT, LAT);
+  if constexpr (LATE_HEADS) {
+    dense16<NT256, NTN>(D.d5, LAT, LAT, a.X, LD, a.T, LD, pf, Ln, Kn, Nn);
+    const LnP<LAT> pl = ln_load<LAT>(*pln0);
+    SYNC();
+    skip_minmax16(a.T, a.L, LD, &pl, emb, a.X, a.L);
+    ST(ST_PASS);
+    SYNC();
+    return;
+  }
   const HeadW hr = head_load(D.reward_head, 3);
   const HeadW hd = head_load(D.discount_head, 3);
   dense16<NT256, NT128>(D.d5, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d67, LAT, 128);

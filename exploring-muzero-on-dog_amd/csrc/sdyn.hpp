@@ -61,21 +61,21 @@ __device__ __forceinline__ void film_trunk16(const TrunkW& W, const FilmIn& in, 
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         s += in.s[i][q];
-        s2 += in.s[i][q] * in.s[i][q];
+        s2 = fmaf(in.s[i][q], in.s[i][q], s2);
       }
     s = row_sum(s);
     s2 = row_sum(s2);
     const float mean = s / (float)LAT;
     const float mean2 = s2 / (float)LAT;
-    const float inv = ln_rstd(fmaxf(0.f, mean2 - mean * mean) + 1e-6f);
+    const float inv = ln_rstd(fmaxf(0.f, fmaf(-mean, mean, mean2)) + 1e-6f);
 #pragma unroll
     for (int i = 0; i < RV::V; ++i) {
       const int c = RV::col(sub, i);
       f32x4 x;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float y = (in.s[i][q] - mean) * (inv * in.ln.sc[i][q]) + in.ln.sh[i][q];
-        x[q] = y * (1.0f + in.sc[i][q]) + in.sh[i][q];
+        const float y = fmaf(in.s[i][q] - mean, inv * in.ln.sc[i][q], in.ln.sh[i][q]);
+        x[q] = fmaf(y, 1.0f + in.sc[i][q], in.sh[i][q]);
       }
       sts4(a.X + row * LD + c, x);
       sts4(a.L + row * LD + c, in.s[i]);

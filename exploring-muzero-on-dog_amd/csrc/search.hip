@@ -35,6 +35,12 @@ __device__ unsigned long long g_muz_stamps[8];
 // them measured within noise on MI355X (B=4096 S=50: +-1 %), so they stay.  A static s_setprio 1 for
 // waves 4-7 also measured within noise (profiles/r1e_prio_ab.log).
 
+// Dyn4's reward / discount trunk inside Pred4's Dense_1 phase (nn.hpp pred16 LATE_HEADS)
+#ifndef MUZ_LATE_HEADS
+#define MUZ_LATE_HEADS 0
+#endif
+constexpr bool kLateHeads = MUZ_LATE_HEADS != 0;
+
 constexpr int kMaxSims = 100;              // S <= 100 (config (e) uses 100)
 constexpr int kMaxNodes = kMaxSims + 1;
 constexpr int kMaxDepth = 64;
@@ -120,6 +126,26 @@ __device__ __forceinline__ void row_argmax(float& v, int& i) {
   }
 }
 
+// ---- the tree arithmetic, bit for bit like the NumPy restatement (oracle/mctx_gumbel.py) -------------------
+// With identical network outputs on both sides the search's floats then agree exactly (tests/_parity.py):
+//  * no fma contraction (q = r + d * v, the mixed value and the backup round twice, like numpy);
+//  * a sum over the 24 actions in numpy's pairwise order for a contiguous row of 24: r_j = (a_j + a_{j+8}) +
+//    a_{j+16} for j < 8, then ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+//  * exp correctly rounded: evaluated in float64 and rounded once (numpy's float32 exp and the device's expf
+//    are each ~1 ulp off in different places; the oracle rounds the float64 exp the same way).
+enum { DPP_ROW_ROR8 = 0x128 };
+__device__ __forceinline__ float row_sum24(float v) {
+  static_assert(kRowLanes == 32, "row_sum24: one game per 32 lanes");
+  if (tsub() >= 24) v = -0.0f;                  // the additive identity for every x, -0 included
+  v = v + dpp<DPP_ROW_ROR8>(v);                 // a_j + a_{j+8} (lanes 16..23: a_{16+j} + -0)
+  const LoHi<float> p = swap16(v);
+  v = p.lo + p.hi;                              // r_j = (a_j + a_{j+8}) + a_{j+16} in lanes j, j+8, j+16, j+24
+  v = v + dpp<DPP_XOR1>(v);                     // r0 + r1 | r2 + r3 | ...
+  v = v + dpp<DPP_XOR2>(v);                     // (r0 + r1) + (r2 + r3) | (r4 + r5) + (r6 + r7)
+  return v + dpp<DPP_HALF_MIRROR>(v);           // lane i <-> 7 - i: the two halves
+}
+__device__ __forceinline__ float exp_cr(float x) { return (float)exp((double)x); }
+
 // seq_halving.get_sequence_of_considered_visits(m, S)[idx] without the table.
 __device__ __forceinline__ int considered_visit(int m, int S, int idx) {
   if (m <= 1) return idx;
@@ -147,16 +173,17 @@ struct Kid {
 
 // qtransform_completed_by_mix_value (value_scale, maxvisit_init, rescale, mixed value, eps 1e-8).
 __device__ __forceinline__ float completed_q(const Kid& k, float raw, const SearchArgs& sa, int& sumv, float& pmax) {
+#pragma clang fp contract(off)
   const float q = k.reward + k.disc * k.value;
   const float pm = row_max(k.ok ? k.prior : -INFINITY);
-  const float e = k.ok ? expf(k.prior - pm) : 0.f;
-  const float es = row_sum(e);
+  const float e = k.ok ? exp_cr(k.prior - pm) : 0.f;
+  const float es = row_sum24(e);
   const float pp = fmaxf(kTinyF, e / es);
   const bool vis = k.ok && k.visits > 0;
   const int sv = row_isum(k.ok ? k.visits : 0);
   const int mv = row_imax(k.ok ? k.visits : 0);
-  const float sp = row_sum(vis ? pp : 0.f);
-  const float wq = row_sum(vis ? pp * q / sp : 0.f);
+  const float sp = row_sum24(vis ? pp : 0.f);
+  const float wq = row_sum24(vis ? pp * q / sp : 0.f);
   const float mixed = (raw + (float)sv * wq) / (float)(sv + 1);
   float cq = vis ? q : mixed;
   const float lo = row_min(k.ok ? cq : INFINITY);
@@ -173,6 +200,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     const float* __restrict__ root_emb, const uint32_t* __restrict__ legal, const float* __restrict__ gumbel_in,
     const int32_t* __restrict__ game_id, int n, const int* __restrict__ n_dev, TreeWs T, int32_t* out_action,
     float* out_weights, float* out_value) {
+  // tree arithmetic exactly as written (see row_sum24); the networks (nn.hpp) keep their own contraction
+#pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
   __shared__ int s_visits[kRows][kMaxNodes];
   __shared__ float s_raw[kRows][kMaxNodes];
@@ -279,8 +308,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
           // gumbel_muzero_interior_action_selection: softmax(prior + cq) - N / (1 + sum N)
           const float z = k.prior + cq;
           const float zm = row_max(ok ? z : -INFINITY);
-          const float ez = ok ? expf(z - zm) : 0.f;
-          const float zs = row_sum(ez);
+          const float ez = ok ? exp_cr(z - zm) : 0.f;
+          const float zs = row_sum24(ez);
           sc = ok ? (ez / zs - (float)k.visits / (float)(1 + sumv)) : -INFINITY;
         }
         int bi = a;
@@ -322,11 +351,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     // the new node's embedding goes to the tree and Pred4's LayerNorm_0 into ar.X straight from Dyn4's
     // min-max pass (registers), so Pred4 starts with its first ResBlock
     const int nx = s_next[row];
-    dyn16<NT256, true>(wl->dyn, A, din, dact, ar, pf, &wl->pred.rb[0].d0, LAT, LAT, &wl->pred.ln0,
-                       valid ? T.e(g, nx) : nullptr);
+    dyn16<NT256, true, kLateHeads>(wl->dyn, A, din, dact, ar, pf, &wl->pred.rb[0].d0, LAT, LAT, &wl->pred.ln0,
+                                   valid ? T.e(g, nx) : nullptr);
     MUZ_STAMP(3);   // dynamics
     MUZ_STAMP(4);   // embedding write (fused)
-    pred16<NT256, true>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d3, LAT, LAT);
+    pred16<NT256, true, kLateHeads, kSplitkLogits>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d3, LAT, LAT, &wl->dyn, dact);
     MUZ_STAMP(5);   // prediction
     if (valid) {
       const bool fresh = nx == sim + 1;
@@ -445,8 +474,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     const float zm = row_max(ok ? z : -INFINITY);
     const float zz = inv ? kFMin : z - zm;
     const float mm = row_max(ok ? zz : -INFINITY);
-    const float ez = ok ? expf(zz - mm) : 0.f;
-    const float zs = row_sum(ez);
+    const float ez = ok ? exp_cr(zz - mm) : 0.f;
+    const float zs = row_sum24(ez);
     if (ok) out_weights[(size_t)g * A + a] = ez / zs;
     if (a == 0) {
       out_action[g] = bi;

@@ -408,6 +408,9 @@ class GradSink:
             _L.check(lib.muz_colsum_grouped(arr, len(self.cs), st), "muz_colsum_grouped")
         for p, g in self.buf.values():
             if id(p) in self.owned:
+                if p.grad is not None and p.grad is not g:
+                    # the parameter also reached autograd through a plain torch op: keep that term
+                    g.add_(p.grad)
                 p.grad = g
         self.wg, self.cs, self.keep, self.owned = [], [], [], set()
 
@@ -919,8 +922,8 @@ class _LossHeads(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_total, g_parts):
-        d = list(ctx.d)
-        torch._foreach_mul_(d, g_total)
+        # out of place: the saved output gradients stay intact for a second backward (retain_graph, gradcheck)
+        d = torch._foreach_mul(list(ctx.d), g_total)
         it = iter(d[2:])
         return (d[0], d[1], *(next(it) if p else None for p in ctx.present), None)
 

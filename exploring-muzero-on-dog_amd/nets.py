@@ -293,17 +293,38 @@ def as_device_net(params, obs_channels: int | None = None, device="cuda") -> Dev
     C = int(flat["representation/Dense_1/kernel"].shape[0]) + 6 if obs_channels is None else int(obs_channels)
     A = int(flat["prediction/Dense_2/kernel"].shape[1])
     net = DeviceNet(flat, C, A, device=device)
+    prev = next(iter(_NET_CACHE.values()), None)
+    if prev is not None and (prev[1].C, prev[1].A) == (C, A) and prev[1].buffer.shape == net.buffer.shape \
+            and prev[1].buffer.device == net.buffer.device:
+        # same shapes: the new weights go into the live DeviceNet, so engines cached on it (game_agent.cached_engine)
+        # keep their state, workspace and buffers across a training loop's iterations
+        prev[1].buffer.copy_(net.buffer)
+        prev[1].prepare()
+        net = prev[1]
     _NET_CACHE.clear()          # one live weight set per process is what the reference's loops use
     _NET_CACHE[id(params)] = (params, net, fp)
     return net
 
 
+_VERSIONED = {}    # id(tree) -> (tree, version()): trees whose owner updates the leaves in place
+
+
+def register_versioned_params(tree, version):
+    """``tree``'s leaves are updated in place by an owner that counts its updates (training.OptState: the
+    learner's steps): params_fingerprint of that tree is then the count, not an inference from the values."""
+    _VERSIONED[id(tree)] = (tree, version)
+
+
 def params_fingerprint(params) -> tuple:
     """Content fingerprint of a parameter tree, so an in-place update of the same dict / arrays between
-    calls invalidates as_device_net's cache: per NumPy leaf a CRC32 of its bytes (~10 ms for the 11 MB det
-    tree); the torch leaves (e.g. a learner's live parameters, which the fused AdamW kernel updates through
+    calls invalidates as_device_net's cache: a tree registered by its owner (register_versioned_params: the
+    learner's live tree) by the owner's update count; otherwise per NumPy leaf a CRC32 of its bytes (~10 ms for
+    the 11 MB det tree), the torch leaves (e.g. a learner's live parameters, which the fused AdamW kernel updates through
     raw pointers, so torch's version counters do not move) by their L2 norms, all in one multi-tensor kernel
     and one device-to-host copy."""
+    hit = _VERSIONED.get(id(params))
+    if hit is not None and hit[0] is params:
+        return (("version", int(hit[1]())),)
     import zlib
     out, tens = [], []
 

@@ -216,6 +216,13 @@ def as_device_classic_net(params, obs_channels: int | None = None, device="cuda"
     flat = {k: np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v, np.float32) for k, v in flat.items()}
     C = int(flat["representation/Dense_1/kernel"].shape[0]) + 6 if obs_channels is None else int(obs_channels)
     net = DeviceClassicNet(flat, C, device=device)
+    prev = next(iter(_NET_CACHE.values()), None)
+    if prev is not None and prev[1].C == C and prev[1].buffer.shape == net.buffer.shape \
+            and prev[1].buffer.device == net.buffer.device:
+        # same shapes: new weights into the live net, so the cached self-play engine keeps its buffers
+        prev[1].buffer.copy_(net.buffer)
+        prev[1].prepare()
+        net = prev[1]
     _NET_CACHE.clear()
     _NET_CACHE[id(params)] = (params, net, fp)
     return net

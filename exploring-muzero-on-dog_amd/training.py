@@ -40,6 +40,9 @@ class OptState:
     def __init__(self, learner: LR.Learner):
         self.learner = learner
         self.tree = CK.flat_to_muzero_tree(learner.nets.p)      # leaves: the live parameter tensors
+        self.version = 0                                        # in-place updates of the tree so far
+        from . import nets as N
+        N.register_versioned_params(self.tree, lambda: self.version)
 
     @property
     def count(self) -> int:
@@ -49,6 +52,7 @@ class OptState:
         """Make the learner's parameters equal ``params`` (a no-op for the tree train_step handed out)."""
         if params is self.tree:
             return
+        self.version += 1
         flat = _flat(params)
         if set(flat) != set(self.learner.nets.p):
             raise ValueError("params do not match the learner's parameter names")
@@ -72,6 +76,7 @@ class OptState:
                 m.copy_(torch.from_numpy(np.asarray(sd["mu"][k], np.float32).reshape(m.shape)))
                 v.copy_(torch.from_numpy(np.asarray(sd["nu"][k], np.float32).reshape(v.shape)))
             self.learner.opt.count.fill_(float(sd["count"]))
+        self.version += 1
 
 
 class Optimizer:
@@ -110,6 +115,7 @@ def train_step(params, opt_state: OptState, batch: dict):
     MuZero loss.  The returned params / opt_state are the learner's live state (the reference rebinds both)."""
     opt_state.bind(params)
     losses = opt_state.learner.train_step(batch)
+    opt_state.version += 1
     return opt_state.tree, opt_state, losses
 
 
@@ -118,6 +124,7 @@ def train_step_from(params, opt_state: OptState, replay):
     captured step's inputs (Learner.train_step_from; same draws, same result)."""
     opt_state.bind(params)
     losses = opt_state.learner.train_step_from(replay)
+    opt_state.version += 1
     return opt_state.tree, opt_state, losses
 
 

@@ -144,6 +144,13 @@ class _WeightUpdate:
             self.work = None
             if self.receiver and hasattr(self.net, "prepare"):
                 self.net.prepare()
+            # RCCL's work.wait() only orders the CURRENT stream after the broadcast (and prepare() is queued on
+            # it), while self-play and the learner run on streams of their own: block the host until the arena
+            # and its FiLM tables are final, so no later launch on any stream reads a half-received arena (an
+            # actor) or overwrites one the broadcast is still sending (the learner's next push_to).
+            buf = getattr(self.net, "buffer", None)
+            if isinstance(buf, torch.Tensor) and buf.is_cuda:
+                torch.cuda.current_stream(buf.device).synchronize()
 
 
 def broadcast_weights_async(net, src: int = 0, group=None) -> _WeightUpdate:

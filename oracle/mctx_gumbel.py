@@ -61,9 +61,16 @@ def score_considered(considered_visit, gumbel, logits, normalized_qvalues, visit
 
 
 # ---------------------------------------------------------------- helpers
+def exp_cr(x):
+    """float32 exp, correctly rounded: evaluated in float64 and rounded once.  numpy's own float32 exp is up to
+    a few ulp off (and its SIMD kernels differ between host CPUs); jax's is another polynomial.  The device
+    search (csrc/search.hip exp_cr) rounds the same float64 exp, so the tree arithmetic compares bit for bit."""
+    return np.exp(np.asarray(x, F32).astype(np.float64)).astype(F32)
+
+
 def softmax(x):
     x = x.astype(F32)
-    u = np.exp(x - x.max(-1, keepdims=True))
+    u = exp_cr(x - x.max(-1, keepdims=True))
     return (u / u.sum(-1, keepdims=True)).astype(F32)
 
 

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 4: pinned network rounding (default build) -- parity tests; late-heads / split-K logits variants -- parity
+# tests and an interleaved A/B (search microbenchmark B=4096 S=50, 3 repetitions).
+set -o pipefail
+O=gpurun_out/r4b
+mkdir -p $O
+rm -f gpurun_out/parity.log
+timeout -k 10 900 python -u -m pytest tests/test_gpu_search.py tests/test_gpu_nets.py tests/test_gpu_headline.py \
+  tests/test_gpu_selfplay.py tests/test_gpu_stochastic.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 \
+  || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+cp gpurun_out/parity.log $O/parity.log
+V=$PWD/exploring-muzero-on-dog_amd/variants
+rm -f gpurun_out/parity.log
+MUZ_LIB=$V/libmuz_lhd2k.so timeout -k 10 600 python -u -m pytest tests/test_gpu_search.py tests/test_gpu_nets.py \
+  -x -q --timeout 300 --timeout-method thread > $O/tests_lhd2k.log 2>&1 || { tail -40 $O/tests_lhd2k.log; exit 1; }
+tail -2 $O/tests_lhd2k.log
+cp gpurun_out/parity.log $O/parity_lhd2k.log
+for rep in 1 2 3; do
+  for v in r3 base pr0 lh d2k lhd2k; do
+    if [ $v = base ]; then unset MUZ_LIB; else export MUZ_LIB=$V/libmuz_$v.so; fi
+    timeout -k 10 120 python3 profiles/search_microbench.py 4096 50 2>/dev/null | tee -a $O/ab.log || exit 1
+  done
+done

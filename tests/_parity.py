@@ -42,10 +42,14 @@ def search_parity(label, ga, gw, grv, a, w, orv, margin, gain=None, tol=TOL, tie
     agree = np.asarray(ga) == np.asarray(a)
     dw = np.abs(np.asarray(gw) - np.asarray(w)).max(-1)
     dv = np.abs(np.asarray(grv) - np.asarray(orv))
-    wtol = tol + DQ * (np.zeros(B) if gain is None else np.asarray(gain))
+    g = np.zeros(B) if gain is None else np.asarray(gain)
+    wtol = tol + DQ * g
+    over = agree & (dw > tol)      # beyond the literal 1e-5: only the Q-rescale allowance admits these
     log(f"{label}: B={B} action agreement {agree.mean():.4f} ({int(agree.sum())}/{B}), differing games excused "
         f"as oracle near-ties {int((~agree).sum())}; agreeing games: max|dw| {dw[agree].max():.2e} "
-        f"(max |dw| / its bound {(dw / wtol)[agree].max():.3f}), max|dv| {dv[agree].max():.2e}")
+        f"(max |dw| / its bound {(dw / wtol)[agree].max():.3f}), max|dv| {dv[agree].max():.2e}; "
+        f"|dw| > {tol:g} in {int(over.sum())} games (largest gain among them "
+        f"{(g[over].max() if over.any() else 0.0):.3g}); bit-identical weights in {int((dw[agree] == 0).sum())}")
     bad = np.flatnonzero(~agree & ~tied)
     assert bad.size == 0, f"{label}: games {bad[:8]} chose differently without a near-tie (margins {np.asarray(margin)[bad[:8]]})"
     assert (dw[agree] <= wtol[agree]).all(), f"{label}: action_weights differ beyond tol + DQ x gain"
@@ -58,6 +62,7 @@ def selfplay_parity(label, buf, ref, exact_keys, float_keys=("val", "pol"), tol=
     [n, T] recorded per MCTS turn)."""
     n = len(ref["idx"])
     diverged, max_d = [], 0.0
+    over, over_gain, turns, exact = 0, 0.0, 0, 0   # turns with a float beyond the literal 1e-5 / bit-identical
     for i in range(n):
         L, Lg = int(ref["idx"][i]), int(buf["idx"][i])
         m = min(L, Lg)
@@ -76,7 +81,15 @@ def selfplay_parity(label, buf, ref, exact_keys, float_keys=("val", "pol"), tol=
             bound = tol + (DQ * ref["gain"][i, :t_star] if k == "pol" and "gain" in ref else 0.0)
             if t_star:
                 max_d = max(max_d, float(d.max()))
+                if k == "pol":
+                    o = d > tol
+                    over += int(o.sum())
+                    turns += t_star
+                    exact += int((d == 0).sum())
+                    if o.any() and "gain" in ref:
+                        over_gain = max(over_gain, float(ref["gain"][i, :t_star][o].max()))
             assert (d <= bound).all(), f"{label}: game {i} {k} differs by {d.max():.2e} beyond its bound"
     log(f"{label}: {n - len(diverged)}/{n} games identical; diverged at oracle near-ties {diverged}; "
-        f"max float |d| {max_d:.2e}; env-steps {int(ref['idx'].sum())}")
+        f"max float |d| {max_d:.2e}; policy turns |d| > {tol:g}: {over} of {turns} (largest gain among them "
+        f"{over_gain:.3g}), bit-identical {exact}; env-steps {int(ref['idx'].sum())}")
     return diverged

@@ -80,3 +80,37 @@ def test_classic_reference_signatures(cuda):
     a2, w2, v2 = ST.stochastic_muzero_mcts(ST.DeviceClassicNet(flat, C), torch.from_numpy(obs).cuda(), bits, 16, 8, 1.0,
                                            seed=9)
     assert torch.equal(pol.action, a2) and torch.equal(pol.action_weights, w2) and torch.equal(rv, v2)
+
+
+def test_play_n_games_v3_keeps_its_engine_across_weight_updates(cuda):
+    """A test_training-style loop hands play_n_games_v3 new weights every iteration: the engine (state, workspace,
+    GB-scale buffers) is reused and the new weights are the ones played (the cache used to miss)."""
+    CK, GA, GS, M, N, ST = _m()
+    C = dm.num_channels(2)
+    tree1 = CK.flat_to_muzero_tree(N.init_muzero_params(3, C))
+    tree2 = CK.flat_to_muzero_tree(N.init_muzero_params(4, C))
+    GA.play_n_games_v3(tree1, 5, (C, 56), 16, 8, 4, 60, 1.0)
+    eng1 = next(iter(GA._ENGINE_CACHE.values()))
+    got = {k: v.clone() for k, v in GA.play_n_games_v3(tree2, 5, (C, 56), 16, 8, 4, 60, 1.0).items()}
+    assert next(iter(GA._ENGINE_CACHE.values())) is eng1
+    GA._ENGINE_CACHE.clear()
+    N._NET_CACHE.clear()
+    want = GA.play_n_games_v3(tree2, 5, (C, 56), 16, 8, 4, 60, 1.0)    # a fresh engine on tree2
+    for k in ("act", "val", "pol", "idx"):
+        assert torch.equal(got[k], want[k]), k
+
+
+def test_learner_tree_version_drives_the_weight_cache(cuda):
+    """The learner's live tree is fingerprinted by its update count (training.OptState.version), not its norms."""
+    from exploring_muzero_on_dog_amd import training as T
+    from exploring_muzero_on_dog_amd import learner as LR
+    CK, GA, GS, M, N, ST = _m()
+    C = dm.num_channels(2)
+    opt = T.Optimizer(LR.Learner, 2, 0.005, 10, (), graph=False).init(N.init_muzero_params(3, C))
+    f0 = N.params_fingerprint(opt.tree)
+    assert f0 == (("version", 0),)
+    net0 = N.as_device_net(opt.tree, C)
+    assert N.as_device_net(opt.tree, C) is net0
+    opt.version += 1                           # what train_step does after every learner step
+    assert N.params_fingerprint(opt.tree) != f0
+    assert N.as_device_net(opt.tree, C) is net0   # re-packed into the same live DeviceNet

@@ -12,7 +12,7 @@ import torch
 from oracle import detmadn as dm
 from oracle import mctx_gumbel as G
 from oracle import nets as ON
-from tests._parity import search_parity
+from tests._parity import DQ, log, search_parity
 from tests.test_gpu_nets import random_obs
 
 pytestmark = pytest.mark.gpu
@@ -75,11 +75,21 @@ def test_search_end_to_end_vs_numpy_networks(cuda):
     a, w, orv, _ = G.gumbel_muzero_policy(params, lg, v, e, ON.recurrent_inference, 50, ~valid, gum, max_depth=25,
                                           trace=trace)
     torch.cuda.synchronize()
-    # the NumPy networks sum in another order (|d logits|, |d values| ~3e-6 = ~6 DQ, tests/test_gpu_nets.py):
-    # decisions count as near-ties within 50x the tree-arithmetic bound, weights get 10x its gain term; the
-    # root value and the weights' base tolerance are the north star's 1e-5 (measured: max|dv| 1.2e-7)
+    # The NumPy networks sum in another order, so every value / reward / discount entering the two trees differs
+    # by up to eps (measured here on the root batch and one recurrent step of it, ~1e-6..3e-6); those differences
+    # reach the weights through the same Q-rescale gain as the tree arithmetic's ulps.  The allowance is scaled
+    # by the MEASURED eps / DQ (logged) instead of a fixed factor; the root value keeps the literal 1e-5.
+    glg, gv, ge = N.root_inference_fn(net, torch.from_numpy(obs).cuda())
+    acts = np.asarray(a, np.int32)
+    gr, gd, _, grv_, _ = N.recurrent_inference_fn(net, torch.from_numpy(acts).cuda(), ge)
+    r_, d_, _, v_, _ = ON.recurrent_inference(params, acts, e)
+    eps = max(np.abs(gv.cpu().numpy() - v).max(), np.abs(gr.cpu().numpy() - r_).max(),
+              np.abs(gd.cpu().numpy() - d_).max(), np.abs(grv_.cpu().numpy() - v_).max())
+    factor = max(1.0, float(eps) / DQ)
+    log(f"search end-to-end (NumPy nets): measured network deviation eps {eps:.2e} -> allowance factor "
+        f"eps / DQ = {factor:.2f} on the gain term and the near-tie bound")
     search_parity("search end-to-end (NumPy nets)", pol.action.cpu().numpy(), pol.action_weights.cpu().numpy(),
-                  rv.cpu().numpy(), a, w, orv, trace["margin"], 10 * trace["gain"], tie=50.0)
+                  rv.cpu().numpy(), a, w, orv, trace["margin"] / factor, factor * trace["gain"])
 
 
 def test_device_noise_is_deterministic_and_valid(cuda):
