@@ -731,6 +731,18 @@ def env_bytes_per_step(P):
     return 2 * state + 2 * 4 + 2 + (8 * P + 2) * 56
 
 
+def measured_env_traffic(B, kernel):
+    """HBM bytes per env-round launch from the newest committed PMC summary of this batch
+    (profiles/r*_env_pmc_<B>.json, profiles/summarize_env_pmc.py: FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE).
+    Returns (bytes, source) or (None, None)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_env_pmc_{B}.json")), reverse=True):
+        t = json.load(open(f))
+        if t.get("kernel", kernel) == kernel and "hbm_bytes_per_launch" in t:
+            return t["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def run_env(args):
     """SURVEY §8(d)(b'): the env kernels alone -- step + legal + encode of det-MADN 2p over the batch -- as the
     fused random-play round (muz_detmadn_random_round), on a mid-game state distribution (ENV_PREROLL rounds
@@ -789,6 +801,10 @@ def run_env(args):
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "avg_launch_ms": round(avg_ms, 5),
                      "bytes_per_env_step": per, "bytes_per_launch": B * per, "traffic": None},
     }
+    traffic, src = measured_env_traffic(B, kernel)
+    if traffic:
+        out["roofline"].update(traffic=round(traffic), traffic_unit="bytes/launch (HBM, PMC)", traffic_source=src,
+                               traffic_over_algorithmic=round(traffic / (B * per), 3))
     if world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_selfplay as CS
         cores, aff = cpu_cores()

@@ -391,6 +391,255 @@ __device__ int dog_env_step(const DetConsts& c, DogG& s, int action, int& reward
   return (nxt == -1 && !done) ? 1 : 0;
 }
 
+// ---- play-phase env_step on one whole wave (k_dog_play) -------------------------------------------------------
+// The same transition as dog_env_step(.., legal = true), with the game's state spread over the 64 lanes instead of
+// re-read from LDS by one lane: lane i < 56 holds board[i], lane j < 16 pins[j], lane 16p + k (k < 14) hands[p][k].
+// The scalar logic runs redundantly on every lane with wave-uniform values, so a board / pin lookup is a readlane
+// (a few cycles) instead of a dependent LDS round trip; the board rebuild, the occupancy tests of the winner check
+// and the hand sums of the next-player search are per-lane work plus a ballot or a 16-lane row sum.  Round 3 measured
+// lane 0's LDS-bound env_step at 30 % of a DOG turn (profiles/r3_dog_stamps.log).
+struct DogWave {
+  int lane;
+  int cell;   // board[lane] (lane < kCells)
+  int pin;    // pins[lane] (lane < 16)
+  int hand;   // hands[lane >> 4][lane & 15] (lane & 15 < kDogCards; 0 otherwise)
+  __device__ __forceinline__ int board(int x) const { return __builtin_amdgcn_readlane(cell, x); }
+  __device__ __forceinline__ void set_board(int x, int v) { cell = lane == x ? v : cell; }
+  __device__ __forceinline__ int pins(int j) const { return __builtin_amdgcn_readlane(pin, j); }
+  __device__ __forceinline__ void set_pin(int j, int v) { pin = lane == j ? v : pin; }
+  // goal cells of every player as 56-bit masks (kernel constants)
+  __device__ __forceinline__ static unsigned long long goal_mask(const DetConsts& c, int p) {
+    unsigned long long m = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) m |= 1ull << dgoal(c, p, g);
+    return m;
+  }
+  __device__ __forceinline__ unsigned long long occupied() const { return __ballot(lane < kCells && cell >= 0); }
+  __device__ __forceinline__ static bool player_done(const DetConsts& c, unsigned long long occ, int p) {
+    const unsigned long long gm = goal_mask(c, p);
+    return p < c.P && (occ & gm) == gm;
+  }
+  // dog_winners over the occupancy mask
+  __device__ __forceinline__ uint32_t winners(const DetConsts& c) const {
+    const unsigned long long occ = occupied();
+    uint32_t d = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) d |= player_done(c, occ, p) ? (1u << p) : 0u;
+    if (!has(c.flags, R_TEAMS)) return d;
+    const bool t0 = (d & 1u) && (d & 4u), t1 = (d & 2u) && (d & 8u);
+    if ((t0 && t1) || !(t0 || t1)) return 0u;
+    return t0 ? 0x5u : 0xAu;
+  }
+  // set_pins_on_board: every cell cleared, then each pin's owner written in (p, k) order
+  __device__ __forceinline__ void rebuild(const DetConsts& c) {
+    int v = -1;
+    for (int j = 0; j < c.P * 4; ++j) {
+      const int pos = pins(j);
+      v = (pos == lane) ? (j >> 2) : v;   // pos in [0, 56) whenever it matches a board lane
+    }
+    cell = v;
+  }
+  __device__ __forceinline__ bool goal_free(const DetConsts& c, int cp, int lo, int hi) const {
+    bool ok = true;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (lo < g && g < hi) ok &= board(dgoal(c, cp, g)) != cp;
+    return ok;
+  }
+};
+
+__device__ __forceinline__ void wv_finish(const DetConsts& c, const DogWave& W, int sdone, int cp, int& reward,
+                                          int& done) {
+  const uint32_t w = W.winners(c);
+  done = (sdone || w) ? 1 : 0;
+  reward = sdone ? 0 : (int)((w >> cp) & 1u);
+}
+
+__device__ __forceinline__ void wv_capture_move(const DetConsts& c, DogWave& W, int sdone, int cp, int pin, int npos,
+                                                int& reward, int& done) {
+  const int at = W.board(jidx(npos, kCells));
+  if (at != -1 && (at != cp || has(c.flags, R_FRIENDLY)))
+    for (int k = 0; k < 4; ++k)
+      if (W.pins(at * 4 + k) == npos) W.set_pin(at * 4 + k, -1);
+  const int cur = W.pins(cp * 4 + pin);
+  W.set_pin(cp * 4 + pin, npos);
+  if (npos >= 0 && npos < kCells) {
+    if (cur >= 0 && cur < kCells) W.set_board(cur, -1);
+    W.set_board(npos, cp);
+  } else {
+    W.rebuild(c);
+  }
+  wv_finish(c, W, sdone, cp, reward, done);
+}
+
+__device__ __forceinline__ void wv_step_normal(const DetConsts& c, DogWave& W, int sdone, int cp, int pin, int move,
+                                               int& reward, int& done) {
+  const uint32_t F = c.flags;
+  const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
+  const int tgt = dcst(c.target, cp);
+  const int g0 = dgoal(c, cp, 0);
+  const int cur = W.pins(cp * 4 + pin);
+  const int moved = cur + move;
+  const int fitted = fmodp(moved, kTrack);
+  const int x = moved - tgt - mt;
+  const bool ing = in_goal_p(c, cp, cur);
+  const bool a = ing ? W.goal_free(c, cp, cur - g0, moved - g0 + 1) : W.goal_free(c, cp, -1, x);
+  const int gx = dgoal(c, cp, jidx(x - 1, 4));
+  const bool A = (W.board(gx) != cp) && (has(F, R_JUMP_GOAL) || a);
+  int npos;
+  if (cur == -1)
+    npos = dcst(c.start, cp);
+  else if (ing)
+    npos = moved;
+  else if (4 >= x && x > 0 && A && cur <= tgt)
+    npos = gx;
+  else
+    npos = fitted;
+  wv_capture_move(c, W, sdone, cp, pin, npos, reward, done);
+}
+
+__device__ __forceinline__ void wv_step_swap(const DetConsts& c, DogWave& W, int sdone, int cp, int pin, int pos,
+                                             int& reward, int& done) {
+  const int sp = W.board(pos);
+  const int pp = W.pins(cp * 4 + pin);
+  W.set_board(pos, cp);
+  W.set_board(pp, sp);
+  W.set_pin(cp * 4 + pin, pos);
+  for (int k = 0; k < 4; ++k)
+    if (W.pins(sp * 4 + k) == pos) W.set_pin(sp * 4 + k, pp);
+  wv_finish(c, W, sdone, cp, reward, done);
+}
+
+__device__ __forceinline__ void wv_step_hot7(const DetConsts& c, DogWave& W, int sdone, int cp, const int (&d)[4],
+                                             int& reward, int& done) {
+  const uint32_t F = c.flags;
+  const int mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
+  const int tgt = dcst(c.target, cp);
+  int cur[4], moved[4], npos[4];
+  bool ing[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    cur[k] = W.pins(cp * 4 + k);
+    moved[k] = cur[k] + d[k];
+    ing[k] = in_goal_p(c, cp, cur[k]);
+  }
+  bool occ[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bool o = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o |= (ing[k] ? moved[k] : cur[k]) == dgoal(c, cp, g);
+    occ[g] = o;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int x = moved[k] - tgt - mt;
+    bool a = true;
+    if (!ing[k])
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (-1 < g && g < x) a &= !occ[g];
+    const bool A = has(F, R_JUMP_GOAL) || a;
+    if (cur[k] == -1)
+      npos[k] = -1;
+    else if (ing[k])
+      npos[k] = moved[k];
+    else if (4 >= x && x > 0 && A && cur[k] <= tgt)
+      npos[k] = dgoal(c, cp, jidx(x - 1, 4));
+    else
+      npos[k] = fmodp(moved[k], kTrack);
+  }
+  unsigned long long row[4];
+  bool cross = false;
+  const int g0 = dgoal(c, cp, 0);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool A0 = in_goal_p(c, cp, cur[k]), B0 = in_goal_p(c, cp, npos[k]);
+    cross |= A0 != B0;
+    row[k] = (A0 == B0) ? path_bits(cur[k], npos[k], kTrack, true)
+                        : (path_bits(cur[k], tgt, kTrack, false) | path_bits(g0, npos[k], kCells, false));
+  }
+  if (cross)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) row[k] |= 1ull << dcst(c.start, cp);
+  const unsigned long long anyp = row[0] | row[1] | row[2] | row[3];
+  // pins hit: lane j tests its own pin (one ballot instead of 16 lookups)
+  const bool hj = W.lane < c.P * 4 && ((anyp >> jidx(W.pin, kCells)) & 1ull);
+  uint32_t hit = (uint32_t)__ballot(hj);
+  hit &= ~(0xFu << (4 * cp));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    unsigned long long other = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j != k) other |= row[j];
+    const bool h = ((other >> jidx(cur[k], kCells)) & 1ull) && ((other >> jidx(npos[k], kCells)) & 1ull);
+    hit |= (uint32_t)h << (4 * cp + k);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) W.set_pin(cp * 4 + k, npos[k]);
+  if (W.lane < 16 && ((hit >> W.lane) & 1u)) W.pin = -1;
+  W.rebuild(c);
+  wv_finish(c, W, sdone, cp, reward, done);
+}
+
+// play-phase env_step for an action drawn from the legal mask, all 64 lanes of one wave (lane = tid); returns 1 when
+// a deal must follow (wave-uniform) and writes the state back to LDS
+__device__ int dog_env_step_play_wave(const DetConsts& c, DogG& s, int action, int lane, int& reward, int& done) {
+  DogWave W;
+  W.lane = lane;
+  W.cell = lane < kCells ? s.board[lane] : -1;
+  W.pin = lane < 16 ? s.pins[lane] : -1;
+  const int hp = lane >> 4, hk = lane & 15;
+  W.hand = hk < kDogCards ? s.hands[hp][hk] : 0;
+  const int scp = s.cp, sdone = s.done;
+  const int cp = (has(c.flags, R_TEAMS) && DogWave::player_done(c, W.occupied(), scp)) ? (scp + 2) % 4 : scp;
+  const bool joker = action < kDogBase;
+  const int act = ((action % kDogBase) + kDogBase) % kDogBase;
+  const int card = joker ? 0 : dog_base_card(act);
+  if (__builtin_amdgcn_readlane(W.hand, cp * 16 + card) <= 0) {
+    reward = -1;
+    done = sdone;
+  } else if (act < kDogSwaps) {
+    wv_step_swap(c, W, sdone, cp, act / kCells, act % kCells, reward, done);
+  } else if (act < kDogNormalBase) {
+    int d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = c_dists7[act - kDogSwaps][k];
+    wv_step_hot7(c, W, sdone, cp, d, reward, done);
+  } else if (act < kDogNegBase) {
+    const int na = act - kDogNormalBase;
+    int mv = na % 12 + 1;
+    mv += mv >= 7 ? 1 : 0;
+    wv_step_normal(c, W, sdone, cp, na / 12, mv, reward, done);
+  } else {
+    wv_capture_move(c, W, sdone, cp, act - kDogNegBase, fmodp(W.pins(cp * 4 + act - kDogNegBase) - 4, kTrack), reward,
+                    done);
+  }
+  if (reward != -1 && lane == cp * 16 + card) W.hand -= 1;
+  // next player holding cards after the unsubstituted current player: per-player hand sums as 16-lane row sums
+  int h = W.hand;
+  h += __builtin_amdgcn_update_dpp(0, h, 0xB1, 0xF, 0xF, false);    // quad_perm xor 1
+  h += __builtin_amdgcn_update_dpp(0, h, 0x4E, 0xF, 0xF, false);    // quad_perm xor 2
+  h += __builtin_amdgcn_update_dpp(0, h, 0x141, 0xF, 0xF, false);   // row_half_mirror
+  h += __builtin_amdgcn_update_dpp(0, h, 0x140, 0xF, 0xF, false);   // row_mirror
+  int nxt = -1;
+  for (int i = 0; i < c.P; ++i) {
+    const int cand = (scp + i + 1) % c.P;
+    if (nxt == -1 && __builtin_amdgcn_readlane(h, cand * 16) > 0) nxt = cand;
+  }
+  // write back
+  if (lane < kCells) s.board[lane] = (int8_t)W.cell;
+  if (lane < 16) s.pins[lane] = (int8_t)W.pin;
+  if (hk < kDogCards) s.hands[hp][hk] = (int8_t)W.hand;
+  if (lane == 0) {
+    s.cp = done ? cp : nxt;
+    s.reward = reward;
+    s.done = done;
+  }
+  return (nxt == -1 && !done) ? 1 : 0;
+}
+
 // no_step (dog.py:713-752) on lane 0; returns 1 when a deal must follow.
 __device__ int dog_no_step(const DetConsts& c, DogG& s) {
   for (int k = 0; k < kDogCards; ++k) s.hands[s.cp][k] = 0;
@@ -652,6 +901,9 @@ __device__ unsigned long long g_dog_stamps[8];
 #ifndef MUZ_DOG_PRIO
 #define MUZ_DOG_PRIO 1
 #endif
+#ifndef MUZ_DOG_WAVE_STEP
+#define MUZ_DOG_WAVE_STEP 1   // the play-phase env_step on wave 0's 64 lanes (dog_env_step_play_wave)
+#endif
 
 struct DogPlayArgs {
   DetConsts c;
@@ -713,11 +965,18 @@ __global__ __launch_bounds__(kDogPlayThreads) __attribute__((amdgpu_waves_per_eu
       int nleg = 0;
       a = dog_pick(s, random_action_uniform(P.seed, g, P.turn0 + t), tid, &nleg);
       DOG_STAMP(2);   // action choice
-      if (tid == 0) {
-        const int mover = s.cp;
+      const int mover = s.cp;
+      int need = 0;
+      if (MUZ_DOG_WAVE_STEP && a >= 0 && s.phase == 0) {   // wave-uniform: the play phase on all 64 lanes
+        int d = 0;
+        need = dog_env_step_play_wave(c, s, a, tid, r, d);
+      } else if (tid == 0) {                              // no_step and the swap phase: lane 0
         int d = s.done;
         r = 0;
-        s.need_deal = a < 0 ? dog_no_step(c, s) : dog_env_step(c, s, a, r, d, true);
+        need = a < 0 ? dog_no_step(c, s) : dog_env_step(c, s, a, r, d, true);
+      }
+      if (tid == 0) {
+        s.need_deal = need;
         if (P.rec.act) {   // the turn's record row (game lane g, row idx[g] + turns recorded this launch)
           const int row = P.rec.idx[g] + played;
           if (row < P.rec.max_steps) {
