@@ -41,21 +41,39 @@ __device__ __forceinline__ void ln_positions(const float* pre, float* out, int o
   }
 }
 
+// Conv_1 / Conv_2 as implicit GEMMs [64 positions (56 + pad)][K] x [K][64]: wave w owns output channels 16 w .. + 15
+// for ALL four 16-position row tiles (the weights packed as 4 groups of one 16-column tile), so each wave streams a
+// quarter of the kernel from L2 once per game.  (Round 3 split the rows instead: every wave streamed the whole
+// [K][64] kernel for its 16 positions, 4x the L2 weight reads -- 328 KB per game for Conv_2.)
 template <int KB>
 __device__ __forceinline__ void conv_mfma(const AS4 muz_dense& L, const float* in, int cin, float* pre) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(L.w)) + (size_t)wv * KB * 64 + lane;
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mfma_rows16<4>(L.w, KB, in + (wv * 16) * cin, cin, acc);
-  // out^T layout (see dense16): lane (r, g) holds columns t*16 + 4g .. +3 of position wv*16 + r
-  const int r = lane & 15, g = lane >> 4;
-  const AS1 f32x4* bias4 = gp(reinterpret_cast<const f32x4*>(L.b));
+  // weights of k-blocks kb + 1, kb + 2 in flight while kb is multiplied
+  f32x4 w0 = wp[0], w1 = KB > 1 ? wp[64] : w0, w2;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int col = t * 16 + 4 * g;
-    *reinterpret_cast<f32x4*>(pre + (wv * 16 + r) * kPreLd + col) = acc[t] + bias4[col >> 2];
+  for (int kb = 0; kb < KB; ++kb) {
+    if (kb + 2 < KB) w2 = wp[(kb + 2) * 64];
+    f32x4 a[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const f32x4*>(in + (t * 16 + r) * cin + kb * 16 + 4 * g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = mfma4(w0[j], a[t][j], acc[t]);
+    w0 = w1;
+    w1 = w2;
   }
+  // out^T layout: lane (r, g) holds channels 16 wv + 4 g .. + 3 of position t * 16 + r
+  const AS1 f32x4* bias4 = gp(reinterpret_cast<const f32x4*>(L.b));
+  const f32x4 bb = bias4[(16 * wv + 4 * g) >> 2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    *reinterpret_cast<f32x4*>(pre + (t * 16 + r) * kPreLd + 16 * wv + 4 * g) = acc[t] + bb;
 }
 
 __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float* __restrict__ obs, int C, int n,

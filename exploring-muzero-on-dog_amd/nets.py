@@ -145,9 +145,10 @@ class _Packer:
         P, put, r = self.params, self._put, "representation"
         return dict(
             conv0=(put(P[f"{r}/Conv_0/kernel"]), put(P[f"{r}/Conv_0/bias"])), ln0=self._ln(f"{r}/LayerNorm_0"),
-            conv1=(put(pack_dense(P[f"{r}/Conv_1/kernel"].reshape(96, 64), 1, 4)), put(P[f"{r}/Conv_1/bias"])),
+            # the conv kernels as 4 column groups of one 16-channel tile each (k_repr_conv: one group per wave)
+            conv1=(put(pack_dense(P[f"{r}/Conv_1/kernel"].reshape(96, 64), 4, 1)), put(P[f"{r}/Conv_1/bias"])),
             ln1=self._ln(f"{r}/LayerNorm_1"),
-            conv2=(put(pack_dense(P[f"{r}/Conv_2/kernel"].reshape(320, 64), 1, 4)), put(P[f"{r}/Conv_2/bias"])),
+            conv2=(put(pack_dense(P[f"{r}/Conv_2/kernel"].reshape(320, 64), 4, 1)), put(P[f"{r}/Conv_2/bias"])),
             ln2=self._ln(f"{r}/LayerNorm_2"), d0=self._dense(f"{r}/Dense_0"), ln3=self._ln(f"{r}/LayerNorm_3"),
             d1=self._dense(f"{r}/Dense_1"), ln4=self._ln(f"{r}/LayerNorm_4"), d2=self._dense(f"{r}/Dense_2"),
             ln5=self._ln(f"{r}/LayerNorm_5"), d3=self._dense(f"{r}/Dense_3"), ln6=self._ln(f"{r}/LayerNorm_6"),

@@ -278,9 +278,9 @@ typedef struct muz_resblock { muz_dense d0; muz_ln ln0; muz_dense d1; muz_ln ln1
 typedef struct muz_repr_w {
   muz_dense conv0;              /* plain [3][6][32] */
   muz_ln ln0;
-  muz_dense conv1;              /* packed, 1 group, K=96  N=64 */
+  muz_dense conv1;              /* packed, 4 groups x 1 tile, K=96  N=64 */
   muz_ln ln1;
-  muz_dense conv2;              /* packed, 1 group, K=320 N=64 */
+  muz_dense conv2;              /* packed, 4 groups x 1 tile, K=320 N=64 */
   muz_ln ln2;
   muz_dense d0;                 /* packed 3584 -> 256 */
   muz_ln ln3;

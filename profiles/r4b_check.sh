@@ -27,3 +27,9 @@ for rep in 1 2 3; do
     timeout -k 10 120 python3 profiles/search_microbench.py 4096 50 2>/dev/null | tee -a $O/ab.log || exit 1
   done
 done
+unset MUZ_LIB
+MUZ_LIB=$V/libmuz_tl.so timeout -k 10 120 python3 profiles/diag_timeline.py 4096 > $O/timeline.log 2>&1 || { tail -20 $O/timeline.log; exit 1; }
+cp gpurun_out/timeline.npy $O/timeline.npy
+MUZ_LIB=$V/libmuz_tllol.so timeout -k 10 120 python3 profiles/diag_timeline.py 4096 > $O/timeline_lol.log 2>&1 || { tail -20 $O/timeline_lol.log; exit 1; }
+cp gpurun_out/timeline.npy $O/timeline_lol.npy
+grep -A9 "mean over SIMDs" $O/timeline.log $O/timeline_lol.log
