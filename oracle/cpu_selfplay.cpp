@@ -322,24 +322,45 @@ struct Tree {
 };
 
 
+// The tree arithmetic rounds exactly like the NumPy restatement (oracle/mctx_gumbel.py) and the device search
+// (csrc/search.hip): each product rounded on its own (rnd() keeps the compiler from fusing it into an fma), sums over
+// the 24 actions in numpy's pairwise order, exp correctly rounded (float64, then rounded once).
+inline float rnd(float x) {
+  asm volatile("" : "+x"(x));
+  return x;
+}
+inline float sum24(const float* v) {   // numpy's pairwise sum of a contiguous row of 24
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = rnd(rnd(v[j] + v[j + 8]) + v[j + 16]);
+  return rnd(rnd(rnd(r[0] + r[1]) + rnd(r[2] + r[3])) + rnd(rnd(r[4] + r[5]) + rnd(r[6] + r[7])));
+}
+inline float exp_cr(float x) { return (float)std::exp((double)x); }
+void softmax_tree(const float* x, float* out) {
+  float m = -kInf, u[kA];
+  for (int i = 0; i < kA; ++i) m = std::max(m, x[i]);
+  for (int i = 0; i < kA; ++i) u[i] = exp_cr(x[i] - m);
+  const float s = sum24(u);
+  for (int i = 0; i < kA; ++i) out[i] = u[i] / s;
+}
+
 // qtransform_completed_by_mix_value(value_scale 0.5, maxvisit_init 50, rescale, mixed value, eps 1e-8)
 void completed_q(const Tree& t, int node, float* cq) {
+  static_assert(kA == 24, "sum24: 24 actions");
   const int* vis = &t.c_visits[(size_t)node * kA];
-  float q[kA], pp[kA];
-  softmax(&t.c_prior[(size_t)node * kA], pp, kA);
+  float q[kA], pp[kA], tmp[kA];
+  softmax_tree(&t.c_prior[(size_t)node * kA], pp);
   int sumv = 0, maxv = 0;
-  float sp = 0.f;
   for (int a = 0; a < kA; ++a) {
-    q[a] = t.c_reward[(size_t)node * kA + a] + t.c_disc[(size_t)node * kA + a] * t.c_value[(size_t)node * kA + a];
+    q[a] = rnd(t.c_reward[(size_t)node * kA + a] + rnd(t.c_disc[(size_t)node * kA + a] * t.c_value[(size_t)node * kA + a]));
     pp[a] = std::max(kTiny, pp[a]);
     sumv += vis[a];
     maxv = std::max(maxv, vis[a]);
-    if (vis[a] > 0) sp += pp[a];
+    tmp[a] = vis[a] > 0 ? pp[a] : 0.f;
   }
-  float wq = 0.f;
-  for (int a = 0; a < kA; ++a)
-    if (vis[a] > 0) wq += pp[a] * q[a] / sp;
-  const float mixed = (t.raw[node] + (float)sumv * wq) / (float)(sumv + 1);
+  const float sp = sum24(tmp);
+  for (int a = 0; a < kA; ++a) tmp[a] = vis[a] > 0 ? rnd(rnd(pp[a] * q[a]) / sp) : 0.f;
+  const float wq = sum24(tmp);
+  const float mixed = rnd(t.raw[node] + rnd((float)sumv * wq)) / (float)(sumv + 1);
   float lo = kInf, hi = -kInf;
   for (int a = 0; a < kA; ++a) {
     cq[a] = vis[a] > 0 ? q[a] : mixed;
@@ -383,7 +404,7 @@ int select_child(const Tree& t, int node, int depth, const bool* invalid, const 
   } else {
     float z[kA], p[kA];
     for (int a = 0; a < kA; ++a) z[a] = prior[a] + cq[a];
-    softmax(z, p, kA);
+    softmax_tree(z, p);
     for (int a = 0; a < kA; ++a) sc[a] = p[a] - (float)vis[a] / (float)(1 + sumv);
   }
   return argmax(sc, kA);
@@ -443,8 +464,8 @@ void gumbel_search(const Net& net, const Search& sr, int B, const float* logits,
         const int pr = t.parent[idx], pa = t.afp[idx];
         const int cnt = t.visits[pr];
         const size_t e = (size_t)pr * kA + pa;
-        leaf = t.c_reward[e] + t.c_disc[e] * leaf;
-        t.value[pr] = (t.value[pr] * (float)cnt + leaf) / ((float)cnt + 1.0f);
+        leaf = rnd(t.c_reward[e] + rnd(t.c_disc[e] * leaf));
+        t.value[pr] = rnd(rnd(t.value[pr] * (float)cnt) + leaf) / ((float)cnt + 1.0f);
         t.visits[pr] = cnt + 1;
         t.c_value[e] = t.value[idx];
         t.c_visits[e] += 1;
@@ -472,7 +493,7 @@ void gumbel_search(const Net& net, const Search& sr, int B, const float* logits,
     float zm = -kInf;
     for (int a = 0; a < kA; ++a) zm = std::max(zm, z[a]);
     for (int a = 0; a < kA; ++a) z[a] = inv[a] ? kFMin : z[a] - zm;
-    softmax(z, weights_out + (size_t)b * kA, kA);
+    softmax_tree(z, weights_out + (size_t)b * kA);
     value_out[b] = t.value[0];
   }
 }
