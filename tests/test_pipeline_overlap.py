@@ -130,3 +130,35 @@ def test_overlap_one_process_threads():
                          deliver=lambda g, games: ring.extend(games), publish=publish, concurrent=True)
     assert n == ITERS + 1 and overlap["n"] == ITERS
     _check_ring(ring, 1)
+
+
+def test_weight_update_wait_applies_and_orders():
+    """transfer._WeightUpdate.wait: completes the broadcast, rebuilds the receiver's derived
+    tables once, and is idempotent; the sender does not rebuild.  (On the GPU it also synchronises the current
+    stream, so self-play / learner streams cannot race the arena; a CPU buffer skips that.)"""
+    import muzpkg
+    muzpkg.load()
+    from exploring_muzero_on_dog_amd import transfer as TR
+
+    class Work:
+        def __init__(self):
+            self.waited = 0
+
+        def wait(self):
+            self.waited += 1
+
+    class Net:
+        def __init__(self):
+            self.buffer = torch.zeros(8)
+            self.prepared = 0
+
+        def prepare(self):
+            self.prepared += 1
+
+    for receiver in (True, False):
+        w, net = Work(), Net()
+        h = TR._WeightUpdate(w, net, receiver)
+        h.wait()
+        h.wait()
+        assert w.waited == 1
+        assert net.prepared == (1 if receiver else 0)
