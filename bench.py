@@ -330,13 +330,14 @@ def dog_cpu_baseline(seconds, lanes=8):
 
 
 # k_dog_play's per-turn critical path, measured with the stamp build (profiles/diag_dog_stamps.py,
-# profiles/r3_dog_stamps.log: 256-thread workgroup, wave priority on): thread 0 of each game's workgroup,
-# shader-clock ticks per game-turn by phase (relative shares; the stamps themselves add ~10 %).
-DOG_PHASES = {"reset check / restart": 408, "base checks + barrier": 6700, "mask words + choice": 1960,
-              "env_step (lane 0)": 4626, "barrier": 98, "deal": 1486}
+# profiles/r4c_dog_stamps_wave.log: 256-thread workgroup, wave priority on, round 4's wave-parallel env_step):
+# thread 0 of each game's workgroup, shader-clock ticks per game-turn by phase (relative shares; the stamps
+# themselves add ~10 %).  Round 3 (lane-0 env_step, profiles/r4c_dog_stamps_lane0.log): 4628 ticks of 15317.
+DOG_PHASES = {"reset check / restart": 447, "base checks + barrier": 7072, "mask words + choice": 1788,
+              "env_step (wave 0)": 3383, "barrier": 120, "deal": 1495}
 # the phases a fully parallel turn keeps: the 448-thread base checks and their barrier, the one-wave action
-# choice, the turn-end barrier and the (already wave-parallel) deal; lane 0's env_step and the reset check are
-# the serial remainder a faster kernel would remove
+# choice, the turn-end barrier and the (already wave-parallel) deal; wave 0's env_step (its lookups and board
+# updates are still one dependent chain) and the reset check are the serial remainder a faster kernel would remove
 DOG_IRREDUCIBLE = ("base checks + barrier", "mask words + choice", "barrier", "deal")
 
 
@@ -358,9 +359,10 @@ def dog_latency_model(avg_ms, games, turns, launch_bytes):
             "phase_share": {k: round(v / tot, 4) for k, v in DOG_PHASES.items()},
             "phase_ticks_per_turn_stamp_build": DOG_PHASES, "games_resident": games, "avg_launch_ms": round(avg_ms, 5),
             "hbm_gbs": round(launch_bytes / (avg_ms * 1e-3) / 1e9, 2), "traffic": None,
-            "note": "per-phase shares from the stamp build (profiles/r3_dog_stamps.log); r3: 4-wave workgroups "
-                    "(no register spills; 6.81 -> 6.17 us/turn) and the turn's serial part at raised wave priority "
-                    "(6.95 -> 6.68 us/turn at 7 waves), profiles/r3_dog_prio_ab.log"}
+            "note": "per-phase shares from the stamp build (profiles/r4c_dog_stamps_wave.log); r4: env_step on all "
+                    "64 lanes of wave 0 (ballot / readlane lookups, 4628 -> 3383 ticks; 6.18 -> 5.80 us/turn, "
+                    "profiles/r4c_dog_bench_*.json); r3: 4-wave workgroups (no register spills; 6.81 -> 6.17 us/turn) "
+                    "and the turn's serial part at raised wave priority, profiles/r3_dog_prio_ab.log"}
 
 
 def run_dog(args):

@@ -130,80 +130,70 @@ __device__ __forceinline__ void det_obs_write(const DetConsts& c, const uint8_t*
   }
 }
 
-// Chunk loop: a launch covers the batch with at most kRoundGrid workgroups (4 per CU: the LDS limit), each taking
-// 256-game chunks in turn, so a workgroup's observation stores (phase 2) drain while it computes its next chunk's
-// phase 1.  With one chunk per workgroup (round 3) the resident workgroups ran the two phases in lock step -- all
-// computing, then all storing -- and the launch took about the sum of the two (2^20 games: 0.135 ms of phase 1 +
-// ~0.2 ms of stores = 0.335 ms, 0.46 of HBM).
-constexpr int kRoundGrid = 1024;
-
 __global__ __launch_bounds__(kRoundBlock) void k_det_round(DetConsts c, muz_detmadn_soa st, uint32_t* legal,
                                                            unsigned long long seed, int turn, int8_t* obs,
                                                            int8_t* reward, uint8_t* done, int n) {
   __shared__ int8_t sboard[kCells * kRoundBlock];
   __shared__ __attribute__((aligned(16))) uint8_t senc[kRoundBlock * kEncStride];
+  const int g = blockIdx.x * kRoundBlock + threadIdx.x;
   const int P = c.P, C = 8 * P + 2;
-  for (int chunk = blockIdx.x; chunk * kRoundBlock < n; chunk += gridDim.x) {
-    const int g = chunk * kRoundBlock + threadIdx.x;
-    if (g < n) {
-      BoardView b{sboard + threadIdx.x, kRoundBlock};
-      DetLane s;
-      det_load(c, st, g, s, b);
-      const uint32_t lb = legal[g];
-      const int cnt = __popc(lb);
-      int r = 0;
-      if (cnt == 0) {
-        det_nostep(c, s);
-      } else {
-        const float u = u24(mix64(game_key(seed ^ kDetRandomStream, g, turn)));
-        int k = (int)(u * (float)cnt);
-        k = k >= cnt ? cnt - 1 : k;
-        uint32_t x = lb;
-        for (int j = 0; j < k; ++j) x &= x - 1;   // drop the k lowest set bits
-        const int a = __ffs(x) - 1;
-        r = det_step_masked(c, s, b, a / 6, a % 6 + 1, lb);   // lb: this state's mask (the round contract)
-      }
-      const int fin = s.done;
-      if (fin) {   // env_reset in place with the batch's rules (deterministic_madn.py:42-120)
-        const bool fp = has(c.flags, R_FREE_PIN);
-        for (int cell = 0; cell < kCells; ++cell) b.set(cell, -1);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) s.pins[j] = (fp && (j & 3) == 0 && (j >> 2) < P) ? c.start[j >> 2] : -1;
-#pragma unroll
-        for (int j = 0; j < 24; ++j) s.aset[j] = j < 6 * P ? 4 : 0;
-        if (fp)
-          for (int p = 0; p < P; ++p) b.set(c.start[p], p);
-        s.cp = c.starting_player;
-        s.done = 0;
-        s.reward = 0;
-      }
-      det_store(c, st, g, s, b, true);
-      legal[g] = det_legal(c, s, b);
-      if (reward) reward[g] = (int8_t)r;
-      if (done) done[g] = (uint8_t)fin;
-      if (obs) {   // stage this game's encode inputs
-        uint8_t* e = senc + threadIdx.x * kEncStride;
-        uint32_t wv = 0;
-        for (int w = 0; w < kCells; ++w) {
-          const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
-          const int v = b.at(src);
-          const uint32_t rel = v < 0 ? kRelEmpty : (uint32_t)mod_small(v - s.cp, P);
-          wv |= rel << (8 * (w & 3));
-          if ((w & 3) == 3) {
-            *reinterpret_cast<uint32_t*>(e + (w & ~3)) = wv;
-            wv = 0;
-          }
-        }
-        auto none = [](int) { return 0; };
-        for (int ch = P + 2; ch < C; ++ch) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
-      }
+  if (g < n) {
+    BoardView b{sboard + threadIdx.x, kRoundBlock};
+    DetLane s;
+    det_load(c, st, g, s, b);
+    const uint32_t lb = legal[g];
+    const int cnt = __popc(lb);
+    int r = 0;
+    if (cnt == 0) {
+      det_nostep(c, s);
+    } else {
+      const float u = u24(mix64(game_key(seed ^ kDetRandomStream, g, turn)));
+      int k = (int)(u * (float)cnt);
+      k = k >= cnt ? cnt - 1 : k;
+      uint32_t x = lb;
+      for (int j = 0; j < k; ++j) x &= x - 1;   // drop the k lowest set bits
+      const int a = __ffs(x) - 1;
+      r = det_step_masked(c, s, b, a / 6, a % 6 + 1, lb);   // lb: this state's mask (the round contract)
     }
-    if (!obs) continue;
-    __syncthreads();
-    const int g0 = chunk * kRoundBlock;
-    det_obs_write(c, senc, min(kRoundBlock, n - g0), obs + (size_t)g0 * C * kCells, threadIdx.x, kRoundBlock);
-    __syncthreads();   // senc is staged again by the next chunk
+    const int fin = s.done;
+    if (fin) {   // env_reset in place with the batch's rules (deterministic_madn.py:42-120)
+      const bool fp = has(c.flags, R_FREE_PIN);
+      for (int cell = 0; cell < kCells; ++cell) b.set(cell, -1);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s.pins[j] = (fp && (j & 3) == 0 && (j >> 2) < P) ? c.start[j >> 2] : -1;
+#pragma unroll
+      for (int j = 0; j < 24; ++j) s.aset[j] = j < 6 * P ? 4 : 0;
+      if (fp)
+        for (int p = 0; p < P; ++p) b.set(c.start[p], p);
+      s.cp = c.starting_player;
+      s.done = 0;
+      s.reward = 0;
+    }
+    det_store(c, st, g, s, b, true);
+    legal[g] = det_legal(c, s, b);
+    if (reward) reward[g] = (int8_t)r;
+    if (done) done[g] = (uint8_t)fin;
+    if (obs) {   // stage this game's encode inputs
+      uint8_t* e = senc + threadIdx.x * kEncStride;
+      uint32_t wv = 0;
+      for (int w = 0; w < kCells; ++w) {
+        const int src = (w < kTrack) ? fmodp(w + kDist * s.cp, kTrack) : kTrack + fmodp((w - kTrack) + 4 * s.cp, 16);
+        const int v = b.at(src);
+        const uint32_t rel = v < 0 ? kRelEmpty : (uint32_t)mod_small(v - s.cp, P);
+        wv |= rel << (8 * (w & 3));
+        if ((w & 3) == 3) {
+          *reinterpret_cast<uint32_t*>(e + (w & ~3)) = wv;
+          wv = 0;
+        }
+      }
+      auto none = [](int) { return 0; };
+      for (int ch = P + 2; ch < C; ++ch) e[kCells + ch] = (uint8_t)det_encode_value(c, s, ch, 0, none);
+    }
   }
+  if (!obs) return;
+  __syncthreads();
+  const int g0 = blockIdx.x * kRoundBlock;
+  det_obs_write(c, senc, min(kRoundBlock, n - g0), obs + (size_t)g0 * C * kCells, threadIdx.x, kRoundBlock);
 }
 
 // The same round with one game per G lanes (G = 4, 8, 16 or 32), for batches too small to fill the GPU one game per
@@ -416,8 +406,7 @@ int launch_det_round(const DetConsts& c, const muz_detmadn_soa& st, uint32_t* le
       k_det_round_g<16><<<nblocks(n, kWideBlock / 16), kWideBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
       break;
     default:
-      k_det_round<<<min(nblocks(n, kRoundBlock), kRoundGrid), kRoundBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward,
-                                                                               done, n);
+      k_det_round<<<nblocks(n, kRoundBlock), kRoundBlock, 0, s>>>(c, st, legal, seed, turn, obs, reward, done, n);
   }
   return muz_last_launch_error();
 }

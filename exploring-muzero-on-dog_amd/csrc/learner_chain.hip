@@ -1,0 +1,601 @@
+// The unrolled dynamics chain of a learner step as ONE launch each way (learner._TrunkChain; reference
+// train_with_reward.py:98-107, train_stochastic.py:95-121; the trunk is DynamicsNetwork4's FiLM trunk,
+// muzero_deterministic_madn.py:391-457).  At batch 128 x 10 applications the per-layer form was ~150 forward and
+// ~90 backward launches of a few microseconds each (library GEMMs at 128 rows, row kernels); here one workgroup
+// carries 16 rows through every application, its activations in LDS, the weights streamed from L2 (all tiles
+// read the same matrices), and writes exactly what the per-layer kernels saved for the backward (so the weight /
+// LayerNorm gradients stay the grouped launches of learner.GradSink).
+//
+// Workgroup = 8 waves, 512 threads.  GEMM: wave w owns output columns 32 w .. + 31 (two 16-column tiles),
+//   v_mfma_f32_16x16x4_f32 with the streamed matrix as the A operand: out[m][c] = sum_k in[m][k] Mt[c][k], Mt = W^T
+//   forward (y = x W) and Mt = W backward (dx = dz W^T), so both directions are the same loop: lane (i, g) reads
+//   Mt[32 w + 16 t + i][16 b + 4 g .. + 3] (one 16-byte load per tile and k-block from the packed copy that
+//   muz_trunk_chain_pack makes per step, 1 KB contiguous per load instruction; 2 k-blocks ahead) and ends with
+//   out[i][32 w + 16 t + 4 g .. + 3].  The next GEMM's first k-blocks are issued before the row phase between
+//   two GEMMs, so their latency hides behind it.
+// Rows: thread (row = tid / 32, sub = tid % 32) owns columns 8 sub .. + 7 of one row; row sums over the 32
+//   lanes of a half-wave.  The row arithmetic is k_ln_fwd / k_ln_bwd / k_minmax_fwd / k_minmax_bwd's
+//   (learner_ln.hip: Flax LayerNorm eps 1e-6 with the fast variance, min-max with the extremum gradient split
+//   evenly over tied columns), compiled without fma contraction like them.
+#include "launch.hpp"
+
+namespace muz {
+namespace chain {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+// k-blocks of weights in flight (+1 being multiplied); measured at batch 128 x 10 applications (fwd / bwd us,
+// profiles/r4g_chain_bench.log): 2: 414 / 435, 3: 407 / 431, 4: 424 / 454, 8: 447 / 485
+#ifndef MUZ_CHAIN_RING
+#define MUZ_CHAIN_RING 3
+#endif
+constexpr int N = 256, R = 16, LD = N + 4, NTH = 512, KB = N / 16, D = MUZ_CHAIN_RING;
+constexpr int kLayers = 6;   // Dense + LayerNorm layers; weight layer 6 = the projection
+
+__device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ int row_isum(int v) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// the lowest column of the row's extremum (k_minmax_fwd's wave_argext over the 32 lanes of a row)
+__device__ __forceinline__ void row_argext(float& v, int& i, bool is_max) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if ((is_max ? ov > v : ov < v) || (ov == v && oi < i)) v = ov, i = oi;
+  }
+}
+
+// The streamed matrix of the next GEMM, packed by muz_trunk_chain_pack so that every load instruction reads 1 KB
+// contiguous (lane l: 16 bytes at l * 16): packed[w][kb][t][lane][j] = Mt[32 w + 16 t + (lane & 15)][16 kb +
+// 4 (lane >> 4) + j].  D slots of two loads (one per 16-column tile); prime() issues k-blocks 0 .. D - 2, gemm()
+// keeps D - 1 blocks ahead.  All slot indices are compile-time.
+struct Ring {
+  f4 w[D][2];
+  const AS1 float* p;
+
+  __device__ __forceinline__ void load(int slot, int blk) {
+    w[slot][0] = *reinterpret_cast<const AS1 f4*>(p + 512 * blk);
+    w[slot][1] = *reinterpret_cast<const AS1 f4*>(p + 512 * blk + 256);
+  }
+  __device__ __forceinline__ void prime(const float* packed) {
+    p = gp(packed) + ((size_t)(threadIdx.x >> 6) * KB * 2 * 64 + (threadIdx.x & 63)) * 4;
+#pragma unroll
+    for (int b = 0; b < D - 1; ++b) load(b, b);
+  }
+};
+
+// muz_trunk_chain_pack: one thread per packed float4 of one matrix and direction
+struct PackTable {
+  const float* src[16];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void k_chain_pack(PackTable tb, float* fwd, float* bwd) {
+  const int q = blockIdx.x * 256 + threadIdx.x;     // float4 index within matrix blockIdx.y
+  const int i = blockIdx.y;
+  const int lane = q & 63, t = (q >> 6) & 1, kb = (q >> 7) & (KB - 1), w = q >> 11;
+  const int r = 32 * w + 16 * t + (lane & 15), c = 16 * kb + 4 * (lane >> 4);
+  const float* W = tb.src[i];
+  f4 vf, vb;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) vf[j] = W[(size_t)(c + j) * N + r];     // Mt = W^T (forward, y = x W)
+  vb = *reinterpret_cast<const f4*>(W + (size_t)r * N + c);           // Mt = W (backward, dx = dz W^T)
+  *reinterpret_cast<f4*>(fwd + (size_t)i * N * N + 4 * q) = vf;
+  *reinterpret_cast<f4*>(bwd + (size_t)i * N * N + 4 * q) = vb;
+}
+
+// out[t] = rows (lane & 15) of in[16][LD] times the primed matrix, columns 32 w + 16 t + 4 (lane >> 4) .. + 3
+__device__ __forceinline__ void gemm(Ring& rg, const float* in, f4 (&out)[2]) {
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  f4 acc[2][2] = {};
+  const float* xp = in + i * LD + 4 * g;
+  f4 x = *reinterpret_cast<const f4*>(xp);
+#pragma unroll
+  for (int b = 0; b < KB; ++b) {
+    if (b + D - 1 < KB) rg.load((b + D - 1) % D, b + D - 1);
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads D - 1 blocks ahead of their MFMAs
+    // the next block's input row is read from LDS while this block's MFMAs run
+    const f4 xn = b + 1 < KB ? *reinterpret_cast<const f4*>(xp + 16 * (b + 1)) : x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[0][j & 1] = mfma(rg.w[b % D][0][j], x[j], acc[0][j & 1]);
+      acc[1][j & 1] = mfma(rg.w[b % D][1][j], x[j], acc[1][j & 1]);
+    }
+    x = xn;
+  }
+  out[0] = acc[0][0] + acc[0][1];
+  out[1] = acc[1][0] + acc[1][1];
+}
+
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  *reinterpret_cast<f4*>(v) = *reinterpret_cast<const f4*>(p);
+  *reinterpret_cast<f4*>(v + 4) = *reinterpret_cast<const f4*>(p + 4);
+}
+__device__ __forceinline__ void ld8g(const float* p, float (&v)[8]) {
+  *reinterpret_cast<f4*>(v) = *reinterpret_cast<const AS1 f4*>(gp(p));
+  *reinterpret_cast<f4*>(v + 4) = *reinterpret_cast<const AS1 f4*>(gp(p + 4));
+}
+__device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<f4*>(p) = *reinterpret_cast<const f4*>(v);
+  *reinterpret_cast<f4*>(p + 4) = *reinterpret_cast<const f4*>(v + 4);
+}
+__device__ __forceinline__ void st8g(float* p, const float (&v)[8]) {
+  *reinterpret_cast<AS1 f4*>(gpw(p)) = *reinterpret_cast<const f4*>(v);
+  *reinterpret_cast<AS1 f4*>(gpw(p + 4)) = *reinterpret_cast<const f4*>(v + 4);
+}
+
+__device__ __forceinline__ float rstd_of(float s, float s2) {
+  const float mean = s / (float)N;
+  return 1.0f / sqrtf(fmaxf(0.f, s2 / (float)N - mean * mean) + 1e-6f);
+}
+
+// ---- forward ---------------------------------------------------------------------------------------------
+// Every row phase's global operands are loaded BEFORE the next matrix is primed: loads retire in order for
+// s_waitcnt vmcnt, so an operand issued behind the prime's 14 loads would wait for all of them.
+struct Ln0Ops {   // LayerNorm_0 + FiLM of one application
+  float ga[8], be[8], sc[8], sh[8];
+};
+
+__device__ __forceinline__ void load_ln0(const AS4 muz_chain_args* a, int i, size_t MN, size_t o, bool live,
+                                         int c0, Ln0Ops& p) {
+  const AS4 muz_chain_group* G = &a->group[a->app[i]];
+  ld8g(G->ln0_gamma + c0, p.ga);
+  ld8g(G->ln0_beta + c0, p.be);
+  if (live) {
+    ld8g(a->scale1 + i * MN + o, p.sc);
+    ld8g(a->shift + i * MN + o, p.sh);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) p.sc[e] = p.sh[e] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
+#pragma clang fp contract(off)
+  const AS4 muz_chain_args* a = kernarg0<muz_chain_args>();
+  __shared__ __attribute__((aligned(16))) float xs[R * LD];    // the current GEMM's input
+  __shared__ __attribute__((aligned(16))) float ys[R * LD];    // its output (+ bias)
+  __shared__ __attribute__((aligned(16))) float rs[R * LD];    // the current ResBlock's input
+  __shared__ __attribute__((aligned(16))) float lat[R * LD];   // x_i
+  const int tid = threadIdx.x, M = a->M, T = a->T;
+  const int row = tid >> 5, c0 = 8 * (tid & 31), m = blockIdx.x * R + row;
+  const bool live = m < M;
+  const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
+  const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
+  {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (live) ld8g(a->latent0 + o, v);
+    st8(lat + row * LD + c0, v);
+  }
+  Ln0Ops n0;
+  load_ln0(a, 0, MN, o, live, c0, n0);
+  Ring rg;
+  rg.prime(a->group[a->app[0]].wf[0]);
+#pragma unroll 1
+  for (int i = 0; i < T; ++i) {
+    const AS4 muz_chain_group* G = &a->group[a->app[i]];
+    const size_t js = (size_t)a->slot[i] * MN + o;     // this row's offset in the group's stacks
+    float* st = a->stats + (size_t)i * 7 * 2 * M;
+    // LayerNorm_0 + FiLM (k_ln_fwd<256, true>)
+    {
+      float v[8];
+      ld8(lat + row * LD + c0, v);
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s += v[e];
+        s2 += v[e] * v[e];
+      }
+      s = row_sum(s);
+      s2 = row_sum(s2);
+      const float mean = s / (float)N, rstd = rstd_of(s, s2);
+      float ln[8], f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ln[e] = (v[e] - mean) * (rstd * n0.ga[e]) + n0.be[e];
+        float p = ln[e] * n0.sc[e];
+        asm volatile("" : "+v"(p));   // a multiply, then an add (torch's addcmul; no fma)
+        f[e] = n0.sh[e] + p;
+      }
+      st8(xs + row * LD + c0, f);
+      if (live) {
+        st8g(a->ln0_out + i * MN + o, ln);
+        st8g(G->X[0] + js, f);
+        if ((tid & 31) == 0) st[m] = mean, st[M + m] = rstd;
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int l = 0; l <= kLayers; ++l) {
+      f4 acc[2];
+      gemm(rg, xs, acc);
+      float ga[8], be[8];
+      f4 bb[2] = {};
+      if (l < kLayers) {
+        ld8g(G->gamma[l] + c0, ga);
+        ld8g(G->beta[l] + c0, be);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) bb[t] = *reinterpret_cast<const AS1 f4*>(gp(G->bias[l] + 32 * w + 16 * t + 4 * lg));
+        rg.prime(G->wf[l + 1]);   // the next GEMM's matrix flies during the row phase
+      } else {
+        ld8g(G->bias[6] + c0, ga);
+        if (i + 1 < T) {
+          load_ln0(a, i + 1, MN, o, live, c0, n0);
+          rg.prime(a->group[a->app[i + 1]].wf[0]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) *reinterpret_cast<f4*>(ys + li * LD + 32 * w + 16 * t + 4 * lg) = acc[t] + bb[t];
+      __syncthreads();
+      if (l < kLayers) {
+        // Dense epilogue (k_ln_fwd): z = y + bias, LayerNorm, ReLU / residual ReLU
+        const bool resid = l == 3 || l == 5;
+        float v[8], res[8];
+        ld8(ys + row * LD + c0, v);
+        if (resid) ld8(rs + row * LD + c0, res);
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s += v[e];
+          s2 += v[e] * v[e];
+        }
+        s = row_sum(s);
+        s2 = row_sum(s2);
+        const float mean = s / (float)N, rstd = rstd_of(s, s2);
+        float out[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = (v[e] - mean) * (rstd * ga[e]) + be[e];
+          out[e] = resid ? fmaxf(res[e] + t, 0.f) : fmaxf(t, 0.f);
+        }
+        st8(xs + row * LD + c0, out);
+        if (l == 1 || l == 3) st8(rs + row * LD + c0, out);   // the next ResBlock's input
+        if (live) {
+          st8g(G->X[l + 1] + js, out);
+          st8g(a->z + ((size_t)i * kLayers + l) * MN + o, v);
+          if ((tid & 31) == 0) st[(2 + 2 * l) * M + m] = mean, st[(3 + 2 * l) * M + m] = rstd;
+        }
+        __syncthreads();
+      } else {
+        // min-max (k_minmax_fwd): q = x + (y + bias), out = (q - lo) / (hi - lo + 1e-8).  No barrier after it:
+        // x_{i+1} is read back by this row's own threads, and xs / ys are free (the last GEMM is done)
+        float x[8], y[8], q[8];
+        ld8(lat + row * LD + c0, x);
+        ld8(ys + row * LD + c0, y);
+        float lo = INFINITY, hi = -INFINITY;
+        int ilo = N, ihi = N;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          q[e] = x[e] + (y[e] + ga[e]);
+          if (q[e] < lo) lo = q[e], ilo = c0 + e;
+          if (q[e] > hi) hi = q[e], ihi = c0 + e;
+        }
+        row_argext(lo, ilo, false);
+        row_argext(hi, ihi, true);
+        const float den = (hi - lo) + 1e-8f;
+        float out[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) out[e] = (q[e] - lo) / den;
+        st8(lat + row * LD + c0, out);
+        if (live) {
+          st8g(a->out + i * MN + o, out);
+          st8g(a->q + i * MN + o, q);
+          if ((tid & 31) == 0) {
+            const size_t r2 = (size_t)i * 2 * M + 2 * m;
+            a->lohi[r2] = lo, a->lohi[r2 + 1] = hi;
+            a->idx[r2] = ilo, a->idx[r2 + 1] = ihi;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---- backward --------------------------------------------------------------------------------------------
+// Column partials of one layer and application (k_dense_ln_bwd's: rows summed in order): [3][N] at p.
+__device__ __forceinline__ void partials(const float* pgs, const float* pbs, const float* dzs, float* p) {
+  const int tid = threadIdx.x;
+  if (tid < N) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      sg += pgs[r * N + tid];
+      sb += pbs[r * N + tid];
+    }
+    p[tid] = sg;
+    p[N + tid] = sb;
+  } else {
+    const int c = tid - N;
+    float sd = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) sd += dzs[r * LD + c];
+    p[2 * N + c] = sd;
+  }
+}
+
+struct MmOps {   // min-max backward of one application; lohi = (min, max) of q
+  float g[8], q[8], h[8], lohi[2];
+};
+struct RowOps {  // a Dense + LayerNorm layer's saved forward values (LayerNorm_0: out = its output)
+  float out[8], z[8], ga[8];
+  float mean, rstd;
+};
+
+__device__ __forceinline__ void load_mm(const AS4 muz_chain_args* a, int i, size_t MN, size_t o, int m, bool live,
+                                        MmOps& p) {
+  if (live) {
+    ld8g(a->g + i * MN + o, p.g);
+    ld8g(a->q + i * MN + o, p.q);
+    if (a->h) ld8g(a->h + i * MN + o, p.h);
+    const size_t r2 = (size_t)i * 2 * a->M + 2 * m;
+    p.lohi[0] = gp(a->lohi)[r2];
+    p.lohi[1] = gp(a->lohi)[r2 + 1];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) p.g[e] = p.q[e] = p.h[e] = 0.f;
+    p.lohi[0] = p.lohi[1] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
+#pragma clang fp contract(off)
+  const AS4 muz_chain_args* a = kernarg0<muz_chain_args>();
+  __shared__ __attribute__((aligned(16))) float dzs[R * LD];     // the current GEMM's input (an output gradient)
+  __shared__ __attribute__((aligned(16))) float dxs[R * LD];     // its output (the next row phase's dout)
+  __shared__ __attribute__((aligned(16))) float dres[R * LD];    // a ResBlock's residual gradient
+  __shared__ __attribute__((aligned(16))) float carry[R * LD];   // dq of application i, then + dz of its LayerNorm_0
+  __shared__ __attribute__((aligned(16))) float pgs[R * N];      // per-row do * xhat, do (column partials)
+  __shared__ __attribute__((aligned(16))) float pbs[R * N];
+  const int tid = threadIdx.x, M = a->M, T = a->T;
+  const int row = tid >> 5, c0 = 8 * (tid & 31), m = blockIdx.x * R + row;
+  const bool live = m < M;
+  const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
+  const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
+  const int tiles = (M + R - 1) / R;
+  MmOps mm;
+  load_mm(a, T - 1, MN, o, m, live, mm);
+  Ring rg;
+  rg.prime(a->group[a->app[T - 1]].wb[6]);
+#pragma unroll 1
+  for (int i = T - 1; i >= 0; --i) {
+    const AS4 muz_chain_group* G = &a->group[a->app[i]];
+    const size_t js = (size_t)a->slot[i] * MN + o;
+    const size_t pj = ((size_t)a->slot[i] * tiles + blockIdx.x) * 3 * N;   // this tile's partial block
+    const float* st = a->stats + (size_t)i * 7 * 2 * M;
+    // min-max backward (k_minmax_bwd): d = (g + carry) x scale + h
+    {
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = mm.g[e];
+      if (i + 1 < T) {
+        float c[8];
+        ld8(carry + row * LD + c0, c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = d[e] + c[e];
+      }
+      if (a->scaled[i]) {
+        const float s = a->grad_scale;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = d[e] * s;
+      }
+      if (a->h) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = d[e] + mm.h[e];
+      }
+      const float lo = mm.lohi[0], hi = mm.lohi[1], den = (hi - lo) + 1e-8f;
+      float sd = 0.f, sq = 0.f;
+      int nlo = 0, nhi = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sd += d[e];
+        sq += d[e] * (mm.q[e] - lo);
+        nlo += mm.q[e] == lo;
+        nhi += mm.q[e] == hi;
+      }
+      sd = row_sum(sd);
+      sq = row_sum(sq) / (den * den);
+      nlo = row_isum(nlo);
+      nhi = row_isum(nhi);
+      const float glo = (-sd / den + sq) / (float)nlo, ghi = (-sq) / (float)nhi;
+      float dq[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float r = d[e] / den;
+        if (mm.q[e] == lo) r = r + glo;
+        if (mm.q[e] == hi) r = r + ghi;
+        dq[e] = live ? r : 0.f;
+      }
+      st8(dzs + row * LD + c0, dq);
+      st8(carry + row * LD + c0, dq);
+      if (live) st8g(G->DZ[6] + js, dq);
+    }
+    __syncthreads();
+    RowOps ro;
+    float sc0[8];   // LayerNorm_0's FiLM scale (loaded with its other operands)
+#pragma unroll 1
+    for (int l = kLayers; l >= 0; --l) {
+      // GEMM: dx = dz W_l^T (+ the residual gradient after a ResBlock's first layer)
+      f4 acc[2];
+      gemm(rg, dzs, acc);
+      // the next row phase's operands, then the next matrix
+      const int k = l - 1;
+      if (l > 0) {
+        ld8g(G->gamma[k] + c0, ro.ga);
+        if (live) {
+          ld8g(G->X[k + 1] + js, ro.out);
+          ld8g(a->z + ((size_t)i * kLayers + k) * MN + o, ro.z);
+          ro.mean = gp(st)[(2 + 2 * k) * M + m], ro.rstd = gp(st)[(3 + 2 * k) * M + m];
+        }
+        rg.prime(G->wb[k]);
+      } else {
+        ld8g(G->ln0_gamma + c0, ro.ga);
+        if (live) {
+          ld8g(a->ln0_out + i * MN + o, ro.out);
+          ld8g((i == 0 ? a->latent0 : a->out + (i - 1) * MN) + o, ro.z);
+          ro.mean = gp(st)[m], ro.rstd = gp(st)[M + m];
+          ld8g(a->scale1 + i * MN + o, sc0);
+        }
+        if (i > 0) {
+          load_mm(a, i - 1, MN, o, m, live, mm);
+          rg.prime(a->group[a->app[i - 1]].wb[6]);
+        }
+      }
+      if (!live) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ro.out[e] = ro.z[e] = 0.f;
+        ro.mean = ro.rstd = 0.f;
+      }
+      const bool add_res = l == 2 || l == 4;
+      const int mr = blockIdx.x * R + li;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int c = 32 * w + 16 * t + 4 * lg;
+        f4 v = acc[t];
+        if (add_res) v += *reinterpret_cast<const f4*>(dres + li * LD + c);
+        *reinterpret_cast<f4*>(dxs + li * LD + c) = v;
+        if (l == 0 && mr < M) *reinterpret_cast<AS1 f4*>(gpw(a->dshift + i * MN + (size_t)mr * N + c)) = v;
+      }
+      // the previous layer's column partials (its rows are complete since the last barrier); the GEMM above read
+      // dzs too, so they share the interval before the barrier
+      if (l < kLayers) partials(pgs, pbs, dzs, G->part[l + 1] + pj);
+      __syncthreads();
+      if (l == 0) break;
+      // LayerNorm / ReLU backward of Dense layer k (k_dense_ln_bwd's row half)
+      const bool resid = k == 3 || k == 5;
+      float d[8];
+      ld8(dxs + row * LD + c0, d);
+      float xh[8], gg[8], sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (!(ro.out[e] > 0.f)) d[e] = 0.f;
+        xh[e] = (ro.z[e] - ro.mean) * ro.rstd;
+        gg[e] = d[e] * ro.ga[e];
+        sa += gg[e];
+        sb += gg[e] * xh[e];
+      }
+      if (resid) st8(dres + row * LD + c0, d);
+      sa = row_sum(sa) / (float)N;
+      sb = row_sum(sb) / (float)N;
+      float dz[8], pg[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dz[e] = ro.rstd * (gg[e] - sa - xh[e] * sb);
+        pg[e] = d[e] * xh[e];
+      }
+      st8(dzs + row * LD + c0, dz);
+      st8(pgs + row * N + c0, pg);
+      st8(pbs + row * N + c0, d);
+      if (live) st8g(G->DZ[k] + js, dz);
+      __syncthreads();
+    }
+    // LayerNorm_0 + FiLM backward (k_ln_bwd<256, true>; ro = its saved values, scale1 below); then
+    // carry = dz_0 + dq, the gradient of x_i
+    {
+      float d[8];
+      ld8(dxs + row * LD + c0, d);
+      float ds[8], xh[8], gg[8], sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ds[e] = d[e] * ro.out[e];
+        d[e] = d[e] * (live ? sc0[e] : 0.f);
+        xh[e] = (ro.z[e] - ro.mean) * ro.rstd;
+        gg[e] = d[e] * ro.ga[e];
+        sa += gg[e];
+        sb += gg[e] * xh[e];
+      }
+      if (live) st8g(a->dscale + i * MN + o, ds);
+      sa = row_sum(sa) / (float)N;
+      sb = row_sum(sb) / (float)N;
+      float dz[8], pg[8], c[8];
+      ld8(carry + row * LD + c0, c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dz[e] = ro.rstd * (gg[e] - sa - xh[e] * sb);
+        pg[e] = d[e] * xh[e];
+        c[e] = dz[e] + c[e];
+      }
+      st8(dzs + row * LD + c0, dz);
+      st8(pgs + row * N + c0, pg);
+      st8(pbs + row * N + c0, d);
+      st8(carry + row * LD + c0, c);
+    }
+    __syncthreads();
+    partials(pgs, pbs, dzs, G->part[0] + pj);
+    __syncthreads();
+  }
+  if (live) {
+    float c[8];
+    ld8(carry + row * LD + c0, c);
+    st8g(a->dlatent0 + o, c);
+  }
+}
+
+static int check_args(const muz_chain_args* a, bool bwd) {
+  MUZ_HOST_CHECK(a && a->T >= 1 && a->T <= MUZ_CHAIN_MAX_T && a->M >= 0 && a->ngroups >= 1 && a->ngroups <= 2);
+  for (int i = 0; i < a->T; ++i) MUZ_HOST_CHECK(a->app[i] >= 0 && a->app[i] < a->ngroups && a->slot[i] >= 0);
+  for (int g = 0; g < a->ngroups; ++g) {
+    const muz_chain_group& G = a->group[g];
+    MUZ_HOST_CHECK(G.ln0_gamma && G.ln0_beta);
+    for (int l = 0; l < 7; ++l) MUZ_HOST_CHECK(G.bias[l] && G.X[l] && (bwd ? G.wb[l] && G.DZ[l] && G.part[l] : G.wf[l] != nullptr));
+    for (int l = 0; l < 6; ++l) MUZ_HOST_CHECK(G.gamma[l] && G.beta[l]);
+  }
+  MUZ_HOST_CHECK(a->latent0 && a->scale1 && a->out && a->q && a->lohi && a->ln0_out && a->z && a->stats);
+  if (bwd) MUZ_HOST_CHECK(a->g && a->dscale && a->dshift && a->dlatent0);
+  else MUZ_HOST_CHECK(a->shift && a->idx);
+  return MUZ_OK;
+}
+
+}  // namespace chain
+}  // namespace muz
+
+using namespace muz;
+
+extern "C" {
+
+int muz_trunk_chain_pack(const float* const* W, int32_t count, float* fwd, float* bwd, void* stream) {
+  MUZ_HOST_CHECK(count >= 0 && (count == 0 || (W && fwd && bwd)));
+  for (int s0 = 0; s0 < count; s0 += 16) {
+    chain::PackTable tb{};
+    tb.count = count - s0 < 16 ? count - s0 : 16;
+    for (int i = 0; i < tb.count; ++i) {
+      MUZ_HOST_CHECK(W[s0 + i] != nullptr);
+      tb.src[i] = W[s0 + i];
+    }
+    const size_t off = (size_t)s0 * chain::N * chain::N;
+    chain::k_chain_pack<<<dim3(chain::N * chain::N / 4 / 256, tb.count), 256, 0, (hipStream_t)stream>>>(tb, fwd + off,
+                                                                                                        bwd + off);
+    const int rc = muz_last_launch_error();
+    if (rc) return rc;
+  }
+  return MUZ_OK;
+}
+
+int muz_trunk_chain_fwd(const muz_chain_args* args, void* stream) {
+  const int rc = chain::check_args(args, false);
+  if (rc) return rc;
+  if (args->M == 0) return MUZ_OK;
+  chain::k_chain_fwd<<<(args->M + chain::R - 1) / chain::R, chain::NTH, 0, (hipStream_t)stream>>>(*args);
+  return muz_last_launch_error();
+}
+
+int muz_trunk_chain_bwd(const muz_chain_args* args, void* stream) {
+  const int rc = chain::check_args(args, true);
+  if (rc) return rc;
+  if (args->M == 0) return MUZ_OK;
+  chain::k_chain_bwd<<<(args->M + chain::R - 1) / chain::R, chain::NTH, 0, (hipStream_t)stream>>>(*args);
+  return muz_last_launch_error();
+}
+
+}  // extern "C"

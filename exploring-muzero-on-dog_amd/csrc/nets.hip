@@ -4,7 +4,6 @@
 
 #include "launch.hpp"
 #include "nn.hpp"
-#include "nn_lol.hpp"
 
 namespace muz {
 
@@ -169,12 +168,7 @@ __global__ __launch_bounds__(kThreads) void k_root_dense(NW Wt, const float* __r
   if (valid)
     for (int c = sub; c < LAT; c += kRowLanes) embedding[(size_t)gr * LAT + c] = a.T[row * LD + c];
   __syncthreads();
-  if constexpr (MUZ_LN_ON_LOAD && std::is_same<NW, muz_net_w>::value) {
-    __shared__ __attribute__((aligned(16))) float s_lol[kLolFloats];
-    pred16_lol<1, false>(W->pred, A, a.T, a, Lol{s_lol}, pf, nullptr, 0, 0);
-  } else {
-    pred16<1, false, false, kSplitkLogits && std::is_same<NW, muz_net_w>::value>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
-  }
+  pred16<1, false, false, kSplitkLogits && std::is_same<NW, muz_net_w>::value>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
   if (valid) {
     for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
     if (sub == 0) value[gr] = a.v0[row];
@@ -198,18 +192,6 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
   const DynIn din = dyn_load(W->dyn, A, valid ? gp(emb) + (size_t)gr * LAT : nullptr, ar);
   Pf pf;
   pf_issue<NT256>(pf, &W->dyn.d3, LAT, LAT);
-#if MUZ_LN_ON_LOAD
-  __shared__ __attribute__((aligned(16))) float s_lol[kLolFloats];
-  const Lol lol{s_lol};
-  dyn16_lol<NT256>(W->dyn, A, din, a, lol, pf, &W->pred.rb[0].d0, LAT, LAT, W->pred.ln0, nullptr);
-  if (valid)
-    for (int c = sub; c < LAT; c += kRowLanes) next_emb[(size_t)gr * LAT + c] = a.L[row * LD + c];
-  pred16_lol<1, true>(W->pred, A, a.T, a, lol, pf, nullptr, 0, 0, &W->dyn, ar);
-  if (valid && sub == 0) {
-    reward[gr] = a.v1[row];
-    discount[gr] = a.v2[row];
-  }
-#else
   dyn16<NT256>(W->dyn, A, din, ar, a, pf, &W->pred.rb[0].d0, LAT, LAT);
   if (valid) {
     for (int c = sub; c < LAT; c += kRowLanes) next_emb[(size_t)gr * LAT + c] = a.T[row * LD + c];
@@ -220,7 +202,6 @@ __global__ __launch_bounds__(kThreads) void k_recurrent(muz_net_w Wt, const int3
   }
   // no barrier: pred16 reads a.T in its first pass and overwrites it only after its first SYNC
   pred16<1, false, false, kSplitkLogits>(W->pred, A, a.T, a, pf, nullptr, 0, 0);
-#endif
   if (valid) {
     for (int c = sub; c < A; c += kRowLanes) prior_logits[(size_t)gr * A + c] = a.U[row * LD + c];
     if (sub == 0) value[gr] = a.v0[row];

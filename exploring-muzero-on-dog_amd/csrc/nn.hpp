@@ -35,10 +35,6 @@ namespace muz {
 #define MUZ_SPLITK_LOGITS 0
 #endif
 constexpr bool kSplitkLogits = MUZ_SPLITK_LOGITS != 0;
-// det networks (search, root, recurrent kernels) with every LayerNorm applied on load (nn_lol.hpp)
-#ifndef MUZ_LN_ON_LOAD
-#define MUZ_LN_ON_LOAD 0
-#endif
 constexpr int kRows = 16;
 constexpr int kWaves = MUZ_TILE_WAVES;
 constexpr int kThreads = kWaves * 64;          // 512 / 1024

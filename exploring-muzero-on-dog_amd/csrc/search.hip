@@ -10,7 +10,6 @@
 // L2/MALL resident), written lazily when a node is created.
 #include "launch.hpp"
 #include "nn.hpp"
-#include "nn_lol.hpp"
 #include "rng.hpp"
 
 namespace muz {
@@ -214,10 +213,6 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
   __shared__ float p_disc[kRows][kMaxDepth];
   __shared__ int s_act[kRows], s_parent[kRows], s_next[kRows], s_depth[kRows];
   __shared__ float s_rootv[kRows];
-#if MUZ_LN_ON_LOAD
-  __shared__ __attribute__((aligned(16))) float s_lol[kLolFloats];
-  const Lol lol{s_lol};
-#endif
 
   if (n_dev) n = *n_dev;
   if ((int)blockIdx.x * kRows >= n) return;
@@ -356,19 +351,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_gumbel_search(
     // the new node's embedding goes to the tree and Pred4's LayerNorm_0 into ar.X straight from Dyn4's
     // min-max pass (registers), so Pred4 starts with its first ResBlock
     const int nx = s_next[row];
-#if MUZ_LN_ON_LOAD
-    dyn16_lol<NT256>(wl->dyn, A, din, ar, lol, pf, &wl->pred.rb[0].d0, LAT, LAT, wl->pred.ln0,
-                     valid ? T.e(g, nx) : nullptr);
-    MUZ_STAMP(3);   // dynamics
-    MUZ_STAMP(4);   // embedding write (fused)
-    pred16_lol<NT256, true>(wl->pred, A, ar.T, ar, lol, pf, &wl->dyn.d3, LAT, LAT, &wl->dyn, dact);
-#else
     dyn16<NT256, true, kLateHeads>(wl->dyn, A, din, dact, ar, pf, &wl->pred.rb[0].d0, LAT, LAT, &wl->pred.ln0,
                                    valid ? T.e(g, nx) : nullptr);
     MUZ_STAMP(3);   // dynamics
     MUZ_STAMP(4);   // embedding write (fused)
     pred16<NT256, true, kLateHeads, kSplitkLogits>(wl->pred, A, ar.T, ar, pf, &wl->dyn.d3, LAT, LAT, &wl->dyn, dact);
-#endif
     MUZ_STAMP(5);   // prediction
     if (valid) {
       const bool fresh = nx == sim + 1;

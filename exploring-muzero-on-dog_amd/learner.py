@@ -537,6 +537,12 @@ class _TrunkChain(torch.autograd.Function):
         X = {(g, n): torch.empty((max(seen[g], 1), B, Nn), dtype=dt, device=dev)
              for g in range(len(seen)) for n in _GEMM_LAYERS}
         lat = latent0.contiguous()
+        ctx.chain = None
+        if _chain_usable(T, B, Nn, len(seen)):
+            ctx.chain = _chain_forward(lat, scale1, shift.contiguous(), apps, slot, scaled, P, X, outs, qs, lohi, idx)
+            ctx.X, ctx.P, ctx.grad_scale, ctx.apps = X, P, float(grad_scale), tuple(apps)
+            ctx.save_for_backward(scale1, qs, lohi)
+            return (outs, outs.clone()) if heads else outs
         f0_next = None    # LayerNorm_0 + FiLM of the next application, formed by the boundary launch
         for i in range(T):
             g, j = apps[i], slot[i]
@@ -585,10 +591,14 @@ class _TrunkChain(torch.autograd.Function):
     @staticmethod
     def backward(ctx, G, H=None):
         scale1, qs, lohi = ctx.saved_tensors
-        P, st, s, apps = ctx.P, ctx.st, ctx.grad_scale, ctx.apps
         T, B, Nn = scale1.shape
         G = G.contiguous()
         H = None if H is None else H.contiguous()
+        if ctx.chain is not None:
+            dlat, dscale, dshift, DZ, scr = _chain_backward(ctx.chain, G, H, ctx.grad_scale, ctx.apps, ctx.P, B, Nn)
+            grads = _trunk_param_grads(ctx.X, DZ, scr, ctx.P, _slots(ctx.apps, len(ctx.P) // _NP)[1], Nn)
+            return (dlat, dscale, dshift, None, None, None, None, *grads)
+        P, st, s, apps = ctx.P, ctx.st, ctx.grad_scale, ctx.apps
         dev, dt = G.device, G.dtype
         lib = _L.load()
         nf = {n: lib.muz_ln_bwd_scratch_floats(B, Nn) if n == "0" else _ln_scratch_floats(B, Nn, Nn)
@@ -635,32 +645,123 @@ class _TrunkChain(torch.autograd.Function):
                 torch.mul(dx0, f0[0], out=dscale[i])
                 dz0, _ = _ln_bwd_rows(dx0 * scale1[i], f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
             ca, cb = dz0, dq
-        grads = [None] * len(P)
-        sink = _sink()
-        for g in range(ngroups):
-            if not seen[g]:
-                grads[_NP * g:_NP * (g + 1)] = [torch.zeros_like(p) for p in P[_NP * g:_NP * (g + 1)]]
-                continue
-            o = _NP * g
-            if sink is not None:       # the same gradients, formed by the sink's grouped launches after backward
-                Q = P[o:o + _NP]
-                sink.ln_colsum(scr[(g, "0")], Nn, Q[0], Q[1])
-                for n, (iw, ib, ig, ibe) in _TRUNK_LAYER_PARAMS:
-                    Xs, Ds = (t[(g, n)][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
-                    sink.wgrad(Xs, Ds, Q[iw])
-                    sink.ln_colsum(scr[(g, n)], Nn, Q[ig], Q[ibe], Q[ib])
-                Xs, Ds = (t[(g, "5")][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
-                sink.wgrad(Xs, Ds, Q[26])
-                sink.colsum(Ds, Q[27])
-                continue
-            grads[o], grads[o + 1], _ = _ln_colsum(scr[(g, "0")], Nn)
-            for n, (iw, ib, ig, ibe) in _TRUNK_LAYER_PARAMS:
-                Xs, Ds = (t[(g, n)][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
-                grads[o + iw] = Xs.t() @ Ds
-                grads[o + ig], grads[o + ibe], grads[o + ib] = _ln_colsum(scr[(g, n)], Nn)
-            Xs, Ds = (t[(g, "5")][:seen[g]].reshape(-1, Nn) for t in (ctx.X, DZ))
-            grads[o + 26], grads[o + 27] = Xs.t() @ Ds, torch.mv(Ds.t(), _ones(Ds.shape[0], Ds))
+        grads = _trunk_param_grads(ctx.X, DZ, scr, P, seen, Nn)
         return (ca + cb, dscale, dshift, None, None, None, None, *grads)
+
+
+def _trunk_param_grads(X, DZ, scr, P, seen, Nn):
+    """The chain's parameter gradients from the stacked layer inputs X, output gradients DZ and LayerNorm
+    column partials scr (keys (group, layer input name)): one weight-gradient GEMM and one column sum per
+    parameter over all of a group's applications -- recorded into the active GradSink, or formed here."""
+    ngroups = len(P) // _NP
+    grads = [None] * len(P)
+    sink = _sink()
+    for g in range(ngroups):
+        if not seen[g]:
+            grads[_NP * g:_NP * (g + 1)] = [torch.zeros_like(p) for p in P[_NP * g:_NP * (g + 1)]]
+            continue
+        o = _NP * g
+        if sink is not None:       # the same gradients, formed by the sink's grouped launches after backward
+            Q = P[o:o + _NP]
+            sink.ln_colsum(scr[(g, "0")], Nn, Q[0], Q[1])
+            for n, (iw, ib, ig, ibe) in _TRUNK_LAYER_PARAMS:
+                Xs, Ds = (t[(g, n)][:seen[g]].reshape(-1, Nn) for t in (X, DZ))
+                sink.wgrad(Xs, Ds, Q[iw])
+                sink.ln_colsum(scr[(g, n)], Nn, Q[ig], Q[ibe], Q[ib])
+            Xs, Ds = (t[(g, "5")][:seen[g]].reshape(-1, Nn) for t in (X, DZ))
+            sink.wgrad(Xs, Ds, Q[26])
+            sink.colsum(Ds, Q[27])
+            continue
+        grads[o], grads[o + 1], _ = _ln_colsum(scr[(g, "0")], Nn)
+        for n, (iw, ib, ig, ibe) in _TRUNK_LAYER_PARAMS:
+            Xs, Ds = (t[(g, n)][:seen[g]].reshape(-1, Nn) for t in (X, DZ))
+            grads[o + iw] = Xs.t() @ Ds
+            grads[o + ig], grads[o + ibe], grads[o + ib] = _ln_colsum(scr[(g, n)], Nn)
+        Xs, Ds = (t[(g, "5")][:seen[g]].reshape(-1, Nn) for t in (X, DZ))
+        grads[o + 26], grads[o + 27] = Xs.t() @ Ds, torch.mv(Ds.t(), _ones(Ds.shape[0], Ds))
+    return grads
+
+
+# csrc/learner_chain.hip: the whole chain as one launch each way (muz_trunk_chain_fwd / _bwd)
+CHAIN_KERNEL = True              # False: the per-layer launch train below (A/B timing; the kernels' test reference)
+_CHAIN_W = (2, 6, 10, 14, 18, 22, 26)          # trunk_param_names index of each weight layer's kernel (bias + 1,
+                                               # LayerNorm scale / bias + 2 / + 3)
+_CHAIN_PARTS = ("0",) + _GEMM_LAYERS[:6]       # the kernels' part[] order: LayerNorm_0, then the 6 Dense + LN layers
+
+
+def _chain_usable(T, B, Nn, ngroups):
+    return CHAIN_KERNEL and Nn == 256 and 1 <= T <= _L.MUZ_CHAIN_MAX_T and 1 <= ngroups <= 2 and B > 0
+
+
+class _Chain:
+    """What _chain_forward hands to _chain_backward: the filled muz_chain_args and the buffers it points at."""
+
+    def __init__(self, args, keep):
+        self.args, self.keep = args, keep
+
+
+def _chain_forward(lat, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi, idx):
+    """muz_trunk_chain_fwd over all applications: writes outs / qs / lohi / idx and the stacks X like the
+    per-layer path, plus the LayerNorm outputs / pre-LayerNorm values / statistics its backward reads."""
+    T, B, Nn = scale1.shape
+    ngroups = len(P) // _NP
+    dev, dt = lat.device, lat.dtype
+    lib = _L.load()
+    # both GEMM directions stream the weights as packed MFMA operands, repacked here every call (one launch)
+    WP = torch.empty((2, ngroups, 7, Nn * Nn), dtype=dt, device=dev)
+    src = (ctypes.c_void_p * (7 * ngroups))(*[P[_NP * g + k].data_ptr() for g in range(ngroups) for k in _CHAIN_W])
+    _L.check(lib.muz_trunk_chain_pack(src, 7 * ngroups, _L.ptr(WP[0]), _L.ptr(WP[1]), _L.stream_ptr()),
+             "muz_trunk_chain_pack")
+    ln0 = torch.empty((T, B, Nn), dtype=dt, device=dev)
+    z = torch.empty((T, 6, B, Nn), dtype=dt, device=dev)
+    stats = torch.empty((T, 7, 2, B), dtype=dt, device=dev)
+    a = _L.MuzChainArgs()
+    a.T, a.M, a.ngroups = T, B, ngroups
+    for i in range(T):
+        a.app[i], a.slot[i], a.scaled[i] = apps[i], slot[i], int(scaled[i])
+    for g in range(ngroups):
+        Q = P[_NP * g:_NP * (g + 1)]
+        grp = a.group[g]
+        grp.ln0_gamma, grp.ln0_beta = Q[0].data_ptr(), Q[1].data_ptr()
+        for l, k in enumerate(_CHAIN_W):
+            grp.wf[l], grp.wb[l], grp.bias[l] = WP[0, g, l].data_ptr(), WP[1, g, l].data_ptr(), Q[k + 1].data_ptr()
+            grp.X[l] = X[(g, _GEMM_LAYERS[l])].data_ptr()
+            if l < 6:
+                grp.gamma[l], grp.beta[l] = Q[k + 2].data_ptr(), Q[k + 3].data_ptr()
+    a.latent0, a.scale1, a.shift = lat.data_ptr(), scale1.data_ptr(), shift.data_ptr()
+    a.out, a.q, a.lohi, a.idx = outs.data_ptr(), qs.data_ptr(), lohi.data_ptr(), idx.data_ptr()
+    a.ln0_out, a.z, a.stats = ln0.data_ptr(), z.data_ptr(), stats.data_ptr()
+    _L.check(lib.muz_trunk_chain_fwd(ctypes.byref(a), _L.stream_ptr()), "muz_trunk_chain_fwd")
+    return _Chain(a, (WP, ln0, z, stats, lat, scale1, shift, outs))
+
+
+def _chain_backward(chain, G, H, grad_scale, apps, P, B, Nn):
+    """muz_trunk_chain_bwd: -> (d latent0, d scale, d shift, DZ stacks, LayerNorm partials) for
+    _trunk_param_grads."""
+    ngroups = len(P) // _NP
+    seen = _slots(apps, ngroups)[1]
+    T = len(apps)
+    dev, dt = G.device, G.dtype
+    tiles = (B + 15) // 16
+    DZ = {(g, n): torch.empty((max(seen[g], 1), B, Nn), dtype=dt, device=dev)
+          for g in range(ngroups) for n in _GEMM_LAYERS}
+    scr = {(g, n): torch.empty((max(seen[g], 1), tiles * 3 * Nn), dtype=dt, device=dev)
+           for g in range(ngroups) for n in _CHAIN_PARTS}
+    dscale = torch.empty((T, B, Nn), dtype=dt, device=dev)
+    dshift = torch.empty_like(dscale)
+    dlat = torch.empty((B, Nn), dtype=dt, device=dev)
+    a = chain.args
+    for g in range(ngroups):
+        grp = a.group[g]
+        for l in range(7):
+            grp.DZ[l] = DZ[(g, _GEMM_LAYERS[l])].data_ptr()
+            grp.part[l] = scr[(g, _CHAIN_PARTS[l])].data_ptr()
+    a.g, a.h = G.data_ptr(), (0 if H is None else H.data_ptr())
+    a.grad_scale = grad_scale
+    a.dscale, a.dshift, a.dlatent0 = dscale.data_ptr(), dshift.data_ptr(), dlat.data_ptr()
+    _L.check(_L.load().muz_trunk_chain_bwd(ctypes.byref(a), _L.stream_ptr()), "muz_trunk_chain_bwd")
+    chain.keep = None
+    return dlat, dscale, dshift, DZ, scr
 
 
 class MuZeroNets:

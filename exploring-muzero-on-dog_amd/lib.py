@@ -45,6 +45,24 @@ class MuzTransposeProblem(ctypes.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("K", ctypes.c_int32), ("N", ctypes.c_int32), ("ldt", ctypes.c_int32)]
 
 
+MUZ_CHAIN_MAX_T = 32
+
+
+class MuzChainGroup(ctypes.Structure):
+    """muz_chain_group (include/muz.h): one trunk's parameters and stacked buffers for muz_trunk_chain_*."""
+    _fields_ = [("ln0_gamma", vp), ("ln0_beta", vp), ("wf", vp * 7), ("wb", vp * 7), ("bias", vp * 7), ("gamma", vp * 6),
+                ("beta", vp * 6), ("X", vp * 7), ("DZ", vp * 7), ("part", vp * 7)]
+
+
+class MuzChainArgs(ctypes.Structure):
+    _fields_ = [("T", ctypes.c_int32), ("M", ctypes.c_int32), ("ngroups", ctypes.c_int32),
+                ("app", ctypes.c_int32 * MUZ_CHAIN_MAX_T), ("slot", ctypes.c_int32 * MUZ_CHAIN_MAX_T),
+                ("scaled", ctypes.c_int32 * MUZ_CHAIN_MAX_T), ("group", MuzChainGroup * 2), ("latent0", vp),
+                ("scale1", vp), ("shift", vp), ("out", vp), ("q", vp), ("lohi", vp), ("idx", vp), ("ln0_out", vp),
+                ("z", vp), ("stats", vp), ("g", vp), ("h", vp), ("grad_scale", ctypes.c_float), ("dscale", vp),
+                ("dshift", vp), ("dlatent0", vp)]
+
+
 class MuzLossTerm(ctypes.Structure):
     _fields_ = [("logits", vp), ("dlogits", vp), ("labels", vp), ("probs", vp), ("ncls", ctypes.c_int32),
                 ("ld", ctypes.c_int32), ("rare_not_one", ctypes.c_int32), ("w_rare", ctypes.c_float),
@@ -336,6 +354,9 @@ SIGNATURES = {
     "muz_dense_ln_bwd_scratch_floats": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     "muz_dense_ln_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp,
                                         ctypes.c_int32, vp, vp, vp, vp, vp, vp]),
+    "muz_trunk_chain_pack": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp]),
+    "muz_trunk_chain_fwd": (ctypes.c_int, [ctypes.POINTER(MuzChainArgs), vp]),
+    "muz_trunk_chain_bwd": (ctypes.c_int, [ctypes.POINTER(MuzChainArgs), vp]),
     "muz_adamw_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32, vp]),
     "muz_adamw_step": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_double,
                                       ctypes.c_double, ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double,

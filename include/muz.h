@@ -799,6 +799,61 @@ int64_t muz_dense_ln_bwd_scratch_floats(int32_t M, int32_t N);
 int muz_dense_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
                      const float* gamma, int32_t M, int32_t N, int32_t mode, const float* W, int32_t K,
                      const float* acc, float* dz, float* dres, float* dx, float* scratch, void* stream);
+/* The unrolled dynamics chain of a learner step as ONE launch each way (csrc/learner_chain.hip; replaces
+ * learner._TrunkChain's per-layer launch train of library GEMMs and row kernels; reference:
+ * train_with_reward.py:98-107 (one trunk, K applications), train_stochastic.py:95-121 (act / chance trunks
+ * alternating)).  Application i maps x_i -> x_{i+1} = minmax(x_i + proj(trunk(LN_0(x_i) * scale1_i + shift_i)))
+ * with group app[i]'s weights, trunk = Dense + LN + ReLU twice, then two ResBlocks (Dense + LN + ReLU,
+ * Dense + LN, + input, ReLU) -- DynamicsNetwork4 / StochasticDynamicsNetwork4's FiLM trunk
+ * (muzero_deterministic_madn.py:391-457).  All widths 256.  One workgroup carries 16 rows through all T
+ * applications (weights streamed from L2, the tile's activations in LDS).
+ * Layer order of the 7-entry arrays: Dense "3", "4", ResBlock_0 Dense_0 / Dense_1, ResBlock_1 Dense_0 / Dense_1,
+ * projection "5"; part[] has LayerNorm_0 first, then the 6 Dense + LayerNorm layers.
+ * Forward writes out / q / lohi / idx (as muz_minmax_fwd, per application), ln0_out (LayerNorm_0 output), z / stats
+ * (pre-LayerNorm y + bias of the 6 layers; mean, rstd of LayerNorm_0 then the 6 layers) and every weight layer's
+ * input into the group's stack X[l] at row block slot[i].  Backward (reads everything the forward wrote) writes
+ * each weight layer's output gradient into DZ[l] (same blocks), column partials [ceil(M / 16)][3][256] per
+ * application into part[] (muz_ln_colsum layout), dscale / dshift [T][M][256] and dlatent0 [M][256]; the incoming
+ * gradient of x_{i+1} is g[i] (+ the carried gradient), x grad_scale where scaled[i], + h[i] (h optional). */
+#define MUZ_CHAIN_MAX_T 32
+typedef struct {
+  const float* ln0_gamma;
+  const float* ln0_beta;
+  const float* wf[7];      /* the weights [256][256] packed for the forward and the backward GEMM */
+  const float* wb[7];      /* (muz_trunk_chain_pack) */
+  const float* bias[7];
+  const float* gamma[6];
+  const float* beta[6];
+  float* X[7];             /* [applications of the group][M][256] */
+  float* DZ[7];
+  float* part[7];          /* [applications of the group][ceil(M / 16)][3][256] */
+} muz_chain_group;
+typedef struct {
+  int32_t T, M, ngroups;
+  int32_t app[MUZ_CHAIN_MAX_T], slot[MUZ_CHAIN_MAX_T], scaled[MUZ_CHAIN_MAX_T];
+  muz_chain_group group[2];
+  const float* latent0;    /* [M][256] */
+  const float* scale1;     /* [T][M][256] */
+  const float* shift;      /* [T][M][256] */
+  float* out;              /* [T][M][256] */
+  float* q;                /* [T][M][256] */
+  float* lohi;             /* [T][M][2] */
+  int32_t* idx;            /* [T][M][2] */
+  float* ln0_out;          /* [T][M][256] */
+  float* z;                /* [T][6][M][256] */
+  float* stats;            /* [T][7][2][M] */
+  const float* g;          /* backward: [T][M][256] */
+  const float* h;          /* optional [T][M][256] */
+  float grad_scale;
+  float* dscale;
+  float* dshift;
+  float* dlatent0;
+} muz_chain_args;
+/* wf / wb of count row-major [256][256] weights W[i] (y = x W): fwd + i * 65536 and bwd + i * 65536 hold them as
+ * the MFMA A-operand stream of y = x W and of dx = dz W^T (one launch; call whenever the weights change). */
+int muz_trunk_chain_pack(const float* const* W, int32_t count, float* fwd, float* bwd, void* stream);
+int muz_trunk_chain_fwd(const muz_chain_args* args, void* stream);
+int muz_trunk_chain_bwd(const muz_chain_args* args, void* stream);
 /* 'SAME' Conv1D as a GEMM: the im2col matrix cols [B][W][K x Cin] of x [B][W][Cin] (zero outside each row;
  * tap d reads column w + d - (K - 1) / 2) and its backward dx = sum over taps (fixed order). */
 int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream);

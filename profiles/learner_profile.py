@@ -43,8 +43,14 @@ def timed(label, fn):
     return ms
 
 
-lr = L.Learner(params, C, unroll_steps=10, graph=True)
 batch = ring.sample_batch()
+# the dynamics chain as the per-layer launch train (round 3) instead of csrc/learner_chain.hip's two launches
+L.CHAIN_KERNEL = False
+lr0 = L.Learner(params, C, unroll_steps=10, graph=True)
+timed("train_step (graph replay, fixed batch, chain kernel off)", lambda: lr0.train_step(batch))
+L.CHAIN_KERNEL = True
+del lr0
+lr = L.Learner(params, C, unroll_steps=10, graph=True)
 timed("sample_batch", ring.sample_batch)
 timed("train_step (graph replay, fixed batch)", lambda: lr.train_step(batch))
 timed("sample_batch + train_step", lambda: lr.train_step(ring.sample_batch()))
@@ -61,7 +67,7 @@ cring = R.VectorizedReplayBufferStochastic(20000, 128, 10, 50, obs_shape=(Cc, 56
                                            rng=np.random.RandomState(0))
 cring.save_games_from_buffers(ceng.play_stream(512, seed=1))
 cbatch = cring.sample_batch()
-for chain in (True, False):
+for chain in (True,):   # (CHAIN = False, the per-step graph, records shared weights twice into a GradSink)
     L.CHAIN = chain
     for graph in (True, False):
         clr = L.StochasticLearner(cparams, Cc, unroll_steps=10, graph=graph)
@@ -70,6 +76,10 @@ for chain in (True, False):
     lr_d = L.Learner(params, C, unroll_steps=10, graph=True)
     timed(f"det train_step (graph replay, chain node {'on' if chain else 'off'})", lambda: lr_d.train_step(batch))
 L.CHAIN = True
+L.CHAIN_KERNEL = False
+clr = L.StochasticLearner(cparams, Cc, unroll_steps=10, graph=True)
+timed("classic train_step (graph replay, chain node on, chain kernel off)", lambda: clr.train_step(cbatch))
+L.CHAIN_KERNEL = True
 
 if len(sys.argv) > 2:   # also time with the other BLAS backend (rocBLAS vs hipBLASLt)
     torch.backends.cuda.preferred_blas_library(sys.argv[2])

@@ -1,4 +1,5 @@
 """Learner on the GPU, wired to the device ring and the self-play engine (config (e) loop, small)."""
+import ctypes
 import numpy as np
 import pytest
 import torch
@@ -293,18 +294,107 @@ def test_chain_boundary_launches_bit_identical(cuda, kind):
     inputs = [lat0, scale, shift] + params
     res = []
     for fused in (True, False):
-        L.FUSED_BOUNDARY = fused
+        L.FUSED_BOUNDARY, L.CHAIN_KERNEL = fused, False     # (the per-layer path: the one with boundary launches)
         try:
             o = L._TrunkChain.apply(lat0, scale, shift, 0.5, apps, scaled, heads, *params)
             out, raw = o if heads else (o, None)
             loss = (out * w).sum() + out[-1].square().sum() + ((raw * wh).sum() if heads else 0.0)
             res.append((out.detach().clone(), torch.autograd.grad(loss, inputs)))
         finally:
-            L.FUSED_BOUNDARY = True
+            L.FUSED_BOUNDARY, L.CHAIN_KERNEL = True, True
     torch.cuda.synchronize()
     assert torch.equal(res[0][0], res[1][0])
     for n, a, b in zip(["latent0", "scale", "shift"] + names, res[0][1], res[1][1]):
         assert torch.equal(a, b), n
+
+
+def _chain_layer_st(chain, X, apps, lat0):
+    """The per-layer backward's saved tuples (_TrunkChain.forward's `st`) rebuilt from the chain kernel's forward
+    buffers: (out, z, mean, rstd) per LayerNorm, out = the next weight layer's stacked input."""
+    _, _, L, _, _ = _mods()
+    WT, ln0, z, stats, lat, scale1, shift, outs = chain.keep
+    slot, _ = L._slots(apps, 2)
+    st = []
+    for i, g in enumerate(apps):
+        j = slot[i]
+        xin = lat0 if i == 0 else outs[i - 1]
+        f = [(X[(g, L._GEMM_LAYERS[k + 1])][j], z[i, k], stats[i, k + 1, 0], stats[i, k + 1, 1]) for k in range(6)]
+        f0 = (ln0[i], xin, stats[i, 0, 0], stats[i, 0, 1])
+        rbs = [(X[(g, "a0")][j], f[2], f[3]), (X[(g, "a1")][j], f[4], f[5])]
+        st.append((f0, X[(g, "3")][j], f[0], f[1], rbs, X[(g, "5")][j]))
+    return st
+
+
+@pytest.mark.parametrize("kind,B,K", [("det", 128, 10), ("det", 40, 3), ("classic", 128, 10), ("classic", 17, 2)])
+def test_chain_kernel_matches_layer_path(cuda, kind, B, K):
+    """csrc/learner_chain.hip (muz_trunk_chain_fwd / _bwd: every application of the unrolled chain in one launch
+    each way, 16 rows per workgroup) against the per-layer launch path of the same node (library GEMMs + the row
+    kernels of learner_ln.hip).  Forward: outputs within 1e-5.  Backward: both backward forms fed the SAME saved
+    forward values (the chain kernel's), every gradient within 1e-5 relative to its largest entry (the GEMMs sum in
+    different orders).  Fed separately because gradients are discontinuous where a ReLU input or a min-max
+    extremum sits within rounding of its kink: two forwards that differ in the last bits can legitimately send a
+    row's gradient down different branches (measured: 1 row of 1280 at batch 128 x 10, profiles/chain_diag.py).
+    The learner's shape (batch 128, 10 unroll steps; classic: 20 alternating applications) and ragged batches
+    (rows past the last 16-row tile masked)."""
+    import types
+    _, _, L, _, _ = _mods()
+    g = torch.Generator().manual_seed(43 + B)
+    if kind == "det":
+        nets = L.MuZeroNets(ON.init_params(18, seed=4, randomize_affine=True), 18, 24, "cuda")
+        names, apps, scaled, heads, T = list(L.DYN_TRUNK_PARAMS), (0,) * K, (True,) * K, True, K
+    else:
+        from exploring_muzero_on_dog_amd import stochastic as ST
+        nets = L.ClassicMuZeroNets(ST.init_classic_params(20, seed=6), 20, "cuda")
+        names = [n for k in ("act", "chance") for n in L.trunk_param_names(k)]
+        apps, scaled, heads, T = (0, 1) * K, (False, True) * K, False, 2 * K
+    lat0 = torch.rand(B, 256, generator=g).cuda()
+    scale = (0.3 * torch.randn(T, B, 256, generator=g)).cuda()
+    shift = (0.3 * torch.randn(T, B, 256, generator=g)).cuda()
+    G = torch.randn(T, B, 256, generator=g).cuda()
+    H = torch.randn(T, B, 256, generator=g).cuda() if heads else None
+    P = [nets.p[n].detach() for n in names]
+    with torch.no_grad():
+        L.CHAIN_KERNEL = False
+        try:
+            ref = L._TrunkChain.apply(lat0, scale, shift, 0.5, apps, scaled, heads, *P)
+        finally:
+            L.CHAIN_KERNEL = True
+        ref = ref[0] if heads else ref
+        slot, seen = L._slots(apps, len(P) // L._NP)
+        X = {(gr, n): torch.empty((max(seen[gr], 1), B, 256), device="cuda")
+             for gr in range(len(seen)) for n in L._GEMM_LAYERS}
+        outs, qs = torch.empty(T, B, 256, device="cuda"), torch.empty(T, B, 256, device="cuda")
+        lohi, idx = torch.empty(T, B, 2, device="cuda"), torch.empty(T, B, 2, dtype=torch.int32, device="cuda")
+        scale1 = 1.0 + scale
+        chain = L._chain_forward(lat0, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi, idx)
+        st = _chain_layer_st(chain, X, apps, lat0)
+        common = dict(saved_tensors=(scale1, qs, lohi), P=P, grad_scale=0.5, apps=tuple(apps), X=X)
+        g_layer = L._TrunkChain.backward(types.SimpleNamespace(chain=None, st=st, boundary=True, scaled=tuple(scaled),
+                                                               **common), G, H)
+        g_chain = L._TrunkChain.backward(types.SimpleNamespace(chain=chain, **common), G, H)
+    torch.cuda.synchronize()
+    err = (outs - ref).abs().max().item()
+    assert err < 1e-5, f"forward differs by {err:.2e}"
+    labels = ["latent0", "scale", "shift", None, None, None, None] + names
+    for n, a, b in zip(labels, g_chain, g_layer):
+        if n is None:
+            continue
+        err = (a - b).abs().max().item() / max(1e-3, b.abs().max().item())
+        assert err < 1e-5, f"{n}: relative gradient difference {err:.2e}"
+
+
+def test_chain_kernel_host_checks(cuda):
+    """muz_trunk_chain_fwd / _bwd reject what the kernels do not implement (before any launch)."""
+    from exploring_muzero_on_dog_amd import lib as _L
+    lib = _L.load()
+    a = _L.MuzChainArgs()
+    assert lib.muz_trunk_chain_fwd(ctypes.byref(a), _L.stream_ptr()) == _L.MUZ_E_INVALID     # T = 0, nulls
+    a.T, a.M, a.ngroups = _L.MUZ_CHAIN_MAX_T + 1, 16, 1
+    assert lib.muz_trunk_chain_fwd(ctypes.byref(a), _L.stream_ptr()) == _L.MUZ_E_INVALID
+    a.T, a.ngroups = 1, 3
+    assert lib.muz_trunk_chain_bwd(ctypes.byref(a), _L.stream_ptr()) == _L.MUZ_E_INVALID
+    src = (ctypes.c_void_p * 1)(None)
+    assert lib.muz_trunk_chain_pack(src, 1, None, None, _L.stream_ptr()) == _L.MUZ_E_INVALID
 
 
 def test_dynamics_chain_node_matches_per_step_autograd(cuda):
@@ -325,8 +415,14 @@ def test_dynamics_chain_node_matches_per_step_autograd(cuda):
     params = [nets.p[n] for n in L.DYN_TRUNK_PARAMS]
     inputs = [lat0, scale, shift] + params
 
-    out, raw = L._TrunkChain.apply(lat0, scale, shift, 0.5, (0,) * K, (True,) * K, True, *params)
-    g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum() + (raw * wh).sum(), inputs)
+    # the node's per-layer form (library GEMMs, like the per-step graph): both forwards round alike, so no row's
+    # gradient takes a different ReLU / min-max branch (the chain kernel: test_chain_kernel_matches_layer_path)
+    L.CHAIN_KERNEL = False
+    try:
+        out, raw = L._TrunkChain.apply(lat0, scale, shift, 0.5, (0,) * K, (True,) * K, True, *params)
+        g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum() + (raw * wh).sum(), inputs)
+    finally:
+        L.CHAIN_KERNEL = True
     lats, raws = [lat0], []
     for k in range(K):
         nxt = nets.dynamics_trunk(lats[-1], scale[k], shift[k])
@@ -399,9 +495,13 @@ def test_classic_chain_node_matches_per_step_autograd(cuda):
 
     film = [torch.stack([nets._dense(f"dynamics/{pre}_film_{x}", e).reshape(K, B, -1)
                          for pre, e in (("act", ea), ("chance", ec))], 1).reshape(2 * K, B, -1) for x in ("scale", "shift")]
-    out = L._TrunkChain.apply(lat0, film[0], film[1], 0.5, (0, 1) * K, (False, True) * K, False,
-                              *(nets.p[n] for n in names[:2 * L._NP]))
-    g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs, retain_graph=True)
+    L.CHAIN_KERNEL = False     # (the node's per-layer form, see test_dynamics_chain_node_matches_per_step_autograd)
+    try:
+        out = L._TrunkChain.apply(lat0, film[0], film[1], 0.5, (0, 1) * K, (False, True) * K, False,
+                                  *(nets.p[n] for n in names[:2 * L._NP]))
+        g1 = torch.autograd.grad((out * w).sum() + out[-1].square().sum(), inputs, retain_graph=True)
+    finally:
+        L.CHAIN_KERNEL = True
     # the per-step graph reads the same FiLM rows (row-wise GEMMs over all steps at once, as loss_fn_stochastic
     # does): a library GEMM over one step's rows may round differently from the same rows inside K steps
     # (rocBLAS picks its kernel by shape), and this test is about the chain node, not the FiLM projections
