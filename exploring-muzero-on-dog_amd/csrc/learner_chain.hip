@@ -28,7 +28,14 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 #ifndef MUZ_CHAIN_RING
 #define MUZ_CHAIN_RING 3
 #endif
-constexpr int N = 256, R = 16, LD = N + 4, NTH = 512, KB = N / 16, D = MUZ_CHAIN_RING;
+// waves per workgroup: 8 (2 per SIMD, each owning two 16-column tiles) or 16 (4 per SIMD, one tile each)
+#ifndef MUZ_CHAIN_WAVES
+#define MUZ_CHAIN_WAVES 8
+#endif
+constexpr int NWAVE = MUZ_CHAIN_WAVES, NT = 16 / NWAVE, LNT = NT == 2 ? 1 : 0;
+constexpr int N = 256, R = 16, LD = N + 4, NTH = 64 * NWAVE, KB = N / 16, D = MUZ_CHAIN_RING;
+constexpr int TPR = NTH / R, E = N / TPR;   // row phases: threads per row, columns per thread
+static_assert(NWAVE == 8 || NWAVE == 16, "8 or 16 waves");
 constexpr int kLayers = 6;   // Dense + LayerNorm layers; weight layer 6 = the projection
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
@@ -37,20 +44,20 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
 
 __device__ __forceinline__ float row_sum(float v) {
 #pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = TPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
 __device__ __forceinline__ int row_isum(int v) {
 #pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = TPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
-// the lowest column of the row's extremum (k_minmax_fwd's wave_argext over the 32 lanes of a row)
+// the lowest column of the row's extremum (k_minmax_fwd's wave_argext over the TPR lanes of a row)
 __device__ __forceinline__ void row_argext(float& v, int& i, bool is_max) {
 #pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) {
+  for (int o = TPR / 2; o >= 1; o >>= 1) {
     const float ov = __shfl_xor(v, o, 64);
     const int oi = __shfl_xor(i, o, 64);
     if ((is_max ? ov > v : ov < v) || (ov == v && oi < i)) v = ov, i = oi;
@@ -58,19 +65,19 @@ __device__ __forceinline__ void row_argext(float& v, int& i, bool is_max) {
 }
 
 // The streamed matrix of the next GEMM, packed by muz_trunk_chain_pack so that every load instruction reads 1 KB
-// contiguous (lane l: 16 bytes at l * 16): packed[w][kb][t][lane][j] = Mt[32 w + 16 t + (lane & 15)][16 kb +
-// 4 (lane >> 4) + j].  D slots of two loads (one per 16-column tile); prime() issues k-blocks 0 .. D - 2, gemm()
+// contiguous (lane l: 16 bytes at l * 16): packed[w][kb][t][lane][j] = Mt[16 NT w + 16 t + (lane & 15)][16 kb +
+// 4 (lane >> 4) + j].  D slots of NT loads (one per 16-column tile); prime() issues k-blocks 0 .. D - 2, gemm()
 // keeps D - 1 blocks ahead.  All slot indices are compile-time.
 struct Ring {
-  f4 w[D][2];
+  f4 w[D][NT];
   const AS1 float* p;
 
   __device__ __forceinline__ void load(int slot, int blk) {
-    w[slot][0] = *reinterpret_cast<const AS1 f4*>(p + 512 * blk);
-    w[slot][1] = *reinterpret_cast<const AS1 f4*>(p + 512 * blk + 256);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) w[slot][t] = *reinterpret_cast<const AS1 f4*>(p + 256 * (NT * blk + t));
   }
   __device__ __forceinline__ void prime(const float* packed) {
-    p = gp(packed) + ((size_t)(threadIdx.x >> 6) * KB * 2 * 64 + (threadIdx.x & 63)) * 4;
+    p = gp(packed) + ((size_t)(threadIdx.x >> 6) * KB * NT * 64 + (threadIdx.x & 63)) * 4;
 #pragma unroll
     for (int b = 0; b < D - 1; ++b) load(b, b);
   }
@@ -85,8 +92,8 @@ struct PackTable {
 __global__ __launch_bounds__(256) void k_chain_pack(PackTable tb, float* fwd, float* bwd) {
   const int q = blockIdx.x * 256 + threadIdx.x;     // float4 index within matrix blockIdx.y
   const int i = blockIdx.y;
-  const int lane = q & 63, t = (q >> 6) & 1, kb = (q >> 7) & (KB - 1), w = q >> 11;
-  const int r = 32 * w + 16 * t + (lane & 15), c = 16 * kb + 4 * (lane >> 4);
+  const int lane = q & 63, t = (q >> 6) & (NT - 1), kb = (q >> (6 + LNT)) & (KB - 1), w = q >> (10 + LNT);
+  const int r = 16 * NT * w + 16 * t + (lane & 15), c = 16 * kb + 4 * (lane >> 4);
   const float* W = tb.src[i];
   f4 vf, vb;
 #pragma unroll
@@ -96,10 +103,10 @@ __global__ __launch_bounds__(256) void k_chain_pack(PackTable tb, float* fwd, fl
   *reinterpret_cast<f4*>(bwd + (size_t)i * N * N + 4 * q) = vb;
 }
 
-// out[t] = rows (lane & 15) of in[16][LD] times the primed matrix, columns 32 w + 16 t + 4 (lane >> 4) .. + 3
-__device__ __forceinline__ void gemm(Ring& rg, const float* in, f4 (&out)[2]) {
+// out[t] = rows (lane & 15) of in[16][LD] times the primed matrix, columns 16 NT w + 16 t + 4 (lane >> 4) .. + 3
+__device__ __forceinline__ void gemm(Ring& rg, const float* in, f4 (&out)[NT]) {
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  f4 acc[2][2] = {};
+  f4 acc[NT][2] = {};
   const float* xp = in + i * LD + 4 * g;
   f4 x = *reinterpret_cast<const f4*>(xp);
 #pragma unroll
@@ -109,31 +116,31 @@ __device__ __forceinline__ void gemm(Ring& rg, const float* in, f4 (&out)[2]) {
     // the next block's input row is read from LDS while this block's MFMAs run
     const f4 xn = b + 1 < KB ? *reinterpret_cast<const f4*>(xp + 16 * (b + 1)) : x;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[0][j & 1] = mfma(rg.w[b % D][0][j], x[j], acc[0][j & 1]);
-      acc[1][j & 1] = mfma(rg.w[b % D][1][j], x[j], acc[1][j & 1]);
-    }
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t][j & 1] = mfma(rg.w[b % D][t][j], x[j], acc[t][j & 1]);
     x = xn;
   }
-  out[0] = acc[0][0] + acc[0][1];
-  out[1] = acc[1][0] + acc[1][1];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) out[t] = acc[t][0] + acc[t][1];
 }
 
-__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
-  *reinterpret_cast<f4*>(v) = *reinterpret_cast<const f4*>(p);
-  *reinterpret_cast<f4*>(v + 4) = *reinterpret_cast<const f4*>(p + 4);
+// E consecutive floats (E = 4 or 8) as 16-byte accesses
+__device__ __forceinline__ void ldE(const float* p, float (&v)[E]) {
+#pragma unroll
+  for (int k = 0; k < E; k += 4) *reinterpret_cast<f4*>(v + k) = *reinterpret_cast<const f4*>(p + k);
 }
-__device__ __forceinline__ void ld8g(const float* p, float (&v)[8]) {
-  *reinterpret_cast<f4*>(v) = *reinterpret_cast<const AS1 f4*>(gp(p));
-  *reinterpret_cast<f4*>(v + 4) = *reinterpret_cast<const AS1 f4*>(gp(p + 4));
+__device__ __forceinline__ void ldEg(const float* p, float (&v)[E]) {
+#pragma unroll
+  for (int k = 0; k < E; k += 4) *reinterpret_cast<f4*>(v + k) = *reinterpret_cast<const AS1 f4*>(gp(p + k));
 }
-__device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
-  *reinterpret_cast<f4*>(p) = *reinterpret_cast<const f4*>(v);
-  *reinterpret_cast<f4*>(p + 4) = *reinterpret_cast<const f4*>(v + 4);
+__device__ __forceinline__ void stE(float* p, const float (&v)[E]) {
+#pragma unroll
+  for (int k = 0; k < E; k += 4) *reinterpret_cast<f4*>(p + k) = *reinterpret_cast<const f4*>(v + k);
 }
-__device__ __forceinline__ void st8g(float* p, const float (&v)[8]) {
-  *reinterpret_cast<AS1 f4*>(gpw(p)) = *reinterpret_cast<const f4*>(v);
-  *reinterpret_cast<AS1 f4*>(gpw(p + 4)) = *reinterpret_cast<const f4*>(v + 4);
+__device__ __forceinline__ void stEg(float* p, const float (&v)[E]) {
+#pragma unroll
+  for (int k = 0; k < E; k += 4) *reinterpret_cast<AS1 f4*>(gpw(p + k)) = *reinterpret_cast<const f4*>(v + k);
 }
 
 __device__ __forceinline__ float rstd_of(float s, float s2) {
@@ -145,20 +152,20 @@ __device__ __forceinline__ float rstd_of(float s, float s2) {
 // Every row phase's global operands are loaded BEFORE the next matrix is primed: loads retire in order for
 // s_waitcnt vmcnt, so an operand issued behind the prime's 14 loads would wait for all of them.
 struct Ln0Ops {   // LayerNorm_0 + FiLM of one application
-  float ga[8], be[8], sc[8], sh[8];
+  float ga[E], be[E], sc[E], sh[E];
 };
 
 __device__ __forceinline__ void load_ln0(const AS4 muz_chain_args* a, int i, size_t MN, size_t o, bool live,
                                          int c0, Ln0Ops& p) {
   const AS4 muz_chain_group* G = &a->group[a->app[i]];
-  ld8g(G->ln0_gamma + c0, p.ga);
-  ld8g(G->ln0_beta + c0, p.be);
+  ldEg(G->ln0_gamma + c0, p.ga);
+  ldEg(G->ln0_beta + c0, p.be);
   if (live) {
-    ld8g(a->scale1 + i * MN + o, p.sc);
-    ld8g(a->shift + i * MN + o, p.sh);
+    ldEg(a->scale1 + i * MN + o, p.sc);
+    ldEg(a->shift + i * MN + o, p.sh);
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) p.sc[e] = p.sh[e] = 0.f;
+    for (int e = 0; e < E; ++e) p.sc[e] = p.sh[e] = 0.f;
   }
 }
 
@@ -170,14 +177,14 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
   __shared__ __attribute__((aligned(16))) float rs[R * LD];    // the current ResBlock's input
   __shared__ __attribute__((aligned(16))) float lat[R * LD];   // x_i
   const int tid = threadIdx.x, M = a->M, T = a->T;
-  const int row = tid >> 5, c0 = 8 * (tid & 31), m = blockIdx.x * R + row;
+  const int row = tid / TPR, c0 = E * (tid % TPR), m = blockIdx.x * R + row;
   const bool live = m < M;
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
   const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
   {
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (live) ld8g(a->latent0 + o, v);
-    st8(lat + row * LD + c0, v);
+    float v[E] = {};
+    if (live) ldEg(a->latent0 + o, v);
+    stE(lat + row * LD + c0, v);
   }
   Ln0Ops n0;
   load_ln0(a, 0, MN, o, live, c0, n0);
@@ -190,94 +197,94 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
     float* st = a->stats + (size_t)i * 7 * 2 * M;
     // LayerNorm_0 + FiLM (k_ln_fwd<256, true>)
     {
-      float v[8];
-      ld8(lat + row * LD + c0, v);
+      float v[E];
+      ldE(lat + row * LD + c0, v);
       float s = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < E; ++e) {
         s += v[e];
         s2 += v[e] * v[e];
       }
       s = row_sum(s);
       s2 = row_sum(s2);
       const float mean = s / (float)N, rstd = rstd_of(s, s2);
-      float ln[8], f[8];
+      float ln[E], f[E];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < E; ++e) {
         ln[e] = (v[e] - mean) * (rstd * n0.ga[e]) + n0.be[e];
         float p = ln[e] * n0.sc[e];
         asm volatile("" : "+v"(p));   // a multiply, then an add (torch's addcmul; no fma)
         f[e] = n0.sh[e] + p;
       }
-      st8(xs + row * LD + c0, f);
+      stE(xs + row * LD + c0, f);
       if (live) {
-        st8g(a->ln0_out + i * MN + o, ln);
-        st8g(G->X[0] + js, f);
-        if ((tid & 31) == 0) st[m] = mean, st[M + m] = rstd;
+        stEg(a->ln0_out + i * MN + o, ln);
+        stEg(G->X[0] + js, f);
+        if ((tid % TPR) == 0) st[m] = mean, st[M + m] = rstd;
       }
     }
     __syncthreads();
 #pragma unroll 1
     for (int l = 0; l <= kLayers; ++l) {
-      f4 acc[2];
+      f4 acc[NT];
       gemm(rg, xs, acc);
-      float ga[8], be[8];
-      f4 bb[2] = {};
+      float ga[E], be[E];
+      f4 bb[NT] = {};
       if (l < kLayers) {
-        ld8g(G->gamma[l] + c0, ga);
-        ld8g(G->beta[l] + c0, be);
+        ldEg(G->gamma[l] + c0, ga);
+        ldEg(G->beta[l] + c0, be);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) bb[t] = *reinterpret_cast<const AS1 f4*>(gp(G->bias[l] + 32 * w + 16 * t + 4 * lg));
+        for (int t = 0; t < NT; ++t) bb[t] = *reinterpret_cast<const AS1 f4*>(gp(G->bias[l] + 16 * NT * w + 16 * t + 4 * lg));
         rg.prime(G->wf[l + 1]);   // the next GEMM's matrix flies during the row phase
       } else {
-        ld8g(G->bias[6] + c0, ga);
+        ldEg(G->bias[6] + c0, ga);
         if (i + 1 < T) {
           load_ln0(a, i + 1, MN, o, live, c0, n0);
           rg.prime(a->group[a->app[i + 1]].wf[0]);
         }
       }
 #pragma unroll
-      for (int t = 0; t < 2; ++t) *reinterpret_cast<f4*>(ys + li * LD + 32 * w + 16 * t + 4 * lg) = acc[t] + bb[t];
+      for (int t = 0; t < NT; ++t) *reinterpret_cast<f4*>(ys + li * LD + 16 * NT * w + 16 * t + 4 * lg) = acc[t] + bb[t];
       __syncthreads();
       if (l < kLayers) {
         // Dense epilogue (k_ln_fwd): z = y + bias, LayerNorm, ReLU / residual ReLU
         const bool resid = l == 3 || l == 5;
-        float v[8], res[8];
-        ld8(ys + row * LD + c0, v);
-        if (resid) ld8(rs + row * LD + c0, res);
+        float v[E], res[E];
+        ldE(ys + row * LD + c0, v);
+        if (resid) ldE(rs + row * LD + c0, res);
         float s = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < E; ++e) {
           s += v[e];
           s2 += v[e] * v[e];
         }
         s = row_sum(s);
         s2 = row_sum(s2);
         const float mean = s / (float)N, rstd = rstd_of(s, s2);
-        float out[8];
+        float out[E];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < E; ++e) {
           const float t = (v[e] - mean) * (rstd * ga[e]) + be[e];
           out[e] = resid ? fmaxf(res[e] + t, 0.f) : fmaxf(t, 0.f);
         }
-        st8(xs + row * LD + c0, out);
-        if (l == 1 || l == 3) st8(rs + row * LD + c0, out);   // the next ResBlock's input
+        stE(xs + row * LD + c0, out);
+        if (l == 1 || l == 3) stE(rs + row * LD + c0, out);   // the next ResBlock's input
         if (live) {
-          st8g(G->X[l + 1] + js, out);
-          st8g(a->z + ((size_t)i * kLayers + l) * MN + o, v);
-          if ((tid & 31) == 0) st[(2 + 2 * l) * M + m] = mean, st[(3 + 2 * l) * M + m] = rstd;
+          stEg(G->X[l + 1] + js, out);
+          stEg(a->z + ((size_t)i * kLayers + l) * MN + o, v);
+          if ((tid % TPR) == 0) st[(2 + 2 * l) * M + m] = mean, st[(3 + 2 * l) * M + m] = rstd;
         }
         __syncthreads();
       } else {
         // min-max (k_minmax_fwd): q = x + (y + bias), out = (q - lo) / (hi - lo + 1e-8).  No barrier after it:
         // x_{i+1} is read back by this row's own threads, and xs / ys are free (the last GEMM is done)
-        float x[8], y[8], q[8];
-        ld8(lat + row * LD + c0, x);
-        ld8(ys + row * LD + c0, y);
+        float x[E], y[E], q[E];
+        ldE(lat + row * LD + c0, x);
+        ldE(ys + row * LD + c0, y);
         float lo = INFINITY, hi = -INFINITY;
         int ilo = N, ihi = N;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < E; ++e) {
           q[e] = x[e] + (y[e] + ga[e]);
           if (q[e] < lo) lo = q[e], ilo = c0 + e;
           if (q[e] > hi) hi = q[e], ihi = c0 + e;
@@ -285,14 +292,14 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
         row_argext(lo, ilo, false);
         row_argext(hi, ihi, true);
         const float den = (hi - lo) + 1e-8f;
-        float out[8];
+        float out[E];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) out[e] = (q[e] - lo) / den;
-        st8(lat + row * LD + c0, out);
+        for (int e = 0; e < E; ++e) out[e] = (q[e] - lo) / den;
+        stE(lat + row * LD + c0, out);
         if (live) {
-          st8g(a->out + i * MN + o, out);
-          st8g(a->q + i * MN + o, q);
-          if ((tid & 31) == 0) {
+          stEg(a->out + i * MN + o, out);
+          stEg(a->q + i * MN + o, q);
+          if ((tid % TPR) == 0) {
             const size_t r2 = (size_t)i * 2 * M + 2 * m;
             a->lohi[r2] = lo, a->lohi[r2 + 1] = hi;
             a->idx[r2] = ilo, a->idx[r2 + 1] = ihi;
@@ -307,7 +314,15 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
 // Column partials of one layer and application (k_dense_ln_bwd's: rows summed in order): [3][N] at p.
 __device__ __forceinline__ void partials(const float* pgs, const float* pbs, const float* dzs, float* p) {
   const int tid = threadIdx.x;
-  if (tid < N) {
+  if constexpr (NTH >= 3 * N) {   // one column sum per thread
+    if (tid >= 3 * N) return;
+    const int q = tid / N, c = tid % N;
+    const float* s = q == 0 ? pgs : pbs;
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc += q == 2 ? dzs[r * LD + c] : s[r * N + c];
+    p[q * N + c] = acc;
+  } else if (tid < N) {
     float sg = 0.f, sb = 0.f;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -326,25 +341,25 @@ __device__ __forceinline__ void partials(const float* pgs, const float* pbs, con
 }
 
 struct MmOps {   // min-max backward of one application; lohi = (min, max) of q
-  float g[8], q[8], h[8], lohi[2];
+  float g[E], q[E], h[E], lohi[2];
 };
 struct RowOps {  // a Dense + LayerNorm layer's saved forward values (LayerNorm_0: out = its output)
-  float out[8], z[8], ga[8];
+  float out[E], z[E], ga[E];
   float mean, rstd;
 };
 
 __device__ __forceinline__ void load_mm(const AS4 muz_chain_args* a, int i, size_t MN, size_t o, int m, bool live,
                                         MmOps& p) {
   if (live) {
-    ld8g(a->g + i * MN + o, p.g);
-    ld8g(a->q + i * MN + o, p.q);
-    if (a->h) ld8g(a->h + i * MN + o, p.h);
+    ldEg(a->g + i * MN + o, p.g);
+    ldEg(a->q + i * MN + o, p.q);
+    if (a->h) ldEg(a->h + i * MN + o, p.h);
     const size_t r2 = (size_t)i * 2 * a->M + 2 * m;
     p.lohi[0] = gp(a->lohi)[r2];
     p.lohi[1] = gp(a->lohi)[r2 + 1];
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) p.g[e] = p.q[e] = p.h[e] = 0.f;
+    for (int e = 0; e < E; ++e) p.g[e] = p.q[e] = p.h[e] = 0.f;
     p.lohi[0] = p.lohi[1] = 0.f;
   }
 }
@@ -359,7 +374,7 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
   __shared__ __attribute__((aligned(16))) float pgs[R * N];      // per-row do * xhat, do (column partials)
   __shared__ __attribute__((aligned(16))) float pbs[R * N];
   const int tid = threadIdx.x, M = a->M, T = a->T;
-  const int row = tid >> 5, c0 = 8 * (tid & 31), m = blockIdx.x * R + row;
+  const int row = tid / TPR, c0 = E * (tid % TPR), m = blockIdx.x * R + row;
   const bool live = m < M;
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
   const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
@@ -376,29 +391,29 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
     const float* st = a->stats + (size_t)i * 7 * 2 * M;
     // min-max backward (k_minmax_bwd): d = (g + carry) x scale + h
     {
-      float d[8];
+      float d[E];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d[e] = mm.g[e];
+      for (int e = 0; e < E; ++e) d[e] = mm.g[e];
       if (i + 1 < T) {
-        float c[8];
-        ld8(carry + row * LD + c0, c);
+        float c[E];
+        ldE(carry + row * LD + c0, c);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d[e] = d[e] + c[e];
+        for (int e = 0; e < E; ++e) d[e] = d[e] + c[e];
       }
       if (a->scaled[i]) {
         const float s = a->grad_scale;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d[e] = d[e] * s;
+        for (int e = 0; e < E; ++e) d[e] = d[e] * s;
       }
       if (a->h) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d[e] = d[e] + mm.h[e];
+        for (int e = 0; e < E; ++e) d[e] = d[e] + mm.h[e];
       }
       const float lo = mm.lohi[0], hi = mm.lohi[1], den = (hi - lo) + 1e-8f;
       float sd = 0.f, sq = 0.f;
       int nlo = 0, nhi = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < E; ++e) {
         sd += d[e];
         sq += d[e] * (mm.q[e] - lo);
         nlo += mm.q[e] == lo;
@@ -409,43 +424,43 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
       nlo = row_isum(nlo);
       nhi = row_isum(nhi);
       const float glo = (-sd / den + sq) / (float)nlo, ghi = (-sq) / (float)nhi;
-      float dq[8];
+      float dq[E];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < E; ++e) {
         float r = d[e] / den;
         if (mm.q[e] == lo) r = r + glo;
         if (mm.q[e] == hi) r = r + ghi;
         dq[e] = live ? r : 0.f;
       }
-      st8(dzs + row * LD + c0, dq);
-      st8(carry + row * LD + c0, dq);
-      if (live) st8g(G->DZ[6] + js, dq);
+      stE(dzs + row * LD + c0, dq);
+      stE(carry + row * LD + c0, dq);
+      if (live) stEg(G->DZ[6] + js, dq);
     }
     __syncthreads();
     RowOps ro;
-    float sc0[8];   // LayerNorm_0's FiLM scale (loaded with its other operands)
+    float sc0[E];   // LayerNorm_0's FiLM scale (loaded with its other operands)
 #pragma unroll 1
     for (int l = kLayers; l >= 0; --l) {
       // GEMM: dx = dz W_l^T (+ the residual gradient after a ResBlock's first layer)
-      f4 acc[2];
+      f4 acc[NT];
       gemm(rg, dzs, acc);
       // the next row phase's operands, then the next matrix
       const int k = l - 1;
       if (l > 0) {
-        ld8g(G->gamma[k] + c0, ro.ga);
+        ldEg(G->gamma[k] + c0, ro.ga);
         if (live) {
-          ld8g(G->X[k + 1] + js, ro.out);
-          ld8g(a->z + ((size_t)i * kLayers + k) * MN + o, ro.z);
+          ldEg(G->X[k + 1] + js, ro.out);
+          ldEg(a->z + ((size_t)i * kLayers + k) * MN + o, ro.z);
           ro.mean = gp(st)[(2 + 2 * k) * M + m], ro.rstd = gp(st)[(3 + 2 * k) * M + m];
         }
         rg.prime(G->wb[k]);
       } else {
-        ld8g(G->ln0_gamma + c0, ro.ga);
+        ldEg(G->ln0_gamma + c0, ro.ga);
         if (live) {
-          ld8g(a->ln0_out + i * MN + o, ro.out);
-          ld8g((i == 0 ? a->latent0 : a->out + (i - 1) * MN) + o, ro.z);
+          ldEg(a->ln0_out + i * MN + o, ro.out);
+          ldEg((i == 0 ? a->latent0 : a->out + (i - 1) * MN) + o, ro.z);
           ro.mean = gp(st)[m], ro.rstd = gp(st)[M + m];
-          ld8g(a->scale1 + i * MN + o, sc0);
+          ldEg(a->scale1 + i * MN + o, sc0);
         }
         if (i > 0) {
           load_mm(a, i - 1, MN, o, m, live, mm);
@@ -454,14 +469,14 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
       }
       if (!live) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ro.out[e] = ro.z[e] = 0.f;
+        for (int e = 0; e < E; ++e) ro.out[e] = ro.z[e] = 0.f;
         ro.mean = ro.rstd = 0.f;
       }
       const bool add_res = l == 2 || l == 4;
       const int mr = blockIdx.x * R + li;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int c = 32 * w + 16 * t + 4 * lg;
+      for (int t = 0; t < NT; ++t) {
+        const int c = 16 * NT * w + 16 * t + 4 * lg;
         f4 v = acc[t];
         if (add_res) v += *reinterpret_cast<const f4*>(dres + li * LD + c);
         *reinterpret_cast<f4*>(dxs + li * LD + c) = v;
@@ -474,40 +489,40 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
       if (l == 0) break;
       // LayerNorm / ReLU backward of Dense layer k (k_dense_ln_bwd's row half)
       const bool resid = k == 3 || k == 5;
-      float d[8];
-      ld8(dxs + row * LD + c0, d);
-      float xh[8], gg[8], sa = 0.f, sb = 0.f;
+      float d[E];
+      ldE(dxs + row * LD + c0, d);
+      float xh[E], gg[E], sa = 0.f, sb = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < E; ++e) {
         if (!(ro.out[e] > 0.f)) d[e] = 0.f;
         xh[e] = (ro.z[e] - ro.mean) * ro.rstd;
         gg[e] = d[e] * ro.ga[e];
         sa += gg[e];
         sb += gg[e] * xh[e];
       }
-      if (resid) st8(dres + row * LD + c0, d);
+      if (resid) stE(dres + row * LD + c0, d);
       sa = row_sum(sa) / (float)N;
       sb = row_sum(sb) / (float)N;
-      float dz[8], pg[8];
+      float dz[E], pg[E];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < E; ++e) {
         dz[e] = ro.rstd * (gg[e] - sa - xh[e] * sb);
         pg[e] = d[e] * xh[e];
       }
-      st8(dzs + row * LD + c0, dz);
-      st8(pgs + row * N + c0, pg);
-      st8(pbs + row * N + c0, d);
-      if (live) st8g(G->DZ[k] + js, dz);
+      stE(dzs + row * LD + c0, dz);
+      stE(pgs + row * N + c0, pg);
+      stE(pbs + row * N + c0, d);
+      if (live) stEg(G->DZ[k] + js, dz);
       __syncthreads();
     }
     // LayerNorm_0 + FiLM backward (k_ln_bwd<256, true>; ro = its saved values, scale1 below); then
     // carry = dz_0 + dq, the gradient of x_i
     {
-      float d[8];
-      ld8(dxs + row * LD + c0, d);
-      float ds[8], xh[8], gg[8], sa = 0.f, sb = 0.f;
+      float d[E];
+      ldE(dxs + row * LD + c0, d);
+      float ds[E], xh[E], gg[E], sa = 0.f, sb = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < E; ++e) {
         ds[e] = d[e] * ro.out[e];
         d[e] = d[e] * (live ? sc0[e] : 0.f);
         xh[e] = (ro.z[e] - ro.mean) * ro.rstd;
@@ -515,31 +530,205 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
         sa += gg[e];
         sb += gg[e] * xh[e];
       }
-      if (live) st8g(a->dscale + i * MN + o, ds);
+      if (live) stEg(a->dscale + i * MN + o, ds);
       sa = row_sum(sa) / (float)N;
       sb = row_sum(sb) / (float)N;
-      float dz[8], pg[8], c[8];
-      ld8(carry + row * LD + c0, c);
+      float dz[E], pg[E], c[E];
+      ldE(carry + row * LD + c0, c);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < E; ++e) {
         dz[e] = ro.rstd * (gg[e] - sa - xh[e] * sb);
         pg[e] = d[e] * xh[e];
         c[e] = dz[e] + c[e];
       }
-      st8(dzs + row * LD + c0, dz);
-      st8(pgs + row * N + c0, pg);
-      st8(pbs + row * N + c0, d);
-      st8(carry + row * LD + c0, c);
+      stE(dzs + row * LD + c0, dz);
+      stE(pgs + row * N + c0, pg);
+      stE(pbs + row * N + c0, d);
+      stE(carry + row * LD + c0, c);
     }
     __syncthreads();
     partials(pgs, pbs, dzs, G->part[0] + pj);
     __syncthreads();
   }
   if (live) {
-    float c[8];
-    ld8(carry + row * LD + c0, c);
-    st8g(a->dlatent0 + o, c);
+    float c[E];
+    ldE(carry + row * LD + c0, c);
+    stEg(a->dlatent0 + o, c);
   }
+}
+
+// ---- ResBlock stacks (muz_rbstack_*) ---------------------------------------------------------------------
+// The same tile, GEMM loop and row arithmetic as the chain: weight layer l = 2 b + k of block b; the ResBlock input
+// stays in LDS (rs) for the second layer's residual.
+struct RowOpsRb {   // a layer's saved forward values for its backward rows; ms = (mean, rstd)
+  float out[E], z[E], ga[E], ms[2];
+};
+
+__device__ __forceinline__ void load_rb_rows(const AS4 muz_rbstack_args* a, int l, size_t MN, size_t o, int m,
+                                             bool live, int c0, RowOpsRb& p) {
+  const int L = 2 * a->nb, M = a->M;
+  ldEg(a->gamma[l] + c0, p.ga);
+  if (live) {
+    ldEg((l + 1 < L ? a->X + (l + 1) * MN : a->out) + o, p.out);
+    ldEg(a->z + l * MN + o, p.z);
+    p.ms[0] = gp(a->stats)[(size_t)(2 * l) * M + m];
+    p.ms[1] = gp(a->stats)[(size_t)(2 * l + 1) * M + m];
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) p.out[e] = p.z[e] = 0.f;
+    p.ms[0] = p.ms[1] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(NTH, 1) void k_rbstack_fwd(muz_rbstack_args) {
+#pragma clang fp contract(off)
+  const AS4 muz_rbstack_args* a = kernarg0<muz_rbstack_args>();
+  __shared__ __attribute__((aligned(16))) float xs[R * LD];    // the current GEMM's input
+  __shared__ __attribute__((aligned(16))) float ys[R * LD];    // its output (+ bias)
+  __shared__ __attribute__((aligned(16))) float rs[R * LD];    // the current ResBlock's input
+  const int tid = threadIdx.x, M = a->M, L = 2 * a->nb;
+  const int row = tid / TPR, c0 = E * (tid % TPR), m = blockIdx.x * R + row;
+  const bool live = m < M;
+  const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
+  const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
+  {
+    float v[E] = {};
+    if (live) ldEg(a->x + o, v);
+    stE(xs + row * LD + c0, v);
+    stE(rs + row * LD + c0, v);
+    if (live) stEg(a->X + o, v);
+  }
+  Ring rg;
+  rg.prime(a->wf[0]);
+  __syncthreads();
+#pragma unroll 1
+  for (int l = 0; l < L; ++l) {
+    f4 acc[NT];
+    gemm(rg, xs, acc);
+    float ga[E], be[E];
+    f4 bb[NT];
+    ldEg(a->gamma[l] + c0, ga);
+    ldEg(a->beta[l] + c0, be);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) bb[t] = *reinterpret_cast<const AS1 f4*>(gp(a->bias[l] + 16 * NT * w + 16 * t + 4 * lg));
+    if (l + 1 < L) rg.prime(a->wf[l + 1]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) *reinterpret_cast<f4*>(ys + li * LD + 16 * NT * w + 16 * t + 4 * lg) = acc[t] + bb[t];
+    __syncthreads();
+    const bool resid = l & 1;
+    float v[E], res[E];
+    ldE(ys + row * LD + c0, v);
+    if (resid) ldE(rs + row * LD + c0, res);
+    float s = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      s += v[e];
+      s2 += v[e] * v[e];
+    }
+    s = row_sum(s);
+    s2 = row_sum(s2);
+    const float mean = s / (float)N, rstd = rstd_of(s, s2);
+    float out[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float t = (v[e] - mean) * (rstd * ga[e]) + be[e];
+      out[e] = resid ? fmaxf(res[e] + t, 0.f) : fmaxf(t, 0.f);
+    }
+    stE(xs + row * LD + c0, out);
+    if (resid) stE(rs + row * LD + c0, out);   // the next ResBlock's input
+    if (live) {
+      stEg((l + 1 < L ? a->X + (l + 1) * MN : a->out) + o, out);
+      stEg(a->z + l * MN + o, v);
+      if ((tid % TPR) == 0) a->stats[(size_t)(2 * l) * M + m] = mean, a->stats[(size_t)(2 * l + 1) * M + m] = rstd;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(NTH, 1) void k_rbstack_bwd(muz_rbstack_args) {
+#pragma clang fp contract(off)
+  const AS4 muz_rbstack_args* a = kernarg0<muz_rbstack_args>();
+  __shared__ __attribute__((aligned(16))) float dzs[R * LD];     // the current GEMM's input (an output gradient)
+  __shared__ __attribute__((aligned(16))) float dxs[R * LD];     // its output (the next row phase's dout)
+  __shared__ __attribute__((aligned(16))) float dres[R * LD];    // the ResBlock's residual gradient
+  __shared__ __attribute__((aligned(16))) float pgs[R * N];      // per-row do * xhat, do (column partials)
+  __shared__ __attribute__((aligned(16))) float pbs[R * N];
+  const int tid = threadIdx.x, M = a->M, L = 2 * a->nb;
+  const int row = tid / TPR, c0 = E * (tid % TPR), m = blockIdx.x * R + row;
+  const bool live = m < M;
+  const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
+  const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
+  const int tiles = (M + R - 1) / R;
+  {
+    float v[E] = {};
+    if (live) ldEg(a->g + o, v);
+    stE(dxs + row * LD + c0, v);
+  }
+  RowOpsRb ro;
+  load_rb_rows(a, L - 1, MN, o, m, live, c0, ro);
+  Ring rg;
+  rg.prime(a->wb[L - 1]);
+  __syncthreads();
+#pragma unroll 1
+  for (int l = L - 1; l >= 0; --l) {
+    // LayerNorm / ReLU backward of layer l (k_dense_ln_bwd's row half); odd l: the residual ReLU
+    const bool resid = l & 1;
+    float d[E];
+    ldE(dxs + row * LD + c0, d);
+    float xh[E], gg[E], sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (!(ro.out[e] > 0.f)) d[e] = 0.f;
+      xh[e] = (ro.z[e] - ro.ms[0]) * ro.ms[1];
+      gg[e] = d[e] * ro.ga[e];
+      sa += gg[e];
+      sb += gg[e] * xh[e];
+    }
+    if (resid) stE(dres + row * LD + c0, d);
+    sa = row_sum(sa) / (float)N;
+    sb = row_sum(sb) / (float)N;
+    float dz[E], pg[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      dz[e] = ro.ms[1] * (gg[e] - sa - xh[e] * sb);
+      pg[e] = d[e] * xh[e];
+    }
+    stE(dzs + row * LD + c0, dz);
+    stE(pgs + row * N + c0, pg);
+    stE(pbs + row * N + c0, d);
+    if (live) stEg(a->DZ + l * MN + o, dz);
+    __syncthreads();
+    // dx = dz W_l^T (+ the residual gradient after a ResBlock's first layer); the next layer's operands first
+    f4 acc[NT];
+    gemm(rg, dzs, acc);
+    if (l > 0) {
+      load_rb_rows(a, l - 1, MN, o, m, live, c0, ro);
+      rg.prime(a->wb[l - 1]);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int c = 16 * NT * w + 16 * t + 4 * lg;
+      f4 v = acc[t];
+      if (!resid) v += *reinterpret_cast<const f4*>(dres + li * LD + c);
+      *reinterpret_cast<f4*>(dxs + li * LD + c) = v;
+    }
+    partials(pgs, pbs, dzs, a->part + ((size_t)l * tiles + blockIdx.x) * 3 * N);
+    __syncthreads();
+  }
+  if (live) {
+    float v[E];
+    ldE(dxs + row * LD + c0, v);
+    stEg(a->dx + o, v);
+  }
+}
+
+static int check_rbstack(const muz_rbstack_args* a, bool bwd) {
+  MUZ_HOST_CHECK(a && a->nb >= 1 && a->nb <= MUZ_RBSTACK_MAX && a->M >= 0);
+  for (int l = 0; l < 2 * a->nb; ++l)
+    MUZ_HOST_CHECK(a->bias[l] && a->gamma[l] && a->beta[l] && (bwd ? a->wb[l] != nullptr : a->wf[l] != nullptr));
+  MUZ_HOST_CHECK(a->x && a->X && a->out && a->z && a->stats);
+  if (bwd) MUZ_HOST_CHECK(a->g && a->DZ && a->part && a->dx);
+  return MUZ_OK;
 }
 
 static int check_args(const muz_chain_args* a, bool bwd) {
@@ -587,6 +776,22 @@ int muz_trunk_chain_fwd(const muz_chain_args* args, void* stream) {
   if (rc) return rc;
   if (args->M == 0) return MUZ_OK;
   chain::k_chain_fwd<<<(args->M + chain::R - 1) / chain::R, chain::NTH, 0, (hipStream_t)stream>>>(*args);
+  return muz_last_launch_error();
+}
+
+int muz_rbstack_fwd(const muz_rbstack_args* args, void* stream) {
+  const int rc = chain::check_rbstack(args, false);
+  if (rc) return rc;
+  if (args->M == 0) return MUZ_OK;
+  chain::k_rbstack_fwd<<<(args->M + chain::R - 1) / chain::R, chain::NTH, 0, (hipStream_t)stream>>>(*args);
+  return muz_last_launch_error();
+}
+
+int muz_rbstack_bwd(const muz_rbstack_args* args, void* stream) {
+  const int rc = chain::check_rbstack(args, true);
+  if (rc) return rc;
+  if (args->M == 0) return MUZ_OK;
+  chain::k_rbstack_bwd<<<(args->M + chain::R - 1) / chain::R, chain::NTH, 0, (hipStream_t)stream>>>(*args);
   return muz_last_launch_error();
 }
 

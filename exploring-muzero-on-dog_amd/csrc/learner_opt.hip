@@ -27,7 +27,7 @@ namespace muz {
 constexpr int kAdamThreads = 256;
 constexpr int kAdamPerThread = 16;
 constexpr int kAdamChunk = kAdamThreads * kAdamPerThread;
-constexpr int kAdamMaxTensors = 40;
+constexpr int kAdamMaxTensors = 80;   // 80: the det learner's 156 tensors in 2 launches per pass (kernargs ~3.6 KB)
 constexpr int kAdamMaxBounds = 4;
 
 struct AdamTable {

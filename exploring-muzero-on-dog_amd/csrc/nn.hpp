@@ -213,6 +213,11 @@ __device__ __forceinline__ P tree_ld(const P* p) {
 #ifndef MUZ_RING_DEPTH
 #define MUZ_RING_DEPTH 2   // k-blocks of weights in flight ahead of the one being multiplied (2 or 3)
 #endif
+// 2: each output tile accumulates into two independent MFMA chains (even / odd k-steps, added at the end), so one
+// wave alone -- its SIMD partner waiting at a barrier -- can issue back to back; 1: one chain per tile
+#ifndef MUZ_ACC_CHAINS
+#define MUZ_ACC_CHAINS 1
+#endif
 
 template <int NT, bool AG>
 __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int KB, const float* A, int lda,
@@ -227,6 +232,9 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
     else return *reinterpret_cast<const f32x4*>(ap + kb * 16);
   };
   constexpr int D = MUZ_RING_DEPTH;
+  f32x4 accb[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) accb[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 a0 = lda4(0), a1 = a0;
   // step kb: issue k-block kb+D into `nxt` (the buffer consumed at step kb-1), read A of kb+1 from LDS,
   // multiply `cur` (= kb) with A of kb
@@ -245,7 +253,10 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma4(cur[t][j], a[j], acc[t]);   // D = W^T A^T
+      for (int t = 0; t < NT; ++t) {   // D = W^T A^T
+        if (MUZ_ACC_CHAINS == 2 && (j & 1)) accb[t] = mfma4(cur[t][j], a[j], accb[t]);
+        else acc[t] = mfma4(cur[t][j], a[j], acc[t]);
+      }
   };
   int kb = 0;
   if constexpr (D == 2) {
@@ -273,6 +284,10 @@ __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int
     if (kb < KB) step(kb, b0, b3, a0, a1);
     if (kb + 1 < KB) step(kb + 1, b1, b0, a1, a0);
     if (kb + 2 < KB) step(kb + 2, b2, b1, a0, a1);
+  }
+  if constexpr (MUZ_ACC_CHAINS == 2) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] += accb[t];
   }
 }
 

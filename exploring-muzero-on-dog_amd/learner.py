@@ -68,6 +68,105 @@ class _DenseLN(torch.autograd.Function):
         return dx, dW, db, dgamma, dbeta, dres, None, None
 
 
+class _ResBlockLN(torch.autograd.Function):
+    """relu(x + LN(Dense_1(relu(LN(Dense_0(x)))))): one ResBlock (muzero_deterministic_madn.py:12-24) as one
+    autograd node.  Forward = the two Dense + LayerNorm forwards of _DenseLN; backward = their two fused
+    LayerNorm-backward + input-gradient launches with the residual gradient accumulated inside the second
+    (dx = dz_0 W_0^T + dres) instead of a separate autograd add.  ``owners`` = the 8 leaf parameters for a
+    GradSink (Dense_0 kernel / bias, LayerNorm_0 scale / bias, then the same of the second layer)."""
+
+    @staticmethod
+    def forward(ctx, x, Wa, ba, ga, bea, Wb, bb, gb, beb, owners=None):
+        fa = _dense_ln_fwd(x, Wa, ba, ga, bea, None, LN_RELU)
+        fb = _dense_ln_fwd(fa[0], Wb, bb, gb, beb, x, LN_RESID_RELU)
+        ctx.save_for_backward(x, Wa, ga, Wb, gb, *fa, *fb)
+        ctx.owners = owners
+        return fb[0]
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, Wa, ga, Wb, gb = ctx.saved_tensors[:5]
+        fa, fb = ctx.saved_tensors[5:9], ctx.saved_tensors[9:13]
+        M, Nn = fb[0].shape
+        dev, dt = dout.device, dout.dtype
+        sa = torch.empty((_ln_scratch_floats(M, Nn, x.shape[1]),), dtype=dt, device=dev)
+        sb = torch.empty((_ln_scratch_floats(M, Nn, Nn),), dtype=dt, device=dev)
+        dzb, dres, t = _dense_ln_bwd(dout, fb, gb, LN_RESID_RELU, Wb, sb)
+        dza, _, dx = _dense_ln_bwd(t, fa, ga, LN_RELU, Wa, sa, acc=dres)
+        sink = _sink()
+        if sink is not None and ctx.owners is not None:
+            o = ctx.owners
+            sink.ln_colsum(sa, Nn, o[2], o[3], o[1])
+            sink.wgrad(x, dza, o[0])
+            sink.ln_colsum(sb, Nn, o[6], o[7], o[5])
+            sink.wgrad(fa[0], dzb, o[4])
+            return (dx,) + (None,) * 9
+        grads = []
+        for inp, dz, s in ((x, dza, sa), (fa[0], dzb, sb)):
+            dg, dbe, db = _ln_colsum(s, Nn)
+            grads += [inp.t() @ dz, db, dg, dbe]
+        return (dx, *grads, None)
+
+
+class _ResStack(torch.autograd.Function):
+    """nb consecutive ResBlocks (the representation's six at the batch's rows, the prediction's two at all unroll
+    steps' rows) as ONE launch each way: csrc/learner_chain.hip's muz_rbstack_fwd / _bwd, 16 rows per workgroup
+    carried through every layer, the weights streamed packed (muz_trunk_chain_pack, per call).  The forward
+    saves what _ResBlockLN's per-layer launches save; the parameter gradients go to the GradSink (or one GEMM /
+    column sum each).  P = the 8 parameters of each block in _ResBlockLN's order; ``owners`` = the same leaves."""
+
+    @staticmethod
+    def forward(ctx, x, owners, *P):
+        nb, (M, Nn) = len(P) // 8, x.shape
+        L2 = 2 * nb
+        dev, dt = x.device, x.dtype
+        lib = _L.load()
+        W = [P[8 * b + 4 * k] for b in range(nb) for k in range(2)]
+        WP = torch.empty((2, L2, Nn * Nn), dtype=dt, device=dev)
+        src = (ctypes.c_void_p * L2)(*[w.data_ptr() for w in W])
+        _L.check(lib.muz_trunk_chain_pack(src, L2, _L.ptr(WP[0]), _L.ptr(WP[1]), _L.stream_ptr()), "muz_trunk_chain_pack")
+        X = torch.empty((L2, M, Nn), dtype=dt, device=dev)
+        out = torch.empty((M, Nn), dtype=dt, device=dev)
+        z = torch.empty((L2, M, Nn), dtype=dt, device=dev)
+        stats = torch.empty((L2, 2, M), dtype=dt, device=dev)
+        a = _L.MuzRbstackArgs()
+        a.nb, a.M = nb, M
+        for l in range(L2):
+            b, k = divmod(l, 2)
+            a.wf[l], a.wb[l] = WP[0, l].data_ptr(), WP[1, l].data_ptr()
+            a.bias[l], a.gamma[l], a.beta[l] = (P[8 * b + 4 * k + i].data_ptr() for i in (1, 2, 3))
+        a.x, a.X, a.out, a.z, a.stats = x.data_ptr(), X.data_ptr(), out.data_ptr(), z.data_ptr(), stats.data_ptr()
+        _L.check(lib.muz_rbstack_fwd(ctypes.byref(a), _L.stream_ptr()), "muz_rbstack_fwd")
+        ctx.args, ctx.keep, ctx.X, ctx.P, ctx.owners = a, (WP, x, out, z, stats), X, P, owners
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        a, X, P = ctx.args, ctx.X, ctx.P
+        L2, M, Nn = X.shape
+        dev, dt = dout.device, dout.dtype
+        tiles = (M + 15) // 16
+        DZ = torch.empty((L2, M, Nn), dtype=dt, device=dev)
+        part = torch.empty((L2, tiles * 3 * Nn), dtype=dt, device=dev)
+        dx = torch.empty((M, Nn), dtype=dt, device=dev)
+        dout = dout.contiguous()
+        a.g, a.DZ, a.part, a.dx = dout.data_ptr(), DZ.data_ptr(), part.data_ptr(), dx.data_ptr()
+        _L.check(_L.load().muz_rbstack_bwd(ctypes.byref(a), _L.stream_ptr()), "muz_rbstack_bwd")
+        ctx.keep = None
+        sink, o = _sink(), ctx.owners
+        if sink is not None and o is not None:
+            for l in range(L2):
+                Wl, bl, gl, bel = o[4 * l:4 * l + 4]
+                sink.ln_colsum(part[l], Nn, gl, bel, bl)
+                sink.wgrad(X[l], DZ[l], Wl)
+            return (dx, None) + (None,) * len(P)
+        grads = []
+        for l in range(L2):
+            dg, dbe, db = _ln_colsum(part[l], Nn)
+            grads += [X[l].t() @ DZ[l], db, dg, dbe]
+        return (dx, None, *grads)
+
+
 _ONES = {}
 
 
@@ -190,6 +289,8 @@ def _ln_fwd(y, bias, gamma, beta, res, mode, out=None):
 FUSED_FWD = False
 FUSED_BWD = True
 FUSED_DENSE = True   # False: neither (A/B timing)
+RESBLOCK_NODE = True  # False: a ResBlock as two _DenseLN nodes + autograd's residual add (A/B timing)
+RESBLOCK_STACK = True  # False: consecutive ResBlocks as one node each instead of one _ResStack (A/B timing)
 
 
 def _fusable(K, Nn, fwd=False):
@@ -823,7 +924,23 @@ class MuZeroNets:
         xp = F.pad(x, (0, 0, pl, K - 1 - pl))
         return torch.cat([xp[:, d:d + W, :] for d in range(K)], dim=-1), k.reshape(K * Cin, Cout)
 
+    def _rbs(self, name, nb, x):
+        """ResBlocks name0 .. name{nb-1} in sequence: one _ResStack node on the GPU (RESBLOCK_STACK)."""
+        if x.is_cuda and RESBLOCK_STACK and x.shape[-1] == 256 and 1 <= nb <= _L.MUZ_RBSTACK_MAX:
+            own = tuple(self.p[f"{name}{b}/{n}"] for b in range(nb) for n in _RB_PARAMS)
+            out = _ResStack.apply(x.reshape(-1, x.shape[-1]).contiguous(), own, *own)
+            return out.reshape(x.shape)
+        for b in range(nb):
+            x = self._rb(f"{name}{b}", x)
+        return x
+
     def _rb(self, name, x):
+        if x.is_cuda and RESBLOCK_NODE:
+            own = tuple(self.p[f"{name}/{n}"] for n in ("Dense_0/kernel", "Dense_0/bias", "LayerNorm_0/scale",
+                                                        "LayerNorm_0/bias", "Dense_1/kernel", "Dense_1/bias",
+                                                        "LayerNorm_1/scale", "LayerNorm_1/bias"))
+            out = _ResBlockLN.apply(x.reshape(-1, x.shape[-1]).contiguous(), *own, own)
+            return out.reshape(x.shape)
         y = self._dense_ln(f"{name}/Dense_0", f"{name}/LayerNorm_0", x, LN_RELU)
         return self._dense_ln(f"{name}/Dense_1", f"{name}/LayerNorm_1", y, LN_RESID_RELU, res=x)
 
@@ -846,8 +963,7 @@ class MuZeroNets:
         g = self._dense_ln(f"{r}/Dense_1", f"{r}/LayerNorm_4", g)
         g = self._dense_ln(f"{r}/Dense_2", f"{r}/LayerNorm_5", g)
         h = self._dense_ln(f"{r}/Dense_3", f"{r}/LayerNorm_6", torch.cat([flat, g], -1))
-        for b in range(6):
-            h = self._rb(f"{r}/ResBlock_{b}", h)
+        h = self._rbs(f"{r}/ResBlock_", 6, h)
         if h.is_cuda and h.shape[-1] == 256 and self.p[f"{r}/Dense_4/kernel"].shape[1] == 256:
             return _DenseMinmax.apply(h.contiguous(), self.p[f"{r}/Dense_4/kernel"], self.p[f"{r}/Dense_4/bias"])
         return self._minmax(self._dense(f"{r}/Dense_4", h))
@@ -888,8 +1004,7 @@ class MuZeroNets:
     def prediction(self, latent):
         p = "prediction"
         x = self._ln(f"{p}/LayerNorm_0", latent)
-        for b in range(2):
-            x = self._rb(f"{p}/ResBlock_{b}", x)
+        x = self._rbs(f"{p}/ResBlock_", 2, x)
         pol = self._dense_ln(f"{p}/Dense_0", f"{p}/LayerNorm_1", x)
         pol = self._dense_ln(f"{p}/Dense_1", f"{p}/LayerNorm_2", pol)
         logits = self._dense(f"{p}/Dense_2", pol)

@@ -63,6 +63,17 @@ class MuzChainArgs(ctypes.Structure):
                 ("dshift", vp), ("dlatent0", vp)]
 
 
+MUZ_RBSTACK_MAX = 6
+
+
+class MuzRbstackArgs(ctypes.Structure):
+    """muz_rbstack_args (include/muz.h): a stack of ResBlocks for muz_rbstack_fwd / _bwd."""
+    _L = 2 * MUZ_RBSTACK_MAX
+    _fields_ = [("nb", ctypes.c_int32), ("M", ctypes.c_int32), ("wf", vp * _L), ("wb", vp * _L), ("bias", vp * _L),
+                ("gamma", vp * _L), ("beta", vp * _L), ("x", vp), ("X", vp), ("out", vp), ("z", vp), ("stats", vp),
+                ("g", vp), ("DZ", vp), ("part", vp), ("dx", vp)]
+
+
 class MuzLossTerm(ctypes.Structure):
     _fields_ = [("logits", vp), ("dlogits", vp), ("labels", vp), ("probs", vp), ("ncls", ctypes.c_int32),
                 ("ld", ctypes.c_int32), ("rare_not_one", ctypes.c_int32), ("w_rare", ctypes.c_float),
@@ -356,6 +367,8 @@ SIGNATURES = {
                                         ctypes.c_int32, vp, vp, vp, vp, vp, vp]),
     "muz_trunk_chain_pack": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp]),
     "muz_trunk_chain_fwd": (ctypes.c_int, [ctypes.POINTER(MuzChainArgs), vp]),
+    "muz_rbstack_fwd": (ctypes.c_int, [ctypes.POINTER(MuzRbstackArgs), vp]),
+    "muz_rbstack_bwd": (ctypes.c_int, [ctypes.POINTER(MuzRbstackArgs), vp]),
     "muz_trunk_chain_bwd": (ctypes.c_int, [ctypes.POINTER(MuzChainArgs), vp]),
     "muz_adamw_scratch_bytes": (ctypes.c_int64, [ctypes.c_int32, vp]),
     "muz_adamw_step": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_double,

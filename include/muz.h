@@ -854,6 +854,33 @@ typedef struct {
 int muz_trunk_chain_pack(const float* const* W, int32_t count, float* fwd, float* bwd, void* stream);
 int muz_trunk_chain_fwd(const muz_chain_args* args, void* stream);
 int muz_trunk_chain_bwd(const muz_chain_args* args, void* stream);
+/* A stack of nb ResBlocks (relu(x + LN(Dense_1(relu(LN(Dense_0(x))))))), muzero_deterministic_madn.py:12-24: the
+ * representation's six and the prediction's two, as trained by train_with_reward.py) as ONE launch each way
+ * (csrc/learner_chain.hip, the chain kernels' 16-row tiles and GEMM loop).  Weight layer l = 2 b + k (block b,
+ * its Dense_k), all widths 256, weights packed by muz_trunk_chain_pack.  Forward writes X[l] (the input of weight
+ * layer l; X[0] = x), out, z (pre-LayerNorm y + bias) and stats (mean, rstd).  Backward (reads what the forward
+ * wrote) writes DZ[l] (the output gradient of weight layer l), the column partials part[l] [ceil(M / 16)][3][256]
+ * (muz_ln_colsum layout) and dx. */
+#define MUZ_RBSTACK_MAX 6
+typedef struct {
+  int32_t nb, M;
+  const float* wf[2 * MUZ_RBSTACK_MAX];
+  const float* wb[2 * MUZ_RBSTACK_MAX];
+  const float* bias[2 * MUZ_RBSTACK_MAX];
+  const float* gamma[2 * MUZ_RBSTACK_MAX];
+  const float* beta[2 * MUZ_RBSTACK_MAX];
+  const float* x;          /* [M][256] */
+  float* X;                /* [2 nb][M][256] */
+  float* out;              /* [M][256] */
+  float* z;                /* [2 nb][M][256] */
+  float* stats;            /* [2 nb][2][M] */
+  const float* g;          /* backward: d out [M][256] */
+  float* DZ;               /* [2 nb][M][256] */
+  float* part;             /* [2 nb][ceil(M / 16)][3][256] */
+  float* dx;               /* [M][256] */
+} muz_rbstack_args;
+int muz_rbstack_fwd(const muz_rbstack_args* args, void* stream);
+int muz_rbstack_bwd(const muz_rbstack_args* args, void* stream);
 /* 'SAME' Conv1D as a GEMM: the im2col matrix cols [B][W][K x Cin] of x [B][W][Cin] (zero outside each row;
  * tap d reads column w + d - (K - 1) / 2) and its backward dx = sum over taps (fixed order). */
 int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream);

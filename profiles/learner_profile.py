@@ -50,6 +50,14 @@ lr0 = L.Learner(params, C, unroll_steps=10, graph=True)
 timed("train_step (graph replay, fixed batch, chain kernel off)", lambda: lr0.train_step(batch))
 L.CHAIN_KERNEL = True
 del lr0
+L.RESBLOCK_STACK = False
+lr0 = L.Learner(params, C, unroll_steps=10, graph=True)
+timed("train_step (graph replay, fixed batch, ResBlock stack kernel off)", lambda: lr0.train_step(batch))
+L.RESBLOCK_NODE = False
+lr0 = L.Learner(params, C, unroll_steps=10, graph=True)
+timed("train_step (graph replay, fixed batch, ResBlock stack kernel and node off)", lambda: lr0.train_step(batch))
+L.RESBLOCK_NODE = L.RESBLOCK_STACK = True
+del lr0
 lr = L.Learner(params, C, unroll_steps=10, graph=True)
 timed("sample_batch", ring.sample_batch)
 timed("train_step (graph replay, fixed batch)", lambda: lr.train_step(batch))

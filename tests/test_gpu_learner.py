@@ -383,6 +383,59 @@ def test_chain_kernel_matches_layer_path(cuda, kind, B, K):
         assert err < 1e-5, f"{n}: relative gradient difference {err:.2e}"
 
 
+@pytest.mark.parametrize("nb,M", [(6, 128), (2, 1408), (2, 37)])
+def test_rbstack_kernel_matches_layer_path(cuda, nb, M):
+    """csrc/learner_chain.hip's ResBlock stack (muz_rbstack_fwd / _bwd: nb ResBlocks in one launch each way; the
+    representation's six at batch 128, the prediction's two at 11 x 128 rows, a ragged batch) against the per-layer
+    launches (_dense_ln_fwd / _dense_ln_bwd, library GEMMs).  Forward: output within 1e-5.  Backward: the per-layer
+    backward fed the stack's saved forward values (ReLU masks must agree -- see test_chain_kernel_matches_layer_path),
+    dx and every parameter gradient within 1e-5 relative to its largest entry."""
+    import types
+    _, _, L, _, _ = _mods()
+    g = torch.Generator().manual_seed(7 + M)
+    P = []
+    for _ in range(nb):
+        for _ in range(2):
+            P += [torch.randn(256, 256, generator=g) / 16, 0.1 * torch.randn(256, generator=g),
+                  1 + 0.2 * torch.randn(256, generator=g), 0.1 * torch.randn(256, generator=g)]
+    P = [p.cuda() for p in P]
+    x = torch.relu(torch.randn(M, 256, generator=g)).cuda()
+    dout = torch.randn(M, 256, generator=g).cuda()
+    with torch.no_grad():
+        ref, fs = x, []
+        for b in range(nb):
+            Wa, ba, ga, bea, Wb, bb, gb, beb = P[8 * b:8 * b + 8]
+            fa = L._dense_ln_fwd(ref, Wa, ba, ga, bea, None, L.LN_RELU)
+            fb = L._dense_ln_fwd(fa[0], Wb, bb, gb, beb, ref, L.LN_RESID_RELU)
+            fs.append((ref, fa, fb))
+            ref = fb[0]
+        ctx = types.SimpleNamespace()
+        out = L._ResStack.forward(ctx, x, None, *P)
+        X, (WP, _, _, z, stats) = ctx.X, ctx.keep
+        torch.cuda.synchronize()
+        err = (out - ref).abs().max().item()
+        assert err < 1e-5, f"forward differs by {err:.2e}"
+        # the per-layer backward on the stack's saved values
+        f = [((X[l + 1] if l + 1 < 2 * nb else out), z[l], stats[l, 0], stats[l, 1]) for l in range(2 * nb)]
+        d, want = dout, [None] * len(P)
+        for b in range(nb - 1, -1, -1):
+            Wa, ba, ga, bea, Wb, bb, gb, beb = P[8 * b:8 * b + 8]
+            sb = torch.empty((L._ln_scratch_floats(M, 256, 256),), device="cuda")
+            sa = torch.empty_like(sb)
+            dzb, dres, t = L._dense_ln_bwd(d, f[2 * b + 1], gb, L.LN_RESID_RELU, Wb, sb)
+            dza, _, d = L._dense_ln_bwd(t, f[2 * b], ga, L.LN_RELU, Wa, sa, acc=dres)
+            for k, (dz, s, inp) in enumerate(((dza, sa, X[2 * b]), (dzb, sb, X[2 * b + 1]))):
+                dg, dbe, dbias = L._ln_colsum(s, 256)
+                want[8 * b + 4 * k:8 * b + 4 * k + 4] = [inp.t() @ dz, dbias, dg, dbe]
+        got = L._ResStack.backward(ctx, dout)
+        torch.cuda.synchronize()
+    err = (got[0] - d).abs().max().item() / max(1e-3, d.abs().max().item())
+    assert err < 1e-5, f"dx: relative difference {err:.2e}"
+    for i, (a, b) in enumerate(zip(got[2:], want)):
+        err = (a - b).abs().max().item() / max(1e-3, b.abs().max().item())
+        assert err < 1e-5, f"parameter {i}: relative gradient difference {err:.2e}"
+
+
 def test_chain_kernel_host_checks(cuda):
     """muz_trunk_chain_fwd / _bwd reject what the kernels do not implement (before any launch)."""
     from exploring_muzero_on_dog_amd import lib as _L
@@ -395,6 +448,10 @@ def test_chain_kernel_host_checks(cuda):
     assert lib.muz_trunk_chain_bwd(ctypes.byref(a), _L.stream_ptr()) == _L.MUZ_E_INVALID
     src = (ctypes.c_void_p * 1)(None)
     assert lib.muz_trunk_chain_pack(src, 1, None, None, _L.stream_ptr()) == _L.MUZ_E_INVALID
+    r = _L.MuzRbstackArgs()
+    assert lib.muz_rbstack_fwd(ctypes.byref(r), _L.stream_ptr()) == _L.MUZ_E_INVALID          # nb = 0, nulls
+    r.nb, r.M = _L.MUZ_RBSTACK_MAX + 1, 16
+    assert lib.muz_rbstack_bwd(ctypes.byref(r), _L.stream_ptr()) == _L.MUZ_E_INVALID
 
 
 def test_dynamics_chain_node_matches_per_step_autograd(cuda):

@@ -153,6 +153,38 @@ def test_det_sink_gradients_equal_per_op_gradients(cuda):
              _grads(L.Learner, params, C, batch, True))
 
 
+def test_resblock_node_gradients_bit_identical(cuda):
+    """learner.RESBLOCK_NODE (a ResBlock's two fused Dense + LayerNorm layers as one autograd node whose backward adds
+    the residual gradient inside the second launch, dx = dz_0 W_0^T + dres) leaves the det step's loss and every
+    parameter gradient bit-identical to two _DenseLN nodes and autograd's separate add (the same kernels, and fp32
+    addition commutes); grouped (GradSink) and per-parameter gradients alike."""
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import game_agent as GA
+    from exploring_muzero_on_dog_amd import learner as L
+    from exploring_muzero_on_dog_amd import nets as N
+    from exploring_muzero_on_dog_amd import replay as R
+    from oracle import nets as ON
+    C = E.num_channels(4)
+    params = ON.init_params(C, seed=14, randomize_affine=True)
+    eng = GA.SelfPlayEngine(N.DeviceNet(params, C), 32, num_players=4, max_steps=120, num_simulations=4, max_depth=4)
+    ring = R.VectorizedReplayBuffer(512, 48, 5, 10, obs_shape=(C, 56), max_episode_length=120,
+                                    rng=np.random.RandomState(3))
+    ring.save_games_from_buffers(eng.play_stream(40, seed=3, temperature=1.0))
+    batch = ring.sample_batch()
+    for grouped in (True, False):
+        res = []
+        for node in (True, False):
+            L.RESBLOCK_NODE, L.RESBLOCK_STACK = node, False    # (the stack kernel would take the ResBlocks)
+            try:
+                res.append(_grads(L.Learner, params, C, batch, grouped))
+            finally:
+                L.RESBLOCK_NODE, L.RESBLOCK_STACK = True, True
+        (la, ga), (lb, gb) = res
+        assert la == lb
+        for k in ga:
+            assert torch.equal(ga[k], gb[k]), (grouped, k)
+
+
 def test_classic_sink_gradients_equal_per_op_gradients(cuda):
     from exploring_muzero_on_dog_amd import classic as CL
     from exploring_muzero_on_dog_amd import game_agent_stochastic as GS
