@@ -47,10 +47,17 @@ def test_det_test_training_tiny(cuda, tmp_path):
         tl, tv = opt_state.learner.nets.prediction(te)
     assert max((e - te).abs().max().item(), (lg - tl).abs().max().item(), (v - tv[:, 0]).abs().max().item()) < 2e-5
     saved = {k: v.detach().cpu().numpy().copy() for k, v in T.CK.muzero_tree_to_flat_any(params).items()}
-    # a further train step changes the live tensors; as_device_net re-packs (content fingerprint)
+    # a further train step changes the live tensors; as_device_net re-packs them (versioned tree) into the cached
+    # DeviceNet in place (same shapes), so engines cached on it see the new weights
     params, opt_state, _ = T.train_step_from(params, opt_state, T.run_training.last["replay"])
     net2 = N.as_device_net(params)
-    assert net2 is not net
+    lg2, v2, e2 = N.root_inference_fn(net2, obs)
+    with torch.no_grad():
+        te2 = opt_state.learner.nets.representation(obs)
+        tl2, tv2 = opt_state.learner.nets.prediction(te2)
+    assert max((e2 - te2).abs().max().item(), (lg2 - tl2).abs().max().item(),
+               (v2 - tv2[:, 0]).abs().max().item()) < 2e-5
+    assert (lg2 - lg).abs().max().item() > 0
     # the checkpoint of the last iteration (train_with_reward.py:301-307 cadence, here every iteration) holds
     # the parameters and Adam state of that moment
     pp, op = TW._checkpoint_names(cfg, 2)
