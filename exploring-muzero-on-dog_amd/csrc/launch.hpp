@@ -24,6 +24,11 @@ int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int
 int launch_root_inference(const muz_classic_net_w& w, const float* obs, int n, const int* n_dev, float* conv_scratch,
                           float* logits, float* value, float* emb, hipStream_t s);
 
+// k_repr_conv (RepresentationNetwork2's convolutions, nets.hip) and k_film (the per-action FiLM table)
+int launch_repr_conv(const muz_repr_w& r, const float* obs, int C, int n, const int* n_dev, float* conv,
+                     hipStream_t s);
+int launch_film(const muz_dyn_w& d, int A, hipStream_t s);
+
 int launch_gumbel_search(const muz_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,
                          const float* root_emb, const uint32_t* legal, const float* gumbel, const int32_t* game_id,
                          int n, const int* n_dev, void* workspace, int32_t* action, float* weights, float* value,

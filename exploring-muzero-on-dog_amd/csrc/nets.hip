@@ -131,37 +131,13 @@ __global__ __launch_bounds__(kThreads) void k_root_dense(NW Wt, const float* __r
   __shared__ __attribute__((aligned(16))) float smem[kArenaFloats];
   const Arena a = Arena::carve(smem);
   const AS4 NW* W = kernarg0<NW>();   // == Wt, read through the kernarg segment
-  const AS4 muz_repr_w& R = W->repr;
-  const int C = Wt.obs_channels, A = Wt.num_actions;
+  const int A = Wt.num_actions;
   const int g0 = blockIdx.x * kRows;
   const int row = trow(), sub = tsub();
   const int gr = g0 + row;
   const bool valid = gr < n;
-  // global stream input: x[:, 6:, 0]
-  const int Kg = C - 6;
-  if (sub < 32) a.E[row * LDE + sub] = (valid && sub < Kg) ? obs[((size_t)gr * C + 6 + sub) * 56] : 0.f;
-  // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16)
   Pf pf;
-  pf_issue<NT256>(pf, &R.d0, 3584, LAT);
-  dense16<NT256, NT64>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW, pf, &R.d1, Kg, 64, true);
-  __syncthreads();
-  ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, R.ln3);
-  dense16<NT64, NT64>(R.d1, Kg, 64, a.E, LDE, a.X, LD, pf, &R.d2, 64, 64);
-  __syncthreads();
-  ln16<64, LN_RELU>(a.X, LD, a.X, LD, R.ln4);
-  __syncthreads();
-  dense16<NT64, NT256>(R.d2, 64, 64, a.X, LD, a.W + 256, LDW, pf, &R.d3, 320, LAT);
-  __syncthreads();
-  ln16<64, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, R.ln5);
-  __syncthreads();
-  dense16<NT256, NT256>(R.d3, 320, LAT, a.W, LDW, a.X, LD, pf, &R.rb[0].d0, LAT, LAT);
-  __syncthreads();
-  ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, R.ln6);
-  __syncthreads();
-#pragma unroll 1
-  for (int b = 0; b < 6; ++b)
-    resblock16<NT256>(R.rb[b], a.X, a.T, a.U, pf, b < 5 ? &R.rb[b + 1].d0 : &R.d4, LAT, LAT);
-  dense16<NT256, NT256>(R.d4, LAT, LAT, a.X, LD, a.T, LD, pf, &W->pred.rb[0].d0, LAT, LAT);
+  repr16<NT256>(W->repr, obs, Wt.obs_channels, convout, g0, n, a, pf, &W->pred.rb[0].d0, LAT, LAT);
   __syncthreads();
   minmax16(a.T, LD);
   __syncthreads();
@@ -233,11 +209,21 @@ int check_net(const muz_net_w* w) {
   return MUZ_OK;
 }
 
+int launch_repr_conv(const muz_repr_w& r, const float* obs, int C, int n, const int* n_dev, float* conv,
+                     hipStream_t s) {
+  k_repr_conv<<<n, 256, 0, s>>>(r, obs, C, n, n_dev, conv);
+  return muz_last_launch_error();
+}
+
+int launch_film(const muz_dyn_w& d, int A, hipStream_t s) {
+  k_film<<<A + 1, 512, 0, s>>>(d, A);
+  return muz_last_launch_error();
+}
+
 template <class NW>
 static int launch_root_impl(const NW& w, const float* obs, int n, const int* n_dev, float* conv, float* logits,
                             float* value, float* emb, hipStream_t s) {
-  k_repr_conv<<<n, 256, 0, s>>>(w.repr, obs, w.obs_channels, n, n_dev, conv);
-  int rc = muz_last_launch_error();
+  int rc = launch_repr_conv(w.repr, obs, w.obs_channels, n, n_dev, conv, s);
   if (rc) return rc;
   k_root_dense<NW><<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, obs, conv, n, n_dev, logits, value, emb);
   return muz_last_launch_error();

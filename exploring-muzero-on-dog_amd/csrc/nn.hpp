@@ -791,10 +791,16 @@ __device__ __forceinline__ float softmax3_support(float l0, float l1, float l2) 
 // discount support values in a.v1 / a.v2 like dyn16.
 // SPLITK_LOGITS: the policy logits by logits16_splitk (partials in a.W, summed per lane at the end into a.U; a
 // caller reads a.U[row][c] only from lane (row, c), as all of them do).
-template <int NTN, bool LN0_DONE = false, bool LATE_HEADS = false, bool SPLITK_LOGITS = false>
+// NO_LOGITS (DOG, A = 806 does not fit a [16][LD] buffer): stop before the policy logits and leave the policy
+// hidden layer in a.T; P.d2 is then the first logits chunk (NTL tiles per wave, 256 columns), whose first k-blocks
+// pf holds on exit (dog_logits16 runs the chunks).  Ln / Kn / Nn are unused then.
+template <int NTN, bool LN0_DONE = false, bool LATE_HEADS = false, bool SPLITK_LOGITS = false, int NTL = NTA,
+          bool NO_LOGITS = false>
 __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const float* lat, const Arena& a, Pf& pf,
                                        const AS4 muz_dense* Ln, int Kn, int Nn, const AS4 muz_dyn_w* D = nullptr,
                                        int ar = 0) {
+  static_assert(!(NO_LOGITS && SPLITK_LOGITS), "split-K logits need the whole logits layer");
+  const int nl = NO_LOGITS ? 256 : A;   // columns of the layer after value Dense_4 (its prefetch)
   if constexpr (!LN0_DONE) {
     ln16<LAT, LN_PLAIN>(lat, LD, a.X, LD, P.ln0);
     SYNC();
@@ -828,7 +834,7 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
       }
     }
     dense16<NT128, NT64>(D->d67, LAT, 128, a.L, LD, a.U, LD, pf, &P.d4, 128, 64);   // [reward | discount] hidden
-    dense16<NT64, NTA>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, A, false,
+    dense16<NT64, NTL>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, nl, false,
                        SPLITK_LOGITS);                                              // value Dense_4 (X is free)
     SYNC();
     ln16<128, LN_RELU>(a.T, LD, a.T, LD, p2);
@@ -845,7 +851,7 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
     }
   } else {
     dense16<NT128, NT64>(P.d1, LAT, 128, a.W, LDW, a.T, LD, pf, &P.d4, 128, 64);     // policy Dense_1
-    dense16<NT64, NTA>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, A, false,
+    dense16<NT64, NTL>(P.d4, 128, 64, a.W + 256, LDW, a.X, LD, pf, &P.d2, 128, nl, false,
                        SPLITK_LOGITS);                                              // value Dense_4 (X is free)
     SYNC();
     ln16<128, LN_RELU>(a.T, LD, a.T, LD, p2);
@@ -853,10 +859,13 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
   }
   ST(ST_PASS);
   SYNC();
-  if constexpr (SPLITK_LOGITS)
+  if constexpr (NO_LOGITS) {
+    // (the logits chunks follow in the caller; pf keeps chunk 0's k-blocks)
+  } else if constexpr (SPLITK_LOGITS) {
     logits16_splitk<NTN>(128, a.T, LD, a.W, pf, Ln, Kn, Nn);                  // policy logits, split over k
-  else
+  } else {
     dense16<NTA, NTN>(P.d2, 128, A, a.T, LD, a.U, LD, pf, Ln, Kn, Nn);         // policy logits
+  }
   {
     const float v = head_dot(a.X, LD, hv, 0);
     if (tsub() == 0) a.v0[trow()] = tanhf(v);
@@ -866,6 +875,44 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
   if constexpr (SPLITK_LOGITS) {
     if (tsub() < A) a.U[trow() * LD + tsub()] = logits16_splitk_sum(P.d2, 128, a.W);
   }
+}
+
+// RepresentationNetwork2's dense part on the tile (muzero_deterministic_madn.py:105-138; the DOG
+// RepresentationNetwork, MuZero_DOG/muzero_dog.py:51-80, is the same): Dense_0 over the flattened conv maps of
+// games g0.. (convout, global memory, rows padded to a multiple of 16), the global stream x[:, 6:, 0], the concat,
+// 6 ResBlocks and Dense_4 into a.T -- the head (min-max / LayerNorm) is the caller's.  pf: on exit Ln's first
+// k-blocks.  Ends without a barrier after Dense_4.
+template <int NTN>
+__device__ __forceinline__ void repr16(const AS4 muz_repr_w& R, const float* __restrict__ obs, int C,
+                                       const float* __restrict__ convout, int g0, int n, const Arena& a, Pf& pf,
+                                       const AS4 muz_dense* Ln, int Kn, int Nn) {
+  const int row = trow(), sub = tsub();
+  const int gr = g0 + row;
+  const bool valid = gr < n;
+  // global stream input: x[:, 6:, 0]
+  const int Kg = C - 6;
+  if (sub < 32) a.E[row * LDE + sub] = (valid && sub < Kg) ? obs[((size_t)gr * C + 6 + sub) * 56] : 0.f;
+  // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16)
+  pf_issue<NT256>(pf, &R.d0, 3584, LAT);
+  dense16<NT256, NT64>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW, pf, &R.d1, Kg, 64, true);
+  __syncthreads();
+  ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, R.ln3);
+  dense16<NT64, NT64>(R.d1, Kg, 64, a.E, LDE, a.X, LD, pf, &R.d2, 64, 64);
+  __syncthreads();
+  ln16<64, LN_RELU>(a.X, LD, a.X, LD, R.ln4);
+  __syncthreads();
+  dense16<NT64, NT256>(R.d2, 64, 64, a.X, LD, a.W + 256, LDW, pf, &R.d3, 320, LAT);
+  __syncthreads();
+  ln16<64, LN_RELU>(a.W + 256, LDW, a.W + 256, LDW, R.ln5);
+  __syncthreads();
+  dense16<NT256, NT256>(R.d3, 320, LAT, a.W, LDW, a.X, LD, pf, &R.rb[0].d0, LAT, LAT);
+  __syncthreads();
+  ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, R.ln6);
+  __syncthreads();
+#pragma unroll 1
+  for (int b = 0; b < 6; ++b)
+    resblock16<NT256>(R.rb[b], a.X, a.T, a.U, pf, b < 5 ? &R.rb[b + 1].d0 : &R.d4, LAT, LAT);
+  dense16<NT256, NTN>(R.d4, LAT, LAT, a.X, LD, a.T, LD, pf, Ln, Kn, Nn);
 }
 
 // Dyn4 inputs of this thread's row, loaded as soon as the parent node and action are known (end of the

@@ -186,6 +186,11 @@ class MuzNetW(ctypes.Structure):
 
 
 
+class MuzDogNetW(ctypes.Structure):
+    _fields_ = [("obs_channels", ctypes.c_int32), ("num_actions", ctypes.c_int32), ("repr", MuzReprW),
+                ("repr_ln7", MuzLn), ("dyn", MuzDynW), ("pred", MuzPredW), ("logits", MuzDense * 4)]
+
+
 class MuzSdynW(ctypes.Structure):
     _fields_ = [("act_embed", MuzDense), ("act_input_ln", MuzLn), ("act_film", MuzDense), ("act_dense1", MuzDense),
                 ("act_ln1", MuzLn), ("act_dense2", MuzDense), ("act_ln2", MuzLn), ("act_rb", MuzResblock * 2),
@@ -374,6 +379,15 @@ SIGNATURES = {
     "muz_adamw_step": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_double,
                                       ctypes.c_double, ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double,
                                       vp, ctypes.c_int32, vp]),
+    "muz_dog_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzDogNetW), vp]),
+    "muz_dog_encode": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_int32, vp]),
+    "muz_dog_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzDogNetW), vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp,
+                                         vp, vp]),
+    "muz_dog_nets_recurrent": (ctypes.c_int, [ctypes.POINTER(MuzDogNetW), vp, vp, ctypes.c_int32, vp, vp, vp, vp,
+                                              vp, vp]),
+    "muz_dog_search_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.POINTER(MuzSearchCfg)]),
+    "muz_dog_gumbel_search": (ctypes.c_int, [ctypes.POINTER(MuzDogNetW), ctypes.POINTER(MuzSearchCfg), vp, vp, vp,
+                                             vp, vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp, vp]),
     "muz_detmadn_selfplay_stream": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzNetW),
                                                    ctypes.POINTER(MuzSearchCfg), MuzDetSoA, MuzTraj, ctypes.c_int32,
                                                    ctypes.c_int32, vp, ctypes.c_int64, ctypes.POINTER(MuzSpStats),

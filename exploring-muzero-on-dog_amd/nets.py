@@ -164,6 +164,23 @@ class _Packer:
             d2=self._dense(f"{p}/Dense_2"), ln3=self._ln(f"{p}/LayerNorm_3"), d4=self._dense(f"{p}/Dense_4"),
             d5=self._plain(f"{p}/Dense_5"))
 
+    def _dyn_spec(self):
+        """DynamicsNetwork4 (lines 391-457); the FiLM table [A + 1][512] is derived on the device (prepare)."""
+        P, put, A, d = self.params, self._put, self.A, "dynamics"
+        k6, k7 = P[f"{d}/Dense_6/kernel"], P[f"{d}/Dense_7/kernel"]
+        return dict(
+            d0=self._plain(f"{d}/Dense_0"), ln0=self._ln(f"{d}/LayerNorm_0"),
+            d12=self._dense_k(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1),
+                              np.concatenate([P[f"{d}/Dense_1/bias"], P[f"{d}/Dense_2/bias"]])),
+            d3=self._dense(f"{d}/Dense_3"), ln1=self._ln(f"{d}/LayerNorm_1"), d4=self._dense(f"{d}/Dense_4"),
+            ln2=self._ln(f"{d}/LayerNorm_2"), rb=[self._rb(f"{d}/ResBlock_{i}") for i in range(2)],
+            d5=self._dense(f"{d}/Dense_5"),
+            d67=self._dense_k(np.concatenate([k6[:LATENT], k7[:LATENT]], 1),
+                              np.concatenate([P[f"{d}/Dense_6/bias"], P[f"{d}/Dense_7/bias"]])),
+            d67_onehot=put(np.concatenate([k6[LATENT:LATENT + A], k7[LATENT:LATENT + A]], 1)),
+            reward_head=self._plain(f"{d}/reward_head"), discount_head=self._plain(f"{d}/discount_head"),
+            film=put(np.zeros((A + 1) * 2 * LATENT, np.float32)))
+
     def _upload(self, w, spec, device):
         host = np.concatenate(self._chunks) if self._chunks else np.zeros(4, np.float32)
         self.buffer = torch.from_numpy(host).to(device)
@@ -181,7 +198,12 @@ class _Packer:
                 field.__setattr__(field._fields_[1][0], base + 4 * val[1])
             elif isinstance(val, list):
                 for i, sub in enumerate(val):
-                    _Packer._fill(field[i], sub, base)
+                    if isinstance(sub, tuple):     # array of muz_dense / muz_ln
+                        f = field[i]
+                        f.__setattr__(f._fields_[0][0], base + 4 * sub[0])
+                        f.__setattr__(f._fields_[1][0], base + 4 * sub[1])
+                    else:
+                        _Packer._fill(field[i], sub, base)
             elif isinstance(val, dict):
                 _Packer._fill(field, val, base)
             else:
@@ -193,24 +215,9 @@ class DeviceNet(_Packer):
 
     def __init__(self, params: dict, obs_channels: int, num_actions: int = 24, device="cuda"):
         super().__init__(params, obs_channels, num_actions)
-        P, put, A, d = self.params, self._put, self.A, "dynamics"
         w = MuzNetW()
         w.obs_channels, w.num_actions = self.C, self.A
-        k6, k7 = P[f"{d}/Dense_6/kernel"], P[f"{d}/Dense_7/kernel"]
-        spec = {"repr": self._repr_spec()}
-        spec["dyn"] = dict(
-            d0=self._plain(f"{d}/Dense_0"), ln0=self._ln(f"{d}/LayerNorm_0"),
-            d12=self._dense_k(np.concatenate([P[f"{d}/Dense_1/kernel"], P[f"{d}/Dense_2/kernel"]], 1),
-                              np.concatenate([P[f"{d}/Dense_1/bias"], P[f"{d}/Dense_2/bias"]])),
-            d3=self._dense(f"{d}/Dense_3"), ln1=self._ln(f"{d}/LayerNorm_1"), d4=self._dense(f"{d}/Dense_4"),
-            ln2=self._ln(f"{d}/LayerNorm_2"), rb=[self._rb(f"{d}/ResBlock_{i}") for i in range(2)],
-            d5=self._dense(f"{d}/Dense_5"),
-            d67=self._dense_k(np.concatenate([k6[:LATENT], k7[:LATENT]], 1),
-                              np.concatenate([P[f"{d}/Dense_6/bias"], P[f"{d}/Dense_7/bias"]])),
-            d67_onehot=put(np.concatenate([k6[LATENT:LATENT + A], k7[LATENT:LATENT + A]], 1)),
-            reward_head=self._plain(f"{d}/reward_head"), discount_head=self._plain(f"{d}/discount_head"),
-            film=put(np.zeros((A + 1) * 2 * LATENT, np.float32)))
-        spec["pred"] = self._pred_spec()
+        spec = {"repr": self._repr_spec(), "dyn": self._dyn_spec(), "pred": self._pred_spec()}
         self._upload(w, spec, device)
         self.prepare()
 

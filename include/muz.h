@@ -899,6 +899,54 @@ int muz_adamw_step(float* const* params, const float* const* grads, float* const
                    float max_norm, double b1, double b2, float eps, float weight_decay, double lr0,
                    double steps_per_iteration, const double* boundaries, int32_t nb, void* stream);
 
+/* ---- DOG MuZero slice (MuZero_DOG/muzero_dog.py, DOG/dog.py:1264-1272) -----------------------------------
+ * The reference defines only the DOG RepresentationNetwork (muzero_dog.py:25-83: RepresentationNetwork2's trunk with
+ * a LayerNorm after its last Dense instead of min-max); encode_board, the dynamics / prediction networks, the
+ * inference functions and the self-play loop are `pass` (dog.py:1264-1272, muzero_dog.py:85-99, game_agent.py:52-57).
+ * Following SURVEY 8(d) ("MCTS with the det-MADN-shaped nets at A=806") this slice defines them: a 34-channel
+ * observation (oracle/dog_muzero.py encode_board), DynamicsNetwork4 / PredictionNetwork4 of the det file at A = 806,
+ * and gumbel_muzero_policy at A = 806 as muzero_dog.py:101-137 calls it.  Parity unpinned beyond the env. */
+#define MUZ_DOG_OBS_CHANNELS 34
+typedef struct muz_dog_net_w {
+  int32_t obs_channels;         /* 34 */
+  int32_t num_actions;          /* 806 */
+  muz_repr_w repr;              /* RepresentationNetwork (muzero_dog.py:25-83) up to Dense_4 */
+  muz_ln repr_ln7;              /* its LayerNorm head (lines 80-81) */
+  muz_dyn_w dyn;                /* DynamicsNetwork4 at A = 806 (film: [807][512]) */
+  muz_pred_w pred;              /* PredictionNetwork4 at A = 806; pred.d2 == logits[0] */
+  muz_dense logits[4];          /* Dense_2 (128 -> 806) as column chunks 0-255, 256-511, 512-767 (packed for 256
+                                   columns) and 768-805 (packed for 38) */
+} muz_dog_net_w;
+
+/* dyn.film of a DOG weight set (muz_net_prepare's table at A = 806). */
+int muz_dog_net_prepare(const muz_dog_net_w* w /*host*/, void* stream);
+
+/* encode_board for n 4-player games (oracle/dog_muzero.py encode_board): obs [n][34][56] fp32. */
+int muz_dog_encode(const muz_rules* rules /*host*/, muz_dog_soa state, float* obs, int32_t n, void* stream);
+
+/* root_inference_fn: obs [n][34][56] -> prior_logits [n][806], value [n], embedding [n][256]; scratch as
+ * muz_nets_root_scratch_bytes(n). */
+int muz_dog_nets_root(const muz_dog_net_w* w /*host*/, const float* obs, int32_t n, void* scratch,
+                      int64_t scratch_bytes, float* prior_logits, float* value, float* embedding, void* stream);
+
+/* recurrent_inference_fn: (action [n], embedding [n][256]) -> reward, discount, prior_logits [n][806], value,
+ * next_embedding. */
+int muz_dog_nets_recurrent(const muz_dog_net_w* w /*host*/, const int32_t* action, const float* embedding, int32_t n,
+                           float* reward, float* discount, float* prior_logits, float* value, float* next_embedding,
+                           void* stream);
+
+/* Workspace bytes of n DOG searches (children arrays [n][S+1][832] x 6 + node embeddings). */
+int64_t muz_dog_search_workspace_bytes(int32_t n, const muz_search_cfg* cfg /*host*/);
+
+/* run_muzero_mcts (muzero_dog.py:101-137): gumbel_muzero_policy at A = 806.  legal: muz_dog_legal's mask
+ * [n][26] words (invalid = ~legal); gumbel [n][806] already scaled, or NULL for the device noise of
+ * (cfg->seed, game, cfg->turn).  Outputs action [n], action_weights [n][806], root_value [n]. */
+int muz_dog_gumbel_search(const muz_dog_net_w* w /*host*/, const muz_search_cfg* cfg /*host*/,
+                          const float* root_logits, const float* root_value, const float* root_embedding,
+                          const uint32_t* legal, const float* gumbel, int32_t n, void* workspace,
+                          int64_t workspace_bytes, int32_t* action, float* action_weights, float* root_value_out,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,10 +68,39 @@ def exp_cr(x):
     return np.exp(np.asarray(x, F32).astype(np.float64)).astype(F32)
 
 
+LANES = 32   # lanes per game of the wide-action device search (csrc/dog_search.hip)
+
+
+def lane_tree_sum(x):
+    """float32 sum over the last axis in the order of the wide-action device search (A > 128, DOG's 806):
+    lane l of a game's 32 lanes adds its entries l, l + 32, l + 64, ... in turn, then the 32 lane sums are
+    combined as a balanced binary tree in lane order (((s0 + s1) + (s2 + s3)) + ...) -- the DPP / permlane
+    butterfly of csrc/nn.hpp row_reduce, whose every step adds a commutative pair."""
+    x = np.asarray(x, F32)
+    A = x.shape[-1]
+    pad = (-A) % LANES
+    xp = np.concatenate([x, np.full(x.shape[:-1] + (pad,), F32(-0.0))], -1) if pad else x
+    cols = xp.reshape(x.shape[:-1] + (-1, LANES))          # [..., j, lane]
+    s = cols[..., 0, :].copy()
+    for j in range(1, cols.shape[-2]):
+        s = (s + cols[..., j, :]).astype(F32)
+    while s.shape[-1] > 1:
+        s = (s[..., 0::2] + s[..., 1::2]).astype(F32)
+    return s[..., 0]
+
+
+def row_sum(x, keepdims=False):
+    """Sum over the action axis: numpy's own (pairwise) order up to 128 actions -- the det / classic kernels
+    restate it (csrc/search.hip row_sum24) -- and the wide search's lane order beyond."""
+    x = np.asarray(x, F32)
+    out = x.sum(-1).astype(F32) if x.shape[-1] <= 128 else lane_tree_sum(x)
+    return out[..., None] if keepdims else out
+
+
 def softmax(x):
     x = x.astype(F32)
     u = exp_cr(x - x.max(-1, keepdims=True))
-    return (u / u.sum(-1, keepdims=True)).astype(F32)
+    return (u / row_sum(u, keepdims=True)).astype(F32)
 
 
 def mask_invalid_actions(logits, invalid):
@@ -157,9 +186,9 @@ def qtransform_completed_by_mix_value(t: Tree, node, value_scale=0.5, maxvisit_i
         sum_visits = visits.sum(-1)
         pp = np.maximum(F32(TINY), prior_probs)
         visited = visits > 0
-        sum_probs = np.where(visited, pp, F32(0.0)).sum(-1).astype(F32)
+        sum_probs = row_sum(np.where(visited, pp, F32(0.0)))
         denom = np.where(visited, sum_probs[:, None], F32(1.0))
-        weighted_q = np.where(visited, (pp * q / denom).astype(F32), F32(0.0)).sum(-1).astype(F32)
+        weighted_q = row_sum(np.where(visited, (pp * q / denom).astype(F32), F32(0.0)))
         value = ((raw + sum_visits.astype(F32) * weighted_q) / (sum_visits + 1).astype(F32)).astype(F32)
     else:
         value = raw

@@ -21,8 +21,9 @@ F32 = np.float32
 
 
 # ---------------------------------------------------------------- parameter layout
-def repr_param_shapes(C: int) -> dict:
-    """RepresentationNetwork2 parameter shapes for an observation of C channels."""
+def repr_param_shapes(C: int, head: str = "minmax") -> dict:
+    """RepresentationNetwork2 parameter shapes for an observation of C channels (head "layernorm": the DOG
+    RepresentationNetwork, MuZero_DOG/muzero_dog.py:25-83, whose last Dense is followed by LayerNorm_7)."""
     s = {}
     s["Conv_0/kernel"] = (3, 6, 32)
     s["Conv_0/bias"] = (32,)
@@ -39,6 +40,9 @@ def repr_param_shapes(C: int) -> dict:
         s[f"{name}/bias"] = (o,)
     for r in range(6):
         _resblock_shapes(s, f"ResBlock_{r}")
+    if head == "layernorm":
+        s["LayerNorm_7/scale"] = (LATENT,)
+        s["LayerNorm_7/bias"] = (LATENT,)
     return s
 
 
@@ -83,23 +87,23 @@ def pred_param_shapes(A: int = 24) -> dict:
     return s
 
 
-def param_shapes(C: int, A: int = 24) -> dict:
+def param_shapes(C: int, A: int = 24, head: str = "minmax") -> dict:
     out = {}
-    for net, shapes in (("representation", repr_param_shapes(C)), ("dynamics", dyn_param_shapes(A)),
+    for net, shapes in (("representation", repr_param_shapes(C, head)), ("dynamics", dyn_param_shapes(A)),
                         ("prediction", pred_param_shapes(A))):
         for k, v in shapes.items():
             out[f"{net}/{k}"] = v
     return out
 
 
-def init_params(C: int, A: int = 24, seed: int = 0, randomize_affine: bool = False) -> dict:
+def init_params(C: int, A: int = 24, seed: int = 0, randomize_affine: bool = False, head: str = "minmax") -> dict:
     """Seeded Flax-default-like init: lecun_normal (truncated) kernels, zero biases, unit LN scale.
 
     ``randomize_affine`` also draws non-trivial biases / LN scales+biases so parity tests
     exercise every parameter.  (The reference's jax threefry init is not reproducible here.)"""
     rng = np.random.default_rng(seed)
     p = {}
-    for k, shp in param_shapes(C, A).items():
+    for k, shp in param_shapes(C, A, head).items():
         if k.endswith("kernel"):
             fan_in = int(np.prod(shp[:-1]))
             std = np.sqrt(1.0 / fan_in) / 0.87962566103423978
@@ -164,7 +168,9 @@ def minmax(x):
 
 # ---------------------------------------------------------------- networks
 def representation(params: dict, obs: np.ndarray) -> np.ndarray:
-    """RepresentationNetwork2 (muzero_deterministic_madn.py:75-141). obs [B, C, 56] -> [B, 256]."""
+    """RepresentationNetwork2 (muzero_deterministic_madn.py:75-141). obs [B, C, 56] -> [B, 256].  With a
+    ``representation/LayerNorm_7`` entry it is the DOG RepresentationNetwork (MuZero_DOG/muzero_dog.py:25-83):
+    the same trunk, LayerNorm instead of min-max after the last Dense (80-81)."""
     p = sub(params, "representation")
     x = obs.astype(F32)
     sp = np.transpose(x[:, :6, :], (0, 2, 1))            # (B, 56, 6)
@@ -179,6 +185,8 @@ def representation(params: dict, obs: np.ndarray) -> np.ndarray:
     h = relu(layer_norm(p, "LayerNorm_6", dense(p, "Dense_3", np.concatenate([flat, g], -1))))
     for r in range(6):
         h = resblock(p, f"ResBlock_{r}", h)
+    if "LayerNorm_7/scale" in p:
+        return layer_norm(p, "LayerNorm_7", dense(p, "Dense_4", h))
     return minmax(dense(p, "Dense_4", h))
 
 
@@ -190,9 +198,11 @@ def one_hot(a, n):
     return out
 
 
-def dynamics(params: dict, latent: np.ndarray, action: np.ndarray, A: int = 24):
-    """DynamicsNetwork4 (muzero_deterministic_madn.py:391-457) -> (next_latent, reward_logits, discount_logits)."""
+def dynamics(params: dict, latent: np.ndarray, action: np.ndarray, A: int | None = None):
+    """DynamicsNetwork4 (muzero_deterministic_madn.py:391-457) -> (next_latent, reward_logits, discount_logits).
+    A (the one-hot width) defaults to the parameters' own (Dense_0's input rows)."""
     p = sub(params, "dynamics")
+    A = p["Dense_0/kernel"].shape[0] if A is None else A
     oh = one_hot(action, A)
     e = relu(dense(p, "Dense_0", oh))
     ln = layer_norm(p, "LayerNorm_0", latent)

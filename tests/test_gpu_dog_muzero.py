@@ -1,0 +1,156 @@
+"""DOG MuZero slice on the GPU (csrc/dog_muzero.hip, csrc/dog_search.hip) against oracle/dog_muzero.py.
+
+The reference defines only the DOG RepresentationNetwork (MuZero_DOG/muzero_dog.py:25-83); the observation, the
+Dyn / Pred networks at A = 806 and the search there are builder-defined (parity unpinned beyond the env, whose
+transitions the other DOG tests pin).  Bars: the encoding bit-exact; network outputs within atol 1e-5 (fp32, MFMA
+k-order vs BLAS order, as tests/test_gpu_nets.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dog as dg
+from oracle import dog_muzero as DM
+from tests.dog_states import RULE_SETS, random_state, reset
+from tests.test_gpu_dog import rules_of, to_gpu
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-5
+
+
+def _MD():
+    from exploring_muzero_on_dog_amd import muzero_dog as MD
+    return MD
+
+
+def dog_states(rule_set, n_rand, n_fresh, seed):
+    kw = RULE_SETS[rule_set]
+    rng = np.random.default_rng(seed)
+    envs = [random_state(rng, kw, seed, g) for g in range(n_rand)] + \
+           [reset(kw, seed, n_rand + g) for g in range(n_fresh)]
+    return kw, envs
+
+
+@pytest.mark.parametrize("rule_set", ["selfplay_4p_teams", "exotic_4p"])
+def test_dog_encode_matches_oracle(cuda, rule_set):
+    MD = _MD()
+    kw, envs = dog_states(rule_set, 80, 16, 7)
+    gpu = to_gpu(envs, rules_of(kw), 7)
+    obs = MD.encode_board(gpu).cpu().numpy()
+    subs = 0
+    for b, e in enumerate(envs):
+        want = DM.encode_board(e)
+        assert np.array_equal(obs[b], want), (rule_set, b, np.argwhere(obs[b] != want)[:6].tolist())
+        subs += int(want[30, 0])
+    if RULE_SETS[rule_set].get("enable_teams"):
+        assert subs > 0   # the substituted hand (a finished player plays the partner's cards) was exercised
+
+
+def test_dog_encode_rejects_non_4p(cuda):
+    MD = _MD()
+    from exploring_muzero_on_dog_amd import dog as D
+    from exploring_muzero_on_dog_amd import lib as L
+    gpu = D.env_reset(8, num_players=2)
+    with pytest.raises(L.MuzError):
+        MD.encode_board(gpu)
+
+
+def _obs(n, seed):
+    kw, envs = dog_states("selfplay_4p_teams", n, 0, seed)
+    return np.stack([DM.encode_board(e) for e in envs]).astype(np.float32)
+
+
+def test_dog_root_inference(cuda):
+    MD = _MD()
+    params = DM.init_params(seed=11, randomize_affine=True)
+    net = MD.DeviceDogNet(params)
+    obs = _obs(61, 3)                                 # 61: a partial 16-row tile
+    lg, v, e = MD.root_inference_fn(net, torch.from_numpy(obs).cuda())
+    rl, rv, re = DM.root_inference(params, obs)
+    d_l = np.abs(lg.cpu().numpy() - rl).max()
+    d_v = np.abs(v.cpu().numpy() - rv).max()
+    d_e = np.abs(e.cpu().numpy() - re).max()
+    print(f"dog root: |dlogits| {d_l:.2e} |dvalue| {d_v:.2e} |dlatent| {d_e:.2e} (latent std {re.std():.2f})")
+    assert d_e < ATOL and d_l < ATOL and d_v < ATOL
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_dog_recurrent_inference(cuda, seed):
+    MD = _MD()
+    params = DM.init_params(seed=20 + seed, randomize_affine=True)
+    net = MD.DeviceDogNet(params)
+    rng = np.random.default_rng(seed)
+    B = 77
+    emb = rng.standard_normal((B, 256)).astype(np.float32)
+    act = rng.integers(0, 806, B).astype(np.int32)
+    act[:3] = [-1, 806, 805]                          # out of range -> zero one-hot row (jax.nn.one_hot)
+    out = MD.recurrent_inference_fn(net, torch.from_numpy(act).cuda(), torch.from_numpy(emb).cuda())
+    want = DM.recurrent_inference(params, act, emb)
+    names = ("reward", "discount", "logits", "value", "next_latent")
+    ds = {k: float(np.abs(o.cpu().numpy() - w).max()) for k, o, w in zip(names, out, want)}
+    print("dog recurrent:", {k: f"{v:.2e}" for k, v in ds.items()})
+    assert all(v < ATOL for v in ds.values()), ds
+
+
+def _search_setup(B, seed):
+    MD = _MD()
+    params = DM.init_params(seed=seed, randomize_affine=True)
+    net = MD.DeviceDogNet(params)
+    kw, envs = dog_states("selfplay_4p_teams", B, 8, seed + 5)
+    valid = np.stack([dg.valid_actions(e) for e in envs]).astype(bool)
+    keep = valid.any(1)
+    envs = [e for e, k in zip(envs, keep) if k]
+    valid = valid[keep]
+    obs = np.stack([DM.encode_board(e) for e in envs]).astype(np.float32)
+    words = MD.invalid_to_words(torch.from_numpy(~valid))
+    return MD, params, net, obs, valid, words
+
+
+def _gpu_recurrent_fn(MD, net):
+    def fn(params, action, emb):
+        out = MD.recurrent_inference_fn(net, torch.from_numpy(np.asarray(action, np.int32)).cuda(),
+                                        torch.from_numpy(np.ascontiguousarray(emb)).cuda())
+        return tuple(t.cpu().numpy() for t in out)
+    return fn
+
+
+def test_dog_invalid_to_words_matches_legal_mask(cuda):
+    MD = _MD()
+    from exploring_muzero_on_dog_amd import dog as D
+    gpu = D.env_reset(40, seed=3, **RULE_SETS["selfplay_4p_teams"])
+    words = D.legal_mask(gpu)
+    valid = D.unpack_mask(words).bool()
+    assert torch.equal(MD.invalid_to_words(~valid.cpu()).cuda(), words)
+
+
+@pytest.mark.parametrize("S,D", [(50, 25), (16, 4), (8, 50)])
+def test_dog_search_logic_matches_mctx_restatement(cuda, S, D):
+    """The oracle search driven by the GPU's own recurrent kernel: both sides see identical network outputs, so the
+    tree arithmetic (lane-order sums at A = 806, oracle/mctx_gumbel.py lane_tree_sum) must agree bit for bit."""
+    from tests._parity import search_parity
+    from oracle import mctx_gumbel as G
+    MD, params, net, obs, valid, words = _search_setup(40, 7)
+    B = obs.shape[0]
+    lg, v, e = MD.root_inference_fn(net, torch.from_numpy(obs).cuda())
+    gum = np.random.default_rng(3).gumbel(size=(B, 806)).astype(np.float32)
+    pol, rv = MD.gumbel_muzero_policy(net, lg, v, e, words, S, D, 1.0, gumbel=torch.from_numpy(gum))
+    trace = {}
+    a, w, orv, _ = G.gumbel_muzero_policy(params, lg.cpu().numpy(), v.cpu().numpy(), e.cpu().numpy(),
+                                          _gpu_recurrent_fn(MD, net), S, ~valid, gum, max_depth=D, trace=trace)
+    torch.cuda.synchronize()
+    ga, gw, grv = pol.action.cpu().numpy(), pol.action_weights.cpu().numpy(), rv.cpu().numpy()
+    search_parity(f"dog search logic A806 S{S} D{D}", ga, gw, grv, a, w, orv, trace["margin"], trace["gain"])
+    assert valid[np.arange(B), ga].all(), "search picked an invalid root action"
+    assert np.array_equal(ga, a) and np.array_equal(gw, w) and np.array_equal(grv, orv), \
+        "identical network outputs: the tree arithmetic must agree bit for bit"
+
+
+def test_dog_run_muzero_mcts_reference_signature(cuda):
+    """muzero_dog.py:101-137's signature on the flat params: same result as the device-native calls."""
+    MD, params, net, obs, valid, words = _search_setup(24, 9)
+    pol, rv = MD.run_muzero_mcts(params, 5, obs, ~valid, 8, 4, 1.0)
+    lg, v, e = MD.root_inference_fn(net, torch.from_numpy(obs).cuda())
+    pol2, rv2 = MD.gumbel_muzero_policy(net, lg, v, e, words, 8, 4, 1.0, seed=5)
+    assert torch.equal(pol.action, pol2.action) and torch.equal(pol.action_weights, pol2.action_weights)
+    assert torch.equal(rv, rv2)
+    assert valid[np.arange(len(valid)), pol.action.cpu().numpy()].all()
