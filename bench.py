@@ -65,14 +65,24 @@ DOG_TURNS_PER_LAUNCH = 1024     # one muz_dog_random_play launch plays 1024 turn
 DOG_LAUNCHES_PER_STEP = 32      # one bench step = 32 launches (~0.3 s: the default 3 steps time ~1 s)
 
 
+# DOG MuZero slice (--workload dog --policy muzero): MuZero_DOG/train.py:337-338 (S = 100, D = 50), 1024 games per GPU.
+# FLOP per simulation at A = 806, counted as the reference would compute it (one-hot Dense layers as matmuls, like
+# the det count): DynamicsNetwork4 679,424 MAC (Dense_0 806 x 64 and the one-hot rows of Dense_6 / 7, 806 x 128, are
+# the A-dependent parts) + PredictionNetwork4 504,640 MAC (policy logits 128 x 806).  Executed on the device:
+# 996,544 MAC (one-hot rows are gathers; the action-only FiLM sub-graph is a per-action table).
+DOG_MZ_SIMS, DOG_MZ_DEPTH, DOG_MZ_TURNS_PER_STEP = 100, 50, 8
+DOG_MZ_FLOP_PER_SIM = 2 * (679_424 + 504_640)
+DOG_MZ_EXEC_FLOP_PER_SIM = 2 * 996_544
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=BATCH)
-    ap.add_argument("--sims", type=int, default=S)
-    ap.add_argument("--depth", type=int, default=D)
+    ap.add_argument("--sims", type=int, default=None, help="MCTS simulations (det / classic 50, dog muzero 100)")
+    ap.add_argument("--depth", type=int, default=None, help="MCTS max depth (det / classic 25, dog muzero 50)")
     ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample (1 core + all cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -91,12 +101,21 @@ def parse():
                     help="dog: record every turn (muz_dog_random_play_record), pack the records each step and gather "
                          "them to rank 0 (RCCL point-to-point at N > 1) inside the timed region -- config (d) as "
                          "BASELINE.json names it")
+    ap.add_argument("--policy", choices=("random", "muzero"), default="random",
+                    help="dog: the reference's config (d) random legal policy, or the DOG MuZero slice (repr net with "
+                         "its LayerNorm head + Dyn4 / Pred4 at A = 806 + Gumbel search, MuZero_DOG/train.py's S = 100, "
+                         "D = 50)")
     ap.add_argument("--split", action="store_true",
                     help="strong scaling (SURVEY §8e): --batch is the WHOLE job's batch, split evenly over the ranks "
                          "(det 4096 -> 2048/1024/512 per GPU); default is weak scaling, --batch games per GPU")
     args = ap.parse_args()
     if args.workload == "dog" and args.batch == BATCH:
         args.batch = DOG_BATCH
+    dog_mz = args.workload == "dog" and args.policy == "muzero"
+    if args.sims is None:
+        args.sims = DOG_MZ_SIMS if dog_mz else S
+    if args.depth is None:
+        args.depth = DOG_MZ_DEPTH if dog_mz else D
     args.job_batch = args.batch
     if args.split:
         world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
@@ -363,6 +382,75 @@ def dog_latency_model(avg_ms, games, turns, launch_bytes):
                     "64 lanes of wave 0 (ballot / readlane lookups, 4628 -> 3383 ticks; 6.18 -> 5.80 us/turn, "
                     "profiles/r4c_dog_bench_*.json); r3: 4-wave workgroups (no register spills; 6.81 -> 6.17 us/turn) "
                     "and the turn's serial part at raised wave priority, profiles/r3_dog_prio_ab.log"}
+
+
+def run_dog_muzero(args):
+    """Config (d) with the DOG MuZero slice: B 4-player DOG games per GPU played by the MuZero policy
+    (game_agent_dog.DogSelfPlay: legal mask -> encode -> RepresentationNetwork + Pred4 -> Gumbel search at A = 806
+    with Dyn4 / Pred4 -> step, finished games restarting in place).  One bench step = DOG_MZ_TURNS_PER_STEP turns of
+    every game; env-steps = games x turns.  Roofline: k_dog_search's algorithmic FLOP over its HIP-event time."""
+    import numpy as np
+    import torch
+    rank, world, dist, device = setup(args)
+    from exploring_muzero_on_dog_amd import game_agent_dog as GA
+    from exploring_muzero_on_dog_amd import muzero_dog as MD
+    net = MD.DeviceDogNet(MD.init_muzero_params(2), device=device)
+    sp = GA.DogSelfPlay(net, args.batch, args.sims, args.depth, 1.0, seed=4 + 1000 * rank, device=device)
+    K = DOG_MZ_TURNS_PER_STEP
+    ev = []
+    orig = MD.gumbel_muzero_policy
+
+    def timed_search(*a, **kw):          # HIP events on the launching stream around every search launch
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = orig(*a, **kw)
+        e1.record()
+        ev.append((e0, e1))
+        return out
+
+    def step(k):
+        sp.play(K)
+
+    sp.play(1)                           # warmup turn (workspace, first launches)
+    for _ in range(args.warmup):
+        step(-1)
+    MD.gumbel_muzero_policy = timed_search
+    try:
+        elapsed = timed_region(dist, step, args.steps)
+    finally:
+        MD.gumbel_muzero_policy = orig
+    search_ms = sum(a.elapsed_time(b) for a, b in ev)
+    turns = args.steps * K
+    (steps_done, sms, games), elapsed = sum_max(dist, device, [args.batch * turns, search_ms,
+                                                             int(sp.episodes.sum().item())], elapsed)
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    avg_ms = sms / (turns * world)
+    flop = args.batch * args.sims * DOG_MZ_FLOP_PER_SIM
+    achieved = flop / (avg_ms * 1e-3) / 1e12
+    out = {
+        "metric": "self-play env steps/sec + MCTS sims/sec, DOG 2v2 MuZero policy (config d, DOG MuZero slice)",
+        "value": round(steps_done / elapsed, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 4), "higher_is_better": True,
+        "scaling": "strong" if args.split else "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded deals, seeded random fp32 weights, counter-RNG Gumbel noise)",
+        "sims_per_s": round(steps_done * args.sims / elapsed, 1), "games_finished": int(games),
+        "config": {"workload": f"DOG 4p teams, {args.batch} games/GPU, MuZero policy (DOG RepresentationNetwork + "
+                               f"Dyn4 / Pred4 at A = 806), Gumbel search S={args.sims} D={args.depth}, {K} turns of "
+                               f"every game per step, finished games restart in place", "games_per_gpu": args.batch,
+                   "num_simulations": args.sims, "max_depth": args.depth, "turns_per_step": K,
+                   "parallelism": parallelism(args, world)},
+        "roofline": {"bound": "mfma", "kernel": "k_dog_search", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "avg_launch_ms": round(avg_ms, 4),
+                     "flop_per_sim": DOG_MZ_FLOP_PER_SIM, "executed_flop_per_sim": DOG_MZ_EXEC_FLOP_PER_SIM,
+                     "tiles": -(-args.batch // 16), "traffic": None,
+                     "note": "one 16-game tile per workgroup: 1024 games fill 64 of the 256 CUs"},
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def run_dog(args):
@@ -968,6 +1056,8 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
+    if args.workload == "dog" and args.policy == "muzero":
+        return run_dog_muzero(args)
     return {"train": run_train, "dog": run_dog, "classic": run_classic, "det": run_det, "env": run_env,
             "selftest": run_selftest}[args.workload](args)
 

@@ -479,7 +479,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     for (int j = 0; j < kWJ; ++j)
       if (wok(sub, j)) out_weights[(size_t)g * kDogA + sub + kRowLanes * j] = exp_cr_w(zz(j) - mm) / zs;
     if (sub == 0) {
-      out_action[g] = bi;
+      out_action[g] = ncons > 0 ? bi : -1;   // no legal action: -1, the self-play loop's no_step
       out_value[g] = s_val[row][0];
     }
   }

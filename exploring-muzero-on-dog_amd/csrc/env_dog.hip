@@ -1013,8 +1013,11 @@ __global__ __launch_bounds__(kDogPlayThreads) __attribute__((amdgpu_waves_per_eu
 }
 
 // mode 0: env_step(action[g]); mode 1: no_step.  action < 0 with mode 0 = no_step as well.
+// restart != 0 (the MuZero self-play loop, muz_dog_step_restart): a game the step finished restarts in place after
+// it (dog_reset_lds with the deal counter continued, as k_dog_play's auto reset) and episodes[g] counts it.
 __global__ __launch_bounds__(256) void k_dog_step(DetConsts c, muz_dog_soa st, const int32_t* action, int mode,
-                                                  unsigned long long seed, int8_t* reward, uint8_t* done, int n) {
+                                                  unsigned long long seed, int8_t* reward, uint8_t* done, int n,
+                                                  int restart = 0, uint32_t* episodes = nullptr) {
   __shared__ DogG sg[kDogGamesPerBlock];
   __shared__ int need_deal[kDogGamesPerBlock];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1038,6 +1041,10 @@ __global__ __launch_bounds__(256) void k_dog_step(DetConsts c, muz_dog_soa st, c
   }
   wave_sync();
   if (need_deal[w]) dog_deal<WaveSync>(c, s, seed, g, lane);
+  if (restart && s.done) {   // (one wave: every lane has read s.done before dog_reset_lds clears it)
+    if (episodes && lane == 0) episodes[g] += 1u;
+    dog_reset_lds<WaveSync>(c, s, seed, g, s.deal, lane);
+  }
   dog_store<WaveSync>(c, st, g, s, lane);
 }
 
@@ -1175,6 +1182,13 @@ int muz_dog_step(const muz_rules* rules, muz_dog_soa st, const int32_t* action, 
                  uint8_t* done, int32_t n, void* stream) {
   DOG_PROLOGUE(action != nullptr)
   k_dog_step<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, action, 0, seed, reward, done, n);
+  return muz_last_launch_error();
+}
+
+int muz_dog_step_restart(const muz_rules* rules, muz_dog_soa st, const int32_t* action, uint64_t seed, int8_t* reward,
+                         uint8_t* done, uint32_t* episodes, int32_t n, void* stream) {
+  DOG_PROLOGUE(action != nullptr)
+  k_dog_step<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, action, 0, seed, reward, done, n, 1, episodes);
   return muz_last_launch_error();
 }
 

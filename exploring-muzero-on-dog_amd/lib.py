@@ -271,6 +271,8 @@ SIGNATURES = {
     "muz_dog_legal": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_int32, vp]),
     "muz_dog_step": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_uint64, vp, vp, ctypes.c_int32,
                                     vp]),
+    "muz_dog_step_restart": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_uint64, vp, vp, vp,
+                                            ctypes.c_int32, vp]),
     "muz_dog_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, vp, vp, ctypes.c_int32,
                                       vp]),
     "muz_dog_step_move": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, vp, vp, vp, ctypes.c_int32, vp]),

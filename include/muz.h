@@ -215,6 +215,11 @@ int muz_dog_step(const muz_rules* rules, muz_dog_soa state, const int32_t* actio
                  uint8_t* done, int32_t n, void* stream);
 
 /* no_step (dog.py:713-752). */
+/* muz_dog_step for the self-play loop: env_step(action[g]) (no_step when action[g] < 0), then a game the step
+ * finished restarts in place (env_reset with the deal counter continued, as muz_dog_random_play's auto reset);
+ * reward / done are the step's, episodes[g] (nullable) counts the restarts. */
+int muz_dog_step_restart(const muz_rules* rules /*host*/, muz_dog_soa state, const int32_t* action, uint64_t seed,
+                         int8_t* reward, uint8_t* done, uint32_t* episodes, int32_t n, void* stream);
 int muz_dog_nostep(const muz_rules* rules, muz_dog_soa state, uint64_t seed, int8_t* reward, uint8_t* done,
                    int32_t n, void* stream);
 
@@ -940,7 +945,8 @@ int64_t muz_dog_search_workspace_bytes(int32_t n, const muz_search_cfg* cfg /*ho
 
 /* run_muzero_mcts (muzero_dog.py:101-137): gumbel_muzero_policy at A = 806.  legal: muz_dog_legal's mask
  * [n][26] words (invalid = ~legal); gumbel [n][806] already scaled, or NULL for the device noise of
- * (cfg->seed, game, cfg->turn).  Outputs action [n], action_weights [n][806], root_value [n]. */
+ * (cfg->seed, game, cfg->turn).  Outputs action [n] (-1 for a game without a legal action: the self-play loop's
+ * no_step), action_weights [n][806], root_value [n]. */
 int muz_dog_gumbel_search(const muz_dog_net_w* w /*host*/, const muz_search_cfg* cfg /*host*/,
                           const float* root_logits, const float* root_value, const float* root_embedding,
                           const uint32_t* legal, const float* gumbel, int32_t n, void* workspace,

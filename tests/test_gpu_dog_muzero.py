@@ -154,3 +154,52 @@ def test_dog_run_muzero_mcts_reference_signature(cuda):
     assert torch.equal(pol.action, pol2.action) and torch.equal(pol.action_weights, pol2.action_weights)
     assert torch.equal(rv, rv2)
     assert valid[np.arange(len(valid)), pol.action.cpu().numpy()].all()
+
+
+def test_dog_muzero_selfplay_followed_by_oracle(cuda):
+    """game_agent_dog.DogSelfPlay (legal -> encode -> root -> search at A = 806 -> step, finished games restarting in
+    place) followed turn by turn by the oracle: oracle/dog.py transitions with the engine's deal keys, the oracle's
+    own encoding fed to the GPU root kernel, and oracle/mctx_gumbel.py driven by the GPU recurrent kernel with the
+    engine's Gumbel stream -- every action, weight, root value and state bit-identical."""
+    from oracle import mctx_gumbel as G
+    from oracle import selfplay as OS
+    from exploring_muzero_on_dog_amd import dog as D
+    from exploring_muzero_on_dog_amd import game_agent_dog as GA
+    MD = _MD()
+    params = DM.init_params(seed=13, randomize_affine=True)
+    net = MD.DeviceDogNet(params)
+    B, S, Dd, T, seed, temp = 10, 4, 3, 24, 21, 1.0
+    sp = GA.DogSelfPlay(net, B, S, Dd, temp, seed=seed)
+    kw = RULE_SETS["selfplay_4p_teams"]
+    envs = [reset(kw, seed, g) for g in range(B)]
+    keys = [dg.engine_shuffle_keys(seed, g) for g in range(B)]
+    rec = _gpu_recurrent_fn(MD, net)
+    searched = 0
+    for t in range(T):
+        act, w, rv = sp.turn()
+        act, w, rv = act.cpu().numpy(), w.cpu().numpy(), rv.cpu().numpy()
+        valid = np.stack([dg.valid_actions(e) for e in envs]).astype(bool)
+        has = np.flatnonzero(valid.any(1))
+        want = np.full(B, -1)
+        if has.size:
+            obs = np.stack([DM.encode_board(envs[g]) for g in has]).astype(np.float32)
+            lg, v, e = (x.cpu().numpy() for x in MD.root_inference_fn(net, torch.from_numpy(obs).cuda()))
+            gum = np.stack([OS.gumbel_noise(seed, int(g), t, A=806, scale=temp) for g in has]).astype(np.float32)
+            a, ow, orv, _ = G.gumbel_muzero_policy(params, lg, v, e, rec, S, ~valid[has], gum, max_depth=Dd)
+            want[has] = a
+            assert np.array_equal(w[has], ow) and np.array_equal(rv[has], orv), t
+            searched += has.size
+        assert np.array_equal(act, want), (t, act.tolist(), want.tolist())
+        for g in range(B):
+            e0 = envs[g]
+            e1 = (dg.no_step(e0, keys[g]) if want[g] < 0 else dg.env_step(e0, int(want[g]), keys[g]))[0]
+            if e1.done:      # muz_dog_step_restart: env_reset in place, deal counter continued
+                base = e1.deal
+                e1 = dg.env_reset(num_players=4, shuffle_keys=lambda x, b=base, k=keys[g]: k(x.replace(deal=x.deal + b)),
+                                  **dg.SELFPLAY_RULES)
+                e1 = e1.replace(deal=e1.deal + base)
+            envs[g] = e1
+        from tests.dog_states import diff
+        bad = diff(D.to_host(sp.env), envs)
+        assert bad is None, (t, bad)
+    assert searched > B * T // 2
