@@ -35,6 +35,7 @@ struct WTree {
   float* c_reward;
   float* c_disc;
   float* emb;
+  float* gum;    // [n][832] the root's Gumbel noise, drawn once per search
   int N;
   __device__ __forceinline__ size_t ca(int g, int node, int a) const { return ((size_t)g * N + node) * kWPad + a; }
   __device__ __forceinline__ AS1 float* e(int g, int node) const { return gpw(emb) + ((size_t)g * N + node) * LAT; }
@@ -65,6 +66,8 @@ static WTree carve_wide(void* ws, int n, int N) {
   t.c_disc = (float*)p;
   p += cb;
   t.emb = (float*)p;
+  p += (size_t)n * N * LAT * 4;
+  t.gum = (float*)p;
   t.N = N;
   return t;
 }
@@ -282,6 +285,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         tree_st(T.value() + e, 0.f);
         tree_st(T.reward() + e, 0.f);
         tree_st(T.disc() + e, 0.f);
+        gpw(T.gum)[(size_t)g * kWPad + a] =
+            gumbel_in ? gumbel_in[(size_t)g * kDogA + a] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, gturn, a);
       }
     }
     AS1 float* e0 = T.e(g, 0);
@@ -295,9 +300,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
   }
   __syncthreads();
 
-  auto gumbel_of = [&](int a) -> float {
-    return gumbel_in ? gumbel_in[(size_t)g * kDogA + a] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, gturn, a);
-  };
+  // (drawn once above: hashing the 806 draws inside the simulation loop made the compiler hoist their per-slot
+  // constants out of it, 52 VGPRs live across the networks)
+  auto gumbel_of = [&](int a) -> float { return tree_ld(gpw(T.gum) + (size_t)g * kWPad + a); };
   auto legal_of = [&](int j) -> bool { return (s_legal[row][j] >> sub) & 1u; };
 
   Pf pf;
@@ -487,7 +492,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
 
 int64_t dog_search_workspace_bytes(int n, int S) {
   const int N = S + 1;
-  return (int64_t)wide_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4;
+  return (int64_t)wide_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4 + (int64_t)n * kWPad * 4;
 }
 
 int launch_dog_search(const muz_dog_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,
