@@ -73,7 +73,13 @@ static WTree carve_wide(void* ws, int n, int N) {
 }
 
 // exp correctly rounded (float64, rounded once): oracle/mctx_gumbel.py exp_cr, search.hip exp_cr
-__device__ __forceinline__ float exp_cr_w(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float exp_cr_w(float x) {
+#ifdef MUZ_DOG_EXPT_FASTEXP   // timing experiment only (wrong rounding)
+  return __expf(x);
+#else
+  return (float)exp((double)x);
+#endif
+}
 
 // sum of this game's 806 entries f(j) (this lane's slot j; padding slots give -0) in the lane order of
 // oracle/mctx_gumbel.py lane_tree_sum: each lane its slots in turn, then a balanced tree over the 32 lanes
@@ -319,9 +325,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         WNode nd;
         nd.pr = smem + row * kDogA;
         nd.cq = smem + (kRows + row) * kDogA;
-        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa);
         int bi;
+#ifdef MUZ_DOG_EXPT_NOSELECT   // timing experiment only (wrong results): a fixed child, no node load
+        bi = (node * 131 + sim * 7 + depth) % kDogA;
+        if (false) {
+#else
+        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa);
         if (depth == 0) {
+#endif
           // gumbel_muzero_root_action_selection: score_considered + masked_argmax
           const int cv = wconsidered_visit(ncons, sa.S, nd.sv);
           bi = wargmax([&](int j) {

@@ -23,11 +23,28 @@ def _MD():
     return MD
 
 
+def finished_mover(e):
+    """e with the current player's four pins in its goal (a finished player: with teams it plays the partner's hand,
+    dog.py sub_player) and the board rebuilt."""
+    pins = np.asarray(e.pins).copy()
+    cp = e.current_player
+    board = np.asarray(e.board).copy()
+    for k in range(4):
+        cell = int(e.goal[cp][k])
+        for p in range(pins.shape[0]):        # a pin of another player on that cell goes home
+            pins[p][pins[p] == cell] = -1
+        pins[cp][k] = cell
+    board = dg.set_pins_on_board(-np.ones(56, np.int8), pins)
+    return e.replace(pins=pins, board=board)
+
+
 def dog_states(rule_set, n_rand, n_fresh, seed):
     kw = RULE_SETS[rule_set]
     rng = np.random.default_rng(seed)
     envs = [random_state(rng, kw, seed, g) for g in range(n_rand)] + \
            [reset(kw, seed, n_rand + g) for g in range(n_fresh)]
+    for g in range(0, n_rand, 8):           # every 8th random state: the mover has finished
+        envs[g] = finished_mover(envs[g])
     return kw, envs
 
 
