@@ -28,23 +28,21 @@ static_assert(kWPad >= kDogA && kWWords * 32 >= kDogA, "slots");
 static_assert(2 * kRows * kDogA <= kArenaFloats, "the walk's per-child arrays live in the idle network arena");
 
 struct WTree {
-  int32_t* c_index;
-  float* c_prior;
-  float* c_value;
-  int32_t* c_visits;
-  float* c_reward;
-  float* c_disc;
-  float* emb;
-  float* gum;    // [n][832] the root's Gumbel noise, drawn once per search
+  f32x4* c_node;      // [n][N][832] per child {prior logit, value, reward, discount}: one 16-byte load per child
+  int32_t* c_visits;  // [n][N][832]
+  int32_t* c_index;   // [n][N][832]
+  float* emb;         // [n][N][256]
+  float* gum;         // [n][832] the root's Gumbel noise + (prior - max prior), drawn once per search
   int N;
   __device__ __forceinline__ size_t ca(int g, int node, int a) const { return ((size_t)g * N + node) * kWPad + a; }
   __device__ __forceinline__ AS1 float* e(int g, int node) const { return gpw(emb) + ((size_t)g * N + node) * LAT; }
+  __device__ __forceinline__ AS1 f32x4* node4() const { return gpw(c_node); }
+  // field k (0 prior, 1 value, 2 reward, 3 discount) of child entry e
+  __device__ __forceinline__ AS1 float* fld(size_t e, int k) const {
+    return gpw(reinterpret_cast<float*>(c_node)) + 4 * e + k;
+  }
   __device__ __forceinline__ AS1 int32_t* index() const { return gpw(c_index); }
-  __device__ __forceinline__ AS1 float* prior() const { return gpw(c_prior); }
-  __device__ __forceinline__ AS1 float* value() const { return gpw(c_value); }
   __device__ __forceinline__ AS1 int32_t* visits() const { return gpw(c_visits); }
-  __device__ __forceinline__ AS1 float* reward() const { return gpw(c_reward); }
-  __device__ __forceinline__ AS1 float* disc() const { return gpw(c_disc); }
 };
 
 static size_t wide_children_bytes(int64_t n, int N) { return (size_t)n * N * kWPad * 4; }
@@ -53,17 +51,11 @@ static WTree carve_wide(void* ws, int n, int N) {
   char* p = (char*)ws;
   const size_t cb = wide_children_bytes(n, N);
   WTree t;
-  t.c_index = (int32_t*)p;
-  p += cb;
-  t.c_prior = (float*)p;
-  p += cb;
-  t.c_value = (float*)p;
-  p += cb;
+  t.c_node = (f32x4*)p;
+  p += 4 * cb;
   t.c_visits = (int32_t*)p;
   p += cb;
-  t.c_reward = (float*)p;
-  p += cb;
-  t.c_disc = (float*)p;
+  t.c_index = (int32_t*)p;
   p += cb;
   t.emb = (float*)p;
   p += (size_t)n * N * LAT * 4;
@@ -89,7 +81,9 @@ __device__ __forceinline__ float wsum(F f) {
 #pragma unroll
   for (int j = 1; j < kWJ; ++j) {
     s = s + f(j);
+#ifndef MUZ_DOG_EXPT_NOBAR
     if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);   // bounded interleaving of the slots (registers)
+#endif
   }
   return row_sum(s);   // xor1, xor2, half mirror, mirror, swap16: the balanced tree in lane order
 }
@@ -97,19 +91,8 @@ __device__ __forceinline__ float wsum(F f) {
 // argmax over the row's 806 children of score f(j) (this lane's slot j), jnp.argmax tie-break (first index):
 // this lane's slots in ascending order (strict >), then row_argmax's (value, index) order across the lanes.
 // Streams the scores: no per-slot array is kept.
-template <class F>
-__device__ __forceinline__ int wargmax(F f, int sub) {
-  float v = -INFINITY;
-  int i = sub;
-#pragma unroll
-  for (int j = 0; j < kWJ; ++j) {
-    const float x = f(j);
-    if (x > v) {
-      v = x;
-      i = sub + kRowLanes * j;
-    }
-    if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);   // bounded interleaving of the slots (registers)
-  }
+// (value, index) argmax across the row's lanes, row_argmax's order (larger value, then smaller index)
+__device__ __forceinline__ int wargmax_row(float v, int i) {
   auto pick = [](float& v, int& i, float ov, int oi) {
     if (ov > v || (ov == v && oi < i)) {
       v = ov;
@@ -126,6 +109,55 @@ __device__ __forceinline__ int wargmax(F f, int sub) {
   i = pi.lo;
   pick(v, i, pv.hi, pi.hi);
   return i;
+}
+
+// argmax over the row's 806 children of score f(j) (this lane's slot j), jnp.argmax tie-break (first index):
+// this lane's slots in ascending order (strict >), then wargmax_row.  Streams the scores: no per-slot array.
+template <class F>
+__device__ __forceinline__ int wargmax(F f, int sub) {
+  float v = -INFINITY;
+  int i = sub;
+#pragma unroll
+  for (int j = 0; j < kWJ; ++j) {
+    const float x = f(j);
+    if (x > v) {
+      v = x;
+      i = sub + kRowLanes * j;
+    }
+#ifndef MUZ_DOG_EXPT_NOBAR
+    if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);   // bounded interleaving of the slots (registers)
+#endif
+  }
+  return wargmax_row(v, i);
+}
+
+constexpr int kWHalf = kWJ / 2;   // slots per load batch
+
+// score_considered + masked_argmax at the root: gp = the root's Gumbel noise + (prior - max prior) (T.gum), loaded in
+// two batches of 13 slots (one at a time, the loads serialised on their uses: 26 L2 round trips)
+template <class Legal>
+__device__ __forceinline__ int wroot_argmax(const WTree& T, int g, int sub, const float* cq, const int (&vis)[kWJ],
+                                            int cv, Legal legal_of) {
+  float v = -INFINITY;
+  int i = sub;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float gp[kWHalf];
+#pragma unroll
+    for (int k = 0; k < kWHalf; ++k) gp[k] = tree_ld(gpw(T.gum) + (size_t)g * kWPad + sub + kRowLanes * (kWHalf * h + k));
+    __builtin_amdgcn_sched_barrier(0);   // the batch's loads in flight together
+#pragma unroll
+    for (int k = 0; k < kWHalf; ++k) {
+      const int j = kWHalf * h + k, a = sub + kRowLanes * j;
+      float x = -INFINITY;
+      if (a < kDogA && legal_of(j)) x = fmaxf(-1e9f, gp[k] + cq[a]) + (vis[j] == cv ? 0.f : -INFINITY);
+      if (x > v) {
+        v = x;
+        i = a;
+      }
+    }
+  }
+  return wargmax_row(v, i);
 }
 
 __device__ __forceinline__ bool wok(int sub, int j) { return sub + kRowLanes * j < kDogA; }
@@ -166,43 +198,55 @@ __device__ __forceinline__ void wnode_load(WNode& nd, const WTree& T, int g, int
 #pragma clang fp contract(off)
   float pm = -INFINITY;
   int sv = 0, mv = 0;
+  // two batches of 13 slots, one 16-byte {prior, value, reward, discount} load + the visit count each, all of a batch in
+  // flight together (left to itself the scheduler serialised them slot by slot to save registers: 26 round trips).
+  // Padding slots are read too (they exist in the node's 832) and their values dropped.
 #pragma unroll
-  for (int j = 0; j < kWJ; ++j) {
-    // (padding slots are read too -- they exist in the node's 832 -- and their values dropped: one base address per
-    // field with immediate offsets)
-    const int a = sub + kRowLanes * j;
-    const bool ok = wok(sub, j);
-    const size_t e = T.ca(g, node, a);
-    const float pr = tree_ld(T.prior() + e);
-    const int vs = tree_ld(T.visits() + e);
-    const float rw = tree_ld(T.reward() + e), dc = tree_ld(T.disc() + e), vl = tree_ld(T.value() + e);
-    nd.vis[j] = ok ? vs : 0;
-    if (ok) {
-      nd.pr[a] = pr;
-      nd.cq[a] = rw + dc * vl;   // q (Tree.qvalues)
-      pm = fmaxf(pm, pr);
+  for (int h = 0; h < 2; ++h) {
+    f32x4 c4[kWHalf];
+    int vs[kWHalf];
+#pragma unroll
+    for (int k = 0; k < kWHalf; ++k) {
+      const size_t e = T.ca(g, node, sub + kRowLanes * (kWHalf * h + k));
+      c4[k] = tree_ld(T.node4() + e);
+      vs[k] = tree_ld(T.visits() + e);
     }
-    sv += nd.vis[j];
-    mv = max(mv, nd.vis[j]);
-    // at most four slots' loads in flight: unfenced, the scheduler hoists all 130 loads of the node (130 VGPRs)
-    if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
+    ST(ST_PASS);   // (diagnostic builds: node loads)
+#pragma unroll
+    for (int k = 0; k < kWHalf; ++k) {
+      const int j = kWHalf * h + k, a = sub + kRowLanes * j;
+      const bool ok = a < kDogA;
+      nd.vis[j] = ok ? vs[k] : 0;
+      if (ok) {
+        nd.pr[a] = c4[k][0];
+        nd.cq[a] = c4[k][2] + c4[k][3] * c4[k][1];   // q = reward + discount * value (Tree.qvalues)
+        pm = fmaxf(pm, c4[k][0]);
+      }
+      sv += nd.vis[j];
+      mv = max(mv, nd.vis[j]);
+    }
   }
   pm = row_max(pm);
   sv = row_isum(sv);
   mv = row_imax(mv);
   const float es = wsum([&](int j) { return wok(sub, j) ? exp_cr_w(nd.pr[sub + kRowLanes * j] - pm) : -0.0f; });
-  // prior probabilities of the visited children, floored at tiny (only those enter the mixed value)
-  auto ppv = [&](int j) -> float {
-    float x = 0.f;
-    if (nd.vis[j] > 0) x = fmaxf(kTinyF, exp_cr_w(nd.pr[sub + kRowLanes * j] - pm) / es);
-    return x;
-  };
-  const float sp = wsum([&](int j) { return wok(sub, j) ? ppv(j) : -0.0f; });
-  const float wq = wsum([&](int j) {
-    float x = wok(sub, j) ? 0.f : -0.0f;
-    if (nd.vis[j] > 0) x = ppv(j) * nd.cq[sub + kRowLanes * j] / sp;
-    return x;
-  });
+  // The mixed value needs the prior probabilities of the VISITED children only: sum_probs and weighted_q are summed
+  // over this lane's visited slots (a bit mask, in slot order) -- the unvisited ones add exact zeros in the
+  // restatement's order (lane_tree_sum), which change no partial sum -- so their exponentials are not recomputed.
+  unsigned vm = 0;
+#pragma unroll
+  for (int j = 0; j < kWJ; ++j) vm |= (nd.vis[j] > 0 ? 1u : 0u) << j;
+  auto ppa = [&](int a) { return fmaxf(kTinyF, exp_cr_w(nd.pr[a] - pm) / es); };
+  float spl = 0.f;
+  for (unsigned m = vm; m; m &= m - 1u) spl = spl + ppa(sub + kRowLanes * (__ffs(m) - 1));
+  const float sp = row_sum(spl);
+  float wql = 0.f;
+  for (unsigned m = vm; m; m &= m - 1u) {
+    const int a = sub + kRowLanes * (__ffs(m) - 1);
+    wql = wql + ppa(a) * nd.cq[a] / sp;
+  }
+  const float wq = row_sum(wql);
   const float mixed = (raw + (float)sv * wq) / (float)(sv + 1);
   float lo = INFINITY, hi = -INFINITY;
 #pragma unroll
@@ -227,6 +271,7 @@ __device__ __forceinline__ void wnode_load(WNode& nd, const WTree& T, int g, int
   nd.pm = pm;
   nd.sv = sv;
   nd.mv = mv;
+  ST(ST_OTHER);   // (diagnostic builds: the completed-Q transform)
 }
 
 __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, SearchArgs sa,
@@ -278,21 +323,29 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
       if (a < kDogA) lm = fmaxf(lm, root_logits[(size_t)g * kDogA + a]);
     }
     lm = row_max(lm);
+    float pr[kWJ], pm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kWJ; ++j) {
+      const int a = sub + kRowLanes * j;
+      pr[j] = kWFMin;
+      if (a < kDogA) {
+        const bool inv = ((legal[(size_t)g * kWWords + j] >> sub) & 1u) == 0u;
+        pr[j] = inv ? kWFMin : root_logits[(size_t)g * kDogA + a] - lm;
+        pm = fmaxf(pm, pr[j]);
+        const size_t e = T.ca(g, 0, a);
+        tree_st(T.node4() + e, f32x4{pr[j], 0.f, 0.f, 0.f});
+        tree_st(T.index() + e, -1);
+        tree_st(T.visits() + e, 0);
+      }
+    }
+    pm = row_max(pm);   // score_considered's logits.max over the root's (masked) priors, fixed for the search
 #pragma unroll
     for (int j = 0; j < kWJ; ++j) {
       const int a = sub + kRowLanes * j;
       if (a < kDogA) {
-        const uint32_t w = legal[(size_t)g * kWWords + j];
-        const bool inv = ((w >> sub) & 1u) == 0u;
-        const size_t e = T.ca(g, 0, a);
-        tree_st(T.prior() + e, inv ? kWFMin : root_logits[(size_t)g * kDogA + a] - lm);
-        tree_st(T.index() + e, -1);
-        tree_st(T.visits() + e, 0);
-        tree_st(T.value() + e, 0.f);
-        tree_st(T.reward() + e, 0.f);
-        tree_st(T.disc() + e, 0.f);
-        gpw(T.gum)[(size_t)g * kWPad + a] =
+        const float gm =
             gumbel_in ? gumbel_in[(size_t)g * kDogA + a] : sa.gumbel_scale * gumbel_noise(sa.seed, gid, gturn, a);
+        gpw(T.gum)[(size_t)g * kWPad + a] = gm + (pr[j] - pm);
       }
     }
     AS1 float* e0 = T.e(g, 0);
@@ -306,13 +359,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
   }
   __syncthreads();
 
-  // (drawn once above: hashing the 806 draws inside the simulation loop made the compiler hoist their per-slot
-  // constants out of it, 52 VGPRs live across the networks)
-  auto gumbel_of = [&](int a) -> float { return tree_ld(gpw(T.gum) + (size_t)g * kWPad + a); };
+  // (the noise is drawn once above: hashing the 806 draws inside the simulation loop made the compiler hoist their
+  // per-slot constants out of it, 52 VGPRs live across the networks)
   auto legal_of = [&](int j) -> bool { return (s_legal[row][j] >> sub) & 1u; };
 
   Pf pf;
   pf_issue<NT256>(pf, &kernarg0<muz_dog_net_w>()->dyn.d3, LAT, LAT);
+  st_begin();
 #pragma unroll 1
   for (int sim = 0; sim < sa.S; ++sim) {
     const AS4 muz_dog_net_w* wl = kernarg0<muz_dog_net_w>();
@@ -329,38 +382,53 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
 #ifdef MUZ_DOG_EXPT_NOSELECT   // timing experiment only (wrong results): a fixed child, no node load
         bi = (node * 131 + sim * 7 + depth) % kDogA;
         if (false) {
+#elif defined(MUZ_DOG_EXPT_LOADONLY)   // timing experiment only: the node load + transform, a fixed child
+        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa);
+        bi = (node * 131 + sim * 7 + depth + (nd.sv & 1)) % kDogA;
+        if (false) {
 #else
         wnode_load(nd, T, g, node, sub, s_raw[row][node], sa);
         if (depth == 0) {
 #endif
           // gumbel_muzero_root_action_selection: score_considered + masked_argmax
           const int cv = wconsidered_visit(ncons, sa.S, nd.sv);
-          bi = wargmax([&](int j) {
-            const int a = sub + kRowLanes * j;
-            if (!wok(sub, j) || !legal_of(j)) return -INFINITY;
-            return fmaxf(-1e9f, gumbel_of(a) + (nd.pr[a] - nd.pm) + nd.cq[a]) + (nd.vis[j] == cv ? 0.f : -INFINITY);
-          }, sub);
+          bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, cv, legal_of);
         } else {
           // gumbel_muzero_interior_action_selection: softmax(prior + cq) - N / (1 + sum N)
+          // (z = prior + cq, then its exponential, replace the priors in LDS: one exp per child)
           float zm = -INFINITY;
 #pragma unroll
-          for (int j = 0; j < kWJ; ++j)
-            if (wok(sub, j)) zm = fmaxf(zm, nd.pr[sub + kRowLanes * j] + nd.cq[sub + kRowLanes * j]);
+          for (int j = 0; j < kWJ; ++j) {
+            const int a = sub + kRowLanes * j;
+            if (a < kDogA) {
+              const float z = nd.pr[a] + nd.cq[a];
+              nd.pr[a] = z;
+              zm = fmaxf(zm, z);
+            }
+          }
           zm = row_max(zm);
-          auto z = [&](int j) { return (nd.pr[sub + kRowLanes * j] + nd.cq[sub + kRowLanes * j]) - zm; };
-          const float zs = wsum([&](int j) { return wok(sub, j) ? exp_cr_w(z(j)) : -0.0f; });
+          const float zs = wsum([&](int j) {
+            const int a = sub + kRowLanes * j;
+            if (a >= kDogA) return -0.0f;
+            const float ez = exp_cr_w(nd.pr[a] - zm);
+            nd.pr[a] = ez;
+            return ez;
+          });
           const float inv_n = (float)(1 + nd.sv);
           bi = wargmax([&](int j) {
-            return wok(sub, j) ? (exp_cr_w(z(j)) / zs - (float)nd.vis[j] / inv_n) : -INFINITY;
+            const int a = sub + kRowLanes * j;
+            return a < kDogA ? (nd.pr[a] / zs - (float)nd.vis[j] / inv_n) : -INFINITY;
           }, sub);
         }
+        ST(ST_SEL);   // (diagnostic builds: scores + argmax)
         const size_t eb = T.ca(g, node, bi);
         const int child = tree_ld(T.index() + eb);
         if (sub == 0) {
+          const f32x4 c4 = tree_ld(T.node4() + eb);
           p_node[row][depth] = node;
           p_act[row][depth] = bi;
-          p_rew[row][depth] = tree_ld(T.reward() + eb);
-          p_disc[row][depth] = tree_ld(T.disc() + eb);
+          p_rew[row][depth] = c4[2];
+          p_disc[row][depth] = c4[3];
           p_cvis[row][depth] = tree_ld(T.visits() + eb);
         }
         act = bi;
@@ -381,41 +449,41 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
       din = dyn_load(wl->dyn, kDogA, nullptr, 0);
       if (sub == 0) s_act[row] = 0;
     }
+    ST(ST_SEL);
     SYNC();
     // ---------------- expand: recurrent_fn on the 16 parents; the 806 prior logits go to the new nodes' children
     const int nx = s_next[row];
+    if (valid && nx == sim + 1) {   // a new node: its children start unvisited (their priors follow below)
+#pragma unroll
+      for (int j = 0; j < kWJ; ++j) {
+        const int a = sub + kRowLanes * j;
+        if (a < kDogA) {
+          const size_t e = T.ca(g, nx, a);
+          tree_st(T.node4() + e, f32x4{0.f, 0.f, 0.f, 0.f});
+          tree_st(T.index() + e, -1);
+          tree_st(T.visits() + e, 0);
+        }
+      }
+    }
+    ST(ST_TREE);
     dyn16<NT256, true, false>(wl->dyn, kDogA, din, dact, ar, pf, &wl->pred.rb[0].d0, LAT, LAT, &wl->pred.ln0,
                               valid ? T.e(g, nx) : nullptr);
     pred16<NT256, true, false, false, NT256, true>(wl->pred, kDogA, ar.T, ar, pf, nullptr, 0, 0);
     // (the hand-out re-reads the new node from LDS: with `nx` itself the compiler precomputed the 806 store
     // addresses before the networks and spilled them)
     dog_logits16<NT256>(wl, ar, pf, [&](int r, int col, float v) {
-      if (valid) tree_st(T.prior() + T.ca(g0 + r, s_next[r], col), v);
+      if (valid) tree_st(T.fld(T.ca(g0 + r, s_next[r], col), 0), v);
     }, &wl->dyn.d3, LAT, LAT);
     if (valid) {
       const int nx = s_next[row];
       const bool fresh = nx == sim + 1;
-      if (fresh) {
-#pragma unroll
-        for (int j = 0; j < kWJ; ++j) {
-          const int a = sub + kRowLanes * j;
-          if (a < kDogA) {
-            const size_t e = T.ca(g, nx, a);
-            tree_st(T.index() + e, -1);
-            tree_st(T.visits() + e, 0);
-            tree_st(T.value() + e, 0.f);
-            tree_st(T.reward() + e, 0.f);
-            tree_st(T.disc() + e, 0.f);
-          }
-        }
-      }
       const int par = s_parent[row], pa = s_act[row];
       const float v = ar.v0[row], rw = ar.v1[row], dc = ar.v2[row];
       if (sub == 0) {
         const size_t eb = T.ca(g, par, pa);
         tree_st(T.index() + eb, nx);
-        tree_st(T.reward() + eb, rw);
-        tree_st(T.disc() + eb, dc);
+        tree_st(T.fld(eb, 2), rw);
+        tree_st(T.fld(eb, 3), dc);
         s_raw[row][nx] = v;
         s_val[row][nx] = v;
         s_visits[row][nx] = fresh ? 1 : s_visits[row][nx] + 1;
@@ -452,7 +520,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         const float child_v = (sub == top) ? carry_v : pv_up;
         if (on) {
           const size_t ei = T.ca(g, parent, pact);
-          tree_st(T.value() + ei, child_v);
+          tree_st(T.fld(ei, 1), child_v);
           tree_st(T.visits() + ei, cvis + 1);
           s_val[row][parent] = pv;
           s_visits[row][parent] = cnt + 1;
@@ -461,8 +529,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         carry_v = __shfl(pv, 0, kRowLanes);
       }
     }
+    ST(ST_TREE);
     SYNC();
   }
+  st_end();
 
   // ---------------- final action + action_weights (policies.py gumbel_muzero_policy tail)
   if (valid) {
@@ -470,30 +540,36 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     nd.pr = smem + row * kDogA;
     nd.cq = smem + (kRows + row) * kDogA;
     wnode_load(nd, T, g, 0, sub, s_raw[row][0], sa);
-    const int bi = wargmax([&](int j) {
-      const int a = sub + kRowLanes * j;
-      if (!wok(sub, j) || !legal_of(j)) return -INFINITY;
-      return fmaxf(-1e9f, gumbel_of(a) + (nd.pr[a] - nd.pm) + nd.cq[a]) +
-             (nd.vis[j] == nd.mv ? 0.f : -INFINITY);   // considered_visit = max(visit_counts)
-    }, sub);
+    const int bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, nd.mv, legal_of);   // considered_visit = max(visits)
     // action_weights = softmax(_mask_invalid_actions(prior + completed_q))
     float zm = -INFINITY;
 #pragma unroll
     for (int j = 0; j < kWJ; ++j)
       if (wok(sub, j)) zm = fmaxf(zm, nd.pr[sub + kRowLanes * j] + nd.cq[sub + kRowLanes * j]);
     zm = row_max(zm);
-    auto zz = [&](int j) {
-      return !legal_of(j) ? kWFMin : (nd.pr[sub + kRowLanes * j] + nd.cq[sub + kRowLanes * j]) - zm;
-    };
     float mm = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < kWJ; ++j)
-      if (wok(sub, j)) mm = fmaxf(mm, zz(j));
+    for (int j = 0; j < kWJ; ++j) {
+      const int a = sub + kRowLanes * j;
+      if (a < kDogA) {
+        const float zz = !legal_of(j) ? kWFMin : (nd.pr[a] + nd.cq[a]) - zm;
+        nd.pr[a] = zz;
+        mm = fmaxf(mm, zz);
+      }
+    }
     mm = row_max(mm);
-    const float zs = wsum([&](int j) { return wok(sub, j) ? exp_cr_w(zz(j) - mm) : -0.0f; });
+    const float zs = wsum([&](int j) {
+      const int a = sub + kRowLanes * j;
+      if (a >= kDogA) return -0.0f;
+      const float ez = exp_cr_w(nd.pr[a] - mm);
+      nd.pr[a] = ez;
+      return ez;
+    });
 #pragma unroll
-    for (int j = 0; j < kWJ; ++j)
-      if (wok(sub, j)) out_weights[(size_t)g * kDogA + sub + kRowLanes * j] = exp_cr_w(zz(j) - mm) / zs;
+    for (int j = 0; j < kWJ; ++j) {
+      const int a = sub + kRowLanes * j;
+      if (a < kDogA) out_weights[(size_t)g * kDogA + a] = nd.pr[a] / zs;
+    }
     if (sub == 0) {
       out_action[g] = ncons > 0 ? bi : -1;   // no legal action: -1, the self-play loop's no_step
       out_value[g] = s_val[row][0];
@@ -554,5 +630,18 @@ int muz_dog_gumbel_search(const muz_dog_net_w* w, const muz_search_cfg* cfg, con
   return launch_dog_search(*w, sa, root_logits, root_value, root_embedding, legal, gumbel, n, workspace, action,
                            action_weights, root_value_out, (hipStream_t)stream);
 }
+
+#ifdef MUZ_STAMPS2
+// the per-category cycle totals of k_dog_search's diagnostic build (this translation unit's g_st2)
+int muz_diag_dog_stamps2(unsigned long long* host_out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_st2), sizeof(unsigned long long) * ST_N);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    unsigned long long z[ST_N] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_st2), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
 
 }  // extern "C"

@@ -1,9 +1,7 @@
-"""Per-phase shader-clock shares of the DOG actor kernel k_dog_play (diagnostic build with -DMUZ_DOG_STAMPS).
+"""Cycle shares inside k_dog_search (diagnostic build with -DMUZ_STAMPS2; thread 0 of each workgroup stamps).
 
-    make -C exploring-muzero-on-dog_amd/csrc BUILD=/tmp/build_dogst EXTRA=-DMUZ_DOG_STAMPS OUT=../variants/libmuz_dogst.so
-    MUZ_LIB=$PWD/exploring-muzero-on-dog_amd/variants/libmuz_dogst.so python profiles/diag_dog_stamps.py
-
-Thread 0 of every workgroup (one game) stamps each phase of every turn; cycles per game-turn."""
+    make -C exploring-muzero-on-dog_amd/csrc BUILD=build_st2 EXTRA=-DMUZ_STAMPS2 OUT=../variants/libmuz_st2.so
+    MUZ_LIB=$PWD/exploring-muzero-on-dog_amd/variants/libmuz_st2.so python profiles/diag_dog_stamps.py [B] [S] [D]"""
 import ctypes
 import os
 import sys
@@ -12,35 +10,45 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import muzpkg  # noqa: E402
 
 muzpkg.load()
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from exploring_muzero_on_dog_amd import dog as DG  # noqa: E402
 from exploring_muzero_on_dog_amd import lib as L  # noqa: E402
+from exploring_muzero_on_dog_amd import muzero_dog as MD  # noqa: E402
 
-CATS = ["reset", "base checks + barrier", "mask words + choice", "env_step (lane 0)", "barrier", "deal"]
+CATS = ["mfma-loops", "dense-epilogue", "barrier-wait", "row-ops", "select scores", "Q transform", "tree / backup",
+        "node loads + passes", "dense-entry"]
 
 
 def main():
     lib = L.load()
-    fn = lib.muz_diag_dog_stamps
+    fn = lib.muz_diag_dog_stamps2
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-    B, T, launches = 1024, 16, 20
-    rp = DG.RandomPlay(B, seed=4, fused=True)
-    steps = torch.zeros(B, dtype=torch.int32, device="cuda")
-    rp.play(T, steps, auto_reset=True)
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    S = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+    D = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+    net = MD.DeviceDogNet(MD.init_muzero_params(0))
+    rng = np.random.default_rng(0)
+    obs = torch.from_numpy(rng.integers(0, 3, (B, 34, 56)).astype(np.float32)).cuda()
+    lg, v, e = MD.root_inference_fn(net, obs)
+    valid = torch.from_numpy(rng.random((B, 806)) < 0.1)
+    words = MD.invalid_to_words(~valid).cuda()
+    ws = MD.SearchWorkspace(B, S)
+    MD.gumbel_muzero_policy(net, lg, v, e, words, S, D, 1.0, seed=1, workspace=ws)
     torch.cuda.synchronize()
-    buf = (ctypes.c_uint64 * 8)()
+    buf = (ctypes.c_uint64 * 12)()
     fn(buf, 1)
-    for _ in range(launches):
-        rp.play(T, steps, auto_reset=True)
+    reps = 2
+    for r in range(reps):
+        MD.gumbel_muzero_policy(net, lg, v, e, words, S, D, 1.0, seed=r, workspace=ws)
     torch.cuda.synchronize()
     fn(buf, 0)
-    tot = sum(buf[i] for i in range(6))
-    turns = B * T * launches
-    print(f"B={B}: {tot / turns:.0f} cycles per game-turn (thread 0 of each game's workgroup)")
+    tot = sum(buf[i] for i in range(12))
+    wg_sims = reps * ((B + 15) // 16) * S
+    print(f"B={B} S={S} D={D}: {tot / wg_sims:.0f} cycles per workgroup-simulation")
     for i, c in enumerate(CATS):
-        print(f"{c:>24}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / turns:8.0f} cycles/turn")
+        print(f"{c:>20}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / wg_sims:9.0f} cycles/sim")
 
 
 if __name__ == "__main__":
