@@ -206,6 +206,77 @@ class _Dense(torch.autograd.Function):
         return dx, dW, db
 
 
+HEAD_PARAMS = ("prediction/Dense_2/kernel", "prediction/Dense_2/bias", "prediction/Dense_4/kernel",
+               "prediction/Dense_4/bias", "prediction/Dense_5/kernel", "prediction/Dense_5/bias",
+               "dynamics/Dense_6/kernel", "dynamics/Dense_6/bias", "dynamics/reward_head/kernel",
+               "dynamics/reward_head/bias", "dynamics/Dense_7/kernel", "dynamics/Dense_7/bias",
+               "dynamics/discount_head/kernel", "dynamics/discount_head/bias")
+
+
+class _OutHeads(torch.autograd.Function):
+    """The output heads of one unrolled batch as one launch each way (csrc/learner_heads.hip, muz_heads_fwd / _bwd):
+    PredictionNetwork4's policy logits (Dense_2) and value head (Dense_4 -> relu -> Dense_5 -> tanh) over the K + 1
+    steps' policy / value hidden layers, DynamicsNetwork4's reward / discount heads (Dense_6 | Dense_7 -> relu ->
+    reward_head | discount_head) over the K steps' [next latent, one_hot(action)] (muzero_deterministic_madn.py:
+    437-455, 572-583).  As library GEMMs, bias adds and activations: ~18 launches forward, ~20 backward.  Weight /
+    bias gradients: X^T dz and column sums, recorded into the active GradSink (grouped launches) or formed here.
+    -> (logits [R, A], value [R, 1], reward logits [Rk, 3], discount logits [Rk, 3])."""
+
+    @staticmethod
+    def forward(ctx, pol_h, v_h, head_in, onehot, *params):
+        W2, b2, W4, b4, W5, b5, W6, b6, Wr, br, W7, b7, Wd, bd = params
+        R, A, Rk = pol_h.shape[0], W2.shape[1], head_in.shape[0]
+        dev, dt = pol_h.device, pol_h.dtype
+        pol_h, v_h, head_in, onehot = (t.contiguous() for t in (pol_h, v_h, head_in, onehot))
+        emp = lambda *shape: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
+        logits, value, h4 = emp(R, A), emp(R, 1), emp(R, 64)
+        rl, dl, h6, h7, ri = emp(Rk, 3), emp(Rk, 3), emp(Rk, 64), emp(Rk, 64), emp(Rk, 256 + A)
+        a = _L.MuzHeadsArgs()
+        a.R, a.Rk, a.A = R, Rk, A
+        for k, t in zip(("pol_h", "v_h", "head_in", "onehot", "W2", "b2", "W4", "b4", "W5", "b5", "W6", "b6", "Wr",
+                         "br", "W7", "b7", "Wd", "bd", "logits", "value", "h4", "rl", "dl", "h6", "h7", "ri"),
+                        (pol_h, v_h, head_in, onehot, *params, logits, value, h4, rl, dl, h6, h7, ri)):
+            setattr(a, k, t.data_ptr())
+        _L.check(_L.load().muz_heads_fwd(ctypes.byref(a), _L.stream_ptr()), "muz_heads_fwd")
+        ctx.save_for_backward(pol_h, v_h, value, h4, h6, h7, ri, *params)
+        ctx.owners = params if all(p.is_leaf for p in params) else None
+        return logits, value, rl, dl
+
+    @staticmethod
+    def backward(ctx, g_logits, g_value, g_rl, g_dl):
+        pol_h, v_h, value, h4, h6, h7, ri, *params = ctx.saved_tensors
+        W2, b2, W4, b4, W5, b5, W6, b6, Wr, br, W7, b7, Wd, bd = params
+        R, A, Rk = pol_h.shape[0], W2.shape[1], ri.shape[0]
+        dev, dt = pol_h.device, pol_h.dtype
+        emp = lambda *shape: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
+        d_pol_h, d_v_h, d_head_in = emp(R, 128), emp(R, 128), emp(Rk, 256)
+        dz4, dv5, dz6, dz7 = emp(R, 64), emp(R, 1), emp(Rk, 64), emp(Rk, 64)
+        z = lambda t, *shape: torch.zeros(shape, dtype=dt, device=dev) if t is None else t.contiguous()  # noqa: E731
+        g_logits, g_value, g_rl, g_dl = z(g_logits, R, A), z(g_value, R, 1), z(g_rl, Rk, 3), z(g_dl, Rk, 3)
+        a = _L.MuzHeadsArgs()
+        a.R, a.Rk, a.A = R, Rk, A
+        for k, t in zip(("pol_h", "v_h", "W2", "b2", "W4", "b4", "W5", "b5", "W6", "b6", "Wr", "br", "W7", "b7", "Wd",
+                         "bd", "value", "h4", "h6", "h7", "ri", "g_logits", "g_value", "g_rl", "g_dl", "d_pol_h", "d_v_h",
+                         "d_head_in", "dz4", "dv5", "dz6", "dz7"),
+                        (pol_h, v_h, *params, value, h4, h6, h7, ri, g_logits, g_value, g_rl, g_dl, d_pol_h, d_v_h,
+                         d_head_in, dz4, dv5, dz6, dz7)):
+            setattr(a, k, t.data_ptr())
+        _L.check(_L.load().muz_heads_bwd(ctypes.byref(a), _L.stream_ptr()), "muz_heads_bwd")
+        # weight / bias gradients: (layer input, its dz) pairs
+        pairs = ((pol_h, g_logits), (v_h, dz4), (h4, dv5), (ri, dz6), (h6, g_rl), (ri, dz7), (h7, g_dl))
+        sink = _sink()
+        if sink is not None and ctx.owners is not None:
+            for (x, dz), W, b in zip(pairs, ctx.owners[0::2], ctx.owners[1::2]):
+                sink.wgrad(x, dz, W)
+                sink.colsum(dz, b)
+            grads = (None,) * 14
+        else:
+            grads = []
+            for (x, dz), W in zip(pairs, params[0::2]):
+                grads += [(x.t() @ dz).reshape(W.shape), dz.sum(0)]
+        return (d_pol_h, d_v_h, d_head_in, None, *grads)
+
+
 class _DenseMinmax(torch.autograd.Function):
     """minmax(x @ W + b) per row of 256 (RepresentationNetwork2's last layer, muzero_deterministic_madn.py:
     139-140): the library GEMM, then the bias add and the min-max scaling in one launch each way
@@ -544,6 +615,7 @@ def _backward(loss, sink):
 
 
 FUSED_LOSS = True      # False: the losses as torch ops (A/B timing, and the fused kernel's test reference)
+FUSED_HEADS = True     # False: the output heads as library GEMMs + torch activations (A/B timing, test reference)
 GROUPED_GRADS = True   # False: every weight / bias / LayerNorm gradient as its own launch (A/B timing)
 _SINK = None     # the active GradSink (module-global: autograd runs GPU backward nodes on its own thread)
 
@@ -1001,6 +1073,15 @@ class MuZeroNets:
         rl, dl = self.dynamics_heads(nxt, oh)
         return nxt, rl, dl
 
+    def prediction_hidden(self, latent):
+        """PredictionNetwork4 up to its heads: (policy hidden after LayerNorm_2, value hidden after LayerNorm_3)."""
+        p = "prediction"
+        x = self._ln(f"{p}/LayerNorm_0", latent)
+        x = self._rbs(f"{p}/ResBlock_", 2, x)
+        pol = self._dense_ln(f"{p}/Dense_0", f"{p}/LayerNorm_1", x)
+        pol = self._dense_ln(f"{p}/Dense_1", f"{p}/LayerNorm_2", pol)
+        return pol, self._dense_ln(f"{p}/Dense_3", f"{p}/LayerNorm_3", x)
+
     def prediction(self, latent):
         p = "prediction"
         x = self._ln(f"{p}/LayerNorm_0", latent)
@@ -1041,8 +1122,13 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
             raws.append(nxt)
             latents.append((nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale)   # gradient scaling (fwd identity)
         head_in = torch.cat(raws, 0) if K else None
-    logits_all, v_all = nets.prediction(torch.cat(latents, 0))
-    rl_all, dl_all = nets.dynamics_heads(head_in, oh) if K else (None, None)
+    if K and obs.is_cuda and FUSED_HEADS and nets.A <= 32:
+        pol_h, v_h = nets.prediction_hidden(torch.cat(latents, 0))
+        logits_all, v_all, rl_all, dl_all = _OutHeads.apply(pol_h, v_h, head_in, oh,
+                                                             *(nets.p[n] for n in HEAD_PARAMS))
+    else:
+        logits_all, v_all = nets.prediction(torch.cat(latents, 0))
+        rl_all, dl_all = nets.dynamics_heads(head_in, oh) if K else (None, None)
     if obs.is_cuda and FUSED_LOSS:
         u = 1.0 / unroll_steps
         spec = dict(batch=batch, K=K, scale_value=u * VALUE_SCALING, scale_policy=u * POLICY_SCALING, norm=0,

@@ -80,6 +80,13 @@ class MuzLossTerm(ctypes.Structure):
                 ("w_common", ctypes.c_float), ("scale", ctypes.c_float)]
 
 
+class MuzHeadsArgs(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int32) for k in ("R", "Rk", "A")] + [(k, vp) for k in (
+        "pol_h", "v_h", "head_in", "onehot", "W2", "b2", "W4", "b4", "W5", "b5", "W6", "b6", "Wr", "br", "W7", "b7",
+        "Wd", "bd", "logits", "value", "h4", "rl", "dl", "h6", "h7", "ri", "g_logits", "g_value", "g_rl", "g_dl",
+        "d_pol_h", "d_v_h", "d_head_in", "dz4", "dv5", "dz6", "dz7")]
+
+
 class MuzLossArgs(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int32) for k in ("K", "B", "A", "T", "nterms", "norm")] + \
         [(k, vp) for k in ("masks", "target_values", "policies", "value", "logits", "dvalue", "dlogits")] + \
@@ -366,6 +373,8 @@ SIGNATURES = {
     "muz_wgrad_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp, ctypes.c_int64, vp]),
     "muz_colsum_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp]),
     "muz_loss_heads": (ctypes.c_int, [vp, vp]),
+    "muz_heads_fwd": (ctypes.c_int, [ctypes.POINTER(MuzHeadsArgs), vp]),
+    "muz_heads_bwd": (ctypes.c_int, [ctypes.POINTER(MuzHeadsArgs), vp]),
     "muz_dense_ln_fwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, ctypes.c_int32, vp, vp, vp, vp,
                                         ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]),
     "muz_transpose_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp]),

@@ -783,6 +783,26 @@ typedef struct {
   int32_t* ticket;         /* a device counter, 0 before the launch (the kernel leaves it 0 again) */
 } muz_loss_args;
 int muz_loss_heads(const muz_loss_args* args, void* stream);
+/* The learner's output heads in one launch each way (csrc/learner_heads.hip): PredictionNetwork4's policy logits
+ * Dense_2 and value head Dense_4 -> relu -> Dense_5 -> tanh over R rows of the policy / value hidden layers
+ * (muzero_deterministic_madn.py:572-583), and DynamicsNetwork4's reward / discount heads Dense_6 | Dense_7 -> relu ->
+ * reward_head | discount_head over Rk rows of [next latent, one_hot(action)] (lines 437-455).  Forward fills logits
+ * [R][A], value [R], the saved relu outputs h4 [R][64], h6 / h7 [Rk][64], ri = [next latent, one_hot] [Rk][256 + A],
+ * rl / dl [Rk][3].  Backward (g_* nullable = zero) fills the input gradients d_pol_h / d_v_h [R][128], d_head_in
+ * [Rk][256] and the pre-activation gradients dz4 [R][64], dv5 [R], dz6 / dz7 [Rk][64] the weight gradients are
+ * formed from.  Weights row-major [in][out]; A <= 32. */
+typedef struct muz_heads_args {
+  int32_t R, Rk, A;
+  const float* pol_h; const float* v_h; const float* head_in; const float* onehot;
+  const float* W2; const float* b2; const float* W4; const float* b4; const float* W5; const float* b5;
+  const float* W6; const float* b6; const float* Wr; const float* br; const float* W7; const float* b7;
+  const float* Wd; const float* bd;
+  float* logits; float* value; float* h4; float* rl; float* dl; float* h6; float* h7; float* ri;
+  const float* g_logits; const float* g_value; const float* g_rl; const float* g_dl;
+  float* d_pol_h; float* d_v_h; float* d_head_in; float* dz4; float* dv5; float* dz6; float* dz7;
+} muz_heads_args;
+int muz_heads_fwd(const muz_heads_args* args, void* stream);
+int muz_heads_bwd(const muz_heads_args* args, void* stream);
 /* One launch per learner layer (csrc/learner_fused.hip): muz_dense_ln_fwd = muz_ln_fwd(x @ W, ...) with the GEMM
  * fused in (x [M][K], W [K][N] row-major, K <= 512, N in {32, 64, 128, 256}; same outputs out / z / mean / rstd);
  * muz_dense_ln_bwd = muz_ln_bwd_rows followed by dx = dz W^T (+ acc) (dx [M][K]; dx null: no input gradient),

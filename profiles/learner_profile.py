@@ -58,6 +58,11 @@ lr0 = L.Learner(params, C, unroll_steps=10, graph=True)
 timed("train_step (graph replay, fixed batch, ResBlock stack kernel and node off)", lambda: lr0.train_step(batch))
 L.RESBLOCK_NODE = L.RESBLOCK_STACK = True
 del lr0
+L.FUSED_HEADS = False
+lr0 = L.Learner(params, C, unroll_steps=10, graph=True)
+timed("train_step (graph replay, fixed batch, fused output heads off)", lambda: lr0.train_step(batch))
+L.FUSED_HEADS = True
+del lr0
 lr = L.Learner(params, C, unroll_steps=10, graph=True)
 timed("sample_batch", ring.sample_batch)
 timed("train_step (graph replay, fixed batch)", lambda: lr.train_step(batch))

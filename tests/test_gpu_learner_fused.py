@@ -424,3 +424,36 @@ def test_dense_ln_host_checks(cuda):
                                 L.ptr(o), L.ptr(o), L.ptr(m), L.ptr(m), L.stream_ptr()) != 0
     assert lib.muz_dense_ln_fwd(L.ptr(x), 16, 500, L.ptr(W), None, 0, L.ptr(v), L.ptr(v), L.ptr(v), None, 256, 2, L.ptr(o),
                                 L.ptr(o), L.ptr(m), L.ptr(m), L.stream_ptr()) != 0
+
+
+def test_fused_output_heads_match_library_form(cuda):
+    """learner.FUSED_HEADS (_OutHeads: the policy / value / reward / discount heads as one launch each way,
+    csrc/learner_heads.hip) against the same heads as library GEMMs + torch activations: the loss within 1e-6
+    relative (k-order fp32 sums instead of BLAS order) and every parameter gradient within 1e-5 relative, with the
+    grouped (GradSink) and the per-parameter gradient paths, eager and graph-captured."""
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import game_agent as GA
+    from exploring_muzero_on_dog_amd import learner as L
+    from exploring_muzero_on_dog_amd import nets as N
+    from exploring_muzero_on_dog_amd import replay as R
+    from oracle import nets as ON
+    C = E.num_channels(4)
+    params = ON.init_params(C, seed=14, randomize_affine=True)
+    eng = GA.SelfPlayEngine(N.DeviceNet(params, C), 32, num_players=4, max_steps=120, num_simulations=4, max_depth=4)
+    ring = R.VectorizedReplayBuffer(512, 48, 5, 10, obs_shape=(C, 56), max_episode_length=120,
+                                    rng=np.random.RandomState(2))
+    ring.save_games_from_buffers(eng.play_stream(40, seed=2, temperature=1.0))
+    batch = ring.sample_batch()
+    old = L.FUSED_HEADS
+    try:
+        for grouped, graph in ((True, False), (False, False), (True, True)):
+            L.FUSED_HEADS = True
+            la, ga = _grads(L.Learner, params, C, batch, grouped, graph=graph)
+            L.FUSED_HEADS = False
+            lb, gb = _grads(L.Learner, params, C, batch, grouped, graph=graph)
+            assert abs(la - lb) <= 1e-6 * abs(lb), (grouped, graph, la, lb)
+            worst = max(float((ga[k] - gb[k]).norm()) / max(float(gb[k].norm()), 1e-20) for k in ga)
+            print(f"fused heads grouped={grouped} graph={graph}: loss {la:.7f} vs {lb:.7f}, worst grad rel {worst:.2e}")
+            assert worst < 1e-5, (grouped, graph, worst)
+    finally:
+        L.FUSED_HEADS = old
