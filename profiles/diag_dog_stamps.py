@@ -51,5 +51,36 @@ def main():
         print(f"{c:>20}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / wg_sims:9.0f} cycles/sim")
 
 
+def selfplay(turns=6):
+    """The same shares over DogSelfPlay turns (real states and legal masks, the bench's setting)."""
+    from exploring_muzero_on_dog_amd import game_agent_dog as GA
+    lib = L.load()
+    fn = lib.muz_diag_dog_stamps2
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    B, S, D = 1024, 100, 50
+    net = MD.DeviceDogNet(MD.init_muzero_params(2))
+    sp = GA.DogSelfPlay(net, B, S, D, 1.0, seed=4)
+    sp.play(2)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_uint64 * 12)()
+    fn(buf, 1)
+    depth = []
+    sp.play(turns)
+    torch.cuda.synchronize()
+    fn(buf, 0)
+    tot = sum(buf[i] for i in range(12))
+    wg_sims = turns * ((B + 15) // 16) * S
+    print(f"DogSelfPlay B={B} S={S} D={D}, {turns} turns: {tot / wg_sims:.0f} cycles per workgroup-simulation")
+    for i, c in enumerate(CATS):
+        print(f"{c:>20}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / wg_sims:9.0f} cycles/sim")
+    words = sp.words.cpu().numpy().view(np.uint32)
+    nleg = np.array([sum(bin(int(w)).count("1") for w in row) for row in words])
+    print(f"legal actions per game: mean {nleg.mean():.1f}, max {nleg.max()}, phase-1 games {int(sp.env.phase.sum())}")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "selfplay":
+        selfplay()
+    else:
+        main()
