@@ -193,8 +193,11 @@ struct WNode {
   int sv, mv;    // sum / max of the visit counts
 };
 
+// ces: this row's per-node sum of exp(prior - max prior) (the softmax normaliser of the node's prior
+// probabilities), computed at the node's first walk and kept until the node is expanded again -- its priors do not
+// change in between, so the 806 exponentials are not recomputed at every visit (< 0: not cached).
 __device__ __forceinline__ void wnode_load(WNode& nd, const WTree& T, int g, int node, int sub, float raw,
-                                           const SearchArgs& sa) {
+                                           const SearchArgs& sa, float* ces) {
 #pragma clang fp contract(off)
   float pm = -INFINITY;
   int sv = 0, mv = 0;
@@ -230,7 +233,11 @@ __device__ __forceinline__ void wnode_load(WNode& nd, const WTree& T, int g, int
   pm = row_max(pm);
   sv = row_isum(sv);
   mv = row_imax(mv);
-  const float es = wsum([&](int j) { return wok(sub, j) ? exp_cr_w(nd.pr[sub + kRowLanes * j] - pm) : -0.0f; });
+  float es = ces[node];
+  if (es < 0.f) {   // (row-uniform)
+    es = wsum([&](int j) { return wok(sub, j) ? exp_cr_w(nd.pr[sub + kRowLanes * j] - pm) : -0.0f; });
+    if (sub == 0) ces[node] = es;
+  }
   // The mixed value needs the prior probabilities of the VISITED children only: sum_probs and weighted_q are summed
   // over this lane's visited slots (a bit mask, in slot order) -- the unvisited ones add exact zeros in the
   // restatement's order (lane_tree_sum), which change no partial sum -- so their exponentials are not recomputed.
@@ -293,6 +300,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
   __shared__ float p_rew[kRows][kWMaxDepth];
   __shared__ float p_disc[kRows][kWMaxDepth];
   __shared__ uint32_t s_legal[kRows][kWWords];
+  __shared__ float s_ces[kRows][kWMaxNodes];   // per-node softmax normalisers of the priors (wnode_load)
   __shared__ int s_act[kRows], s_parent[kRows], s_next[kRows], s_depth[kRows];
 
   if ((int)blockIdx.x * kRows >= n) return;
@@ -348,6 +356,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         gpw(T.gum)[(size_t)g * kWPad + a] = gm + (pr[j] - pm);
       }
     }
+    for (int i = sub; i < kWMaxNodes; i += kRowLanes) s_ces[row][i] = -1.f;
     AS1 float* e0 = T.e(g, 0);
     for (int c = sub; c < LAT; c += kRowLanes) e0[c] = root_emb[(size_t)g * LAT + c];
     if (sub == 0) {
@@ -383,11 +392,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         bi = (node * 131 + sim * 7 + depth) % kDogA;
         if (false) {
 #elif defined(MUZ_DOG_EXPT_LOADONLY)   // timing experiment only: the node load + transform, a fixed child
-        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa);
+        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa, s_ces[row]);
         bi = (node * 131 + sim * 7 + depth + (nd.sv & 1)) % kDogA;
         if (false) {
 #else
-        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa);
+        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa, s_ces[row]);
         if (depth == 0) {
 #endif
           // gumbel_muzero_root_action_selection: score_considered + masked_argmax
@@ -486,6 +495,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         tree_st(T.fld(eb, 3), dc);
         s_raw[row][nx] = v;
         s_val[row][nx] = v;
+        s_ces[row][nx] = -1.f;   // new priors: the node's normaliser is recomputed at its next walk
         s_visits[row][nx] = fresh ? 1 : s_visits[row][nx] + 1;
       }
       // ---------------- backward along the recorded path, one level per lane (search.hip's scheme; the root's
@@ -539,7 +549,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     WNode nd;
     nd.pr = smem + row * kDogA;
     nd.cq = smem + (kRows + row) * kDogA;
-    wnode_load(nd, T, g, 0, sub, s_raw[row][0], sa);
+    wnode_load(nd, T, g, 0, sub, s_raw[row][0], sa, s_ces[row]);
     const int bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, nd.mv, legal_of);   // considered_visit = max(visits)
     // action_weights = softmax(_mask_invalid_actions(prior + completed_q))
     float zm = -INFINITY;
