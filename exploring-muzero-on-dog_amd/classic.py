@@ -130,11 +130,18 @@ def _call(name, *args):
 
 
 def env_reset(batch: int, num_players=4, layout=(True, True, True, True), distance=10, starting_player=0,
-              device="cuda", **rules) -> ClassicMADNState:
-    """Batched env_reset (classic_madn.py:51-131)."""
+              device="cuda", seeds=None, **rules) -> ClassicMADNState:
+    """Batched env_reset (classic_madn.py:51-131); ``seeds`` as detmadn.env_reset (a random starting player)."""
     r = make_rules(num_players, layout, distance, starting_player, **rules)
     st = _alloc(batch, int(num_players), r, device)
-    _call("muz_classic_reset", r, st.soa(), batch, _L.stream_ptr())
+    if seeds is None:
+        _call("muz_classic_reset", r, st.soa(), batch, _L.stream_ptr())
+    else:
+        sd = torch.as_tensor(np.asarray(seeds, np.int64) & 0xFFFFFFFF).to(torch.int64)
+        sd = (sd - ((sd >> 31) << 32)).to(device=device, dtype=torch.int32).contiguous()
+        if sd.numel() != batch:
+            raise ValueError("one seed per game")
+        _call("muz_classic_reset_seeded", r, st.soa(), _L.ptr(sd), batch, _L.stream_ptr())
     return st
 
 

@@ -149,7 +149,7 @@ int check_dog_net(const muz_dog_net_w* w) {
 }
 
 int dog_muzero_consts(const muz_rules* rules, DetConsts* c) {
-  int rc = make_det_consts(rules, c);
+  int rc = make_det_consts(rules, c, true);
   if (rc) return rc;
   if (c->P != 4) return MUZ_E_UNSUPPORTED;   // the slice plays config (d): 4-player DOG
   if (rules->disable_swapping || rules->disable_hot_seven || rules->disable_joker) return MUZ_E_UNSUPPORTED;

@@ -2,12 +2,14 @@
 // One board per lane; 256-lane workgroups; the lane's board is staged in LDS.
 #include "classic.hpp"
 #include "host_consts.hpp"
+#include "rng.hpp"
 
 namespace muz {
 
 constexpr int kClsBlock = 256;
 
-__global__ __launch_bounds__(kClsBlock) void k_cls_reset(DetConsts c, muz_classic_soa st, int n) {
+__global__ __launch_bounds__(kClsBlock) void k_cls_reset(DetConsts c, muz_classic_soa st, int n,
+                                                       const int32_t* seeds = nullptr) {
   const int g = blockIdx.x * kClsBlock + threadIdx.x;
   if (g >= n) return;
   const int S = st.stride;
@@ -17,7 +19,8 @@ __global__ __launch_bounds__(kClsBlock) void k_cls_reset(DetConsts c, muz_classi
     for (int k = 0; k < 4; ++k) st.pins[(p * 4 + k) * S + g] = (int8_t)((fp && k == 0) ? c.start[p] : -1);
     if (fp) st.board[c.start[p] * S + g] = (int8_t)p;
   }
-  st.current_player[g] = (int8_t)c.starting_player;
+  st.current_player[g] =
+      (int8_t)(c.starting_player >= 0 ? c.starting_player : start_seat((unsigned long long)(uint32_t)seeds[g], c.P));
   st.reward[g] = 0;
   st.done[g] = 0;
   st.die[g] = 0;
@@ -135,6 +138,17 @@ extern "C" {
 int muz_classic_reset(const muz_rules* rules, muz_classic_soa st, int32_t n, void* stream) {
   CLS_PROLOGUE(true)
   k_cls_reset<<<cls_blocks(n), kClsBlock, 0, (hipStream_t)stream>>>(c, st, n);
+  return muz_last_launch_error();
+}
+
+int muz_classic_reset_seeded(const muz_rules* rules, muz_classic_soa st, const int32_t* seeds, int32_t n,
+                             void* stream) {
+  DetConsts c;
+  int rc = make_det_consts(rules, &c, true);
+  if (rc) return rc;
+  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && seeds);
+  if (n == 0) return MUZ_OK;
+  k_cls_reset<<<cls_blocks(n), kClsBlock, 0, (hipStream_t)stream>>>(c, st, n, seeds);
   return muz_last_launch_error();
 }
 

@@ -8,7 +8,8 @@ namespace muz {
 
 constexpr int kEnvBlock = 256;
 
-__global__ __launch_bounds__(kEnvBlock) void k_det_reset(DetConsts c, muz_detmadn_soa st, int n) {
+__global__ __launch_bounds__(kEnvBlock) void k_det_reset(DetConsts c, muz_detmadn_soa st, int n,
+                                                       const int32_t* seeds = nullptr) {
   const int g = blockIdx.x * kEnvBlock + threadIdx.x;
   if (g >= n) return;
   const int S = st.stride;
@@ -19,7 +20,8 @@ __global__ __launch_bounds__(kEnvBlock) void k_det_reset(DetConsts c, muz_detmad
     for (int m = 0; m < 6; ++m) st.action_set[(p * 6 + m) * S + g] = 4;
     if (fp) st.board[c.start[p] * S + g] = (int8_t)p;
   }
-  st.current_player[g] = (int8_t)c.starting_player;
+  st.current_player[g] =
+      (int8_t)(c.starting_player >= 0 ? c.starting_player : start_seat((unsigned long long)(uint32_t)seeds[g], c.P));
   st.reward[g] = 0;
   st.done[g] = 0;
 }
@@ -425,6 +427,17 @@ int muz_detmadn_reset(const muz_rules* rules, muz_detmadn_soa st, int32_t n, voi
   MUZ_HOST_CHECK(n >= 0 && st.stride >= n);
   if (n == 0) return MUZ_OK;
   k_det_reset<<<nblocks(n, kEnvBlock), kEnvBlock, 0, (hipStream_t)stream>>>(c, st, n);
+  return muz_last_launch_error();
+}
+
+int muz_detmadn_reset_seeded(const muz_rules* rules, muz_detmadn_soa st, const int32_t* seeds, int32_t n,
+                             void* stream) {
+  DetConsts c;
+  int rc = make_det_consts(rules, &c, true);
+  if (rc) return rc;
+  MUZ_HOST_CHECK(n >= 0 && st.stride >= n && seeds);
+  if (n == 0) return MUZ_OK;
+  k_det_reset<<<nblocks(n, kEnvBlock), kEnvBlock, 0, (hipStream_t)stream>>>(c, st, n, seeds);
   return muz_last_launch_error();
 }
 

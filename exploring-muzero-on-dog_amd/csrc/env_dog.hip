@@ -668,7 +668,7 @@ __device__ void dog_reset_lds(const DetConsts& c, DogG& s, unsigned long long se
   if (tid < kDogCards) s.deck[tid] = tid == 0 ? 6 : 8;   // env_reset: joker 6, others 8 (dog.py:143-145)
   if (tid < 4) s.swap_choices[tid] = -1;
   if (tid == 0) {
-    s.cp = c.starting_player;
+    s.cp = c.starting_player >= 0 ? c.starting_player : start_seat(game_key(seed, g, (int)deal), c.P);
     s.round_starter = -1;
     s.phase = 0;
     s.hand_size = 6;
@@ -1110,7 +1110,7 @@ __global__ __launch_bounds__(256) void k_dog_random_action(const uint32_t* mask,
 }
 
 static int dog_consts(const muz_rules* rules, DetConsts* c) {
-  int rc = make_det_consts(rules, c);
+  int rc = make_det_consts(rules, c, true);   // every DOG reset has its seed (muz_dog_reset, the in-place restarts)
   if (rc) return rc;
   if (rules->disable_swapping || rules->disable_hot_seven || rules->disable_joker) return MUZ_E_UNSUPPORTED;
   return MUZ_OK;

@@ -5,12 +5,16 @@
 
 namespace muz {
 
-static inline int make_det_consts(const muz_rules* r, DetConsts* c) {
+// allow_random_start: the entry point can draw a random starting player (env_reset's starting_player < 0 or >= P,
+// deterministic_madn.py:60-62, classic_madn.py:70-72, dog.py:102-104) -- it has a reset seed; c->starting_player is
+// then -1 and the reset kernels draw the seat (rng.hpp start_seat).  Elsewhere such rules are MUZ_E_UNSUPPORTED.
+static inline int make_det_consts(const muz_rules* r, DetConsts* c, bool allow_random_start = false) {
   if (!r || !c) return MUZ_E_INVALID;
   const int P = r->num_players;
   if (P < 2 || P > 4) return MUZ_E_UNSUPPORTED;
   if (r->distance != kDist) return MUZ_E_UNSUPPORTED;
-  if (r->starting_player < 0 || r->starting_player >= P) return MUZ_E_UNSUPPORTED;
+  const bool random_start = r->starting_player < 0 || r->starting_player >= P;
+  if (random_start && !allow_random_start) return MUZ_E_UNSUPPORTED;
   bool layout[4];
   int nset = 0, nall = 1;
   for (int i = 0; i < 4; ++i) {
@@ -21,7 +25,7 @@ static inline int make_det_consts(const muz_rules* r, DetConsts* c) {
   if (nset != P || (nall && P < 4))
     for (int i = 0; i < 4; ++i) layout[i] = i < P;
   c->P = P;
-  c->starting_player = r->starting_player;
+  c->starting_player = random_start ? -1 : r->starting_player;
   uint32_t f = 0;
   if (r->enable_teams && P == 4) f |= R_TEAMS;
   if (r->enable_initial_free_pin) f |= R_FREE_PIN;

@@ -20,6 +20,15 @@ __device__ __forceinline__ unsigned long long game_key(unsigned long long seed, 
 // U[0, 1) on a 24-bit grid
 __device__ __forceinline__ float u24(unsigned long long h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
 
+// env_reset's random starting player (deterministic_madn.py:60-62, classic_madn.py:70-72, dog.py:102-104: jax
+// randint(split(PRNGKey(seed))[1], (), 0, P); threefry is not restated): seat floor(U * P) of the counter RNG of the
+// reset's key (det / classic: the game's seed; DOG: game_key(seed, game, deal counter)).
+constexpr unsigned long long kStartStream = 0x57A27C0DE5ull;
+__device__ __forceinline__ int start_seat(unsigned long long key, int P) {
+  const int s = (int)(u24(mix64(key ^ kStartStream)) * (float)P);
+  return s < P ? s : P - 1;
+}
+
 // jax.random.gumbel semantics on the counter RNG: -log(-log(U[tiny, 1)))
 __device__ __forceinline__ float gumbel_noise(unsigned long long seed, int gid, int turn, int a) {
   const unsigned long long h = mix64(game_key(seed, gid, turn) ^ (unsigned long long)(a + 1) * 0xD6E8FEB86659FD93ull);

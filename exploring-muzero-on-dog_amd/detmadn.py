@@ -132,12 +132,22 @@ def _alloc(batch: int, P: int, rules, device) -> DetMADNState:
 
 
 def env_reset(batch: int, num_players=4, layout=(True, True, True, True), distance=10, starting_player=0,
-              device="cuda", **rules) -> DetMADNState:
-    """Batched env_reset (deterministic_madn.py:42-120, game_agent.py:24-44)."""
+              device="cuda", seeds=None, **rules) -> DetMADNState:
+    """Batched env_reset (deterministic_madn.py:42-120, game_agent.py:24-44).  ``seeds`` (one int per game, the
+    reference's ``seed`` argument) are needed only by a random starting player (starting_player < 0 or >= P,
+    line 62): each game's seat is drawn from its seed (muz_detmadn_reset_seeded)."""
     r = make_rules(num_players, layout, distance, starting_player, **rules)
     st = _alloc(batch, int(num_players), r, device)
     lib = _L.load()
-    _L.check(lib.muz_detmadn_reset(r, st.soa(), batch, _L.stream_ptr()), "muz_detmadn_reset")
+    if seeds is None:
+        _L.check(lib.muz_detmadn_reset(r, st.soa(), batch, _L.stream_ptr()), "muz_detmadn_reset")
+    else:
+        sd = torch.as_tensor(np.asarray(seeds, np.int64) & 0xFFFFFFFF).to(torch.int64)
+        sd = (sd - ((sd >> 31) << 32)).to(device=device, dtype=torch.int32).contiguous()   # uint32 bits as int32
+        if sd.numel() != batch:
+            raise ValueError("one seed per game")
+        _L.check(lib.muz_detmadn_reset_seeded(r, st.soa(), _L.ptr(sd), batch, _L.stream_ptr()),
+                 "muz_detmadn_reset_seeded")
     return st
 
 

@@ -260,6 +260,7 @@ SIGNATURES = {
     "muz_version": (ctypes.c_char_p, []),
     "muz_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "muz_detmadn_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, ctypes.c_int32, vp]),
+    "muz_detmadn_reset_seeded": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_legal": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, ctypes.c_int32, vp]),
     "muz_detmadn_step": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, vp, vp, vp, ctypes.c_int32, vp]),
     "muz_detmadn_step_pin_move": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDetSoA, vp, vp, vp, vp,
@@ -292,6 +293,7 @@ SIGNATURES = {
                                                   ctypes.c_int32, vp]),
     "muz_dog_random_action": (ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_int32, vp, ctypes.c_int32, vp]),
     "muz_classic_reset": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, ctypes.c_int32, vp]),
+    "muz_classic_reset_seeded": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_set_die": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_dice_probs": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, ctypes.c_int32, vp]),
     "muz_classic_throw_die": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, ctypes.c_int32, vp]),

@@ -40,7 +40,9 @@ typedef struct muz_rules {
   int32_t num_players;        /* 2..4 */
   int32_t distance;           /* must be 10 (board of 56 cells) */
   int32_t layout[4];          /* seat mask; fixed up exactly like env_reset:70-74 */
-  int32_t starting_player;    /* 0 <= s < num_players (random start is not restated) */
+  int32_t starting_player;    /* 0 <= s < num_players, or out of range = a random seat per game (env_reset's
+                                 jax randint, restated on the counter RNG: see muz_detmadn_reset_seeded); accepted
+                                 by the seeded resets and every DOG entry point, MUZ_E_UNSUPPORTED elsewhere */
   int32_t enable_teams;
   int32_t enable_initial_free_pin;
   int32_t enable_circular_board;
@@ -92,6 +94,12 @@ const char* muz_error_string(int code);        /* host string */
 int muz_detmadn_reset(const muz_rules* rules /*host*/, muz_detmadn_soa state, int32_t n, void* stream);
 
 /* valid_action (deterministic_madn.py:299-393): legal_bits[b] bit (pin*6+move-1). */
+/* env_reset with the reference's seed argument (deterministic_madn.py:42-62): as muz_detmadn_reset, and when
+ * rules->starting_player is out of range each game's seat is drawn from its seed seeds[g] (the reference draws it
+ * with jax.random.randint(split(PRNGKey(seed))[1], (), 0, P); here floor(U * P) of the counter RNG of the seed --
+ * threefry is not restated, so the seat a seed gives differs from jax's; the distribution is the same). */
+int muz_detmadn_reset_seeded(const muz_rules* rules /*host*/, muz_detmadn_soa state, const int32_t* seeds, int32_t n,
+                             void* stream);
 int muz_detmadn_legal(const muz_rules* rules, muz_detmadn_soa state, uint32_t* legal_bits, int32_t n,
                       void* stream);
 
@@ -151,6 +159,9 @@ int muz_detmadn_policy_action(const muz_rules* rules, muz_detmadn_soa state, con
 int muz_classic_reset(const muz_rules* rules /*host*/, muz_classic_soa state, int32_t n, void* stream);
 
 /* set_die (classic_madn.py:244-255): die[b] (1..6) into the state. */
+/* env_reset with the reference's seed argument (classic_madn.py:51-72): random seat as muz_detmadn_reset_seeded. */
+int muz_classic_reset_seeded(const muz_rules* rules /*host*/, muz_classic_soa state, const int32_t* seeds, int32_t n,
+                             void* stream);
 int muz_classic_set_die(const muz_rules* rules, muz_classic_soa state, const int32_t* die, int32_t n, void* stream);
 
 /* dice_probabilities (208-228) -> probs[b][6] fp32; soft_locked[b] (is_soft_locked 180-206) may be null. */

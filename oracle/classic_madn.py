@@ -68,13 +68,17 @@ class State(_DetState):
     die: int = 0
 
 
-def env_reset(num_players=4, layout=(True, True, True, True), distance=10, starting_player=0, **rules) -> State:
-    """classic_madn.py:51-131 (random starting player not restated, as in oracle.detmadn)."""
+def env_reset(num_players=4, layout=(True, True, True, True), distance=10, starting_player=0, seed=None,
+              **rules) -> State:
+    """classic_madn.py:51-131 (a random starting player from ``seed`` as oracle.detmadn.env_reset)."""
+    from .detmadn import start_seat
     r = dict(DEFAULT_RULES)
     r.update(rules)
     P = int(num_players)
     if not (0 <= starting_player < P):
-        raise ValueError("random starting player (threefry) is not restated; pass 0 <= starting_player < P")
+        if seed is None:
+            raise ValueError("a random starting player needs the reset seed")
+        starting_player = start_seat(int(seed) & 0xFFFFFFFF, P)
     board_size = 4 * int(distance)
     total = board_size + 16
     r["enable_teams"] = bool(r["enable_teams"] and P == 4)

@@ -97,19 +97,40 @@ def set_pins_on_board(board, pins):
     return out
 
 
-def env_reset(num_players=4, layout=(True, True, True, True), distance=10, starting_player=0,
+_M64 = 0xFFFFFFFFFFFFFFFF
+START_STREAM = 0x57A27C0DE5
+
+
+def _mix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def start_seat(key: int, P: int) -> int:
+    """The engine's random starting player (csrc/rng.hpp start_seat): floor(U * P) in float32 of the counter RNG of
+    ``key`` (det / classic: the game's reset seed as uint32; DOG: the deal key).  The reference draws the seat with
+    jax.random.randint(split(PRNGKey(seed))[1], (), 0, P) (deterministic_madn.py:60-62); threefry is not restated,
+    so parity of WHICH seat a seed gives is unpinned, only the uniform distribution over seats is shared."""
+    u = np.float32((_mix64((key ^ START_STREAM) & _M64) >> 40) * (1.0 / 16777216.0))
+    s = int(np.float32(u) * np.float32(P))
+    return min(s, P - 1)
+
+
+def env_reset(num_players=4, layout=(True, True, True, True), distance=10, starting_player=0, seed=None,
               **rules) -> State:
     """deterministic_madn.py:42-120.
 
-    The reference draws a random starting player with jax threefry when
-    ``starting_player`` is out of range (line 62); that branch is not restated
-    (parity unpinned) -- callers must pass a valid seat, as game_agent.py:30 does.
-    """
+    ``starting_player`` out of range: a random seat drawn from ``seed`` (line 62) with the engine's counter RNG
+    (``start_seat``; jax threefry is not restated, parity of the seat unpinned)."""
     r = dict(DEFAULT_RULES)
     r.update(rules)
     P = int(num_players)
     if not (0 <= starting_player < P):
-        raise ValueError("random starting player (threefry) is not restated; pass 0 <= starting_player < P")
+        if seed is None:
+            raise ValueError("a random starting player needs the reset seed")
+        starting_player = start_seat(int(seed) & 0xFFFFFFFF, P)
     board_size = 4 * int(distance)
     total = board_size + 16
     r["enable_teams"] = bool(r["enable_teams"] and P == 4)

@@ -132,14 +132,17 @@ def set_pins_on_board(board, pins):
 
 
 def env_reset(num_players=4, layout=(True, True, True, True), distance=10, starting_player=0, shuffle_keys=None,
-              **rules) -> State:
+              start_key=None, **rules) -> State:
     """dog.py:83-186.  ``shuffle_keys(env)`` -> float keys [120] for each distribute_cards call (default:
     the deal-count-seeded numpy generator of ``default_shuffle_keys``)."""
     r = dict(DEFAULT_RULES)
     r.update(rules)
     P = int(num_players)
-    if not (0 <= starting_player < P):
-        raise ValueError("random starting player (threefry) is not restated")
+    if not (0 <= starting_player < P):   # dog.py:102-104: a random seat, here from the engine's key (start_seat)
+        if start_key is None:
+            raise ValueError("a random starting player needs the reset's key (engine_start_key)")
+        from .detmadn import start_seat
+        starting_player = start_seat(int(start_key), P)
     board_size = 4 * int(distance)
     total = board_size + 16
     r["enable_teams"] = bool(r["enable_teams"] and P == 4)
@@ -240,6 +243,12 @@ def engine_shuffle_keys(seed, game):
         return np.array([_u24(_mix64(base ^ (((k + 1) * 0xA24BAED4963EE407) & M64))) for k in range(MAX_CARDS)],
                         np.float32)
     return keys
+
+
+def engine_start_key(seed, game, deal=0):
+    """The key of the device's random starting player for game ``game`` of a batch reset with ``seed`` (deal counter
+    ``deal``: 0 for muz_dog_reset, the running count for an in-place restart): csrc/env_dog.hip dog_reset_lds."""
+    return _game_key(seed, game, deal)
 
 
 def engine_random_action(mask, seed, game, turn):

@@ -85,3 +85,24 @@ def test_dog_repr_layernorm_head():
     assert lg.shape == (3, 806) and v.shape == (3,) and np.array_equal(e, emb)
     r, d, lg2, v2, n2 = DM.recurrent_inference(p, np.array([0, 805, -1]), e)
     assert lg2.shape == (3, 806) and n2.shape == (3, 256) and (np.abs(r) <= 1).all() and (np.abs(d) <= 1).all()
+
+
+def test_oracle_random_starting_player():
+    """env_reset's random seat (starting_player out of range) in the three oracles: deterministic per seed / key,
+    every seat reachable, the rest of the reset unchanged; without a seed / key it is refused."""
+    import pytest
+    from oracle import classic_madn as cm
+    from oracle import detmadn as dm
+    seats = [dm.start_seat(s, 4) for s in range(2000)]
+    assert all(0 <= x < 4 for x in seats) and min(seats.count(k) for k in range(4)) > 400
+    assert dm.start_seat(12345, 3) == dm.start_seat(12345, 3)
+    e = dm.env_reset(num_players=4, starting_player=-1, seed=77, **dm.SELFPLAY_RULES)
+    f = dm.env_reset(num_players=4, starting_player=dm.start_seat(77, 4), **dm.SELFPLAY_RULES)
+    assert e.current_player == f.current_player and np.array_equal(e.pins, f.pins)
+    assert cm.env_reset(num_players=2, starting_player=5, seed=3).current_player == dm.start_seat(3, 2)
+    with pytest.raises(ValueError):
+        dm.env_reset(num_players=2, starting_player=-1)
+    kw = dict(RULE_SETS["selfplay_4p_teams"])
+    kw.pop("num_players")
+    d = dg.env_reset(4, starting_player=-1, start_key=dg.engine_start_key(5, 1), **kw)
+    assert d.current_player == d.round_starter == dm.start_seat(dg.engine_start_key(5, 1), 4)
