@@ -65,13 +65,8 @@ static WTree carve_wide(void* ws, int n, int N) {
 }
 
 // exp correctly rounded (float64, rounded once): oracle/mctx_gumbel.py exp_cr, search.hip exp_cr
-__device__ __forceinline__ float exp_cr_w(float x) {
-#ifdef MUZ_DOG_EXPT_FASTEXP   // timing experiment only (wrong rounding)
-  return __expf(x);
-#else
-  return (float)exp((double)x);
-#endif
-}
+// (A/B, profiles/r4k_dog_ab.log: a float __expf in its place -- wrong rounding -- was 22-27 % faster per search)
+__device__ __forceinline__ float exp_cr_w(float x) { return (float)exp((double)x); }
 
 // sum of this game's 806 entries f(j) (this lane's slot j; padding slots give -0) in the lane order of
 // oracle/mctx_gumbel.py lane_tree_sum: each lane its slots in turn, then a balanced tree over the 32 lanes
@@ -81,9 +76,7 @@ __device__ __forceinline__ float wsum(F f) {
 #pragma unroll
   for (int j = 1; j < kWJ; ++j) {
     s = s + f(j);
-#ifndef MUZ_DOG_EXPT_NOBAR
     if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);   // bounded interleaving of the slots (registers)
-#endif
   }
   return row_sum(s);   // xor1, xor2, half mirror, mirror, swap16: the balanced tree in lane order
 }
@@ -124,9 +117,7 @@ __device__ __forceinline__ int wargmax(F f, int sub) {
       v = x;
       i = sub + kRowLanes * j;
     }
-#ifndef MUZ_DOG_EXPT_NOBAR
     if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);   // bounded interleaving of the slots (registers)
-#endif
   }
   return wargmax_row(v, i);
 }
@@ -388,17 +379,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         nd.pr = smem + row * kDogA;
         nd.cq = smem + (kRows + row) * kDogA;
         int bi;
-#ifdef MUZ_DOG_EXPT_NOSELECT   // timing experiment only (wrong results): a fixed child, no node load
-        bi = (node * 131 + sim * 7 + depth) % kDogA;
-        if (false) {
-#elif defined(MUZ_DOG_EXPT_LOADONLY)   // timing experiment only: the node load + transform, a fixed child
-        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa, s_ces[row]);
-        bi = (node * 131 + sim * 7 + depth + (nd.sv & 1)) % kDogA;
-        if (false) {
-#else
         wnode_load(nd, T, g, node, sub, s_raw[row][node], sa, s_ces[row]);
         if (depth == 0) {
-#endif
           // gumbel_muzero_root_action_selection: score_considered + masked_argmax
           const int cv = wconsidered_visit(ncons, sa.S, nd.sv);
           bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, cv, legal_of);
