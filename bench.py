@@ -64,8 +64,9 @@ DOG_BATCH = 1024
 DOG_TURNS_PER_LAUNCH = 1024     # one muz_dog_random_play launch plays 1024 turns of every game (~10 ms)
 DOG_LAUNCHES_PER_STEP = 32      # one bench step = 32 launches (~0.3 s: the default 3 steps time ~1 s)
 
-
-# DOG MuZero slice (--workload dog --policy muzero): MuZero_DOG/train.py:337-338 (S = 100, D = 50), 1024 games per GPU.
+# DOG MuZero slice (--workload dog --policy muzero): MuZero_DOG/train.py:337-338 (S = 100, D = 50), 1500 games per GPU
+# (train.py:332 num_games_per_iteration; the random-policy config (d) is 1024).
+DOG_MZ_GAMES = 1500
 # FLOP per simulation at A = 806, counted as the reference would compute it (one-hot Dense layers as matmuls, like
 # the det count): DynamicsNetwork4 679,424 MAC (Dense_0 806 x 64 and the one-hot rows of Dense_6 / 7, 806 x 128, are
 # the A-dependent parts) + PredictionNetwork4 504,640 MAC (policy logits 128 x 806).  Executed on the device:
@@ -109,9 +110,9 @@ def parse():
                     help="strong scaling (SURVEY §8e): --batch is the WHOLE job's batch, split evenly over the ranks "
                          "(det 4096 -> 2048/1024/512 per GPU); default is weak scaling, --batch games per GPU")
     args = ap.parse_args()
-    if args.workload == "dog" and args.batch == BATCH:
-        args.batch = DOG_BATCH
     dog_mz = args.workload == "dog" and args.policy == "muzero"
+    if args.workload == "dog" and args.batch == BATCH:
+        args.batch = DOG_MZ_GAMES if dog_mz else DOG_BATCH
     if args.sims is None:
         args.sims = DOG_MZ_SIMS if dog_mz else S
     if args.depth is None:

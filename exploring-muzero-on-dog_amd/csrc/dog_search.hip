@@ -33,6 +33,9 @@ struct WTree {
   int32_t* c_index;   // [n][N][832]
   float* emb;         // [n][N][256]
   float* gum;         // [n][832] the root's Gumbel noise + (prior - max prior), drawn once per search
+  int32_t* vlist;     // [n][N][32] each node's visited children in first-visit order (s_vcnt: how many; -1 overflow)
+  float* topp;        // [n][N][8] each node's 8 largest prior logits (value desc, index asc) ...
+  int32_t* topi;      // [n][N][8] ... and their children
   int N;
   __device__ __forceinline__ size_t ca(int g, int node, int a) const { return ((size_t)g * N + node) * kWPad + a; }
   __device__ __forceinline__ AS1 float* e(int g, int node) const { return gpw(emb) + ((size_t)g * N + node) * LAT; }
@@ -43,7 +46,14 @@ struct WTree {
   }
   __device__ __forceinline__ AS1 int32_t* index() const { return gpw(c_index); }
   __device__ __forceinline__ AS1 int32_t* visits() const { return gpw(c_visits); }
+  __device__ __forceinline__ AS1 int32_t* vl(int g, int node) const {
+    return gpw(vlist) + ((size_t)g * N + node) * 32;
+  }
+  __device__ __forceinline__ AS1 float* tp(int g, int node) const { return gpw(topp) + ((size_t)g * N + node) * 8; }
+  __device__ __forceinline__ AS1 int32_t* ti(int g, int node) const { return gpw(topi) + ((size_t)g * N + node) * 8; }
 };
+constexpr int kWList = 32;   // visited children a node's list holds
+constexpr int kWTop = 8;     // largest priors a node keeps
 
 static size_t wide_children_bytes(int64_t n, int N) { return (size_t)n * N * kWPad * 4; }
 
@@ -60,6 +70,12 @@ static WTree carve_wide(void* ws, int n, int N) {
   t.emb = (float*)p;
   p += (size_t)n * N * LAT * 4;
   t.gum = (float*)p;
+  p += (size_t)n * kWPad * 4;
+  t.vlist = (int32_t*)p;
+  p += (size_t)n * N * kWList * 4;
+  t.topp = (float*)p;
+  p += (size_t)n * N * kWTop * 4;
+  t.topi = (int32_t*)p;
   t.N = N;
   return t;
 }
@@ -85,7 +101,7 @@ __device__ __forceinline__ float wsum(F f) {
 // this lane's slots in ascending order (strict >), then row_argmax's (value, index) order across the lanes.
 // Streams the scores: no per-slot array is kept.
 // (value, index) argmax across the row's lanes, row_argmax's order (larger value, then smaller index)
-__device__ __forceinline__ int wargmax_row(float v, int i) {
+__device__ __forceinline__ void wargmax_row2(float& v, int& i) {
   auto pick = [](float& v, int& i, float ov, int oi) {
     if (ov > v || (ov == v && oi < i)) {
       v = ov;
@@ -101,6 +117,9 @@ __device__ __forceinline__ int wargmax_row(float v, int i) {
   v = pv.lo;
   i = pi.lo;
   pick(v, i, pv.hi, pi.hi);
+}
+__device__ __forceinline__ int wargmax_row(float v, int i) {
+  wargmax_row2(v, i);
   return i;
 }
 
@@ -178,20 +197,51 @@ __device__ __forceinline__ int wconsidered_visit(int m, int S, int idx) {
 // the kernel spilled; the exponentials are recomputed where they are needed for the same reason.
 struct WNode {
   float* pr;     // [806] of this row, LDS
-  float* cq;     // [806] of this row, LDS
+  float* cq;     // [806] of this row, LDS (the visited children's; wfill_unvisited writes the rest)
   int vis[kWJ];
   float pm;      // max prior logit
   int sv, mv;    // sum / max of the visit counts
+  float es;      // sum of exp(prior - pm) (the prior normaliser)
+  float K;       // the transformed completed Q every unvisited child shares
+  float u1, u2;  // the largest and second-largest prior logit among the unvisited children (u2 = u1 on a tie)
+  int ui;        // the child holding u1 (the smallest such index)
+  unsigned vm;   // this lane's visited slots (bit j: slot j)
 };
 
-// ces: this row's per-node sum of exp(prior - max prior) (the softmax normaliser of the node's prior
-// probabilities), computed at the node's first walk and kept until the node is expanded again -- its priors do not
-// change in between, so the 806 exponentials are not recomputed at every visit (< 0: not cached).
-__device__ __forceinline__ void wnode_load(WNode& nd, const WTree& T, int g, int node, int sub, float raw,
-                                           const SearchArgs& sa, float* ces) {
+// (value, index) top-2 across the row's lanes: the first by (larger value, smaller index), the second the largest
+// of the rest (equal to the first on a tie).  Each butterfly step merges disjoint lane sets.
+__device__ __forceinline__ void wtop2_row(float& v1, int& i1, float& v2) {
+  auto merge = [&](float o1, int oi, float o2) {
+    float lo1 = o1;
+    if (o1 > v1 || (o1 == v1 && oi < i1)) {
+      lo1 = v1;
+      v1 = o1;
+      i1 = oi;
+    }
+    v2 = fmaxf(fmaxf(v2, o2), lo1);
+  };
+  merge(dpp<DPP_XOR1>(v1), dpp<DPP_XOR1>(i1), dpp<DPP_XOR1>(v2));
+  merge(dpp<DPP_XOR2>(v1), dpp<DPP_XOR2>(i1), dpp<DPP_XOR2>(v2));
+  merge(dpp<DPP_HALF_MIRROR>(v1), dpp<DPP_HALF_MIRROR>(i1), dpp<DPP_HALF_MIRROR>(v2));
+  merge(dpp<DPP_MIRROR>(v1), dpp<DPP_MIRROR>(i1), dpp<DPP_MIRROR>(v2));
+  const LoHi<float> p1 = swap16(v1), p2 = swap16(v2);
+  const LoHi<int> pi = swap16(i1);
+  v1 = p1.lo;
+  i1 = pi.lo;
+  v2 = p2.lo;
+  merge(p1.hi, pi.hi, p2.hi);
+}
+
+// Full load of one node: all 806 children (priors and q into LDS, visit counts into registers), their maximum prior,
+// visit sum / maximum, the two largest unvisited priors and this lane's visited slots.  ces: this row's per-node sum
+// of exp(prior - max prior) (the softmax normaliser of the node's prior probabilities), computed at the node's first
+// walk and kept until the node is expanded again -- its priors do not change in between, so the 806 exponentials
+// are not recomputed at every visit (< 0: not cached); with it the node's kWTop largest priors go to T.tp / T.ti for
+// the compact loads.
+__device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int node, int sub, float* ces) {
 #pragma clang fp contract(off)
-  float pm = -INFINITY;
-  int sv = 0, mv = 0;
+  float pm = -INFINITY, u1 = -INFINITY, u2 = -INFINITY;
+  int sv = 0, mv = 0, ui = kDogA;
   // two batches of 13 slots, one 16-byte {prior, value, reward, discount} load + the visit count each, all of a batch in
   // flight together (left to itself the scheduler serialised them slot by slot to save registers: 26 round trips).
   // Padding slots are read too (they exist in the node's 832) and their values dropped.
@@ -213,9 +263,19 @@ __device__ __forceinline__ void wnode_load(WNode& nd, const WTree& T, int g, int
       const bool ok = a < kDogA;
       nd.vis[j] = ok ? vs[k] : 0;
       if (ok) {
-        nd.pr[a] = c4[k][0];
+        const float p = c4[k][0];
+        nd.pr[a] = p;
         nd.cq[a] = c4[k][2] + c4[k][3] * c4[k][1];   // q = reward + discount * value (Tree.qvalues)
-        pm = fmaxf(pm, c4[k][0]);
+        pm = fmaxf(pm, p);
+        if (vs[k] == 0) {   // slots in ascending order: the first of equal priors keeps u1
+          if (p > u1) {
+            u2 = u1;
+            u1 = p;
+            ui = a;
+          } else {
+            u2 = fmaxf(u2, p);
+          }
+        }
       }
       sv += nd.vis[j];
       mv = max(mv, nd.vis[j]);
@@ -224,17 +284,121 @@ __device__ __forceinline__ void wnode_load(WNode& nd, const WTree& T, int g, int
   pm = row_max(pm);
   sv = row_isum(sv);
   mv = row_imax(mv);
+  wtop2_row(u1, ui, u2);
   float es = ces[node];
   if (es < 0.f) {   // (row-uniform)
     es = wsum([&](int j) { return wok(sub, j) ? exp_cr_w(nd.pr[sub + kRowLanes * j] - pm) : -0.0f; });
     if (sub == 0) ces[node] = es;
+    // the kWTop largest priors in (value desc, index asc) order, one row argmax after another
+    float pv = INFINITY;
+    int pi = -1;
+#pragma unroll 1
+    for (int r = 0; r < kWTop; ++r) {
+      float v = -INFINITY;
+      int i = kDogA;
+#pragma unroll
+      for (int j = 0; j < kWJ; ++j) {
+        const int a = sub + kRowLanes * j;
+        if (a < kDogA) {
+          const float p = nd.pr[a];
+          if ((p < pv || (p == pv && a > pi)) && p > v) {
+            v = p;
+            i = a;
+          }
+        }
+      }
+      wargmax_row2(v, i);
+      if (sub == r) {
+        T.tp(g, node)[r] = v;
+        T.ti(g, node)[r] = i;
+      }
+      pv = v;
+      pi = i;
+    }
   }
-  // The mixed value needs the prior probabilities of the VISITED children only: sum_probs and weighted_q are summed
-  // over this lane's visited slots (a bit mask, in slot order) -- the unvisited ones add exact zeros in the
-  // restatement's order (lane_tree_sum), which change no partial sum -- so their exponentials are not recomputed.
   unsigned vm = 0;
 #pragma unroll
   for (int j = 0; j < kWJ; ++j) vm |= (nd.vis[j] > 0 ? 1u : 0u) << j;
+  nd.pm = pm;
+  nd.sv = sv;
+  nd.mv = mv;
+  nd.es = es;
+  nd.u1 = u1;
+  nd.u2 = u2;
+  nd.ui = ui;
+  nd.vm = vm;
+}
+
+// lane l: the node's l-th visited child (a < 0: none) -- its index, visit count, prior and transformed completed Q
+struct WEntry {
+  int a, n;
+  float p, c;
+};
+
+// Compact load of a node walked before (its normaliser es and top-prior list cached, its visited list not
+// overflowed): only the visited children (lane l the list's l-th, one 16-byte load + the visit count) and the
+// top-prior list -- everything the certified selection reads; their priors / q go to LDS at their slots for the
+// mixed value's lane-order sums.  nd.vis is not filled.  False when the list has fewer than two unvisited children
+// (u2 unknown): the caller loads the node in full.
+__device__ __forceinline__ bool wnode_compact(WNode& nd, const WTree& T, int g, int node, int sub, float es, int vc,
+                                              WEntry& en) {
+#pragma clang fp contract(off)
+  const bool has = sub < vc;
+  en.a = -1;
+  en.n = 0;
+  en.p = 0.f;
+  f32x4 c4 = {0.f, 0.f, 0.f, 0.f};
+  float tp = -INFINITY;
+  int ti = kDogA;
+  if (has) en.a = tree_ld(T.vl(g, node) + sub);
+  if (sub < kWTop) {
+    tp = tree_ld(T.tp(g, node) + sub);
+    ti = tree_ld(T.ti(g, node) + sub);
+  }
+  if (has) {
+    const size_t e = T.ca(g, node, en.a);
+    c4 = tree_ld(T.node4() + e);
+    en.n = tree_ld(T.visits() + e);
+  }
+  ST(ST_PASS);   // (diagnostic builds: node loads)
+  if (has) {
+    en.p = c4[0];
+    nd.pr[en.a] = c4[0];
+    nd.cq[en.a] = c4[2] + c4[3] * c4[1];   // q = reward + discount * value (Tree.qvalues)
+  }
+  // this lane's visited slots: the list entries whose child sits in this lane
+  unsigned vm = 0;
+  for (int k = 0; k < vc; ++k) {
+    const int a = __shfl(en.a, k, kRowLanes);
+    if ((a & (kRowLanes - 1)) == sub) vm |= 1u << (a >> 5);
+  }
+  // the first two unvisited children of the top-prior list
+  const unsigned vmt = __shfl(vm, ti & (kRowLanes - 1), kRowLanes);
+  const bool unv = sub < kWTop && ((vmt >> (ti >> 5)) & 1u) == 0u;
+  const unsigned long long bal = __ballot(unv);
+  const unsigned bits = (unsigned)(bal >> (threadIdx.x & 32u)) & ((1u << kWTop) - 1u);
+  if (__popc(bits) < 2) return false;
+  const int k1 = __ffs(bits) - 1, k2 = __ffs(bits & (bits - 1u)) - 1;
+  nd.pm = __shfl(tp, 0, kRowLanes);   // the list's first prior is the node's largest
+  nd.u1 = __shfl(tp, k1, kRowLanes);
+  nd.ui = __shfl(ti, k1, kRowLanes);
+  nd.u2 = __shfl(tp, k2, kRowLanes);
+  nd.sv = row_isum(en.n);
+  nd.mv = row_imax(en.n);
+  nd.es = es;
+  nd.vm = vm;
+  return true;
+}
+
+// qtransform_completed_by_mix_value (value_scale, maxvisit_init, rescale, mixed value, eps 1e-8) over a loaded node:
+// the visited children's transformed completed Q into cq (LDS) and the value every unvisited child shares (nd.K).
+// The mixed value needs the prior probabilities of the VISITED children only: sum_probs and weighted_q are summed
+// over this lane's visited slots (a bit mask, in slot order) -- the unvisited ones add exact zeros in the
+// restatement's order (lane_tree_sum), which change no partial sum -- so their exponentials are not recomputed.
+__device__ __forceinline__ void wnode_tail(WNode& nd, int sub, float raw, const SearchArgs& sa) {
+#pragma clang fp contract(off)
+  const float pm = nd.pm, es = nd.es;
+  const unsigned vm = nd.vm;
   auto ppa = [&](int a) { return fmaxf(kTinyF, exp_cr_w(nd.pr[a] - pm) / es); };
   float spl = 0.f;
   for (unsigned m = vm; m; m &= m - 1u) spl = spl + ppa(sub + kRowLanes * (__ffs(m) - 1));
@@ -245,33 +409,117 @@ __device__ __forceinline__ void wnode_load(WNode& nd, const WTree& T, int g, int
     wql = wql + ppa(a) * nd.cq[a] / sp;
   }
   const float wq = row_sum(wql);
+  const int sv = nd.sv;
   const float mixed = (raw + (float)sv * wq) / (float)(sv + 1);
-  float lo = INFINITY, hi = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < kWJ; ++j) {
-    const int a = sub + kRowLanes * j;
-    if (wok(sub, j)) {
-      const float c = nd.vis[j] > 0 ? nd.cq[a] : mixed;
-      nd.cq[a] = c;
-      lo = fminf(lo, c);
-      hi = fmaxf(hi, c);
-    }
+  // completed Q: the visited children's q, `mixed` for the rest (there are unvisited children: S <= 100 < 806), so
+  // its minimum / maximum are those of the visited q and `mixed`, and every unvisited child transforms to the same K
+  float lo = mixed, hi = mixed;
+  for (unsigned m = vm; m; m &= m - 1u) {
+    const float c = nd.cq[sub + kRowLanes * (__ffs(m) - 1)];
+    lo = fminf(lo, c);
+    hi = fmaxf(hi, c);
   }
   lo = row_min(lo);
   hi = row_max(hi);
   const float den = fmaxf(hi - lo, 1e-8f);
-  const float scale = (sa.maxvisit_init + (float)mv) * sa.value_scale;
-#pragma unroll
-  for (int j = 0; j < kWJ; ++j) {
-    const int a = sub + kRowLanes * j;
-    if (wok(sub, j)) nd.cq[a] = scale * ((nd.cq[a] - lo) / den);
+  const float scale = (sa.maxvisit_init + (float)nd.mv) * sa.value_scale;
+  for (unsigned m = vm; m; m &= m - 1u) {
+    const int a = sub + kRowLanes * (__ffs(m) - 1);
+    nd.cq[a] = scale * ((nd.cq[a] - lo) / den);
   }
-  nd.pm = pm;
-  nd.sv = sv;
-  nd.mv = mv;
+  nd.K = scale * ((mixed - lo) / den);
   ST(ST_OTHER);   // (diagnostic builds: the completed-Q transform)
 }
 
+// the visited-list entries of a fully loaded node (priors / transformed Q from LDS); vc < 0 (overflowed list): none
+__device__ __forceinline__ void wentries(const WNode& nd, const WTree& T, int g, int node, int sub, int vc,
+                                         WEntry& en) {
+  en.a = -1;
+  en.n = 0;
+  en.p = en.c = 0.f;
+  if (sub < vc) {
+    en.a = tree_ld(T.vl(g, node) + sub);
+    en.n = tree_ld(T.visits() + T.ca(g, node, en.a));
+    en.p = nd.pr[en.a];
+    en.c = nd.cq[en.a];
+  }
+}
+
+// the unvisited children's transformed completed Q (K) into cq: the root's selection, the final weights and the
+// interior selection's exact path read all 806
+__device__ __forceinline__ void wfill_unvisited(const WNode& nd, int sub) {
+#pragma unroll
+  for (int j = 0; j < kWJ; ++j)
+    if (wok(sub, j) && nd.vis[j] == 0) nd.cq[sub + kRowLanes * j] = nd.K;
+}
+
+// gumbel_muzero_interior_action_selection's argmax without the 806 exponentials, when it can be certified:
+// score(a) = exp(z_a - zm) / zs - N_a / (1 + sum N) with z = prior + completed Q.  Every unvisited child has the same
+// completed Q (K) and N = 0, so its score is non-decreasing in its prior: the best unvisited child is the one with
+// the largest prior (u1), and the candidates are it and the visited children.  Their exponentials are computed
+// exactly as the exact path does; only zs is bounded instead of summed: the unvisited part is exp(K + pm - zm) x
+// (es - the visited children's exp(prior - pm)), within a relative error bound of the restatement's float sum
+// (argument roundings, exp, the lane-order sums).  The pick is returned when the best candidate's lower bound
+// clears every other candidate's upper bound (and, when it is u1's child, when no other unvisited child can tie
+// it: its exponential is more than a few ulps above the second prior's) -- then the exact path's argmax is the
+// same index; otherwise -1 (the exact path runs).
+__device__ __forceinline__ int wselect_certified(const WNode& nd, const WEntry& en, int sub) {
+#pragma clang fp contract(off)
+  const float K = nd.K, zU = nd.u1 + K;
+  const bool has = en.a >= 0;
+  const float z = has ? en.p + en.c : -INFINITY;
+  const float zm = fmaxf(row_max(z), zU);   // fl(p + K) is monotone in p: zU is the unvisited maximum
+  const float ez = has ? exp_cr_w(z - zm) : 0.f;
+  const float sez = row_sum(ez);
+  const float sep = row_sum(has ? exp_cr_w(en.p - nd.pm) : 0.f);
+  const double f = exp((double)K + (double)nd.pm - (double)zm);
+  const double zsa = (double)sez + f * fmax((double)nd.es - (double)sep, 0.0);
+  // per-element relative error of the argument roundings <= 2^-24 (c0 + 3 d) e^-d summed (d e^-d <= 1/e over 806
+  // children), exp and the lane-order sums <= 2^-18; es's own sum error scaled by f; all doubled
+  const double c0 = 4.0 * (fabs((double)zm) + fabs((double)K) + fabs((double)nd.pm) + 1.0);
+  const double err = zsa * (0x1p-23 * (c0 + 900.0) + 0x1p-17) + f * (double)nd.es * 0x1p-17;
+  if (!(zsa - err > 0.0) || !(err < 0.01 * zsa)) return -1;
+  const float zlo = (float)(zsa - err) * (1.f - 0x1p-22f), zhi = (float)(zsa + err) * (1.f + 0x1p-22f);
+  const float n = has ? (float)en.n / (float)(1 + nd.sv) : 0.f;
+  const float q_hi = ez / zlo, slack = 0x1p-20f * (q_hi + n);
+  // the best visited candidate of the row by lower bound
+  float blo = has ? (ez / zhi - n) - slack : -INFINITY;
+  int bi = has ? en.a : kDogA;
+  wargmax_row2(blo, bi);
+  const float ezU = exp_cr_w(zU - zm);
+  const float loU = ezU / zhi - 0x1p-20f * (ezU / zlo), hiU = ezU / zlo + 0x1p-20f * (ezU / zlo);
+  const bool pick_u = loU > blo || bi >= kDogA;
+  if (pick_u) {
+    bi = nd.ui;
+    blo = loU;
+    if (!(loU > 0x1p-100f)) return -1;   // (normal range: the ulp argument below holds)
+    // no other unvisited child may reach u1's score: its exponential more than 4 ulps above the runner-up's
+    if (nd.u2 != -INFINITY && !(ezU > exp_cr_w((nd.u2 + K) - zm) * (1.f + 0x1p-21f))) return -1;
+  }
+  // upper bounds of every other candidate
+  const float hub = fmaxf(row_max(has && en.a != bi ? (q_hi - n) + slack : -INFINITY), pick_u ? -INFINITY : hiU);
+  return blo > hub ? bi : -1;
+}
+
+// gumbel_muzero_interior_action_selection by certification (wselect_certified) over the node's visited-list entries,
+// or -1: the exact path (exact_select, an overflowed list, or no certificate)
+__device__ __forceinline__ int wselect_interior(const WNode& nd, WEntry& en, const WTree& T, int g, int node, int sub,
+                                                int vc, bool compact, bool exact_select) {
+  st_count(9);   // (diagnostic builds: interior selections)
+  if (exact_select || vc < 0) return -1;
+  if (compact) {
+    en.c = en.a >= 0 ? nd.cq[en.a] : 0.f;
+  } else {
+    wentries(nd, T, g, node, sub, vc, en);
+  }
+  return wselect_certified(nd, en, sub);
+}
+
+// SPARSE: one game per wave (the even rows of the 16-row tile; the odd rows are padding the networks carry along), 8
+// games per workgroup.  A wave's two rows walk their trees one after the other wherever their paths differ (depth,
+// exact-path fallbacks), so with one game per wave the walk and the barrier waits behind it shrink; the networks cost
+// the same per tile.  Chosen when the grid still fits the chip (n <= 2048: <= 256 workgroups of 8).
+template <bool SPARSE>
 __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, SearchArgs sa,
                                                         const float* __restrict__ root_logits,
                                                         const float* __restrict__ root_value,
@@ -291,15 +539,17 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
   __shared__ float p_rew[kRows][kWMaxDepth];
   __shared__ float p_disc[kRows][kWMaxDepth];
   __shared__ uint32_t s_legal[kRows][kWWords];
-  __shared__ float s_ces[kRows][kWMaxNodes];   // per-node softmax normalisers of the priors (wnode_load)
+  __shared__ float s_ces[kRows][kWMaxNodes];   // per-node softmax normalisers of the priors (wnode_full)
+  __shared__ signed char s_vcnt[kRows][kWMaxNodes];   // per-node visited-list lengths (-1: overflowed)
   __shared__ int s_act[kRows], s_parent[kRows], s_next[kRows], s_depth[kRows];
 
-  if ((int)blockIdx.x * kRows >= n) return;
+  constexpr int kGames = SPARSE ? kRows / 2 : kRows;   // games per workgroup
+  if ((int)blockIdx.x * kGames >= n) return;
+  auto game_of = [](int r) { return (int)blockIdx.x * kGames + (SPARSE ? (r >> 1) : r); };
   const Arena ar = Arena::carve(smem);
   const int row = trow(), sub = tsub();
-  const int g0 = blockIdx.x * kRows;
-  const int g = g0 + row;
-  const bool valid = g < n;
+  const int g = game_of(row);
+  const bool valid = (!SPARSE || (row & 1) == 0) && g < n;
   int gid = g, gturn = sa.turn;
   int ncons = 0;
 
@@ -347,7 +597,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         gpw(T.gum)[(size_t)g * kWPad + a] = gm + (pr[j] - pm);
       }
     }
-    for (int i = sub; i < kWMaxNodes; i += kRowLanes) s_ces[row][i] = -1.f;
+    for (int i = sub; i < kWMaxNodes; i += kRowLanes) {
+      s_ces[row][i] = -1.f;
+      s_vcnt[row][i] = 0;
+    }
     AS1 float* e0 = T.e(g, 0);
     for (int c = sub; c < LAT; c += kRowLanes) e0[c] = root_emb[(size_t)g * LAT + c];
     if (sub == 0) {
@@ -379,37 +632,54 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         nd.pr = smem + row * kDogA;
         nd.cq = smem + (kRows + row) * kDogA;
         int bi;
-        wnode_load(nd, T, g, node, sub, s_raw[row][node], sa, s_ces[row]);
-        if (depth == 0) {
-          // gumbel_muzero_root_action_selection: score_considered + masked_argmax
-          const int cv = wconsidered_visit(ncons, sa.S, nd.sv);
-          bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, cv, legal_of);
-        } else {
-          // gumbel_muzero_interior_action_selection: softmax(prior + cq) - N / (1 + sum N)
-          // (z = prior + cq, then its exponential, replace the priors in LDS: one exp per child)
-          float zm = -INFINITY;
+        WEntry en;
+        const int vc = s_vcnt[row][node];
+        // interior nodes walked before: the compact load (the visited children and the top-prior list); the exact path
+        // (no certificate) reloads the node in full on a second pass
+        bool compact = depth > 0 && !sa.exact_select && vc >= 0 && s_ces[row][node] >= 0.f;
+        if (compact) compact = wnode_compact(nd, T, g, node, sub, s_ces[row][node], vc, en);
+        bi = -1;
+#pragma unroll 1
+        for (int pass = 0; pass < 2 && bi < 0; ++pass) {
+          if (!compact) wnode_full(nd, T, g, node, sub, s_ces[row]);
+          wnode_tail(nd, sub, s_raw[row][node], sa);
+          if (depth == 0) {
+            // gumbel_muzero_root_action_selection: score_considered + masked_argmax
+            const int cv = wconsidered_visit(ncons, sa.S, nd.sv);
+            wfill_unvisited(nd, sub);
+            bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, cv, legal_of);
+          } else if (pass == 0 && (bi = wselect_interior(nd, en, T, g, node, sub, vc, compact, sa.exact_select)) >= 0) {
+          } else if (compact) {
+            compact = false;   // the exact path reads all 806 children
+          } else {
+            st_count(10);   // (diagnostic builds: exact-path fallbacks)
+            // gumbel_muzero_interior_action_selection: softmax(prior + cq) - N / (1 + sum N), the exact path
+            // (z = prior + cq, then its exponential, replace the priors in LDS: one exp per child)
+            wfill_unvisited(nd, sub);
+            float zm = -INFINITY;
 #pragma unroll
-          for (int j = 0; j < kWJ; ++j) {
-            const int a = sub + kRowLanes * j;
-            if (a < kDogA) {
-              const float z = nd.pr[a] + nd.cq[a];
-              nd.pr[a] = z;
-              zm = fmaxf(zm, z);
+            for (int j = 0; j < kWJ; ++j) {
+              const int a = sub + kRowLanes * j;
+              if (a < kDogA) {
+                const float z = nd.pr[a] + nd.cq[a];
+                nd.pr[a] = z;
+                zm = fmaxf(zm, z);
+              }
             }
+            zm = row_max(zm);
+            const float zs = wsum([&](int j) {
+              const int a = sub + kRowLanes * j;
+              if (a >= kDogA) return -0.0f;
+              const float ez = exp_cr_w(nd.pr[a] - zm);
+              nd.pr[a] = ez;
+              return ez;
+            });
+            const float inv_n = (float)(1 + nd.sv);
+            bi = wargmax([&](int j) {
+              const int a = sub + kRowLanes * j;
+              return a < kDogA ? (nd.pr[a] / zs - (float)nd.vis[j] / inv_n) : -INFINITY;
+            }, sub);
           }
-          zm = row_max(zm);
-          const float zs = wsum([&](int j) {
-            const int a = sub + kRowLanes * j;
-            if (a >= kDogA) return -0.0f;
-            const float ez = exp_cr_w(nd.pr[a] - zm);
-            nd.pr[a] = ez;
-            return ez;
-          });
-          const float inv_n = (float)(1 + nd.sv);
-          bi = wargmax([&](int j) {
-            const int a = sub + kRowLanes * j;
-            return a < kDogA ? (nd.pr[a] / zs - (float)nd.vis[j] / inv_n) : -INFINITY;
-          }, sub);
         }
         ST(ST_SEL);   // (diagnostic builds: scores + argmax)
         const size_t eb = T.ca(g, node, bi);
@@ -463,7 +733,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     // (the hand-out re-reads the new node from LDS: with `nx` itself the compiler precomputed the 806 store
     // addresses before the networks and spilled them)
     dog_logits16<NT256>(wl, ar, pf, [&](int r, int col, float v) {
-      if (valid) tree_st(T.fld(T.ca(g0 + r, s_next[r], col), 0), v);
+      if (valid) tree_st(T.fld(T.ca(game_of(r), s_next[r], col), 0), v);
     }, &wl->dyn.d3, LAT, LAT);
     if (valid) {
       const int nx = s_next[row];
@@ -478,6 +748,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         s_raw[row][nx] = v;
         s_val[row][nx] = v;
         s_ces[row][nx] = -1.f;   // new priors: the node's normaliser is recomputed at its next walk
+        if (fresh) s_vcnt[row][nx] = 0;
         s_visits[row][nx] = fresh ? 1 : s_visits[row][nx] + 1;
       }
       // ---------------- backward along the recorded path, one level per lane (search.hip's scheme; the root's
@@ -516,6 +787,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
           tree_st(T.visits() + ei, cvis + 1);
           s_val[row][parent] = pv;
           s_visits[row][parent] = cnt + 1;
+          if (cvis == 0) {   // the edge's first visit: onto the parent's visited list (a path holds a node once)
+            const int k = s_vcnt[row][parent];
+            if (k >= 0) {
+              if (k < kWList) T.vl(g, parent)[k] = pact;
+              s_vcnt[row][parent] = (signed char)(k < kWList ? k + 1 : -1);
+            }
+          }
         }
         carry = __shfl(leaf, 0, kRowLanes);
         carry_v = __shfl(pv, 0, kRowLanes);
@@ -531,7 +809,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     WNode nd;
     nd.pr = smem + row * kDogA;
     nd.cq = smem + (kRows + row) * kDogA;
-    wnode_load(nd, T, g, 0, sub, s_raw[row][0], sa, s_ces[row]);
+    wnode_full(nd, T, g, 0, sub, s_ces[row]);
+    wnode_tail(nd, sub, s_raw[row][0], sa);
+    wfill_unvisited(nd, sub);
     const int bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, nd.mv, legal_of);   // considered_visit = max(visits)
     // action_weights = softmax(_mask_invalid_actions(prior + completed_q))
     float zm = -INFINITY;
@@ -571,15 +851,20 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
 
 int64_t dog_search_workspace_bytes(int n, int S) {
   const int N = S + 1;
-  return (int64_t)wide_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4 + (int64_t)n * kWPad * 4;
+  return (int64_t)wide_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4 + (int64_t)n * kWPad * 4 +
+         (int64_t)n * N * (kWList + 2 * kWTop) * 4;
 }
 
 int launch_dog_search(const muz_dog_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,
                       const float* root_emb, const uint32_t* legal, const float* gumbel, int n, void* workspace,
-                      int32_t* action, float* weights, float* value, hipStream_t s) {
+                      int32_t* action, float* weights, float* value, bool sparse, hipStream_t s) {
   WTree T = carve_wide(workspace, n, sa.S + 1);
-  k_dog_search<<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, sa, root_logits, root_value, root_emb, legal, gumbel, n,
-                                                            T, action, weights, value);
+  if (sparse)
+    k_dog_search<true><<<(n + kRows / 2 - 1) / (kRows / 2), kThreads, 0, s>>>(w, sa, root_logits, root_value, root_emb,
+                                                                             legal, gumbel, n, T, action, weights, value);
+  else
+    k_dog_search<false><<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, sa, root_logits, root_value, root_emb, legal,
+                                                                     gumbel, n, T, action, weights, value);
   return muz_last_launch_error();
 }
 
@@ -619,8 +904,15 @@ int muz_dog_gumbel_search(const muz_dog_net_w* w, const muz_search_cfg* cfg, con
   sa.gumbel_scale = cfg->gumbel_scale;
   sa.seed = cfg->seed;
   sa.turn = cfg->turn;
+  {   // MUZ_DOG_EXACT_SELECT=1: every interior selection on the exact path (tests of that path)
+    const char* e = getenv("MUZ_DOG_EXACT_SELECT");
+    sa.exact_select = e && e[0] == '1';
+  }
+  // one game per wave while the grid fits the chip's 256 CUs; MUZ_DOG_TILE_ROWS=8 / 16 forces either form
+  bool sparse = n <= 2048;
+  if (const char* e = getenv("MUZ_DOG_TILE_ROWS")) sparse = atoi(e) == 8;
   return launch_dog_search(*w, sa, root_logits, root_value, root_embedding, legal, gumbel, n, workspace, action,
-                           action_weights, root_value_out, (hipStream_t)stream);
+                           action_weights, root_value_out, sparse, (hipStream_t)stream);
 }
 
 #ifdef MUZ_STAMPS2

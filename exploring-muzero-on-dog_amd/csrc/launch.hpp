@@ -16,6 +16,7 @@ struct SearchArgs {
   // whichever lane and global turn it is played in.
   const int32_t* key_game = nullptr;
   const int32_t* key_turn = nullptr;
+  int exact_select = 0;   // k_dog_search: every interior selection on the exact path (MUZ_DOG_EXACT_SELECT)
 };
 
 int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv_scratch,

@@ -78,6 +78,10 @@ __device__ __forceinline__ void st_end() {
     ST(ST_BAR);        \
   } while (0)
 __device__ __forceinline__ void st_sim(int) {}
+// an event count in category cat (thread 0's row): the categories past ST_DENTRY
+__device__ __forceinline__ void st_count(int cat) {
+  if (threadIdx.x == 0) st_state().acc[cat] += 1;
+}
 #elif defined(MUZ_TIMELINE)
 // ---- diagnostic per-wave timeline (make EXTRA=-DMUZ_TIMELINE): lane 0 of every wave of workgroup
 // MUZ_TL_WG records (s_memtime << 8 | category) at each segment end of simulation MUZ_TL_SIM.
@@ -130,6 +134,7 @@ __device__ __forceinline__ void st_sim(int sim) {
   ST(ST_N - 1);
 }
 __device__ __forceinline__ void st_end() {}
+__device__ __forceinline__ void st_count(int) {}
 #define SYNC()         \
   do {                 \
     ST(ST_OTHER);      \
@@ -141,6 +146,7 @@ __device__ __forceinline__ void st_sim(int) {}
 __device__ __forceinline__ void st_begin() {}
 __device__ __forceinline__ void ST(int) {}
 __device__ __forceinline__ void st_end() {}
+__device__ __forceinline__ void st_count(int) {}
 #define SYNC() __syncthreads()
 #endif
 

@@ -20,6 +20,12 @@ CATS = ["mfma-loops", "dense-epilogue", "barrier-wait", "row-ops", "select score
         "node loads + passes", "dense-entry"]
 
 
+def games_per_wg(B):
+    """k_dog_search's games per workgroup: one per wave (8) up to 2048 games unless MUZ_DOG_TILE_ROWS says 16."""
+    rows = os.environ.get("MUZ_DOG_TILE_ROWS")
+    return 8 if (rows == "8" if rows else B <= 2048) else 16
+
+
 def main():
     lib = L.load()
     fn = lib.muz_diag_dog_stamps2
@@ -44,11 +50,12 @@ def main():
         MD.gumbel_muzero_policy(net, lg, v, e, words, S, D, 1.0, seed=r, workspace=ws)
     torch.cuda.synchronize()
     fn(buf, 0)
-    tot = sum(buf[i] for i in range(12))
-    wg_sims = reps * ((B + 15) // 16) * S
+    tot = sum(buf[i] for i in range(len(CATS)))
+    wg_sims = reps * ((B + games_per_wg(B) - 1) // games_per_wg(B)) * S
     print(f"B={B} S={S} D={D}: {tot / wg_sims:.0f} cycles per workgroup-simulation")
     for i, c in enumerate(CATS):
         print(f"{c:>20}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / wg_sims:9.0f} cycles/sim")
+    print(f"interior selections of thread 0's game: {buf[9]}, on the exact path: {buf[10]}")
 
 
 def selfplay(turns=6):
@@ -58,7 +65,7 @@ def selfplay(turns=6):
     fn = lib.muz_diag_dog_stamps2
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-    B, S, D = 1024, 100, 50
+    B, S, D = int(os.environ.get("DIAG_B", "1500")), 100, 50
     net = MD.DeviceDogNet(MD.init_muzero_params(2))
     sp = GA.DogSelfPlay(net, B, S, D, 1.0, seed=4)
     sp.play(2)
@@ -69,11 +76,12 @@ def selfplay(turns=6):
     sp.play(turns)
     torch.cuda.synchronize()
     fn(buf, 0)
-    tot = sum(buf[i] for i in range(12))
-    wg_sims = turns * ((B + 15) // 16) * S
+    tot = sum(buf[i] for i in range(len(CATS)))
+    wg_sims = turns * ((B + games_per_wg(B) - 1) // games_per_wg(B)) * S
     print(f"DogSelfPlay B={B} S={S} D={D}, {turns} turns: {tot / wg_sims:.0f} cycles per workgroup-simulation")
     for i, c in enumerate(CATS):
         print(f"{c:>20}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / wg_sims:9.0f} cycles/sim")
+    print(f"interior selections of thread 0's game: {buf[9]}, on the exact path: {buf[10]}")
     words = sp.words.cpu().numpy().view(np.uint32)
     nleg = np.array([sum(bin(int(w)).count("1") for w in row) for row in words])
     print(f"legal actions per game: mean {nleg.mean():.1f}, max {nleg.max()}, phase-1 games {int(sp.env.phase.sum())}")

@@ -140,10 +140,18 @@ def test_dog_invalid_to_words_matches_legal_mask(cuda):
     assert torch.equal(MD.invalid_to_words(~valid.cpu()).cuda(), words)
 
 
-@pytest.mark.parametrize("S,D", [(50, 25), (16, 4), (8, 50)])
-def test_dog_search_logic_matches_mctx_restatement(cuda, S, D):
+@pytest.mark.parametrize("S,D,exact,rows", [(50, 25, False, None), (16, 4, False, None), (8, 50, False, "16"),
+                                            (50, 25, True, "16"), (100, 50, False, None), (100, 50, False, "16")])
+def test_dog_search_logic_matches_mctx_restatement(cuda, S, D, exact, rows, monkeypatch):
     """The oracle search driven by the GPU's own recurrent kernel: both sides see identical network outputs, so the
-    tree arithmetic (lane-order sums at A = 806, oracle/mctx_gumbel.py lane_tree_sum) must agree bit for bit."""
+    tree arithmetic (lane-order sums at A = 806, oracle/mctx_gumbel.py lane_tree_sum) must agree bit for bit.
+    exact: every interior selection on the 806-exponential path (MUZ_DOG_EXACT_SELECT=1) instead of the certified
+    argmax (dog_search.hip wselect_certified) -- both must give the restatement's actions.  rows: 16 games per
+    workgroup (MUZ_DOG_TILE_ROWS=16) instead of the one game per wave this batch size gets by default."""
+    if exact:
+        monkeypatch.setenv("MUZ_DOG_EXACT_SELECT", "1")
+    if rows:
+        monkeypatch.setenv("MUZ_DOG_TILE_ROWS", rows)
     from tests._parity import search_parity
     from oracle import mctx_gumbel as G
     MD, params, net, obs, valid, words = _search_setup(40, 7)
@@ -173,11 +181,14 @@ def test_dog_run_muzero_mcts_reference_signature(cuda):
     assert valid[np.arange(len(valid)), pol.action.cpu().numpy()].all()
 
 
-def test_dog_muzero_selfplay_followed_by_oracle(cuda):
+@pytest.mark.parametrize("rows", [None, "16"])
+def test_dog_muzero_selfplay_followed_by_oracle(cuda, rows, monkeypatch):
     """game_agent_dog.DogSelfPlay (legal -> encode -> root -> search at A = 806 -> step, finished games restarting in
     place) followed turn by turn by the oracle: oracle/dog.py transitions with the engine's deal keys, the oracle's
     own encoding fed to the GPU root kernel, and oracle/mctx_gumbel.py driven by the GPU recurrent kernel with the
-    engine's Gumbel stream -- every action, weight, root value and state bit-identical."""
+    engine's Gumbel stream -- every action, weight, root value and state bit-identical.  rows: as above."""
+    if rows:
+        monkeypatch.setenv("MUZ_DOG_TILE_ROWS", rows)
     from oracle import mctx_gumbel as G
     from oracle import selfplay as OS
     from exploring_muzero_on_dog_amd import dog as D
