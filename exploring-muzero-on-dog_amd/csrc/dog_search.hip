@@ -24,6 +24,7 @@ constexpr int kWMaxSims = 100, kWMaxNodes = kWMaxSims + 1, kWMaxDepth = 64;
 constexpr int kWWords = 26;                  // legal mask words (MUZ_DOG_MASK_WORDS)
 constexpr float kWFMin = -3.4028234663852886e38f;
 static_assert(kRowLanes == 32, "one game per 32 lanes");
+static_assert(kWMaxSims <= 255, "visit counts in 8 bits (WNode::vis4)");
 static_assert(kWPad >= kDogA && kWWords * 32 >= kDogA, "slots");
 static_assert(2 * kRows * kDogA <= kArenaFloats, "the walk's per-child arrays live in the idle network arena");
 
@@ -145,8 +146,8 @@ constexpr int kWHalf = kWJ / 2;   // slots per load batch
 
 // score_considered + masked_argmax at the root: gp = the root's Gumbel noise + (prior - max prior) (T.gum), loaded in
 // two batches of 13 slots (one at a time, the loads serialised on their uses: 26 L2 round trips)
-template <class Legal>
-__device__ __forceinline__ int wroot_argmax(const WTree& T, int g, int sub, const float* cq, const int (&vis)[kWJ],
+template <class Vis, class Legal>
+__device__ __forceinline__ int wroot_argmax(const WTree& T, int g, int sub, const float* cq, Vis vis,
                                             int cv, Legal legal_of) {
   float v = -INFINITY;
   int i = sub;
@@ -160,7 +161,7 @@ __device__ __forceinline__ int wroot_argmax(const WTree& T, int g, int sub, cons
     for (int k = 0; k < kWHalf; ++k) {
       const int j = kWHalf * h + k, a = sub + kRowLanes * j;
       float x = -INFINITY;
-      if (a < kDogA && legal_of(j)) x = fmaxf(-1e9f, gp[k] + cq[a]) + (vis[j] == cv ? 0.f : -INFINITY);
+      if (a < kDogA && legal_of(j)) x = fmaxf(-1e9f, gp[k] + cq[a]) + (vis(j) == cv ? 0.f : -INFINITY);
       if (x > v) {
         v = x;
         i = a;
@@ -198,7 +199,8 @@ __device__ __forceinline__ int wconsidered_visit(int m, int S, int idx) {
 struct WNode {
   float* pr;     // [806] of this row, LDS
   float* cq;     // [806] of this row, LDS (the visited children's; wfill_unvisited writes the rest)
-  int vis[kWJ];
+  uint32_t vis4[(kWJ + 3) / 4];   // visit counts, 8 bits per slot (<= S <= 100): registers the walk cannot spare
+  __device__ __forceinline__ int vis(int j) const { return (int)((vis4[j >> 2] >> (8 * (j & 3))) & 255u); }
   float pm;      // max prior logit
   int sv, mv;    // sum / max of the visit counts
   float es;      // sum of exp(prior - pm) (the prior normaliser)
@@ -242,6 +244,8 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
 #pragma clang fp contract(off)
   float pm = -INFINITY, u1 = -INFINITY, u2 = -INFINITY;
   int sv = 0, mv = 0, ui = kDogA;
+#pragma unroll
+  for (int w = 0; w < (kWJ + 3) / 4; ++w) nd.vis4[w] = 0u;
   // two batches of 13 slots, one 16-byte {prior, value, reward, discount} load + the visit count each, all of a batch in
   // flight together (left to itself the scheduler serialised them slot by slot to save registers: 26 round trips).
   // Padding slots are read too (they exist in the node's 832) and their values dropped.
@@ -261,7 +265,8 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
     for (int k = 0; k < kWHalf; ++k) {
       const int j = kWHalf * h + k, a = sub + kRowLanes * j;
       const bool ok = a < kDogA;
-      nd.vis[j] = ok ? vs[k] : 0;
+      const int vj = ok ? vs[k] : 0;
+      nd.vis4[j >> 2] |= (uint32_t)vj << (8 * (j & 3));
       if (ok) {
         const float p = c4[k][0];
         nd.pr[a] = p;
@@ -277,8 +282,8 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
           }
         }
       }
-      sv += nd.vis[j];
-      mv = max(mv, nd.vis[j]);
+      sv += vj;
+      mv = max(mv, vj);
     }
   }
   pm = row_max(pm);
@@ -318,7 +323,7 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
   }
   unsigned vm = 0;
 #pragma unroll
-  for (int j = 0; j < kWJ; ++j) vm |= (nd.vis[j] > 0 ? 1u : 0u) << j;
+  for (int j = 0; j < kWJ; ++j) vm |= (nd.vis(j) > 0 ? 1u : 0u) << j;
   nd.pm = pm;
   nd.sv = sv;
   nd.mv = mv;
@@ -450,7 +455,7 @@ __device__ __forceinline__ void wentries(const WNode& nd, const WTree& T, int g,
 __device__ __forceinline__ void wfill_unvisited(const WNode& nd, int sub) {
 #pragma unroll
   for (int j = 0; j < kWJ; ++j)
-    if (wok(sub, j) && nd.vis[j] == 0) nd.cq[sub + kRowLanes * j] = nd.K;
+    if (wok(sub, j) && ((nd.vm >> j) & 1u) == 0u) nd.cq[sub + kRowLanes * j] = nd.K;
 }
 
 // gumbel_muzero_interior_action_selection's argmax without the 806 exponentials, when it can be certified:
@@ -647,7 +652,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
             // gumbel_muzero_root_action_selection: score_considered + masked_argmax
             const int cv = wconsidered_visit(ncons, sa.S, nd.sv);
             wfill_unvisited(nd, sub);
-            bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, cv, legal_of);
+            bi = wroot_argmax(T, g, sub, nd.cq, [&](int j) { return nd.vis(j); }, cv, legal_of);
           } else if (pass == 0 && (bi = wselect_interior(nd, en, T, g, node, sub, vc, compact, sa.exact_select)) >= 0) {
           } else if (compact) {
             compact = false;   // the exact path reads all 806 children
@@ -677,7 +682,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
             const float inv_n = (float)(1 + nd.sv);
             bi = wargmax([&](int j) {
               const int a = sub + kRowLanes * j;
-              return a < kDogA ? (nd.pr[a] / zs - (float)nd.vis[j] / inv_n) : -INFINITY;
+              return a < kDogA ? (nd.pr[a] / zs - (float)nd.vis(j) / inv_n) : -INFINITY;
             }, sub);
           }
         }
@@ -812,7 +817,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     wnode_full(nd, T, g, 0, sub, s_ces[row]);
     wnode_tail(nd, sub, s_raw[row][0], sa);
     wfill_unvisited(nd, sub);
-    const int bi = wroot_argmax(T, g, sub, nd.cq, nd.vis, nd.mv, legal_of);   // considered_visit = max(visits)
+    const int bi = wroot_argmax(T, g, sub, nd.cq, [&](int j) { return nd.vis(j); }, nd.mv, legal_of);   // considered_visit = max(visits)
     // action_weights = softmax(_mask_invalid_actions(prior + completed_q))
     float zm = -INFINITY;
 #pragma unroll
