@@ -12,6 +12,7 @@
 //    agrees with the restatement bit for bit;
 //  * expand runs DynamicsNetwork4 + PredictionNetwork4 at A = 806 on the 16-row tile (nn.hpp, dog_nets.hpp), the
 //    806 prior logits going from the logits chunks straight into the new node's children.
+#define MUZ_OPAQUE_TID 1   // (nn.hpp tid())
 #include "dog_nets.hpp"
 #include "launch.hpp"
 #include "rng.hpp"

@@ -40,6 +40,18 @@ constexpr int kWaves = MUZ_TILE_WAVES;
 constexpr int kThreads = kWaves * 64;          // 512 / 1024
 constexpr int kRowLanes = kThreads / kRows;    // lanes per row in row-wise phases: 32 / 64
 constexpr int LAT = 256;
+// The thread index for the network helpers' lane / wave offsets.  MUZ_OPAQUE_TID (dog_search.hip): an opaque copy at
+// every use, so the offsets derived from it are recomputed where they are needed instead of being hoisted out of the
+// search loop into registers the networks need (the compiler spilled them and reloaded them inside the MFMA loops).
+#ifdef MUZ_OPAQUE_TID
+__device__ __forceinline__ unsigned tid() {
+  unsigned t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+#else
+__device__ __forceinline__ unsigned tid() { return threadIdx.x; }
+#endif
 // ---- diagnostic fine-grained stamps (make EXTRA=-DMUZ_STAMPS2); compiled out otherwise -------------
 enum { ST_MFMA = 0, ST_EPI = 1, ST_BAR = 2, ST_ROW = 3, ST_SEL = 4, ST_OTHER = 5, ST_TREE = 6, ST_PASS = 7, ST_DENTRY = 8,
        ST_N = 12 };
@@ -228,7 +240,7 @@ __device__ __forceinline__ P tree_ld(const P* p) {
 template <int NT, bool AG>
 __device__ __forceinline__ void mfma_ring_impl(const float* __restrict__ Wg, int KB, const float* A, int lda,
                                                f32x4 (&acc)[NT], f32x4 (&b0)[NT], f32x4 (&b1)[NT]) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tid() & 63;
   const int r = lane & 15, g = lane >> 4;
   const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(Wg)) + lane * NT;
   const int wstep = 64 * NT;   // f32x4 per k-block
@@ -309,7 +321,7 @@ __device__ __forceinline__ void mfma_ring(const float* __restrict__ Wg, int KB, 
 template <int NT>
 __device__ __forceinline__ void mfma_rows16(const float* __restrict__ Wg, int KB, const float* A, int lda,
                                             f32x4 (&acc)[NT]) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tid() & 63;
   const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(Wg)) + lane * NT;
   f32x4 b0[NT], b1[NT];
 #pragma unroll
@@ -329,7 +341,7 @@ struct Pf {
 };
 
 __device__ __forceinline__ const float* wave_group(const AS4 muz_dense& L, int KB, int NT) {
-  return L.w + (size_t)(threadIdx.x >> 6) * KB * 64 * NT * 4;
+  return L.w + (size_t)(tid() >> 6) * KB * 64 * NT * 4;
 }
 
 template <int NT>
@@ -337,8 +349,8 @@ __device__ __forceinline__ void pf_issue(Pf& pf, const AS4 muz_dense* L, int K, 
   static_assert(NT <= kPfMax, "prefetch buffer too small");
   if (!L) return;
   const int KB = (K + 15) >> 4;
-  if ((threadIdx.x >> 6) * NT * 16 >= N) return;
-  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(wave_group(*L, KB, NT))) + (threadIdx.x & 63) * NT;
+  if ((tid() >> 6) * NT * 16 >= N) return;
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(wave_group(*L, KB, NT))) + (tid() & 63) * NT;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     pf.v0[t] = wp[t];
@@ -351,9 +363,9 @@ __device__ __forceinline__ void pf_issue(Pf& pf, const AS4 muz_dense* L, int K, 
 // on exit.  A may live in LDS or global memory.  Caller synchronises before/after.
 // split-K prefetch of a <= 32-column layer (logits16_splitk): wave w takes k-block w of column tiles 0 and 1
 __device__ __forceinline__ void pf_issue_splitk(Pf& pf, const AS4 muz_dense* L, int K) {
-  const int KB = (K + 15) >> 4, w = threadIdx.x >> 6;
+  const int KB = (K + 15) >> 4, w = tid() >> 6;
   if (w >= KB) return;
-  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(L->w)) + (threadIdx.x & 63);
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(L->w)) + (tid() & 63);
   pf.v0[0] = wp[(0 * KB + w) * 64];   // packed [group][kb][lane][t = 0][4], groups = 16-column tiles
   pf.v1[0] = wp[(1 * KB + w) * 64];
 }
@@ -362,7 +374,7 @@ template <int NT, int NTN>
 __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, const float* A, int lda, float* out,
                                         int ldo, Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn,
                                         bool a_global = false, bool next_splitk = false) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = tid() & 63, wv = tid() >> 6;
   const int KB = (K + 15) >> 4;
   const int col0 = wv * NT * 16;
   auto pf_next = [&]() {
@@ -399,8 +411,8 @@ __device__ __forceinline__ void dense16(const AS4 muz_dense& L, int K, int N, co
 }
 
 // ---- row-wise ops: thread t -> row t/32, lane-in-row t%32 (half a wave per row) ---------------------
-__device__ __forceinline__ int trow() { return threadIdx.x / kRowLanes; }
-__device__ __forceinline__ int tsub() { return threadIdx.x % kRowLanes; }
+__device__ __forceinline__ int trow() { return tid() / kRowLanes; }
+__device__ __forceinline__ int tsub() { return tid() % kRowLanes; }
 // Row reductions on the DPP / permlane network (helpers above): xor-1 and xor-2 as quad_perm, then
 // half-row and row mirrors, then a permlane swap across the two 16-lane rows of a 32-lane row (and
 // across wave halves for 64-lane rows).  Every lane of a row ends with the same bits: each step
@@ -644,7 +656,7 @@ __device__ __forceinline__ void relu16(float* buf, int ld, int col0, int n) {
 template <int NTN>
 __device__ __forceinline__ void logits16_splitk(int K, const float* A, int lda, float* part, Pf& pf,
                                                 const AS4 muz_dense* Ln, int Kn, int Nn) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = tid() & 63, w = tid() >> 6;
   const int KB = (K + 15) >> 4;
   if (w >= KB) {
     pf_issue<NTN>(pf, Ln, Kn, Nn);
