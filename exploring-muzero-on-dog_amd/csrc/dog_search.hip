@@ -35,7 +35,8 @@ struct WTree {
   int32_t* c_index;   // [n][N][832]
   float* emb;         // [n][N][256]
   float* gum;         // [n][832] the root's Gumbel noise + (prior - max prior), drawn once per search
-  int32_t* vlist;     // [n][N][32] each node's visited children in first-visit order (s_vcnt: how many; -1 overflow)
+  f32x4* vrec;        // [n][N][32][2] each node's visited children in first-visit order (s_vcnt: how many; -1
+                      // overflow), one 32-byte record each: {child, visits, prior, value} {reward, discount, node, -}
   float* topp;        // [n][N][8] each node's 8 largest prior logits (value desc, index asc) ...
   int32_t* topi;      // [n][N][8] ... and their children
   int N;
@@ -48,9 +49,7 @@ struct WTree {
   }
   __device__ __forceinline__ AS1 int32_t* index() const { return gpw(c_index); }
   __device__ __forceinline__ AS1 int32_t* visits() const { return gpw(c_visits); }
-  __device__ __forceinline__ AS1 int32_t* vl(int g, int node) const {
-    return gpw(vlist) + ((size_t)g * N + node) * 32;
-  }
+  __device__ __forceinline__ AS1 f32x4* vr(int g, int node) const { return gpw(vrec) + ((size_t)g * N + node) * 64; }
   __device__ __forceinline__ AS1 float* tp(int g, int node) const { return gpw(topp) + ((size_t)g * N + node) * 8; }
   __device__ __forceinline__ AS1 int32_t* ti(int g, int node) const { return gpw(topi) + ((size_t)g * N + node) * 8; }
 };
@@ -73,8 +72,8 @@ static WTree carve_wide(void* ws, int n, int N) {
   p += (size_t)n * N * LAT * 4;
   t.gum = (float*)p;
   p += (size_t)n * kWPad * 4;
-  t.vlist = (int32_t*)p;
-  p += (size_t)n * N * kWList * 4;
+  t.vrec = (f32x4*)p;
+  p += (size_t)n * N * kWList * 32;
   t.topp = (float*)p;
   p += (size_t)n * N * kWTop * 4;
   t.topi = (int32_t*)p;
@@ -337,9 +336,31 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
 
 // lane l: the node's l-th visited child (a < 0: none) -- its index, visit count, prior and transformed completed Q
 struct WEntry {
-  int a, n;
-  float p, c;
+  int a, n, child;   // child index, visit count, the node it leads to
+  float p, c;        // prior, transformed completed Q
+  float r, d;        // reward, discount
 };
+
+// record l of a node's visited list into e (a = -1 when l >= vc) and its q = reward + discount * value
+__device__ __forceinline__ float wrec_load(WEntry& e, const WTree& T, int g, int node, int l, int vc) {
+  e.a = -1;
+  e.n = 0;
+  e.child = -1;
+  e.p = e.c = e.r = e.d = 0.f;
+  float q = 0.f;
+  if (l < vc) {
+    const AS1 f32x4* rp = T.vr(g, node) + 2 * l;
+    const f32x4 r0 = tree_ld(rp), r1 = tree_ld(rp + 1);
+    e.a = __float_as_int(r0[0]);
+    e.n = __float_as_int(r0[1]);
+    e.p = r0[2];
+    e.r = r1[0];
+    e.d = r1[1];
+    e.child = __float_as_int(r1[2]);
+    q = r1[0] + r1[1] * r0[3];   // q = reward + discount * value (Tree.qvalues)
+  }
+  return q;
+}
 
 // Compact load of a node walked before (its normaliser es and top-prior list cached, its visited list not
 // overflowed): only the visited children (lane l the list's l-th, one 16-byte load + the visit count) and the
@@ -349,28 +370,17 @@ struct WEntry {
 __device__ __forceinline__ bool wnode_compact(WNode& nd, const WTree& T, int g, int node, int sub, float es, int vc,
                                               WEntry& en) {
 #pragma clang fp contract(off)
-  const bool has = sub < vc;
-  en.a = -1;
-  en.n = 0;
-  en.p = 0.f;
-  f32x4 c4 = {0.f, 0.f, 0.f, 0.f};
   float tp = -INFINITY;
   int ti = kDogA;
-  if (has) en.a = tree_ld(T.vl(g, node) + sub);
   if (sub < kWTop) {
     tp = tree_ld(T.tp(g, node) + sub);
     ti = tree_ld(T.ti(g, node) + sub);
   }
-  if (has) {
-    const size_t e = T.ca(g, node, en.a);
-    c4 = tree_ld(T.node4() + e);
-    en.n = tree_ld(T.visits() + e);
-  }
+  const float q = wrec_load(en, T, g, node, sub, vc);
   ST(ST_PASS);   // (diagnostic builds: node loads)
-  if (has) {
-    en.p = c4[0];
-    nd.pr[en.a] = c4[0];
-    nd.cq[en.a] = c4[2] + c4[3] * c4[1];   // q = reward + discount * value (Tree.qvalues)
+  if (en.a >= 0) {
+    nd.pr[en.a] = en.p;
+    nd.cq[en.a] = q;
   }
   // this lane's visited slots: the list entries whose child sits in this lane
   unsigned vm = 0;
@@ -440,14 +450,12 @@ __device__ __forceinline__ void wnode_tail(WNode& nd, int sub, float raw, const 
 // the visited-list entries of a fully loaded node (priors / transformed Q from LDS); vc < 0 (overflowed list): none
 __device__ __forceinline__ void wentries(const WNode& nd, const WTree& T, int g, int node, int sub, int vc,
                                          WEntry& en) {
-  en.a = -1;
-  en.n = 0;
-  en.p = en.c = 0.f;
-  if (sub < vc) {
-    en.a = tree_ld(T.vl(g, node) + sub);
-    en.n = tree_ld(T.visits() + T.ca(g, node, en.a));
+  wrec_load(en, T, g, node, sub, vc);
+  if (en.a >= 0) {
     en.p = nd.pr[en.a];
     en.c = nd.cq[en.a];
+    // (the record's prior refreshed: the node's priors change when it is expanded again at the depth limit)
+    tree_st(reinterpret_cast<AS1 float*>(T.vr(g, node) + 2 * sub) + 2, en.p);
   }
 }
 
@@ -544,6 +552,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
   __shared__ int p_cvis[kRows][kWMaxDepth];
   __shared__ float p_rew[kRows][kWMaxDepth];
   __shared__ float p_disc[kRows][kWMaxDepth];
+  __shared__ float p_prior[kRows][kWMaxDepth];
   __shared__ uint32_t s_legal[kRows][kWWords];
   __shared__ float s_ces[kRows][kWMaxNodes];   // per-node softmax normalisers of the priors (wnode_full)
   __shared__ signed char s_vcnt[kRows][kWMaxNodes];   // per-node visited-list lengths (-1: overflowed)
@@ -639,6 +648,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         nd.cq = smem + (kRows + row) * kDogA;
         int bi;
         WEntry en;
+        en.a = -1;
+        bool cert = false;
         const int vc = s_vcnt[row][node];
         // interior nodes walked before: the compact load (the visited children and the top-prior list); the exact path
         // (no certificate) reloads the node in full on a second pass
@@ -655,6 +666,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
             wfill_unvisited(nd, sub);
             bi = wroot_argmax(T, g, sub, nd.cq, [&](int j) { return nd.vis(j); }, cv, legal_of);
           } else if (pass == 0 && (bi = wselect_interior(nd, en, T, g, node, sub, vc, compact, sa.exact_select)) >= 0) {
+            cert = true;
           } else if (compact) {
             compact = false;   // the exact path reads all 806 children
           } else {
@@ -688,15 +700,41 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
           }
         }
         ST(ST_SEL);   // (diagnostic builds: scores + argmax)
-        const size_t eb = T.ca(g, node, bi);
-        const int child = tree_ld(T.index() + eb);
-        if (sub == 0) {
+        // the chosen child's place in the node's visited list (-1: not on it; -2: the list was not loaded)
+        int lpos = -2;
+        if (depth > 0 && !sa.exact_select && vc >= 0) {
+          const unsigned bits = (unsigned)(__ballot(en.a == bi) >> (threadIdx.x & 32u));
+          lpos = bits ? __ffs(bits) - 1 : -1;
+        }
+        int child, cvis;
+        float crw, cdc, cpr;
+        if (cert && lpos >= 0) {   // a visited child: its record (the tree holds the same values)
+          child = __shfl(en.child, lpos, kRowLanes);
+          cvis = __shfl(en.n, lpos, kRowLanes);
+          crw = __shfl(en.r, lpos, kRowLanes);
+          cdc = __shfl(en.d, lpos, kRowLanes);
+          cpr = __shfl(en.p, lpos, kRowLanes);
+        } else if (cert) {         // the unvisited child of the largest prior: not expanded, zero reward / discount
+          child = -1;
+          cvis = 0;
+          crw = cdc = 0.f;
+          cpr = nd.u1;
+        } else {
+          const size_t eb = T.ca(g, node, bi);
           const f32x4 c4 = tree_ld(T.node4() + eb);
+          child = tree_ld(T.index() + eb);
+          cvis = tree_ld(T.visits() + eb);
+          crw = c4[2];
+          cdc = c4[3];
+          cpr = c4[0];
+        }
+        if (sub == 0) {
           p_node[row][depth] = node;
           p_act[row][depth] = bi;
-          p_rew[row][depth] = c4[2];
-          p_disc[row][depth] = c4[3];
-          p_cvis[row][depth] = tree_ld(T.visits() + eb);
+          p_rew[row][depth] = crw;
+          p_disc[row][depth] = cdc;
+          p_prior[row][depth] = cpr;
+          p_cvis[row][depth] = cvis | ((lpos + 2) << 16);
         }
         act = bi;
         nxt = child;
@@ -765,12 +803,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         const int l = base + sub;
         const int top = min(d, base + kRowLanes) - 1 - base;
         const bool on = sub <= top;
-        int parent = 0, pact = 0, cvis = 0, cnt = 0;
+        int parent = 0, pact = 0, cvis = 0, cnt = 0, lpos = -2;
         float r = 0.f, dsc = 0.f, pval = 0.f;
         if (on) {
           parent = p_node[row][l];
           pact = p_act[row][l];
-          cvis = p_cvis[row][l];
+          const int pc = p_cvis[row][l];
+          cvis = pc & 0xFFFF;
+          lpos = (pc >> 16) - 2;
           r = (l == d - 1) ? rw : p_rew[row][l];
           dsc = (l == d - 1) ? dc : p_disc[row][l];
           cnt = s_visits[row][parent];
@@ -793,12 +833,18 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
           tree_st(T.visits() + ei, cvis + 1);
           s_val[row][parent] = pv;
           s_visits[row][parent] = cnt + 1;
-          if (cvis == 0) {   // the edge's first visit: onto the parent's visited list (a path holds a node once)
-            const int k = s_vcnt[row][parent];
-            if (k >= 0) {
-              if (k < kWList) T.vl(g, parent)[k] = pact;
-              s_vcnt[row][parent] = (signed char)(k < kWList ? k + 1 : -1);
-            }
+          // the edge's record in the parent's visited list: appended at its first visit (a path holds a node once),
+          // rewritten at later ones (place known from the selection)
+          int k = lpos;
+          if (cvis == 0) {
+            k = s_vcnt[row][parent];
+            if (k >= 0) s_vcnt[row][parent] = (signed char)(k < kWList ? k + 1 : -1);
+          }
+          if (k >= 0 && k < kWList) {
+            const int cnode = (l == d - 1) ? nx : p_node[row][l + 1];
+            AS1 f32x4* rp = T.vr(g, parent) + 2 * k;
+            tree_st(rp, f32x4{__int_as_float(pact), __int_as_float(cvis + 1), p_prior[row][l], child_v});
+            tree_st(rp + 1, f32x4{r, dsc, __int_as_float(cnode), 0.f});
           }
         }
         carry = __shfl(leaf, 0, kRowLanes);
@@ -858,7 +904,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
 int64_t dog_search_workspace_bytes(int n, int S) {
   const int N = S + 1;
   return (int64_t)wide_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4 + (int64_t)n * kWPad * 4 +
-         (int64_t)n * N * (kWList + 2 * kWTop) * 4;
+         (int64_t)n * N * (kWList * 32 + 2 * kWTop * 4);
 }
 
 int launch_dog_search(const muz_dog_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,
