@@ -431,6 +431,9 @@ def run_dog_muzero(args):
     avg_ms = sms / (turns * world)
     flop = args.batch * args.sims * DOG_MZ_FLOP_PER_SIM
     achieved = flop / (avg_ms * 1e-3) / 1e12
+    # k_dog_search's games per workgroup (dog_search.hip muz_dog_gumbel_search): one per wave up to 2048 games
+    rows_env = os.environ.get("MUZ_DOG_TILE_ROWS")
+    gpw = 8 if ((rows_env == "8") if rows_env else args.batch <= 2048) else 16
     out = {
         "metric": "self-play env steps/sec + MCTS sims/sec, DOG 2v2 MuZero policy (config d, DOG MuZero slice)",
         "value": round(steps_done / elapsed, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
@@ -446,8 +449,10 @@ def run_dog_muzero(args):
         "roofline": {"bound": "mfma", "kernel": "k_dog_search", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "avg_launch_ms": round(avg_ms, 4),
                      "flop_per_sim": DOG_MZ_FLOP_PER_SIM, "executed_flop_per_sim": DOG_MZ_EXEC_FLOP_PER_SIM,
-                     "tiles": -(-args.batch // 16), "traffic": None,
-                     "note": "one 16-game tile per workgroup: 1024 games fill 64 of the 256 CUs"},
+                     "workgroups": -(-args.batch // gpw), "games_per_workgroup": gpw, "traffic": None,
+                     "note": f"{gpw} games per 16-row workgroup ({'one per wave' if gpw == 8 else 'two per wave'}): "
+                             f"{args.batch} games occupy {-(-args.batch // gpw)} of the 256 CUs; a workgroup's "
+                             f"search time is its serial chain of 100 simulations"},
     }
     print(json.dumps(out), flush=True)
     if dist is not None:
