@@ -971,13 +971,16 @@ int muz_dog_nets_recurrent(const muz_dog_net_w* w /*host*/, const int32_t* actio
                            float* reward, float* discount, float* prior_logits, float* value, float* next_embedding,
                            void* stream);
 
-/* Workspace bytes of n DOG searches (children arrays [n][S+1][832] x 6 + node embeddings). */
+/* Workspace bytes of n DOG searches (children arrays [n][S+1][832] x 6 + node embeddings + the root noise + per-node
+ * visited-child records [n][S+1][32] x 32 B and top-prior lists [n][S+1][8] x 8 B). */
 int64_t muz_dog_search_workspace_bytes(int32_t n, const muz_search_cfg* cfg /*host*/);
 
 /* run_muzero_mcts (muzero_dog.py:101-137): gumbel_muzero_policy at A = 806.  legal: muz_dog_legal's mask
  * [n][26] words (invalid = ~legal); gumbel [n][806] already scaled, or NULL for the device noise of
  * (cfg->seed, game, cfg->turn).  Outputs action [n] (-1 for a game without a legal action: the self-play loop's
- * no_step), action_weights [n][806], root_value [n]. */
+ * no_step), action_weights [n][806], root_value [n].  Results do not depend on the two environment switches it
+ * reads (tests use them): MUZ_DOG_EXACT_SELECT=1 runs every interior selection over all 806 exponentials instead of
+ * the certified argmax; MUZ_DOG_TILE_ROWS=8|16 forces one / two games per wave (default: one up to n = 2048). */
 int muz_dog_gumbel_search(const muz_dog_net_w* w /*host*/, const muz_search_cfg* cfg /*host*/,
                           const float* root_logits, const float* root_value, const float* root_embedding,
                           const uint32_t* legal, const float* gumbel, int32_t n, void* workspace,
