@@ -49,12 +49,21 @@ struct WTree {
   }
   __device__ __forceinline__ AS1 int32_t* index() const { return gpw(c_index); }
   __device__ __forceinline__ AS1 int32_t* visits() const { return gpw(c_visits); }
-  __device__ __forceinline__ AS1 f32x4* vr(int g, int node) const { return gpw(vrec) + ((size_t)g * N + node) * 64; }
-  __device__ __forceinline__ AS1 float* tp(int g, int node) const { return gpw(topp) + ((size_t)g * N + node) * 8; }
-  __device__ __forceinline__ AS1 int32_t* ti(int g, int node) const { return gpw(topi) + ((size_t)g * N + node) * 8; }
+  __device__ __forceinline__ AS1 f32x4* vr(int g, int node) const;
+  __device__ __forceinline__ AS1 float* tp(int g, int node) const;
+  __device__ __forceinline__ AS1 int32_t* ti(int g, int node) const;
 };
 constexpr int kWList = 32;   // visited children a node's list holds
 constexpr int kWTop = 8;     // largest priors a node keeps
+__device__ __forceinline__ AS1 f32x4* WTree::vr(int g, int node) const {
+  return gpw(vrec) + ((size_t)g * N + node) * (2 * kWList);
+}
+__device__ __forceinline__ AS1 float* WTree::tp(int g, int node) const {
+  return gpw(topp) + ((size_t)g * N + node) * kWTop;
+}
+__device__ __forceinline__ AS1 int32_t* WTree::ti(int g, int node) const {
+  return gpw(topi) + ((size_t)g * N + node) * kWTop;
+}
 
 static size_t wide_children_bytes(int64_t n, int N) { return (size_t)n * N * kWPad * 4; }
 
