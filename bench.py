@@ -442,15 +442,19 @@ def run_dog_muzero(args):
     sp = GA.DogSelfPlay(net, args.batch, args.sims, args.depth, 1.0, seed=4 + 1000 * rank, device=device)
     K = DOG_MZ_TURNS_PER_STEP
     ev = []
-    orig = MD.gumbel_muzero_policy
+    from exploring_muzero_on_dog_amd import lib as L
+    clib = L.load()
+    orig = clib.muz_dog_gumbel_search
 
-    def timed_search(*a, **kw):          # HIP events on the launching stream around every search launch
+    # HIP events on the launching stream around every search launch: the C call alone, so the host's argument
+    # preparation in muzero_dog.gumbel_muzero_policy stays outside (profiles/r4zf_dog_kernel_stats.csv)
+    def timed_search(*a):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        out = orig(*a, **kw)
+        rc = orig(*a)
         e1.record()
         ev.append((e0, e1))
-        return out
+        return rc
 
     def step(k):
         sp.play(K)
@@ -458,11 +462,11 @@ def run_dog_muzero(args):
     sp.play(1)                           # warmup turn (workspace, first launches)
     for _ in range(args.warmup):
         step(-1)
-    MD.gumbel_muzero_policy = timed_search
+    clib.muz_dog_gumbel_search = timed_search
     try:
         elapsed = timed_region(dist, step, args.steps)
     finally:
-        MD.gumbel_muzero_policy = orig
+        clib.muz_dog_gumbel_search = orig
     search_ms = sum(a.elapsed_time(b) for a, b in ev)
     turns = args.steps * K
     (steps_done, sms, games), elapsed = sum_max(dist, device, [args.batch * turns, search_ms,
