@@ -2,14 +2,17 @@
 // qtransform_completed_by_mix_value(value_scale=0.5), gumbel_scale = temperature) at A = 806, as ONE persistent
 // kernel per search -- k_gumbel_search's structure (csrc/search.hip) with wide nodes:
 //
-//  * a workgroup owns 16 games; game `row` has 32 lanes and lane `sub` holds children sub, sub + 32, ..., sub + 800
-//    (26 slots, 832 per node; slots >= 806 are padding);
+//  * a workgroup owns 16 games (8 -- one per wave -- up to 2048 games: SPARSE); game `row` has 32 lanes and lane
+//    `sub` holds children sub, sub + 32, ..., sub + 800 (26 slots, 832 per node; slots >= 806 are padding);
 //  * every node's children (the root's included) live in the workspace, [n][S+1][832] per field; the root's legal
 //    words sit in LDS (word j bit `sub` is child sub + 32 j, the layout of muz_dog_legal's mask);
 //  * sums over a node's children run in the lane order oracle/mctx_gumbel.py lane_tree_sum restates (each lane its
 //    slots in turn, then a balanced tree over the 32 lanes), maxima / minima / integer sums are exact, exp is
 //    correctly rounded and nothing contracts to fma -- so with identical network outputs the tree arithmetic
 //    agrees with the restatement bit for bit;
+//  * interior selections are certified from the visited children and the best unvisited prior (wselect_certified;
+//    the exact 806-exponential path when no certificate), nodes walked before are loaded compactly from their
+//    visited-child records and top-prior lists (wnode_compact), the root and first walks in full (wnode_full);
 //  * expand runs DynamicsNetwork4 + PredictionNetwork4 at A = 806 on the 16-row tile (nn.hpp, dog_nets.hpp), the
 //    806 prior logits going from the logits chunks straight into the new node's children.
 #define MUZ_OPAQUE_TID 1   // (nn.hpp tid())
