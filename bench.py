@@ -81,7 +81,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--batch", type=int, default=None,
+                    help=f"games per GPU (default: {BATCH}; dog: {DOG_BATCH}, dog --policy muzero: {DOG_MZ_GAMES})")
     ap.add_argument("--sims", type=int, default=None, help="MCTS simulations (det / classic 50, dog muzero 100)")
     ap.add_argument("--depth", type=int, default=None, help="MCTS max depth (det / classic 25, dog muzero 50)")
     ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
@@ -111,8 +112,8 @@ def parse():
                          "(det 4096 -> 2048/1024/512 per GPU); default is weak scaling, --batch games per GPU")
     args = ap.parse_args()
     dog_mz = args.workload == "dog" and args.policy == "muzero"
-    if args.workload == "dog" and args.batch == BATCH:
-        args.batch = DOG_MZ_GAMES if dog_mz else DOG_BATCH
+    if args.batch is None:
+        args.batch = (DOG_MZ_GAMES if dog_mz else DOG_BATCH) if args.workload == "dog" else BATCH
     if args.sims is None:
         args.sims = DOG_MZ_SIMS if dog_mz else S
     if args.depth is None:
