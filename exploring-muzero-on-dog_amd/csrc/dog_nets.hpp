@@ -5,6 +5,7 @@
 #include "nn.hpp"
 
 namespace muz {
+inline namespace MUZ_NN_NS {   // (nn.hpp)
 
 constexpr int kDogA = 806;                  // MUZ_DOG_ACTIONS
 constexpr int kDogC = 34;                   // MUZ_DOG_OBS_CHANNELS
@@ -37,4 +38,5 @@ __device__ __forceinline__ void dog_logits16(const AS4 muz_dog_net_w* W, const A
   hand(a.W, LDW, 768, kDogLastCols);
 }
 
+}  // namespace MUZ_NN_NS
 }  // namespace muz

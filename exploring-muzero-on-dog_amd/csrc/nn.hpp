@@ -24,7 +24,18 @@
 #pragma clang fp contract(off)
 #endif
 
+// Every entity below lives in an inline namespace named after the tid() variant (MUZ_OPAQUE_TID, set by
+// dog_search.hip only), so the two variants' inline functions and templates are distinct entities with distinct
+// mangled names -- no ODR violation even if the translation units were linked into one device code object
+// (-fgpu-rdc); muz::name still finds them.
+#ifdef MUZ_OPAQUE_TID
+#define MUZ_NN_NS nn_opaque_tid
+#else
+#define MUZ_NN_NS nn_direct_tid
+#endif
+
 namespace muz {
+inline namespace MUZ_NN_NS {
 
 #ifndef MUZ_TILE_WAVES
 #define MUZ_TILE_WAVES 8   // waves per 16-row tile workgroup: 8 (2 per SIMD) or 16 (4 per SIMD)
@@ -1066,4 +1077,5 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
   if constexpr (!PRED_LN0) SYNC();
 }
 
+}  // namespace MUZ_NN_NS
 }  // namespace muz

@@ -9,6 +9,7 @@
 #include "nn.hpp"
 
 namespace muz {
+inline namespace MUZ_NN_NS {   // (nn.hpp)
 
 constexpr int NT32 = nt_for(32), NT70 = nt_for(70);
 
@@ -155,4 +156,5 @@ __device__ __forceinline__ void sdyn_chance16(const AS4 muz_sdyn_w& D, const Fil
   film_trunk16<NTN>(chance_trunk(D), in, a, pf, Ln, Kn, Nn);
 }
 
+}  // namespace MUZ_NN_NS
 }  // namespace muz

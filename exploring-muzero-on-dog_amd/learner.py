@@ -137,7 +137,10 @@ class _ResStack(torch.autograd.Function):
             a.bias[l], a.gamma[l], a.beta[l] = (P[8 * b + 4 * k + i].data_ptr() for i in (1, 2, 3))
         a.x, a.X, a.out, a.z, a.stats = x.data_ptr(), X.data_ptr(), out.data_ptr(), z.data_ptr(), stats.data_ptr()
         _L.check(lib.muz_rbstack_fwd(ctypes.byref(a), _L.stream_ptr()), "muz_rbstack_fwd")
-        ctx.args, ctx.keep, ctx.X, ctx.P, ctx.owners = a, (WP, x, out, z, stats), X, P, owners
+        # the buffers the backward's pointers (ctx.args) read stay alive as long as ctx does, so a second backward
+        # (retain_graph) reads valid memory; the output is held by save_for_backward (no output -> ctx cycle)
+        ctx.save_for_backward(out)
+        ctx.args, ctx.keep, ctx.X, ctx.P, ctx.owners = a, (WP, x, z, stats), X, P, owners
         return out
 
     @staticmethod
@@ -151,8 +154,8 @@ class _ResStack(torch.autograd.Function):
         dx = torch.empty((M, Nn), dtype=dt, device=dev)
         dout = dout.contiguous()
         a.g, a.DZ, a.part, a.dx = dout.data_ptr(), DZ.data_ptr(), part.data_ptr(), dx.data_ptr()
+        ctx.saved_tensors   # (raises if the graph was freed by an earlier backward)
         _L.check(_L.load().muz_rbstack_bwd(ctypes.byref(a), _L.stream_ptr()), "muz_rbstack_bwd")
-        ctx.keep = None
         sink, o = _sink(), ctx.owners
         if sink is not None and o is not None:
             for l in range(L2):
@@ -714,7 +717,7 @@ class _TrunkChain(torch.autograd.Function):
         if _chain_usable(T, B, Nn, len(seen)):
             ctx.chain = _chain_forward(lat, scale1, shift.contiguous(), apps, slot, scaled, P, X, outs, qs, lohi, idx)
             ctx.X, ctx.P, ctx.grad_scale, ctx.apps = X, P, float(grad_scale), tuple(apps)
-            ctx.save_for_backward(scale1, qs, lohi)
+            ctx.save_for_backward(scale1, qs, lohi, outs)    # outs: read by the backward kernel (a.out)
             return (outs, outs.clone()) if heads else outs
         f0_next = None    # LayerNorm_0 + FiLM of the next application, formed by the boundary launch
         for i in range(T):
@@ -763,7 +766,7 @@ class _TrunkChain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, G, H=None):
-        scale1, qs, lohi = ctx.saved_tensors
+        scale1, qs, lohi = ctx.saved_tensors[:3]
         T, B, Nn = scale1.shape
         G = G.contiguous()
         H = None if H is None else H.contiguous()
@@ -905,7 +908,9 @@ def _chain_forward(lat, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi,
     a.out, a.q, a.lohi, a.idx = outs.data_ptr(), qs.data_ptr(), lohi.data_ptr(), idx.data_ptr()
     a.ln0_out, a.z, a.stats = ln0.data_ptr(), z.data_ptr(), stats.data_ptr()
     _L.check(lib.muz_trunk_chain_fwd(ctypes.byref(a), _L.stream_ptr()), "muz_trunk_chain_fwd")
-    return _Chain(a, (WP, ln0, z, stats, lat, scale1, shift, outs))
+    # kept as long as the autograd node (a second backward, retain_graph, reads them again); outs is the node's output
+    # and is held by its save_for_backward instead (an output stored on ctx would make an output -> ctx cycle)
+    return _Chain(a, (WP, ln0, z, stats, lat, scale1, shift))
 
 
 def _chain_backward(chain, G, H, grad_scale, apps, P, B, Nn):
@@ -933,7 +938,6 @@ def _chain_backward(chain, G, H, grad_scale, apps, P, B, Nn):
     a.grad_scale = grad_scale
     a.dscale, a.dshift, a.dlatent0 = dscale.data_ptr(), dshift.data_ptr(), dlat.data_ptr()
     _L.check(_L.load().muz_trunk_chain_bwd(ctypes.byref(a), _L.stream_ptr()), "muz_trunk_chain_bwd")
-    chain.keep = None
     return dlat, dscale, dshift, DZ, scr
 
 

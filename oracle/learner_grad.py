@@ -27,7 +27,8 @@ SCALES_CLASSIC = dict(value=4.0, policy=2.0, chance=0.5, discount=1.0, reward=1.
 
 
 class _Net:
-    def __init__(self, params: dict, dtype=torch.float64):
+    def __init__(self, params: dict, dtype=torch.float64, record: bool = False):
+        self.rec = [] if record else None
         self.p = {k: torch.tensor(np.asarray(v), dtype=dtype, requires_grad=True) for k, v in params.items()}
         self.dt = dtype
 
@@ -49,9 +50,21 @@ class _Net:
         return cols @ k.reshape(K * Cin, Cout) + self.p[f"{name}/bias"]
 
     def resblock(self, name, x):
-        y = torch.relu(self.ln(f"{name}/LayerNorm_0", self.dense(f"{name}/Dense_0", x)))
+        y = self.relu(self.ln(f"{name}/LayerNorm_0", self.dense(f"{name}/Dense_0", x)))
         y = self.ln(f"{name}/LayerNorm_1", self.dense(f"{name}/Dense_1", y))
-        return torch.relu(x + y)
+        return self.relu(x + y)
+
+    def relu(self, x):
+        if self.rec is not None:    # decision_margins: distance of every ReLU input to the kink, per batch row
+            self.rec.append(("relu", x.detach().reshape(x.shape[0], -1).abs()))
+        return torch.relu(x)
+
+    def _mm(self, x):
+        if self.rec is not None:    # decision_margins: gap of the two largest / smallest entries over the range
+            s = torch.sort(x.detach(), -1)[0]
+            gap = torch.minimum(s[:, -1] - s[:, -2], s[:, 1] - s[:, 0]) / (s[:, -1] - s[:, 0]).clamp_min(1e-30)
+            self.rec.append(("minmax", gap[:, None]))
+        return self.minmax(x)
 
     @staticmethod
     def minmax(x):
@@ -69,14 +82,14 @@ class _Net:
         x = torch.as_tensor(np.asarray(obs, np.float32)).to(self.dt)
         sp, g = x[:, :6, :].transpose(1, 2), x[:, 6:, 0]
         for i in range(3):
-            sp = torch.relu(self.ln(f"{r}/LayerNorm_{i}", self.conv(f"{r}/Conv_{i}", sp)))
-        flat = torch.relu(self.ln(f"{r}/LayerNorm_3", self.dense(f"{r}/Dense_0", sp.reshape(sp.shape[0], -1))))
-        g = torch.relu(self.ln(f"{r}/LayerNorm_4", self.dense(f"{r}/Dense_1", g)))
-        g = torch.relu(self.ln(f"{r}/LayerNorm_5", self.dense(f"{r}/Dense_2", g)))
-        h = torch.relu(self.ln(f"{r}/LayerNorm_6", self.dense(f"{r}/Dense_3", torch.cat([flat, g], -1))))
+            sp = self.relu(self.ln(f"{r}/LayerNorm_{i}", self.conv(f"{r}/Conv_{i}", sp)))
+        flat = self.relu(self.ln(f"{r}/LayerNorm_3", self.dense(f"{r}/Dense_0", sp.reshape(sp.shape[0], -1))))
+        g = self.relu(self.ln(f"{r}/LayerNorm_4", self.dense(f"{r}/Dense_1", g)))
+        g = self.relu(self.ln(f"{r}/LayerNorm_5", self.dense(f"{r}/Dense_2", g)))
+        h = self.relu(self.ln(f"{r}/LayerNorm_6", self.dense(f"{r}/Dense_3", torch.cat([flat, g], -1))))
         for b in range(6):
             h = self.resblock(f"{r}/ResBlock_{b}", h)
-        return self.minmax(self.dense(f"{r}/Dense_4", h))
+        return self._mm(self.dense(f"{r}/Dense_4", h))
 
     # PredictionNetwork4 (muzero_deterministic_madn.py:549-583; classic 192-226)
     def prediction(self, latent):
@@ -84,26 +97,26 @@ class _Net:
         x = self.ln(f"{p}/LayerNorm_0", latent)
         for b in range(2):
             x = self.resblock(f"{p}/ResBlock_{b}", x)
-        pol = torch.relu(self.ln(f"{p}/LayerNorm_1", self.dense(f"{p}/Dense_0", x)))
-        pol = torch.relu(self.ln(f"{p}/LayerNorm_2", self.dense(f"{p}/Dense_1", pol)))
-        v = torch.relu(self.ln(f"{p}/LayerNorm_3", self.dense(f"{p}/Dense_3", x)))
-        v = torch.relu(self.dense(f"{p}/Dense_4", v))
+        pol = self.relu(self.ln(f"{p}/LayerNorm_1", self.dense(f"{p}/Dense_0", x)))
+        pol = self.relu(self.ln(f"{p}/LayerNorm_2", self.dense(f"{p}/Dense_1", pol)))
+        v = self.relu(self.ln(f"{p}/LayerNorm_3", self.dense(f"{p}/Dense_3", x)))
+        v = self.relu(self.dense(f"{p}/Dense_4", v))
         return self.dense(f"{p}/Dense_2", pol), torch.tanh(self.dense(f"{p}/Dense_5", v))
 
     # DynamicsNetwork4 (muzero_deterministic_madn.py:391-457)
     def dynamics(self, latent, action, A=24):
         d = "dynamics"
         oh = self.one_hot(action, A)
-        e = torch.relu(self.dense(f"{d}/Dense_0", oh))
+        e = self.relu(self.dense(f"{d}/Dense_0", oh))
         x = self.ln(f"{d}/LayerNorm_0", latent) * (1.0 + self.dense(f"{d}/Dense_1", e)) + self.dense(f"{d}/Dense_2", e)
-        x = torch.relu(self.ln(f"{d}/LayerNorm_1", self.dense(f"{d}/Dense_3", x)))
-        x = torch.relu(self.ln(f"{d}/LayerNorm_2", self.dense(f"{d}/Dense_4", x)))
+        x = self.relu(self.ln(f"{d}/LayerNorm_1", self.dense(f"{d}/Dense_3", x)))
+        x = self.relu(self.ln(f"{d}/LayerNorm_2", self.dense(f"{d}/Dense_4", x)))
         for b in range(2):
             x = self.resblock(f"{d}/ResBlock_{b}", x)
-        nxt = self.minmax(latent + self.dense(f"{d}/Dense_5", x))
+        nxt = self._mm(latent + self.dense(f"{d}/Dense_5", x))
         ri = torch.cat([nxt, oh], -1)
-        rl = self.dense(f"{d}/reward_head", torch.relu(self.dense(f"{d}/Dense_6", ri)))
-        dl = self.dense(f"{d}/discount_head", torch.relu(self.dense(f"{d}/Dense_7", ri)))
+        rl = self.dense(f"{d}/reward_head", self.relu(self.dense(f"{d}/Dense_6", ri)))
+        dl = self.dense(f"{d}/discount_head", self.relu(self.dense(f"{d}/Dense_7", ri)))
         return nxt, rl, dl
 
     # StochasticDynamicsNetwork4 (muzero_classic_madn.py:314-408)
@@ -111,22 +124,22 @@ class _Net:
         d = "dynamics"
         x = self.ln(f"{d}/{pre}_input_ln", x_in) * (1.0 + self.dense(f"{d}/{pre}_film_scale", e)) + \
             self.dense(f"{d}/{pre}_film_shift", e)
-        x = torch.relu(self.ln(f"{d}/{pre}_ln1", self.dense(f"{d}/{pre}_dense1", x)))
-        x = torch.relu(self.ln(f"{d}/{pre}_ln2", self.dense(f"{d}/{pre}_dense2", x)))
+        x = self.relu(self.ln(f"{d}/{pre}_ln1", self.dense(f"{d}/{pre}_dense1", x)))
+        x = self.relu(self.ln(f"{d}/{pre}_ln2", self.dense(f"{d}/{pre}_dense2", x)))
         for r in range(rb0, rb0 + 2):
             x = self.resblock(f"{d}/ResBlock_{r}", x)
-        return self.minmax(x_in + self.dense(f"{d}/{pre}_proj", x))
+        return self._mm(x_in + self.dense(f"{d}/{pre}_proj", x))
 
     def action_dynamics(self, latent, action, A=4):
         d = "dynamics"
         oh = self.one_hot(action, A)
-        after = self._film_trunk("act", 0, latent, torch.relu(self.dense(f"{d}/act_embed", oh)))
-        rl = self.dense(f"{d}/reward_head", torch.relu(self.dense(f"{d}/reward_dense", torch.cat([after, oh], -1))))
-        dl = self.dense(f"{d}/discount_head", torch.relu(self.ln(f"{d}/discount_ln", self.dense(f"{d}/discount_dense", latent))))
+        after = self._film_trunk("act", 0, latent, self.relu(self.dense(f"{d}/act_embed", oh)))
+        rl = self.dense(f"{d}/reward_head", self.relu(self.dense(f"{d}/reward_dense", torch.cat([after, oh], -1))))
+        dl = self.dense(f"{d}/discount_head", self.relu(self.ln(f"{d}/discount_ln", self.dense(f"{d}/discount_dense", latent))))
         return after, rl, self.dense(f"{d}/chance_head", after), dl
 
     def chance_dynamics(self, after, chance, C=6):
-        e = torch.relu(self.dense("dynamics/chance_embed", self.one_hot(chance, C)))
+        e = self.relu(self.dense("dynamics/chance_embed", self.one_hot(chance, C)))
         return self._film_trunk("chance", 2, after, e)
 
 
@@ -240,3 +253,27 @@ def loss_and_grads(params: dict, batch: dict, unroll_steps: int = 10, classic: b
     total.backward()
     grads = {k: (p.grad if p.grad is not None else torch.zeros_like(p)).detach().numpy() for k, p in net.p.items()}
     return float(total.detach()), tuple(float(x.detach()) for x in parts), grads
+
+
+def decision_margins(params: dict, batch: dict, unroll_steps: int = 10, classic: bool = False):
+    """The loss's discontinuities, measured in float64: -> (dist [B], sites).  dist[b] = the smallest distance of batch
+    row b's forward (every unroll step) to a decision -- a ReLU input's |x| (the kink), or a min-max row's gap between
+    its two largest (smallest) entries over its range (the argmax / argmin that takes the extremum's gradient).  A
+    fp32 forward that differs from float64 by more than that may take the other side, which moves the gradient by
+    a fixed quantum (one ReLU element's or one extremum's whole contribution): the learner gradient test exempts
+    such rows, logged (tests/test_gpu_learner_oracle.py).  sites = [(distance, kind, call #, row, column)] sorted,
+    the 3 closest of every call."""
+    net = _Net(params, torch.float64, record=True)
+    with torch.no_grad():
+        (classic_loss if classic else det_loss)(net, batch, unroll_steps)
+    B = np.asarray(batch["actions"]).shape[0]
+    dist = np.full(B, np.inf)
+    sites = []
+    for call, (kind, t) in enumerate(net.rec):
+        m, idx = t.min(1)
+        dist = np.minimum(dist, m.numpy())
+        for r in torch.argsort(m)[:3].tolist():
+            sites.append((float(m[r]), kind, call, r, int(idx[r])))
+    sites.sort()
+    return dist, sites
+

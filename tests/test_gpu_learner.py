@@ -308,11 +308,11 @@ def test_chain_boundary_launches_bit_identical(cuda, kind):
         assert torch.equal(a, b), n
 
 
-def _chain_layer_st(chain, X, apps, lat0):
+def _chain_layer_st(chain, X, apps, lat0, outs):
     """The per-layer backward's saved tuples (_TrunkChain.forward's `st`) rebuilt from the chain kernel's forward
     buffers: (out, z, mean, rstd) per LayerNorm, out = the next weight layer's stacked input."""
     _, _, L, _, _ = _mods()
-    WT, ln0, z, stats, lat, scale1, shift, outs = chain.keep
+    WT, ln0, z, stats, lat, scale1, shift = chain.keep
     slot, _ = L._slots(apps, 2)
     st = []
     for i, g in enumerate(apps):
@@ -367,7 +367,7 @@ def test_chain_kernel_matches_layer_path(cuda, kind, B, K):
         lohi, idx = torch.empty(T, B, 2, device="cuda"), torch.empty(T, B, 2, dtype=torch.int32, device="cuda")
         scale1 = 1.0 + scale
         chain = L._chain_forward(lat0, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi, idx)
-        st = _chain_layer_st(chain, X, apps, lat0)
+        st = _chain_layer_st(chain, X, apps, lat0, outs)
         common = dict(saved_tensors=(scale1, qs, lohi), P=P, grad_scale=0.5, apps=tuple(apps), X=X)
         g_layer = L._TrunkChain.backward(types.SimpleNamespace(chain=None, st=st, boundary=True, scaled=tuple(scaled),
                                                                **common), G, H)
@@ -409,9 +409,12 @@ def test_rbstack_kernel_matches_layer_path(cuda, nb, M):
             fb = L._dense_ln_fwd(fa[0], Wb, bb, gb, beb, ref, L.LN_RESID_RELU)
             fs.append((ref, fa, fb))
             ref = fb[0]
-        ctx = types.SimpleNamespace()
+        class _Ctx(types.SimpleNamespace):    # what the forward / backward use of autograd's ctx
+            def save_for_backward(self, *t):
+                self.saved_tensors = t
+        ctx = _Ctx()
         out = L._ResStack.forward(ctx, x, None, *P)
-        X, (WP, _, _, z, stats) = ctx.X, ctx.keep
+        X, (WP, _, z, stats) = ctx.X, ctx.keep
         torch.cuda.synchronize()
         err = (out - ref).abs().max().item()
         assert err < 1e-5, f"forward differs by {err:.2e}"
@@ -575,6 +578,38 @@ def test_classic_chain_node_matches_per_step_autograd(cuda):
     for n, a, b in zip(["latent0", "act_embed", "chance_embed"] + names, g1, g2):
         err = (a - b).abs().max().item() / max(1e-3, b.abs().max().item())
         assert err < 1e-5, f"{n}: relative gradient difference {err:.2e}"
+
+
+def test_chain_and_stack_kernels_survive_a_second_backward(cuda):
+    """_TrunkChain (CHAIN_KERNEL) and _ResStack (RESBLOCK_STACK) hand raw device pointers to their backward
+    kernels; a second backward through the same graph (retain_graph) must read live buffers and give the same
+    gradients, and a backward after the graph was freed must raise instead of reading freed memory."""
+    _, _, L, _, _ = _mods()
+    from exploring_muzero_on_dog_amd import stochastic as ST
+    C, B, K = 20, 48, 4
+    params = ST.init_classic_params(C, seed=9)
+    nets = L.ClassicMuZeroNets(params, C, "cuda")
+    g = torch.Generator().manual_seed(3)
+    lat0 = torch.rand(B, 256, generator=g).cuda().requires_grad_(True)
+    film = [torch.randn(2 * K, B, 256, generator=g).cuda().mul_(0.1).requires_grad_(True) for _ in range(2)]
+    names = [n for kind in ("act", "chance") for n in L.trunk_param_names(kind)]
+    assert L.CHAIN_KERNEL and L.RESBLOCK_STACK
+    out = L._TrunkChain.apply(lat0, film[0], film[1], 0.5, (0, 1) * K, (False, True) * K, False,
+                              *(nets.p[n] for n in names))
+    h = nets._rbs("prediction/ResBlock_", 2, out.reshape(-1, 256))
+    w = torch.randn(h.shape, generator=g).cuda()
+    loss = (h * w).sum()
+    inputs = [lat0, film[0], film[1]] + [nets.p[n] for n in names]
+    g1 = torch.autograd.grad(loss, inputs, retain_graph=True)
+    torch.cuda.synchronize()
+    junk = [torch.full((1 << 22,), float("nan"), device="cuda") for _ in range(8)]   # reuse any freed block
+    g2 = torch.autograd.grad(loss, inputs)
+    torch.cuda.synchronize()
+    del junk
+    for n, a, b in zip(["latent0", "scale", "shift"] + names, g1, g2):
+        assert torch.equal(a, b), n
+    with pytest.raises(RuntimeError):
+        torch.autograd.grad(loss, inputs)
 
 
 def test_fused_adamw_matches_foreach_form(cuda):

@@ -1,19 +1,30 @@
 """The device learner against the oracle at config (e)'s shape.
 
 One graph-captured ``Learner.train_step`` -- fused bias / LayerNorm epilogues (_DenseLN), the K-step
-latent chain as one node (_TrunkChain), im2col convolutions, clip + AdamW in muz_adamw_step -- on a
-batch drawn from the device ring (4 players in teams, batch 128, unroll 10, td 50:
-train_with_reward.py:327-352) against:
+latent chain as one launch each way (_TrunkChain / csrc/learner_chain.hip), the ResBlock stacks (_ResStack), im2col
+convolutions, clip + AdamW in muz_adamw_step -- on a batch drawn from the device ring (4 players in teams, batch 128,
+unroll 10, td 50: train_with_reward.py:327-352) against:
   * oracle/learner.py ``loss_fn`` (the fp32 NumPy restatement of train_with_reward.py:24-146): total and
     every part within 1e-5 relative;
   * oracle/learner_grad.py (float64 restatement of value_and_grad in the reference's step order): every
-    parameter gradient, Frobenius-relative error per tensor <= max(1e-3, 3x the deviation of the same
-    restatement run in fp32, the reference's own precision; the ADVICE round-2 head-scaling bug was 0.2);
+    parameter gradient, Frobenius-relative error per tensor <= 3x the deviation of the same restatement run in fp32
+    (the reference's own precision: that tensor's, or the worst tensor's where the fp32 run is luckier) -- no
+    absolute floor;
   * oracle/learner.py ``AdamW`` (optax clip_by_global_norm(5) -> adamw restated): applied to the device's own
     gradients, the device's update within 1e-6; applied to the float64 oracle's gradients, the updated
     parameters -- entries off by > 1e-6 may only be where the exact gradient is below 1e-3 of its tensor's
     largest (Adam's first step is lr * sign(g), so fp32 noise flips it on near-zero gradients).
-The same for ``StochasticLearner`` against train_stochastic.py:34-199 (classic ring, td 25)."""
+The same for ``StochasticLearner`` against train_stochastic.py:34-199 (classic ring, td 25).
+
+Row exemption (round 5).  The loss is not continuous: a ReLU input at its kink or two tied min-max extrema decide
+where a whole gradient element goes, so a forward that differs from float64 by delta can move the gradient by a
+fixed quantum wherever a decision lies within delta.  profiles/r5c_sensitivity.log measured it: a 3e-7 relative
+perturbation of ONE forward tensor of the exact per-layer path moves the classic gradient from 1.6e-6 to exactly the
+2.34e-4 / 1.71e-4 the fused kernels showed (whose own outputs differ from the per-layer path's by <= 6.6e-7,
+r5b_chain_vs_layers.log); the oracle's closest decision in that batch is a ReLU input of 1.8e-8 (batch row 91).
+So the strict gradient bound is asserted on the batch without the rows whose float64 forward has a decision within
+TAU of its threshold (oracle/learner_grad.py decision_margins); the exempt rows, their distances and the full-batch
+error are logged.  Losses are continuous and are checked on the full batch."""
 import numpy as np
 import pytest
 import torch
@@ -25,18 +36,30 @@ from tests._parity import log
 pytestmark = pytest.mark.gpu
 
 LOSS_TOL = 1e-5
+TAU = 1e-6     # > the fp32 forward's deviation from float64 at a decision (measured <= 6.6e-7 relative, O(1) values)
 
 
 def _np_batch(batch):
     return {k: v.detach().cpu().numpy() for k, v in batch.items()}
 
 
-def _check(name, learner, params, batch, classic):
+def _grads(learner):
+    return {k: p.grad.detach().double().cpu().numpy() for k, p in learner.nets.p.items()}
+
+
+def _rel(g, ref):
+    """per tensor: (max-abs error / max |g|, Frobenius error / Frobenius norm)"""
+    return {k: (float(np.abs(g[k] - ref[k]).max()) / max(float(np.abs(ref[k]).max()), 1e-12),
+                float(np.linalg.norm(g[k] - ref[k])) / max(float(np.linalg.norm(ref[k])), 1e-12)) for k in ref}
+
+
+def _check(name, make, params, batch, classic):
+    learner = make(True)
     K = learner.unroll_steps
     b = _np_batch(batch)
+    # full batch: the losses (continuous) against the fp32 NumPy restatement
     out = learner.train_step(batch)
     torch.cuda.synchronize()
-    # losses vs the fp32 NumPy restatement
     if classic:
         wt, wparts = OL.loss_fn_stochastic(params, b, unroll_steps=K)
         keys = ("v_loss", "p_loss", "c_loss", "d_loss", "r_loss")
@@ -45,19 +68,33 @@ def _check(name, learner, params, batch, classic):
         keys = ("v_loss", "p_loss", "d_loss", "r_loss")
     lerr = abs(float(out["total_loss"]) - wt) / abs(wt)
     perr = max(abs(float(out[k]) - y) / max(abs(y), 1e-3) for k, y in zip(keys, wparts))
+    assert lerr <= LOSS_TOL and perr <= LOSS_TOL, (lerr, perr)
+    full_dev = _grads(learner)
+    _, _, full_ref = OG.loss_and_grads(params, b, unroll_steps=K, classic=classic)
+    fe = _rel(full_dev, full_ref)
+    full_worst = max(fe, key=lambda k: fe[k][1])
+    # the rows whose float64 forward lies within TAU of a decision are exempt from the strict gradient bound
+    dist, sites = OG.decision_margins(params, b, unroll_steps=K, classic=classic)
+    exempt = np.flatnonzero(dist < TAU)
+    keep = np.flatnonzero(dist >= TAU)
+    near = [s for s in sites if s[0] < TAU]
+    if len(exempt):
+        idx = torch.as_tensor(keep, device=batch["actions"].device)
+        batch = {k: v.index_select(0, idx) for k, v in batch.items()}
+        b = _np_batch(batch)
+        learner = make(True)
+        learner.train_step(batch)
+        torch.cuda.synchronize()
+    dev = _grads(learner)
     # gradients vs the float64 restatement, with the same restatement in fp32 (the reference's own precision)
     # as the yardstick: the device may deviate from exact arithmetic by no more than the fp32 reference does
     _, _, ref = OG.loss_and_grads(params, b, unroll_steps=K, classic=classic)
     _, _, r32 = OG.loss_and_grads(params, b, unroll_steps=K, classic=classic, dtype=torch.float32)
-    dev = {k: p.grad.detach().double().cpu().numpy() for k, p in learner.nets.p.items()}
-
-    def rel(g):     # per tensor: (max-abs error / max |g|, Frobenius error / Frobenius norm)
-        return {k: (float(np.abs(g[k] - ref[k]).max()) / max(float(np.abs(ref[k]).max()), 1e-12),
-                    float(np.linalg.norm(g[k] - ref[k])) / max(float(np.linalg.norm(ref[k])), 1e-12)) for k in ref}
-    gerr, gerr32 = rel(dev), rel({k: v.astype(np.float64) for k, v in r32.items()})
+    gerr, gerr32 = _rel(dev, ref), _rel({k: v.astype(np.float64) for k, v in r32.items()}, ref)
     worst = max(gerr, key=lambda k: gerr[k][0])
     worst_f = max(gerr, key=lambda k: gerr[k][1])
     worst32 = max(gerr32, key=lambda k: gerr32[k][1])
+    ratio = max(gerr, key=lambda k: gerr[k][1] / max(gerr32[k][1], 1e-30))
     # one clipped AdamW step: the oracle's update of the float64 / fp32 oracle gradients and of the device's
     f32 = lambda g: {k: v.astype(np.float32) for k, v in g.items()}      # noqa: E731
     ora = OL.AdamW(params).update(params, f32(ref))
@@ -75,20 +112,26 @@ def _check(name, learner, params, batch, classic):
     # m / (sqrt(v) + eps) = sign(g) for any |g| >> eps, so fp32 noise on a near-zero g flips the update)
     g_at_off = max([float(np.abs(ref[k][m]).max()) / max(float(np.abs(ref[k]).max()), 1e-30)
                     for k, m in off.items() if m.any()] or [0.0])
-    log(f"{name}: loss rel err {lerr:.2e}, parts {perr:.2e}; grads vs float64 (max-abs / Frobenius relative): "
+    log(f"{name}: loss rel err {lerr:.2e}, parts {perr:.2e}; full batch grads vs float64 Frobenius worst "
+        f"{fe[full_worst][1]:.2e} ({full_worst}); exempt rows (float64 decision within {TAU:.0e}) {exempt.tolist()} "
+        f"at {[f'{s[1]} call {s[2]} row {s[3]} col {s[4]}: {s[0]:.1e}' for s in near]}; on the other {len(keep)} rows: "
         f"device worst {gerr[worst][0]:.2e} ({worst}) / {gerr[worst_f][1]:.2e} ({worst_f}); fp32 restatement "
-        f"Frobenius worst {gerr32[worst32][1]:.2e} ({worst32}); global norm {gnorm:.3f}; one AdamW step vs the "
+        f"Frobenius worst {gerr32[worst32][1]:.2e} ({worst32}); largest device / fp32 ratio "
+        f"{gerr[ratio][1] / max(gerr32[ratio][1], 1e-30):.2f} ({ratio}); global norm {gnorm:.3f}; one AdamW step vs the "
         f"float64 oracle step: {n_off} of {n_par} entries differ > 1e-6 (fp32 restatement: {n_off32}), max |d| "
         f"{max(d_ora.values()):.2e}, all at |g| <= {g_at_off:.1e} x max|g| of their tensor; optimizer vs oracle "
         f"AdamW of the device grads: {d_own:.2e}")
-    assert lerr <= LOSS_TOL and perr <= LOSS_TOL, (lerr, perr)
-    for k in ref:     # per tensor, Frobenius: within 1e-3 or 3x the fp32 reference's own deviation
-        assert gerr[k][1] <= max(1e-3, 3.0 * gerr32[k][1]), (k, gerr[k], gerr32[k])
+    # per tensor, Frobenius: within 3x the fp32 restatement's deviation -- of that tensor, or its worst over all
+    # tensors where the fp32 run happens to be more exact than that (a one-output bias can land within 1e-8)
+    bound32 = gerr32[worst32][1]
+    for k in ref:
+        assert gerr[k][1] <= 3.0 * max(gerr32[k][1], bound32), (k, gerr[k], gerr32[k], bound32)
     assert d_own <= 1e-6, d_own
     assert g_at_off <= 1e-3, g_at_off
 
 
-def test_det_learner_step_matches_oracle_config_e(cuda):
+def _det_setup():
+    """config (e)'s det shape: 4 players in teams, a ring of 96 streamed games, batch 128, unroll 10, td 50"""
     from exploring_muzero_on_dog_amd import detmadn as E
     from exploring_muzero_on_dog_amd import game_agent as GA
     from exploring_muzero_on_dog_amd import learner as L
@@ -103,12 +146,11 @@ def test_det_learner_step_matches_oracle_config_e(cuda):
     ring = R.VectorizedReplayBuffer(20000, 128, 10, 50, obs_shape=(C, 56), max_episode_length=T,
                                     rng=np.random.RandomState(5))
     ring.save_games_from_buffers(eng.play_stream(96, seed=2, temperature=1.0))
-    learner = L.Learner(params, C, unroll_steps=10, graph=True)
-    _check("det learner (config e: 4p, batch 128, unroll 10, td 50)", learner, params, ring.sample_batch(),
-           classic=False)
+    return params, ring.sample_batch(), lambda graph=False: L.Learner(params, C, unroll_steps=10, graph=graph)
 
 
-def test_classic_learner_step_matches_oracle(cuda):
+def _classic_setup():
+    """the classic twin: 4p teams, batch 128, unroll 10, td 25"""
     from exploring_muzero_on_dog_amd import classic as CL
     from exploring_muzero_on_dog_amd import game_agent_stochastic as GS
     from exploring_muzero_on_dog_amd import learner as L
@@ -122,5 +164,50 @@ def test_classic_learner_step_matches_oracle(cuda):
     ring = R.VectorizedReplayBufferStochastic(20000, 128, 10, 25, obs_shape=(C, 56), max_episode_length=T,
                                               rng=np.random.RandomState(6))
     ring.save_games_from_buffers(eng.play_stream(96, seed=3))
-    learner = L.StochasticLearner(params, C, unroll_steps=10, graph=True)
-    _check("classic learner (4p, batch 128, unroll 10, td 25)", learner, params, ring.sample_batch(), classic=True)
+    return params, ring.sample_batch(), lambda graph=False: L.StochasticLearner(params, C, unroll_steps=10, graph=graph)
+
+
+def test_det_learner_step_matches_oracle_config_e(cuda):
+    params, batch, make = _det_setup()
+    _check("det learner (config e: 4p, batch 128, unroll 10, td 50)", make, params, batch, classic=False)
+
+
+def test_classic_learner_step_matches_oracle(cuda):
+    params, batch, make = _classic_setup()
+    _check("classic learner (4p, batch 128, unroll 10, td 25)", make, params, batch, classic=True)
+
+
+@pytest.mark.parametrize("classic", [False, True])
+def test_fused_kernels_match_per_layer_path_end_to_end(cuda, classic):
+    """The learner with its fused chain / ResBlock-stack kernels (CHAIN_KERNEL, RESBLOCK_STACK, RESBLOCK_NODE) against
+    the per-layer path, forward AND backward end to end on the same batch (each path computes its own forward values;
+    test_gpu_learner.py's kernel test shares saved values): losses within 1e-6 relative and every parameter gradient
+    within 1e-5 Frobenius-relative on the rows without a decision within TAU (see the module docstring)."""
+    from exploring_muzero_on_dog_amd import learner as L
+    params, batch, make = _classic_setup() if classic else _det_setup()
+    b = _np_batch(batch)
+    dist, _ = OG.decision_margins(params, b, unroll_steps=10, classic=classic)
+    idx = torch.as_tensor(np.flatnonzero(dist >= TAU), device=batch["actions"].device)
+    batch = {k: v.index_select(0, idx) for k, v in batch.items()}
+    switches = ("CHAIN_KERNEL", "RESBLOCK_STACK", "RESBLOCK_NODE")
+    saved = {s: getattr(L, s) for s in switches}
+    res = {}
+    try:
+        for fused in (True, False):
+            for s in switches:
+                setattr(L, s, fused)
+            learner = make()
+            out = learner.train_step(batch)
+            torch.cuda.synchronize()
+            res[fused] = ({k: float(v) for k, v in out.items()}, _grads(learner))
+    finally:
+        for s, v in saved.items():
+            setattr(L, s, v)
+    (lf, gf), (ll, gl) = res[True], res[False]
+    lerr = max(abs(lf[k] - ll[k]) / max(abs(ll[k]), 1e-3) for k in ll)
+    e = _rel(gf, gl)
+    worst = max(e, key=lambda k: e[k][1])
+    log(f"{'classic' if classic else 'det'} learner, fused kernels vs per-layer path end to end on {len(idx)} rows: "
+        f"losses {lerr:.2e}, gradients Frobenius worst {e[worst][1]:.2e} ({worst})")
+    assert lerr <= 1e-6, lerr
+    assert e[worst][1] <= 1e-5, (worst, e[worst])
