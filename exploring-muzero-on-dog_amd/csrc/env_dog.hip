@@ -1048,6 +1048,139 @@ __global__ __launch_bounds__(256) void k_dog_step(DetConsts c, muz_dog_soa st, c
   dog_store<WaveSync>(c, st, g, s, lane);
 }
 
+// ---- DOG MuZero self-play records (config (e) as MuZero_DOG/train.py trains: play_n_games_v3's buffer dict) ------
+// MuZero_DOG/game_agent.py:52-57 is `pass`; the det loop it copies (MuZero_det_MADN/game_agent.py:64-141) defines the
+// record of a turn: obs (zeros on a no-move turn), action (-1), reward class {0: -1, 1: 0, 2: +1} of a game-ending
+// step, root value, the search's action weights (zeros), mask (1 search turn, 0 no-move turn), the player and team
+// BEFORE the move, and the discount class (1 terminal or no-move turn, 2 same team moves next, 0 the other team).
+// One wave per lane (game in flight): the turn's record goes to row idx[slot] of the lane's trajectory slot
+// (lane_game[g]; < 0: an idle lane, left untouched), then env_step / no_step as k_dog_step; a game that ended (done,
+// or its max_steps-th record) restarts in place (deal counter continued) and sets ended[g] for k_dog_sp_assign.
+constexpr int kDogObsBytes = 34 * kCells;   // (dog_nets.hpp kDogC x 56)
+
+struct DogSpArgs {
+  DetConsts c;
+  muz_dog_soa st;
+  const float* obs;         // [n][34][56] this turn's encode_board (the networks' input)
+  const int32_t* action;    // [n] (-1: no legal action -> no_step)
+  const float* weights;     // [n][806]
+  const float* root_value;  // [n]
+  unsigned long long seed;
+  muz_traj traj;            // [num_games][T], obs int8 [34][56], pol [806]
+  int32_t* lane_game;       // [n] trajectory slot of the lane's game, -1 idle
+  int32_t* ended;           // [n] out: 1 when the lane's game ended this turn
+  uint32_t* episodes;       // [n] nullable: finished (done) games per lane
+  int n;
+};
+
+__global__ __launch_bounds__(256) void k_dog_sp_record_step(DogSpArgs P) {
+  __shared__ DogG sg[kDogGamesPerBlock];
+  __shared__ int sh_deal[kDogGamesPerBlock], sh_end[kDogGamesPerBlock];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = blockIdx.x * kDogGamesPerBlock + w;
+  if (g >= P.n) return;
+  const int slot = P.lane_game[g];
+  if (slot < 0) {
+    if (lane == 0) P.ended[g] = 0;
+    return;
+  }
+  const DetConsts& c = P.c;
+  DogG& s = sg[w];
+  dog_load<WaveSync>(c, P.st, g, s, lane);
+  const int T = P.traj.max_steps;
+  const int t = P.traj.idx[slot];
+  const int a = P.action[g];
+  const int cp0 = s.cp;
+  const size_t row = (size_t)slot * T + t;
+  {   // the observation (int8, exact: values 0..110) and the policy of the turn
+    const float* src = P.obs + (size_t)g * kDogObsBytes;
+    int8_t* o = P.traj.obs + row * kDogObsBytes;
+    for (int i = lane; i < kDogObsBytes; i += 64) o[i] = a >= 0 ? (int8_t)src[i] : (int8_t)0;
+    const float* ws = P.weights + (size_t)g * kDogActions;
+    float* pp = P.traj.pol + row * kDogActions;
+    for (int i = lane; i < kDogActions; i += 64) pp[i] = a >= 0 ? ws[i] : 0.f;
+  }
+  int r = 0, d = 0;
+  if (lane == 0) {
+    int deal;
+    if (a < 0) {
+      deal = dog_no_step(c, s);
+      d = s.done;
+    } else {
+      deal = dog_env_step(c, s, a, r, d);
+    }
+    sh_deal[w] = deal;
+  }
+  wave_sync();
+  if (sh_deal[w]) dog_deal<WaveSync>(c, s, P.seed, g, lane);
+  if (lane == 0) {
+    const int cp1 = s.cp;     // next_env.current_player (after the step's deal)
+    const bool teams = has(c.flags, R_TEAMS);
+    const muz_traj& tr = P.traj;
+    int rew = 1, disc = 1;
+    if (a >= 0) {
+      rew = (d && r > 0) ? 2 : ((d && r < 0) ? 0 : 1);
+      disc = d ? 1 : ((teams ? (cp0 & 1) == (cp1 & 1) : cp0 == cp1) ? 2 : 0);
+    }
+    tr.act[row] = a >= 0 ? a : -1;
+    tr.rew[row] = rew;
+    tr.val[row] = a >= 0 ? P.root_value[g] : 0.f;
+    tr.mask[row] = a >= 0 ? 1.f : 0.f;
+    tr.player[row] = cp0;
+    tr.team[row] = teams ? (cp0 & 1) : -1;
+    tr.discount[row] = disc;
+    tr.idx[slot] = t + 1;
+    const int end = (d || t + 1 >= T) ? 1 : 0;
+    P.ended[g] = end;
+    sh_end[w] = end;
+    if (P.episodes && d) P.episodes[g] += 1u;
+  }
+  wave_sync();
+  if (sh_end[w]) dog_reset_lds<WaveSync>(c, s, P.seed, g, s.deal, lane);   // (every lane has read s.done / cp)
+  dog_store<WaveSync>(c, P.st, g, s, lane);
+}
+
+// The lanes whose game ended take the next game numbers in lane order (one workgroup, deterministic): ctr[0] = next
+// game number, ctr[1] = num_games, ctr[2] (out) = lanes still holding a game.  A lane past num_games goes idle.
+__global__ __launch_bounds__(1024) void k_dog_sp_assign(int32_t* lane_game, const int32_t* ended, int32_t* idx,
+                                                        int32_t* ctr, int n) {
+  __shared__ int wsum[16];
+  __shared__ int base_s, active_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) base_s = ctr[0], active_s = 0;
+  __syncthreads();
+  const int ng = ctr[1];
+  for (int l0 = 0; l0 < n; l0 += 1024) {
+    const int l = l0 + tid;
+    const bool fin = l < n && lane_game[l] >= 0 && ended[l];
+    const unsigned long long b = __ballot(fin);
+    const int pre = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(b);
+    __syncthreads();
+    int off = base_s;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    if (fin) {
+      const int slot = off + pre;
+      lane_game[l] = slot < ng ? slot : -1;
+      if (slot < ng) idx[slot] = 0;
+    }
+    const int act = (l < n && lane_game[l] >= 0) ? 1 : 0;
+    const int wa = __popcll(__ballot(act));
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int k = 0; k < 16; ++k) tot += wsum[k];
+      base_s += tot;
+    }
+    if (lane == 0 && wa) atomicAdd(&active_s, wa);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    ctr[0] = base_s;
+    ctr[2] = active_s;
+  }
+}
+
 // One step_* function of dog.py on its own (the form DOG/test.py calls): kind 0 step_swap(pin, pos),
 // 1 step_normal_move(pin, move), 2 step_neg_move(pin, move), 3 step_hot_7(d0..d3).  Board and pins change;
 // hands, turn and the state's reward / done fields do not (the reference returns them separately).
@@ -1189,6 +1322,24 @@ int muz_dog_step_restart(const muz_rules* rules, muz_dog_soa st, const int32_t* 
                          uint8_t* done, uint32_t* episodes, int32_t n, void* stream) {
   DOG_PROLOGUE(action != nullptr)
   k_dog_step<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(c, st, action, 0, seed, reward, done, n, 1, episodes);
+  return muz_last_launch_error();
+}
+
+int muz_dog_sp_record_step(const muz_rules* rules, muz_dog_soa st, const float* obs, const int32_t* action,
+                           const float* action_weights, const float* root_value, uint64_t seed, muz_traj traj,
+                           int32_t* lane_game, int32_t* ended, uint32_t* episodes, int32_t n, void* stream) {
+  DOG_PROLOGUE(obs && action && action_weights && root_value && lane_game && ended)
+  MUZ_HOST_CHECK(c.P == 4 && traj.max_steps > 0 && traj.obs && traj.act && traj.rew && traj.val && traj.pol &&
+                 traj.mask && traj.player && traj.team && traj.discount && traj.idx);
+  k_dog_sp_record_step<<<dog_blocks(n), 256, 0, (hipStream_t)stream>>>(
+      DogSpArgs{c, st, obs, action, action_weights, root_value, seed, traj, lane_game, ended, episodes, n});
+  return muz_last_launch_error();
+}
+
+int muz_dog_sp_assign(int32_t* lane_game, const int32_t* ended, int32_t* traj_idx, int32_t* counters, int32_t n,
+                      void* stream) {
+  MUZ_HOST_CHECK(n >= 0 && lane_game && ended && traj_idx && counters);
+  k_dog_sp_assign<<<1, 1024, 0, (hipStream_t)stream>>>(lane_game, ended, traj_idx, counters, n);
   return muz_last_launch_error();
 }
 

@@ -281,6 +281,9 @@ SIGNATURES = {
                                     vp]),
     "muz_dog_step_restart": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_uint64, vp, vp, vp,
                                             ctypes.c_int32, vp]),
+    "muz_dog_sp_record_step": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, vp, vp, vp, ctypes.c_uint64,
+                                              MuzTraj, vp, vp, vp, ctypes.c_int32, vp]),
+    "muz_dog_sp_assign": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int32, vp]),
     "muz_dog_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, ctypes.c_uint64, vp, vp, ctypes.c_int32,
                                       vp]),
     "muz_dog_step_move": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, vp, vp, vp, ctypes.c_int32, vp]),

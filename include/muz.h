@@ -987,6 +987,23 @@ int muz_dog_gumbel_search(const muz_dog_net_w* w /*host*/, const muz_search_cfg*
                           int64_t workspace_bytes, int32_t* action, float* action_weights, float* root_value_out,
                           void* stream);
 
+/* The DOG MuZero self-play turn's bookkeeping (config (e) as MuZero_DOG/train.py:168-300 trains; its
+ * play_batch_of_games_jitted, MuZero_DOG/game_agent.py:52-57, is `pass` -- the record is the det loop's,
+ * MuZero_det_MADN/game_agent.py:64-141) fused with the step: for every lane g with lane_game[g] >= 0 writes the
+ * turn's row idx[slot] of trajectory slot lane_game[g] (traj: [num_games][max_steps], obs int8 [34][56] from this
+ * turn's muz_dog_encode `obs`, pol [806] = action_weights; zero obs / pol, act -1, value 0, mask 0, reward and
+ * discount class 1 on a no-move turn, action[g] < 0), applies env_step / no_step (+ deal), and restarts a game that
+ * ended (done, or its max_steps-th record) in place (deal counter continued), setting ended[g].  Lanes with
+ * lane_game[g] < 0 are idle (untouched).  episodes[g] (nullable) counts finished games. */
+int muz_dog_sp_record_step(const muz_rules* rules /*host*/, muz_dog_soa state, const float* obs, const int32_t* action,
+                           const float* action_weights, const float* root_value, uint64_t seed, muz_traj traj,
+                           int32_t* lane_game, int32_t* ended, uint32_t* episodes, int32_t n, void* stream);
+/* After muz_dog_sp_record_step: lanes whose game ended take the next game numbers in lane order (deterministic):
+ * counters (device int32[3]) = {next game number, num_games, out: lanes still holding a game}; a newly assigned
+ * slot's traj_idx is zeroed; a lane past num_games goes idle (-1). */
+int muz_dog_sp_assign(int32_t* lane_game, const int32_t* ended, int32_t* traj_idx, int32_t* counters, int32_t n,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -89,3 +89,24 @@ def root_inference(params, obs):
 def recurrent_inference(params, action, emb):
     """recurrent_inference_fn for the slice: DynamicsNetwork4 (one-hot 806) -> PredictionNetwork4."""
     return ON.recurrent_inference(params, action, emb)
+
+
+def turn_record(env: D.State, action: int, weights, root_value: float, reward: int, done: bool, next_player: int):
+    """One turn's row of the DOG self-play buffers (MuZero_DOG/game_agent.py:52-57 is ``pass``; the det loop it copies,
+    MuZero_det_MADN/game_agent.py:64-141, defines it): ``env`` the state before the move, ``action`` < 0 a turn without
+    a legal action (no_step), (reward, done, next_player) the step's result.  -> dict of the row's fields."""
+    teams = bool(env.rules["enable_teams"])
+    cp = int(env.current_player)
+    team = cp % 2 if teams else -1
+    if action < 0:       # do_skip (game_agent.py:112-116): zeros, act -1, value 0, mask 0, discount / reward class 1
+        return dict(obs=np.zeros((NUM_CHANNELS, CELLS), np.int8), act=-1, rew=1, val=np.float32(0.0),
+                    pol=np.zeros(NUM_ACTIONS, np.float32), mask=0.0, player=cp, team=team, discount=1)
+    rew = 2 if (done and reward > 0) else (0 if (done and reward < 0) else 1)              # lines 95-99
+    if done:
+        disc = 1                                                                          # lines 102-109
+    elif teams:
+        disc = 2 if cp % 2 == next_player % 2 else 0
+    else:
+        disc = 2 if cp == next_player else 0
+    return dict(obs=encode_board(env).astype(np.int8), act=int(action), rew=rew, val=np.float32(root_value),
+                pol=np.asarray(weights, np.float32), mask=1.0, player=cp, team=team, discount=disc)

@@ -1,0 +1,117 @@
+"""DOG self-play records on the GPU (config (e) as MuZero_DOG/train.py trains: play_n_games_v3's buffer dict).
+
+The reference's DOG loop (MuZero_DOG/game_agent.py:52-57) is ``pass``; the record of a turn is the det loop's
+(MuZero_det_MADN/game_agent.py:64-141), restated by oracle/dog_muzero.py ``turn_record``.  game_agent_dog.DogSelfPlay in
+recording mode (muz_dog_sp_record_step + muz_dog_sp_assign) is followed turn by turn by oracle/dog.py with the
+engine's deal keys: every lane's state, and in the end every field of every recorded row, identical.  The actions,
+weights and values the rows carry are the device search's (their parity vs the mctx restatement is
+tests/test_gpu_dog_muzero.py's); here they are checked legal and copied exactly."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dog as dg
+from oracle import dog_muzero as DM
+from tests.dog_states import RULE_SETS, reset
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("obs", "act", "rew", "val", "pol", "mask", "player", "team", "discount")
+
+
+def _restart(e1, keys_g):
+    """muz_dog_sp_record_step's in-place restart: env_reset with the lane's deal counter continued."""
+    base = e1.deal
+    e2 = dg.env_reset(num_players=4, shuffle_keys=lambda x, b=base, k=keys_g: k(x.replace(deal=x.deal + b)),
+                      **dg.SELFPLAY_RULES)
+    return e2.replace(deal=e2.deal + base)
+
+
+def test_dog_records_followed_by_oracle(cuda):
+    """4 lanes, 7 games of at most 40 records each (every game is cut at max_steps, lanes reassigned in lane order,
+    the last lane going idle): the device buffers equal the oracle's rows."""
+    from exploring_muzero_on_dog_amd import dog as D
+    from exploring_muzero_on_dog_amd import game_agent_dog as GA
+    from exploring_muzero_on_dog_amd import muzero_dog as MD
+    from tests.dog_states import diff
+    params = DM.init_params(seed=17, randomize_affine=True)
+    net = MD.DeviceDogNet(params)
+    B, G, T, seed = 4, 7, 40, 33
+    sp = GA.DogSelfPlay(net, B, 4, 3, 1.0, seed=seed)
+    rec = sp.start_records(G, T)
+    keys = [dg.engine_shuffle_keys(seed, g) for g in range(B)]
+    envs = [reset(RULE_SETS["selfplay_4p_teams"], seed, g) for g in range(B)]
+    lane_game = [g if g < G else -1 for g in range(B)]
+    nxt = min(B, G)
+    want = {k: [[None] * T for _ in range(G)] for k in FIELDS}
+    length = [0] * G
+    turns = 0
+    while any(x >= 0 for x in lane_game):
+        act, w, rv = (x.cpu().numpy() for x in sp.turn())
+        ended = []
+        for g in range(B):
+            slot = lane_game[g]
+            if slot < 0:
+                continue
+            e0 = envs[g]
+            valid = dg.valid_actions(e0).astype(bool)
+            a = int(act[g])
+            assert (a < 0) == (not valid.any()) and (a < 0 or valid[a]), (turns, g, a)
+            e1, r, d = dg.no_step(e0, keys[g]) if a < 0 else dg.env_step(e0, a, keys[g])
+            row = DM.turn_record(e0, a, w[g], rv[g], int(r), bool(d), int(e1.current_player))
+            t = length[slot]
+            for k in FIELDS:
+                want[k][slot][t] = row[k]
+            length[slot] = t + 1
+            if d or t + 1 >= T:
+                e1 = _restart(e1, keys[g])
+                ended.append(g)
+            envs[g] = e1
+        for g in ended:                 # muz_dog_sp_assign: next game numbers in lane order
+            lane_game[g] = nxt if nxt < G else -1
+            nxt += 1
+        turns += 1
+        assert torch.equal(sp.lane_game.cpu(), torch.tensor(lane_game, dtype=torch.int32)), turns
+        live = [g for g in range(B) if lane_game[g] >= 0]
+        host = D.to_host(sp.env)
+        bad = diff({k: v[live] for k, v in host.items()} if live else {}, [envs[g] for g in live]) if live else None
+        assert bad is None, (turns, bad)
+        assert turns < 400
+    assert sp.active_lanes() == 0
+    got = {k: v.cpu().numpy() for k, v in rec.items()}
+    assert got["idx"].tolist() == length
+    for slot in range(G):
+        for t in range(length[slot]):
+            for k in FIELDS:
+                assert np.array_equal(np.asarray(got[k][slot, t]), np.asarray(want[k][slot][t])), (slot, t, k)
+    assert all(x == T for x in length)          # every game ran into max_steps
+    assert got["mask"][:, :T].sum() > 0.5 * G * T
+
+
+def test_dog_play_stream_finished_games(cuda):
+    """Long games (max_steps 3000, practically no cut): a game ends done, its last row is the terminal one (discount class 1,
+    reward class 2 for the winning side's move), rows are consistent (mask 1 <=> act >= 0 <=> a probability
+    vector in pol; no-move rows all zero), players / teams alternate as recorded, and the reference-signature
+    play_n_games_v3 returns the same buffers for the same key."""
+    from exploring_muzero_on_dog_amd import game_agent_dog as GA
+    from exploring_muzero_on_dog_amd import muzero_dog as MD
+    net = MD.DeviceDogNet(MD.init_muzero_params(3))
+    B, G, T = 32, 40, 3000
+    sp = GA.DogSelfPlay(net, B, 2, 2, 1.0, seed=5)
+    buf = {k: v.clone() for k, v in sp.play_stream(G, T, seed=9).items()}
+    b = {k: v.cpu().numpy() for k, v in buf.items()}
+    n = b["idx"]
+    assert (n > 0).all() and (n < T).sum() >= 0.9 * G, n
+    for g in range(G):
+        L = n[g]
+        if L == T:
+            continue
+        m, a = b["mask"][g, :L], b["act"][g, :L]
+        assert np.array_equal(m > 0, a >= 0)
+        assert np.allclose(b["pol"][g, :L][m > 0].sum(-1), 1.0, atol=1e-5)
+        assert not b["pol"][g, :L][m == 0].any() and not b["obs"][g, :L][m == 0].any()
+        assert b["discount"][g, L - 1] == 1 and b["rew"][g, L - 1] == 2 and m[L - 1] == 1
+        assert set(np.unique(b["discount"][g, :L - 1])) <= {0, 1, 2}
+        assert (b["team"][g, :L] == b["player"][g, :L] % 2).all()
+    ref = GA.play_n_games_v3(net, 9, (34, 56), B, 2, 2, T, 1.0, obs_dtype=torch.int8)
+    assert ref["idx"].shape == (B,) and int(ref["idx"].min()) > 0
