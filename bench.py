@@ -51,6 +51,9 @@ PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E
 # Pred4 K + 1 = 11 times (404,544), Dyn4 K = 10 times (529,280) -> 13,123,264 MAC forward; x2 FLOP, x3 for
 # forward + backward, x batch 128
 LEARNER_FLOP_PER_STEP = 3 * 2 * 13_123_264 * 128
+# MuZero_DOG/train.py's learner step on the DOG slice's nets: Repr 3,380,480 + 11 x Pred4 at A = 806 (504,640) + 10 x
+# Dyn4 at A = 806 (679,424, its one-hot layers counted as the reference computes them) = 15,725,760 MAC per sample
+DOG_LEARNER_FLOP_PER_STEP = 3 * 2 * 15_725_760 * 128
 # Config (c): classic MADN 4p teams.  Algorithmic MAC per simulation (one branch evaluated):
 # decision = StochasticDynamics afterstate path + Pred4(A=4); chance = StochasticDynamics chance path + Pred4.
 CLASSIC_PLAYERS = 4
@@ -103,6 +106,10 @@ def parse():
                     help="dog: record every turn (muz_dog_random_play_record), pack the records each step and gather "
                          "them to rank 0 (RCCL point-to-point at N > 1) inside the timed region -- config (d) as "
                          "BASELINE.json names it")
+    ap.add_argument("--game", choices=("det", "dog"), default="det",
+                    help="train workload: det = train_with_reward.py (det-MADN 4p), dog = MuZero_DOG/train.py (the DOG "
+                         "slice's nets, A = 806, DogSelfPlay records) -- BASELINE configs[4]'s 'full MuZero_DOG train "
+                         "loop'")
     ap.add_argument("--policy", choices=("random", "muzero"), default="random",
                     help="dog: the reference's config (d) random legal policy, or the DOG MuZero slice (repr net with "
                          "its LayerNorm head + Dyn4 / Pred4 at A = 806 + Gumbel search, MuZero_DOG/train.py's S = 100, "
@@ -676,7 +683,7 @@ def run_classic(args):
 
 
 def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, games, stats, C, is_actor, is_learner,
-                      learner_rank, empty_packed):
+                      learner_rank, empty_packed, A=24):
     """--workload train --overlap: pipeline.OverlappedIterations with this process's roles.  1 GPU: self-play in
     a worker thread on its own stream while the learner's graph replays on another; N ranks: actors play while
     the learner trains, then gather_packed + an async weight broadcast.  Returns the timed region's seconds."""
@@ -713,7 +720,7 @@ def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, 
                 ring.save_games_from_buffers(got)
             return
         packed = got if is_actor else empty_packed(C, device)
-        recv = TR.gather_packed(packed, C, 24, dst=learner_rank)
+        recv = TR.gather_packed(packed, C, A, dst=learner_rank)
         if is_learner:
             with torch.cuda.stream(s_learn):
                 for r, p in enumerate(recv):
@@ -752,10 +759,24 @@ def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, 
     return timed_region(dist, timed, args.steps)
 
 
+class _DogActor:
+    """The DOG actor of the train workload: game_agent_dog.DogSelfPlay's recorded stream with SelfPlayEngine's
+    play_stream signature (the stream argument: the records are written on the current torch stream)."""
+
+    def __init__(self, net, games, T, S, D, device):
+        from exploring_muzero_on_dog_amd import game_agent_dog as GAD
+        self.sp = GAD.DogSelfPlay(net, games, S, D, 1.0, seed=0, device=device)
+        self.games, self.T = games, T
+
+    def play_stream(self, num_games, seed, temperature=1.0, stream=None):
+        return self.sp.play_stream(num_games, self.T, temperature=temperature, seed=seed)
+
+
 def run_train(args):
-    """Config (e): the det-MADN training loop (train_with_reward.py:167-311) at its hyper-parameters --
-    4 players, 1500 games per iteration (S=100, D=50, max_len 550), replay ring 20000 x 550, batch 128,
-    unroll 10, td 50, 2500 learner steps per iteration.  One bench step = one iteration.
+    """Config (e): the training loop at its reference hyper-parameters -- --game det: train_with_reward.py:167-311
+    (det-MADN 4 players); --game dog: MuZero_DOG/train.py:168-300 with its config 311-352 (4p DOG teams, the DOG slice's
+    nets at A = 806, its loss = train_with_reward.py's) -- 1500 games per iteration (S=100, D=50, max_len 550), replay
+    ring 20000 x 550, batch 128, unroll 10, td 50, 2500 learner steps per iteration.  One bench step = one iteration.
     1 GPU: actor and learner share it.  N GPUs: ranks 0..N-2 are actors (the games split between them,
     packed and gathered to the learner over RCCL point-to-point), rank N-1 is the learner, which
     broadcasts the new weights back (one collective) -- SURVEY §8(e)."""
@@ -768,20 +789,29 @@ def run_train(args):
     from exploring_muzero_on_dog_amd import nets as N
     from exploring_muzero_on_dog_amd import replay as R
     from exploring_muzero_on_dog_amd import transfer as TR
+    dog = args.game == "dog"
     P, GAMES, T, S, D = 4, 1500, 550, 100, 50
-    C = E.num_channels(P)
-    params = N.init_muzero_params(42, C)
-    net = N.DeviceNet(params, C, device=device)
     learner_rank = world - 1
     actors = max(world - 1, 1)
     is_actor = world == 1 or rank != learner_rank
     is_learner = world == 1 or rank == learner_rank
     games = (GAMES + actors - 1) // actors
-    eng = GA.SelfPlayEngine(net, games, num_players=P, max_steps=T, num_simulations=S, max_depth=D,
-                            device=device) if is_actor else None
-    ring = R.VectorizedReplayBuffer(20000, 128, 10, 50, obs_shape=(C, 56), max_episode_length=T, device=device,
-                                    rng=np.random.RandomState(rank)) if is_learner else None
-    learner = LR.Learner(params, C, unroll_steps=10, device=device, graph=True) if is_learner else None
+    if dog:
+        from exploring_muzero_on_dog_amd import muzero_dog as MD
+        C, A = MD.NUM_CHANNELS, MD.NUM_ACTIONS
+        params = MD.init_muzero_params(0)                       # MuZero_DOG/train.py:326 seed 0
+        net = MD.DeviceDogNet(params, device=device)
+        eng = _DogActor(net, games, T, S, D, device) if is_actor else None
+        learner = LR.DogLearner(params, unroll_steps=10, device=device, graph=True) if is_learner else None
+    else:
+        C, A = E.num_channels(P), 24
+        params = N.init_muzero_params(42, C)
+        net = N.DeviceNet(params, C, device=device)
+        eng = GA.SelfPlayEngine(net, games, num_players=P, max_steps=T, num_simulations=S, max_depth=D,
+                                device=device) if is_actor else None
+        learner = LR.Learner(params, C, unroll_steps=10, device=device, graph=True) if is_learner else None
+    ring = R.VectorizedReplayBuffer(20000, 128, 10, 50, obs_shape=(C, 56), action_dim=A, max_episode_length=T,
+                                    device=device, rng=np.random.RandomState(rank)) if is_learner else None
     stats = {"env_steps": 0, "train_steps": 0, "learner_ms": 0.0}
 
     def iteration(seed, train_steps):
@@ -792,7 +822,7 @@ def run_train(args):
             ring.save_games_from_buffers(buf)
         else:
             packed = TR.pack(buf) if is_actor else _empty_packed(C, device)
-            got = TR.gather_packed(packed, C, 24, dst=learner_rank)
+            got = TR.gather_packed(packed, C, A, dst=learner_rank)
             if is_learner:
                 for r, p in enumerate(got):
                     if r != learner_rank:
@@ -811,14 +841,14 @@ def run_train(args):
             TR.broadcast_weights(net, src=learner_rank)
 
     def _empty_packed(C, dev):
-        z = {name: torch.empty((0,) + shp, dtype=dt, device=dev) for name, dt, shp in TR.fields(C, 24, False)}
+        z = {name: torch.empty((0,) + shp, dtype=dt, device=dev) for name, dt, shp in TR.fields(C, A, False)}
         z["idx"] = torch.empty((0,), dtype=torch.int32, device=dev)
         z["row_offset"] = torch.empty((0,), dtype=torch.int64, device=dev)
         return z
 
     if args.overlap:
         elapsed = _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, games, stats, C,
-                                    is_actor, is_learner, learner_rank, _empty_packed)
+                                    is_actor, is_learner, learner_rank, _empty_packed, A)
     else:
         for w in range(max(args.warmup, 1)):       # fills the ring and captures the learner's HIP graph
             iteration(100 * w, 2)
@@ -831,29 +861,36 @@ def run_train(args):
         if dist is not None:
             dist.destroy_process_group()
         return
+    flop_step = DOG_LEARNER_FLOP_PER_STEP if dog else LEARNER_FLOP_PER_STEP
     out = {
-        "metric": "MuZero training iterations/sec, det-MADN 4p (config e: self-play + replay + learner)",
+        "metric": ("MuZero training iterations/sec, DOG 2v2 (config e as BASELINE names it: the MuZero_DOG train loop, "
+                   "self-play + replay + learner)" if dog else
+                   "MuZero training iterations/sec, det-MADN 4p (config e: self-play + replay + learner)"),
         "value": round(args.steps / elapsed, 5), "unit": "iterations/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 1), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (self-generated games, seeded random fp32 weights)",
-        "config": {"workload": f"train_with_reward.py config: {GAMES} games/iter (S={S}, D={D}, max_len {T}), "
+        "config": {"workload": (f"MuZero_DOG/train.py config: 4p DOG teams, the DOG slice's nets (A = 806), "
+                                if dog else "train_with_reward.py config: ") +
+                               f"{GAMES} games/iter (S={S}, D={D}, max_len {T}), "
                                f"ring 20000, batch 128, unroll 10, td 50, {args.train_steps} learner steps/iter",
+                   "game": args.game,
                    "parallelism": ("1 GPU (actor + learner)" if world == 1 else
                                    f"{world - 1} actor ranks + 1 learner rank (packed-trajectory gather, weight "
                                    f"broadcast)"),
                    "schedule": ("overlapped: iteration i+1's self-play runs while iteration i trains; games played "
                                 "with weights one iteration staler than the reference's sequential loop"
-                                if args.overlap else "sequential, as train_with_reward.py:244-292")},
+                                if args.overlap else "sequential, as " +
+                                ("MuZero_DOG/train.py:243-276" if dog else "train_with_reward.py:244-292"))},
         "env_steps_per_s": round(env_steps / elapsed, 1), "train_steps_per_s": round(train_steps / elapsed, 2),
     }
     if train_steps:
         step_ms = learner_ms / train_steps
-        achieved = LEARNER_FLOP_PER_STEP / (step_ms * 1e-3) / 1e12
+        achieved = flop_step / (step_ms * 1e-3) / 1e12
         out["roofline"] = {"bound": "mfma", "kernel": "learner train_step (forward + backward + AdamW, one HIP graph)",
                            "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                            "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 5), "avg_step_ms": round(step_ms, 3),
-                           "flop_per_step": LEARNER_FLOP_PER_STEP,
+                           "flop_per_step": flop_step,
                            "note": "batch 128 x unroll 10 of 256-wide fp32 layers: hundreds of small GEMMs and "
                                    "LayerNorms per step, latency-bound, not MFMA-bound", "traffic": None}
     print(json.dumps(out), flush=True)

@@ -25,7 +25,8 @@ __device__ __forceinline__ float wave_sum_f(float v) {
   return v;
 }
 
-constexpr int kLossMaxA = 32;     // policy width
+constexpr int kLossMaxA = 32;     // policy width of the per-thread rows (det 24, classic 4)
+constexpr int kLossMaxWideA = 1024;   // wider policies (DOG 806): one wave per row
 constexpr int kLossMaxCls = 8;    // classes of a CE term
 
 // rare predicate of term t for (sample b, step k)
@@ -77,6 +78,49 @@ __device__ __forceinline__ float loss_ce_row(const float* __restrict__ l, float*
 #pragma unroll
   for (int a = 0; a < NMAX; ++a)
     if (a < n) dl[a] = coef * (expf(x[a] - lse) * st - t[a]);
+  return ce;
+}
+
+// loss_ce_row for a row of n <= kLossMaxWideA logits held by one wave (lane a, a + 64, ...); returns the row's
+// cross-entropy in every lane (wave sums in a fixed butterfly order)
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ __forceinline__ float loss_ce_row_wide(const float* __restrict__ l, float* __restrict__ dl, int n,
+                                                  const float* __restrict__ tgt, float coef, int lane) {
+  constexpr int J = kLossMaxWideA / 64;
+  float x[J], t[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int a = lane + 64 * j;
+    x[j] = a < n ? l[a] : -INFINITY;
+    t[j] = a < n ? tgt[a] : 0.f;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < J; ++j) mx = fmaxf(mx, x[j]);
+  mx = wave_max_f(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) s += lane + 64 * j < n ? expf(x[j] - mx) : 0.f;
+  s = wave_sum_f(s);
+  const float lse = mx + logf(s);
+  float ce = 0.f, st = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    if (lane + 64 * j < n) {
+      ce -= t[j] * (x[j] - lse);
+      st += t[j];
+    }
+  }
+  ce = wave_sum_f(ce);
+  st = wave_sum_f(st);
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+    if (lane + 64 * j < n) dl[lane + 64 * j] = coef * (expf(x[j] - lse) * st - t[j]);
   return ce;
 }
 
@@ -137,8 +181,9 @@ __global__ __launch_bounds__(kLossThreads) void k_loss_heads(muz_loss_args g) {
     const float d = val - tv;
     v[0] = m * d * d;
     g.dvalue[row] = g.scale_value * invB * m * 2.0f * d;
-    v[1] = m * loss_ce_row<kLossMaxA>(g.logits + row * g.A, g.dlogits + row * g.A, g.A, -1,
-                                      g.policies + ((size_t)b * g.T + k) * g.A, g.scale_policy * invB * m);
+    if (g.A <= kLossMaxA)
+      v[1] = m * loss_ce_row<kLossMaxA>(g.logits + row * g.A, g.dlogits + row * g.A, g.A, -1,
+                                        g.policies + ((size_t)b * g.T + k) * g.A, g.scale_policy * invB * m);
     if (k < K) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
@@ -153,6 +198,18 @@ __global__ __launch_bounds__(kLossThreads) void k_loss_heads(muz_loss_args g) {
                                                  tg, t.scale * w);
       }
     }
+  }
+  if (g.A > kLossMaxA) {   // the policy cross-entropy of wide rows: one wave per row, the wave's rows summed in order
+    const int lane = tid & 63, wv = tid >> 6;
+    float acc = 0.f;
+    for (int b = wv; b < B; b += kLossWaves) {
+      const size_t row = (size_t)k * B + b;
+      const float m = g.masks[(size_t)b * g.T + k];
+      const float ce = m * loss_ce_row_wide(g.logits + row * g.A, g.dlogits + row * g.A, g.A,
+                                            g.policies + ((size_t)b * g.T + k) * g.A, g.scale_policy * invB * m, lane);
+      acc += ce;
+    }
+    v[1] = lane == 0 ? acc : 0.f;
   }
   block_sum<5>(v, red5);
   // phase 3: this step's sums; the last workgroup adds all steps in order
@@ -195,7 +252,7 @@ extern "C" int muz_loss_heads(const muz_loss_args* args, void* stream) {
   const muz_loss_args& a = *args;
   MUZ_HOST_CHECK(a.K >= 0 && a.B > 0 && a.A > 0 && a.T >= a.K + 1 && a.nterms >= 0 && a.nterms <= 3);
   MUZ_HOST_CHECK(a.masks && a.target_values && a.policies && a.value && a.logits && a.dvalue && a.dlogits && a.parts && a.total);
-  if (a.K > kLossMaxK || a.A > kLossMaxA) return MUZ_E_UNSUPPORTED;
+  if (a.K > kLossMaxK || a.A > kLossMaxWideA) return MUZ_E_UNSUPPORTED;
   MUZ_HOST_CHECK(a.partials && a.ticket);
   for (int j = 0; j < a.nterms; ++j) {
     const muz_loss_term& t = a.term[j];

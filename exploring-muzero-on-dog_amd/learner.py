@@ -1029,6 +1029,16 @@ class MuZeroNets:
 
     # ---- networks ------------------------------------------------------------------------------------
     def representation(self, obs):
+        """RepresentationNetwork2: the trunk, then Dense_4 and the min-max scaling (muzero_deterministic_madn.py:
+        139-140)."""
+        r = "representation"
+        h = self.representation_trunk(obs)
+        if h.is_cuda and h.shape[-1] == 256 and self.p[f"{r}/Dense_4/kernel"].shape[1] == 256:
+            return _DenseMinmax.apply(h.contiguous(), self.p[f"{r}/Dense_4/kernel"], self.p[f"{r}/Dense_4/bias"])
+        return self._minmax(self._dense(f"{r}/Dense_4", h))
+
+    def representation_trunk(self, obs):
+        """RepresentationNetwork2 up to its last Dense: convolutions, global features, Dense_3 and 6 ResBlocks."""
         r = "representation"
         sp = obs[:, :6, :].transpose(1, 2)
         g = obs[:, 6:, 0]
@@ -1039,10 +1049,7 @@ class MuZeroNets:
         g = self._dense_ln(f"{r}/Dense_1", f"{r}/LayerNorm_4", g)
         g = self._dense_ln(f"{r}/Dense_2", f"{r}/LayerNorm_5", g)
         h = self._dense_ln(f"{r}/Dense_3", f"{r}/LayerNorm_6", torch.cat([flat, g], -1))
-        h = self._rbs(f"{r}/ResBlock_", 6, h)
-        if h.is_cuda and h.shape[-1] == 256 and self.p[f"{r}/Dense_4/kernel"].shape[1] == 256:
-            return _DenseMinmax.apply(h.contiguous(), self.p[f"{r}/Dense_4/kernel"], self.p[f"{r}/Dense_4/bias"])
-        return self._minmax(self._dense(f"{r}/Dense_4", h))
+        return self._rbs(f"{r}/ResBlock_", 6, h)
 
     def dynamics_film(self, action):
         """The action-only FiLM sub-graph of DynamicsNetwork4 (one_hot -> Dense_0 -> Dense_1 | Dense_2); it
@@ -1616,6 +1623,44 @@ class StochasticLearner(Learner):
     def _device_net(self, net):
         from .stochastic import DeviceClassicNet
         return DeviceClassicNet(self.nets.numpy(), net.C, device=net.buffer.device)
+
+
+# ---- DOG: MuZero_DOG/train.py (its loss_fn / train_step, 24-164, are train_with_reward.py's) ------------------------
+class DogMuZeroNets(MuZeroNets):
+    """The DOG MuZero slice's networks (muzero_dog.py): MuZero_DOG/muzero_dog.py:25-83's RepresentationNetwork (the det
+    trunk with LayerNorm_7 after its last Dense instead of the min-max scaling, lines 80-81) and DynamicsNetwork4 /
+    PredictionNetwork4 at A = 806 (the slice's definition; muzero_dog.py:85-99 are `pass`), on 34 x 56 observations.
+    The 806-wide one-hot inputs (Dynamics Dense_0, Dense_6 / Dense_7's action rows) stay matrix products, as the
+    reference computes them (66 MFLOP per step at batch 128 x 10, against ~10 GFLOP for the whole step)."""
+
+    def __init__(self, params: dict, device="cuda", dtype=torch.float32):
+        from . import muzero_dog as MD
+        super().__init__(params, MD.NUM_CHANNELS, MD.NUM_ACTIONS, device, dtype, shapes=MD.param_shapes())
+
+    def representation(self, obs):
+        r = "representation"
+        return self._dense_ln(f"{r}/Dense_4", f"{r}/LayerNorm_7", self.representation_trunk(obs), LN_PLAIN)
+
+
+class DogLearner(Learner):
+    """train_step of MuZero_DOG/train.py:148-164 (= train_with_reward.py's: clip 5.0 -> adamw, lr 0.005 x0.2 @ it 30,
+    x0.2 @ 60, x0.5 @ 85 of 2500 steps, wd 1e-4; train.py:355-373) on the DOG nets, batches from a device ring at
+    action_dim 806, obs (34, 56)."""
+
+    def __init__(self, params: dict, unroll_steps: int = 10, device="cuda", graph: bool = False, **opt):
+        prefer_rocblas()
+        self.nets = DogMuZeroNets(params, device)
+        self.opt = AdamW(self.nets.parameters(), **opt)
+        self.unroll_steps = int(unroll_steps)
+        self.graph = bool(graph)
+        self._g = None
+        self.sink = GradSink() if GROUPED_GRADS and torch.device(device).type == "cuda" else None
+        self.wt = WeightTranspose(self.nets.p) if FUSED_DENSE and FUSED_FWD and torch.device(device).type == "cuda" \
+            else None
+
+    def _device_net(self, net):
+        from .muzero_dog import DeviceDogNet
+        return DeviceDogNet(self.nets.numpy(), device=net.buffer.device)
 
 
 def train_loop(learner: Learner, engine, ring, iterations: int, train_steps: int, games_per_iteration: int,

@@ -91,12 +91,25 @@ class DeviceDogNet(N._Packer):
             _L.check(_L.load().muz_dog_net_prepare(ctypes.byref(self.w), _L.stream_ptr()), "muz_dog_net_prepare")
 
 
+_NET_CACHE = []
+
+
 def as_device_net(params, device="cuda") -> DeviceDogNet:
-    """A flat ``net/Layer/param`` dict (or a DeviceDogNet) -> DeviceDogNet."""
+    """A flat ``net/Layer/param`` dict or a Flax tree (or a DeviceDogNet) -> DeviceDogNet.  New weights go into the
+    DeviceDogNet of the previous call in place (same arena layout), so an engine cached on it (game_agent_dog.
+    play_n_games_v3) keeps its buffers -- the reference's train loop passes a fresh params tree every iteration."""
     if isinstance(params, DeviceDogNet):
         return params
     flat = params if all(isinstance(k, str) and "/" in k for k in params) else _flat(params)
-    return DeviceDogNet({k: np.asarray(v, np.float32) for k, v in flat.items()}, device=device)
+    flat = {k: np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v, np.float32) for k, v in flat.items()}
+    net = DeviceDogNet(flat, device=device)
+    prev = _NET_CACHE[0] if _NET_CACHE else None
+    if prev is not None and prev.buffer.shape == net.buffer.shape and prev.buffer.device == net.buffer.device:
+        prev.buffer.copy_(net.buffer)
+        prev.prepare()
+        return prev
+    _NET_CACHE[:] = [net]
+    return net
 
 
 def _flat(tree) -> dict:

@@ -777,7 +777,8 @@ typedef struct {
   float w_rare, w_common, scale;
 } muz_loss_term;
 typedef struct {
-  int32_t K, B, A, T;      /* unroll steps, batch, policy width, time stride of masks / target_values / policies */
+  int32_t K, B, A, T;      /* unroll steps (<= 64), batch, policy width (<= 1024: <= 32 a thread per row, wider a
+                              wave per row -- the DOG learner's 806), time stride of masks / target_values / policies */
   int32_t nterms, norm;    /* CE terms (<= 3), n_common form */
   const float* masks;      /* [B][T] */
   const float* target_values;

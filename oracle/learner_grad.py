@@ -89,6 +89,8 @@ class _Net:
         h = self.relu(self.ln(f"{r}/LayerNorm_6", self.dense(f"{r}/Dense_3", torch.cat([flat, g], -1))))
         for b in range(6):
             h = self.resblock(f"{r}/ResBlock_{b}", h)
+        if f"{r}/LayerNorm_7/scale" in self.p:     # the DOG RepresentationNetwork (MuZero_DOG/muzero_dog.py:80-81)
+            return self.ln(f"{r}/LayerNorm_7", self.dense(f"{r}/Dense_4", h))
         return self._mm(self.dense(f"{r}/Dense_4", h))
 
     # PredictionNetwork4 (muzero_deterministic_madn.py:549-583; classic 192-226)
@@ -104,8 +106,9 @@ class _Net:
         return self.dense(f"{p}/Dense_2", pol), torch.tanh(self.dense(f"{p}/Dense_5", v))
 
     # DynamicsNetwork4 (muzero_deterministic_madn.py:391-457)
-    def dynamics(self, latent, action, A=24):
+    def dynamics(self, latent, action, A=None):
         d = "dynamics"
+        A = self.p[f"{d}/Dense_0/kernel"].shape[0] if A is None else A     # 24 det, 806 DOG
         oh = self.one_hot(action, A)
         e = self.relu(self.dense(f"{d}/Dense_0", oh))
         x = self.ln(f"{d}/LayerNorm_0", latent) * (1.0 + self.dense(f"{d}/Dense_1", e)) + self.dense(f"{d}/Dense_2", e)

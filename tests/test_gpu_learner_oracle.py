@@ -167,6 +167,33 @@ def _classic_setup():
     return params, ring.sample_batch(), lambda graph=False: L.StochasticLearner(params, C, unroll_steps=10, graph=graph)
 
 
+def _dog_setup():
+    """config (e) as MuZero_DOG/train.py:325-352 trains: 4p DOG, the DOG slice's nets, a ring at action_dim 806 / obs
+    (34, 56) filled by DogSelfPlay's recorded stream (64 lanes, 96 games cut at 200 records, S 4 / D 3 -- the shape of
+    the batch is the reference's: 128 x unroll 10, td 50)."""
+    from exploring_muzero_on_dog_amd import game_agent_dog as GA
+    from exploring_muzero_on_dog_amd import learner as L
+    from exploring_muzero_on_dog_amd import muzero_dog as MD
+    from exploring_muzero_on_dog_amd import replay as R
+    from oracle import dog_muzero as DM
+    T = 200
+    params = DM.init_params(seed=35, randomize_affine=True)
+    sp = GA.DogSelfPlay(MD.DeviceDogNet(params), 64, 4, 3, 1.0, seed=7)
+    ring = R.VectorizedReplayBuffer(2000, 128, 10, 50, obs_shape=(MD.NUM_CHANNELS, 56), action_dim=MD.NUM_ACTIONS,
+                                    max_episode_length=T, rng=np.random.RandomState(9))
+    ring.save_games_from_buffers(sp.play_stream(96, T, seed=11))
+    return params, ring.sample_batch(), lambda graph=False: L.DogLearner(params, unroll_steps=10, graph=graph)
+
+
+def test_dog_learner_step_matches_oracle(cuda):
+    """MuZero_DOG/train.py:24-164 (train_with_reward.py's loss on the DOG nets: LayerNorm-headed representation, Dyn4 /
+    Pred4 at A = 806, the 806-wide policy cross-entropy in the fused loss kernel's wide-row path)."""
+    params, batch, make = _dog_setup()
+    assert batch["policies"].shape[-1] == 806 and batch["observations"].shape[1:] == (34, 56)
+    _check("DOG learner (MuZero_DOG/train.py: 4p teams, batch 128, unroll 10, td 50, A 806)", make, params, batch,
+           classic=False)
+
+
 def test_det_learner_step_matches_oracle_config_e(cuda):
     params, batch, make = _det_setup()
     _check("det learner (config e: 4p, batch 128, unroll 10, td 50)", make, params, batch, classic=False)

@@ -125,3 +125,28 @@ def test_classic_test_training_tiny(cuda, tmp_path):
         te = opt_state.learner.nets.representation(obs)
         tl, tv = opt_state.learner.nets.prediction(te)
     assert max((e - te).abs().max().item(), (lg - tl).abs().max().item()) < 2e-5
+
+
+def test_dog_test_training_tiny(cuda, tmp_path):
+    """MuZero_DOG/train.py's test_training (train_dog.py) with a tiny config: DOG games recorded by
+    game_agent_dog.play_n_games_v3 into a ring at action_dim 806, DogLearner steps, the bootstrap switch, checkpoints;
+    the learner's weights reach the self-play arena (the root inference equals the torch forward)."""
+    from exploring_muzero_on_dog_amd import muzero_dog as MD
+    from exploring_muzero_on_dog_amd import train_dog as TD
+    from exploring_muzero_on_dog_amd import training as T
+    cfg = _tiny(TD.config, tmp_path)
+    lines = []
+    params, opt_state, times = TD.test_training(cfg, log=lines.append)
+    assert len(times) == 2 and sum("SWITCHING TO BOOTSTRAP" in s for s in lines) == 1
+    replay = T.run_training.last["replay"]
+    assert replay.action_dim == 806 and replay.size == 3 * 24
+    assert opt_state.count == 2 * 3 and all(np.isfinite(list(h.values())).all() for h in T.run_training.last["history"])
+    net = MD.as_device_net(params)
+    obs = replay.observations[:16, 3].float()
+    lg, v, e = MD.root_inference_fn(net, obs)
+    with torch.no_grad():
+        te = opt_state.learner.nets.representation(obs)
+        tl, tv = opt_state.learner.nets.prediction(te)
+    assert max((e - te).abs().max().item(), (lg - tl).abs().max().item(), (v - tv[:, 0]).abs().max().item()) < 2e-5
+    p2, o2 = T.load_checkpoint(*TD._checkpoint_names(cfg, 2), TD.optimizer)
+    assert o2.count == opt_state.count
