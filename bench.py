@@ -470,6 +470,7 @@ def run_dog_muzero(args):
     sp.play(1)                           # warmup turn (workspace, first launches)
     for _ in range(args.warmup):
         step(-1)
+    games0 = int(sp.episodes.sum().item())     # games finished before the timed region
     clib.muz_dog_gumbel_search = timed_search
     try:
         elapsed = timed_region(dist, step, args.steps)
@@ -478,7 +479,7 @@ def run_dog_muzero(args):
     search_ms = sum(a.elapsed_time(b) for a, b in ev)
     turns = args.steps * K
     (steps_done, sms, games), elapsed = sum_max(dist, device, [args.batch * turns, search_ms,
-                                                             int(sp.episodes.sum().item())], elapsed)
+                                                             int(sp.episodes.sum().item()) - games0], elapsed)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()

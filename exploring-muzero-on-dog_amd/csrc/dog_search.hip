@@ -40,8 +40,8 @@ struct WTree {
   float* gum;         // [n][832] the root's Gumbel noise + (prior - max prior), drawn once per search
   f32x4* vrec;        // [n][N][32][2] each node's visited children in first-visit order (s_vcnt: how many; -1
                       // overflow), one 32-byte record each: {child, visits, prior, value} {reward, discount, node, -}
-  float* topp;        // [n][N][8] each node's 8 largest prior logits (value desc, index asc) ...
-  int32_t* topi;      // [n][N][8] ... and their children
+  float* topp;        // [n][N][kWTop] each node's kWTop largest prior logits (value desc, index asc) ...
+  int32_t* topi;      // [n][N][kWTop] ... and their children
   int N;
   __device__ __forceinline__ size_t ca(int g, int node, int a) const { return ((size_t)g * N + node) * kWPad + a; }
   __device__ __forceinline__ AS1 float* e(int g, int node) const { return gpw(emb) + ((size_t)g * N + node) * LAT; }
@@ -57,9 +57,21 @@ struct WTree {
   __device__ __forceinline__ AS1 int32_t* ti(int g, int node) const;
 };
 constexpr int kWList = 32;   // visited children a node's list holds
-constexpr int kWTop = 8;     // largest priors a node keeps
+#ifndef MUZ_DOG_WTOP
+#define MUZ_DOG_WTOP 8       // (a build switch for the A/B of the top-prior list's length)
+#endif
+constexpr int kWTop = MUZ_DOG_WTOP;   // largest priors a node keeps
+// The per-node sizes of the compact-load arrays: the accessors below, carve_wide and dog_search_workspace_bytes all
+// derive their strides from these (round 4's kWTop = 4 fault: an accessor kept a literal 8 the carve did not)
+constexpr int kWRecF4 = 2 * kWList;                        // f32x4 per node's visited list (two per record)
+constexpr size_t kWRecBytes = sizeof(f32x4) * kWRecF4;     // = kWList 32-byte records
+constexpr size_t kWTopBytes = sizeof(float) * kWTop;       // topp; topi the same in int32
+static_assert(kWRecBytes == (size_t)kWList * 32, "a visited-child record is 32 bytes");
+static_assert(sizeof(int32_t) == sizeof(float), "topi and topp share the stride");
+static_assert(kWList <= kRowLanes && kWList < 127, "one record per lane (wrec_load), lengths in signed char");
+static_assert(kWTop >= 2 && kWTop < kRowLanes, "top list: one entry per lane, a 32-bit ballot mask (wnode_compact)");
 __device__ __forceinline__ AS1 f32x4* WTree::vr(int g, int node) const {
-  return gpw(vrec) + ((size_t)g * N + node) * (2 * kWList);
+  return gpw(vrec) + ((size_t)g * N + node) * kWRecF4;
 }
 __device__ __forceinline__ AS1 float* WTree::tp(int g, int node) const {
   return gpw(topp) + ((size_t)g * N + node) * kWTop;
@@ -85,9 +97,9 @@ static WTree carve_wide(void* ws, int n, int N) {
   t.gum = (float*)p;
   p += (size_t)n * kWPad * 4;
   t.vrec = (f32x4*)p;
-  p += (size_t)n * N * kWList * 32;
+  p += (size_t)n * N * kWRecBytes;
   t.topp = (float*)p;
-  p += (size_t)n * N * kWTop * 4;
+  p += (size_t)n * N * kWTopBytes;
   t.topi = (int32_t*)p;
   t.N = N;
   return t;
@@ -916,7 +928,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
 int64_t dog_search_workspace_bytes(int n, int S) {
   const int N = S + 1;
   return (int64_t)wide_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4 + (int64_t)n * kWPad * 4 +
-         (int64_t)n * N * (kWList * 32 + 2 * kWTop * 4);
+         (int64_t)n * N * (int64_t)(kWRecBytes + 2 * kWTopBytes);
 }
 
 int launch_dog_search(const muz_dog_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,

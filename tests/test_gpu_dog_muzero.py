@@ -231,3 +231,29 @@ def test_dog_muzero_selfplay_followed_by_oracle(cuda, rows, monkeypatch):
         bad = diff(D.to_host(sp.env), envs)
         assert bad is None, (t, bad)
     assert searched > B * T // 2
+
+
+def test_dog_certified_select_equals_exact_at_bench_shape(cuda, monkeypatch):
+    """the certified interior argmax (wselect_certified) at the benched shape -- 1500 games, S = 100, D = 50,
+    seeded random weights, roots from 8 self-play turns -- against the exact 806-exponential selection
+    (MUZ_DOG_EXACT_SELECT=1) on the same roots: actions, weights and root values bit-identical (about 10^6 interior
+    selections, no oracle involved)."""
+    from exploring_muzero_on_dog_amd import dog as D
+    from exploring_muzero_on_dog_amd import game_agent_dog as GA
+    MD = _MD()
+    net = MD.DeviceDogNet(MD.init_muzero_params(2))
+    B, S, Dd = 1500, 100, 50
+    sp = GA.DogSelfPlay(net, B, S, Dd, 1.0, seed=4)
+    sp.play(8)
+    words = D.legal_mask(sp.env)
+    obs = MD.encode_board(sp.env)
+    lg, v, e = MD.root_inference_fn(net, obs)
+    out = {}
+    for exact in ("0", "1"):
+        monkeypatch.setenv("MUZ_DOG_EXACT_SELECT", exact)
+        pol, rv = MD.gumbel_muzero_policy(net, lg, v, e, words, S, Dd, 1.0, seed=4, turn=8)
+        torch.cuda.synchronize()
+        out[exact] = (pol.action.clone(), pol.action_weights.clone(), rv.clone())
+    (a0, w0, v0), (a1, w1, v1) = out["0"], out["1"]
+    assert int((a0 >= 0).sum()) > B // 2
+    assert torch.equal(a0, a1) and torch.equal(w0, w1) and torch.equal(v0, v1)
