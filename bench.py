@@ -225,47 +225,63 @@ def cpu_baseline(seconds, sims, depth, max_steps, lanes=16):
                       f"({allc['env_steps']} env-steps); affinity shows {aff} CPUs"}
 
 
-def measured_traffic():
-    """HBM bytes per k_gumbel_search launch from the newest committed PMC summary (profiles/*_traffic.json,
-    written by profiles/summarize_profile.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
-    if not files:
+# The committed measurement summaries the bench lines quote, named explicitly (not picked by filename order): each is
+# re-taken on the round's kernel by profiles/r5i_measure.sh and checked for the kernel it describes.
+MEASURED = {
+    "traffic": "profiles/r5i_traffic.json",           # HBM bytes per k_gumbel_search launch (FETCH_SIZE x2 + WRITE_SIZE)
+    "pmc": "profiles/r5i_pmc.json",                   # TCP_TCC_READ_REQ, SQ_VALU_MFMA_BUSY_CYCLES, ... (k_gumbel_search)
+    "loop": "profiles/r5i_loop_bench.log",            # the weight-stream MFMA loop alone (profiles/loop_bench.hip)
+    "dog_traffic": "profiles/r5i_dog_traffic.json",   # HBM bytes per k_dog_search launch
+}
+
+
+def _measured_json(key, kernel):
+    path = os.path.join(ROOT, MEASURED[key])
+    if not os.path.exists(path):
         return None, None
-    t = json.load(open(files[-1]))
-    return t.get("bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+    t = json.load(open(path))
+    if t.get("kernel") != kernel:
+        return None, None
+    return t, MEASURED[key]
+
+
+def measured_traffic(key="traffic", kernel="k_gumbel_search"):
+    """HBM bytes per launch of `kernel` from its committed PMC summary (profiles/summarize_profile.py from
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench): (bytes, source) or (None, None)."""
+    t, src = _measured_json(key, kernel)
+    return (t.get("bytes_per_launch"), src) if t else (None, None)
 
 
 L2_SERVED_TBS = 18.8   # MI355X_MICROARCH.md, rows shared by every workgroup, served by the XCD's L2 (16.8-18.8)
 
 
 def measured_l2_reads():
-    """L1 -> L2 read bytes per k_gumbel_search launch from the newest committed PMC summary that has
-    TCP_TCC_READ_REQ_sum (128-byte requests): the per-simulation weight stream (3.6 MB per 16-game tile)
-    plus the tree reads.  Returns (bytes, source) or (None, None)."""
-    import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
-        per = json.load(open(f)).get("per_launch_mean", {})
-        if "TCP_TCC_READ_REQ_sum" in per:
-            return per["TCP_TCC_READ_REQ_sum"] * 128, os.path.relpath(f, ROOT)
-    return None, None
+    """L1 -> L2 read bytes per k_gumbel_search launch (TCP_TCC_READ_REQ_sum, 128-byte requests) and the MFMA-busy
+    fraction (SQ_VALU_MFMA_BUSY_CYCLES) from the round's PMC summary: (bytes, mfma_busy_frac, source)."""
+    t, src = _measured_json("pmc", "k_gumbel_search")
+    if not t:
+        return None, None, None
+    per = t.get("per_launch_mean", {})
+    l2 = per["TCP_TCC_READ_REQ_sum"] * 128 if "TCP_TCC_READ_REQ_sum" in per else None
+    return l2, t.get("mfma_busy_frac"), src
 
 
 def measured_loop_ceiling():
     """The search kernel's weight-stream MFMA loop alone (profiles/loop_bench.hip: 14 resident 256x256 fp32
-    layers on a 16-row LDS tile, a barrier per layer, every CU busy) from the newest committed loop-bench
-    log: its TFLOP/s / the fp32 MFMA peak is the fraction the kernel could reach if its serial phases (tree
-    walk, LayerNorm passes, epilogues, heads, backup) cost nothing.  Returns a dict or None."""
-    import glob
+    layers on a 16-row LDS tile, a barrier per layer, every CU busy) from the round's loop-bench log: its TFLOP/s /
+    the fp32 MFMA peak is the fraction the kernel could reach if its serial phases (tree walk, LayerNorm passes,
+    epilogues, heads, backup) cost nothing.  Returns a dict or None."""
     import re
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_loop_bench.log")), reverse=True):
-        for line in open(f):
-            m = re.match(r"grid 256 lb_base: .*MFMA busy ([0-9.]+) of SIMD cycles, clock ([0-9.]+) GHz, ([0-9.]+) TFLOP/s",
-                         line)
-            if m:
-                busy, clk, tf = (float(x) for x in m.groups())
-                return {"frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4), "tflops": tf, "mfma_busy": busy, "clock_GHz": clk,
-                        "source": os.path.relpath(f, ROOT)}
+    path = os.path.join(ROOT, MEASURED["loop"])
+    if not os.path.exists(path):
+        return None
+    for line in open(path):
+        m = re.match(r"grid 256 lb_base: .*MFMA busy ([0-9.]+) of SIMD cycles, clock ([0-9.]+) GHz, ([0-9.]+) TFLOP/s",
+                     line)
+        if m:
+            busy, clk, tf = (float(x) for x in m.groups())
+            return {"frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4), "tflops": tf, "mfma_busy": busy, "clock_GHz": clk,
+                    "source": MEASURED["loop"]}
     return None
 
 
@@ -1126,7 +1142,7 @@ def run_det(args):
                      "executed_frac": round(achieved * EXEC_FLOP_PER_SIM / FLOP_PER_SIM / PEAK_FP32_MFMA_TFLOPS, 4),
                      "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src},
     }
-    l2, l2_src = measured_l2_reads()
+    l2, mfma_busy, l2_src = measured_l2_reads()
     if l2 and launches:
         avg_s = search_ms / launches * 1e-3
         # second ceiling: the weights stream from L2 every simulation (a 16-row tile reuses each weight byte
@@ -1136,6 +1152,9 @@ def run_det(args):
                                         "mfma_frac_at_l2_ceiling": round(achieved / PEAK_FP32_MFMA_TFLOPS * avg_s /
                                                                          (l2 / (L2_SERVED_TBS * 1e12)), 4),
                                         "source": l2_src}
+    if mfma_busy is not None:
+        out["roofline"]["mfma_busy_frac"] = {"value": round(mfma_busy, 4), "counter": "SQ_VALU_MFMA_BUSY_CYCLES / "
+                                             "(GRBM_GUI_ACTIVE / 8 x 256 CUs x 4 SIMDs)", "source": l2_src}
     loop = measured_loop_ceiling()
     if loop:
         out["roofline"]["loop_ceiling"] = dict(loop, frac_of_ceiling=round(achieved / PEAK_FP32_MFMA_TFLOPS / loop["frac"], 4))
