@@ -409,47 +409,30 @@ def dog_latency_model(avg_ms, games, turns, launch_bytes):
                     "and the turn's serial part at raised wave priority, profiles/r3_dog_prio_ab.log"}
 
 
-def dog_muzero_cpu_baseline(seconds, sims, depth, games=8, temperature=1.0, seed=5):
-    """A CPU timing for the DOG MuZero line: the NumPy restatement of the slice (oracle/dog_muzero.py networks,
-    oracle/mctx_gumbel.py search at A = 806, oracle/dog.py transitions with the engine's deal keys) plays `games`
-    4p games turn by turn on the host for about `seconds` (the turn in flight finishes).  Pure NumPy, so its matrix
-    products may use the BLAS thread pool; the search's tree arithmetic is single-threaded."""
-    import numpy as np
+def dog_muzero_cpu_baseline(seconds, sims, depth, lanes=4, temperature=1.0, seed=5):
+    """SURVEY §8(d)'s CPU timing for the DOG MuZero line: the C++ restatement of the slice (oracle/cpu_dog.cpp: the
+    34-channel encoding, the DOG RepresentationNetwork + Dyn4 / Pred4 at A = 806 in fp32 AVX2/FMA, mctx's Gumbel
+    search with lane-order sums (oracle/cpu_search.hpp), dog.py transitions with the engine's deal keys, finished
+    games restarted; checked against the NumPy oracle -- networks at 1e-5, the search bit for bit, the self-play turn
+    action for action -- by tests/test_cpu_baseline_dog.py) plays `lanes` games per thread on the host for `seconds`,
+    at 1 thread and at all cores.  Same parameter init as the device line (init seed 2)."""
+    from oracle import cpu_selfplay as CS
     from oracle import dog as dg
     from oracle import dog_muzero as DM
-    from oracle import mctx_gumbel as G
-    from oracle import selfplay as OS
-    params = DM.init_params(seed=seed)
-    kw = dict(dg.SELFPLAY_RULES)
-    keys = [dg.engine_shuffle_keys(seed, g) for g in range(games)]
-    envs = [dg.env_reset(num_players=4, shuffle_keys=keys[g], **kw) for g in range(games)]
-
-    def rec(p, action, emb):
-        return DM.recurrent_inference(p, np.asarray(action), np.asarray(emb))
-
-    steps = turns = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        valid = np.stack([dg.valid_actions(e) for e in envs]).astype(bool)
-        has = np.flatnonzero(valid.any(1))
-        act = np.full(games, -1)
-        if has.size:
-            obs = np.stack([DM.encode_board(envs[g]) for g in has]).astype(np.float32)
-            lg, v, e = DM.root_inference(params, obs)
-            gum = np.stack([OS.gumbel_noise(seed, int(g), turns, A=806, scale=temperature) for g in has])
-            a, _, _, _ = G.gumbel_muzero_policy(params, lg, v, e, rec, sims, ~valid[has], gum.astype(np.float32),
-                                                max_depth=depth)
-            act[has] = a
-        for g in range(games):
-            e1 = (dg.no_step(envs[g], keys[g]) if act[g] < 0 else dg.env_step(envs[g], int(act[g]), keys[g]))[0]
-            envs[g] = dg.env_reset(num_players=4, shuffle_keys=keys[g], **kw) if e1.done else e1
-        steps += games
-        turns += 1
-    el = time.perf_counter() - t0
-    return {"value": round(steps / el, 2), "unit": "env_steps/s", "cores": 1, "kind": "port",
-            "sample": f"NumPy restatement of the DOG MuZero slice (oracle/dog_muzero.py + oracle/mctx_gumbel.py + "
-                      f"oracle/dog.py), {games} games x {turns} turns at S={sims} D={depth} in {el:.1f} s (one "
-                      f"Python thread; NumPy's BLAS pool for the matrix products)"}
+    net = CS.CpuNet(DM.init_params(seed=2), DM.NUM_CHANNELS)
+    cores, aff = cpu_cores()
+    half = seconds / 2
+    one = net.dog_bench(dg.SELFPLAY_RULES, lanes, sims, depth, temperature, seed, 1, half)
+    allc = net.dog_bench(dg.SELFPLAY_RULES, lanes, sims, depth, temperature, seed, cores, half)
+    v1 = one["env_steps"] / one["elapsed"]
+    vn = allc["env_steps"] / allc["elapsed"]
+    return {"value": round(vn, 2), "unit": "env_steps/s", "cores": cores, "kind": "port",
+            "value_1core": round(v1, 2), "value_allcores": round(vn, 2), "cores_affinity": aff,
+            "sims_per_s_allcores": round(allc["searches"] * sims / allc["elapsed"], 1),
+            "sample": f"C++ restatement of the DOG MuZero slice (oracle/cpu_dog.cpp + oracle/cpu_search.hpp, fp32 "
+                      f"AVX2/FMA, OpenMP): 4p teams, {lanes} games per thread, S={sims} D={depth}, {half:.0f} s at 1 "
+                      f"thread ({one['env_steps']} env-steps, {one['searches']} searches) and {half:.0f} s at {cores} "
+                      f"threads ({allc['env_steps']} env-steps, {allc['searches']} searches); affinity shows {aff} CPUs"}
 
 
 def run_dog_muzero(args):
@@ -527,7 +510,7 @@ def run_dog_muzero(args):
                              f"search time is its serial chain of 100 simulations"},
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = dog_muzero_cpu_baseline(min(args.cpu_seconds, 12.0), args.sims, args.depth)
+        out["cpu_baseline"] = dog_muzero_cpu_baseline(args.cpu_seconds, args.sims, args.depth)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -9,7 +9,7 @@
 // (oracle/dog.py:engine_shuffle_keys / engine_random_action), and is checked against it by
 // tests/test_cpu_baseline_dog.py (the reference's golden step vectors, lockstep random play through deals and
 // restarts).  Only tests/ and bench.py's cpu_baseline leg load it; the product path never does.
-#include "cpu_nets.hpp"
+#include "cpu_search.hpp"
 
 namespace {
 
@@ -658,6 +658,163 @@ int random_action(const uint8_t* mask, uint64_t seed, int game, int turn) {
   return legal[std::min((int)(u * (float)n), n - 1)];
 }
 
+// ------------------------------------------------------------------------------------- DOG MuZero slice
+// The reference's DOG MuZero is a skeleton (MuZero_DOG/muzero_dog.py:85-99 and game_agent.py:52-57 are `pass`);
+// this follows the builder-defined slice the device runs and oracle/dog_muzero.py restates: the 34-channel
+// encoding, the DOG RepresentationNetwork (LayerNorm head), Dyn4 / Pred4 at A = 806, mctx's Gumbel search.
+constexpr int kDogC = 34;
+
+// oracle/dog_muzero.py:encode_board -> out [34][56] (spatial channels 0..5, global features 6..33 broadcast)
+void encode_board(const muzcpu_dog& e, float* out) {
+  const int cp = e.current_player, bs = e.board_size, dist = bs / 4, ng = e.total - bs;
+  const bool teams = has(e, R_TEAMS);
+  int b[kCells];
+  for (int i = 0; i < bs; ++i) b[i] = e.board[(i + dist * cp) % bs];
+  for (int i = 0; i < ng; ++i) b[bs + i] = e.board[bs + (i + 4 * cp) % ng];
+  int rolled[4];
+  for (int r = 0; r < 4; ++r) rolled[r] = (cp + r) % 4;
+  for (int r = 0; r < 4; ++r)
+    for (int w = 0; w < kCells; ++w) out[r * kCells + w] = (float)(b[w] == rolled[r]);
+  for (int w = 0; w < kCells; ++w) {
+    const float* pc = out;
+    out[4 * kCells + w] = teams ? pc[w] + pc[2 * kCells + w] : pc[w];
+    out[5 * kCells + w] = teams ? pc[kCells + w] + pc[3 * kCells + w] : pc[kCells + w] + pc[2 * kCells + w] + pc[3 * kCells + w];
+  }
+  const int sub = sub_player(e);
+  int g[28] = {0};
+  for (int r = 0; r < 4; ++r)
+    for (int k = 0; k < 4; ++k) g[r] += e.pins[rolled[r] * 4 + k] == -1;
+  for (int c = 0; c < kNC; ++c) g[4 + c] = e.hands[sub * kNC + c];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < kNC; ++c) g[18 + r] += e.hands[rolled[r] * kNC + c];
+  g[22] = e.phase;
+  g[23] = e.hand_size;
+  g[24] = sub != cp;
+  for (int c = 0; c < kNC; ++c) g[25] += e.deck[c];
+  g[26] = (int)pymod(e.round_starter - cp, 4);
+  const int mates[2] = {cp, (cp + 2) % 4};
+  for (int m = 0; m < (teams ? 2 : 1); ++m)
+    for (int k = 0; k < 4; ++k) g[27] += e.pins[mates[m] * 4 + k] >= bs;
+  for (int c = 0; c < 28; ++c)
+    for (int w = 0; w < kCells; ++w) out[(6 + c) * kCells + w] = (float)g[c];
+}
+
+// recurrent_inference_fn of the slice: DynamicsNetwork4 (MuZero_det_MADN/muzero_deterministic_madn.py:391-457)
+// at one-hot width A = net.A, then PredictionNetwork4.  The one-hot products are row gathers (Dense_0: bias +
+// W[a]; Dense_6 / Dense_7: the latent rows' fma chain + W[256 + a]), the same roundings as the full products
+// with a one-hot operand (every other term adds an exact zero).
+void recurrent_wide(const Net& net, const int* action, const float* emb, int B, float* reward, float* discount,
+                    float* logits, float* value, float* nxt, Scratch& s) {
+  const std::string d = "dynamics/";
+  const int A = net.A;
+  const float *W0 = net.w(d + "Dense_0/kernel"), *b0 = net.w(d + "Dense_0/bias");
+  std::vector<float> e((size_t)B * 64), sc((size_t)B * kLat), shf((size_t)B * kLat);
+  for (int b = 0; b < B; ++b) {
+    const int a = action[b];
+    for (int j = 0; j < 64; ++j) {
+      const float v = (a >= 0 && a < A) ? b0[j] + W0[(size_t)a * 64 + j] : b0[j];
+      e[(size_t)b * 64 + j] = std::max(v, 0.f);
+    }
+  }
+  std::vector<float> x(emb, emb + (size_t)B * kLat);
+  layer_norm(net, d + "LayerNorm_0", x.data(), B, kLat, false);
+  dense(net, d + "Dense_1", e.data(), B, 64, kLat, sc.data());
+  dense(net, d + "Dense_2", e.data(), B, 64, kLat, shf.data());
+  for (size_t i = 0; i < x.size(); ++i) x[i] = x[i] * (1.0f + sc[i]) + shf[i];
+  std::vector<float> y((size_t)B * kLat);
+  dense(net, d + "Dense_3", x.data(), B, kLat, kLat, y.data());
+  layer_norm(net, d + "LayerNorm_1", y.data(), B, kLat, true);
+  dense(net, d + "Dense_4", y.data(), B, kLat, kLat, x.data());
+  layer_norm(net, d + "LayerNorm_2", x.data(), B, kLat, true);
+  for (int i = 0; i < 2; ++i) resblock(net, d + "ResBlock_" + std::to_string(i), x.data(), B, s.t1, s.t2);
+  dense(net, d + "Dense_5", x.data(), B, kLat, kLat, y.data());
+  for (size_t i = 0; i < y.size(); ++i) nxt[i] = emb[i] + y[i];
+  minmax(nxt, B, kLat);
+  std::vector<float> h((size_t)B * 64), l3((size_t)B * 3);
+  const char* hid[2] = {"Dense_6", "Dense_7"};
+  const char* head[2] = {"reward_head", "discount_head"};
+  float* out[2] = {reward, discount};
+  for (int k = 0; k < 2; ++k) {
+    const float* W = net.w(d + hid[k] + "/kernel");
+    dense_raw(W, net.w(d + hid[k] + "/bias"), nxt, B, kLat, 64, h.data());   // the latent rows of [nxt, one-hot]
+    for (int b = 0; b < B; ++b) {
+      const int a = action[b];
+      for (int j = 0; j < 64; ++j) {
+        float v = h[(size_t)b * 64 + j];
+        if (a >= 0 && a < A) v += W[(size_t)(kLat + a) * 64 + j];
+        h[(size_t)b * 64 + j] = std::max(v, 0.f);
+      }
+    }
+    dense(net, d + head[k], h.data(), B, 64, 3, l3.data());
+    for (int b = 0; b < B; ++b) out[k][b] = support3(&l3[(size_t)b * 3]);
+  }
+  prediction(net, nxt, B, logits, value, s);
+}
+
+struct DogRec {
+  const Net& net;
+  Scratch& s;
+  void operator()(const int* action, const float* emb, int B, float* reward, float* discount, float* logits,
+                  float* value, float* nxt) const {
+    recurrent_wide(net, action, emb, B, reward, discount, logits, value, nxt, s);
+  }
+};
+
+// One self-play turn of `n` DOG lanes (MuZero_det_MADN/game_agent.py:64-192's turn at A = 806, as
+// game_agent_dog.DogSelfPlay.turn runs it): legal mask -> (no legal action: no_step) -> encode -> root inference
+// -> Gumbel search with the engine's noise of (seed, game id, turn) -> env_step.  act_out[i] = the action (-1:
+// no_step).  Returns the number of searched games.
+struct DogTurn {
+  Search sr;
+  Scratch s;
+  std::vector<Tree<kActions>> trees;
+  std::vector<float> obs, lg, v, e, gum, w, rv;
+  std::vector<int> act, search;
+  std::unique_ptr<bool[]> inv;
+  void init(int n, int S, int D) {
+    sr.init(S, D);
+    obs.resize((size_t)n * kDogC * kCells);
+    lg.resize((size_t)n * kActions);
+    v.resize(n);
+    e.resize((size_t)n * kLat);
+    gum.resize((size_t)n * kActions);
+    w.resize((size_t)n * kActions);
+    rv.resize(n);
+    act.resize(n);
+    inv.reset(new bool[(size_t)n * kActions]);
+  }
+  int run(const Net& net, muzcpu_dog* envs, const int* gid, int n, int turn, float temp, uint64_t seed, int* act_out) {
+    search.clear();
+    uint8_t mask[kActions];
+    for (int i = 0; i < n; ++i) {
+      valid_actions(envs[i], mask);
+      bool any = false;
+      for (int a = 0; a < kActions; ++a) any = any || mask[a];
+      act_out[i] = -1;
+      if (!any) continue;
+      const int k = (int)search.size();
+      for (int a = 0; a < kActions; ++a) inv[(size_t)k * kActions + a] = !mask[a];
+      encode_board(envs[i], &obs[(size_t)k * kDogC * kCells]);
+      gumbel_noise<kActions>(seed, gid[i], turn, temp, &gum[(size_t)k * kActions]);
+      search.push_back(i);
+    }
+    const int B = (int)search.size();
+    if (B) {
+      representation(net, obs.data(), B, e.data(), s);
+      prediction(net, e.data(), B, lg.data(), v.data(), s);
+      gumbel_search<kActions>(sr, B, lg.data(), v.data(), e.data(), inv.get(), gum.data(), trees, act.data(), w.data(),
+                              rv.data(), DogRec{net, s});
+      for (int k = 0; k < B; ++k) act_out[search[k]] = act[k];
+    }
+    for (int i = 0; i < n; ++i) {
+      int r, d;
+      if (act_out[i] < 0) no_step(envs[i]);
+      else env_step(envs[i], act_out[i], r, d);
+    }
+    return B;
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -737,6 +894,90 @@ int64_t muzcpu_dog_bench(int P, int rules, int lanes, uint64_t seed, int threads
     steps += mine;
     games += fin;
   }
+  if (games_out) *games_out = games.load();
+  if (elapsed_out) *elapsed_out = elapsed();
+  return steps.load();
+}
+
+// ---- DOG MuZero slice (see DogTurn) ------------------------------------------------------------------------------
+void muzcpu_dog_encode(const muzcpu_dog* e, float* out) { encode_board(*e, out); }
+
+// recurrent inference of a DOG net (muzcpu_net_create with the slice's parameters: A = 806)
+void muzcpu_dog_recurrent(void* net, const int* action, const float* emb, int B, float* reward, float* discount,
+                          float* logits, float* value, float* nxt) {
+  Scratch s;
+  recurrent_wide(*(Net*)net, action, emb, B, reward, discount, logits, value, nxt, s);
+}
+
+// one batched gumbel_muzero_policy at A = 806 from given root outputs (invalid: uint8 [B][806], gumbel: scaled
+// noise [B][806]) -> action [B], action_weights [B][806], root value [B]
+void muzcpu_dog_search(void* net, int B, int S, int D, const float* logits, const float* value, const float* emb,
+                       const uint8_t* invalid, const float* gumbel, int* action, float* weights, float* root_value) {
+  Search sr;
+  sr.init(S, D);
+  Scratch s;
+  std::vector<Tree<kActions>> trees(B);
+  std::unique_ptr<bool[]> inv(new bool[(size_t)B * kActions]);
+  for (size_t i = 0; i < (size_t)B * kActions; ++i) inv[i] = invalid[i] != 0;
+  gumbel_search<kActions>(sr, B, logits, value, emb, inv.get(), gumbel, trees, action, weights, root_value,
+                          DogRec{*(Net*)net, s});
+}
+
+// n lanes of DOG MuZero self-play on one thread for `turns` turns: lane i starts game i, a finished game is
+// replaced before its lane's next turn by a fresh one with the next game id (deal keys and Gumbel noise of that
+// id).  actions [turns][n] (-1 = no_step).  Returns the number of searches.
+int64_t muzcpu_dog_mz_play(void* netp, int rules, int n, int turns, int S, int D, float temp, uint64_t seed,
+                           int32_t* actions) {
+  const Net& net = *(Net*)netp;
+  std::vector<muzcpu_dog> envs(n);
+  std::vector<int> gid(n), act(n);
+  for (int i = 0; i < n; ++i) env_reset(envs[i], 4, rules, seed, gid[i] = i);
+  int next = n;
+  DogTurn dt;
+  dt.init(n, S, D);
+  int64_t searches = 0;
+  for (int t = 0; t < turns; ++t) {
+    for (int i = 0; i < n; ++i)
+      if (envs[i].done) env_reset(envs[i], 4, rules, seed, gid[i] = next++);
+    searches += dt.run(net, envs.data(), gid.data(), n, t, temp, seed, act.data());
+    for (int i = 0; i < n; ++i) actions[(size_t)t * n + i] = act[i];
+  }
+  return searches;
+}
+
+// The DOG MuZero CPU baseline (config (d), MuZero policy): `threads` OpenMP threads, each playing `lanes` games
+// turn by turn as muzcpu_dog_mz_play (fresh game ids from a shared counter) until `seconds` have passed.  Returns
+// env-steps (lanes x turns, no_step turns included, as the device bench counts them); searches, finished games
+// and elapsed seconds through the pointers.
+int64_t muzcpu_dog_mz_bench(void* netp, int rules, int lanes, int S, int D, float temp, uint64_t seed, int threads,
+                            double seconds, int64_t* searches_out, int64_t* games_out, double* elapsed_out) {
+  const Net& net = *(Net*)netp;
+  std::atomic<int> next_game{0};
+  std::atomic<int64_t> steps{0}, searches{0}, games{0};
+  const auto t0 = std::chrono::steady_clock::now();
+  auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+#pragma omp parallel num_threads(threads)
+  {
+    std::vector<muzcpu_dog> envs(lanes);
+    std::vector<int> gid(lanes), act(lanes);
+    for (int i = 0; i < lanes; ++i) env_reset(envs[i], 4, rules, seed, gid[i] = next_game.fetch_add(1));
+    DogTurn dt;
+    dt.init(lanes, S, D);
+    int64_t my_steps = 0, my_searches = 0, my_games = 0;
+    for (int t = 0; elapsed() < seconds; ++t) {
+      for (int i = 0; i < lanes; ++i)
+        if (envs[i].done) {
+          env_reset(envs[i], 4, rules, seed, gid[i] = next_game.fetch_add(1));
+          ++my_games;
+        }
+      my_searches += dt.run(net, envs.data(), gid.data(), lanes, t, temp, seed, act.data());
+      my_steps += lanes;
+    }
+    steps += my_steps;
+    searches += my_searches;
+    games += my_games;
+  }
+  if (searches_out) *searches_out = searches.load();
   if (games_out) *games_out = games.load();
   if (elapsed_out) *elapsed_out = elapsed();
   return steps.load();

@@ -167,7 +167,8 @@ void conv1d(const Net& net, const std::string& name, const float* in, int B, int
   dense(net, name, cols.data(), B * kCells, K * Cin, Cout, out);   // kernel [K][Cin][Cout] = [K*Cin][Cout]
 }
 
-// RepresentationNetwork2 (75-141): obs [B][C][56] -> latent [B][256]
+// RepresentationNetwork2 (75-141): obs [B][C][56] -> latent [B][256]; with representation/LayerNorm_7 the DOG
+// RepresentationNetwork (MuZero_DOG/muzero_dog.py:25-83: LayerNorm instead of min-max after Dense_4)
 void representation(const Net& net, const float* obs, int B, float* lat, Scratch& s) {
   const int C = net.C;
   const std::string r = "representation/";
@@ -203,7 +204,8 @@ void representation(const Net& net, const float* obs, int B, float* lat, Scratch
   layer_norm(net, r + "LayerNorm_6", h.data(), B, kLat, true);
   for (int i = 0; i < 6; ++i) resblock(net, r + "ResBlock_" + std::to_string(i), h.data(), B, s.t1, s.t2);
   dense(net, r + "Dense_4", h.data(), B, kLat, kLat, lat);
-  minmax(lat, B, kLat);
+  if (net.w(r + "LayerNorm_7/scale")) layer_norm(net, r + "LayerNorm_7", lat, B, kLat, false);   // DOG head (80-81)
+  else minmax(lat, B, kLat);
 }
 
 // PredictionNetwork4 (549-583): latent [B][256] -> logits [B][A], value [B]

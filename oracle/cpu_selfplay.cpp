@@ -12,7 +12,7 @@
 // Parallelism mirrors the reference's vmap over games: each OpenMP thread owns a batch of game lanes,
 // searches them together (batched network calls, per-game trees) and refills a lane with the next game
 // when its game ends.
-#include "cpu_nets.hpp"
+#include "cpu_search.hpp"
 
 extern "C" {
 
@@ -271,243 +271,15 @@ void recurrent(const Net& net, const int* action, const float* emb, int B, float
   prediction(net, nxt, B, logits, value, s);
 }
 
-// ------------------------------------------------------------------------------ mctx gumbel_muzero_policy
-std::vector<int> considered_sequence(int m, int S) {   // seq_halving.get_sequence_of_considered_visits
-  std::vector<int> seq;
-  if (m <= 1) {
-    for (int i = 0; i < S; ++i) seq.push_back(i);
-    return seq;
-  }
-  const int log2max = (int)std::ceil(std::log2((double)m));
-  std::vector<int> visits(m, 0);
-  int k = m;
-  while ((int)seq.size() < S) {
-    const int extra = std::max(1, (int)(S / (log2max * k)));
-    for (int e = 0; e < extra; ++e) {
-      for (int i = 0; i < k; ++i) seq.push_back(visits[i]);
-      for (int i = 0; i < k; ++i) visits[i] += 1;
-    }
-    k = std::max(2, k / 2);
-  }
-  seq.resize(S);
-  return seq;
-}
-
-struct Tree {
-  int N;
-  std::vector<int> visits, parent, afp, c_index, c_visits;
-  std::vector<float> raw, value, c_prior, c_value, c_reward, c_disc, emb;
-  void init(int n) {
-    N = n;
-    visits.assign(n, 0);
-    parent.assign(n, -1);
-    afp.assign(n, -1);
-    raw.assign(n, 0.f);
-    value.assign(n, 0.f);
-    c_index.assign((size_t)n * kA, -1);
-    c_visits.assign((size_t)n * kA, 0);
-    c_prior.assign((size_t)n * kA, 0.f);
-    c_value.assign((size_t)n * kA, 0.f);
-    c_reward.assign((size_t)n * kA, 0.f);
-    c_disc.assign((size_t)n * kA, 0.f);
-    emb.assign((size_t)n * kLat, 0.f);
-  }
-  void update(int node, const float* prior, float v, const float* e) {
-    std::memcpy(&c_prior[(size_t)node * kA], prior, sizeof(float) * kA);
-    raw[node] = v;
-    value[node] = v;
-    visits[node] += 1;
-    std::memcpy(&emb[(size_t)node * kLat], e, sizeof(float) * kLat);
+// the search: oracle/cpu_search.hpp (gumbel_search<24>) driving this file's recurrent inference
+struct DetRec {
+  const Net& net;
+  Scratch& s;
+  void operator()(const int* action, const float* emb, int B, float* reward, float* discount, float* logits,
+                  float* value, float* nxt) const {
+    recurrent(net, action, emb, B, reward, discount, logits, value, nxt, s);
   }
 };
-
-
-// The tree arithmetic rounds exactly like the NumPy restatement (oracle/mctx_gumbel.py) and the device search
-// (csrc/search.hip): each product rounded on its own (rnd() keeps the compiler from fusing it into an fma), sums over
-// the 24 actions in numpy's pairwise order, exp correctly rounded (float64, then rounded once).
-inline float rnd(float x) {
-  asm volatile("" : "+x"(x));
-  return x;
-}
-inline float sum24(const float* v) {   // numpy's pairwise sum of a contiguous row of 24
-  float r[8];
-  for (int j = 0; j < 8; ++j) r[j] = rnd(rnd(v[j] + v[j + 8]) + v[j + 16]);
-  return rnd(rnd(rnd(r[0] + r[1]) + rnd(r[2] + r[3])) + rnd(rnd(r[4] + r[5]) + rnd(r[6] + r[7])));
-}
-inline float exp_cr(float x) { return (float)std::exp((double)x); }
-void softmax_tree(const float* x, float* out) {
-  float m = -kInf, u[kA];
-  for (int i = 0; i < kA; ++i) m = std::max(m, x[i]);
-  for (int i = 0; i < kA; ++i) u[i] = exp_cr(x[i] - m);
-  const float s = sum24(u);
-  for (int i = 0; i < kA; ++i) out[i] = u[i] / s;
-}
-
-// qtransform_completed_by_mix_value(value_scale 0.5, maxvisit_init 50, rescale, mixed value, eps 1e-8)
-void completed_q(const Tree& t, int node, float* cq) {
-  static_assert(kA == 24, "sum24: 24 actions");
-  const int* vis = &t.c_visits[(size_t)node * kA];
-  float q[kA], pp[kA], tmp[kA];
-  softmax_tree(&t.c_prior[(size_t)node * kA], pp);
-  int sumv = 0, maxv = 0;
-  for (int a = 0; a < kA; ++a) {
-    q[a] = rnd(t.c_reward[(size_t)node * kA + a] + rnd(t.c_disc[(size_t)node * kA + a] * t.c_value[(size_t)node * kA + a]));
-    pp[a] = std::max(kTiny, pp[a]);
-    sumv += vis[a];
-    maxv = std::max(maxv, vis[a]);
-    tmp[a] = vis[a] > 0 ? pp[a] : 0.f;
-  }
-  const float sp = sum24(tmp);
-  for (int a = 0; a < kA; ++a) tmp[a] = vis[a] > 0 ? rnd(rnd(pp[a] * q[a]) / sp) : 0.f;
-  const float wq = sum24(tmp);
-  const float mixed = rnd(t.raw[node] + rnd((float)sumv * wq)) / (float)(sumv + 1);
-  float lo = kInf, hi = -kInf;
-  for (int a = 0; a < kA; ++a) {
-    cq[a] = vis[a] > 0 ? q[a] : mixed;
-    lo = std::min(lo, cq[a]);
-    hi = std::max(hi, cq[a]);
-  }
-  const float den = std::max(hi - lo, 1e-8f);
-  const float scale = (50.0f + (float)maxv) * 0.5f;
-  for (int a = 0; a < kA; ++a) cq[a] = scale * ((cq[a] - lo) / den);
-}
-
-
-struct Search {
-  int S, D;
-  std::vector<std::vector<int>> table;   // [m][sim]
-  void init(int s, int d) {
-    S = s;
-    D = d;
-    table.clear();
-    for (int m = 0; m <= 16; ++m) table.push_back(considered_sequence(m, S));
-  }
-};
-
-// score_considered + masked argmax (root) / softmax(prior + cq) - N / (1 + sum N) (interior)
-int select_child(const Tree& t, int node, int depth, const bool* invalid, const float* gumbel, const Search& sr,
-                 int ncons) {
-  float cq[kA], sc[kA];
-  completed_q(t, node, cq);
-  const int* vis = &t.c_visits[(size_t)node * kA];
-  const float* prior = &t.c_prior[(size_t)node * kA];
-  int sumv = 0;
-  for (int a = 0; a < kA; ++a) sumv += vis[a];
-  if (depth == 0) {
-    const int cv = sr.table[ncons][std::min(sumv, sr.S - 1)];
-    float pm = -kInf;
-    for (int a = 0; a < kA; ++a) pm = std::max(pm, prior[a]);
-    for (int a = 0; a < kA; ++a) {
-      const float s = std::max(-1e9f, gumbel[a] + (prior[a] - pm) + cq[a]) + (vis[a] == cv ? 0.f : -kInf);
-      sc[a] = invalid[a] ? -kInf : s;
-    }
-  } else {
-    float z[kA], p[kA];
-    for (int a = 0; a < kA; ++a) z[a] = prior[a] + cq[a];
-    softmax_tree(z, p);
-    for (int a = 0; a < kA; ++a) sc[a] = p[a] - (float)vis[a] / (float)(1 + sumv);
-  }
-  return argmax(sc, kA);
-}
-
-// one batched gumbel_muzero_policy over `B` games (root inference outputs given)
-void gumbel_search(const Net& net, const Search& sr, int B, const float* logits, const float* rvalue,
-                   const float* remb, const bool* invalid, const float* gumbel, std::vector<Tree>& trees,
-                   int* action_out, float* weights_out, float* value_out, Scratch& s) {
-  const int S = sr.S;
-  std::vector<int> ncons(B), parent(B), act(B), nxt(B);
-  std::vector<float> rew(B), disc(B), lg((size_t)B * kA), val(B), ne((size_t)B * kLat), pe((size_t)B * kLat);
-  for (int b = 0; b < B; ++b) {
-    Tree& t = trees[b];
-    t.init(S + 1);
-    float pr[kA];
-    float m = -kInf;
-    for (int a = 0; a < kA; ++a) m = std::max(m, logits[(size_t)b * kA + a]);
-    int nv = 0;
-    for (int a = 0; a < kA; ++a) {
-      pr[a] = invalid[(size_t)b * kA + a] ? kFMin : logits[(size_t)b * kA + a] - m;
-      nv += !invalid[(size_t)b * kA + a];
-    }
-    ncons[b] = std::min(16, nv);
-    t.update(0, pr, rvalue[b], remb + (size_t)b * kLat);
-  }
-  for (int sim = 0; sim < S; ++sim) {
-    for (int b = 0; b < B; ++b) {   // simulate
-      const Tree& t = trees[b];
-      int node = 0, depth = 0, a = 0;
-      while (true) {
-        a = select_child(t, node, depth, invalid + (size_t)b * kA, gumbel + (size_t)b * kA, sr, ncons[b]);
-        const int child = t.c_index[(size_t)node * kA + a];
-        ++depth;
-        if (child == -1 || depth >= sr.D) break;
-        node = child;
-      }
-      parent[b] = node;
-      act[b] = a;
-      const int c = t.c_index[(size_t)node * kA + a];
-      nxt[b] = c == -1 ? sim + 1 : c;
-      std::memcpy(&pe[(size_t)b * kLat], &t.emb[(size_t)node * kLat], sizeof(float) * kLat);
-    }
-    recurrent(net, act.data(), pe.data(), B, rew.data(), disc.data(), lg.data(), val.data(), ne.data(), s);
-    for (int b = 0; b < B; ++b) {   // expand + backward
-      Tree& t = trees[b];
-      const int p = parent[b], a = act[b], nn = nxt[b];
-      t.update(nn, &lg[(size_t)b * kA], val[b], &ne[(size_t)b * kLat]);
-      t.c_index[(size_t)p * kA + a] = nn;
-      t.c_reward[(size_t)p * kA + a] = rew[b];
-      t.c_disc[(size_t)p * kA + a] = disc[b];
-      t.parent[nn] = p;
-      t.afp[nn] = a;
-      float leaf = t.value[nn];
-      int idx = nn;
-      while (idx != 0) {
-        const int pr = t.parent[idx], pa = t.afp[idx];
-        const int cnt = t.visits[pr];
-        const size_t e = (size_t)pr * kA + pa;
-        leaf = rnd(t.c_reward[e] + rnd(t.c_disc[e] * leaf));
-        t.value[pr] = rnd(rnd(t.value[pr] * (float)cnt) + leaf) / ((float)cnt + 1.0f);
-        t.visits[pr] = cnt + 1;
-        t.c_value[e] = t.value[idx];
-        t.c_visits[e] += 1;
-        idx = pr;
-      }
-    }
-  }
-  for (int b = 0; b < B; ++b) {   // final action + action_weights (policies.py tail)
-    const Tree& t = trees[b];
-    float cq[kA], sc[kA], z[kA];
-    completed_q(t, 0, cq);
-    int cv = 0;
-    for (int a = 0; a < kA; ++a) cv = std::max(cv, t.c_visits[a]);
-    const float* prior = &t.c_prior[0];
-    float pm = -kInf;
-    for (int a = 0; a < kA; ++a) pm = std::max(pm, prior[a]);
-    const bool* inv = invalid + (size_t)b * kA;
-    for (int a = 0; a < kA; ++a) {
-      const float sv = std::max(-1e9f, gumbel[(size_t)b * kA + a] + (prior[a] - pm) + cq[a]) +
-                       (t.c_visits[a] == cv ? 0.f : -kInf);
-      sc[a] = inv[a] ? -kInf : sv;
-      z[a] = prior[a] + cq[a];
-    }
-    action_out[b] = argmax(sc, kA);
-    float zm = -kInf;
-    for (int a = 0; a < kA; ++a) zm = std::max(zm, z[a]);
-    for (int a = 0; a < kA; ++a) z[a] = inv[a] ? kFMin : z[a] - zm;
-    softmax_tree(z, weights_out + (size_t)b * kA);
-    value_out[b] = t.value[0];
-  }
-}
-
-// counter-based Gumbel noise of the engine (csrc/rng.hpp, oracle/selfplay.py:gumbel_noise)
-void gumbel_noise(uint64_t seed, int gid, int turn, float scale, float* out) {
-  for (int a = 0; a < kA; ++a) {
-    const uint64_t h = mix64(seed ^ mix64(((uint64_t)(uint32_t)gid << 32) | (uint32_t)turn) ^
-                             ((uint64_t)(a + 1) * 0xD6E8FEB86659FD93ull));
-    float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-    u = std::max(u, kTiny);
-    out[a] = scale * (-std::log(-std::log(u)));
-  }
-}
 
 struct Lane {
   muzcpu_det env;
@@ -530,6 +302,7 @@ void* muzcpu_net_create(const char** names, const float** data, const int64_t* s
   Net* n = new Net;
   n->C = obs_channels;
   for (int i = 0; i < count; ++i) n->p[names[i]] = std::vector<float>(data[i], data[i] + sizes[i]);
+  if (n->w("prediction/Dense_2/bias")) n->A = (int)n->n("prediction/Dense_2/bias");   // 24 det, 806 DOG
   return n;
 }
 void muzcpu_net_destroy(void* n) { delete (Net*)n; }
@@ -569,7 +342,7 @@ int muzcpu_selfplay(void* netp, int P, int rules, int n, int S, int D, int T, fl
   Search sr;
   sr.init(S, D);
   Scratch s;
-  std::vector<Tree> trees(n);
+  std::vector<Tree<kA>> trees(n);
   std::vector<int> idx(n, 0);
   int step = 0;
   while (step < T) {
@@ -596,15 +369,15 @@ int muzcpu_selfplay(void* netp, int P, int rules, int n, int S, int D, int T, fl
       std::vector<int> act(B);
       for (int k = 0; k < B; ++k) {
         encode_board(envs[search[k]], &obs[(size_t)k * C * kCells]);
-        gumbel_noise(seed, search[k], step, temp, &gum[(size_t)k * kA]);
+        gumbel_noise<kA>(seed, search[k], step, temp, &gum[(size_t)k * kA]);
       }
       representation(net, obs.data(), B, e.data(), s);
       prediction(net, e.data(), B, lg.data(), v.data(), s);
       std::vector<bool> invb(inv.begin(), inv.end());
       std::unique_ptr<bool[]> ib(new bool[invb.size()]);
       for (size_t q = 0; q < invb.size(); ++q) ib[q] = invb[q];
-      gumbel_search(net, sr, B, lg.data(), v.data(), e.data(), ib.get(), gum.data(), trees, act.data(), w.data(),
-                    rv.data(), s);
+      gumbel_search<kA>(sr, B, lg.data(), v.data(), e.data(), ib.get(), gum.data(), trees, act.data(), w.data(),
+                        rv.data(), DetRec{net, s});
       for (int k = 0; k < B; ++k) {
         const int i = search[k], t = idx[i];
         if (tr) {
@@ -652,7 +425,7 @@ int64_t muzcpu_bench(void* netp, int P, int rules, int lanes, int S, int D, int 
     Search sr;
     sr.init(S, D);
     Scratch s;
-    std::vector<Tree> trees(lanes);
+    std::vector<Tree<kA>> trees(lanes);
     std::vector<Lane> L(lanes);
     auto fresh = [&](Lane& l) {
       env_reset(l.env, P, layout, 10, 0, rules);
@@ -677,7 +450,7 @@ int64_t muzcpu_bench(void* netp, int P, int rules, int lanes, int S, int D, int 
           const int k = (int)search.size();
           for (int q = 0; q < 24; ++q) inv[(size_t)k * kA + q] = !va[q / 6][q % 6];
           encode_board(l.env, &obs[(size_t)k * C * kCells]);
-          gumbel_noise(seed, l.game, l.t, temp, &gum[(size_t)k * kA]);
+          gumbel_noise<kA>(seed, l.game, l.t, temp, &gum[(size_t)k * kA]);
           search.push_back(i);
         } else {
           no_step(l.env);
@@ -687,8 +460,8 @@ int64_t muzcpu_bench(void* netp, int P, int rules, int lanes, int S, int D, int 
       if (B) {
         representation(net, obs.data(), B, e.data(), s);
         prediction(net, e.data(), B, lg.data(), v.data(), s);
-        gumbel_search(net, sr, B, lg.data(), v.data(), e.data(), inv.get(), gum.data(), trees, act.data(), w.data(),
-                      rv.data(), s);
+        gumbel_search<kA>(sr, B, lg.data(), v.data(), e.data(), inv.get(), gum.data(), trees, act.data(), w.data(),
+                          rv.data(), DetRec{net, s});
         for (int k = 0; k < B; ++k) {
           int r, d;
           env_step(L[search[k]].env, act[k] / 6, act[k] % 6 + 1, r, d);

@@ -88,6 +88,7 @@ class CpuNet:
         sizes = (ctypes.c_int64 * n)(*[v.size for v in self._keep.values()])
         self.h = L.muzcpu_net_create(cn, ptrs, sizes, n, obs_channels)
         self.C = obs_channels
+        self.A = int(self._keep["prediction/Dense_2/bias"].size) if "prediction/Dense_2/bias" in self._keep else 24
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
@@ -97,7 +98,7 @@ class CpuNet:
     def root(self, obs):
         obs = np.ascontiguousarray(obs, np.float32)
         B = obs.shape[0]
-        lg, v, e = np.empty((B, 24), np.float32), np.empty(B, np.float32), np.empty((B, 256), np.float32)
+        lg, v, e = np.empty((B, self.A), np.float32), np.empty(B, np.float32), np.empty((B, 256), np.float32)
         load().muzcpu_root(self.h, _p(obs), B, _p(lg), _p(v), _p(e))
         return lg, v, e
 
@@ -106,9 +107,35 @@ class CpuNet:
         emb = np.ascontiguousarray(emb, np.float32)
         B = emb.shape[0]
         r, d, v = (np.empty(B, np.float32) for _ in range(3))
-        lg, nx = np.empty((B, 24), np.float32), np.empty((B, 256), np.float32)
-        load().muzcpu_recurrent(self.h, _p(a), _p(emb), B, _p(r), _p(d), _p(lg), _p(v), _p(nx))
+        lg, nx = np.empty((B, self.A), np.float32), np.empty((B, 256), np.float32)
+        fn = load().muzcpu_recurrent if self.A == 24 else _dog_lib().muzcpu_dog_recurrent
+        fn(self.h, _p(a), _p(emb), B, _p(r), _p(d), _p(lg), _p(v), _p(nx))
         return r, d, lg, v, nx
+
+    # ---- the DOG MuZero slice (A = 806; oracle/cpu_dog.cpp) ----
+    def dog_search(self, logits, value, emb, invalid, gumbel, S, D):
+        """One batched gumbel_muzero_policy at A = 806: (action [B], action_weights [B, 806], root_value [B])."""
+        lg = np.ascontiguousarray(logits, np.float32)
+        B = lg.shape[0]
+        v, e = np.ascontiguousarray(value, np.float32), np.ascontiguousarray(emb, np.float32)
+        inv = np.ascontiguousarray(invalid, np.uint8)
+        g = np.ascontiguousarray(gumbel, np.float32)
+        act, w, rv = np.empty(B, np.int32), np.empty((B, 806), np.float32), np.empty(B, np.float32)
+        _dog_lib().muzcpu_dog_search(self.h, B, S, D, _p(lg), _p(v), _p(e), _p(inv), _p(g), _p(act), _p(w), _p(rv))
+        return act, w, rv
+
+    def dog_play(self, rules, n, turns, S, D, temp, seed):
+        """n lanes of DOG MuZero self-play on one thread: (actions [turns, n], searches)."""
+        acts = np.zeros((turns, n), np.int32)
+        k = _dog_lib().muzcpu_dog_mz_play(self.h, dog_rule_bits(**rules), n, turns, S, D, temp, seed, _p(acts))
+        return acts, int(k)
+
+    def dog_bench(self, rules, lanes, S, D, temp, seed, threads, seconds):
+        """DOG MuZero self-play on `threads` cores for `seconds`: dict(env_steps, searches, games, elapsed)."""
+        s, g, t = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+        steps = _dog_lib().muzcpu_dog_mz_bench(self.h, dog_rule_bits(**rules), lanes, S, D, temp, seed, threads, seconds,
+                                               ctypes.byref(s), ctypes.byref(g), ctypes.byref(t))
+        return dict(env_steps=int(steps), searches=int(s.value), games=int(g.value), elapsed=float(t.value))
 
     def selfplay(self, P, rules, n, S, D, T, temp, seed):
         """play_batch_of_games of n games (one thread): (buffers act / val / pol / mask / idx, turns)."""
@@ -377,6 +404,14 @@ def _dog_lib():
         L.muzcpu_dog_play.argtypes = [ip, ip, ip, ip, u64, vp]
         L.muzcpu_dog_bench.restype = ctypes.c_int64
         L.muzcpu_dog_bench.argtypes = [ip, ip, ip, u64, ip, ctypes.c_double, vp, vp]
+        fp = ctypes.c_float
+        L.muzcpu_dog_encode.argtypes = [vp, vp]
+        L.muzcpu_dog_recurrent.argtypes = [vp, vp, vp, ip, vp, vp, vp, vp, vp]
+        L.muzcpu_dog_search.argtypes = [vp, ip, ip, ip, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.muzcpu_dog_mz_play.restype = ctypes.c_int64
+        L.muzcpu_dog_mz_play.argtypes = [vp, ip, ip, ip, ip, ip, fp, u64, vp]
+        L.muzcpu_dog_mz_bench.restype = ctypes.c_int64
+        L.muzcpu_dog_mz_bench.argtypes = [vp, ip, ip, ip, ip, fp, u64, ip, ctypes.c_double, vp, vp, vp]
         _dog_bound = True
     return L
 
@@ -445,6 +480,13 @@ def dog_play(P, rules, n, turns, seed):
     acts = np.zeros((turns, n), np.int32)
     steps = _dog_lib().muzcpu_dog_play(P, dog_rule_bits(**rules), n, turns, seed, _p(acts))
     return acts, int(steps)
+
+
+def dog_encode(d: Dog) -> np.ndarray:
+    """The DOG MuZero slice's observation [34, 56] (oracle/dog_muzero.encode_board)."""
+    out = np.zeros((34, 56), np.float32)
+    _dog_lib().muzcpu_dog_encode(ctypes.byref(d), _p(out))
+    return out
 
 
 def dog_bench(P, rules, lanes, seed, threads, seconds):
