@@ -231,7 +231,7 @@ MEASURED = {
     "traffic": "profiles/r5i_traffic.json",           # HBM bytes per k_gumbel_search launch (FETCH_SIZE x2 + WRITE_SIZE)
     "pmc": "profiles/r5i_pmc.json",                   # TCP_TCC_READ_REQ, SQ_VALU_MFMA_BUSY_CYCLES, ... (k_gumbel_search)
     "loop": "profiles/r5i_loop_bench.log",            # the weight-stream MFMA loop alone (profiles/loop_bench.hip)
-    "dog_traffic": "profiles/r5i_dog_traffic.json",   # HBM bytes per k_dog_search launch
+    "dog_traffic": "profiles/r5j_dog_traffic.json",   # HBM bytes per k_dog_search launch (FETCH_SIZE x2 + WRITE_SIZE)
 }
 
 
@@ -484,8 +484,11 @@ def run_dog_muzero(args):
             dist.destroy_process_group()
         return
     avg_ms = sms / (turns * world)
-    flop = args.batch * args.sims * DOG_MZ_FLOP_PER_SIM
-    achieved = flop / (avg_ms * 1e-3) / 1e12
+    # frac counts the FLOP the search executes: one-hot rows as gathers, the action-only FiLM
+    # sub-graph as a table; the reference-form count (one-hot Dense layers as matmuls) is reported beside it
+    achieved = args.batch * args.sims * DOG_MZ_EXEC_FLOP_PER_SIM / (avg_ms * 1e-3) / 1e12
+    achieved_alg = args.batch * args.sims * DOG_MZ_FLOP_PER_SIM / (avg_ms * 1e-3) / 1e12
+    traffic, traffic_src = measured_traffic("dog_traffic", "k_dog_search")
     # k_dog_search's games per workgroup (dog_search.hip muz_dog_gumbel_search): one per wave up to 2048 games
     rows_env = os.environ.get("MUZ_DOG_TILE_ROWS")
     gpw = 8 if ((rows_env == "8") if rows_env else args.batch <= 2048) else 16
@@ -503,8 +506,13 @@ def run_dog_muzero(args):
                    "parallelism": parallelism(args, world)},
         "roofline": {"bound": "mfma", "kernel": "k_dog_search", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "avg_launch_ms": round(avg_ms, 4),
-                     "flop_per_sim": DOG_MZ_FLOP_PER_SIM, "executed_flop_per_sim": DOG_MZ_EXEC_FLOP_PER_SIM,
-                     "workgroups": -(-args.batch // gpw), "games_per_workgroup": gpw, "traffic": None,
+                     "flop_per_sim": DOG_MZ_EXEC_FLOP_PER_SIM, "flop_counted": "executed (one-hot rows as gathers)",
+                     "reference_form_flop_per_sim": DOG_MZ_FLOP_PER_SIM,
+                     "reference_form_frac": round(achieved_alg / PEAK_FP32_MFMA_TFLOPS, 4),
+                     "workgroups": -(-args.batch // gpw), "games_per_workgroup": gpw,
+                     "traffic": None if traffic is None else round(traffic),
+                     "traffic_achieved_tbs": None if traffic is None else round(traffic / (avg_ms * 1e-3) / 1e12, 3),
+                     "traffic_source": traffic_src,
                      "note": f"{gpw} games per 16-row workgroup ({'one per wave' if gpw == 8 else 'two per wave'}): "
                              f"{args.batch} games occupy {-(-args.batch // gpw)} of the 256 CUs; a workgroup's "
                              f"search time is its serial chain of 100 simulations"},

@@ -26,6 +26,10 @@ constexpr int kSA = 16;                 // child slots per node (A' = 10 used)
 constexpr int kCls = 4, kChance = MUZ_CHANCE_OUTCOMES, kAp = kCls + kChance;
 constexpr float kSFMin = -3.4028234663852886e38f;
 
+#ifdef MUZ_BRANCH_STATS
+__device__ unsigned long long g_branch_hist[(kRows + 1) * (kRows + 1)];
+#endif
+
 struct STree {
   int32_t* c_index;
   float* c_prior;
@@ -356,6 +360,16 @@ __global__ __launch_bounds__(kThreads, 1) void k_stochastic_search(
       need_dec |= s_decp[r] == 1;
       need_cha |= s_decp[r] == 0;
     }
+#ifdef MUZ_BRANCH_STATS
+    if (threadIdx.x == 0) {   // diagnostic: the tile's (decision-parent rows, chance-parent rows) of this expansion
+      int nd = 0, nc = 0;
+      for (int r = 0; r < kRows; ++r) {
+        nd += s_decp[r] == 1;
+        nc += s_decp[r] == 0;
+      }
+      atomicAdd(&g_branch_hist[nd * (kRows + 1) + nc], 1ull);
+    }
+#endif
     f32x4 keep[RowVec<LAT>::V];
     if (need_dec) {
       sdyn_action16<NT256>(wl->sdyn, A, fin, dact, ar, pf, need_cha ? &wl->sdyn.chance_dense1 : &wl->pred.rb[0].d0,
@@ -524,6 +538,19 @@ int check_classic_net(const muz_classic_net_w* w) {
 using namespace muz;
 
 extern "C" {
+
+#ifdef MUZ_BRANCH_STATS
+// diagnostic build: histogram [17][17] of (decision-parent rows, chance-parent rows) per tile expansion
+int muz_diag_branch_hist(unsigned long long* host_out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(muz::g_branch_hist), sizeof(unsigned long long) * 289);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    unsigned long long z[289] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(muz::g_branch_hist), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
 
 int muz_classic_net_prepare(const muz_classic_net_w* w, void* stream) {
   if (!w || !w->sdyn.act_film_tab || !w->sdyn.chance_film_tab) return MUZ_E_INVALID;
