@@ -10,6 +10,10 @@
 #include "detmadn.hpp"
 #include "rng.hpp"
 
+#ifndef MUZ_DOG_GOAL_CHAIN
+#define MUZ_DOG_GOAL_CHAIN 1   // 0: closed-form goal cells (A/B r5m: checks -8 %, env_step +33 %, bench 0.7 % slower)
+#endif
+
 namespace muz {
 
 constexpr int kDogCards = 14;
@@ -45,13 +49,28 @@ struct DogG {   // one game in LDS
 
 // (DOG keeps the plain select chains: k_dog_play runs at 64 VGPRs, where rsel / goal_of's VGPR guards add
 // spills -- its lane-0 transitions index wave-uniform values)
+// Goal cells: the host fills goal[p][g] = goal[p][0] + g for p < P and kTrack for p >= P (host_consts.hpp), so a
+// goal cell is a 4-way select of the seat's first goal cell plus g, and "pos in p's goal" a range test -- instead of
+// 16-way select chains over the kernarg table, which made the legality checks SALU-bound (k_dog_play's check phase).
+// (g in [0, 4) at every call site.)
+__device__ __forceinline__ int dgoal0(const DetConsts& c, int p) {
+  int r = c.goal[0][0];
+  r = p == 1 ? c.goal[1][0] : r;
+  r = p == 2 ? c.goal[2][0] : r;
+  r = p == 3 ? c.goal[3][0] : r;
+  return r;
+}
 __device__ __forceinline__ int dgoal(const DetConsts& c, int p, int g) {
+#if MUZ_DOG_GOAL_CHAIN
   int r = c.goal[0][0];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int h = 0; h < 4; ++h) r = (p == q && g == h) ? c.goal[q][h] : r;
   return r;
+#else
+  return p < c.P ? dgoal0(c, p) + g : kTrack;
+#endif
 }
 
 __device__ __forceinline__ int dcst(const int (&a)[4], int i) {
@@ -86,7 +105,11 @@ __device__ __forceinline__ int dog_sub(const DetConsts& c, const DogG& s) {
 __device__ __forceinline__ int dpin(const DogG& s, int p, int k) { return s.pins[p * 4 + k]; }
 
 __device__ __forceinline__ bool in_goal_p(const DetConsts& c, int p, int pos) {
+#if MUZ_DOG_GOAL_CHAIN
   return pos == dgoal(c, p, 0) || pos == dgoal(c, p, 1) || pos == dgoal(c, p, 2) || pos == dgoal(c, p, 3);
+#else
+  return p < c.P ? (unsigned)(pos - dgoal0(c, p)) < 4u : pos == kTrack;
+#endif
 }
 
 // all(board[goal[cp][g]] != cp  for lo < g < hi)

@@ -725,12 +725,26 @@ __device__ __forceinline__ void dog_checks_block(const DetConsts& c, DogG& s, in
 // is the k-th legal action in action order (joker copies [0, 396) before real copies [396, 792)).
 // (thread t of an NTH-thread workgroup takes check threads t, t + NTH, ... of the 448; NTH a multiple of 64, so
 // each pass is whole waves and the ballots stay per check wave)
+#ifdef MUZ_DOG_STAMPS
+// diagnostic: per physical wave w, cycles of its check pass p (slot 8 + 4 p + w) and the number of passes that ran
+// a check (slot 16 + 4 p + w), lane 0 of every wave; summed in LDS over the launch, added to the global totals once
+// per workgroup at its end (per-pass global atomics from every workgroup serialised and distorted the turn)
+__device__ unsigned long long g_dog_wave_stamps[24];
+__device__ __forceinline__ unsigned long long* dog_wave_acc() {
+  __shared__ unsigned long long acc[24];
+  return acc;
+}
+#endif
 template <int NTH = kDogBlockThreads>
 __device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int tid) {
   if (s.phase == 0) {
     const int cp = dog_sub(c, s);
     const bool hj = s.hands[cp][0] > 0;
-    for (int vt = tid; vt < kDogBlockThreads; vt += NTH) {
+    int pass = 0;
+    for (int vt = tid; vt < kDogBlockThreads; vt += NTH, ++pass) {
+#ifdef MUZ_DOG_STAMPS
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
       const int i = dog_check_of(vt);
       const bool hr = i >= 0 && s.hands[cp][dog_base_card(i)] > 0;
       const bool v = i >= 0 && (hj || hr) && dog_base_valid(c, s, cp, i);
@@ -739,6 +753,13 @@ __device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int
         s.wj[vt >> 6] = bj;
         s.wr[vt >> 6] = br;
       }
+#ifdef MUZ_DOG_STAMPS
+      const bool ran = __ballot(i >= 0 && (hj || hr)) != 0ull;
+      if ((tid & 63) == 0 && pass < 2) {
+        dog_wave_acc()[8 + 4 * pass + (tid >> 6)] += __builtin_amdgcn_s_memtime() - t0;
+        if (ran) dog_wave_acc()[16 + 4 * pass + (tid >> 6)] += 1ull;
+      }
+#endif
     }
   }
   __syncthreads();
@@ -871,8 +892,10 @@ __device__ __forceinline__ int kth_legal(const unsigned long long (&m)[13], floa
 // Diagnostic build only (EXTRA=-DMUZ_DOG_STAMPS): per-phase shader-clock totals of k_dog_play, thread 0.
 #ifdef MUZ_DOG_STAMPS
 __device__ unsigned long long g_dog_stamps[8];
-#define DOG_STAMP_INIT() \
-  unsigned long long ds_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ds_last = __builtin_amdgcn_s_memtime()
+#define DOG_STAMP_INIT()                                                           \
+  unsigned long long ds_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ds_last = __builtin_amdgcn_s_memtime(); \
+  if (tid < 24) dog_wave_acc()[tid] = 0ull;                                          \
+  __syncthreads()
 #define DOG_STAMP(i)                                          \
   do {                                                        \
     if (tid == 0) {                                           \
@@ -881,10 +904,12 @@ __device__ unsigned long long g_dog_stamps[8];
       ds_last = _t;                                           \
     }                                                         \
   } while (0)
-#define DOG_STAMP_END() \
-  do {                  \
-    if (tid == 0)       \
-      for (int i = 0; i < 8; ++i) atomicAdd(&g_dog_stamps[i], ds_acc[i]); \
+#define DOG_STAMP_END()                                                       \
+  do {                                                                        \
+    if (tid == 0)                                                             \
+      for (int i = 0; i < 8; ++i) atomicAdd(&g_dog_stamps[i], ds_acc[i]);    \
+    __syncthreads();                                                          \
+    if (tid >= 8 && tid < 24) atomicAdd(&g_dog_wave_stamps[tid], dog_wave_acc()[tid]); \
   } while (0)
 #else
 #define DOG_STAMP_INIT() do {} while (0)
@@ -1294,6 +1319,16 @@ int muz_diag_dog_stamps(unsigned long long* host_out, int reset) {
   if (reset) {
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_dog_stamps), z, sizeof(z));
+  }
+  return (int)e;
+}
+// per-wave check passes (dog_checks_play): host_out[24] (slots 0..7 unused)
+int muz_diag_dog_wave_stamps(unsigned long long* host_out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_dog_wave_stamps), sizeof(unsigned long long) * 24);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    unsigned long long z[24] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_dog_wave_stamps), z, sizeof(z));
   }
   return (int)e;
 }
