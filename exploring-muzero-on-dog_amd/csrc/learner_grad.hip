@@ -24,7 +24,11 @@ namespace muz {
 typedef float f32x4_g __attribute__((ext_vector_type(4)));
 
 constexpr int kWgMax = 48;    // problems per launch (kernel-argument table)
-constexpr int kWgSeg = 2048;  // rows per workgroup
+#ifndef MUZ_WGRAD_SEG
+#define MUZ_WGRAD_SEG 2048
+#endif
+constexpr int kWgSeg = MUZ_WGRAD_SEG;  // rows per workgroup (a multiple of 64)
+static_assert(kWgSeg % 64 == 0, "segments are whole 64-row steps");
 
 __host__ __device__ constexpr int wgrad_segs(int M) { return M <= kWgSeg ? 1 : (M + kWgSeg - 1) / kWgSeg; }
 

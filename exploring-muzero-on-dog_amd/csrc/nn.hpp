@@ -704,7 +704,8 @@ constexpr int kLdPad = 8;
 constexpr int LD = LAT + kLdPad;     // row stride of 256-wide buffers
 constexpr int LDW = 512 + kLdPad;    // wide buffer (FiLM scale|shift 512, pred heads 384, concat 320)
 constexpr int LDE = 64 + kLdPad;     // small buffer (action embed, global features)
-constexpr int kArenaFloats = 4 * kRows * LD + kRows * LDW + kRows * LDE + 4 * kRows;
+constexpr int kLnPartFloats = kRows * kWaves * 2;   // dense_ln16's per-wave LayerNorm partial sums [16][waves][2]
+constexpr int kArenaFloats = 4 * kRows * LD + kRows * LDW + kRows * LDE + 4 * kRows + kLnPartFloats;
 
 struct Arena {
   float* L;   // latent input (parent embedding)           [16][LD]
@@ -717,6 +718,7 @@ struct Arena {
   float* v1;  // reward                                    [16]
   float* v2;  // discount                                  [16]
   float* v3;  // spare                                     [16]
+  float* P;   // dense_ln16's LayerNorm partials            [16][kWaves][2]
   __device__ static Arena carve(float* base) {
     Arena a;
     a.L = base;
@@ -729,15 +731,137 @@ struct Arena {
     a.v1 = a.v0 + kRows;
     a.v2 = a.v1 + kRows;
     a.v3 = a.v2 + kRows;
+    a.P = a.v3 + kRows;
     return a;
   }
 };
 
+// ---- Dense + LayerNorm with the statistics in the dense epilogue ("Option A") -------------
+// A 256-wide dense layer followed by its Flax LayerNorm (eps 1e-6, fast variance) [+ ReLU / residual ReLU]: each
+// wave sums its 32 output columns of every row into (sum, sum of squares) partials right in the MFMA epilogue (lane
+// (r, g) holds 4 consecutive columns of row r per tile: its 8 values in tile / column order, then the 4 g-lanes of
+// the row pairwise over the permlane network), one barrier publishes the 8 waves' partials, and every lane
+// normalises its own accumulator registers and stores the layer output once.  This replaces dense16's store, the
+// barrier, ln16's row pass (reload, 32-lane reductions, store) and its barrier -- the row|row idle bucket of the
+// search's timeline (profiles/r4_timeline.log).  The statistics' summation order differs from ln16's (a fixed
+// order again), so every kernel built on these helpers -- search, root and recurrent alike -- rounds the same.
+// MUZ_LN_EPILOGUE=0 builds the dense16 + ln16 pairs.  Caller synchronises before (A ready) and after (out ready).
+#ifndef MUZ_LN_EPILOGUE
+#define MUZ_LN_EPILOGUE 0   // 1: dense_ln16 (measured slower: profiles/r5_timeline.log)
+#endif
+template <int NT>
+struct LnE {   // this lane's LayerNorm scale / bias columns in the MFMA output layout
+  f32x4 sc[NT], sh[NT];
+};
+template <int NT>
+__device__ __forceinline__ LnE<NT> lne_load(const AS4 muz_ln& P) {
+  LnE<NT> p;
+  const int lane = tid() & 63, col0 = (int)(tid() >> 6) * NT * 16 + 4 * (lane >> 4);
+  const AS1 f32x4* sc = gp(reinterpret_cast<const f32x4*>(P.scale));
+  const AS1 f32x4* sh = gp(reinterpret_cast<const f32x4*>(P.bias));
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    p.sc[t] = sc[(col0 + 16 * t) >> 2];
+    p.sh[t] = sh[(col0 + 16 * t) >> 2];
+  }
+  return p;
+}
+
+template <int NT, int NTN, int MODE>
+__device__ __forceinline__ void dense_ln16(const AS4 muz_dense& L, int K, const float* A, int lda, float* out, int ldo,
+                                           Pf& pf, const AS4 muz_dense* Ln, int Kn, int Nn, const LnE<NT>& lp,
+                                           float* part) {
+  static_assert(NT * 16 * kWaves == LAT, "dense_ln16: the waves' columns cover exactly the 256 outputs");
+  const int lane = tid() & 63, wv = tid() >> 6;
+  const int KB = (K + 15) >> 4;
+  const int col0 = wv * NT * 16;
+  const int r = lane & 15, g = lane >> 4;
+  const AS1 f32x4* bias4 = gp(reinterpret_cast<const f32x4*>(L.b));
+  f32x4 acc[NT], b0[NT], b1[NT], bb[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    bb[t] = bias4[(col0 + t * 16 + 4 * g) >> 2];
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    b0[t] = pf.v0[t];
+    b1[t] = pf.v1[t];
+  }
+  ST(ST_DENTRY);
+  mfma_ring<NT>(wave_group(L, KB, NT), KB, A, lda, acc, b0, b1, false);
+  ST(ST_MFMA);
+  pf_issue<NTN>(pf, Ln, Kn, Nn);
+  float s = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    acc[t] += bb[t];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s += acc[t][q];
+      s2 = fmaf(acc[t][q], acc[t][q], s2);
+    }
+  }
+  {   // the row's 4 g-lanes: (g0 + g1) + (g2 + g3)
+    LoHi<float> p = swap16(s), p2 = swap16(s2);
+    s = p.lo + p.hi;
+    s2 = p2.lo + p2.hi;
+    p = swap32(s);
+    p2 = swap32(s2);
+    s = p.lo + p.hi;
+    s2 = p2.lo + p2.hi;
+  }
+  if (g == 0) {
+    part[(r * kWaves + wv) * 2] = s;
+    part[(r * kWaves + wv) * 2 + 1] = s2;
+  }
+  ST(ST_EPI);
+  SYNC();
+  float ps[kWaves], ps2[kWaves];
+#pragma unroll
+  for (int w = 0; w < kWaves; w += 2) {
+    const f32x4 v = lds4(part + (r * kWaves + w) * 2);
+    ps[w] = v[0];
+    ps2[w] = v[1];
+    ps[w + 1] = v[2];
+    ps2[w + 1] = v[3];
+  }
+#pragma unroll
+  for (int h = 1; h < kWaves; h *= 2)   // balanced tree over the waves in wave order
+#pragma unroll
+    for (int w = 0; w < kWaves; w += 2 * h) {
+      ps[w] += ps[w + h];
+      ps2[w] += ps2[w + h];
+    }
+  const float mean = ps[0] / (float)LAT;
+  const float mean2 = ps2[0] / (float)LAT;
+  const float var = fmaxf(0.f, fmaf(-mean, mean, mean2));
+  const float inv = ln_rstd(var + 1e-6f);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = col0 + t * 16 + 4 * g;
+    f32x4 y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = fmaf(acc[t][q] - mean, inv * lp.sc[t][q], lp.sh[t][q]);
+    if (MODE == LN_RELU) y = relu4(y);
+    if (MODE == LN_RESID_RELU) y = relu4(lds4(out + r * ldo + c) + y);
+    sts4(out + r * ldo + c, y);
+  }
+  ST(ST_ROW);
+}
+
 // ResBlock (muzero_deterministic_madn.py:12-24): X <- relu(X + LN1(D1(relu(LN0(D0(X))))))
-// pf: rb.d0 on entry, (Ln: Kn x Nn, NTN tiles) on exit.
+// pf: rb.d0 on entry, (Ln: Kn x Nn, NTN tiles) on exit.  `part`: the arena's LayerNorm partials (MUZ_LN_EPILOGUE).
 template <int NTN>
 __device__ __forceinline__ void resblock16(const AS4 muz_resblock& R, float* X, float* T, float* U, Pf& pf,
-                                           const AS4 muz_dense* Ln, int Kn, int Nn) {
+                                           const AS4 muz_dense* Ln, int Kn, int Nn, float* part) {
+  if constexpr (MUZ_LN_EPILOGUE != 0) {
+    const LnE<NT256> q0 = lne_load<NT256>(R.ln0);
+    dense_ln16<NT256, NT256, LN_RELU>(R.d0, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT, q0, part);
+    SYNC();
+    const LnE<NT256> q1 = lne_load<NT256>(R.ln1);
+    dense_ln16<NT256, NTN, LN_RESID_RELU>(R.d1, LAT, T, LD, X, LD, pf, Ln, Kn, Nn, q1, part);
+    SYNC();
+    return;
+  }
+  (void)part;
   const LnP<LAT> p0 = ln_load<LAT>(R.ln0);
   dense16<NT256, NT256>(R.d0, LAT, LAT, X, LD, T, LD, pf, &R.d1, LAT, LAT);
   SYNC();
@@ -834,8 +958,8 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
     ln16<LAT, LN_PLAIN>(lat, LD, a.X, LD, P.ln0);
     SYNC();
   }
-  resblock16<NT256>(P.rb[0], a.X, a.T, a.U, pf, &P.rb[1].d0, LAT, LAT);
-  resblock16<NT384>(P.rb[1], a.X, a.T, a.U, pf, &P.d03, LAT, 384);
+  resblock16<NT256>(P.rb[0], a.X, a.T, a.U, pf, &P.rb[1].d0, LAT, LAT, a.P);
+  resblock16<NT384>(P.rb[1], a.X, a.T, a.U, pf, &P.d03, LAT, 384, a.P);
   const LnP<LAT> p1 = ln_load<LAT>(P.ln1);
   const LnP<128> p3 = ln_load<128>(P.ln3);
   dense16<NT384, NT128>(P.d03, LAT, 384, a.X, LD, a.W, LDW, pf, &P.d1, LAT, 128);   // [policy Dense_0 | value Dense_3]
@@ -940,7 +1064,7 @@ __device__ __forceinline__ void repr16(const AS4 muz_repr_w& R, const float* __r
   __syncthreads();
 #pragma unroll 1
   for (int b = 0; b < 6; ++b)
-    resblock16<NT256>(R.rb[b], a.X, a.T, a.U, pf, b < 5 ? &R.rb[b + 1].d0 : &R.d4, LAT, LAT);
+    resblock16<NT256>(R.rb[b], a.X, a.T, a.U, pf, b < 5 ? &R.rb[b + 1].d0 : &R.d4, LAT, LAT, a.P);
   dense16<NT256, NTN>(R.d4, LAT, LAT, a.X, LD, a.T, LD, pf, Ln, Kn, Nn);
 }
 
@@ -1016,18 +1140,27 @@ __device__ __forceinline__ void dyn16(const AS4 muz_dyn_w& D, int A, const DynIn
     ST(ST_ROW);
   }
   SYNC();
-  const LnP<LAT> p1 = ln_load<LAT>(D.ln1);
-  dense16<NT256, NT256>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT);
-  SYNC();
-  ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, p1);
-  SYNC();
-  const LnP<LAT> p2 = ln_load<LAT>(D.ln2);
-  dense16<NT256, NT256>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT);
-  SYNC();
-  ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, p2);
-  SYNC();
-  resblock16<NT256>(D.rb[0], a.X, a.T, a.U, pf, &D.rb[1].d0, LAT, LAT);
-  resblock16<NT256>(D.rb[1], a.X, a.T, a.U, pf, &D.d5, LAT, LAT);
+  if constexpr (MUZ_LN_EPILOGUE != 0) {
+    const LnE<NT256> q1 = lne_load<NT256>(D.ln1);
+    dense_ln16<NT256, NT256, LN_RELU>(D.d3, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT, q1, a.P);
+    SYNC();
+    const LnE<NT256> q2 = lne_load<NT256>(D.ln2);
+    dense_ln16<NT256, NT256, LN_RELU>(D.d4, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT, q2, a.P);
+    SYNC();
+  } else {
+    const LnP<LAT> p1 = ln_load<LAT>(D.ln1);
+    dense16<NT256, NT256>(D.d3, LAT, LAT, a.X, LD, a.T, LD, pf, &D.d4, LAT, LAT);
+    SYNC();
+    ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, p1);
+    SYNC();
+    const LnP<LAT> p2 = ln_load<LAT>(D.ln2);
+    dense16<NT256, NT256>(D.d4, LAT, LAT, a.T, LD, a.X, LD, pf, &D.rb[0].d0, LAT, LAT);
+    SYNC();
+    ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, p2);
+    SYNC();
+  }
+  resblock16<NT256>(D.rb[0], a.X, a.T, a.U, pf, &D.rb[1].d0, LAT, LAT, a.P);
+  resblock16<NT256>(D.rb[1], a.X, a.T, a.U, pf, &D.d5, LAT, LAT, a.P);
   if constexpr (LATE_HEADS) {
     dense16<NT256, NTN>(D.d5, LAT, LAT, a.X, LD, a.T, LD, pf, Ln, Kn, Nn);
     const LnP<LAT> pl = ln_load<LAT>(*pln0);

@@ -84,18 +84,27 @@ __device__ __forceinline__ void film_trunk16(const TrunkW& W, const FilmIn& in, 
     ST(ST_ROW);
   }
   SYNC();
-  const LnP<LAT> p1 = ln_load<LAT>(*W.l1);
-  dense16<NT256, NT256>(*W.d1, LAT, LAT, a.X, LD, a.T, LD, pf, W.d2, LAT, LAT);
-  SYNC();
-  ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, p1);
-  SYNC();
-  const LnP<LAT> p2 = ln_load<LAT>(*W.l2);
-  dense16<NT256, NT256>(*W.d2, LAT, LAT, a.T, LD, a.X, LD, pf, &W.rb[0].d0, LAT, LAT);
-  SYNC();
-  ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, p2);
-  SYNC();
-  resblock16<NT256>(W.rb[0], a.X, a.T, a.U, pf, &W.rb[1].d0, LAT, LAT);
-  resblock16<NT256>(W.rb[1], a.X, a.T, a.U, pf, W.proj, LAT, LAT);
+  if constexpr (MUZ_LN_EPILOGUE != 0) {
+    const LnE<NT256> q1 = lne_load<NT256>(*W.l1);
+    dense_ln16<NT256, NT256, LN_RELU>(*W.d1, LAT, a.X, LD, a.T, LD, pf, W.d2, LAT, LAT, q1, a.P);
+    SYNC();
+    const LnE<NT256> q2 = lne_load<NT256>(*W.l2);
+    dense_ln16<NT256, NT256, LN_RELU>(*W.d2, LAT, a.T, LD, a.X, LD, pf, &W.rb[0].d0, LAT, LAT, q2, a.P);
+    SYNC();
+  } else {
+    const LnP<LAT> p1 = ln_load<LAT>(*W.l1);
+    dense16<NT256, NT256>(*W.d1, LAT, LAT, a.X, LD, a.T, LD, pf, W.d2, LAT, LAT);
+    SYNC();
+    ln16<LAT, LN_RELU>(a.T, LD, a.T, LD, p1);
+    SYNC();
+    const LnP<LAT> p2 = ln_load<LAT>(*W.l2);
+    dense16<NT256, NT256>(*W.d2, LAT, LAT, a.T, LD, a.X, LD, pf, &W.rb[0].d0, LAT, LAT);
+    SYNC();
+    ln16<LAT, LN_RELU>(a.X, LD, a.X, LD, p2);
+    SYNC();
+  }
+  resblock16<NT256>(W.rb[0], a.X, a.T, a.U, pf, &W.rb[1].d0, LAT, LAT, a.P);
+  resblock16<NT256>(W.rb[1], a.X, a.T, a.U, pf, W.proj, LAT, LAT, a.P);
   dense16<NT256, NTN>(*W.proj, LAT, LAT, a.X, LD, a.T, LD, pf, Ln, Kn, Nn);
   SYNC();
   skip_minmax16(a.T, a.L, LD);

@@ -182,6 +182,47 @@ def _ones(M, like):
     return v
 
 
+_ZEROS = {}
+
+
+def _zeros(N, like):
+    """A cached zero vector of length N (muz_ln_fwd's bias operand for a plain LayerNorm; filled on the eager
+    warm-up step, so a captured graph reuses it)."""
+    key = (N, like.device, like.dtype)
+    v = _ZEROS.get(key)
+    if v is None:
+        v = _ZEROS[key] = torch.zeros((N,), dtype=like.dtype, device=like.device)
+    return v
+
+
+class _LN(torch.autograd.Function):
+    """A plain Flax LayerNorm (eps 1e-6, fast variance) as one launch each way (muz_ln_fwd / muz_ln_bwd_rows),
+    its scale / bias gradients as column partials for the GradSink's grouped column sums (torch's layer_norm took
+    one launch forward and three backward).  For a LayerNorm applied once per loss (PredictionNetwork4's
+    LayerNorm_0 over all unrolled steps): a GradSink owns each parameter once."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta):
+        x = x.contiguous()
+        fwd = _ln_fwd(x, _zeros(x.shape[1], x), gamma, beta, None, LN_PLAIN)
+        ctx.save_for_backward(gamma, *fwd)
+        ctx.owners = (gamma, beta) if gamma.is_leaf and beta.is_leaf else None
+        return fwd[0]
+
+    @staticmethod
+    def backward(ctx, dout):
+        gamma, out, z, mean, rstd = ctx.saved_tensors
+        M, Nn = out.shape
+        scratch = torch.empty((_L.load().muz_ln_bwd_scratch_floats(M, Nn),), dtype=out.dtype, device=out.device)
+        dz, _ = _ln_bwd_rows(dout, (out, z, mean, rstd), gamma, LN_PLAIN, scratch)
+        sink = _sink()
+        if sink is not None and ctx.owners is not None:
+            sink.ln_colsum(scratch, Nn, ctx.owners[0], ctx.owners[1])
+            return dz, None, None
+        dgamma, dbeta, _ = _ln_colsum(scratch, Nn)
+        return dz, dgamma, dbeta
+
+
 class _Dense(torch.autograd.Function):
     """x @ W + b whose bias gradient is a BLAS GEMV (dy^T @ 1) instead of torch's column-sum reduction
     (~12 us per call at the learner's 1280-1408 rows, against ~5 us); with a GradSink active both parameter
@@ -214,6 +255,62 @@ HEAD_PARAMS = ("prediction/Dense_2/kernel", "prediction/Dense_2/bias", "predicti
                "dynamics/Dense_6/kernel", "dynamics/Dense_6/bias", "dynamics/reward_head/kernel",
                "dynamics/reward_head/bias", "dynamics/Dense_7/kernel", "dynamics/Dense_7/bias",
                "dynamics/discount_head/kernel", "dynamics/discount_head/bias")
+
+
+FUSED_FILM_EMBED = True   # False: the FiLM sub-graph as one-hot + library GEMMs + torch ops (A/B, test reference)
+FUSED_LN_ONCE = True      # False: Pred4's LayerNorm_0 as torch layer_norm (A/B, test reference)
+_FILM_PARAMS = ("Dense_0/kernel", "Dense_0/bias", "Dense_1/kernel", "Dense_1/bias", "Dense_2/kernel", "Dense_2/bias")
+
+
+class _Film(torch.autograd.Function):
+    """DynamicsNetwork4's action-only FiLM sub-graph for all unrolled rows as one launch each way
+    (csrc/learner_film.hip, muz_film_fwd / _bwd; muzero_deterministic_madn.py:404-418): -> (one_hot [M, A],
+    scale [M, 256], shift [M, 256]).  The one-hot product is a row gather (exact); the backward forms d e with one
+    launch and records e^T dscale, e^T dshift, one_hot^T de and the bias column sums into the active GradSink (or
+    forms them here)."""
+
+    @staticmethod
+    def forward(ctx, action, W0, b0, W1, b1, W2, b2):
+        a = action.reshape(-1).to(torch.int32).contiguous()
+        M, A = a.numel(), W0.shape[0]
+        dev, dt = W0.device, W0.dtype
+        oh = torch.empty((M, A), dtype=dt, device=dev)
+        e = torch.empty((M, 64), dtype=dt, device=dev)
+        scale = torch.empty((M, 256), dtype=dt, device=dev)
+        shift = torch.empty((M, 256), dtype=dt, device=dev)
+        P = [t.contiguous() for t in (W0, b0, W1, b1, W2, b2)]
+        scale1 = torch.empty_like(scale)
+        _L.check(_L.load().muz_film_fwd(_L.ptr(a), M, A, *(_L.ptr(t) for t in P), _L.ptr(oh), _L.ptr(e),
+                                        _L.ptr(scale), _L.ptr(shift), _L.ptr(scale1), _L.stream_ptr()), "muz_film_fwd")
+        scale._muz_scale1 = scale1             # 1 + scale, bit-identical to the chain's own (fp32 add)
+        ctx.save_for_backward(oh, e, P[2], P[4])
+        ctx.owners = (W0, b0, W1, b1, W2, b2) if all(t.is_leaf for t in (W0, b0, W1, b1, W2, b2)) else None
+        ctx.mark_non_differentiable(oh)
+        ctx.set_materialize_grads(False)       # (no zero-filled gradient for the one-hot output)
+        return oh, scale, shift
+
+    @staticmethod
+    def backward(ctx, doh, dscale, dshift):
+        oh, e, W1, W2 = ctx.saved_tensors
+        M = e.shape[0]
+        dscale = torch.zeros_like(e[:, :1].expand(M, 256)) if dscale is None else dscale.reshape(M, 256).contiguous()
+        dshift = torch.zeros_like(dscale) if dshift is None else dshift.reshape(M, 256).contiguous()
+        de = torch.empty_like(e)
+        _L.check(_L.load().muz_film_bwd(_L.ptr(dscale), _L.ptr(dshift), _L.ptr(e), _L.ptr(W1), _L.ptr(W2), M,
+                                        _L.ptr(de), _L.stream_ptr()), "muz_film_bwd")
+        sink = _sink()
+        if sink is not None and ctx.owners is not None:
+            W0, b0, W1p, b1, W2p, b2 = ctx.owners
+            sink.wgrad(oh, de, W0)
+            sink.colsum(de, b0)
+            sink.wgrad(e, dscale, W1p)
+            sink.colsum(dscale, b1)
+            sink.wgrad(e, dshift, W2p)
+            sink.colsum(dshift, b2)
+            return (None,) * 7
+        ones = _ones(M, e)
+        return (None, oh.t() @ de, torch.mv(de.t(), ones), e.t() @ dscale, torch.mv(dscale.t(), ones),
+                e.t() @ dshift, torch.mv(dshift.t(), ones))
 
 
 class _OutHeads(torch.autograd.Function):
@@ -607,13 +704,26 @@ class _transposed:
         return False
 
 
+_UNIT = {}
+
+
+def _unit_grad(like):
+    """A cached scalar 1 (filled on the eager warm-up step): the learner's root gradient, so _LossHeads can hand its
+    saved output gradients on without a scaling launch and autograd fills no ones tensor."""
+    key = (like.device, like.dtype)
+    v = _UNIT.get(key)
+    if v is None:
+        v = _UNIT[key] = torch.ones((), dtype=like.dtype, device=like.device)
+    return v
+
+
 def _backward(loss, sink):
     """loss.backward() with the parameter gradients formed by `sink`'s grouped launches (None: by autograd)."""
     if sink is None:
-        loss.backward()
+        loss.backward(_unit_grad(loss))
         return
     with sink:
-        loss.backward()
+        loss.backward(_unit_grad(loss))
     sink.flush()
 
 
@@ -703,7 +813,12 @@ class _TrunkChain(torch.autograd.Function):
         qs = torch.empty((T, B, Nn), dtype=dt, device=dev)                  # min-max inputs and their extrema
         lohi = torch.empty((T, B, 2), dtype=dt, device=dev)
         idx = torch.empty((T, B, 2), dtype=torch.int32, device=dev)
-        scale1 = 1.0 + scale
+        src = scale if scale._base is None else scale._base     # (_Film's output, or the view the loss passes)
+        scale1 = getattr(src, "_muz_scale1", None)
+        if scale1 is None or scale1.numel() != scale.numel() or src.data_ptr() != scale.data_ptr():
+            scale1 = 1.0 + scale
+        else:
+            scale1 = scale1.view(scale.shape)
         lib = _L.load()
         st = []
         slot, seen = _slots(apps, len(P) // _NP)
@@ -972,6 +1087,13 @@ class MuZeroNets:
         # ~1e-7 relative on these activations (tests/test_learner.py holds the forward to 1e-5)
         return F.layer_norm(x, (x.shape[-1],), self.p[f"{name}/scale"], self.p[f"{name}/bias"], EPS_LN)
 
+    def _ln_once(self, name, x):
+        """_ln for a LayerNorm applied once per loss: one launch each way (_LN) on the GPU."""
+        g, b = self.p[f"{name}/scale"], self.p[f"{name}/bias"]
+        if FUSED_LN_ONCE and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] in (32, 64, 128, 256):
+            return _LN.apply(x, g, b)
+        return self._ln(name, x)
+
     def _dense_ln(self, dense, ln, x, mode=LN_RELU, res=None, W=None):
         """act(LayerNorm(Dense(x))) (mode: LN_RELU, LN_RESID_RELU = relu(res + .), LN_PLAIN).  On the GPU the
         fused epilogue of csrc/learner_ln.hip; on the CPU (the host tests) the same layers as torch ops."""
@@ -1055,6 +1177,10 @@ class MuZeroNets:
         """The action-only FiLM sub-graph of DynamicsNetwork4 (one_hot -> Dense_0 -> Dense_1 | Dense_2); it
         does not depend on the latent, so the learner evaluates it for all unroll steps in one batch."""
         d = "dynamics"
+        W0 = self.p[f"{d}/Dense_0/kernel"]
+        if FUSED_FILM_EMBED and W0.is_cuda and W0.dtype == torch.float32 and W0.shape[1] == 64 and \
+                self.p[f"{d}/Dense_1/kernel"].shape == (64, 256):
+            return _Film.apply(action, *(self.p[f"{d}/{n}"] for n in _FILM_PARAMS))
         oh = (action.long()[:, None] == torch.arange(self.A, device=action.device)[None, :]).to(
             self.p[f"{d}/Dense_0/bias"].dtype)
         e = F.relu(self._dense(f"{d}/Dense_0", oh))
@@ -1087,7 +1213,7 @@ class MuZeroNets:
     def prediction_hidden(self, latent):
         """PredictionNetwork4 up to its heads: (policy hidden after LayerNorm_2, value hidden after LayerNorm_3)."""
         p = "prediction"
-        x = self._ln(f"{p}/LayerNorm_0", latent)
+        x = self._ln_once(f"{p}/LayerNorm_0", latent)
         x = self._rbs(f"{p}/ResBlock_", 2, x)
         pol = self._dense_ln(f"{p}/Dense_0", f"{p}/LayerNorm_1", x)
         pol = self._dense_ln(f"{p}/Dense_1", f"{p}/LayerNorm_2", pol)
@@ -1095,7 +1221,7 @@ class MuZeroNets:
 
     def prediction(self, latent):
         p = "prediction"
-        x = self._ln(f"{p}/LayerNorm_0", latent)
+        x = self._ln_once(f"{p}/LayerNorm_0", latent)
         x = self._rbs(f"{p}/ResBlock_", 2, x)
         pol = self._dense_ln(f"{p}/Dense_0", f"{p}/LayerNorm_1", x)
         pol = self._dense_ln(f"{p}/Dense_1", f"{p}/LayerNorm_2", pol)
@@ -1231,10 +1357,17 @@ class _LossHeads(torch.autograd.Function):
         ctx.d = (dlogits, dvalue, *dts)
         ctx.present = tuple(t is not None for t in (t0, t1, t2))
         ctx.mark_non_differentiable(parts)
+        ctx.set_materialize_grads(False)       # (no zero-filled gradient for `parts`)
         return total, parts
 
     @staticmethod
     def backward(ctx, g_total, g_parts):
+        if g_total is None:
+            return (None,) * 6
+        if g_total.data_ptr() == _unit_grad(g_total).data_ptr():
+            # the learner's own backward (_backward: loss.backward(_unit_grad)): the saved gradients are the answer
+            it = iter(ctx.d[2:])
+            return (ctx.d[0], ctx.d[1], *(next(it) if p else None for p in ctx.present), None)
         # out of place: the saved output gradients stay intact for a second backward (retain_graph, gradcheck)
         d = torch._foreach_mul(list(ctx.d), g_total)
         it = iter(d[2:])

@@ -362,6 +362,9 @@ SIGNATURES = {
     "muz_ln_colsum": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp, vp]),
     "muz_ln_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
                                   vp, vp, vp, vp]),
+    "muz_film_fwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                    vp]),
+    "muz_film_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp]),
     "muz_ln_film_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp]),
     "muz_ln_film_bwd_rows": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
                                             vp]),

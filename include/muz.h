@@ -697,6 +697,17 @@ int muz_ln_colsum(const float* scratch, int64_t nblk, int32_t N, float* dgamma, 
 int muz_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
                const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
                float* dgamma, float* dbeta, float* dbias, void* stream);
+/* DynamicsNetwork4's action-only FiLM sub-graph over M learner rows (muzero_deterministic_madn.py:404-418; replaces
+ * the reference's one_hot -> Dense_0 -> relu -> Dense_1 | Dense_2 of each unroll step, train_with_reward.py:98-105):
+ * e = relu(b0 + W0[action]) ([M][64]; action outside [0, A) -> the all-zero one-hot row), scale = e W1 + b1,
+ * shift = e W2 + b2 ([M][256]), optional scale1 = 1 + scale and optional float one-hot rows [M][A].  W0 [A][64],
+ * W1 / W2 [64][256], row-major.  Backward: de = (dscale W1^T + dshift W2^T) * [e > 0] ([M][64]); the weight and
+ * bias gradients are the caller's (e^T dscale, e^T dshift, one_hot^T de, column sums). */
+int muz_film_fwd(const int32_t* action, int32_t M, int32_t A, const float* W0, const float* b0, const float* W1,
+                 const float* b1, const float* W2, const float* b2, float* onehot, float* e, float* scale,
+                 float* shift, float* scale1, void* stream);
+int muz_film_bwd(const float* dscale, const float* dshift, const float* e, const float* W1, const float* W2,
+                 int32_t M, float* de, void* stream);
 /* The FiLM input of a dynamics trunk (muzero_deterministic_madn.py:421-427; learner._TrunkChain): out = LayerNorm(x)
  * (Flax, eps 1e-6, no bias), film = shift + out * scale1 (scale1 = 1 + FiLM scale), saving z / mean / rstd like
  * muz_ln_fwd; and its backward half from d(film): dscale = d(film) * out and the LayerNorm row backward of

@@ -457,3 +457,76 @@ def test_fused_output_heads_match_library_form(cuda):
             assert worst < 1e-5, (grouped, graph, worst)
     finally:
         L.FUSED_HEADS = old
+
+
+@pytest.mark.parametrize("M,A", [(1280, 24), (1283, 806), (5, 24)])
+def test_film_kernels_match_float64(cuda, M, A):
+    """muz_film_fwd / muz_film_bwd (learner._Film: DynamicsNetwork4's one_hot -> Dense_0 -> relu -> Dense_1 | Dense_2
+    for all unrolled rows) against float64 torch: the one-hot rows exact (actions outside [0, A) give the all-zero
+    row), e = relu(b0 + W0[a]) bit-identical to the fp32 one-hot product, scale / shift / d e within 1e-5 relative,
+    and the six parameter gradients of the autograd node against float64 autograd.  Ragged M (not a multiple of 16)
+    and the DOG width A = 806."""
+    from exploring_muzero_on_dog_amd import learner as L
+    g = torch.Generator(device="cuda").manual_seed(M + A)
+    act = torch.randint(-1, A + 1, (M,), generator=g, device="cuda")
+    P = [torch.randn(s, generator=g, device="cuda") * f for s, f in
+         (((A, 64), 0.3), ((64,), 0.1), ((64, 256), 0.2), ((256,), 0.1), ((64, 256), 0.2), ((256,), 0.1))]
+    P = [p.requires_grad_(True) for p in P]
+    oh, scale, shift = L._Film.apply(act, *P)
+    P64 = [p.detach().double().requires_grad_(True) for p in P]
+    ok = (act >= 0) & (act < A)
+    oh64 = torch.zeros((M, A), dtype=torch.float64, device="cuda")
+    oh64[ok, act[ok]] = 1.0
+    e64 = torch.relu(oh64 @ P64[0] + P64[1])
+    s64, t64 = e64 @ P64[2] + P64[3], e64 @ P64[4] + P64[5]
+    assert torch.equal(oh, oh64.float())
+    W0, b0 = P[0].detach(), P[1].detach()
+    e32 = torch.relu(torch.where(ok[:, None], W0[act.clamp(0, A - 1)] + b0, b0.expand(M, 64)))
+    lib, Lb = L._L.load(), L._L
+    e = torch.empty((M, 64), device="cuda")
+    scr = [torch.empty((M, 256), device="cuda") for _ in range(3)]
+    a32 = act.to(torch.int32)
+    Lb.check(lib.muz_film_fwd(Lb.ptr(a32), M, A, *(Lb.ptr(q.detach()) for q in P), None, Lb.ptr(e), Lb.ptr(scr[0]),
+                              Lb.ptr(scr[1]), Lb.ptr(scr[2]), Lb.stream_ptr()), "muz_film_fwd")
+    assert torch.equal(e, e32)
+    assert torch.equal(scr[2], 1.0 + scr[0]) and torch.equal(scr[0], scale.detach())
+    for a, b in ((scale, s64), (shift, t64)):
+        assert float((a.double() - b).norm() / b.norm()) < 1e-6
+    ds, dt = (torch.randn((M, 256), generator=g, device="cuda") for _ in range(2))
+    torch.autograd.backward((scale, shift), (ds, dt))
+    torch.autograd.backward((s64, t64), (ds.double(), dt.double()))
+    for p, q in zip(P, P64):
+        err = float((p.grad.double() - q.grad).norm() / max(float(q.grad.norm()), 1e-30))
+        assert err < 1e-5, err
+
+
+def test_fused_film_and_layernorm_match_library_form(cuda):
+    """learner.FUSED_FILM_EMBED (_Film) and FUSED_LN_ONCE (_LN for PredictionNetwork4's LayerNorm_0) against the
+    torch / library form of the same sub-graphs in a whole det learner step: loss within 1e-6 relative, every
+    parameter gradient within 1e-5 relative, with the grouped and the per-parameter gradient paths."""
+    from exploring_muzero_on_dog_amd import detmadn as E
+    from exploring_muzero_on_dog_amd import game_agent as GA
+    from exploring_muzero_on_dog_amd import learner as L
+    from exploring_muzero_on_dog_amd import nets as N
+    from exploring_muzero_on_dog_amd import replay as R
+    from oracle import nets as ON
+    C = E.num_channels(4)
+    params = ON.init_params(C, seed=15, randomize_affine=True)
+    eng = GA.SelfPlayEngine(N.DeviceNet(params, C), 32, num_players=4, max_steps=120, num_simulations=4, max_depth=4)
+    ring = R.VectorizedReplayBuffer(512, 48, 5, 10, obs_shape=(C, 56), max_episode_length=120,
+                                    rng=np.random.RandomState(3))
+    ring.save_games_from_buffers(eng.play_stream(40, seed=3, temperature=1.0))
+    batch = ring.sample_batch()
+    old = (L.FUSED_FILM_EMBED, L.FUSED_LN_ONCE)
+    try:
+        for grouped in (True, False):
+            L.FUSED_FILM_EMBED = L.FUSED_LN_ONCE = True
+            la, ga = _grads(L.Learner, params, C, batch, grouped)
+            L.FUSED_FILM_EMBED = L.FUSED_LN_ONCE = False
+            lb, gb = _grads(L.Learner, params, C, batch, grouped)
+            assert abs(la - lb) <= 1e-6 * abs(lb), (grouped, la, lb)
+            worst = max(float((ga[k] - gb[k]).norm()) / max(float(gb[k].norm()), 1e-20) for k in ga)
+            print(f"fused film + ln grouped={grouped}: loss {la:.7f} vs {lb:.7f}, worst grad rel {worst:.2e}")
+            assert worst < 1e-5, (grouped, worst)
+    finally:
+        L.FUSED_FILM_EMBED, L.FUSED_LN_ONCE = old
