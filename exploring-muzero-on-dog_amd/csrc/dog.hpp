@@ -293,4 +293,239 @@ __device__ __forceinline__ int dog_base_card(int i) {
   return 4;
 }
 
+// ---- k_dog_play's legality checks, lean form (MUZ_DOG_LEAN_CHECKS) ------------------------------------------------
+// The same predicates as dog_val_swap / dog_val7 / dog_val_normal / dog_val_neg (dog.py:350-615), with everything
+// that depends only on the mover -- its pins, target, goal cells, the seats' start cells, which starts are occupied
+// by their owners, the goal-cell occupancy -- gathered once per check phase into DogCtx in LDS instead of being
+// recomputed inside every check through select chains over the kernarg tables and runtime-P modulos.  Seat geometry
+// facts used (host_consts.hpp): goal[p][g] = goal[p][0] + g for p < P; starts are distinct.  (Held in registers,
+// built by every wave, it cost 224 SGPR spills and made the phase slower than the select chains it replaced.)
+struct DogCtx {
+  int P, cp, tgt, g0, start_cp;
+  bool circ, sb, jump, friendly;
+  int mt;
+  int start[4];          // seat start cells (p >= P: the host's 0)
+  int cur[4];            // the mover's pins
+  int nsb_start[4];      // dog_val7 / dog_val_normal: start cell of the seat after the pin's section
+  unsigned posbits;      // bit q: q < P and board[start[q]] == q (pos_on_start)
+  unsigned gocc;         // bit g: board[goal[cp][g]] == cp
+  unsigned ingbits;      // bit k: pin k in the mover's goal
+  unsigned long long goal_cells;   // bit c: c is a goal cell of some seat q < P
+  // per-launch copies of the rule constants the per-turn build reads (LDS instead of dependent kernarg loads)
+  bool teams;
+  int goal0[4];          // goal[q][0] (q >= P: unused)
+  int target[4];
+};
+
+// dog_ctx in LDS, in two parts: the rule constants once per launch (dog_ctx_static, one lane), and the mover's
+// facts once per turn by one full wave (dog_ctx_turn: lane q computes seat / pin / goal-cell q's facts, the bit sets
+// are ballots) reading only LDS -- a few dependent LDS round trips instead of one lane's serial chain of kernarg and
+// LDS loads (measured ~4.5k cycles per turn with tid 0 building all of dog_ctx, ~2.3k with the wave on kernarg).
+__device__ __forceinline__ void dog_ctx_static(const DetConsts& c, DogCtx* out) {
+  const uint32_t F = c.flags;
+  out->P = c.P;
+  out->circ = has(F, R_CIRCULAR);
+  out->sb = has(F, R_START_BLOCK);
+  out->jump = has(F, R_JUMP_GOAL);
+  out->friendly = has(F, R_FRIENDLY);
+  out->teams = has(F, R_TEAMS);
+  out->mt = has(F, R_MUST_TRAVERSE) ? 1 : 0;
+  unsigned long long gc = 0ull;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    out->start[p] = c.start[p];
+    out->goal0[p] = c.goal[p][0];
+    out->target[p] = c.target[p];
+    if (p < c.P) gc |= 0xFull << c.goal[p][0];
+  }
+  out->goal_cells = gc;
+}
+
+// dog_sub (dog.hpp) on the LDS constants: the teammate moves for a seat whose pins are all home
+__device__ __forceinline__ int dog_sub_lean(const DogCtx& x, const DogG& s) {
+  const int p = s.cp;
+  if (!x.teams || p >= x.P) return p;
+  const int g = x.goal0[p];
+  const bool done = s.board[g] >= 0 && s.board[g + 1] >= 0 && s.board[g + 2] >= 0 && s.board[g + 3] >= 0;
+  return done ? (p + 2) % 4 : p;
+}
+
+__device__ __forceinline__ void dog_ctx_turn(const DogG& s, int lane, DogCtx* out) {
+  const DogCtx& x = *out;
+  const int P = x.P;
+  const int cp = dog_sub_lean(x, s);
+  const int q = lane & 3;
+  const int start_q = x.start[q];
+  const int g0 = cp < P ? x.goal0[cp] : kTrack;
+  const int cur = dpin(s, cp, q);
+  const bool pos_q = lane < 4 && q < P && s.board[start_q] == q;
+  const bool occ_g = lane < 4 && s.board[g0 + q] == cp;
+  const bool ing_k = lane < 4 && (unsigned)(cur - g0) < 4u;
+  const unsigned posbits = (unsigned)__ballot(pos_q) & 0xFu;
+  const unsigned gocc = (unsigned)__ballot(occ_g) & 0xFu;
+  const unsigned ingbits = (unsigned)__ballot(ing_k) & 0xFu;
+  const int nsb = x.start[mod_small(fdiv(cur, kDist) + 1, P)];
+  const int tgt = x.target[cp], start_cp = x.start[cp];
+  __builtin_amdgcn_wave_barrier();   // every lane has read the static part before lane 0 writes the turn part
+  if (lane < 4) {
+    out->cur[q] = cur;
+    out->nsb_start[q] = nsb;
+  }
+  if (lane == 0) {
+    out->cp = cp;
+    out->tgt = tgt;
+    out->g0 = g0;
+    out->start_cp = start_cp;
+    out->posbits = posbits;
+    out->gocc = gocc;
+    out->ingbits = ingbits;
+  }
+}
+
+// val_swap (dog.py:317-348), pin / pos per lane
+__device__ __forceinline__ bool dog_val_swap_lean(const DogCtx& x, const DogG& s, int pin, int pos) {
+  const int b = s.board[pos];
+  bool ok = !(b == -1 || b == x.cp);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < x.P && x.start[q] == pos) ok = !((b == q) && x.sb) && (b != -1);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = x.cur[k];
+    if ((p < 0 ? p + kCells : p) == pos) ok = false;
+  }
+  if ((x.goal_cells >> pos) & 1ull) ok = false;
+  const int cur = x.cur[pin];
+  const bool dis = cur == -1 || (x.sb && cur == x.start_cp) || (unsigned)(cur - x.g0) < 4u;
+  return ok && !dis;
+}
+
+// val_action_7 (dog.py:393-481) for distribution d
+__device__ __forceinline__ bool dog_val7_lean(const DogCtx& x, const int (&d)[4]) {
+  int moved[4];
+  bool pos_cp = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    moved[k] = x.cur[k] + d[k];
+    pos_cp |= (x.cur[k] == x.start_cp) && (d[k] == 0);
+  }
+  unsigned occ = 0u;   // goal cells of the mover occupied after its in-goal pins moved
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int v = ((x.ingbits >> k) & 1u) ? moved[k] : x.cur[k];
+    if ((unsigned)(v - x.g0) < 4u) occ |= 1u << (v - x.g0);
+  }
+  const int g3 = x.g0 + 3;
+  bool all = true;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int cur = x.cur[k], mv = moved[k];
+    const int fitted = mv < 0 ? mv + kTrack : (mv >= kTrack ? mv - kTrack : mv);   // mv in [-1, 62]
+    int xx = mv - x.tgt - x.mt;
+    bool res = x.circ ? true : !((cur <= x.tgt) && ((mv > x.tgt + 4) || (xx == 0 && x.mt)));
+    const int nsa = (fitted >= 10) + (fitted >= 20) + (fitted >= 30);
+    const int nsa_j = nsa < x.P - 1 ? nsa : x.P - 1;
+    const bool trav = x.nsb_start[k] == x.start[nsa_j];
+    const bool pa = (nsa_j == x.cp) ? pos_cp : ((x.posbits >> nsa_j) & 1u) != 0u;
+    if (x.sb && trav) res = !pa && res;
+    if (x.mt && x.sb && trav && pa) xx = 0;
+    if (4 >= xx && xx > 0 && cur <= x.tgt) {
+      const bool A = x.circ && res;
+      const bool C = x.jump || (occ & ((1u << xx) - 1u)) == 0u;   // !occ[g] for 0 <= g < xx
+      res = A || C;
+    }
+    if ((x.ingbits >> k) & 1u) {
+      bool D = x.jump;
+      if (!D) {
+        D = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!(x.cur[j] >= kTrack)) continue;
+          const int so = (cur > x.cur[j]) - (cur < x.cur[j]);
+          const int sn = (mv > moved[j]) - (mv < moved[j]);
+          D &= so == sn;
+        }
+      }
+      res = (mv <= g3) && D;
+    }
+    const bool mover = cur == -1 ? mv == -1 : true;
+    all &= res && mover;
+  }
+  return all;
+}
+
+// val_action_normal_move (dog.py:483-566)
+__device__ __forceinline__ bool dog_val_normal_lean(const DogCtx& x, const DogG& s, int pin, int move) {
+  const int cur = x.cur[pin];
+  if (cur == -1) return (move == 1 || move == 11 || move == 13) && !((x.posbits >> x.cp) & 1u) && move > 0;
+  const int moved = cur + move;                                  // in [0, 68]
+  const int fitted = moved >= kTrack ? moved - kTrack : moved;
+  int xx = moved - x.tgt - x.mt;
+  bool res = (s.board[fitted] != x.cp) || x.friendly;
+  const int nsa = (fitted >= 10) + (fitted >= 20) + (fitted >= 30);
+  const int nsa_j = nsa < x.P - 1 ? nsa : x.P - 1;
+  const bool trav = x.nsb_start[pin] == x.start[nsa_j];
+  const bool pa = ((x.posbits >> nsa_j) & 1u) != 0u;
+  if (x.sb && trav) res = (!pa || cur == x.start_cp) && res;
+  if (x.mt && x.sb && trav && pa) xx = 0;
+  if (!x.circ && cur <= x.tgt && (xx > 4 || (xx == 0 && x.mt))) res = false;
+  if (4 >= xx && xx > 0 && cur <= x.tgt) {
+    const bool A = x.circ && res;
+    const bool B = ((x.gocc >> (xx - 1)) & 1u) == 0u;             // jidx(x - 1, 4) = x - 1 here
+    const bool C = x.jump || (x.gocc & ((1u << xx) - 1u)) == 0u;   // goal_free(cp, -1, x)
+    res = A || (B && C);
+  }
+  if ((unsigned)(cur - x.g0) < 4u) {
+    const int lo = cur - x.g0, hi = moved - x.g0 + 1;            // goal_free(cp, lo, hi): lo < g < hi
+    unsigned m = 0u;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (lo < g && g < hi) m |= 1u << g;
+    const bool D = x.jump || (x.gocc & m) == 0u;
+    res = (moved <= x.g0 + 3) && (s.board[moved < kCells ? moved : kCells - 1] != x.cp) && D;
+  }
+  return res && move > 0;
+}
+
+// val_neg_move (dog.py:568-614), move = -4
+__device__ __forceinline__ bool dog_val_neg_lean(const DogCtx& x, const DogG& s, int pin) {
+  const int cur = x.cur[pin];
+  if (cur == -1 || (unsigned)(cur - x.g0) < 4u) return false;
+  const int moved = cur - 4;                                     // cur in [0, 39]: moved in [-4, 35]
+  const int fitted = moved < 0 ? moved + kTrack : moved;
+  bool res = (s.board[fitted] != x.cp) || x.friendly;
+  const int nsb = (cur >= 10) + (cur >= 20) + (cur >= 30);
+  const int nsb_j = nsb < x.P - 1 ? nsb : x.P - 1;
+  const int nsa_j = mod_small((fitted >= 10) + (fitted >= 20) + (fitted >= 30) + 1, x.P);
+  const bool cond = x.start[nsb_j] == x.start[nsa_j];
+  if (x.sb && cond) res = (!((x.posbits >> nsa_j) & 1u) || cur == x.start_cp) && res;
+  return res && (x.circ || moved >= x.start_cp);
+}
+
+// dog_base_valid on the lean predicates (base action i in [0, 396)); d7: the 120 distributions packed one per u32
+// (byte k = pin k's share) in LDS, or null for the __constant__ table (a per-lane global load)
+__device__ __forceinline__ bool dog_base_valid_lean(const DogCtx& x, const DogG& s, int i, const uint32_t* d7) {
+  if (i < kDogSwaps) return dog_val_swap_lean(x, s, i / kCells, i % kCells);
+  if (i < kDogNormalBase) {
+    int d[4];
+    if (d7) {
+      const uint32_t w = d7[i - kDogSwaps];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = (int)((w >> (8 * k)) & 0xFFu);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = c_dists7[i - kDogSwaps][k];
+    }
+    return dog_val7_lean(x, d);
+  }
+  if (i < kDogNegBase) {
+    const int na = i - kDogNormalBase;
+    int mv = na % 12 + 1;
+    mv += mv >= 7 ? 1 : 0;
+    return dog_val_normal_lean(x, s, na / 12, mv);
+  }
+  return dog_val_neg_lean(x, s, i - kDogNegBase);
+}
+
 }  // namespace muz
+

@@ -725,9 +725,16 @@ __device__ __forceinline__ void dog_checks_block(const DetConsts& c, DogG& s, in
 // is the k-th legal action in action order (joker copies [0, 396) before real copies [396, 792)).
 // (thread t of an NTH-thread workgroup takes check threads t, t + NTH, ... of the 448; NTH a multiple of 64, so
 // each pass is whole waves and the ballots stay per check wave)
+#ifndef MUZ_DOG_D7_LDS
+#define MUZ_DOG_D7_LDS 1        // the hot-7 distribution table in LDS for the lean checks (0: __constant__ loads)
+#endif
+#ifndef MUZ_DOG_LEAN_CHECKS
+#define MUZ_DOG_LEAN_CHECKS 1   // k_dog_play's checks on dog.hpp's lean predicates (0: dog_base_valid, A/B)
+#endif
 #ifdef MUZ_DOG_STAMPS
 // diagnostic: per physical wave w, cycles of its check pass p (slot 8 + 4 p + w) and the number of passes that ran
-// a check (slot 16 + 4 p + w), lane 0 of every wave; summed in LDS over the launch, added to the global totals once
+// a check (slot 16 + 4 p + w), of the phase's setup before the passes (slot w: context build, its barrier, hoisted
+// loads) and of the wait at the closing barrier (slot 4 + w), lane 0 of every wave; summed in LDS over the launch, added to the global totals once
 // per workgroup at its end (per-pass global atomics from every workgroup serialised and distorted the turn)
 __device__ unsigned long long g_dog_wave_stamps[24];
 __device__ __forceinline__ unsigned long long* dog_wave_acc() {
@@ -736,10 +743,24 @@ __device__ __forceinline__ unsigned long long* dog_wave_acc() {
 }
 #endif
 template <int NTH = kDogBlockThreads>
-__device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int tid) {
+__device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int tid, const uint32_t* d7 = nullptr,
+                                                DogCtx* ctx = nullptr) {
   if (s.phase == 0) {
+#ifdef MUZ_DOG_STAMPS
+    const unsigned long long tp = __builtin_amdgcn_s_memtime();
+#endif
+#if MUZ_DOG_LEAN_CHECKS
+    if (tid < 64) dog_ctx_turn(s, tid, ctx);   // the mover's uniform facts, once per check phase, in LDS
+    __syncthreads();
+    const DogCtx& x = *ctx;
+    const int cp = x.cp;
+#else
     const int cp = dog_sub(c, s);
+#endif
     const bool hj = s.hands[cp][0] > 0;
+#ifdef MUZ_DOG_STAMPS
+    if ((tid & 63) == 0) dog_wave_acc()[tid >> 6] += __builtin_amdgcn_s_memtime() - tp;   // slots 0-3: setup
+#endif
     int pass = 0;
     for (int vt = tid; vt < kDogBlockThreads; vt += NTH, ++pass) {
 #ifdef MUZ_DOG_STAMPS
@@ -747,7 +768,11 @@ __device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int
 #endif
       const int i = dog_check_of(vt);
       const bool hr = i >= 0 && s.hands[cp][dog_base_card(i)] > 0;
+#if MUZ_DOG_LEAN_CHECKS
+      const bool v = i >= 0 && (hj || hr) && dog_base_valid_lean(x, s, i, d7);
+#else
       const bool v = i >= 0 && (hj || hr) && dog_base_valid(c, s, cp, i);
+#endif
       const unsigned long long bj = __ballot(v && hj), br = __ballot(v && hr);
       if ((vt & 63) == 0) {
         s.wj[vt >> 6] = bj;
@@ -761,6 +786,11 @@ __device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int
       }
 #endif
     }
+#ifdef MUZ_DOG_STAMPS
+    const unsigned long long te = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if ((tid & 63) == 0) dog_wave_acc()[4 + (tid >> 6)] += __builtin_amdgcn_s_memtime() - te;   // slots 4-7: wait
+#endif
   }
   __syncthreads();
 }
@@ -909,7 +939,7 @@ __device__ unsigned long long g_dog_stamps[8];
     if (tid == 0)                                                             \
       for (int i = 0; i < 8; ++i) atomicAdd(&g_dog_stamps[i], ds_acc[i]);    \
     __syncthreads();                                                          \
-    if (tid >= 8 && tid < 24) atomicAdd(&g_dog_wave_stamps[tid], dog_wave_acc()[tid]); \
+    if (tid < 24) atomicAdd(&g_dog_wave_stamps[tid], dog_wave_acc()[tid]); \
   } while (0)
 #else
 #define DOG_STAMP_INIT() do {} while (0)
@@ -962,6 +992,24 @@ __global__ __launch_bounds__(kDogPlayThreads) __attribute__((amdgpu_waves_per_eu
     return;
   }
   dog_load<PlaySync>(A().c, A().st, g, s, tid);
+#if MUZ_DOG_LEAN_CHECKS && MUZ_DOG_D7_LDS
+  // the hot-7 distributions packed into LDS once per launch (the checks read them per lane every turn)
+  __shared__ uint32_t s_d7[kDogHot];
+  for (int i = tid; i < kDogHot; i += kDogPlayThreads)
+    s_d7[i] = (uint32_t)(uint8_t)c_dists7[i][0] | ((uint32_t)(uint8_t)c_dists7[i][1] << 8) |
+              ((uint32_t)(uint8_t)c_dists7[i][2] << 16) | ((uint32_t)(uint8_t)c_dists7[i][3] << 24);
+  __syncthreads();
+  const uint32_t* d7 = s_d7;
+#else
+  const uint32_t* d7 = nullptr;
+#endif
+#if MUZ_DOG_LEAN_CHECKS
+  __shared__ DogCtx s_ctx;
+  DogCtx* ctx = &s_ctx;
+  if (tid == 0) dog_ctx_static(A().c, ctx);   // ordered before the first turn's reads by dog_checks_play's barrier
+#else
+  DogCtx* ctx = nullptr;
+#endif
   const int nturns = A().nturns;
   int played = 0, finished = 0, a = -2, r = 0;
   DOG_STAMP_INIT();
@@ -980,7 +1028,7 @@ __global__ __launch_bounds__(kDogPlayThreads) __attribute__((amdgpu_waves_per_eu
       dog_reset_lds<PlaySync>(c, s, P.seed, g, deal, tid);
     }
     DOG_STAMP(0);   // reset
-    dog_checks_play<kDogPlayThreads>(c, s, tid);
+    dog_checks_play<kDogPlayThreads>(c, s, tid, d7, ctx);
     DOG_STAMP(1);   // base checks (+ barrier)
     if (tid < 64) {
       // the turn's serial part (choice, lane 0's env_step) runs at raised wave priority: the CU's other
@@ -1322,7 +1370,7 @@ int muz_diag_dog_stamps(unsigned long long* host_out, int reset) {
   }
   return (int)e;
 }
-// per-wave check passes (dog_checks_play): host_out[24] (slots 0..7 unused)
+// per-wave check passes (dog_checks_play): host_out[24] (slot layout at g_dog_wave_stamps)
 int muz_diag_dog_wave_stamps(unsigned long long* host_out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_dog_wave_stamps), sizeof(unsigned long long) * 24);
   if (e != hipSuccess) return (int)e;

@@ -145,6 +145,110 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_update(AdamTable t, const
 
 static int64_t adam_chunks(int64_t numel) { return (numel + kAdamChunk - 1) / kAdamChunk; }
 
+// ---- one launch per pass: the tensor table in device memory (inside the caller's scratch) ----------------------
+// The kernel-argument table holds 80 tensors, so the det learner's 156 took two launches per pass; with the table in
+// the scratch buffer (uploaded by an eager call, read unchanged by a graph capture of the same step) each pass is one
+// launch.  Same per-chunk arithmetic and the same fixed reduction order as the kernels above (bit-identical).
+struct AdamDesc {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t numel;
+};
+
+__device__ __forceinline__ int adam_tensor_of_dev(const int* __restrict__ cstart, int n, int b) {
+  int lo = 0, hi = n - 1;   // largest ti with cstart[ti] <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (cstart[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kAdamThreads) void k_adam_sqnorm_t(const AdamDesc* __restrict__ desc,
+                                                                const int* __restrict__ cstart, int n,
+                                                                float* __restrict__ partial, double* __restrict__ count,
+                                                                double* __restrict__ stepbuf) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  const int ti = adam_tensor_of_dev(cstart, n, b);
+  const float* g = desc[ti].g;
+  const int64_t base = (int64_t)(b - cstart[ti]) * kAdamChunk;
+  const int64_t num = desc[ti].numel;
+  float s = 0.f;
+  if (g) {
+#pragma unroll
+    for (int k = 0; k < kAdamPerThread; ++k) {
+      const int64_t i = base + k * kAdamThreads + threadIdx.x;
+      if (i < num) {
+        const float x = g[i];
+        s += x * x;
+      }
+    }
+  }
+  s = adam_block_sum(s, red);
+  if (threadIdx.x == 0) {
+    partial[b] = s;
+    if (b == 0) {
+      const double c = *count;
+      *stepbuf = c;
+      *count = c + 1.0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kAdamThreads) void k_adam_update_t(const AdamDesc* __restrict__ desc,
+                                                                const int* __restrict__ cstart, int n,
+                                                                const float* __restrict__ partial,
+                                                                const double* __restrict__ stepbuf, AdamHyper h,
+                                                                float* __restrict__ gnorm_out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < h.nchunks; i += kAdamThreads) s += partial[i];
+  const float gnorm = sqrtf(adam_block_sum(s, red));
+  const bool trigger = gnorm < h.max_norm;
+  const float denom = trigger ? 1.f : gnorm;
+  const float mult = trigger ? 1.f : h.max_norm;
+  const double prev = *stepbuf;
+  double lr = h.lr0;
+  for (int j = 0; j < h.nb; ++j)
+    if (prev >= h.bound[j] * h.spi) lr *= h.factor[j];
+  const float lrf = (float)lr;
+  const float c1 = (float)(1.0 - pow(h.b1, prev + 1.0));
+  const float c2 = (float)(1.0 - pow(h.b2, prev + 1.0));
+  const float b1 = (float)h.b1, b2 = (float)h.b2;
+  const float a1 = (float)(1.0 - h.b1), a2 = (float)(1.0 - h.b2);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *gnorm_out = gnorm;
+
+  const int b = blockIdx.x;
+  const int ti = adam_tensor_of_dev(cstart, n, b);
+  const AdamDesc d = desc[ti];
+  const int64_t base = (int64_t)(b - cstart[ti]) * kAdamChunk;
+#pragma unroll 4
+  for (int k = 0; k < kAdamPerThread; ++k) {
+    const int64_t i = base + k * kAdamThreads + threadIdx.x;
+    if (i >= d.numel) break;
+    float gr = d.g ? d.g[i] : 0.f;
+    gr = gr / denom;
+    gr = gr * mult;
+    const float mu = d.m[i] * b1 + a1 * gr;
+    const float nu = d.v[i] * b2 + a2 * (gr * gr);
+    const float pv = d.p[i];
+    float u = (mu / c1) / (sqrtf(nu / c2) + h.eps);
+    u = u + h.wd * pv;
+    u = u * lrf;
+    d.m[i] = mu;
+    d.v[i] = nu;
+    d.p[i] = pv - u;
+  }
+}
+
+// scratch layout: [stepbuf f64][partials f32 x nchunks][pad to 16 B][AdamDesc x ntensors][cstart i32 x (ntensors + 1)]
+static size_t adam_table_offset(int64_t nchunks) { return ((size_t)(8 + 4 * nchunks) + 15) / 16 * 16; }
+static size_t adam_table_bytes(int ntensors) { return sizeof(AdamDesc) * ntensors + 4 * (size_t)(ntensors + 1); }
+
 }  // namespace muz
 
 using namespace muz;
@@ -158,7 +262,7 @@ int64_t muz_adamw_scratch_bytes(int32_t ntensors, const int64_t* numel) {
     if (numel[i] < 0) return -1;
     c += adam_chunks(numel[i]);
   }
-  return 8 + 4 * c;
+  return (int64_t)(adam_table_offset(c) + adam_table_bytes(ntensors));
 }
 
 int muz_adamw_step(float* const* params, const float* const* grads, float* const* mu, float* const* nu,
@@ -196,6 +300,48 @@ int muz_adamw_step(float* const* params, const float* const* grads, float* const
     t.p[t.n] = params[i], t.g[t.n] = grads[i], t.m[t.n] = mu[i], t.v[t.n] = nu[i];
     chunk += (int)adam_chunks(numel[i]);
     t.cstart[++t.n] = chunk - t.chunk0;
+  }
+  // one launch per pass with the table in the scratch: uploaded by an eager call; a graph capture reads the table an
+  // earlier eager call of the same step wrote (the host keeps the last upload per scratch buffer to check that)
+  {
+    std::vector<char> tab(adam_table_bytes(ntensors));
+    AdamDesc* dd = reinterpret_cast<AdamDesc*>(tab.data());
+    int* cs = reinterpret_cast<int*>(tab.data() + sizeof(AdamDesc) * ntensors);
+    int nz = 0, c = 0;
+    for (int i = 0; i < ntensors; ++i) {
+      if (!numel[i]) continue;
+      dd[nz] = AdamDesc{params[i], grads[i], mu[i], nu[i], numel[i]};
+      cs[nz++] = c;
+      c += (int)adam_chunks(numel[i]);
+    }
+    cs[nz] = c;
+    char* dev = (char*)scratch + adam_table_offset(total);
+    static std::vector<std::pair<void*, std::vector<char>>> uploaded;   // last table uploaded per scratch buffer
+    std::vector<char>* last = nullptr;
+    for (auto& u : uploaded)
+      if (u.first == scratch) last = &u.second;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    MUZ_HIP_RET(hipStreamIsCapturing(s, &cap));
+    bool ready = false;
+    if (cap == hipStreamCaptureStatusNone) {
+      if (!last) {
+        uploaded.emplace_back(scratch, std::vector<char>());
+        last = &uploaded.back().second;
+      }
+      *last = tab;
+      MUZ_HIP_RET(hipMemcpyAsync(dev, last->data(), tab.size(), hipMemcpyHostToDevice, s));
+      ready = true;
+    } else {
+      ready = last && *last == tab;   // captured: only if this exact table is already in the scratch
+    }
+    if (ready && nz > 0) {
+      const AdamDesc* ddev = reinterpret_cast<const AdamDesc*>(dev);
+      const int* cdev = reinterpret_cast<const int*>(dev + sizeof(AdamDesc) * ntensors);
+      k_adam_sqnorm_t<<<c, kAdamThreads, 0, s>>>(ddev, cdev, nz, partial, count, stepbuf);
+      if (int rc = muz_last_launch_error()) return rc;
+      k_adam_update_t<<<c, kAdamThreads, 0, s>>>(ddev, cdev, nz, partial, stepbuf, h, gnorm);
+      return muz_last_launch_error();
+    }
   }
   for (size_t k = 0; k < tabs.size(); ++k) {
     k_adam_sqnorm<<<tabs[k].cstart[tabs[k].n], kAdamThreads, 0, s>>>(tabs[k], partial, count, stepbuf);

@@ -80,10 +80,14 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
   if (n_dev) n = *n_dev;
   if ((int)blockIdx.x >= n) return;
   const AS4 muz_repr_w& R = *kernarg0<muz_repr_w>();   // == Rarg, read through the kernarg segment
-  __shared__ __attribute__((aligned(16))) float in0[58 * 6];
-  __shared__ __attribute__((aligned(16))) float c1in[66 * 32];
+  // LDS: pre + one buffer holding in0 | c1in until Conv_1 has read them, then c2in (34.8 KB: 4 workgroups per CU
+  // instead of 3 with separate buffers)
   __shared__ __attribute__((aligned(16))) float pre[kConvRowsPad * kPreLd];
-  __shared__ __attribute__((aligned(16))) float c2in[68 * 64];
+  __shared__ __attribute__((aligned(16))) float buf[68 * 64];
+  float* in0 = buf;                 // [58][6]
+  float* c1in = buf + 352;          // [66][32]
+  float* c2in = buf;                // [68][64]
+  static_assert(352 >= 58 * 6 && 352 + 66 * 32 <= 68 * 64, "conv LDS carve");
   const int g = blockIdx.x;
   const int tid = threadIdx.x;
   const float* o = obs + (size_t)g * C * 56;
@@ -92,7 +96,6 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
     in0[i] = (w >= 0 && w < 56) ? o[ch * 56 + w] : 0.f;
   }
   for (int i = tid; i < 66 * 32; i += 256) c1in[i] = 0.f;
-  for (int i = tid; i < 68 * 64; i += 256) c2in[i] = 0.f;
   __syncthreads();
   // Conv_0 (K = 3*6 = 18, N = 32) on VALU
   for (int i = tid; i < 56 * 32; i += 256) {
@@ -109,6 +112,8 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
   __syncthreads();
   conv_mfma<6>(R.conv1, c1in, 32, pre);     // K = 3*32 = 96
   __syncthreads();
+  // c2in now reuses in0 | c1in: zero its pad rows (0, 1 and 58..67; the LayerNorm writes rows 2..57)
+  for (int i = tid; i < 12 * 64; i += 256) c2in[(i < 128 ? 0 : 56 * 64) + i] = 0.f;
   ln_positions<64>(pre, c2in, 2, R.ln1);   // pad 2 rows for k=5
   __syncthreads();
   conv_mfma<20>(R.conv2, c2in, 64, pre);    // K = 5*64 = 320

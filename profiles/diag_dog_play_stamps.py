@@ -47,6 +47,9 @@ def main():
     print(f"B={B}: {tot / turns:.0f} cycles per game-turn (thread 0 of each game's workgroup)")
     for i, c in enumerate(CATS):
         print(f"{c:>24}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / turns:8.0f} cycles/turn")
+    for w in range(4):
+        print(f"  wave {w}: setup before the passes {wb[w] / turns:7.0f} cycles/turn, closing-barrier wait "
+              f"{wb[4 + w] / turns:7.0f} cycles/turn")
     print("check passes per physical wave (cycles per turn over all turns; cycles per pass that ran a check; share run):")
     for w in range(4):
         for p in range(2):
