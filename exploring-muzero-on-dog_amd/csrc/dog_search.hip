@@ -266,6 +266,7 @@ __device__ __forceinline__ void wtop2_row(float& v1, int& i1, float& v2) {
 // the compact loads.
 __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int node, int sub, float* ces) {
 #pragma clang fp contract(off)
+  st_count(13);   // (diagnostic builds: full node loads)
   float pm = -INFINITY, u1 = -INFINITY, u2 = -INFINITY;
   int sv = 0, mv = 0, ui = kDogA;
 #pragma unroll
@@ -315,7 +316,9 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
   mv = row_imax(mv);
   wtop2_row(u1, ui, u2);
   float es = ces[node];
+  ST(ST_OTHER);   // (diagnostic builds)
   if (es < 0.f) {   // (row-uniform)
+    st_count(12);   // (diagnostic builds: first walks)
     es = wsum([&](int j) { return wok(sub, j) ? exp_cr_w(nd.pr[sub + kRowLanes * j] - pm) : -0.0f; });
     if (sub == 0) ces[node] = es;
     // the kWTop largest priors in (value desc, index asc) order, one row argmax after another
@@ -344,6 +347,7 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
       pv = v;
       pi = i;
     }
+    ST(ST_FIRST);   // (diagnostic builds: first-walk normaliser + top-prior list)
   }
   unsigned vm = 0;
 #pragma unroll

@@ -65,7 +65,8 @@ __device__ __forceinline__ unsigned tid() { return threadIdx.x; }
 #endif
 // ---- diagnostic fine-grained stamps (make EXTRA=-DMUZ_STAMPS2); compiled out otherwise -------------
 enum { ST_MFMA = 0, ST_EPI = 1, ST_BAR = 2, ST_ROW = 3, ST_SEL = 4, ST_OTHER = 5, ST_TREE = 6, ST_PASS = 7, ST_DENTRY = 8,
-       ST_N = 12 };
+       ST_FIRST = 11,   // (k_dog_search: a node's first-walk normaliser + top-prior list; counts at 9, 10, 12)
+       ST_N = 14 };
 #ifdef MUZ_STAMPS2
 __device__ unsigned long long g_st2[ST_N];
 struct StampState {

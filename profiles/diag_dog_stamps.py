@@ -16,8 +16,16 @@ import torch  # noqa: E402
 from exploring_muzero_on_dog_amd import lib as L  # noqa: E402
 from exploring_muzero_on_dog_amd import muzero_dog as MD  # noqa: E402
 
-CATS = ["mfma-loops", "dense-epilogue", "barrier-wait", "row-ops", "select scores", "Q transform", "tree / backup",
-        "node loads + passes", "dense-entry"]
+CATS = {0: "mfma-loops", 1: "dense-epilogue", 2: "barrier-wait", 3: "row-ops", 4: "select scores", 5: "Q transform",
+        6: "tree / backup", 7: "node loads + passes", 8: "dense-entry", 11: "first-walk es + top"}
+
+
+def report(buf, wg_sims, header):
+    tot = sum(buf[i] for i in CATS)
+    print(f"{header}: {tot / wg_sims:.0f} cycles per workgroup-simulation")
+    for i, c in CATS.items():
+        print(f"{c:>20}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / wg_sims:9.0f} cycles/sim")
+    print(f"interior selections of thread 0's game: {buf[9]}, on the exact path: {buf[10]}, first walks: {buf[12]}, full loads: {buf[13]}")
 
 
 def games_per_wg(B):
@@ -43,19 +51,15 @@ def main():
     ws = MD.SearchWorkspace(B, S)
     MD.gumbel_muzero_policy(net, lg, v, e, words, S, D, 1.0, seed=1, workspace=ws)
     torch.cuda.synchronize()
-    buf = (ctypes.c_uint64 * 12)()
+    buf = (ctypes.c_uint64 * 14)()
     fn(buf, 1)
     reps = 2
     for r in range(reps):
         MD.gumbel_muzero_policy(net, lg, v, e, words, S, D, 1.0, seed=r, workspace=ws)
     torch.cuda.synchronize()
     fn(buf, 0)
-    tot = sum(buf[i] for i in range(len(CATS)))
     wg_sims = reps * ((B + games_per_wg(B) - 1) // games_per_wg(B)) * S
-    print(f"B={B} S={S} D={D}: {tot / wg_sims:.0f} cycles per workgroup-simulation")
-    for i, c in enumerate(CATS):
-        print(f"{c:>20}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / wg_sims:9.0f} cycles/sim")
-    print(f"interior selections of thread 0's game: {buf[9]}, on the exact path: {buf[10]}")
+    report(buf, wg_sims, f"B={B} S={S} D={D}")
 
 
 def selfplay(turns=6):
@@ -70,18 +74,14 @@ def selfplay(turns=6):
     sp = GA.DogSelfPlay(net, B, S, D, 1.0, seed=4)
     sp.play(2)
     torch.cuda.synchronize()
-    buf = (ctypes.c_uint64 * 12)()
+    buf = (ctypes.c_uint64 * 14)()
     fn(buf, 1)
     depth = []
     sp.play(turns)
     torch.cuda.synchronize()
     fn(buf, 0)
-    tot = sum(buf[i] for i in range(len(CATS)))
     wg_sims = turns * ((B + games_per_wg(B) - 1) // games_per_wg(B)) * S
-    print(f"DogSelfPlay B={B} S={S} D={D}, {turns} turns: {tot / wg_sims:.0f} cycles per workgroup-simulation")
-    for i, c in enumerate(CATS):
-        print(f"{c:>20}: {100.0 * buf[i] / tot:6.2f} %   {buf[i] / wg_sims:9.0f} cycles/sim")
-    print(f"interior selections of thread 0's game: {buf[9]}, on the exact path: {buf[10]}")
+    report(buf, wg_sims, f"DogSelfPlay B={B} S={S} D={D}, {turns} turns")
     words = sp.words.cpu().numpy().view(np.uint32)
     nleg = np.array([sum(bin(int(w)).count("1") for w in row) for row in words])
     print(f"legal actions per game: mean {nleg.mean():.1f}, max {nleg.max()}, phase-1 games {int(sp.env.phase.sum())}")
