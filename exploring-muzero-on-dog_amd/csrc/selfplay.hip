@@ -20,6 +20,9 @@ namespace muz {
 
 // lane kernels' workgroup size; 64 / 128 measured within noise of 256 (profiles/r1g_sp_block_ab.log)
 constexpr int kSpBlock = 256;
+#ifndef MUZ_SP_FUSED_HEAD
+#define MUZ_SP_FUSED_HEAD 1   // the turn head as one launch (k_sp_head); 0: refill / flags / compact / encode (A/B)
+#endif
 
 // Legal masks + flags of every lane, one game per kFlagLanes lanes (a lane per game would leave a 4096-game batch
 // on 16 of 256 CUs, its launch one lane's 24 serial legality checks): the workgroup copies its games' SoA rows into
@@ -231,6 +234,177 @@ __global__ __launch_bounds__(kScanThreads) void k_ss_refill(DetConsts c, muz_det
   if (t == kScanThreads - 1) next[0] = min(num_games, base + part[t]);
 }
 
+// ---- the turn head as one launch (MUZ_SP_FUSED_HEAD, default): refill + flags + compaction + encode ------------
+// The four launches above cost ~37 us per turn at 4096 lanes, most of it two single-workgroup scans and kernel
+// boundaries (profiles/r5s_kernel_stats.csv).  Here every workgroup (8 lanes) loads its rows once and takes its
+// share of the two lane-order counts the head needs -- refilled lanes' game numbers, searching games' slots -- with
+// one device atomic each.  The workgroups' order among themselves then decides which lane takes which new game
+// number and which slot a searching game gets, but no result: a game's search, records and noise depend on its
+// game number and its own step count only (key_game / key_turn), never on its lane or its slot, and the set of game
+// numbers handed out per turn is the same (tests/test_gpu_selfplay.py: stream == batch, oracle parity).  (Ordered
+// alternatives measured: a decoupled look-back over the 512 workgroups, 262 us serial / 69 us 64-wide -- each poll
+// an agent-scope load across XCDs.)
+// counts: this turn's [searching, active, -, arrivals]; the next turn's four (the other parity) are zeroed here.
+
+struct SpHead {
+  uint32_t* legal;
+  int32_t* flag;
+  int32_t* list;
+  int32_t* slot;
+  int32_t* counts;        // this turn's four counters (zeroed by the previous turn's head or the driver)
+  int32_t* counts_next;   // the next turn's four, zeroed here
+  uint32_t* legal_c;
+  float* obs;
+  int8_t* traj_obs;
+  int32_t* host_counts;   // the turn's pinned ledger slot (device-visible), or null
+};
+
+// STREAM: k_ss_refill's lane refill first (lane_game / next); otherwise lane g plays game g.
+template <bool STREAM>
+__global__ __launch_bounds__(kSpBlock) void k_sp_head(DetConsts c, muz_detmadn_soa st, int n, const int32_t* idx, int T,
+                                                      int32_t* lane_game, int32_t* next, int num_games, SpHead o) {
+  constexpr int G = kFlagLanes, NG = kSpBlock / G;
+  __shared__ int8_t sboard[NG][kCells];
+  __shared__ int8_t sstate[NG][kStateRow];
+  __shared__ __attribute__((aligned(16))) uint8_t senc[NG][kEncStride];
+  __shared__ int s_gn[NG], s_f[NG], s_pre, s_reset;
+  const int t = threadIdx.x, lg = t / G, a = t % G;
+  const int b = blockIdx.x, nb = gridDim.x;
+  const int g0 = b * NG, games = min(NG, n - g0), g = g0 + lg;
+  det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
+  if (t < NG) {
+    s_gn[t] = -1;
+    s_f[t] = 0;
+  }
+  if (t == 0) s_reset = 0;
+  if (b == 0 && t < 4) o.counts_next[t] = 0;
+  __syncthreads();
+  if constexpr (STREAM) {
+    // refill (k_ss_refill): every lane whose game ended takes the next unplayed game number (next[0] counts the
+    // numbers handed out, possibly past num_games: those lanes go idle)
+    if (t < games) {
+      const int gn = lane_game[g0 + t];
+      s_gn[t] = gn;
+      s_f[t] = gn >= 0 && (sstate[t][41] || idx[gn] >= T);
+    }
+    __syncthreads();
+    if (t == 0) {
+      int cnt = 0;
+      for (int i = 0; i < games; ++i) cnt += s_f[i];
+      int r = cnt ? atomicAdd(next, cnt) : 0;
+      for (int i = 0; i < games; ++i)
+        if (s_f[i]) {
+          s_gn[i] = r < num_games ? r : -1;
+          s_reset |= r < num_games;
+          ++r;
+        }
+    }
+    __syncthreads();
+    if (t < games && s_f[t]) lane_game[g0 + t] = s_gn[t];
+    if (s_reset) {   // det_reset_lane on the LDS rows of the refilled lanes (stored back below)
+      const bool fp = has(c.flags, R_FREE_PIN);
+      for (int i = t; i < NG * kCells; i += kSpBlock) {
+        const int gi = i / kCells, cell = i % kCells;
+        if (gi < games && s_f[gi] && s_gn[gi] >= 0) {
+          int v = -1;
+          for (int p = 0; p < c.P; ++p)
+            if (fp && cell == c.start[p]) v = p;
+          sboard[gi][cell] = (int8_t)v;
+        }
+      }
+      for (int i = t; i < NG * kStateRow; i += kSpBlock) {
+        const int gi = i / kStateRow, r = i % kStateRow;
+        if (gi < games && s_f[gi] && s_gn[gi] >= 0) {
+          int8_t v = sstate[gi][r];
+          if (r < 16) v = r < 4 * c.P ? (int8_t)((fp && (r & 3) == 0) ? c.start[r >> 2] : -1) : (int8_t)-1;
+          else if (r < 40) v = r - 16 < 6 * c.P ? (int8_t)4 : (int8_t)0;
+          else if (r == 40) v = (int8_t)c.starting_player;
+          else if (r == 41 || r == 42) v = 0;
+          sstate[gi][r] = v;
+        }
+      }
+    }
+    __syncthreads();
+    if (t < NG) s_f[t] = 0;
+    __syncthreads();
+  }
+  // flags (k_sp_flags_g): 1 = searches (a legal move), 2 = no move (no_step), 0 = idle
+  if (lg < games) {
+    const int gn = STREAM ? s_gn[lg] : g;
+    const bool idle = sstate[lg][41] || (STREAM && (gn < 0 || idx[gn] >= T));
+    uint32_t l = 0;
+    int f = 0;
+    if (!idle) {   // (uniform over the game's lanes)
+      l = det_legal_g<G>(c, LdsLane{sstate[lg], sstate[lg][40], 0, 0}, BoardView{sboard[lg], 1}, a, t);
+      f = l ? 1 : 2;
+    }
+    if (a == 0) {
+      o.legal[g] = l;
+      o.flag[g] = f;
+      s_f[lg] = f;
+    }
+  }
+  __syncthreads();
+  // compaction (k_sp_compact): slots of the searching games; counts = (searching, active); the last workgroup to
+  // arrive hands the totals to the host ledger
+  if (t == 0) {
+    int c1 = 0, c2 = 0;
+    for (int i = 0; i < games; ++i) {
+      c1 += s_f[i] == 1;
+      c2 += s_f[i] != 0;
+    }
+    s_pre = c1 ? atomicAdd(&o.counts[0], c1) : 0;
+    if (c2) atomicAdd(&o.counts[1], c2);
+    if (o.host_counts) {
+      __threadfence();
+      if (atomicAdd(&o.counts[3], 1) == nb - 1) {
+        __threadfence();
+        const int tot1 = __hip_atomic_load(&o.counts[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int tot2 = __hip_atomic_load(&o.counts[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&o.host_counts[0], tot1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&o.host_counts[1], tot2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  __syncthreads();
+  int sl = -1;
+  if (lg < games && s_f[lg] == 1) {
+    sl = s_pre;
+    for (int i = 0; i < lg; ++i) sl += s_f[i] == 1;
+  }
+  if (a == 0 && lg < games) {
+    o.slot[g] = sl;
+    if (sl >= 0) {
+      o.list[sl] = g;
+      o.legal_c[sl] = o.legal[g];
+    }
+  }
+  // encode (k_sp_encode_g) of this workgroup's searching games at their slots
+  if (sl >= 0) det_enc_stage<G>(c, LdsLane{sstate[lg], sstate[lg][40], 0, 0}, BoardView{sboard[lg], 1}, senc[lg], a);
+  __syncthreads();
+  if (sl >= 0) {
+    const int P = c.P, C = 8 * P + 2;
+    const bool teams = has(c.flags, R_TEAMS);
+    const uint8_t* e = senc[lg];
+    float4* ob = reinterpret_cast<float4*>(o.obs + (size_t)sl * C * kCells);
+    for (int q = a; q < C * 14; q += G) {
+      const int ch = q / 14, w0 = (q - ch * 14) * 4;
+      const uint32_t rel4 = *reinterpret_cast<const uint32_t*>(e + w0);
+      const uint32_t v4 = ch < P + 2 ? __builtin_amdgcn_perm(0u, det_obs_table(ch, P, teams), rel4)
+                                     : (uint32_t)e[kCells + ch] * 0x01010101u;
+      ob[q] = make_float4((float)(v4 & 0xFFu), (float)((v4 >> 8) & 0xFFu), (float)((v4 >> 16) & 0xFFu),
+                          (float)(v4 >> 24));
+    }
+    const int gn = STREAM ? s_gn[lg] : g;
+    uint4* to = reinterpret_cast<uint4*>(o.traj_obs + ((size_t)gn * T + idx[gn]) * C * kCells);
+    for (int q = a; q < C * 7 / 2; q += G) {
+      const uint2 lo = det_obs_half(e, 2 * q, P, teams), hi = det_obs_half(e, 2 * q + 1, P, teams);
+      to[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+  }
+  if (STREAM && s_reset) det_rows_store<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
+}
+
 struct SpWs {
   void* tree;
   float* conv;
@@ -312,25 +486,39 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
 
   TurnLedger led(s, stats != nullptr);
   if ((rc = led.begin())) return rc;
+  MUZ_HIP_RET(hipMemsetAsync(ws.counts, 0, 8 * sizeof(int32_t), s));   // both parities of k_sp_head's counters
   int turns = 0;
   rc = MUZ_OK;
   for (int turn = 0; turn < max_turns; ++turn) {
     if (!led.proceed(turn)) break;
+    const int nbk = (n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes);
+#if MUZ_SP_FUSED_HEAD
+    int32_t* const counts = ws.counts + 4 * (turn & 1);   // (the other parity: the next turn's, zeroed by the head)
+    const SpHead h{ws.legal, ws.flag, ws.list, ws.slot, counts, ws.counts + 4 * ((turn + 1) & 1), ws.legal_c, ws.obs,
+                   tr.obs, led.device_slot(turn)};
+    if (lane_game)
+      k_sp_head<true><<<nbk, kSpBlock, 0, s>>>(c, st, n, tr.idx, T, ws.lane_game, ws.next_game, num_games, h);
+    else
+      k_sp_head<false><<<nbk, kSpBlock, 0, s>>>(c, st, n, tr.idx, T, nullptr, nullptr, num_games, h);
+    if (h.host_counts) led.counts_written(turn);
+    else led.counts(turn, counts);
+#else
+    int32_t* const counts = ws.counts;
     if (lane_game)
       k_ss_refill<<<1, kScanThreads, 0, s>>>(c, st, ws.lane_game, tr.idx, T, ws.next_game, num_games, n);
-    k_sp_flags_g<<<(n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes), kSpBlock, 0, s>>>(
-        c, st, ws.legal, ws.flag, n, lane_game, tr.idx, T);
+    k_sp_flags_g<<<nbk, kSpBlock, 0, s>>>(c, st, ws.legal, ws.flag, n, lane_game, tr.idx, T);
     k_sp_compact<<<1, kScanThreads, 0, s>>>(ws.flag, n, ws.list, ws.slot, ws.counts);
     led.counts(turn, ws.counts);
-    k_sp_encode_g<<<(n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes), kSpBlock, 0, s>>>(
-        c, st, ws.list, ws.counts, ws.legal, ws.legal_c, ws.obs, tr.obs, tr.idx, T, lane_game);
+    k_sp_encode_g<<<nbk, kSpBlock, 0, s>>>(c, st, ws.list, ws.counts, ws.legal, ws.legal_c, ws.obs, tr.obs, tr.idx,
+                                           T, lane_game);
+#endif
     if ((rc = muz_last_launch_error())) break;
-    if ((rc = launch_root_inference(*w, ws.obs, n, ws.counts, ws.conv, ws.root_logits, ws.root_value, ws.root_emb,
+    if ((rc = launch_root_inference(*w, ws.obs, n, counts, ws.conv, ws.root_logits, ws.root_value, ws.root_emb,
                                     s)))
       break;
     sa.turn = turn;
     led.search_begin(turn);
-    if ((rc = launch_gumbel_search(*w, sa, ws.root_logits, ws.root_value, ws.root_emb, ws.legal_c, nullptr, ws.list, n, ws.counts, ws.tree, ws.action, ws.weights,
+    if ((rc = launch_gumbel_search(*w, sa, ws.root_logits, ws.root_value, ws.root_emb, ws.legal_c, nullptr, ws.list, n, counts, ws.tree, ws.action, ws.weights,
                                    ws.value, s)))
       break;
     led.search_end(turn);

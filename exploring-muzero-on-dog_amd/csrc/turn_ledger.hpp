@@ -30,8 +30,9 @@ class TurnLedger {
     if (host_) (void)hipHostFree(host_);
   }
   int begin() {
-    hipError_t e = hipHostMalloc((void**)&host_, (size_t)kRing * 2 * sizeof(int32_t), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc((void**)&host_, (size_t)kRing * 2 * sizeof(int32_t), hipHostMallocMapped);
     if (e != hipSuccess) return (int)e;
+    if (hipHostGetDevicePointer((void**)&dev_, host_, 0) != hipSuccess) dev_ = nullptr;
     // every create is checked; on a failure the events made so far (and the pinned ring) are released by the
     // destructor, which only touches handles that were created (nullptr-initialised members)
     for (int i = 0; i < kRing; ++i) {
@@ -56,6 +57,10 @@ class TurnLedger {
     retire(u);
     return !stopped_;
   }
+  // the device-visible address of `turn`'s pinned counts slot, for a kernel that writes the counts there itself
+  // (then counts_written instead of counts); null when the ring has no device mapping
+  int32_t* device_slot(int turn) const { return dev_ ? dev_ + 2 * (turn % kRing) : nullptr; }
+  void counts_written(int turn) { (void)hipEventRecord(ev_[turn % kRing], s_); }
   // after the counts of `turn` are final on the device (2 int32: searching, active)
   void counts(int turn, const int32_t* dev_counts) {
     (void)hipMemcpyAsync(host_ + 2 * (turn % kRing), dev_counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s_);
@@ -105,6 +110,7 @@ class TurnLedger {
   hipStream_t s_;
   bool timing_, ok_ = false, stopped_ = false;
   int32_t* host_ = nullptr;
+  int32_t* dev_ = nullptr;   // host_ as the device sees it (mapped pinned memory)
   hipEvent_t ev_[kRing] = {}, tev_[kRing][2] = {}, t0_ = nullptr, t1_ = nullptr;
   int retired_ = 0, timed_ = 0, active_ = 0;
   long long searches_ = 0;

@@ -21,6 +21,7 @@ self-play kernels' arena (nets.DeviceNet).  Everything is fp32.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -621,7 +622,9 @@ class GradSink:
 
     def __init__(self):
         self.buf, self.wg, self.cs, self.keep, self.owned = {}, [], [], [], set()
-        self.scratch = None     # segment partials of the long weight-gradient reductions
+        self.scratch = {}       # segment partials of the long weight-gradient reductions, one buffer per launch
+        self.side = None        # the stream the grouped launches run on (ASYNC_GRADS), joined at flush()
+        self.nlaunch = 0        # grouped launches issued in this backward (their scratch buffers' keys)
 
     def __enter__(self):
         global _SINK
@@ -666,18 +669,46 @@ class GradSink:
         self.keep.append(dz2d)
         self.cs.append((dz2d.data_ptr(), g.data_ptr(), 0, 0, 1, dz2d.shape[0], dz2d.shape[1], dz2d.stride(0)))
 
-    def flush(self):
-        lib, st = _L.load(), _L.stream_ptr()
+    def _launch(self):
+        """The grouped launches of everything recorded since the last one (on the side stream when ASYNC_GRADS)."""
+        if not self.wg and not self.cs:
+            return
+        lib, cur = _L.load(), torch.cuda.current_stream()
+        if ASYNC_GRADS:
+            if self.side is None:
+                self.side = torch.cuda.Stream(device=cur.device)
+            self.side.wait_stream(cur)    # the recorded inputs are complete on the backward's stream
+            stream = self.side
+        else:
+            stream = cur
+        st = _L.stream_ptr(stream)
         if self.wg:
             arr = (_L.MuzWgradProblem * len(self.wg))(*[_L.MuzWgradProblem(*w) for w in self.wg])
             need = lib.muz_wgrad_scratch_floats(arr, len(self.wg))
-            if self.scratch is None or self.scratch.numel() < need:    # kept: a captured graph replays into it
-                self.scratch = torch.empty((max(need, 1),), dtype=torch.float32, device=self.keep[0].device)
-            _L.check(lib.muz_wgrad_grouped(arr, len(self.wg), _L.ptr(self.scratch), self.scratch.numel(), st),
-                     "muz_wgrad_grouped")
+            sc = self.scratch.get(self.nlaunch)
+            if sc is None or sc.numel() < need:    # kept: a captured graph replays into it
+                with torch.cuda.stream(stream):
+                    sc = self.scratch[self.nlaunch] = torch.empty((max(need, 1),), dtype=torch.float32,
+                                                                  device=self.keep[0].device)
+            _L.check(lib.muz_wgrad_grouped(arr, len(self.wg), _L.ptr(sc), sc.numel(), st), "muz_wgrad_grouped")
         if self.cs:
             arr = (_L.MuzColsumProblem * len(self.cs))(*[_L.MuzColsumProblem(*c) for c in self.cs])
             _L.check(lib.muz_colsum_grouped(arr, len(self.cs), st), "muz_colsum_grouped")
+        self.wg, self.cs = [], []
+        self.nlaunch += 1
+
+    def flush_early(self):
+        """Called by a backward node before / after a long launch of its own (the trunk chain on 8 CUs): the
+        gradients recorded so far are formed on the side stream meanwhile.  No-op unless ASYNC_GRADS."""
+        if ASYNC_GRADS:
+            self._launch()
+
+    def flush(self):
+        self._launch()
+        if self.side is not None and ASYNC_GRADS:
+            # the recorded tensors (self.keep) stay referenced until here, after the join
+            torch.cuda.current_stream().wait_stream(self.side)
+        self.nlaunch = 0
         for p, g in self.buf.values():
             if id(p) in self.owned:
                 if p.grad is not None and p.grad is not g:
@@ -730,6 +761,10 @@ def _backward(loss, sink):
 FUSED_LOSS = True      # False: the losses as torch ops (A/B timing, and the fused kernel's test reference)
 FUSED_HEADS = True     # False: the output heads as library GEMMs + torch activations (A/B timing, test reference)
 GROUPED_GRADS = True   # False: every weight / bias / LayerNorm gradient as its own launch (A/B timing)
+# MUZ_ASYNC_GRADS=1: the grouped gradient launches on a side stream, the ones recorded before / during the trunk
+# chain's backward overlapping it and the representation's backward.  Off: measured slower (1.607 -> 1.741 ms per det
+# step, profiles/r5y_async_grads.log -- k_chain_bwd 429 -> 475 us beside the gradient launches on its CUs)
+ASYNC_GRADS = os.environ.get("MUZ_ASYNC_GRADS", "0") == "1"
 _SINK = None     # the active GradSink (module-global: autograd runs GPU backward nodes on its own thread)
 
 
@@ -886,8 +921,13 @@ class _TrunkChain(torch.autograd.Function):
         G = G.contiguous()
         H = None if H is None else H.contiguous()
         if ctx.chain is not None:
+            sink = _sink()
+            if sink is not None:     # the heads' / prediction stack's gradients run beside the chain kernel
+                sink.flush_early()
             dlat, dscale, dshift, DZ, scr = _chain_backward(ctx.chain, G, H, ctx.grad_scale, ctx.apps, ctx.P, B, Nn)
             grads = _trunk_param_grads(ctx.X, DZ, scr, ctx.P, _slots(ctx.apps, len(ctx.P) // _NP)[1], Nn)
+            if sink is not None:     # the chain's own beside the representation's backward
+                sink.flush_early()
             return (dlat, dscale, dshift, None, None, None, None, *grads)
         P, st, s, apps = ctx.P, ctx.st, ctx.grad_scale, ctx.apps
         dev, dt = G.device, G.dtype
