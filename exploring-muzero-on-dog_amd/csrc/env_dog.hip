@@ -731,6 +731,9 @@ __device__ __forceinline__ void dog_checks_block(const DetConsts& c, DogG& s, in
 #ifndef MUZ_DOG_LEAN_CHECKS
 #define MUZ_DOG_LEAN_CHECKS 1   // k_dog_play's checks on dog.hpp's lean predicates (0: dog_base_valid, A/B)
 #endif
+#ifndef MUZ_DOG_PAIRING
+#define MUZ_DOG_PAIRING 0       // 1: k_dog_play pairs the hot-7 check waves with the normal wave / nothing (A/B: 0.4 % slower)
+#endif
 #ifdef MUZ_DOG_STAMPS
 // diagnostic: per physical wave w, cycles of its check pass p (slot 8 + 4 p + w) and the number of passes that ran
 // a check (slot 16 + 4 p + w), of the phase's setup before the passes (slot w: context build, its barrier, hoisted
@@ -761,8 +764,16 @@ __device__ __forceinline__ void dog_checks_play(const DetConsts& c, DogG& s, int
 #ifdef MUZ_DOG_STAMPS
     if ((tid & 63) == 0) dog_wave_acc()[tid >> 6] += __builtin_amdgcn_s_memtime() - tp;   // slots 0-3: setup
 #endif
-    int pass = 0;
-    for (int vt = tid; vt < kDogBlockThreads; vt += NTH, ++pass) {
+    // check wave of (physical wave w, pass p): NTH = 256 pairs the two hot-7 waves (the costliest pass, ~5.5 k
+    // cycles when a 7 or joker is in hand) with the normal / -4 wave and nothing, and the four swap waves two by two,
+    // so the longest physical wave of a joker turn is hot-7 + normal (~7.5 k) rather than swap + hot-7 (~8.8 k,
+    // profiles/r5v_dog_play_stamps_lean.log); otherwise wave w takes check waves w, w + NTH / 64, ...
+    for (int pass = 0; pass * NTH < kDogBlockThreads; ++pass) {
+      const int pw = tid >> 6;
+      int cw = (pass * NTH + tid) >> 6;
+      if (NTH == 256 && MUZ_DOG_PAIRING) cw = pass == 0 ? (pw < 2 ? pw : pw + 2) : (pw < 2 ? pw + 2 : (pw == 2 ? 6 : 7));
+      if (cw * 64 >= kDogBlockThreads) continue;   // (wave-uniform)
+      const int vt = cw * 64 + (tid & 63);
 #ifdef MUZ_DOG_STAMPS
       const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif

@@ -17,7 +17,10 @@ constexpr int kFilmRows = 16, kFilmE = 64, kFilmN = 256, kFilmThreads = 256;
 
 // grid (rows / 16, 2): blockIdx.y picks 128 of the 256 output columns; thread t owns column 128 y + (t & 127) of
 // rows 8 (t >> 7) .. + 7 of the tile, for both products (e rows read as float4 over j from LDS)
-__global__ __launch_bounds__(kFilmThreads) void k_film_fwd(const int32_t* __restrict__ action, int M, int A,
+// row r of the M = B x K learner rows (step-major: r = k B + b) reads action[b * lda + k] -- the batch's [B][lda]
+// action rows directly, no transposed copy (B = M, lda = 1: a plain vector)
+__global__ __launch_bounds__(kFilmThreads) void k_film_fwd(const int32_t* __restrict__ action, int B, int lda, int M,
+                                                            int A,
                                                             const float* __restrict__ W0, const float* __restrict__ b0,
                                                             const float* __restrict__ W1, const float* __restrict__ b1,
                                                             const float* __restrict__ W2, const float* __restrict__ b2,
@@ -30,7 +33,7 @@ __global__ __launch_bounds__(kFilmThreads) void k_film_fwd(const int32_t* __rest
     const int r = i / kFilmE, j = i % kFilmE, row = r0 + r;
     float v = 0.f;
     if (row < M) {
-      const int a = action[row];
+      const int a = action[(size_t)(row % B) * lda + row / B];
       v = (a >= 0 && a < A) ? W0[(size_t)a * kFilmE + j] + b0[j] : b0[j];
       v = fmaxf(v, 0.f);
       if (first) e_out[(size_t)row * kFilmE + j] = v;
@@ -40,7 +43,7 @@ __global__ __launch_bounds__(kFilmThreads) void k_film_fwd(const int32_t* __rest
   if (onehot && first) {
     for (int i = t; i < kFilmRows * A; i += kFilmThreads) {
       const int r = i / A, c = i % A, row = r0 + r;
-      if (row < M) onehot[(size_t)row * A + c] = action[row] == c ? 1.f : 0.f;
+      if (row < M) onehot[(size_t)row * A + c] = action[(size_t)(row % B) * lda + row / B] == c ? 1.f : 0.f;
     }
   }
   __syncthreads();
@@ -140,14 +143,23 @@ using namespace muz;
 
 extern "C" {
 
+int muz_film_fwd_strided(const int32_t* action, int32_t B, int32_t K, int32_t lda, int32_t A, const float* W0,
+                         const float* b0, const float* W1, const float* b1, const float* W2, const float* b2,
+                         float* onehot, float* e, float* scale, float* shift, float* scale1, void* stream) {
+  MUZ_HOST_CHECK(B >= 0 && K >= 0 && lda >= K && A > 0 && action && W0 && b0 && W1 && b1 && W2 && b2 && e && scale &&
+                 shift);
+  const int M = B * K;
+  if (M == 0) return MUZ_OK;
+  k_film_fwd<<<dim3((M + kFilmRows - 1) / kFilmRows, 2), kFilmThreads, 0, (hipStream_t)stream>>>(
+      action, B, lda, M, A, W0, b0, W1, b1, W2, b2, onehot, e, scale, shift, scale1);
+  return muz_last_launch_error();
+}
+
 int muz_film_fwd(const int32_t* action, int32_t M, int32_t A, const float* W0, const float* b0, const float* W1,
                  const float* b1, const float* W2, const float* b2, float* onehot, float* e, float* scale,
                  float* shift, float* scale1, void* stream) {
-  MUZ_HOST_CHECK(M >= 0 && A > 0 && action && W0 && b0 && W1 && b1 && W2 && b2 && e && scale && shift);
-  if (M == 0) return MUZ_OK;
-  k_film_fwd<<<dim3((M + kFilmRows - 1) / kFilmRows, 2), kFilmThreads, 0, (hipStream_t)stream>>>(
-      action, M, A, W0, b0, W1, b1, W2, b2, onehot, e, scale, shift, scale1);
-  return muz_last_launch_error();
+  MUZ_HOST_CHECK(M >= 0);
+  return muz_film_fwd_strided(action, M, 1, 1, A, W0, b0, W1, b1, W2, b2, onehot, e, scale, shift, scale1, stream);
 }
 
 int muz_film_bwd(const float* dscale, const float* dshift, const float* e, const float* W1, const float* W2,

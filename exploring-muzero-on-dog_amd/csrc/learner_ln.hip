@@ -434,8 +434,9 @@ __global__ __launch_bounds__(256) void k_film_minmax_bwd(const float* __restrict
 // 'SAME' Conv1D as one GEMM (learner.MuZeroNets._conv_cols): the im2col matrix of x [B][W][Cin] is
 // cols [B][W][K * Cin], cols[b][w][d * Cin + c] = x[b][w + d - (K - 1) / 2][c] (0 outside the row), and its
 // backward dx[b][w][c] = sum_d dcols[b][w - d + (K - 1) / 2][d * Cin + c] (d ascending: deterministic).
+// x element (b, w, c) at x[b sb + w sw + c sc] (a strided view, e.g. the observation's first channels transposed)
 __global__ __launch_bounds__(256) void k_im2col_fwd(const float* __restrict__ x, int B, int W, int Cin, int K,
-                                                    float* __restrict__ cols) {
+                                                    int64_t sb, int64_t sw, int64_t sc, float* __restrict__ cols) {
   const int64_t n = (int64_t)B * W * K * Cin;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
@@ -443,7 +444,8 @@ __global__ __launch_bounds__(256) void k_im2col_fwd(const float* __restrict__ x,
   const int d = (int)((i / Cin) % K);
   const int64_t bw = i / ((int64_t)K * Cin);
   const int w = (int)(bw % W), src = w + d - (K - 1) / 2;
-  cols[i] = (src >= 0 && src < W) ? x[(bw - w + src) * Cin + c] : 0.f;
+  const int64_t b = bw / W;
+  cols[i] = (src >= 0 && src < W) ? x[b * sb + src * sw + c * sc] : 0.f;
 }
 
 __global__ __launch_bounds__(256) void k_im2col_bwd(const float* __restrict__ dcols, int B, int W, int Cin, int K,
@@ -598,12 +600,17 @@ int muz_film_minmax_bwd(const float* dfilm, const float* out, const float* z, co
   return muz_last_launch_error();
 }
 
-int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream) {
+int muz_im2col_fwd_strided(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, int64_t sb, int64_t sw,
+                           int64_t sc, float* cols, void* stream) {
   MUZ_HOST_CHECK(B >= 0 && W > 0 && Cin > 0 && K > 0 && x && cols);
   const int64_t n = (int64_t)B * W * K * Cin;
   if (n == 0) return MUZ_OK;
-  k_im2col_fwd<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, B, W, Cin, K, cols);
+  k_im2col_fwd<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, B, W, Cin, K, sb, sw, sc, cols);
   return muz_last_launch_error();
+}
+
+int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream) {
+  return muz_im2col_fwd_strided(x, B, W, Cin, K, (int64_t)W * Cin, Cin, 1, cols, stream);
 }
 
 int muz_im2col_bwd(const float* dcols, int32_t B, int32_t W, int32_t Cin, int32_t K, float* dx, void* stream) {

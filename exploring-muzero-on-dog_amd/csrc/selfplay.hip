@@ -387,7 +387,11 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_head(DetConsts c, muz_detmadn_s
     const bool teams = has(c.flags, R_TEAMS);
     const uint8_t* e = senc[lg];
     float4* ob = reinterpret_cast<float4*>(o.obs + (size_t)sl * C * kCells);
-    for (int q = a; q < C * 14; q += G) {
+    // channels >= 6 are constant planes (the global features): root inference reads them at cell 0 only
+    // (k_root_dense: x[:, 6:, 0]; k_repr_conv reads channels 0..5), so only their first float4 is written
+    const int nq = 6 * 14 + (C - 6);
+    for (int u = a; u < nq; u += G) {
+      const int q = u < 6 * 14 ? u : (u - 6 * 14 + 6) * 14;
       const int ch = q / 14, w0 = (q - ch * 14) * 4;
       const uint32_t rel4 = *reinterpret_cast<const uint32_t*>(e + w0);
       const uint32_t v4 = ch < P + 2 ? __builtin_amdgcn_perm(0u, det_obs_table(ch, P, teams), rel4)

@@ -272,8 +272,14 @@ class _Film(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, action, W0, b0, W1, b1, W2, b2):
-        a = action.reshape(-1).to(torch.int32).contiguous()
-        M, A = a.numel(), W0.shape[0]
+        # action: the M rows as a vector, or a [B, K] int32 view with unit column stride (row k B + b = action[b, k],
+        # read in place by the kernel)
+        if action.dim() == 2 and action.dtype == torch.int32 and action.stride(1) == 1:
+            a, (Bk, Kk), lda = action, action.shape, action.stride(0)
+        else:
+            a = (action.transpose(0, 1) if action.dim() == 2 else action).reshape(-1).to(torch.int32).contiguous()
+            Bk, Kk, lda = a.numel(), 1, 1
+        M, A = Bk * Kk, W0.shape[0]
         dev, dt = W0.device, W0.dtype
         oh = torch.empty((M, A), dtype=dt, device=dev)
         e = torch.empty((M, 64), dtype=dt, device=dev)
@@ -281,8 +287,9 @@ class _Film(torch.autograd.Function):
         shift = torch.empty((M, 256), dtype=dt, device=dev)
         P = [t.contiguous() for t in (W0, b0, W1, b1, W2, b2)]
         scale1 = torch.empty_like(scale)
-        _L.check(_L.load().muz_film_fwd(_L.ptr(a), M, A, *(_L.ptr(t) for t in P), _L.ptr(oh), _L.ptr(e),
-                                        _L.ptr(scale), _L.ptr(shift), _L.ptr(scale1), _L.stream_ptr()), "muz_film_fwd")
+        _L.check(_L.load().muz_film_fwd_strided(_L.ptr(a), Bk, Kk, lda, A, *(_L.ptr(t) for t in P), _L.ptr(oh),
+                                                _L.ptr(e), _L.ptr(scale), _L.ptr(shift), _L.ptr(scale1),
+                                                _L.stream_ptr()), "muz_film_fwd_strided")
         scale._muz_scale1 = scale1             # 1 + scale, bit-identical to the chain's own (fp32 add)
         ctx.save_for_backward(oh, e, P[2], P[4])
         ctx.owners = (W0, b0, W1, b1, W2, b2) if all(t.is_leaf for t in (W0, b0, W1, b1, W2, b2)) else None
@@ -423,9 +430,10 @@ class _Im2col(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, K):
         B, W, Cin = x.shape
-        x = x.contiguous()
         cols = torch.empty((B, W, K * Cin), dtype=x.dtype, device=x.device)
-        _L.check(_L.load().muz_im2col_fwd(_L.ptr(x), B, W, Cin, K, _L.ptr(cols), _L.stream_ptr()), "muz_im2col_fwd")
+        # (a strided view -- the observation's first channels transposed -- is read in place)
+        _L.check(_L.load().muz_im2col_fwd_strided(_L.ptr(x), B, W, Cin, K, *x.stride(), _L.ptr(cols),
+                                                  _L.stream_ptr()), "muz_im2col_fwd_strided")
         ctx.K, ctx.shape = K, (B, W, Cin)
         return cols
 
@@ -1221,6 +1229,8 @@ class MuZeroNets:
         if FUSED_FILM_EMBED and W0.is_cuda and W0.dtype == torch.float32 and W0.shape[1] == 64 and \
                 self.p[f"{d}/Dense_1/kernel"].shape == (64, 256):
             return _Film.apply(action, *(self.p[f"{d}/{n}"] for n in _FILM_PARAMS))
+        if action.dim() == 2:       # a [B, K] batch view: rows step-major
+            action = action.transpose(0, 1).reshape(-1)
         oh = (action.long()[:, None] == torch.arange(self.A, device=action.device)[None, :]).to(
             self.p[f"{d}/Dense_0/bias"].dtype)
         e = F.relu(self._dense(f"{d}/Dense_0", oh))
@@ -1282,7 +1292,7 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     # Only the latent chain is sequential: the action FiLM rows, Pred4 on every step's latent and the
     # reward / discount heads are row-wise, so each runs once over all K (+1) steps stacked along the batch
     # (same per-row arithmetic as the step-by-step loop of the reference; far fewer kernel launches).
-    oh, scale, shift = nets.dynamics_film(batch["actions"][:, :K].transpose(0, 1).reshape(-1))
+    oh, scale, shift = nets.dynamics_film(batch["actions"][:, :K])     # (rows step-major: k B + b)
     latents = [latent]
     # The reward / discount heads read the next latent inside dynamics_net (muzero_deterministic_madn.py:
     # 437-455), BEFORE the loss scales the gradient of the latent it carries on (line 105): the heads take

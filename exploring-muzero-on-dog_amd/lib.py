@@ -364,6 +364,8 @@ SIGNATURES = {
                                   vp, vp, vp, vp]),
     "muz_film_fwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                     vp]),
+    "muz_film_fwd_strided": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp,
+                                            vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "muz_film_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp]),
     "muz_ln_film_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp]),
     "muz_ln_film_bwd_rows": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
@@ -376,6 +378,8 @@ SIGNATURES = {
     "muz_minmax_bwd": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, ctypes.c_int32, vp, vp, ctypes.c_int32,
                                       ctypes.c_int32, vp, vp]),
     "muz_im2col_fwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),
+    "muz_im2col_fwd_strided": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                              ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, vp, vp]),
     "muz_im2col_bwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),
     "muz_wgrad_scratch_floats": (ctypes.c_int64, [vp, ctypes.c_int32]),
     "muz_wgrad_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp, ctypes.c_int64, vp]),

@@ -706,6 +706,11 @@ int muz_ln_bwd(const float* dout, const float* out, const float* z, const float*
 int muz_film_fwd(const int32_t* action, int32_t M, int32_t A, const float* W0, const float* b0, const float* W1,
                  const float* b1, const float* W2, const float* b2, float* onehot, float* e, float* scale,
                  float* shift, float* scale1, void* stream);
+/* The same over the M = B x K step-major rows of a [B][lda] action array (row k B + b reads action[b lda + k]): the
+ * learner's batch["actions"][:, :K] without a transposed copy.  muz_film_fwd is B = M, K = 1, lda = 1. */
+int muz_film_fwd_strided(const int32_t* action, int32_t B, int32_t K, int32_t lda, int32_t A, const float* W0,
+                         const float* b0, const float* W1, const float* b1, const float* W2, const float* b2,
+                         float* onehot, float* e, float* scale, float* shift, float* scale1, void* stream);
 int muz_film_bwd(const float* dscale, const float* dshift, const float* e, const float* W1, const float* W2,
                  int32_t M, float* de, void* stream);
 /* The FiLM input of a dynamics trunk (muzero_deterministic_madn.py:421-427; learner._TrunkChain): out = LayerNorm(x)
@@ -932,6 +937,9 @@ int muz_rbstack_bwd(const muz_rbstack_args* args, void* stream);
 /* 'SAME' Conv1D as a GEMM: the im2col matrix cols [B][W][K x Cin] of x [B][W][Cin] (zero outside each row;
  * tap d reads column w + d - (K - 1) / 2) and its backward dx = sum over taps (fixed order). */
 int muz_im2col_fwd(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, float* cols, void* stream);
+/* muz_im2col_fwd of a strided view: x element (b, w, c) at x[b sb + w sw + c sc] (element strides). */
+int muz_im2col_fwd_strided(const float* x, int32_t B, int32_t W, int32_t Cin, int32_t K, int64_t sb, int64_t sw,
+                           int64_t sc, float* cols, void* stream);
 int muz_im2col_bwd(const float* dcols, int32_t B, int32_t W, int32_t Cin, int32_t K, float* dx, void* stream);
 
 /* One optimizer step over ntensors parameter tensors (csrc/learner_opt.hip): optax.chain(

@@ -21,6 +21,8 @@ from exploring_muzero_on_dog_amd import lib as L  # noqa: E402
 
 CATS = ["reset", "base checks + barrier", "mask words + choice", "env_step", "barrier", "deal"]
 CHECK_WAVES = ["swap 0-63 | hot-7 0-63", "swap 64-127 | hot-7 64-119", "swap 128-191 | normal + -4", "swap 192-223 | -"]
+if os.environ.get("MUZ_DOG_PAIRING", "0") == "1":   # a -DMUZ_DOG_PAIRING=1 build (env_dog.hip dog_checks_play)
+    CHECK_WAVES = ["swap 0-63 | swap 128-191", "swap 64-127 | swap 192-223", "hot-7 0-63 | normal + -4", "hot-7 64-119 | -"]
 
 
 def main():
