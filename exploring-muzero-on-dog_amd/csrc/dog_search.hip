@@ -586,13 +586,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
   __shared__ signed char s_vcnt[kRows][kWMaxNodes];   // per-node visited-list lengths (-1: overflowed)
   __shared__ int s_act[kRows], s_parent[kRows], s_next[kRows], s_depth[kRows];
 
-  constexpr int kGames = SPARSE ? kRows / 2 : kRows;   // games per workgroup
+  const int kGames = SPARSE ? sa.games_per_wg : kRows;   // games per workgroup
   if ((int)blockIdx.x * kGames >= n) return;
-  auto game_of = [](int r) { return (int)blockIdx.x * kGames + (SPARSE ? (r >> 1) : r); };
+  auto game_of = [kGames](int r) { return (int)blockIdx.x * kGames + (SPARSE ? (r >> 1) : r); };
   const Arena ar = Arena::carve(smem);
   const int row = trow(), sub = tsub();
   const int g = game_of(row);
-  const bool valid = (!SPARSE || (row & 1) == 0) && g < n;
+  const bool valid = (!SPARSE || ((row & 1) == 0 && (row >> 1) < kGames)) && g < n;
   int gid = g, gturn = sa.turn;
   int ncons = 0;
 
@@ -940,7 +940,7 @@ int launch_dog_search(const muz_dog_net_w& w, const SearchArgs& sa, const float*
                       int32_t* action, float* weights, float* value, bool sparse, hipStream_t s) {
   WTree T = carve_wide(workspace, n, sa.S + 1);
   if (sparse)
-    k_dog_search<true><<<(n + kRows / 2 - 1) / (kRows / 2), kThreads, 0, s>>>(w, sa, root_logits, root_value, root_emb,
+    k_dog_search<true><<<(n + sa.games_per_wg - 1) / sa.games_per_wg, kThreads, 0, s>>>(w, sa, root_logits, root_value, root_emb,
                                                                              legal, gumbel, n, T, action, weights, value);
   else
     k_dog_search<false><<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, sa, root_logits, root_value, root_emb, legal,
@@ -991,6 +991,11 @@ int muz_dog_gumbel_search(const muz_dog_net_w* w, const muz_search_cfg* cfg, con
   // one game per wave while the grid fits the chip's 256 CUs; MUZ_DOG_TILE_ROWS=8 / 16 forces either form
   bool sparse = n <= 2048;
   if (const char* e = getenv("MUZ_DOG_TILE_ROWS")) sparse = atoi(e) == 8;
+  // games per workgroup of the one-game-per-wave form: fewer than 8 while the grid still fits the chip's 256 CUs
+  // (a simulation waits for the slowest of the workgroup's walks): 6 at the reference's 1500 games, 250 workgroups
+  // -- 0.8 % faster than 8 (profiles/r5zb_dog_gpw_ab.log; 7: 0.2 % slower)
+  sa.games_per_wg = std::min(8, std::max(6, (n + 255) / 256));
+  if (const char* e = getenv("MUZ_DOG_GPW")) sa.games_per_wg = std::min(8, std::max(1, atoi(e)));
   return launch_dog_search(*w, sa, root_logits, root_value, root_embedding, legal, gumbel, n, workspace, action,
                            action_weights, root_value_out, sparse, (hipStream_t)stream);
 }

@@ -17,6 +17,7 @@ struct SearchArgs {
   const int32_t* key_game = nullptr;
   const int32_t* key_turn = nullptr;
   int exact_select = 0;   // k_dog_search: every interior selection on the exact path (MUZ_DOG_EXACT_SELECT)
+  int games_per_wg = 8;   // k_dog_search one-game-per-wave form: games per workgroup (<= 8; MUZ_DOG_GPW)
 };
 
 int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv_scratch,
