@@ -231,7 +231,7 @@ MEASURED = {
     "traffic": "profiles/r5i_traffic.json",           # HBM bytes per k_gumbel_search launch (FETCH_SIZE x2 + WRITE_SIZE)
     "pmc": "profiles/r5i_pmc.json",                   # TCP_TCC_READ_REQ, SQ_VALU_MFMA_BUSY_CYCLES, ... (k_gumbel_search)
     "loop": "profiles/r5i_loop_bench.log",            # the weight-stream MFMA loop alone (profiles/loop_bench.hip)
-    "dog_traffic": "profiles/r5j_dog_traffic.json",   # HBM bytes per k_dog_search launch (FETCH_SIZE x2 + WRITE_SIZE)
+    "dog_traffic": "profiles/r5zd_dog_traffic.json",  # HBM bytes per k_dog_search launch (FETCH_SIZE x2 + WRITE_SIZE), 6 games / WG
 }
 
 
