@@ -1047,8 +1047,12 @@ __device__ __forceinline__ void repr16(const AS4 muz_repr_w& R, const float* __r
   const int Kg = C - 6;
   if (sub < 32) a.E[row * LDE + sub] = (valid && sub < Kg) ? obs[((size_t)gr * C + 6 + sub) * 56] : 0.f;
   // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16)
+#ifdef MUZ_EXPT_SKIP_D0   // timing experiment only (wrong results): Dense_0 left out of the root kernel
+  pf_issue<NT64>(pf, &R.d1, Kg, 64);
+#else
   pf_issue<NT256>(pf, &R.d0, 3584, LAT);
   dense16<NT256, NT64>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW, pf, &R.d1, Kg, 64, true);
+#endif
   __syncthreads();
   ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, R.ln3);
   dense16<NT64, NT64>(R.d1, Kg, 64, a.E, LDE, a.X, LD, pf, &R.d2, 64, 64);
