@@ -184,6 +184,7 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
   {
     float v[E] = {};
     if (live) ldEg(a->latent0 + o, v);
+    if (live && a->stack0) stEg(a->stack0 + o, v);
     stE(lat + row * LD + c0, v);
   }
   Ln0Ops n0;
@@ -298,6 +299,7 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
         stE(lat + row * LD + c0, out);
         if (live) {
           stEg(a->out + i * MN + o, out);
+          if (a->out_twin) stEg(a->out_twin + i * MN + o, out);
           stEg(a->q + i * MN + o, q);
           if ((tid % TPR) == 0) {
             const size_t r2 = (size_t)i * 2 * M + 2 * m;
@@ -553,6 +555,12 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
   if (live) {
     float c[E];
     ldE(carry + row * LD + c0, c);
+    if (a->g0) {   // + the stack's block-0 gradient (what autograd's accumulation added, same single rounding)
+      float g[E];
+      ldEg(a->g0 + o, g);
+#pragma unroll
+      for (int e = 0; e < E; ++e) c[e] = c[e] + g[e];
+    }
     stEg(a->dlatent0 + o, c);
   }
 }

@@ -123,9 +123,12 @@ class _ResStack(torch.autograd.Function):
         dev, dt = x.device, x.dtype
         lib = _L.load()
         W = [P[8 * b + 4 * k] for b in range(nb) for k in range(2)]
-        WP = torch.empty((2, L2, Nn * Nn), dtype=dt, device=dev)
-        src = (ctypes.c_void_p * L2)(*[w.data_ptr() for w in W])
-        _L.check(lib.muz_trunk_chain_pack(src, L2, _L.ptr(WP[0]), _L.ptr(WP[1]), _L.stream_ptr()), "muz_trunk_chain_pack")
+        WP = _packed(W)
+        if WP is None:
+            WP = torch.empty((2, L2, Nn * Nn), dtype=dt, device=dev)
+            src = (ctypes.c_void_p * L2)(*[w.data_ptr() for w in W])
+            _L.check(lib.muz_trunk_chain_pack(src, L2, _L.ptr(WP[0]), _L.ptr(WP[1]), _L.stream_ptr()),
+                     "muz_trunk_chain_pack")
         X = torch.empty((L2, M, Nn), dtype=dt, device=dev)
         out = torch.empty((M, Nn), dtype=dt, device=dev)
         z = torch.empty((L2, M, Nn), dtype=dt, device=dev)
@@ -806,7 +809,67 @@ def trunk_param_names(kind: str = "det") -> list:
 
 
 DYN_TRUNK_PARAMS = tuple(trunk_param_names("det"))
+
+
+# ---- one packing launch per step for every persistent GEMM kernel's weights ----------------------------------------
+# _ResStack (representation, prediction) and the trunk chain each repacked their weights into MFMA operand order with
+# a launch of their own (3 per step).  prepack() packs all of them with ONE muz_trunk_chain_pack at the top of the
+# loss; each forward finds its slice by the weights' data pointers (a forward whose weights were not pre-packed packs
+# them itself, as before).  The buffer is kept by the caller (a captured graph replays into it).
+_PACKED = {}
+
+
+def prepack(weight_lists, keep):
+    """Pack the lists of [256, 256] weights (each one consumer's, in its layer order) with one launch; ``keep``:
+    a dict owned by the caller that holds the buffer across graph replays."""
+    _PACKED.clear()
+    ws = [w for lst in weight_lists for w in lst]
+    if not ws or not all(w.is_cuda and w.dtype == torch.float32 and tuple(w.shape) == (256, 256) for w in ws):
+        return
+    n = len(ws)
+    WP = keep.get("WP")
+    if WP is None or WP.shape[1] != n:
+        WP = keep["WP"] = torch.empty((2, n, 256 * 256), dtype=torch.float32, device=ws[0].device)
+    src = (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws])
+    _L.check(_L.load().muz_trunk_chain_pack(src, n, _L.ptr(WP[0]), _L.ptr(WP[1]), _L.stream_ptr()),
+             "muz_trunk_chain_pack")
+    o = 0
+    for lst in weight_lists:
+        _PACKED[tuple(w.data_ptr() for w in lst)] = WP[:, o:o + len(lst)]
+        o += len(lst)
+
+
+def _packed(ws):
+    """The pre-packed [2, len(ws), 65536] slice of these weights (prepack), or None."""
+    return _PACKED.get(tuple(w.data_ptr() for w in ws))
+
+
+def _rbstack_weights(p, name, nb):
+    return [p[f"{name}{b}/Dense_{k}/kernel"] for b in range(nb) for k in range(2)]
+
+
+def _cat0(ts):
+    """torch.cat(ts, 0), without the copy when ts is one tensor already (the chain's stacked latents)."""
+    return ts[0] if len(ts) == 1 else torch.cat(ts, 0)
+
+
+def _prepack_nets(nets):
+    """prepack() of the det / DOG loss's three packed consumers: the representation's six ResBlocks, the dynamics trunk
+    chain, the prediction's two ResBlocks (whichever the parameter set has; the lists _PACKED serves are cleared again
+    once the loss's forward is built)."""
+    p = nets.p
+    if not (RESBLOCK_STACK and CHAIN and p[DYN_TRUNK_PARAMS[_CHAIN_W[0]]].is_cuda):
+        return
+    lists = []
+    for name, nb in (("representation/ResBlock_", 6), ("prediction/ResBlock_", 2)):
+        if all(f"{name}{b}/Dense_{k}/kernel" in p for b in range(nb) for k in range(2)) and f"{name}{nb}/Dense_0/kernel" not in p:
+            lists.append(_rbstack_weights(p, name, nb))
+    if all(n in p for n in DYN_TRUNK_PARAMS):
+        lists.append([p[DYN_TRUNK_PARAMS[k]] for k in _CHAIN_W])
+    keep = nets.__dict__.setdefault("_packkeep", {})
+    prepack(lists, keep)
 CHAIN = True                     # False: the losses build the per-step autograd graph instead (A/B timing)
+STACK_LATENTS = True             # the det loss takes the chain's output as the stacked latents (False: torch.cat, A/B)
 FUSED_FILM = True                # False: a trunk's LayerNorm_0 + FiLM as LayerNorm + addcmul (A/B, diagnosis)
 FUSED_BOUNDARY = True            # False: min-max of application i and LayerNorm_0 + FiLM of i + 1 as separate launches
 _NP = len(DYN_TRUNK_PARAMS)      # 28 per trunk
@@ -852,7 +915,12 @@ class _TrunkChain(torch.autograd.Function):
         if len(apps) != T or len(scaled) != T or len(P) != _NP * (max(apps) + 1):
             raise ValueError("apps / scaled / parameters do not match the FiLM rows")
         dev, dt = latent0.device, latent0.dtype
-        outs = torch.empty((T, B, Nn), dtype=dt, device=dev)
+        # heads == 2 (the det loss): the first output is the stack [latent0, x_1 .. x_T] the prediction reads whole
+        # (no torch.cat of the latents, no unbind / stack in the backward), the twin written by the chain kernel
+        # itself (no clone), the stack's block-0 gradient added to d latent0 inside the backward kernel
+        stack = heads == 2
+        full = torch.empty((T + 1, B, Nn), dtype=dt, device=dev) if stack else None
+        outs = full[1:] if stack else torch.empty((T, B, Nn), dtype=dt, device=dev)
         qs = torch.empty((T, B, Nn), dtype=dt, device=dev)                  # min-max inputs and their extrema
         lohi = torch.empty((T, B, 2), dtype=dt, device=dev)
         idx = torch.empty((T, B, 2), dtype=torch.int32, device=dev)
@@ -872,10 +940,16 @@ class _TrunkChain(torch.autograd.Function):
              for g in range(len(seen)) for n in _GEMM_LAYERS}
         lat = latent0.contiguous()
         ctx.chain = None
+        ctx.stack = stack
         if _chain_usable(T, B, Nn, len(seen)):
-            ctx.chain = _chain_forward(lat, scale1, shift.contiguous(), apps, slot, scaled, P, X, outs, qs, lohi, idx)
+            twin = torch.empty_like(outs) if stack else None
+            ctx.chain = _chain_forward(lat, scale1, shift.contiguous(), apps, slot, scaled, P, X, outs, qs, lohi, idx,
+                                       twin=twin, stack0=full[0] if stack else None)
             ctx.X, ctx.P, ctx.grad_scale, ctx.apps = X, P, float(grad_scale), tuple(apps)
-            ctx.save_for_backward(scale1, qs, lohi, outs)    # outs: read by the backward kernel (a.out)
+            # outs (a view of full when stacked): read by the backward kernel (a.out); the output itself is saved
+            ctx.save_for_backward(scale1, qs, lohi, full if stack else outs)
+            if stack:
+                return full, twin
             return (outs, outs.clone()) if heads else outs
         f0_next = None    # LayerNorm_0 + FiLM of the next application, formed by the boundary launch
         for i in range(T):
@@ -920,19 +994,27 @@ class _TrunkChain(torch.autograd.Function):
         ctx.boundary = FUSED_BOUNDARY and FUSED_FILM
         ctx.apps, ctx.scaled = tuple(apps), tuple(scaled)
         ctx.save_for_backward(scale1, qs, lohi)
+        if stack:
+            full[0].copy_(latent0)
+            return full, outs.clone()
         return (outs, outs.clone()) if heads else outs
 
     @staticmethod
     def backward(ctx, G, H=None):
         scale1, qs, lohi = ctx.saved_tensors[:3]
         T, B, Nn = scale1.shape
+        G0 = None
+        if getattr(ctx, "stack", False):   # G: the stack's gradient [T + 1, B, N]; block 0 belongs to latent0
+            G = G.contiguous()
+            G0, G = G[0], G[1:]
         G = G.contiguous()
         H = None if H is None else H.contiguous()
         if ctx.chain is not None:
             sink = _sink()
             if sink is not None:     # the heads' / prediction stack's gradients run beside the chain kernel
                 sink.flush_early()
-            dlat, dscale, dshift, DZ, scr = _chain_backward(ctx.chain, G, H, ctx.grad_scale, ctx.apps, ctx.P, B, Nn)
+            dlat, dscale, dshift, DZ, scr = _chain_backward(ctx.chain, G, H, ctx.grad_scale, ctx.apps, ctx.P, B, Nn,
+                                                            G0=G0)
             grads = _trunk_param_grads(ctx.X, DZ, scr, ctx.P, _slots(ctx.apps, len(ctx.P) // _NP)[1], Nn)
             if sink is not None:     # the chain's own beside the representation's backward
                 sink.flush_early()
@@ -985,7 +1067,8 @@ class _TrunkChain(torch.autograd.Function):
                 dz0, _ = _ln_bwd_rows(dx0 * scale1[i], f0, Q[0], LN_PLAIN, scr[(g, "0")][j])
             ca, cb = dz0, dq
         grads = _trunk_param_grads(ctx.X, DZ, scr, P, seen, Nn)
-        return (ca + cb, dscale, dshift, None, None, None, None, *grads)
+        dlat = ca + cb
+        return (dlat if G0 is None else dlat + G0, dscale, dshift, None, None, None, None, *grads)
 
 
 def _trunk_param_grads(X, DZ, scr, P, seen, Nn):
@@ -1039,7 +1122,7 @@ class _Chain:
         self.args, self.keep = args, keep
 
 
-def _chain_forward(lat, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi, idx):
+def _chain_forward(lat, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi, idx, twin=None, stack0=None):
     """muz_trunk_chain_fwd over all applications: writes outs / qs / lohi / idx and the stacks X like the
     per-layer path, plus the LayerNorm outputs / pre-LayerNorm values / statistics its backward reads."""
     T, B, Nn = scale1.shape
@@ -1047,10 +1130,14 @@ def _chain_forward(lat, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi,
     dev, dt = lat.device, lat.dtype
     lib = _L.load()
     # both GEMM directions stream the weights as packed MFMA operands, repacked here every call (one launch)
-    WP = torch.empty((2, ngroups, 7, Nn * Nn), dtype=dt, device=dev)
-    src = (ctypes.c_void_p * (7 * ngroups))(*[P[_NP * g + k].data_ptr() for g in range(ngroups) for k in _CHAIN_W])
-    _L.check(lib.muz_trunk_chain_pack(src, 7 * ngroups, _L.ptr(WP[0]), _L.ptr(WP[1]), _L.stream_ptr()),
-             "muz_trunk_chain_pack")
+    WP = _packed([P[_NP * g + k] for g in range(ngroups) for k in _CHAIN_W])
+    if WP is not None:
+        WP = WP.view(2, ngroups, 7, Nn * Nn)
+    else:
+        WP = torch.empty((2, ngroups, 7, Nn * Nn), dtype=dt, device=dev)
+        src = (ctypes.c_void_p * (7 * ngroups))(*[P[_NP * g + k].data_ptr() for g in range(ngroups) for k in _CHAIN_W])
+        _L.check(lib.muz_trunk_chain_pack(src, 7 * ngroups, _L.ptr(WP[0]), _L.ptr(WP[1]), _L.stream_ptr()),
+                 "muz_trunk_chain_pack")
     ln0 = torch.empty((T, B, Nn), dtype=dt, device=dev)
     z = torch.empty((T, 6, B, Nn), dtype=dt, device=dev)
     stats = torch.empty((T, 7, 2, B), dtype=dt, device=dev)
@@ -1069,6 +1156,8 @@ def _chain_forward(lat, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi,
                 grp.gamma[l], grp.beta[l] = Q[k + 2].data_ptr(), Q[k + 3].data_ptr()
     a.latent0, a.scale1, a.shift = lat.data_ptr(), scale1.data_ptr(), shift.data_ptr()
     a.out, a.q, a.lohi, a.idx = outs.data_ptr(), qs.data_ptr(), lohi.data_ptr(), idx.data_ptr()
+    a.out_twin = 0 if twin is None else twin.data_ptr()
+    a.stack0 = 0 if stack0 is None else stack0.data_ptr()
     a.ln0_out, a.z, a.stats = ln0.data_ptr(), z.data_ptr(), stats.data_ptr()
     _L.check(lib.muz_trunk_chain_fwd(ctypes.byref(a), _L.stream_ptr()), "muz_trunk_chain_fwd")
     # kept as long as the autograd node (a second backward, retain_graph, reads them again); outs is the node's output
@@ -1076,9 +1165,9 @@ def _chain_forward(lat, scale1, shift, apps, slot, scaled, P, X, outs, qs, lohi,
     return _Chain(a, (WP, ln0, z, stats, lat, scale1, shift))
 
 
-def _chain_backward(chain, G, H, grad_scale, apps, P, B, Nn):
+def _chain_backward(chain, G, H, grad_scale, apps, P, B, Nn, G0=None):
     """muz_trunk_chain_bwd: -> (d latent0, d scale, d shift, DZ stacks, LayerNorm partials) for
-    _trunk_param_grads."""
+    _trunk_param_grads.  G0: the stacked form's block-0 gradient, added to d latent0 inside the kernel."""
     ngroups = len(P) // _NP
     seen = _slots(apps, ngroups)[1]
     T = len(apps)
@@ -1098,6 +1187,7 @@ def _chain_backward(chain, G, H, grad_scale, apps, P, B, Nn):
             grp.DZ[l] = DZ[(g, _GEMM_LAYERS[l])].data_ptr()
             grp.part[l] = scr[(g, _CHAIN_PARTS[l])].data_ptr()
     a.g, a.h = G.data_ptr(), (0 if H is None else H.data_ptr())
+    a.g0 = 0 if G0 is None else G0.data_ptr()
     a.grad_scale = grad_scale
     a.dscale, a.dshift, a.dlatent0 = dscale.data_ptr(), dshift.data_ptr(), dlat.data_ptr()
     _L.check(_L.load().muz_trunk_chain_bwd(ctypes.byref(a), _L.stream_ptr()), "muz_trunk_chain_bwd")
@@ -1286,6 +1376,7 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     grad_scale: the gradient share carried through the unrolled latent (0.5 in the reference, line 106;
     the forward value does not depend on it)."""
     obs = batch["observations"].to(nets.p["prediction/Dense_5/bias"].dtype)
+    _prepack_nets(nets)
     latent = nets.representation(obs)
     B, K = batch["actions"].shape
     dev = obs.device
@@ -1299,8 +1390,12 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
     # the unscaled outputs.
     if K and latent.is_cuda and CHAIN:     # the whole latent chain as one autograd node (fused kernels, batched weight grads)
         chain, raw = _TrunkChain.apply(latent, scale.reshape(K, B, -1), shift.reshape(K, B, -1), grad_scale,
-                                       (0,) * K, (True,) * K, True, *(nets.p[n] for n in DYN_TRUNK_PARAMS))
-        latents += list(chain.unbind(0))
+                                       (0,) * K, (True,) * K, 2 if STACK_LATENTS else True,
+                                       *(nets.p[n] for n in DYN_TRUNK_PARAMS))
+        if STACK_LATENTS:            # chain = [latent, x_1 .. x_K] already stacked
+            latents = [chain.reshape((K + 1) * B, -1)]
+        else:
+            latents += list(chain.unbind(0))
         head_in = raw.reshape(K * B, -1)
     else:
         raws = []
@@ -1310,11 +1405,11 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
             latents.append((nxt * (1.0 - grad_scale)).detach() + nxt * grad_scale)   # gradient scaling (fwd identity)
         head_in = torch.cat(raws, 0) if K else None
     if K and obs.is_cuda and FUSED_HEADS and nets.A <= 32:
-        pol_h, v_h = nets.prediction_hidden(torch.cat(latents, 0))
+        pol_h, v_h = nets.prediction_hidden(_cat0(latents))
         logits_all, v_all, rl_all, dl_all = _OutHeads.apply(pol_h, v_h, head_in, oh,
                                                              *(nets.p[n] for n in HEAD_PARAMS))
     else:
-        logits_all, v_all = nets.prediction(torch.cat(latents, 0))
+        logits_all, v_all = nets.prediction(_cat0(latents))
         rl_all, dl_all = nets.dynamics_heads(head_in, oh) if K else (None, None)
     if obs.is_cuda and FUSED_LOSS:
         u = 1.0 / unroll_steps
@@ -1322,7 +1417,9 @@ def loss_fn(nets: MuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: f
                     terms=[(batch["discount_targets"], 0, 1.0, 0.1, u * DISCOUNT_SCALING),     # terminal 1.0, other 0.1
                            (batch["rewards"], 0, 0.1, 1.0, u * REWARD_SCALING)])               # neutral 0.1, win/lose 1.0
         total, parts = _LossHeads.apply(logits_all, v_all, dl_all, rl_all, None, spec)
+        _PACKED.clear()
         return total, (parts[1], parts[2], parts[3], parts[4])
+    _PACKED.clear()
     # The per-step losses, all K (+1) steps at once ([K+1, B] views; row k = unroll step k).
     disc_t, rew_t = batch["discount_targets"].int(), batch["rewards"].int()
     m = batch["masks"][:, :K + 1].transpose(0, 1).to(obs.dtype)
@@ -1345,9 +1442,11 @@ _TICKETS = {}
 
 
 def _loss_ticket(dev):
-    """The loss kernel's last-workgroup counter: zero between launches (the kernel resets it), one per device and
-    stream (launches on one stream are ordered; kept alive, so a captured graph replays with the same one)."""
-    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    """The loss kernel's last-workgroup counter: zero between launches (the kernel resets it), one per device, kept
+    alive so a captured graph replays with the same one.  Launches sharing it must not overlap: the learner's are
+    ordered on one stream (its eager warm-up step completes before the capture).  Made on the first (eager) step --
+    keyed by stream, the capture stream's own counter was a zero-fill launch inside every replayed step."""
+    key = str(dev)
     t = _TICKETS.get(key)
     if t is None:
         t = _TICKETS[key] = torch.zeros((1,), dtype=torch.int32, device=dev)
@@ -1701,6 +1800,7 @@ class ClassicMuZeroNets(MuZeroNets):
 
 def loss_fn_stochastic(nets: ClassicMuZeroNets, batch: dict, unroll_steps: int = 10, grad_scale: float = 0.5):
     """train_stochastic.py:34-180 -> (total, (value, policy, chance, discount, reward) losses)."""
+    _PACKED.clear()   # (its consumers pack their own weights)
     dt = nets.p["prediction/Dense_5/bias"].dtype
     obs = batch["observations"].to(dt)
     latent = nets.representation(obs)

@@ -60,7 +60,7 @@ class MuzChainArgs(ctypes.Structure):
                 ("scaled", ctypes.c_int32 * MUZ_CHAIN_MAX_T), ("group", MuzChainGroup * 2), ("latent0", vp),
                 ("scale1", vp), ("shift", vp), ("out", vp), ("q", vp), ("lohi", vp), ("idx", vp), ("ln0_out", vp),
                 ("z", vp), ("stats", vp), ("g", vp), ("h", vp), ("grad_scale", ctypes.c_float), ("dscale", vp),
-                ("dshift", vp), ("dlatent0", vp)]
+                ("dshift", vp), ("dlatent0", vp), ("out_twin", vp), ("stack0", vp), ("g0", vp)]
 
 
 MUZ_RBSTACK_MAX = 6

@@ -901,6 +901,10 @@ typedef struct {
   float* dscale;
   float* dshift;
   float* dlatent0;
+  /* optional (null: unused) -- the learner's stacked-latent form, no copies around the chain: */
+  float* out_twin;         /* forward: a second copy of out (the heads' unscaled-gradient input) */
+  float* stack0;           /* forward: latent0 copied here (block 0 of a [T + 1][M][256] stack whose rest is out) */
+  const float* g0;         /* backward: added to dlatent0 (the stack's block-0 gradient) */
 } muz_chain_args;
 /* wf / wb of count row-major [256][256] weights W[i] (y = x W): fwd + i * 65536 and bwd + i * 65536 hold them as
  * the MFMA A-operand stream of y = x W and of dx = dz W^T (one launch; call whenever the weights change). */
