@@ -25,6 +25,7 @@ sequential order stays the default everywhere (``bench.py --workload train`` wit
 """
 from __future__ import annotations
 
+import os
 import threading
 
 
@@ -41,6 +42,11 @@ class OverlappedIterations:
         self.is_actor, self.is_learner = bool(is_actor), bool(is_learner)
         self.play, self.train, self.deliver, self.publish = play, train, deliver, publish
         self.concurrent = bool(concurrent)
+        if self.concurrent and self.is_actor and self.is_learner:
+            # the DOG search beside a learner on the same GPU keeps 8 games per workgroup (188 workgroups at 1500
+            # games, one per CU, 68 CUs left to the learner) instead of the standalone 6 (250): the overlapped DOG
+            # iteration 11.98 -> 8.29 s (profiles/r5zk_dog_train.log).  (An explicit MUZ_DOG_GPW wins.)
+            os.environ.setdefault("MUZ_DOG_GPW", "8")
         self.i = 0
         self.pending = _Done()
 
