@@ -87,6 +87,7 @@ template <class Sync>
 __device__ void dog_deal(const DetConsts& c, DogG& s, unsigned long long seed, int gid, int lane) {
   const int P = c.P;
   const int q = s.hand_size;
+  const unsigned deal = s.deal;
   if (lane == 0) {
     int tot = 0;
     for (int k = 0; k < kDogCards; ++k) tot += s.deck[k];
@@ -94,13 +95,20 @@ __device__ void dog_deal(const DetConsts& c, DogG& s, unsigned long long seed, i
       for (int k = 0; k < kDogCards; ++k) s.deck[k] = 8;
       s.deck[0] = 8;
     }
-    int p = 0;
-    for (int k = 0; k < kDogCards; ++k)
-      for (int j = 0; j < s.deck[k] && p < kMaxPool; ++j) s.pool[p++] = (int8_t)k;
-    for (; p < kMaxPool; ++p) s.pool[p] = (int8_t)kDogCards;   // dummies
   }
   Sync()();
-  for (int k = lane; k < kMaxPool; k += Sync::N) s.key[k] = s.pool[k] == kDogCards ? 2.0f : deal_key(seed, gid, s.deal, k);
+  // the pool in deck order (entry k: the card whose running count covers k; dummies past the deck) and its sort
+  // keys, one entry per lane (lane 0 filled it serially before: ~120 dependent LDS writes per deal)
+  for (int k = lane; k < kMaxPool; k += Sync::N) {
+    int acc = 0, card = kDogCards;
+    for (int d = 0; d < kDogCards; ++d) {
+      const int n = s.deck[d];
+      if (card == kDogCards && k < acc + n) card = d;
+      acc += n;
+    }
+    s.pool[k] = (int8_t)card;
+    s.key[k] = card == kDogCards ? 2.0f : deal_key(seed, gid, deal, k);
+  }
   Sync()();
   // stable argsort: rank = #smaller keys + #equal keys at a lower index
   for (int k = lane; k < kMaxPool; k += Sync::N) {
@@ -113,22 +121,29 @@ __device__ void dog_deal(const DetConsts& c, DogG& s, unsigned long long seed, i
     s.shuffled[r] = s.pool[k];
   }
   Sync()();
-  if (lane == 0) {
+  // player p takes shuffled[p q .. p q + q): counted per (player, card) and per card in parallel (the same sums as
+  // the serial hand-by-hand increments)
+  const int qq = q < 6 ? q : 6;
+  for (int t = lane; t < P * kDogCards; t += Sync::N) {
+    const int p = t / kDogCards, card = t % kDogCards;
+    int n = 0;
+    for (int sl = 0; sl < qq; ++sl) n += s.shuffled[p * q + sl] == card;
+    s.hands[p][card] = (int8_t)(s.hands[p][card] + n);
+  }
+  for (int card = lane; card < kDogCards; card += Sync::N) {
+    int n = 0;
     for (int p = 0; p < P; ++p)
-      for (int sl = 0; sl < q && sl < 6; ++sl) {
-        const int card = s.shuffled[p * q + sl];
-        if (card < kDogCards) {
-          s.hands[p][card] = (int8_t)(s.hands[p][card] + 1);
-          s.deck[card] = (int8_t)(s.deck[card] - 1);
-        }
-      }
+      for (int sl = 0; sl < qq; ++sl) n += s.shuffled[p * q + sl] == card;
+    s.deck[card] = (int8_t)(s.deck[card] - n);
+  }
+  if (lane == 0) {
     const int rs = s.round_starter == -1 ? s.cp : (s.round_starter + 1) % P;
     s.cp = rs;
     s.round_starter = rs;
     for (int i = 0; i < 4; ++i) s.swap_choices[i] = -1;
     s.phase = (has(c.flags, R_TEAMS) && P == 4) ? 1 : 0;
     s.hand_size = q == 2 ? 6 : q - 1;
-    s.deal = s.deal + 1;
+    s.deal = deal + 1;
   }
   Sync()();
 }
