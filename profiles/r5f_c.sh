@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5 end check after the learner launch reductions: the full GPU suite and smoke.
 set -o pipefail
-O=gpurun_out/r5fc
+O=gpurun_out/${R5FC_OUT:-r5fc}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 \
