@@ -245,6 +245,9 @@ __global__ __launch_bounds__(kScanThreads) void k_ss_refill(DetConsts c, muz_det
 // alternatives measured: a decoupled look-back over the 512 workgroups, 262 us serial / 69 us 64-wide -- each poll
 // an agent-scope load across XCDs.)
 // counts: this turn's [searching, active, -, arrivals]; the next turn's four (the other parity) are zeroed here.
+// 32 games per workgroup (128 workgroups at 4096 lanes): the same-address atomics serialise, so fewer, larger
+// workgroups take fewer of them.
+constexpr int kHeadBlock = 1024;
 
 struct SpHead {
   uint32_t* legal;
@@ -261,9 +264,9 @@ struct SpHead {
 
 // STREAM: k_ss_refill's lane refill first (lane_game / next); otherwise lane g plays game g.
 template <bool STREAM>
-__global__ __launch_bounds__(kSpBlock) void k_sp_head(DetConsts c, muz_detmadn_soa st, int n, const int32_t* idx, int T,
+__global__ __launch_bounds__(kHeadBlock) void k_sp_head(DetConsts c, muz_detmadn_soa st, int n, const int32_t* idx, int T,
                                                       int32_t* lane_game, int32_t* next, int num_games, SpHead o) {
-  constexpr int G = kFlagLanes, NG = kSpBlock / G;
+  constexpr int G = kFlagLanes, NG = kHeadBlock / G;
   __shared__ int8_t sboard[NG][kCells];
   __shared__ int8_t sstate[NG][kStateRow];
   __shared__ __attribute__((aligned(16))) uint8_t senc[NG][kEncStride];
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_head(DetConsts c, muz_detmadn_s
   const int t = threadIdx.x, lg = t / G, a = t % G;
   const int b = blockIdx.x, nb = gridDim.x;
   const int g0 = b * NG, games = min(NG, n - g0), g = g0 + lg;
-  det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
+  det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kHeadBlock);
   if (t < NG) {
     s_gn[t] = -1;
     s_f[t] = 0;
@@ -303,7 +306,7 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_head(DetConsts c, muz_detmadn_s
     if (t < games && s_f[t]) lane_game[g0 + t] = s_gn[t];
     if (s_reset) {   // det_reset_lane on the LDS rows of the refilled lanes (stored back below)
       const bool fp = has(c.flags, R_FREE_PIN);
-      for (int i = t; i < NG * kCells; i += kSpBlock) {
+      for (int i = t; i < NG * kCells; i += kHeadBlock) {
         const int gi = i / kCells, cell = i % kCells;
         if (gi < games && s_f[gi] && s_gn[gi] >= 0) {
           int v = -1;
@@ -312,7 +315,7 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_head(DetConsts c, muz_detmadn_s
           sboard[gi][cell] = (int8_t)v;
         }
       }
-      for (int i = t; i < NG * kStateRow; i += kSpBlock) {
+      for (int i = t; i < NG * kStateRow; i += kHeadBlock) {
         const int gi = i / kStateRow, r = i % kStateRow;
         if (gi < games && s_f[gi] && s_gn[gi] >= 0) {
           int8_t v = sstate[gi][r];
@@ -353,8 +356,9 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_head(DetConsts c, muz_detmadn_s
       c1 += s_f[i] == 1;
       c2 += s_f[i] != 0;
     }
-    s_pre = c1 ? atomicAdd(&o.counts[0], c1) : 0;
-    if (c2) atomicAdd(&o.counts[1], c2);
+    // (searching, active) as one 64-bit add: counts[0] the low word, counts[1] the high word
+    const unsigned long long add = ((unsigned long long)(unsigned)c2 << 32) | (unsigned)c1;
+    s_pre = add ? (int)(unsigned)atomicAdd(reinterpret_cast<unsigned long long*>(o.counts), add) : 0;
     if (o.host_counts) {
       __threadfence();
       if (atomicAdd(&o.counts[3], 1) == nb - 1) {
@@ -406,7 +410,7 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_head(DetConsts c, muz_detmadn_s
       to[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
     }
   }
-  if (STREAM && s_reset) det_rows_store<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
+  if (STREAM && s_reset) det_rows_store<NG>(c, st, g0, games, sboard, sstate, t, kHeadBlock);
 }
 
 struct SpWs {
@@ -497,13 +501,14 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
     if (!led.proceed(turn)) break;
     const int nbk = (n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes);
 #if MUZ_SP_FUSED_HEAD
+    const int nbh = (n + kHeadBlock / kFlagLanes - 1) / (kHeadBlock / kFlagLanes);
     int32_t* const counts = ws.counts + 4 * (turn & 1);   // (the other parity: the next turn's, zeroed by the head)
     const SpHead h{ws.legal, ws.flag, ws.list, ws.slot, counts, ws.counts + 4 * ((turn + 1) & 1), ws.legal_c, ws.obs,
                    tr.obs, led.device_slot(turn)};
     if (lane_game)
-      k_sp_head<true><<<nbk, kSpBlock, 0, s>>>(c, st, n, tr.idx, T, ws.lane_game, ws.next_game, num_games, h);
+      k_sp_head<true><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, ws.lane_game, ws.next_game, num_games, h);
     else
-      k_sp_head<false><<<nbk, kSpBlock, 0, s>>>(c, st, n, tr.idx, T, nullptr, nullptr, num_games, h);
+      k_sp_head<false><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, nullptr, nullptr, num_games, h);
     if (h.host_counts) led.counts_written(turn);
     else led.counts(turn, counts);
 #else
