@@ -111,38 +111,28 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_encode_g(DetConsts c, muz_detma
 // Apply the searched action (env_step) or no_step, and write the trajectory record (game_agent.py:79-141): one
 // game per kFlagLanes lanes, like k_sp_flags_g -- the workgroup's SoA rows go through LDS both ways (coalesced),
 // lane 0 of a game steps it on its LDS rows (LdsLane), its lanes copy the 24 action weights into the record.
-__global__ __launch_bounds__(kSpBlock) void k_sp_apply_g(DetConsts c, muz_detmadn_soa st, const int32_t* flag,
-                                                         const int32_t* slot, const int32_t* s_action,
-                                                         const float* s_weights, const float* s_value, muz_traj tr,
-                                                         int n, const int32_t* lane_game, const uint32_t* legal) {
-  constexpr int G = kFlagLanes, NG = kSpBlock / G;
-  __shared__ int8_t sboard[NG][kCells];
-  __shared__ int8_t sstate[NG][kStateRow];
-  const int t = threadIdx.x, lg = t / G, a = t % G;
-  const int g0 = blockIdx.x * NG, games = min(NG, n - g0), g = g0 + lg;
-  det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
-  const int f = lg < games ? flag[g] : 0;
+// The apply of one game's searched action (or no_step) on its LDS rows and its trajectory record; lane a of the
+// game's G lanes, f / sl / leg: the game's flag, slot and legal mask of the turn being applied.
+template <int G>
+__device__ __forceinline__ void sp_apply_game(const DetConsts& c, int8_t* sp, int8_t* board, int f, int sl, uint32_t leg,
+                                              int gn, int tt, const int32_t* s_action, const float* s_weights,
+                                              const float* s_value, const muz_traj& tr, int a) {
   const int T = tr.max_steps;
-  const int gn = f ? (lane_game ? lane_game[g] : g) : 0;
-  const int tt = f ? tr.idx[gn] : 0;   // read by every lane of the game before lane 0 advances it
   const size_t rec = (size_t)gn * T + tt;
-  __syncthreads();
   if (f == 1 && a < MUZ_DET_ACTIONS)
-    tr.pol[rec * MUZ_DET_ACTIONS + a] = s_weights[(size_t)slot[g] * MUZ_DET_ACTIONS + a];
+    tr.pol[rec * MUZ_DET_ACTIONS + a] = s_weights[(size_t)sl * MUZ_DET_ACTIONS + a];
   if (f != 0 && a == 0) {
-    int8_t* sp = sstate[lg];
     LdsLane s{sp, sp[40], sp[41], sp[42]};
-    const BoardView b{sboard[lg], 1};
+    const BoardView b{board, 1};
     const bool teams = has(c.flags, R_TEAMS);
     const int cp_before = s.cp;
     const int team_before = teams ? cp_before % 2 : -1;
     int act, rew_cls, disc_cls;
     float val, mask;
     if (f == 1) {
-      const int sl = slot[g];
       act = s_action[sl];
-      // legal[g]: this state's mask from k_sp_flags_g (the state is unchanged since), so no second legality pass
-      const int r = det_step_masked(c, s, b, fdiv(act, 6), fmodp(act, 6) + 1, legal[g]);
+      // leg: this state's mask from the flags pass (the state is unchanged since), so no second legality pass
+      const int r = det_step_masked(c, s, b, fdiv(act, 6), fmodp(act, 6) + 1, leg);
       const bool nd = s.done != 0;
       const int next_player = s.cp;
       const int next_team = teams ? next_player % 2 : -1;
@@ -170,6 +160,23 @@ __global__ __launch_bounds__(kSpBlock) void k_sp_apply_g(DetConsts c, muz_detmad
     tr.discount[rec] = disc_cls;
     tr.idx[gn] = tt + 1;
   }
+}
+
+__global__ __launch_bounds__(kSpBlock) void k_sp_apply_g(DetConsts c, muz_detmadn_soa st, const int32_t* flag,
+                                                         const int32_t* slot, const int32_t* s_action,
+                                                         const float* s_weights, const float* s_value, muz_traj tr,
+                                                         int n, const int32_t* lane_game, const uint32_t* legal) {
+  constexpr int G = kFlagLanes, NG = kSpBlock / G;
+  __shared__ int8_t sboard[NG][kCells];
+  __shared__ int8_t sstate[NG][kStateRow];
+  const int t = threadIdx.x, lg = t / G, a = t % G;
+  const int g0 = blockIdx.x * NG, games = min(NG, n - g0), g = g0 + lg;
+  det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
+  const int f = lg < games ? flag[g] : 0;
+  const int gn = f ? (lane_game ? lane_game[g] : g) : 0;
+  const int tt = f ? tr.idx[gn] : 0;   // read by every lane of the game before lane 0 advances it
+  __syncthreads();
+  if (f) sp_apply_game<G>(c, sstate[lg], sboard[lg], f, slot[g], legal[g], gn, tt, s_action, s_weights, s_value, tr, a);
   __syncthreads();
   det_rows_store<NG>(c, st, g0, games, sboard, sstate, t, kSpBlock);
 }
@@ -260,10 +267,17 @@ struct SpHead {
   float* obs;
   int8_t* traj_obs;
   int32_t* host_counts;   // the turn's pinned ledger slot (device-visible), or null
+  // APPLY: the previous turn's search results, applied first (what k_sp_apply_g did at the end of that turn)
+  const int32_t* s_action;
+  const float* s_weights;
+  const float* s_value;
+  muz_traj tr;
 };
 
 // STREAM: k_ss_refill's lane refill first (lane_game / next); otherwise lane g plays game g.
-template <bool STREAM>
+// APPLY: the previous turn's apply first (k_sp_apply_g, on the rows this launch loads anyway): one launch and one
+// round trip of the rows fewer per turn.
+template <bool STREAM, bool APPLY>
 __global__ __launch_bounds__(kHeadBlock) void k_sp_head(DetConsts c, muz_detmadn_soa st, int n, const int32_t* idx, int T,
                                                       int32_t* lane_game, int32_t* next, int num_games, SpHead o) {
   constexpr int G = kFlagLanes, NG = kHeadBlock / G;
@@ -275,6 +289,17 @@ __global__ __launch_bounds__(kHeadBlock) void k_sp_head(DetConsts c, muz_detmadn
   const int b = blockIdx.x, nb = gridDim.x;
   const int g0 = b * NG, games = min(NG, n - g0), g = g0 + lg;
   det_rows_load<NG>(c, st, g0, games, sboard, sstate, t, kHeadBlock);
+  int fprev = 0, slprev = 0, gnprev = 0, ttprev = 0;
+  uint32_t legprev = 0;
+  if (APPLY && lg < games) {   // the previous turn's flag / slot / mask, read before this turn's passes rewrite them
+    fprev = o.flag[g];
+    if (fprev) {
+      slprev = o.slot[g];
+      legprev = o.legal[g];
+      gnprev = STREAM ? lane_game[g] : g;
+      ttprev = idx[gnprev];
+    }
+  }
   if (t < NG) {
     s_gn[t] = -1;
     s_f[t] = 0;
@@ -282,6 +307,12 @@ __global__ __launch_bounds__(kHeadBlock) void k_sp_head(DetConsts c, muz_detmadn
   if (t == 0) s_reset = 0;
   if (b == 0 && t < 4) o.counts_next[t] = 0;
   __syncthreads();
+  if (APPLY) {
+    if (fprev)
+      sp_apply_game<G>(c, sstate[lg], sboard[lg], fprev, slprev, legprev, gnprev, ttprev, o.s_action, o.s_weights,
+                       o.s_value, o.tr, a);
+    __syncthreads();   // (the refill below reads the advanced idx and the new done flags)
+  }
   if constexpr (STREAM) {
     // refill (k_ss_refill): every lane whose game ended takes the next unplayed game number (next[0] counts the
     // numbers handed out, possibly past num_games: those lanes go idle)
@@ -410,7 +441,7 @@ __global__ __launch_bounds__(kHeadBlock) void k_sp_head(DetConsts c, muz_detmadn
       to[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
     }
   }
-  if (STREAM && s_reset) det_rows_store<NG>(c, st, g0, games, sboard, sstate, t, kHeadBlock);
+  if (APPLY || (STREAM && s_reset)) det_rows_store<NG>(c, st, g0, games, sboard, sstate, t, kHeadBlock);
 }
 
 struct SpWs {
@@ -496,6 +527,7 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
   if ((rc = led.begin())) return rc;
   MUZ_HIP_RET(hipMemsetAsync(ws.counts, 0, 8 * sizeof(int32_t), s));   // both parities of k_sp_head's counters
   int turns = 0;
+  bool pending = false;   // a turn's searched actions not applied yet
   rc = MUZ_OK;
   for (int turn = 0; turn < max_turns; ++turn) {
     if (!led.proceed(turn)) break;
@@ -504,11 +536,19 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
     const int nbh = (n + kHeadBlock / kFlagLanes - 1) / (kHeadBlock / kFlagLanes);
     int32_t* const counts = ws.counts + 4 * (turn & 1);   // (the other parity: the next turn's, zeroed by the head)
     const SpHead h{ws.legal, ws.flag, ws.list, ws.slot, counts, ws.counts + 4 * ((turn + 1) & 1), ws.legal_c, ws.obs,
-                   tr.obs, led.device_slot(turn)};
-    if (lane_game)
-      k_sp_head<true><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, ws.lane_game, ws.next_game, num_games, h);
-    else
-      k_sp_head<false><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, nullptr, nullptr, num_games, h);
+                   tr.obs, led.device_slot(turn), ws.action, ws.weights, ws.value, tr};
+    if (lane_game) {
+      if (pending)
+        k_sp_head<true, true><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, ws.lane_game, ws.next_game, num_games, h);
+      else
+        k_sp_head<true, false><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, ws.lane_game, ws.next_game, num_games, h);
+    } else {
+      if (pending)
+        k_sp_head<false, true><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, nullptr, nullptr, num_games, h);
+      else
+        k_sp_head<false, false><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, nullptr, nullptr, num_games, h);
+    }
+    pending = false;
     if (h.host_counts) led.counts_written(turn);
     else led.counts(turn, counts);
 #else
@@ -531,10 +571,19 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
                                    ws.value, s)))
       break;
     led.search_end(turn);
-    k_sp_apply_g<<<(n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes), kSpBlock, 0, s>>>(
-        c, st, ws.flag, ws.slot, ws.action, ws.weights, ws.value, tr, n, lane_game, ws.legal);
+#if MUZ_SP_FUSED_HEAD
+    pending = true;   // applied by the next turn's head (or after the loop)
+#else
+    k_sp_apply_g<<<nbk, kSpBlock, 0, s>>>(c, st, ws.flag, ws.slot, ws.action, ws.weights, ws.value, tr, n, lane_game,
+                                          ws.legal);
+#endif
     if ((rc = muz_last_launch_error())) break;
     ++turns;
+  }
+  if (pending && rc == MUZ_OK) {   // the last launched turn's apply
+    k_sp_apply_g<<<(n + kSpBlock / kFlagLanes - 1) / (kSpBlock / kFlagLanes), kSpBlock, 0, s>>>(
+        c, st, ws.flag, ws.slot, ws.action, ws.weights, ws.value, tr, n, lane_game, ws.legal);
+    rc = muz_last_launch_error();
   }
   led.finish(turns, stats);
   return rc;
