@@ -2,7 +2,7 @@
 # Round 5 final, part A: the full GPU suite, smoke, the headline bench line (default flags) and its rocprofv3 kernel
 # statistics (--steps 2 --warmup 1).
 set -o pipefail
-O=gpurun_out/r5f
+O=gpurun_out/${R5F_OUT:-r5f}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 \
