@@ -2,7 +2,7 @@
 # Round 5 final, part B: the other workload lines (default flags): DOG MuZero self-play at 1500 games, DOG random
 # policy, classic MADN, and the DOG train loop (--overlap).
 set -o pipefail
-O=gpurun_out/r5f
+O=gpurun_out/${R5F_OUT:-r5f}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 python3 bench.py --workload dog --policy muzero > $O/dog_mz.json 2> $O/dog_mz.err || { tail -20 $O/dog_mz.err; exit 1; }
