@@ -20,15 +20,17 @@ struct SearchArgs {
   int games_per_wg = 8;   // k_dog_search one-game-per-wave form: games per workgroup (<= 8; MUZ_DOG_GPW)
 };
 
+// host_counts (optional): the self-play ledger's mapped pinned slot; k_repr_conv's first workgroup copies n_dev[0..1]
+// (the turn's searching / active counts, final once the turn head has run) into it
 int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv_scratch,
-                          float* logits, float* value, float* emb, hipStream_t s);
+                          float* logits, float* value, float* emb, hipStream_t s, int32_t* host_counts = nullptr);
 
 int launch_root_inference(const muz_classic_net_w& w, const float* obs, int n, const int* n_dev, float* conv_scratch,
                           float* logits, float* value, float* emb, hipStream_t s);
 
 // k_repr_conv (RepresentationNetwork2's convolutions, nets.hip) and k_film (the per-action FiLM table)
 int launch_repr_conv(const muz_repr_w& r, const float* obs, int C, int n, const int* n_dev, float* conv,
-                     hipStream_t s);
+                     hipStream_t s, int32_t* host_counts = nullptr);
 int launch_film(const muz_dyn_w& d, int A, hipStream_t s);
 
 int launch_gumbel_search(const muz_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,

@@ -76,7 +76,12 @@ __device__ __forceinline__ void conv_mfma(const AS4 muz_dense& L, const float* i
 }
 
 __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float* __restrict__ obs, int C, int n,
-                                                   const int* __restrict__ n_dev, float* __restrict__ convout) {
+                                                   const int* __restrict__ n_dev, float* __restrict__ convout,
+                                                   int32_t* host_counts) {
+  if (host_counts && blockIdx.x == 0 && threadIdx.x == 0) {   // (n_dev set: the self-play turn's counts)
+    __hip_atomic_store(&host_counts[0], n_dev[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host_counts[1], n_dev[1], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (n_dev) n = *n_dev;
   if ((int)blockIdx.x >= n) return;
   const AS4 muz_repr_w& R = *kernarg0<muz_repr_w>();   // == Rarg, read through the kernarg segment
@@ -215,8 +220,9 @@ int check_net(const muz_net_w* w) {
 }
 
 int launch_repr_conv(const muz_repr_w& r, const float* obs, int C, int n, const int* n_dev, float* conv,
-                     hipStream_t s) {
-  k_repr_conv<<<n, 256, 0, s>>>(r, obs, C, n, n_dev, conv);
+                     hipStream_t s, int32_t* host_counts) {
+  if (host_counts && !n_dev) return MUZ_E_INVALID;
+  k_repr_conv<<<n, 256, 0, s>>>(r, obs, C, n, n_dev, conv, host_counts);
   return muz_last_launch_error();
 }
 
@@ -227,16 +233,16 @@ int launch_film(const muz_dyn_w& d, int A, hipStream_t s) {
 
 template <class NW>
 static int launch_root_impl(const NW& w, const float* obs, int n, const int* n_dev, float* conv, float* logits,
-                            float* value, float* emb, hipStream_t s) {
-  int rc = launch_repr_conv(w.repr, obs, w.obs_channels, n, n_dev, conv, s);
+                            float* value, float* emb, hipStream_t s, int32_t* host_counts = nullptr) {
+  int rc = launch_repr_conv(w.repr, obs, w.obs_channels, n, n_dev, conv, s, host_counts);
   if (rc) return rc;
   k_root_dense<NW><<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, obs, conv, n, n_dev, logits, value, emb);
   return muz_last_launch_error();
 }
 
 int launch_root_inference(const muz_net_w& w, const float* obs, int n, const int* n_dev, float* conv, float* logits,
-                          float* value, float* emb, hipStream_t s) {
-  return launch_root_impl(w, obs, n, n_dev, conv, logits, value, emb, s);
+                          float* value, float* emb, hipStream_t s, int32_t* host_counts) {
+  return launch_root_impl(w, obs, n, n_dev, conv, logits, value, emb, s, host_counts);
 }
 
 int launch_root_inference(const muz_classic_net_w& w, const float* obs, int n, const int* n_dev, float* conv,

@@ -535,8 +535,10 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
 #if MUZ_SP_FUSED_HEAD
     const int nbh = (n + kHeadBlock / kFlagLanes - 1) / (kHeadBlock / kFlagLanes);
     int32_t* const counts = ws.counts + 4 * (turn & 1);   // (the other parity: the next turn's, zeroed by the head)
+    // (the ledger's counts reach the host through root inference's first kernel: no last-arrival ticket here)
+    int32_t* const host_counts = led.device_slot(turn);
     const SpHead h{ws.legal, ws.flag, ws.list, ws.slot, counts, ws.counts + 4 * ((turn + 1) & 1), ws.legal_c, ws.obs,
-                   tr.obs, led.device_slot(turn), ws.action, ws.weights, ws.value, tr};
+                   tr.obs, nullptr, ws.action, ws.weights, ws.value, tr};
     if (lane_game) {
       if (pending)
         k_sp_head<true, true><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, ws.lane_game, ws.next_game, num_games, h);
@@ -549,9 +551,9 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
         k_sp_head<false, false><<<nbh, kHeadBlock, 0, s>>>(c, st, n, tr.idx, T, nullptr, nullptr, num_games, h);
     }
     pending = false;
-    if (h.host_counts) led.counts_written(turn);
-    else led.counts(turn, counts);
+    if (!host_counts) led.counts(turn, counts);
 #else
+    int32_t* const host_counts = nullptr;
     int32_t* const counts = ws.counts;
     if (lane_game)
       k_ss_refill<<<1, kScanThreads, 0, s>>>(c, st, ws.lane_game, tr.idx, T, ws.next_game, num_games, n);
@@ -563,8 +565,9 @@ static int sp_turns(const DetConsts& c, const muz_net_w* w, const muz_search_cfg
 #endif
     if ((rc = muz_last_launch_error())) break;
     if ((rc = launch_root_inference(*w, ws.obs, n, counts, ws.conv, ws.root_logits, ws.root_value, ws.root_emb,
-                                    s)))
+                                    s, host_counts)))
       break;
+    if (host_counts) led.counts_written(turn);
     sa.turn = turn;
     led.search_begin(turn);
     if ((rc = launch_gumbel_search(*w, sa, ws.root_logits, ws.root_value, ws.root_emb, ws.legal_c, nullptr, ws.list, n, counts, ws.tree, ws.action, ws.weights,
