@@ -489,9 +489,8 @@ def run_dog_muzero(args):
     achieved = args.batch * args.sims * DOG_MZ_EXEC_FLOP_PER_SIM / (avg_ms * 1e-3) / 1e12
     achieved_alg = args.batch * args.sims * DOG_MZ_FLOP_PER_SIM / (avg_ms * 1e-3) / 1e12
     traffic, traffic_src = measured_traffic("dog_traffic", "k_dog_search")
-    # k_dog_search's games per workgroup (dog_search.hip muz_dog_gumbel_search): one per wave up to 2048 games
-    rows_env = os.environ.get("MUZ_DOG_TILE_ROWS")
-    gpw = 8 if ((rows_env == "8") if rows_env else args.batch <= 2048) else 16
+    # k_dog_search's games per workgroup as the library launches it (was hard-coded)
+    gpw = int(clib.muz_dog_search_games_per_workgroup(args.batch))
     out = {
         "metric": "self-play env steps/sec + MCTS sims/sec, DOG 2v2 MuZero policy (config d, DOG MuZero slice)",
         "value": round(steps_done / elapsed, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
@@ -513,7 +512,7 @@ def run_dog_muzero(args):
                      "traffic": None if traffic is None else round(traffic),
                      "traffic_achieved_tbs": None if traffic is None else round(traffic / (avg_ms * 1e-3) / 1e12, 3),
                      "traffic_source": traffic_src,
-                     "note": f"{gpw} games per 16-row workgroup ({'one per wave' if gpw == 8 else 'two per wave'}): "
+                     "note": f"{gpw} games per 16-row workgroup ({'two per wave' if gpw == 16 else 'one per wave'}): "
                              f"{args.batch} games occupy {-(-args.batch // gpw)} of the 256 CUs; a workgroup's "
                              f"search time is its serial chain of 100 simulations"},
     }
@@ -691,7 +690,7 @@ def run_classic(args):
 
 
 def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, games, stats, C, is_actor, is_learner,
-                      learner_rank, empty_packed, A=24):
+                      learner_rank, A=24):
     """--workload train --overlap: pipeline.OverlappedIterations with this process's roles.  1 GPU: self-play in
     a worker thread on its own stream while the learner's graph replays on another; N ranks: actors play while
     the learner trains, then gather_packed + an async weight broadcast.  Returns the timed region's seconds."""
@@ -727,23 +726,22 @@ def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, 
             with torch.cuda.stream(s_learn):
                 ring.save_games_from_buffers(got)
             return
-        packed = got if is_actor else empty_packed(C, device)
-        recv = TR.gather_packed(packed, C, A, dst=learner_rank)
+        with torch.cuda.stream(s_learn if is_learner else torch.cuda.current_stream(device)):
+            TR.deliver_to_learner(got if is_actor else None, ring, C, A, learner_rank, device=device)
         if is_learner:
-            with torch.cuda.stream(s_learn):
-                for r, p in enumerate(recv):
-                    if r != learner_rank:
-                        ring.save_packed(p)
             s_learn.synchronize()
 
     def publish(i):
-        if is_learner:
+        if world == 1:
             with torch.cuda.stream(s_learn):
                 learner.push_to(net)
             s_learn.synchronize()
-        if world == 1:
             return PL._Done()
-        return TR.broadcast_weights_async(net, src=learner_rank)
+        with torch.cuda.stream(s_learn if is_learner else torch.cuda.current_stream(device)):
+            handle = TR.publish_weights(net, learner, learner_rank, async_op=True)
+        if is_learner:
+            s_learn.synchronize()
+        return handle
 
     loop = PL.OverlappedIterations(is_actor=is_actor, is_learner=is_learner, play=play, train=train, deliver=deliver,
                                    publish=publish, concurrent=(world == 1))
@@ -829,12 +827,7 @@ def run_train(args):
         if world == 1:
             ring.save_games_from_buffers(buf)
         else:
-            packed = TR.pack(buf) if is_actor else _empty_packed(C, device)
-            got = TR.gather_packed(packed, C, A, dst=learner_rank)
-            if is_learner:
-                for r, p in enumerate(got):
-                    if r != learner_rank:
-                        ring.save_packed(p)
+            TR.deliver_to_learner(TR.pack(buf) if is_actor else None, ring, C, A, learner_rank, device=device)
         if is_learner:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -844,19 +837,14 @@ def run_train(args):
             e1.synchronize()
             stats["learner_ms"] += e0.elapsed_time(e1)
             stats["train_steps"] += train_steps
-            learner.push_to(net)
+            if world == 1:
+                learner.push_to(net)
         if world > 1:
-            TR.broadcast_weights(net, src=learner_rank)
-
-    def _empty_packed(C, dev):
-        z = {name: torch.empty((0,) + shp, dtype=dt, device=dev) for name, dt, shp in TR.fields(C, A, False)}
-        z["idx"] = torch.empty((0,), dtype=torch.int32, device=dev)
-        z["row_offset"] = torch.empty((0,), dtype=torch.int64, device=dev)
-        return z
+            TR.publish_weights(net, learner, learner_rank)
 
     if args.overlap:
         elapsed = _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, games, stats, C,
-                                    is_actor, is_learner, learner_rank, _empty_packed, A)
+                                    is_actor, is_learner, learner_rank, A)
     else:
         for w in range(max(args.warmup, 1)):       # fills the ring and captures the learner's HIP graph
             iteration(100 * w, 2)

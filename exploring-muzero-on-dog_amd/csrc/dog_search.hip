@@ -954,11 +954,30 @@ int check_dog_net(const muz_dog_net_w* w);
 
 using namespace muz;
 
+// one game per wave while the grid fits the chip's 256 CUs; MUZ_DOG_TILE_ROWS=8 / 16 forces either form
+static bool dog_search_sparse(int n) {
+  if (const char* e = getenv("MUZ_DOG_TILE_ROWS")) return atoi(e) == 8;
+  return n <= 2048;
+}
+
+// games per workgroup of the one-game-per-wave form: fewer than 8 while the grid still fits the chip's 256 CUs
+// (a simulation waits for the slowest of the workgroup's walks): 6 at the reference's 1500 games, 250 workgroups
+// -- 0.8 % faster than 8 (profiles/r5zb_dog_gpw_ab.log; 7: 0.2 % slower); MUZ_DOG_GPW overrides
+static int dog_search_gpw(int n) {
+  if (const char* e = getenv("MUZ_DOG_GPW")) return std::min(8, std::max(1, atoi(e)));
+  return std::min(8, std::max(6, (n + 255) / 256));
+}
+
 extern "C" {
 
 int64_t muz_dog_search_workspace_bytes(int32_t n, const muz_search_cfg* cfg) {
   if (!cfg || n < 0) return -1;
   return dog_search_workspace_bytes(n, cfg->num_simulations);
+}
+
+int32_t muz_dog_search_games_per_workgroup(int32_t n) {
+  if (n < 0) return -1;
+  return dog_search_sparse(n) ? dog_search_gpw(n) : 16;
 }
 
 int muz_dog_gumbel_search(const muz_dog_net_w* w, const muz_search_cfg* cfg, const float* root_logits,
@@ -988,14 +1007,8 @@ int muz_dog_gumbel_search(const muz_dog_net_w* w, const muz_search_cfg* cfg, con
     const char* e = getenv("MUZ_DOG_EXACT_SELECT");
     sa.exact_select = e && e[0] == '1';
   }
-  // one game per wave while the grid fits the chip's 256 CUs; MUZ_DOG_TILE_ROWS=8 / 16 forces either form
-  bool sparse = n <= 2048;
-  if (const char* e = getenv("MUZ_DOG_TILE_ROWS")) sparse = atoi(e) == 8;
-  // games per workgroup of the one-game-per-wave form: fewer than 8 while the grid still fits the chip's 256 CUs
-  // (a simulation waits for the slowest of the workgroup's walks): 6 at the reference's 1500 games, 250 workgroups
-  // -- 0.8 % faster than 8 (profiles/r5zb_dog_gpw_ab.log; 7: 0.2 % slower)
-  sa.games_per_wg = std::min(8, std::max(6, (n + 255) / 256));
-  if (const char* e = getenv("MUZ_DOG_GPW")) sa.games_per_wg = std::min(8, std::max(1, atoi(e)));
+  const bool sparse = dog_search_sparse(n);
+  sa.games_per_wg = dog_search_gpw(n);
   return launch_dog_search(*w, sa, root_logits, root_value, root_embedding, legal, gumbel, n, workspace, action,
                            action_weights, root_value_out, sparse, (hipStream_t)stream);
 }

@@ -179,10 +179,10 @@ __global__ __launch_bounds__(kLossThreads) void k_loss_heads(muz_loss_args g) {
     for (int j = 0; j < 3; ++j)
       if (j < nt && k < K && g.term[j].labels) lab[j] = g.term[j].labels[(size_t)b * g.term[j].ld + k];
     const float d = val - tv;
-    v[0] = m * d * d;
+    v[0] += m * d * d;
     g.dvalue[row] = g.scale_value * invB * m * 2.0f * d;
     if (g.A <= kLossMaxA)
-      v[1] = m * loss_ce_row<kLossMaxA>(g.logits + row * g.A, g.dlogits + row * g.A, g.A, -1,
+      v[1] += m * loss_ce_row<kLossMaxA>(g.logits + row * g.A, g.dlogits + row * g.A, g.A, -1,
                                         g.policies + ((size_t)b * g.T + k) * g.A, g.scale_policy * invB * m);
     if (k < K) {
 #pragma unroll

@@ -14,8 +14,10 @@
 //     mu = b1 mu + (1 - b1) g;  nu = b2 nu + (1 - b2) g^2
 //     p -= lr * (mu / c1 / (sqrt(nu / c2) + eps) + wd p),  c_i = 1 - b_i^(step), lr = lr(step - 1)
 //   with the scalars in float64 on the device as learner.AdamW computes them.
-// Tensors travel in the kernel arguments, kAdamMaxTensors per launch (no device pointer table: nothing to
-// upload, so the step stays capturable in a HIP graph).
+// muz_adamw_step: the tensors travel in the kernel arguments, kAdamMaxTensors per launch (nothing to upload, so
+// the step is capturable in a HIP graph as it stands).  muz_adamw_step_table: one launch per pass over a
+// caller-owned device table (muz_adamw_table_write, eager and blocking); the caller keeps that table unchanged
+// for as long as a graph that captured the step may replay (learner.AdamW keeps one table per pointer set).
 #include "launch.hpp"
 
 #include <math.h>
@@ -245,9 +247,29 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_update_t(const AdamDesc* 
   }
 }
 
-// scratch layout: [stepbuf f64][partials f32 x nchunks][pad to 16 B][AdamDesc x ntensors][cstart i32 x (ntensors + 1)]
-static size_t adam_table_offset(int64_t nchunks) { return ((size_t)(8 + 4 * nchunks) + 15) / 16 * 16; }
+// scratch layout: [stepbuf f64][partials f32 x nchunks]
+// table layout (muz_adamw_table_*): [AdamDesc x ntensors][cstart i32 x (ntensors + 1)]
 static size_t adam_table_bytes(int ntensors) { return sizeof(AdamDesc) * ntensors + 4 * (size_t)(ntensors + 1); }
+
+static int adam_hyper(AdamHyper& h, float max_norm, double b1, double b2, float eps, float weight_decay, double lr0,
+                      double steps_per_iteration, const double* boundaries, int32_t nb) {
+  if (nb < 0 || nb > kAdamMaxBounds || (nb && !boundaries)) return MUZ_E_INVALID;
+  h = AdamHyper{};
+  h.b1 = b1, h.b2 = b2, h.lr0 = lr0, h.spi = steps_per_iteration;
+  for (int j = 0; j < nb; ++j) h.bound[j] = boundaries[2 * j], h.factor[j] = boundaries[2 * j + 1];
+  h.max_norm = max_norm, h.eps = eps, h.wd = weight_decay, h.nb = nb;
+  return MUZ_OK;
+}
+
+// chunks over all tensors (-1: a negative size or more than 2^30 chunks)
+static int64_t adam_total_chunks(const int64_t* numel, int32_t ntensors) {
+  int64_t total = 0;
+  for (int i = 0; i < ntensors; ++i) {
+    if (numel[i] < 0) return -1;
+    total += adam_chunks(numel[i]);
+  }
+  return total > (1 << 30) ? -1 : total;
+}
 
 }  // namespace muz
 
@@ -257,36 +279,85 @@ extern "C" {
 
 int64_t muz_adamw_scratch_bytes(int32_t ntensors, const int64_t* numel) {
   if (ntensors < 0 || (ntensors && !numel)) return -1;
-  int64_t c = 0;
+  const int64_t c = adam_total_chunks(numel, ntensors);
+  return c < 0 ? -1 : 8 + 4 * c;
+}
+
+int64_t muz_adamw_table_bytes(int32_t ntensors) {
+  return ntensors < 0 ? -1 : (int64_t)adam_table_bytes(ntensors);
+}
+
+int muz_adamw_table_write(void* table, float* const* params, const float* const* grads, float* const* mu,
+                          float* const* nu, const int64_t* numel, int32_t ntensors, void* stream) {
+  if (ntensors < 0 || !table || (ntensors && (!params || !grads || !mu || !nu || !numel))) return MUZ_E_INVALID;
+  if (adam_total_chunks(numel, ntensors) < 0) return MUZ_E_INVALID;
+  std::vector<char> tab(adam_table_bytes(ntensors), 0);
+  AdamDesc* dd = reinterpret_cast<AdamDesc*>(tab.data());
+  int* cs = reinterpret_cast<int*>(tab.data() + sizeof(AdamDesc) * ntensors);
+  int nz = 0, c = 0;
   for (int i = 0; i < ntensors; ++i) {
-    if (numel[i] < 0) return -1;
-    c += adam_chunks(numel[i]);
+    if (!numel[i]) continue;
+    if (!params[i] || !mu[i] || !nu[i]) return MUZ_E_INVALID;
+    dd[nz] = AdamDesc{params[i], grads[i], mu[i], nu[i], numel[i]};
+    cs[nz++] = c;
+    c += (int)adam_chunks(numel[i]);
   }
-  return (int64_t)(adam_table_offset(c) + adam_table_bytes(ntensors));
+  cs[nz] = c;
+  hipStream_t s = (hipStream_t)stream;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  MUZ_HIP_RET(hipStreamIsCapturing(s, &cap));
+  if (cap != hipStreamCaptureStatusNone) return MUZ_E_INVALID;   // a table is written eagerly, never captured
+  // stream-ordered after earlier steps that read the table, and complete before the host vector goes away
+  MUZ_HIP_RET(hipMemcpyAsync(table, tab.data(), tab.size(), hipMemcpyHostToDevice, s));
+  MUZ_HIP_RET(hipStreamSynchronize(s));
+  return MUZ_OK;
+}
+
+int muz_adamw_step_table(const void* table, const int64_t* numel, int32_t ntensors, double* count, void* scratch,
+                         float* gnorm, float max_norm, double b1, double b2, float eps, float weight_decay, double lr0,
+                         double steps_per_iteration, const double* boundaries, int32_t nb, void* stream) {
+  if (ntensors < 0 || !table || !count || !scratch || !gnorm || (ntensors && !numel)) return MUZ_E_INVALID;
+  AdamHyper h;
+  if (int rc = adam_hyper(h, max_norm, b1, b2, eps, weight_decay, lr0, steps_per_iteration, boundaries, nb))
+    return rc;
+  const int64_t total = adam_total_chunks(numel, ntensors);
+  if (total < 0) return MUZ_E_INVALID;
+  if (total == 0) return MUZ_OK;
+  h.nchunks = (int)total;
+  int nz = 0;
+  for (int i = 0; i < ntensors; ++i) nz += numel[i] != 0;
+  double* stepbuf = (double*)scratch;
+  float* partial = (float*)((char*)scratch + 8);
+  hipStream_t s = (hipStream_t)stream;
+  const AdamDesc* ddev = reinterpret_cast<const AdamDesc*>(table);
+  const int* cdev = reinterpret_cast<const int*>((const char*)table + sizeof(AdamDesc) * ntensors);
+  k_adam_sqnorm_t<<<(int)total, kAdamThreads, 0, s>>>(ddev, cdev, nz, partial, count, stepbuf);
+  if (int rc = muz_last_launch_error()) return rc;
+  k_adam_update_t<<<(int)total, kAdamThreads, 0, s>>>(ddev, cdev, nz, partial, stepbuf, h, gnorm);
+  return muz_last_launch_error();
 }
 
 int muz_adamw_step(float* const* params, const float* const* grads, float* const* mu, float* const* nu,
                    const int64_t* numel, int32_t ntensors, double* count, void* scratch, float* gnorm,
                    float max_norm, double b1, double b2, float eps, float weight_decay, double lr0,
                    double steps_per_iteration, const double* boundaries, int32_t nb, void* stream) {
-  if (ntensors < 0 || nb < 0 || nb > kAdamMaxBounds || (nb && !boundaries)) return MUZ_E_INVALID;
+  if (ntensors < 0) return MUZ_E_INVALID;
   if (!count || !scratch || !gnorm || (ntensors && (!params || !grads || !mu || !nu || !numel))) return MUZ_E_INVALID;
-  AdamHyper h{};
-  h.b1 = b1, h.b2 = b2, h.lr0 = lr0, h.spi = steps_per_iteration;
-  for (int j = 0; j < nb; ++j) h.bound[j] = boundaries[2 * j], h.factor[j] = boundaries[2 * j + 1];
-  h.max_norm = max_norm, h.eps = eps, h.wd = weight_decay, h.nb = nb;
-  int64_t total = 0;
-  for (int i = 0; i < ntensors; ++i) {
+  AdamHyper h;
+  if (int rc = adam_hyper(h, max_norm, b1, b2, eps, weight_decay, lr0, steps_per_iteration, boundaries, nb))
+    return rc;
+  for (int i = 0; i < ntensors; ++i)
     if (numel[i] < 0 || (numel[i] && (!params[i] || !mu[i] || !nu[i]))) return MUZ_E_INVALID;
-    total += adam_chunks(numel[i]);
-  }
-  if (total == 0 || total > (1 << 30)) return total == 0 ? MUZ_OK : MUZ_E_INVALID;
+  const int64_t total = adam_total_chunks(numel, ntensors);
+  if (total < 0) return MUZ_E_INVALID;
+  if (total == 0) return MUZ_OK;
   h.nchunks = (int)total;
   double* stepbuf = (double*)scratch;
   float* partial = (float*)((char*)scratch + 8);
   hipStream_t s = (hipStream_t)stream;
 
-  // the launches' tables (tensors without elements are skipped)
+  // the tensors travel in the kernel arguments (copied at launch and at capture: nothing the host or a later
+  // call could change under a replayed graph); muz_adamw_step_table is the one-launch-per-pass form
   std::vector<AdamTable> tabs;
   int chunk = 0;
   for (int i = 0; i < ntensors; ++i) {
@@ -300,48 +371,6 @@ int muz_adamw_step(float* const* params, const float* const* grads, float* const
     t.p[t.n] = params[i], t.g[t.n] = grads[i], t.m[t.n] = mu[i], t.v[t.n] = nu[i];
     chunk += (int)adam_chunks(numel[i]);
     t.cstart[++t.n] = chunk - t.chunk0;
-  }
-  // one launch per pass with the table in the scratch: uploaded by an eager call; a graph capture reads the table an
-  // earlier eager call of the same step wrote (the host keeps the last upload per scratch buffer to check that)
-  {
-    std::vector<char> tab(adam_table_bytes(ntensors));
-    AdamDesc* dd = reinterpret_cast<AdamDesc*>(tab.data());
-    int* cs = reinterpret_cast<int*>(tab.data() + sizeof(AdamDesc) * ntensors);
-    int nz = 0, c = 0;
-    for (int i = 0; i < ntensors; ++i) {
-      if (!numel[i]) continue;
-      dd[nz] = AdamDesc{params[i], grads[i], mu[i], nu[i], numel[i]};
-      cs[nz++] = c;
-      c += (int)adam_chunks(numel[i]);
-    }
-    cs[nz] = c;
-    char* dev = (char*)scratch + adam_table_offset(total);
-    static std::vector<std::pair<void*, std::vector<char>>> uploaded;   // last table uploaded per scratch buffer
-    std::vector<char>* last = nullptr;
-    for (auto& u : uploaded)
-      if (u.first == scratch) last = &u.second;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    MUZ_HIP_RET(hipStreamIsCapturing(s, &cap));
-    bool ready = false;
-    if (cap == hipStreamCaptureStatusNone) {
-      if (!last) {
-        uploaded.emplace_back(scratch, std::vector<char>());
-        last = &uploaded.back().second;
-      }
-      *last = tab;
-      MUZ_HIP_RET(hipMemcpyAsync(dev, last->data(), tab.size(), hipMemcpyHostToDevice, s));
-      ready = true;
-    } else {
-      ready = last && *last == tab;   // captured: only if this exact table is already in the scratch
-    }
-    if (ready && nz > 0) {
-      const AdamDesc* ddev = reinterpret_cast<const AdamDesc*>(dev);
-      const int* cdev = reinterpret_cast<const int*>(dev + sizeof(AdamDesc) * ntensors);
-      k_adam_sqnorm_t<<<c, kAdamThreads, 0, s>>>(ddev, cdev, nz, partial, count, stepbuf);
-      if (int rc = muz_last_launch_error()) return rc;
-      k_adam_update_t<<<c, kAdamThreads, 0, s>>>(ddev, cdev, nz, partial, stepbuf, h, gnorm);
-      return muz_last_launch_error();
-    }
   }
   for (size_t k = 0; k < tabs.size(); ++k) {
     k_adam_sqnorm<<<tabs[k].cstart[tabs[k].n], kAdamThreads, 0, s>>>(tabs[k], partial, count, stepbuf);

@@ -133,6 +133,21 @@ REFERENCE_DTYPES = {"obs": torch.float32, "act": torch.int32, "rew": torch.int32
                     "discount": torch.int32, "idx": torch.int32}
 
 
+def reference_buffers(buf: dict, dtypes: dict) -> dict:
+    """Fresh copies of the engine's (reused) record buffers in the reference dtypes, with every row at or past a
+    game's ``idx`` as the reference's initial buffers hold it: zeros, ``team`` -1 (game_agent.py:158-169,
+    game_agent_stochastic.py:191-204).  The native loops write only rows below ``idx``."""
+    idx = buf["idx"].long()
+    past = torch.arange(buf["act"].shape[1], device=idx.device)[None, :] >= idx[:, None]
+    out = {}
+    for k, v in buf.items():
+        x = v.to(dtypes[k], copy=True)
+        if k != "idx":
+            x.masked_fill_(past.view(past.shape + (1,) * (x.dim() - 2)), -1 if k == "team" else 0)
+        out[k] = x
+    return out
+
+
 def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_depth, max_steps, temp,
                     rules: dict | None = None, obs_dtype=torch.float32) -> dict:
     """play_n_games_v3 (MuZero_det_MADN/game_agent.py:185-192), reference signature.
@@ -142,11 +157,12 @@ def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_
     ``input_shape``: (C, 56) with C = 8P + 2, which fixes the player count (the reference's game_agent
     plays P = 4, C = 34).  Returns the reference's buffer dict (game_agent.py:158-169): obs fp32
     [num_envs, max_steps, C, 56] (``obs_dtype=torch.int8`` keeps the engine's exact int8 copy), act / rew /
-    player / team / discount int32, val / mask fp32, pol fp32 [.., 24], idx int32 -- device tensors."""
+    player / team / discount int32, val / mask fp32, pol fp32 [.., 24], idx int32 -- fresh device tensors, rows past
+    ``idx`` zero (``team`` -1) as the reference initialises them."""
     C = int(input_shape[0])
     if (C - 2) % 8 or int(input_shape[-1]) != E.CELLS:
         raise ValueError(f"input_shape {tuple(input_shape)} is not (8P + 2, 56)")
     net = N.as_device_net(params, C)
     eng = cached_engine(net, num_envs, (C - 2) // 8, max_steps, num_simulation, max_depth, rules)
     buf = eng.play(N.rng_key_to_seed(rng_key), temp)
-    return {k: v.to(REFERENCE_DTYPES[k] if k != "obs" else obs_dtype) for k, v in buf.items()}
+    return reference_buffers(buf, dict(REFERENCE_DTYPES, obs=obs_dtype))

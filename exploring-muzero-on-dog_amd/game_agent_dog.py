@@ -160,5 +160,6 @@ def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_
         _ENGINE.clear()
         sp = _ENGINE[key] = DogSelfPlay(net, num_envs, num_simulation, max_depth, temp)
     buf = sp.play_stream(num_envs, max_steps, temperature=temp, seed=N.rng_key_to_seed(rng_key))
-    return {k: v.to(REFERENCE_DTYPES[k] if k != "obs" else obs_dtype) for k, v in buf.items()}
+    from .game_agent import reference_buffers
+    return reference_buffers(buf, dict(REFERENCE_DTYPES, obs=obs_dtype))   # copies: the engine reuses its buffers
 

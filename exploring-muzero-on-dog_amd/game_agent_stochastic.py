@@ -112,7 +112,7 @@ def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_
     params dict (or flat dict / DeviceClassicNet), int / uint32[2] key (the engine's counter RNG), input_shape
     (2P + 3, 56).  Returns the reference's buffers (obs fp32 unless ``obs_dtype``; dice int32, dice_dist fp32)
     as device tensors.  The reference's reset seeds only feed jax's unused random start."""
-    from .game_agent import REFERENCE_DTYPES
+    from .game_agent import REFERENCE_DTYPES, reference_buffers
     from .nets import rng_key_to_seed
     C = int(input_shape[0])
     if (C - 3) % 2 or int(input_shape[-1]) != E.CELLS:
@@ -128,4 +128,4 @@ def play_n_games_v3(params, rng_key, input_shape, num_envs, num_simulation, max_
     eng = hit
     buf = eng.play(rng_key_to_seed(rng_key), temp)
     dt = dict(REFERENCE_DTYPES, obs=obs_dtype, dice=torch.int32, dice_dist=torch.float32)
-    return {k: v.to(dt[k]) for k, v in buf.items()}
+    return reference_buffers(buf, dt)

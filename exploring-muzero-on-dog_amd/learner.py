@@ -1589,7 +1589,7 @@ class AdamW:
                 m=(ctypes.c_void_p * n)(*[q.data_ptr() for q in self.mu]),
                 v=(ctypes.c_void_p * n)(*[q.data_ptr() for q in self.nu]),
                 bounds=(ctypes.c_double * max(1, 2 * len(boundaries)))(*[float(x) for b in boundaries for x in b]),
-                gtype=ctypes.c_void_p * n)
+                gtype=ctypes.c_void_p * n, tables={}, max_tables=8)
 
     @torch.no_grad()
     def step(self):
@@ -1601,10 +1601,24 @@ class AdamW:
             if any(q.grad is not None and (q.grad.dtype != torch.float32 or not q.grad.is_contiguous())
                    for q in self.params):
                 raise ValueError("AdamW on the GPU takes contiguous float32 gradients")
-            _L.check(_L.load().muz_adamw_step(f["p"], grads, f["m"], f["v"], f["numel"], f["n"], _L.ptr(self.count),
-                                              _L.ptr(f["scratch"]), _L.ptr(f["gnorm"]), self.max_norm, self.b1, self.b2,
-                                              self.eps, self.wd, self.lr0, float(self.spi), f["bounds"],
-                                              len(self.boundaries), _L.stream_ptr()), "muz_adamw_step")
+            lib = _L.load()
+            # one device tensor table per gradient-pointer set, written once (eagerly) and never rewritten: a
+            # graph that captured a step keeps reading exactly the table it was captured with
+            key = tuple(grads[i] or 0 for i in range(f["n"]))
+            table = f["tables"].get(key)
+            if table is None and len(f["tables"]) < f["max_tables"] and not torch.cuda.is_current_stream_capturing():
+                table = torch.empty((lib.muz_adamw_table_bytes(f["n"]),), dtype=torch.uint8,
+                                    device=self.params[0].device)
+                _L.check(lib.muz_adamw_table_write(_L.ptr(table), f["p"], grads, f["m"], f["v"], f["numel"], f["n"],
+                                                   _L.stream_ptr()), "muz_adamw_table_write")
+                f["tables"][key] = table
+            hyper = (_L.ptr(self.count), _L.ptr(f["scratch"]), _L.ptr(f["gnorm"]), self.max_norm, self.b1, self.b2,
+                     self.eps, self.wd, self.lr0, float(self.spi), f["bounds"], len(self.boundaries), _L.stream_ptr())
+            if table is not None:
+                _L.check(lib.muz_adamw_step_table(_L.ptr(table), f["numel"], f["n"], *hyper), "muz_adamw_step_table")
+            else:   # first seen under capture, or too many pointer sets: the tensors go in the kernel arguments
+                _L.check(lib.muz_adamw_step(f["p"], grads, f["m"], f["v"], f["numel"], f["n"], *hyper),
+                         "muz_adamw_step")
             return f["gnorm"]
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
         # per-tensor norms in one multi-tensor kernel (a sum(g * g) per tensor was ~200 launches per step)

@@ -402,6 +402,11 @@ SIGNATURES = {
     "muz_adamw_step": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_double,
                                       ctypes.c_double, ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double,
                                       vp, ctypes.c_int32, vp]),
+    "muz_adamw_table_bytes": (ctypes.c_int64, [ctypes.c_int32]),
+    "muz_adamw_table_write": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, vp]),
+    "muz_adamw_step_table": (ctypes.c_int, [vp, vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_double,
+                                            ctypes.c_double, ctypes.c_float, ctypes.c_float, ctypes.c_double,
+                                            ctypes.c_double, vp, ctypes.c_int32, vp]),
     "muz_dog_net_prepare": (ctypes.c_int, [ctypes.POINTER(MuzDogNetW), vp]),
     "muz_dog_encode": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzDogSoA, vp, ctypes.c_int32, vp]),
     "muz_dog_nets_root": (ctypes.c_int, [ctypes.POINTER(MuzDogNetW), vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp,
@@ -409,6 +414,7 @@ SIGNATURES = {
     "muz_dog_nets_recurrent": (ctypes.c_int, [ctypes.POINTER(MuzDogNetW), vp, vp, ctypes.c_int32, vp, vp, vp, vp,
                                               vp, vp]),
     "muz_dog_search_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.POINTER(MuzSearchCfg)]),
+    "muz_dog_search_games_per_workgroup": (ctypes.c_int32, [ctypes.c_int32]),
     "muz_dog_gumbel_search": (ctypes.c_int, [ctypes.POINTER(MuzDogNetW), ctypes.POINTER(MuzSearchCfg), vp, vp, vp,
                                              vp, vp, ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp, vp]),
     "muz_detmadn_selfplay_stream": (ctypes.c_int, [ctypes.POINTER(MuzRules), ctypes.POINTER(MuzNetW),

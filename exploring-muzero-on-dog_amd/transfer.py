@@ -14,6 +14,9 @@ device -> host with ``np.array`` and are copied slot by slot (vec_replay_buffer.
   (``muz_ring_save_packed``).
 * ``broadcast_weights(net, src)``: the packed fp32 weight arena is ONE tensor, so a parameter update is
   one ``broadcast``; receivers re-derive their FiLM tables (``net.prepare()``).
+* ``deliver_to_learner`` / ``publish_weights``: config (e)'s two exchanges per iteration as bench.py's train
+  workload (and its multi-rank tests) run them -- every actor's packed games into the learner's ring, the learner's
+  new weights back to every rank.
 
 ``gather_packed`` / ``broadcast_weights`` are backend-agnostic (RCCL for device tensors, gloo for CPU
 tensors in the multi-process tests).
@@ -121,6 +124,54 @@ def gather_packed(packed: dict, obs_channels: int = 0, num_actions: int = 0, cha
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     return result
+
+
+def empty_packed(obs_channels: int, num_actions: int, device, chance: bool = False) -> dict:
+    """A rank's packed store without games (the learner's own part of a gather, or an actor with none)."""
+    z = {name: torch.empty((0,) + shp, dtype=dt, device=device) for name, dt, shp in fields(obs_channels, num_actions,
+                                                                                           chance)}
+    z["idx"] = torch.empty((0,), dtype=torch.int32, device=device)
+    z["row_offset"] = torch.empty((0,), dtype=torch.int64, device=device)
+    return z
+
+
+def deliver_to_learner(packed: dict | None, ring, obs_channels: int, num_actions: int, learner_rank: int,
+                       chance: bool = False, group=None, device=None) -> int:
+    """One iteration's finished games of every actor rank -> the learner rank's replay ring (config (e): the
+    reference's ``replay.save_games_from_buffers(buffers)`` after ``play_n_games_v3``, MuZero_DOG/train.py:255-268,
+    train_with_reward.py:255-268, with the actors on other GPUs).  A collective over all ranks of ``group``: each actor
+    passes its ``pack``ed rows, the learner passes None (its own part is empty) and its ring (any object with
+    ``save_packed``); the learner writes every actor's rows in rank order.  Returns the number of games the learner
+    saved (0 on an actor)."""
+    rank = dist.get_rank(group)
+    if rank == learner_rank:
+        if device is None:
+            device = getattr(ring, "device", "cpu")
+        packed = empty_packed(obs_channels, num_actions, device, chance)
+    elif packed is None:
+        raise ValueError("an actor rank must pass its packed games")
+    got = gather_packed(packed, obs_channels, num_actions, chance, dst=learner_rank, group=group)
+    if got is None:
+        return 0
+    n = 0
+    for r, p in enumerate(got):
+        if r != learner_rank and p["idx"].shape[0]:
+            ring.save_packed(p)
+            n += int(p["idx"].shape[0])
+    return n
+
+
+def publish_weights(net, learner, learner_rank: int, group=None, async_op: bool = False):
+    """The learner's new parameters -> every rank's self-play network (MuZero_DOG/train.py:276, where the next
+    play_n_games_v3 simply reads the updated ``params``): the learner rank packs them into its arena
+    (``learner.push_to(net)``), then one broadcast of the arena.  ``async_op``: returns the broadcast's handle
+    (``_WeightUpdate``; the overlapped loop waits on it before the next self-play call)."""
+    if dist.get_rank(group) == learner_rank:
+        learner.push_to(net)
+    if async_op:
+        return broadcast_weights_async(net, src=learner_rank, group=group)
+    broadcast_weights(net, src=learner_rank, group=group)
+    return None
 
 
 def broadcast_weights(net, src: int = 0, group=None):

@@ -958,6 +958,16 @@ int muz_adamw_step(float* const* params, const float* const* grads, float* const
                    const int64_t* numel, int32_t ntensors, double* count, void* scratch, float* gnorm,
                    float max_norm, double b1, double b2, float eps, float weight_decay, double lr0,
                    double steps_per_iteration, const double* boundaries, int32_t nb, void* stream);
+/* The same step in one launch per pass over a caller-owned device tensor table: muz_adamw_table_bytes(ntensors)
+ * device bytes, filled by muz_adamw_table_write (eager only -- MUZ_E_INVALID under stream capture; returns once the
+ * table is in device memory).  muz_adamw_step_table reads the table at run time, so a graph that captured it updates
+ * whatever the table holds at replay: keep it unchanged while such a graph may replay. */
+int64_t muz_adamw_table_bytes(int32_t ntensors);
+int muz_adamw_table_write(void* table, float* const* params, const float* const* grads, float* const* mu,
+                          float* const* nu, const int64_t* numel, int32_t ntensors, void* stream);
+int muz_adamw_step_table(const void* table, const int64_t* numel, int32_t ntensors, double* count, void* scratch,
+                         float* gnorm, float max_norm, double b1, double b2, float eps, float weight_decay, double lr0,
+                         double steps_per_iteration, const double* boundaries, int32_t nb, void* stream);
 
 /* ---- DOG MuZero slice (MuZero_DOG/muzero_dog.py, DOG/dog.py:1264-1272) -----------------------------------
  * The reference defines only the DOG RepresentationNetwork (muzero_dog.py:25-83: RepresentationNetwork2's trunk with
@@ -1005,6 +1015,9 @@ int64_t muz_dog_search_workspace_bytes(int32_t n, const muz_search_cfg* cfg /*ho
  * no_step), action_weights [n][806], root_value [n].  Results do not depend on the two environment switches it
  * reads (tests use them): MUZ_DOG_EXACT_SELECT=1 runs every interior selection over all 806 exponentials instead of
  * the certified argmax; MUZ_DOG_TILE_ROWS=8|16 forces one / two games per wave (default: one up to n = 2048). */
+/* Games per workgroup muz_dog_gumbel_search launches k_dog_search with for n games (reads the same environment
+ * switches: MUZ_DOG_TILE_ROWS, MUZ_DOG_GPW): 6-8 in the one-game-per-wave form, 16 in the two-per-wave form. */
+int32_t muz_dog_search_games_per_workgroup(int32_t n);
 int muz_dog_gumbel_search(const muz_dog_net_w* w /*host*/, const muz_search_cfg* cfg /*host*/,
                           const float* root_logits, const float* root_value, const float* root_embedding,
                           const uint32_t* legal, const float* gumbel, int32_t n, void* workspace,

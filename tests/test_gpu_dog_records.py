@@ -115,3 +115,45 @@ def test_dog_play_stream_finished_games(cuda):
         assert (b["team"][g, :L] == b["player"][g, :L] % 2).all()
     ref = GA.play_n_games_v3(net, 9, (34, 56), B, 2, 2, T, 1.0, obs_dtype=torch.int8)
     assert ref["idx"].shape == (B,) and int(ref["idx"].min()) > 0
+    # fresh copies with the reference's initial values past idx (zeros, team -1)
+    past = torch.arange(T, device="cuda")[None, :] >= ref["idx"][:, None].long()
+    assert bool((ref["team"][past] == -1).all()) and not bool(ref["pol"][past].any())
+    assert not bool(ref["obs"][past].any()) and not bool(ref["mask"][past].any())
+    eng = next(iter(GA._ENGINE.values()))
+    assert ref["act"].data_ptr() != eng._rec_cache["act"].data_ptr()
+
+
+def test_dog_records_packed_into_the_806_ring(cuda):
+    """Config (e)'s actor -> learner path at A = 806: DogSelfPlay.play_stream records, packed by
+    transfer.pack (the rows an actor rank sends) and written by save_packed into a [cap][T] ring with obs (34, 56)
+    int8 and 806-wide policies, equal -- ring and a seeded sample_batch, bit for bit -- the ring fed the same buffers
+    through save_games_from_buffers (MuZero_DOG/train.py:268, vec_replay_buffer.py:36-61); twice, so the ring
+    wraps."""
+    from exploring_muzero_on_dog_amd import game_agent_dog as GA
+    from exploring_muzero_on_dog_amd import muzero_dog as MD
+    from exploring_muzero_on_dog_amd import replay as R
+    from exploring_muzero_on_dog_amd import transfer as TR
+    from tests.test_gpu_replay import _assert_rings_identical, _host_pack
+    net = MD.DeviceDogNet(MD.init_muzero_params(5))
+    B, G, T = 16, 24, 60
+    sp = GA.DogSelfPlay(net, B, 4, 3, 1.0, seed=2)
+    buf = {k: v.clone() for k, v in sp.play_stream(G, T, seed=4).items()}
+    assert buf["pol"].shape == (G, T, MD.NUM_ACTIONS) and buf["obs"].shape == (G, T, MD.NUM_CHANNELS, 56)
+    packed = TR.pack(buf)
+    want = _host_pack({k: v.cpu().numpy() for k, v in buf.items()}, T)
+    for k, v in want.items():
+        assert np.array_equal(packed[k].cpu().numpy(), v), k
+    mk = lambda: R.VectorizedReplayBuffer(40, 32, 10, 20, obs_shape=(MD.NUM_CHANNELS, 56),  # noqa: E731
+                                          action_dim=MD.NUM_ACTIONS, max_episode_length=T,
+                                          rng=np.random.RandomState(8))
+    a, b = mk(), mk()
+    for _ in range(2):                                           # 48 games into 40 slots: wraps
+        a.save_games_from_buffers(buf)
+        b.save_packed(packed)
+    _assert_rings_identical(a, b)
+    for _ in range(3):
+        ba, bb = a.sample_batch(), b.sample_batch()
+        assert set(ba) == set(bb)
+        for k in ba:
+            assert torch.equal(ba[k], bb[k]), k
+    assert ba["policies"].shape[-1] == MD.NUM_ACTIONS

@@ -612,11 +612,13 @@ def test_chain_and_stack_kernels_survive_a_second_backward(cuda):
         torch.autograd.grad(loss, inputs)
 
 
-def test_fused_adamw_matches_foreach_form(cuda):
+@pytest.mark.parametrize("max_tables", [8, 0])
+def test_fused_adamw_matches_foreach_form(cuda, max_tables):
     """csrc/learner_opt.hip (global-norm clip + AdamW + lr schedule in two passes over all tensors) against the
     torch._foreach form of the same step (learner.AdamW on the CPU path, here run on the GPU): 45 tensors (two
     kernel-argument tables), sizes across the 4096-element chunk edges, an empty tensor and one without a
-    gradient; clipped and unclipped steps across two lr boundaries."""
+    gradient; clipped and unclipped steps across two lr boundaries.  max_tables 8: every step through
+    muz_adamw_step_table (a fresh device table per gradient-pointer set); 0: muz_adamw_step (kernel arguments)."""
     _, _, L, _, _ = _mods()
     rng = np.random.default_rng(12)
     sizes = [1, 3, 4095, 4096, 4097, 9000, 0, 256 * 256] + list(rng.integers(1, 3000, 37))
@@ -626,6 +628,7 @@ def test_fused_adamw_matches_foreach_form(cuda):
     kw = dict(steps_per_iteration=1, boundaries=((2, 0.2), (4, 0.5)))
     fused, ref = L.AdamW(p1, **kw), L.AdamW(p2, **kw)
     assert fused._fused is not None
+    fused._fused["max_tables"] = max_tables
     ref._fused = None
     for step in range(7):
         scale = 3.0 if step in (1, 4) else 0.01                 # global norm above / below max_norm 5
@@ -642,6 +645,45 @@ def test_fused_adamw_matches_foreach_form(cuda):
             for i, (a, b) in enumerate(zip(xs, ys)):
                 assert torch.allclose(a, b, rtol=2e-6, atol=1e-8), (step, name, i, (a - b).abs().max().item())
     assert float(fused.count) == float(ref.count) == 7.0
+    assert len(fused._fused["tables"]) == min(7, max_tables)
+
+
+def test_adamw_table_survives_later_steps_in_a_graph(cuda):
+    """a captured step must keep updating with the gradients it was captured with, whatever eager steps
+    with other gradient pointers ran in between (each pointer set has its own never-rewritten device table).
+    Sequence eager(A), capture(A), eager(B), replay(A) against the foreach form run as A, B, A."""
+    _, _, L, _, _ = _mods()
+    g = torch.Generator().manual_seed(3)
+    init = [torch.randn(5000, generator=g), torch.randn(300, generator=g)]
+    ga = [torch.randn(5000, generator=g).cuda(), torch.randn(300, generator=g).cuda()]
+    gb = [torch.randn(5000, generator=g).cuda() * 50, torch.randn(300, generator=g).cuda() * 50]
+    ps = [x.clone().cuda().requires_grad_(True) for x in init]
+    qs = [x.clone().cuda().requires_grad_(True) for x in init]
+    opt = L.AdamW(ps, steps_per_iteration=1, boundaries=())
+    ref = L.AdamW(qs, steps_per_iteration=1, boundaries=())
+    ref._fused = None
+    for p, x in zip(ps, ga):
+        p.grad = x
+    opt.step()                                    # eager: writes the table of pointer set A
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            opt.step()
+    torch.cuda.current_stream().wait_stream(s)
+    for p, x in zip(ps, gb):
+        p.grad = x
+    opt.step()                                    # eager, pointer set B: its own table
+    graph.replay()
+    torch.cuda.synchronize()
+    for grads in (ga, gb, ga):
+        for q, x in zip(qs, grads):
+            q.grad = x.clone()
+        ref.step()
+    for a, b in zip(ps, qs):
+        assert torch.allclose(a, b, rtol=2e-6, atol=1e-7), float((a - b).abs().max())
+    assert len(opt._fused["tables"]) == 2
 
 
 @pytest.mark.parametrize("K,Cin", [(3, 6), (3, 32), (5, 64)])

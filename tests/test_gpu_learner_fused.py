@@ -303,7 +303,9 @@ def _loss_only(L, classic, b, outs, K, U):
 
 @pytest.mark.parametrize("classic,K,B,zero_mask", [(False, 10, 128, False), (False, 5, 100, False),
                                                    (False, 0, 64, False), (False, 3, 70, True),
-                                                   (True, 10, 128, False), (True, 4, 33, False), (True, 2, 64, True)])
+                                                   (True, 10, 128, False), (True, 4, 33, False), (True, 2, 64, True),
+                                                   # B > the kernel's 256 threads: a thread sums several rows
+                                                   (False, 3, 384, False), (True, 3, 384, False)])
 def test_fused_loss_matches_torch_ops(cuda, classic, K, B, zero_mask):
     b, outs = _loss_case(classic, K, B, seed=K * 7 + B, zero_mask=zero_mask)
     (pf, gf), (pt, gt) = _loss_both(classic, b, outs, K, U=10)

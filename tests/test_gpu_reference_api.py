@@ -29,15 +29,23 @@ def test_det_play_n_games_v3_reference_signature(cuda, P):
     tree = CK.flat_to_muzero_tree(flat)
     got = GA.play_n_games_v3(tree, np.array([0, 77], np.uint32), (C, 56), 24, 8, 4, 120, 1.0)
     eng = GA.SelfPlayEngine(N.DeviceNet(flat, C), 24, num_players=P, max_steps=120, num_simulations=8, max_depth=4)
-    want = eng.play(77, 1.0)
+    want = GA.reference_buffers(eng.play(77, 1.0), GA.REFERENCE_DTYPES)
     assert set(got) == set(GA.REFERENCE_DTYPES)
+    # rows at or past idx hold the reference's initial values (game_agent.py:158-169: zeros, team -1)
+    past = torch.arange(120, device="cuda")[None, :] >= got["idx"][:, None].long()
+    assert bool(past.any())
+    assert bool((got["team"][past] == -1).all()) and not bool(got["act"][past].any())
+    assert not bool(got["obs"][past].any()) and not bool(got["pol"][past].any())
     for k, v in got.items():
         assert v.dtype == GA.REFERENCE_DTYPES[k], k
         assert tuple(v.shape) == tuple(want[k].shape), k
         assert torch.equal(v, want[k].to(v.dtype)), k
     assert got["obs"].dtype == torch.float32 and tuple(got["obs"].shape) == (24, 120, C, 56)
+    keep = {k: v.clone() for k, v in got.items()}
     again = GA.play_n_games_v3(tree, 77, (C, 56), 24, 8, 4, 120, 1.0)   # int key == uint32[2] key (0, 77)
     assert torch.equal(again["act"], got["act"])
+    GA.play_n_games_v3(tree, 78, (C, 56), 24, 8, 4, 120, 1.0)           # fresh copies: no aliasing of the engine
+    assert all(torch.equal(keep[k], got[k]) for k in keep)
 
 
 def test_det_run_muzero_mcts_reference_signature(cuda):
@@ -66,7 +74,10 @@ def test_classic_reference_signatures(cuda):
     tree = CK.flat_to_muzero_tree(flat)
     got = GS.play_n_games_v3(tree, 55, (C, 56), 12, 8, 4, 80, 1.0)
     eng = GS.StochasticSelfPlayEngine(ST.DeviceClassicNet(flat, C), 12, max_steps=80, num_simulations=8, max_depth=4)
-    want = eng.play(55, 1.0)
+    want = GA.reference_buffers(eng.play(55, 1.0), dict(GA.REFERENCE_DTYPES, dice=torch.int32,
+                                                         dice_dist=torch.float32))
+    past = torch.arange(80, device="cuda")[None, :] >= got["idx"][:, None].long()
+    assert bool((got["team"][past] == -1).all()) and not bool(got["dice_dist"][past].any())
     for k, v in got.items():
         assert torch.equal(v, want[k].to(v.dtype)), k
     assert got["obs"].dtype == torch.float32
