@@ -32,10 +32,17 @@ static_assert(kWMaxSims <= 255, "visit counts in 8 bits (WNode::vis4)");
 static_assert(kWPad >= kDogA && kWWords * 32 >= kDogA, "slots");
 static_assert(2 * kRows * kDogA <= kArenaFloats, "the walk's per-child arrays live in the idle network arena");
 
+// A node's children: the 806 prior logits are written when the node is expanded; the statistics of a child are
+// written only when it is first visited (its expansion writes index / reward / discount, the backups value / visits),
+// and the node's visited mask says which children hold them -- every other child is {value 0, reward 0, discount 0,
+// index -1, visits 0}, as mctx initialises them.  (Round 5 initialised all 806 children's statistics at every
+// expansion: ~20 KB of HBM writes per expansion of the ~4.6 KB the search needs, and the root's full load per
+// simulation read 24 B per child.)
 struct WTree {
-  f32x4* c_node;      // [n][N][832] per child {prior logit, value, reward, discount}: one 16-byte load per child
-  int32_t* c_visits;  // [n][N][832]
-  int32_t* c_index;   // [n][N][832]
+  float* c_prior;     // [n][N][832] prior logits
+  f32x4* c_stat;      // [n][N][832] per visited child {value, reward, discount, index (int bits)}
+  int32_t* c_visits;  // [n][N][832] per visited child
+  uint32_t* c_vmask;  // [n][N][32] lane-major visited mask: word l, bit j <=> child l + 32 j visited
   float* emb;         // [n][N][256]
   float* gum;         // [n][832] the root's Gumbel noise + (prior - max prior), drawn once per search
   f32x4* vrec;        // [n][N][32][2] each node's visited children in first-visit order (s_vcnt: how many; -1
@@ -45,13 +52,16 @@ struct WTree {
   int N;
   __device__ __forceinline__ size_t ca(int g, int node, int a) const { return ((size_t)g * N + node) * kWPad + a; }
   __device__ __forceinline__ AS1 float* e(int g, int node) const { return gpw(emb) + ((size_t)g * N + node) * LAT; }
-  __device__ __forceinline__ AS1 f32x4* node4() const { return gpw(c_node); }
-  // field k (0 prior, 1 value, 2 reward, 3 discount) of child entry e
+  __device__ __forceinline__ AS1 float* prior() const { return gpw(c_prior); }
+  __device__ __forceinline__ AS1 f32x4* stat() const { return gpw(c_stat); }
+  // field k (0 value, 1 reward, 2 discount, 3 index) of child entry e
   __device__ __forceinline__ AS1 float* fld(size_t e, int k) const {
-    return gpw(reinterpret_cast<float*>(c_node)) + 4 * e + k;
+    return gpw(reinterpret_cast<float*>(c_stat)) + 4 * e + k;
   }
-  __device__ __forceinline__ AS1 int32_t* index() const { return gpw(c_index); }
   __device__ __forceinline__ AS1 int32_t* visits() const { return gpw(c_visits); }
+  __device__ __forceinline__ AS1 uint32_t* vmask(int g, int node) const {
+    return gpw(c_vmask) + ((size_t)g * N + node) * kRowLanes;
+  }
   __device__ __forceinline__ AS1 f32x4* vr(int g, int node) const;
   __device__ __forceinline__ AS1 float* tp(int g, int node) const;
   __device__ __forceinline__ AS1 int32_t* ti(int g, int node) const;
@@ -86,12 +96,14 @@ static WTree carve_wide(void* ws, int n, int N) {
   char* p = (char*)ws;
   const size_t cb = wide_children_bytes(n, N);
   WTree t;
-  t.c_node = (f32x4*)p;
+  t.c_stat = (f32x4*)p;
   p += 4 * cb;
+  t.c_prior = (float*)p;
+  p += cb;
   t.c_visits = (int32_t*)p;
   p += cb;
-  t.c_index = (int32_t*)p;
-  p += cb;
+  t.c_vmask = (uint32_t*)p;
+  p += (size_t)n * N * kRowLanes * 4;
   t.emb = (float*)p;
   p += (size_t)n * N * LAT * 4;
   t.gum = (float*)p;
@@ -271,33 +283,26 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
   int sv = 0, mv = 0, ui = kDogA;
 #pragma unroll
   for (int w = 0; w < (kWJ + 3) / 4; ++w) nd.vis4[w] = 0u;
-  // two batches of 13 slots, one 16-byte {prior, value, reward, discount} load + the visit count each, all of a batch in
-  // flight together (left to itself the scheduler serialised them slot by slot to save registers: 26 round trips).
-  // Padding slots are read too (they exist in the node's 832) and their values dropped.
+  // this lane's visited slots (one 128-byte line per node); the 26 prior logits in two batches of 13, all of a batch
+  // in flight together (left to itself the scheduler serialised them slot by slot to save registers: 26 round trips;
+  // padding slots are read too -- they exist in the node's 832 -- and dropped); then the statistics of the few
+  // visited children
+  const unsigned vm_ld = tree_ld(T.vmask(g, node) + sub);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    f32x4 c4[kWHalf];
-    int vs[kWHalf];
+    float pk[kWHalf];
 #pragma unroll
-    for (int k = 0; k < kWHalf; ++k) {
-      const size_t e = T.ca(g, node, sub + kRowLanes * (kWHalf * h + k));
-      c4[k] = tree_ld(T.node4() + e);
-      vs[k] = tree_ld(T.visits() + e);
-    }
+    for (int k = 0; k < kWHalf; ++k) pk[k] = tree_ld(T.prior() + T.ca(g, node, sub + kRowLanes * (kWHalf * h + k)));
     __builtin_amdgcn_sched_barrier(0);
     ST(ST_PASS);   // (diagnostic builds: node loads)
 #pragma unroll
     for (int k = 0; k < kWHalf; ++k) {
       const int j = kWHalf * h + k, a = sub + kRowLanes * j;
-      const bool ok = a < kDogA;
-      const int vj = ok ? vs[k] : 0;
-      nd.vis4[j >> 2] |= (uint32_t)vj << (8 * (j & 3));
-      if (ok) {
-        const float p = c4[k][0];
+      if (a < kDogA) {
+        const float p = pk[k];
         nd.pr[a] = p;
-        nd.cq[a] = c4[k][2] + c4[k][3] * c4[k][1];   // q = reward + discount * value (Tree.qvalues)
         pm = fmaxf(pm, p);
-        if (vs[k] == 0) {   // slots in ascending order: the first of equal priors keeps u1
+        if (((vm_ld >> j) & 1u) == 0u) {   // unvisited; slots in ascending order: the first of equal priors keeps u1
           if (p > u1) {
             u2 = u1;
             u1 = p;
@@ -307,9 +312,20 @@ __device__ __forceinline__ void wnode_full(WNode& nd, const WTree& T, int g, int
           }
         }
       }
-      sv += vj;
-      mv = max(mv, vj);
     }
+  }
+#pragma unroll 1
+  for (unsigned m = vm_ld; m; m &= m - 1u) {
+    const int j = __ffs(m) - 1, a = sub + kRowLanes * j;
+    const size_t e = T.ca(g, node, a);
+    const f32x4 c4 = tree_ld(T.stat() + e);
+    const int vj = tree_ld(T.visits() + e);
+    nd.cq[a] = c4[1] + c4[2] * c4[0];   // q = reward + discount * value (Tree.qvalues)
+    const uint32_t vb = (uint32_t)vj << (8 * (j & 3));
+#pragma unroll
+    for (int w = 0; w < (kWJ + 3) / 4; ++w) nd.vis4[w] |= (j >> 2) == w ? vb : 0u;   // (static indices: registers)
+    sv += vj;
+    mv = max(mv, vj);
   }
   pm = row_max(pm);
   sv = row_isum(sv);
@@ -624,12 +640,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         const bool inv = ((legal[(size_t)g * kWWords + j] >> sub) & 1u) == 0u;
         pr[j] = inv ? kWFMin : root_logits[(size_t)g * kDogA + a] - lm;
         pm = fmaxf(pm, pr[j]);
-        const size_t e = T.ca(g, 0, a);
-        tree_st(T.node4() + e, f32x4{pr[j], 0.f, 0.f, 0.f});
-        tree_st(T.index() + e, -1);
-        tree_st(T.visits() + e, 0);
+        tree_st(T.prior() + T.ca(g, 0, a), pr[j]);
       }
     }
+    tree_st(T.vmask(g, 0) + sub, 0u);   // no child visited
     pm = row_max(pm);   // score_considered's logits.max over the root's (masked) priors, fixed for the search
 #pragma unroll
     for (int j = 0; j < kWJ; ++j) {
@@ -749,12 +763,17 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
           cpr = nd.u1;
         } else {
           const size_t eb = T.ca(g, node, bi);
-          const f32x4 c4 = tree_ld(T.node4() + eb);
-          child = tree_ld(T.index() + eb);
-          cvis = tree_ld(T.visits() + eb);
-          crw = c4[2];
-          cdc = c4[3];
-          cpr = c4[0];
+          cpr = tree_ld(T.prior() + eb);
+          child = -1;
+          cvis = 0;
+          crw = cdc = 0.f;
+          if ((tree_ld(T.vmask(g, node) + (bi & (kRowLanes - 1))) >> (bi >> 5)) & 1u) {   // visited: its statistics
+            const f32x4 c4 = tree_ld(T.stat() + eb);
+            child = __float_as_int(c4[3]);
+            cvis = tree_ld(T.visits() + eb);
+            crw = c4[1];
+            cdc = c4[2];
+          }
         }
         if (sub == 0) {
           p_node[row][depth] = node;
@@ -786,18 +805,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     SYNC();
     // ---------------- expand: recurrent_fn on the 16 parents; the 806 prior logits go to the new nodes' children
     const int nx = s_next[row];
-    if (valid && nx == sim + 1) {   // a new node: its children start unvisited (their priors follow below)
-#pragma unroll
-      for (int j = 0; j < kWJ; ++j) {
-        const int a = sub + kRowLanes * j;
-        if (a < kDogA) {
-          const size_t e = T.ca(g, nx, a);
-          tree_st(T.node4() + e, f32x4{0.f, 0.f, 0.f, 0.f});
-          tree_st(T.index() + e, -1);
-          tree_st(T.visits() + e, 0);
-        }
-      }
-    }
+    if (valid && nx == sim + 1) tree_st(T.vmask(g, nx) + sub, 0u);   // a new node: no child visited (priors below)
     ST(ST_TREE);
     dyn16<NT256, true, false>(wl->dyn, kDogA, din, dact, ar, pf, &wl->pred.rb[0].d0, LAT, LAT, &wl->pred.ln0,
                               valid ? T.e(g, nx) : nullptr);
@@ -805,7 +813,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     // (the hand-out re-reads the new node from LDS: with `nx` itself the compiler precomputed the 806 store
     // addresses before the networks and spilled them)
     dog_logits16<NT256>(wl, ar, pf, [&](int r, int col, float v) {
-      if (valid) tree_st(T.fld(T.ca(game_of(r), s_next[r], col), 0), v);
+      if (valid) tree_st(T.prior() + T.ca(game_of(r), s_next[r], col), v);
     }, &wl->dyn.d3, LAT, LAT);
     if (valid) {
       const int nx = s_next[row];
@@ -813,10 +821,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
       const int par = s_parent[row], pa = s_act[row];
       const float v = ar.v0[row], rw = ar.v1[row], dc = ar.v2[row];
       if (sub == 0) {
+        // the edge's statistics (its value and visit count follow in the backup) and its bit in the visited mask
         const size_t eb = T.ca(g, par, pa);
-        tree_st(T.index() + eb, nx);
-        tree_st(T.fld(eb, 2), rw);
-        tree_st(T.fld(eb, 3), dc);
+        tree_st(T.fld(eb, 3), __int_as_float(nx));
+        tree_st(T.fld(eb, 1), rw);
+        tree_st(T.fld(eb, 2), dc);
+        AS1 uint32_t* mw = T.vmask(g, par) + (pa & (kRowLanes - 1));
+        tree_st(mw, tree_ld(mw) | (1u << (pa >> 5)));
         s_raw[row][nx] = v;
         s_val[row][nx] = v;
         s_ces[row][nx] = -1.f;   // new priors: the node's normaliser is recomputed at its next walk
@@ -857,7 +868,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
         const float child_v = (sub == top) ? carry_v : pv_up;
         if (on) {
           const size_t ei = T.ca(g, parent, pact);
-          tree_st(T.fld(ei, 1), child_v);
+          tree_st(T.fld(ei, 0), child_v);
           tree_st(T.visits() + ei, cvis + 1);
           s_val[row][parent] = pv;
           s_visits[row][parent] = cnt + 1;
@@ -931,7 +942,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
 
 int64_t dog_search_workspace_bytes(int n, int S) {
   const int N = S + 1;
-  return (int64_t)wide_children_bytes(n, N) * 6 + (int64_t)n * N * LAT * 4 + (int64_t)n * kWPad * 4 +
+  return (int64_t)wide_children_bytes(n, N) * 6 + (int64_t)n * N * kRowLanes * 4 + (int64_t)n * N * LAT * 4 +
+         (int64_t)n * kWPad * 4 +
          (int64_t)n * N * (int64_t)(kWRecBytes + 2 * kWTopBytes);
 }
 

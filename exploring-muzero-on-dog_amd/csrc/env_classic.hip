@@ -120,6 +120,81 @@ __global__ __launch_bounds__(64) void k_cls_encode(DetConsts c, muz_classic_soa 
   for (int ch = 0; ch < C; ++ch) out[ch * kCells + w] = (T)cls_encode_value(c, s, ch, w, owner);
 }
 
+// ---- evaluation agents (MuZero_Classic_MADN/evaluate_agent_stochastic.py play_eval_loop_jitted) -----------------
+// mode 0: the random agent (do_random, 800-804: jax.random.categorical over 0 / -1e9 logits of the legal pins);
+// mode 1: the rule-based agent (do_rule_based, 806-866): per pin i a score
+//   goal_bonus  if the pin (not yet in the goal area) lands on one of the player's goal cells
+//   + out_many / out_few (>= 2 / < 2 pins at home) if a home pin moves to the start
+//   + hit_bonus if the pin moves onto an opponent pin (teams: the partner is no opponent)
+// (base score 0) with the landing cell of cur + die (the UNSUBSTITUTED current player's pins, as written); illegal
+// pins -inf; action = argmax(score / temperature + gumbel) with the counter Gumbel draws of det's agents
+// (policy_gumbel, actions 0..3).  -1 when no pin is legal.
+__global__ __launch_bounds__(kClsBlock) void k_cls_policy(DetConsts c, muz_classic_soa st, const uint32_t* legal,
+                                                          int mode, muz_rule_agent ag, unsigned long long seed, int turn,
+                                                          const int32_t* game_id, int32_t* action, int n) {
+  const int g = blockIdx.x * kClsBlock + threadIdx.x;
+  if (g >= n) return;
+  const int S = st.stride;
+  const uint32_t lb = legal[g] & 15u;
+  if (lb == 0u) {
+    action[g] = -1;
+    return;
+  }
+  const unsigned long long key = game_key(seed ^ kPolicyStream, game_id ? game_id[g] : g, turn);
+  int best = -1;
+  float bv = -INFINITY;
+  if (mode == 0) {
+    for (int a = 0; a < 4; ++a) {
+      const float v = (((lb >> a) & 1u) ? 0.0f : -1e9f) + policy_gumbel(key, a);
+      if (v > bv) {
+        bv = v;
+        best = a;
+      }
+    }
+    action[g] = best;
+    return;
+  }
+  const int P = c.P, cp = st.current_player[g], die = st.die[g];
+  const int mt = has(c.flags, R_MUST_TRAVERSE) ? 1 : 0;
+  const int tgt = cst(c.target, cp), start = cst(c.start, cp);
+  int pins[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) pins[j] = j < P * 4 ? st.pins[min(j, P * 4 - 1) * S + g] : -1;
+  int home = 0;
+  for (int k = 0; k < 4; ++k) home += rsel(pins, cp * 4 + k) < 0 ? 1 : 0;
+  const int partner = has(c.flags, R_TEAMS) ? (cp + 2) % 4 : -1;
+  for (int i = 0; i < 4; ++i) {
+    if (((lb >> i) & 1u) == 0u) continue;
+    const int cur = rsel(pins, cp * 4 + i);
+    const int moved = cur + die;
+    const int x = moved - tgt - mt;
+    int np;
+    if (cur < 0) np = start;
+    else if (cur >= kTrack) np = moved;
+    else if (4 >= x && x > 0 && cur <= tgt) np = goal_of(c, cp, jidx(x - 1, 4));
+    else np = fmodp(moved, kTrack);
+    bool in_goal = false;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) in_goal |= np == goal_of(c, cp, h);
+    const float gb = (in_goal && cur < kTrack) ? ag.goal_bonus : 0.0f;
+    const float ob = (cur < 0 && np == start) ? (home >= 2 ? ag.out_many : ag.out_few) : 0.0f;
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int p = j >> 2;
+      hit |= p < P && p != cp && p != partner && pins[j] == np;
+    }
+    const float hb = (np != cur && hit) ? ag.hit_bonus : 0.0f;
+    const float score = ((0.0f + gb) + ob) + hb;
+    const float v = score / ag.temperature + policy_gumbel(key, i);
+    if (v > bv) {
+      bv = v;
+      best = i;
+    }
+  }
+  action[g] = best;
+}
+
 }  // namespace muz
 
 using namespace muz;
@@ -189,6 +264,20 @@ int muz_classic_nostep(const muz_rules* rules, muz_classic_soa st, int8_t* rewar
                        void* stream) {
   CLS_PROLOGUE(true)
   k_cls_nostep<<<cls_blocks(n), kClsBlock, 0, (hipStream_t)stream>>>(c, st, reward, done, n);
+  return muz_last_launch_error();
+}
+
+int muz_classic_policy_action(const muz_rules* rules, muz_classic_soa st, const uint32_t* legal_bits, int32_t mode,
+                              const muz_rule_agent* agent, uint64_t seed, int32_t turn, const int32_t* game_id,
+                              int32_t* action, int32_t n, void* stream) {
+  CLS_PROLOGUE(legal_bits && action && (mode == 0 || mode == 1) && (mode == 0 || agent))
+  muz_rule_agent ag{};
+  if (mode == 1) {
+    ag = *agent;
+    MUZ_HOST_CHECK(ag.temperature > 0.f);
+  }
+  k_cls_policy<<<cls_blocks(n), kClsBlock, 0, (hipStream_t)stream>>>(c, st, legal_bits, mode, ag,
+                                                                     (unsigned long long)seed, turn, game_id, action, n);
   return muz_last_launch_error();
 }
 

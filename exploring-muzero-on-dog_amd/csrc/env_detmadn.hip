@@ -291,8 +291,6 @@ __global__ __launch_bounds__(kWideBlock) void k_det_round_g(DetConsts c, muz_det
 // player; illegal actions -inf; action = argmax(score / temperature + gumbel) -- jax.random.categorical,
 // the Gumbel draw from the engine's counter RNG (seed ^ kPolicyStream, game, turn, action).  -1 when
 // nothing is legal.
-constexpr unsigned long long kPolicyStream = 0x9011C7A6E47ull;
-
 __global__ __launch_bounds__(256) void k_det_policy(DetConsts c, muz_detmadn_soa st, const uint32_t* legal, int mode,
                                                     muz_rule_agent ag, unsigned long long seed, int turn,
                                                     const int32_t* game_id, int32_t* action, int n) {
@@ -306,10 +304,7 @@ __global__ __launch_bounds__(256) void k_det_policy(DetConsts c, muz_detmadn_soa
   }
   const int gid = game_id ? game_id[g] : g;
   const unsigned long long key = game_key(seed ^ kPolicyStream, gid, turn);
-  auto gum = [&](int a) {
-    const float u = fmaxf(u24(mix64(key ^ (unsigned long long)(a + 1) * 0xD6E8FEB86659FD93ull)), kTinyF);
-    return -logf(-logf(u));
-  };
+  auto gum = [&](int a) { return policy_gumbel(key, a); };
   int best = -1;
   float bv = -INFINITY;
   if (mode == 0) {

@@ -68,4 +68,12 @@ __device__ __forceinline__ float gamma_sample(float alpha, unsigned long long ke
   return g;
 }
 
+// The evaluation agents' sampling (jax.random.categorical as argmax(logits + Gumbel)): the Gumbel draw of action a
+// from key = game_key(seed ^ kPolicyStream, game, turn) (det and classic agents, oracle/evaluate.py policy_gumbel)
+constexpr unsigned long long kPolicyStream = 0x9011C7A6E47ull;
+__device__ __forceinline__ float policy_gumbel(unsigned long long key, int a) {
+  const float u = fmaxf(u24(mix64(key ^ (unsigned long long)(a + 1) * 0xD6E8FEB86659FD93ull)), kTinyF);
+  return -logf(-logf(u));
+}
+
 }  // namespace muz

@@ -303,6 +303,9 @@ SIGNATURES = {
     "muz_classic_legal": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_step": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, vp, ctypes.c_int32, vp]),
     "muz_classic_nostep": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, vp, ctypes.c_int32, vp]),
+    "muz_classic_policy_action": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32,
+                                                 ctypes.POINTER(MuzRuleAgent), ctypes.c_uint64, ctypes.c_int32, vp, vp,
+                                                 ctypes.c_int32, vp]),
     "muz_classic_encode_f32": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_classic_encode_i8": (ctypes.c_int, [ctypes.POINTER(MuzRules), MuzClassicSoA, vp, ctypes.c_int32, vp]),
     "muz_tile_waves": (ctypes.c_int32, []),

@@ -185,6 +185,15 @@ int muz_classic_nostep(const muz_rules* rules, muz_classic_soa state, int8_t* re
                        void* stream);
 
 /* encode_board (463-497): obs[b][c][w], C = 2P+3 (last channel = die), W = 56. */
+/* The classic evaluation agents of MuZero_Classic_MADN/evaluate_agent_stochastic.py play_eval_loop_jitted (the harness
+ * evaluate_agent_parallel runs): mode 0 = the random agent (do_random, 800-804), mode 1 = the rule-based agent
+ * (do_rule_based, 806-866: per pin goal / out-of-home / hit bonuses for the landing cell of cur + die, base score 0;
+ * the reference's weights {0.25, 5.0, 3.0, 2.0, 2.5}).  Sampling as muz_detmadn_policy_action (argmax(logits +
+ * Gumbel), the same counter draws for actions 0..3).  legal_bits: muz_classic_legal's 4-bit masks for the die in the
+ * state; action[g] = -1 when no pin is legal. */
+int muz_classic_policy_action(const muz_rules* rules, muz_classic_soa state, const uint32_t* legal_bits, int32_t mode,
+                              const muz_rule_agent* agent /*host, mode 1*/, uint64_t seed, int32_t turn,
+                              const int32_t* game_id, int32_t* action, int32_t n, void* stream);
 int muz_classic_encode_f32(const muz_rules* rules, muz_classic_soa state, float* obs, int32_t n, void* stream);
 int muz_classic_encode_i8(const muz_rules* rules, muz_classic_soa state, int8_t* obs, int32_t n, void* stream);
 

@@ -39,6 +39,17 @@ LOSS_TOL = 1e-5
 TAU = 1e-6     # > the fp32 forward's deviation from float64 at a decision (measured <= 6.6e-7 relative, O(1) values)
 
 
+# Tensors allowed a floor of a few fp32 ulps instead of 3x their own fp32 deviation (the fp32 restatement lands them
+# within ~0.3-0.6 ulp of float64 by luck), by the learner name's first word; measured on the GPU (round 6,
+# profiles/r6a_parity.log): DOG prediction/Dense_5/bias 4.89x (device 2.24e-7 relative Frobenius, fp32 4.6e-8);
+# classic dynamics/discount_head/kernel 3.48x (2.44e-7 vs 7.0e-8) and /bias 3.21x (1.07e-7 vs 3.3e-8); det: none.
+FLOOR_OK = {
+    "DOG": ("prediction/Dense_5/bias",),
+    "classic": ("dynamics/discount_head/kernel", "dynamics/discount_head/bias"),
+}
+ULP_FLOOR = 4 * 2.0 ** -23   # relative Frobenius error of 4 fp32 ulps
+
+
 def _np_batch(batch):
     return {k: v.detach().cpu().numpy() for k, v in batch.items()}
 
@@ -121,11 +132,19 @@ def _check(name, make, params, batch, classic):
         f"float64 oracle step: {n_off} of {n_par} entries differ > 1e-6 (fp32 restatement: {n_off32}), max |d| "
         f"{max(d_ora.values()):.2e}, all at |g| <= {g_at_off:.1e} x max|g| of their tensor; optimizer vs oracle "
         f"AdamW of the device grads: {d_own:.2e}")
-    # per tensor, Frobenius: within 3x the fp32 restatement's deviation -- of that tensor, or its worst over all
-    # tensors where the fp32 run happens to be more exact than that (a one-output bias can land within 1e-8)
-    bound32 = gerr32[worst32][1]
+    # per tensor, Frobenius: within 3x the fp32 restatement's deviation OF THAT TENSOR.  A tensor
+    # may fall back to ULP_FLOOR (4 fp32 ulps) only if it is listed in FLOOR_OK (the fp32 run can land a tiny tensor --
+    # a one-output bias -- within a fraction of an ulp by luck); every tensor above 3x its own is logged by name
+    floored = {k: gerr[k][1] / max(gerr32[k][1], 1e-30) for k in ref if gerr[k][1] > 3.0 * gerr32[k][1]}
+    log(f"{name}: tensors above 3x their own fp32 deviation: "
+        + (", ".join(f"{k} {r:.2f}x (device {gerr[k][1]:.2e}, fp32 {gerr32[k][1]:.2e}, ulp floor {ULP_FLOOR:.2e})"
+                     for k, r in sorted(floored.items(), key=lambda kv: -kv[1])) or "none"))
     for k in ref:
-        assert gerr[k][1] <= 3.0 * max(gerr32[k][1], bound32), (k, gerr[k], gerr32[k], bound32)
+        if k in floored:
+            assert k in FLOOR_OK.get(name.split()[0], ()), (k, gerr[k], gerr32[k], "not in FLOOR_OK")
+            assert gerr[k][1] <= ULP_FLOOR, (k, gerr[k], gerr32[k], ULP_FLOOR)
+        else:
+            assert gerr[k][1] <= 3.0 * gerr32[k][1], (k, gerr[k], gerr32[k])
     assert d_own <= 1e-6, d_own
     assert g_at_off <= 1e-3, g_at_off
 
