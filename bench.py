@@ -231,7 +231,8 @@ MEASURED = {
     "traffic": "profiles/r5i_traffic.json",           # HBM bytes per k_gumbel_search launch (FETCH_SIZE x2 + WRITE_SIZE)
     "pmc": "profiles/r5i_pmc.json",                   # TCP_TCC_READ_REQ, SQ_VALU_MFMA_BUSY_CYCLES, ... (k_gumbel_search)
     "loop": "profiles/r5i_loop_bench.log",            # the weight-stream MFMA loop alone (profiles/loop_bench.hip)
-    "dog_traffic": "profiles/r5zd_dog_traffic.json",  # HBM bytes per k_dog_search launch (FETCH_SIZE x2 + WRITE_SIZE), 6 games / WG
+    "dog_traffic": "profiles/r6b_dog_traffic.json",   # HBM bytes per k_dog_search launch (FETCH_SIZE x2 + WRITE_SIZE), 6 games / WG
+    "classic_traffic": "profiles/r6b_classic_traffic.json",   # the same for k_stochastic_search (config c)
 }
 
 
@@ -680,8 +681,12 @@ def run_classic(args):
     achieved = searches * args.sims * CLASSIC_FLOP_PER_SIM / (search_ms * 1e-3) / 1e12 if search_ms > 0 else 0.0
     out["roofline"] = {"bound": "mfma", "kernel": "k_stochastic_search", "achieved": round(achieved, 3),
                        "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-                       "avg_launch_ms": round(search_ms / max(1, turns), 4), "flop_per_sim": CLASSIC_FLOP_PER_SIM,
-                       "traffic": None}
+                       "avg_launch_ms": round(search_ms / max(1, turns), 4), "flop_per_sim": CLASSIC_FLOP_PER_SIM}
+    traffic, traffic_src = measured_traffic("classic_traffic", "k_stochastic_search")
+    avg_s = search_ms * 1e-3 / max(1, turns)
+    out["roofline"].update({"traffic": None if traffic is None else round(traffic),
+                            "traffic_achieved_tbs": None if traffic is None or avg_s <= 0 else
+                            round(traffic / avg_s / 1e12, 3), "traffic_source": traffic_src})
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = classic_cpu_baseline(min(args.cpu_seconds, 20.0), args.sims, args.depth, args.max_steps)
     print(json.dumps(out), flush=True)

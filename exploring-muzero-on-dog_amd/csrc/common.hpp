@@ -16,6 +16,11 @@
     if (_e != hipSuccess) return (int)_e;  \
   } while (0)
 
+// Root scratch row (muz_nets_root_scratch_bytes): RepresentationNetwork2's flattened conv maps (k_repr_conv) and, after
+// them, its Dense_0 output before LayerNorm_3 (k_dense0) -- one row per game
+constexpr int kConvMapFloats = 56 * 64;
+constexpr int kConvRowFloats = kConvMapFloats + 256;
+
 static inline int muz_last_launch_error() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? MUZ_OK : (int)e;

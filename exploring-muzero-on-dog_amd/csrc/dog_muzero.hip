@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kThreads) void k_dog_root_dense(muz_dog_net_w Wt, c
   const int gr = g0 + row;
   const bool valid = gr < n;
   Pf pf;
-  repr16<NT256>(W->repr, obs, kDogC, convout, g0, n, a, pf, &W->pred.rb[0].d0, LAT, LAT);
+  repr16<NT256, true>(W->repr, obs, kDogC, convout, g0, n, a, pf, &W->pred.rb[0].d0, LAT, LAT);
   __syncthreads();
   ln16<LAT, LN_PLAIN>(a.T, LD, a.T, LD, W->repr_ln7);   // muzero_dog.py:80-81: LayerNorm instead of min-max
   __syncthreads();
@@ -164,6 +164,8 @@ int launch_dog_encode(const DetConsts& c, const muz_dog_soa& st, float* obs, int
 int launch_dog_root(const muz_dog_net_w& w, const float* obs, int n, float* conv, float* logits, float* value,
                     float* emb, hipStream_t s) {
   int rc = launch_repr_conv(w.repr, obs, kDogC, n, nullptr, conv, s);
+  if (rc) return rc;
+  rc = launch_dense0(w.repr.d0, n, nullptr, conv, s);
   if (rc) return rc;
   k_dog_root_dense<<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, obs, conv, n, logits, value, emb);
   return muz_last_launch_error();

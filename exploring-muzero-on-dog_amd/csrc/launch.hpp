@@ -31,6 +31,8 @@ int launch_root_inference(const muz_classic_net_w& w, const float* obs, int n, c
 // k_repr_conv (RepresentationNetwork2's convolutions, nets.hip) and k_film (the per-action FiLM table)
 int launch_repr_conv(const muz_repr_w& r, const float* obs, int C, int n, const int* n_dev, float* conv,
                      hipStream_t s, int32_t* host_counts = nullptr);
+// k_dense0 (nets.hip): Dense_0 (3584 -> 256) of every row of the root scratch, 64 x 64 output tiles
+int launch_dense0(const muz_dense& d0, int n, const int* n_dev, float* conv, hipStream_t s);
 int launch_film(const muz_dyn_w& d, int A, hipStream_t s);
 
 int launch_gumbel_search(const muz_net_w& w, const SearchArgs& sa, const float* root_logits, const float* root_value,

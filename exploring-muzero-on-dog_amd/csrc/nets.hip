@@ -13,9 +13,14 @@ namespace muz {
 // is read as a Toeplitz matrix A[w][dk*Cin+ci] = in[(w+dk)*Cin+ci], waves own 16-position row tiles.
 constexpr int kConvRowsPad = 64;          // 56 positions padded to 4 MFMA row tiles
 constexpr int kPreLd = 64 + 4;
+// Conv_1 / Conv_2 input rows (32 / 64 channels) padded by 8 floats: the MFMA A-fragment reads (ds_read_b128, 16 rows
+// per fragment) then hit 16 different bank groups -- with unpadded rows (a multiple of 64 floats apart) every row of a
+// fragment started in the same banks (round 6; the search kernel's tiles measured the same)
+constexpr int kC1Ld = 32 + 8;
+constexpr int kC2Ld = 64 + 8;
 
 // LayerNorm over channels for 56 positions, 4 lanes per position.
-template <int N>
+template <int N, int LDO>
 __device__ __forceinline__ void ln_positions(const float* pre, float* out, int out_row0, const AS4 muz_ln& P) {
   const int pos = threadIdx.x >> 2, q = threadIdx.x & 3;
   if (pos >= 56) return;
@@ -36,16 +41,18 @@ __device__ __forceinline__ void ln_positions(const float* pre, float* out, int o
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = q + 4 * i;
-    out[(out_row0 + pos) * N + c] = fmaxf(fmaf(v[i] - mean, inv * gp(P.scale)[c], gp(P.bias)[c]), 0.f);
+    out[(out_row0 + pos) * LDO + c] = fmaxf(fmaf(v[i] - mean, inv * gp(P.scale)[c], gp(P.bias)[c]), 0.f);
   }
 }
 
 // Conv_1 / Conv_2 as implicit GEMMs [64 positions (56 + pad)][K] x [K][64]: wave w owns output channels 16 w .. + 15
 // for ALL four 16-position row tiles (the weights packed as 4 groups of one 16-column tile), so each wave streams a
 // quarter of the kernel from L2 once per game.  (Round 3 split the rows instead: every wave streamed the whole
-// [K][64] kernel for its 16 positions, 4x the L2 weight reads -- 328 KB per game for Conv_2.)
-template <int KB>
-__device__ __forceinline__ void conv_mfma(const AS4 muz_dense& L, const float* in, int cin, float* pre) {
+// [K][64] kernel for its 16 positions, 4x the L2 weight reads -- 328 KB per game for Conv_2.)  The Toeplitz read:
+// A[w][dk * CIN + ci] = in[(w + dk) * LDI + ci], a k-block (16 consecutive k) never straddles two taps.
+template <int KB, int CIN, int LDI>
+__device__ __forceinline__ void conv_mfma(const AS4 muz_dense& L, const float* in, float* pre) {
+  static_assert(CIN % 16 == 0, "a k-block within one tap");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(L.w)) + (size_t)wv * KB * 64 + lane;
@@ -59,7 +66,8 @@ __device__ __forceinline__ void conv_mfma(const AS4 muz_dense& L, const float* i
     if (kb + 2 < KB) w2 = wp[(kb + 2) * 64];
     f32x4 a[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const f32x4*>(in + (t * 16 + r) * cin + kb * 16 + 4 * g);
+    for (int t = 0; t < 4; ++t)
+      a[t] = *reinterpret_cast<const f32x4*>(in + (t * 16 + r + (kb * 16) / CIN) * LDI + (kb * 16) % CIN + 4 * g);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -88,11 +96,11 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
   // LDS: pre + one buffer holding in0 | c1in until Conv_1 has read them, then c2in (34.8 KB: 4 workgroups per CU
   // instead of 3 with separate buffers)
   __shared__ __attribute__((aligned(16))) float pre[kConvRowsPad * kPreLd];
-  __shared__ __attribute__((aligned(16))) float buf[68 * 64];
+  __shared__ __attribute__((aligned(16))) float buf[68 * kC2Ld];
   float* in0 = buf;                 // [58][6]
-  float* c1in = buf + 352;          // [66][32]
-  float* c2in = buf;                // [68][64]
-  static_assert(352 >= 58 * 6 && 352 + 66 * 32 <= 68 * 64, "conv LDS carve");
+  float* c1in = buf + 352;          // [66][kC1Ld]
+  float* c2in = buf;                // [68][kC2Ld]
+  static_assert(352 >= 58 * 6 && 352 + 66 * kC1Ld <= 68 * kC2Ld, "conv LDS carve");
   const int g = blockIdx.x;
   const int tid = threadIdx.x;
   const float* o = obs + (size_t)g * C * 56;
@@ -100,33 +108,150 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
     const int w = i / 6 - 1, ch = i % 6;
     in0[i] = (w >= 0 && w < 56) ? o[ch * 56 + w] : 0.f;
   }
-  for (int i = tid; i < 66 * 32; i += 256) c1in[i] = 0.f;
+  for (int i = tid; i < 66 * kC1Ld; i += 256) c1in[i] = 0.f;
   __syncthreads();
-  // Conv_0 (K = 3*6 = 18, N = 32) on VALU
-  for (int i = tid; i < 56 * 32; i += 256) {
-    const int w = i >> 5, co = i & 31;
-    float s = 0.f;
+  // Conv_0 (K = 3*6 = 18, N = 32) on VALU: a thread keeps one output channel, its 18 weights in registers
+  {
+    const int co = tid & 31;
+    float wk[18];
 #pragma unroll
-    for (int dk = 0; dk < 3; ++dk)
+    for (int k = 0; k < 18; ++k) wk[k] = gp(R.conv0.w)[k * 32 + co];
+    const float bco = gp(R.conv0.b)[co];
+    for (int w = tid >> 5; w < 56; w += 8) {
+      float s = 0.f;
 #pragma unroll
-      for (int ci = 0; ci < 6; ++ci) s = fmaf(in0[(w + dk) * 6 + ci], gp(R.conv0.w)[(dk * 6 + ci) * 32 + co], s);
-    pre[w * kPreLd + co] = s + gp(R.conv0.b)[co];
+      for (int k = 0; k < 18; ++k) s = fmaf(in0[w * 6 + k], wk[k], s);   // in0[(w + dk) * 6 + ci], k = dk * 6 + ci
+      pre[w * kPreLd + co] = s + bco;
+    }
   }
   __syncthreads();
-  ln_positions<32>(pre, c1in, 1, R.ln0);   // pad 1 row on each side for k=3
+  ln_positions<32, kC1Ld>(pre, c1in, 1, R.ln0);   // pad 1 row on each side for k=3
   __syncthreads();
-  conv_mfma<6>(R.conv1, c1in, 32, pre);     // K = 3*32 = 96
+  conv_mfma<6, 32, kC1Ld>(R.conv1, c1in, pre);     // K = 3*32 = 96
   __syncthreads();
   // c2in now reuses in0 | c1in: zero its pad rows (0, 1 and 58..67; the LayerNorm writes rows 2..57)
-  for (int i = tid; i < 12 * 64; i += 256) c2in[(i < 128 ? 0 : 56 * 64) + i] = 0.f;
-  ln_positions<64>(pre, c2in, 2, R.ln1);   // pad 2 rows for k=5
+  for (int i = tid; i < 12 * kC2Ld; i += 256) c2in[(i < 2 * kC2Ld ? 0 : 56 * kC2Ld) + i] = 0.f;
+  ln_positions<64, kC2Ld>(pre, c2in, 2, R.ln1);   // pad 2 rows for k=5
   __syncthreads();
-  conv_mfma<20>(R.conv2, c2in, 64, pre);    // K = 5*64 = 320
+  conv_mfma<20, 64, kC2Ld>(R.conv2, c2in, pre);    // K = 5*64 = 320
   __syncthreads();
-  ln_positions<64>(pre, c2in, 0, R.ln2);   // reuse c2in rows 0..55 as the flattened output
+  ln_positions<64, 64>(pre, c2in, 0, R.ln2);   // reuse c2in as the flattened output [56][64] (dense rows)
   __syncthreads();
-  float* dst = convout + (size_t)g * 3584;
-  for (int i = tid; i < 3584; i += 256) dst[i] = c2in[i];   // flatten (w, ch) -> w*64 + ch
+  float* dst = convout + (size_t)g * kConvRowFloats;
+  for (int i = tid; i < kConvMapFloats; i += 256) dst[i] = c2in[i];   // flatten (w, ch) -> w*64 + ch
+}
+
+// RepresentationNetwork2's Dense_0 (3584 -> 256, muzero_deterministic_madn.py:107) for every game as ONE GEMM over
+// 64-row x 64-column output tiles.  k_root_dense used to run it on its 16-row tiles, each tile streaming the layer's
+// 3.67 MB of weights from L2 for 16 rows (~80 us of a 4096-game root inference at the L2-served rate,
+// profiles/r5zf_root_dense0.log); a 64 x 64 tile reads 0.92 MB of weights and 0.92 MB of rows -- half the L2 bytes per
+// FLOP -- staged through LDS in chunks of 4 k-blocks (double buffered).  8 waves: wave w owns rows 16 (w & 3) .. + 15
+// and the packed column group 2 cb + (w >> 2) (dense16's NT256 packing: two 16-column MFMA tiles).  The MFMA order is
+// dense16's (k-blocks in order, for each its 4 k-steps; then the bias), so the output is the one dense16 computes.
+// XCD-aware: workgroup i runs on XCD i % 8, and the 4 column blocks of a row block are consecutive slots of one XCD,
+// so a row block's rows are read into one L2.
+#ifndef MUZ_D0_NG
+#define MUZ_D0_NG 2   // packed column groups (32 columns each) per workgroup: 2 (64 x 64 tiles) or 1 (64 x 32)
+#endif
+#ifndef MUZ_D0_KC
+#define MUZ_D0_KC 4   // k-blocks (16 k each) per staged chunk
+#endif
+constexpr int kD0Rows = 64, kD0NG = MUZ_D0_NG, kD0KC = MUZ_D0_KC, kD0Ld = kD0KC * 16 + 8;
+constexpr int kD0KB = kConvMapFloats / 16, kD0Chunks = kD0KB / kD0KC;
+constexpr int kD0CB = 8 / kD0NG;          // column blocks per row block
+constexpr int kD0AF4 = kD0Rows * kD0KC * 4;            // float4 of a chunk's rows
+constexpr int kD0WF4 = kD0NG * kD0KC * 128;            // float4 of a chunk's weights (per group: [kb][lane][tile])
+static_assert(kD0KB % kD0KC == 0 && (kD0NG == 1 || kD0NG == 2), "Dense_0 chunks");
+static_assert(kD0AF4 % 512 == 0 && kD0WF4 % 512 == 0, "Dense_0 staging: whole float4 per thread");
+
+__global__ __launch_bounds__(512) void k_dense0(muz_dense d0, int n, const int* __restrict__ n_dev, float* conv) {
+  if (n_dev) n = *n_dev;
+  const int id = blockIdx.x, slot = id >> 3;
+  const int rb = (slot / kD0CB) * 8 + (id & 7), cb = slot % kD0CB;
+  const int row0 = rb * kD0Rows;
+  if (row0 >= n) return;
+  __shared__ __attribute__((aligned(16))) float sA[2][kD0Rows * kD0Ld];
+  __shared__ f32x4 sW[2][kD0WF4];   // [buffer][group][kb][tile][lane]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // wave: 16 rows (row tile rt) x 32 columns (NG 2: group wv >> 2, both tiles) or 16 (NG 1: tile wv >> 2)
+  constexpr int TW = kD0NG;   // MFMA tiles per wave
+  const int rt = wv & 3, part = wv >> 2, r = lane & 15, g = lane >> 4;
+  constexpr int kGroupF4 = kD0KB * 64 * 2;   // float4 per packed column group
+  const AS1 f32x4* Wg = gp(reinterpret_cast<const f32x4*>(d0.w)) + (size_t)(kD0NG * cb) * kGroupF4;
+  constexpr int QA = kD0AF4 / 512, QW = kD0WF4 / 512;
+  f32x4 ra[QA], rw[QW];
+  // chunk c: rows row0 .. + 63 x k 16 KC c .. (4 KC float4 per row) and the groups' KC k-blocks (KC * 128 float4 each)
+  auto gload = [&](int c) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int i = t + 512 * q;
+      const int row = row0 + i / (4 * kD0KC);
+      ra[q] = row < n ? *gp(reinterpret_cast<const f32x4*>(conv + (size_t)row * kConvRowFloats + c * 16 * kD0KC) +
+                            i % (4 * kD0KC))
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const int i = t + 512 * q;
+      rw[q] = Wg[(size_t)(i / (kD0KC * 128)) * kGroupF4 + c * (kD0KC * 128) + i % (kD0KC * 128)];
+    }
+  };
+  auto lstore = [&](int b) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int i = t + 512 * q;
+      *reinterpret_cast<f32x4*>(&sA[b][(i / (4 * kD0KC)) * kD0Ld + 4 * (i % (4 * kD0KC))]) = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const int i = t + 512 * q;
+      const int j = i % (kD0KC * 128), kb = j >> 7, ln = (j >> 1) & 63, tt = j & 1;   // global order [kb][lane][tile]
+      sW[b][(i / (kD0KC * 128)) * (kD0KC * 128) + (kb * 2 + tt) * 64 + ln] = rw[q];
+    }
+  };
+  f32x4 acc[TW];
+#pragma unroll
+  for (int tt = 0; tt < TW; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  lstore(0);
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < kD0Chunks; ++c) {
+    const int b = c & 1;
+    if (c + 1 < kD0Chunks) gload(c + 1);
+#pragma unroll
+    for (int kb = 0; kb < kD0KC; ++kb) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(&sA[b][(rt * 16 + r) * kD0Ld + kb * 16 + 4 * g]);
+      f32x4 w[TW];
+#pragma unroll
+      for (int tt = 0; tt < TW; ++tt) {
+        const int grp = kD0NG == 2 ? part : 0, tile = kD0NG == 2 ? tt : part;
+        w[tt] = sW[b][grp * (kD0KC * 128) + (kb * 2 + tile) * 64 + lane];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int tt = 0; tt < TW; ++tt) acc[tt] = mfma4(w[tt][j], a[j], acc[tt]);   // D = W^T A^T, dense16's order
+    }
+    if (c + 1 < kD0Chunks) lstore(b ^ 1);
+    __syncthreads();
+  }
+  const int row = row0 + rt * 16 + r;
+  if (row < n) {
+    const AS1 f32x4* bias4 = gp(reinterpret_cast<const f32x4*>(d0.b));
+#pragma unroll
+    for (int tt = 0; tt < TW; ++tt) {
+      const int col = kD0NG == 2 ? (2 * cb + part) * 32 + tt * 16 + 4 * g : cb * 32 + part * 16 + 4 * g;
+      *reinterpret_cast<f32x4*>(conv + (size_t)row * kConvRowFloats + kConvMapFloats + col) = acc[tt] + bias4[col >> 2];
+    }
+  }
+}
+
+int launch_dense0(const muz_dense& d0, int n, const int* n_dev, float* conv, hipStream_t s) {
+  const int rbs = (n + kD0Rows - 1) / kD0Rows;
+  const int wgs = (rbs + 7) / 8 * 8 * kD0CB;   // kD0CB column blocks per row block, row blocks dealt over the 8 XCDs
+  k_dense0<<<wgs, 512, 0, s>>>(d0, n, n_dev, conv);
+  return muz_last_launch_error();
 }
 
 // Rest of RepresentationNetwork2 + PredictionNetwork4 on 16-game tiles.  NW = muz_net_w (det) or
@@ -147,7 +272,7 @@ __global__ __launch_bounds__(kThreads) void k_root_dense(NW Wt, const float* __r
   const int gr = g0 + row;
   const bool valid = gr < n;
   Pf pf;
-  repr16<NT256>(W->repr, obs, Wt.obs_channels, convout, g0, n, a, pf, &W->pred.rb[0].d0, LAT, LAT);
+  repr16<NT256, true>(W->repr, obs, Wt.obs_channels, convout, g0, n, a, pf, &W->pred.rb[0].d0, LAT, LAT);
   __syncthreads();
   minmax16(a.T, LD);
   __syncthreads();
@@ -236,6 +361,8 @@ static int launch_root_impl(const NW& w, const float* obs, int n, const int* n_d
                             float* value, float* emb, hipStream_t s, int32_t* host_counts = nullptr) {
   int rc = launch_repr_conv(w.repr, obs, w.obs_channels, n, n_dev, conv, s, host_counts);
   if (rc) return rc;
+  rc = launch_dense0(w.repr.d0, n, n_dev, conv, s);
+  if (rc) return rc;
   k_root_dense<NW><<<(n + kRows - 1) / kRows, kThreads, 0, s>>>(w, obs, conv, n, n_dev, logits, value, emb);
   return muz_last_launch_error();
 }
@@ -267,7 +394,7 @@ int muz_net_prepare(const muz_net_w* w, void* stream) {
 
 int64_t muz_nets_root_scratch_bytes(int32_t n) {
   const int64_t rows = ((int64_t)n + kRows - 1) / kRows * kRows;
-  return rows * 3584 * (int64_t)sizeof(float);
+  return rows * kConvRowFloats * (int64_t)sizeof(float);
 }
 
 int muz_nets_root(const muz_net_w* w, const float* obs, int32_t n, void* scratch, int64_t scratch_bytes,

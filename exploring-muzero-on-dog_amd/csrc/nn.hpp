@@ -1036,7 +1036,8 @@ __device__ __forceinline__ void pred16(const AS4 muz_pred_w& P, int A, const flo
 // games g0.. (convout, global memory, rows padded to a multiple of 16), the global stream x[:, 6:, 0], the concat,
 // 6 ResBlocks and Dense_4 into a.T -- the head (min-max / LayerNorm) is the caller's.  pf: on exit Ln's first
 // k-blocks.  Ends without a barrier after Dense_4.
-template <int NTN>
+__device__ __forceinline__ bool gr_valid(int g, int n) { return g < n; }
+template <int NTN, bool D0_DONE = false>
 __device__ __forceinline__ void repr16(const AS4 muz_repr_w& R, const float* __restrict__ obs, int C,
                                        const float* __restrict__ convout, int g0, int n, const Arena& a, Pf& pf,
                                        const AS4 muz_dense* Ln, int Kn, int Nn) {
@@ -1046,13 +1047,23 @@ __device__ __forceinline__ void repr16(const AS4 muz_repr_w& R, const float* __r
   // global stream input: x[:, 6:, 0]
   const int Kg = C - 6;
   if (sub < 32) a.E[row * LDE + sub] = (valid && sub < Kg) ? obs[((size_t)gr * C + 6 + sub) * 56] : 0.f;
-  // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16)
-#ifdef MUZ_EXPT_SKIP_D0   // timing experiment only (wrong results): Dense_0 left out of the root kernel
-  pf_issue<NT64>(pf, &R.d1, Kg, 64);
-#else
-  pf_issue<NT256>(pf, &R.d0, 3584, LAT);
-  dense16<NT256, NT64>(R.d0, 3584, LAT, convout + (size_t)g0 * 3584, 3584, a.W, LDW, pf, &R.d1, Kg, 64, true);
-#endif
+  // spatial: Dense_0 over the flattened conv maps (scratch rows padded to a multiple of 16; row stride
+  // kConvRowFloats), or -- D0_DONE -- its output, computed by k_dense0 into the scratch row after the maps
+  if constexpr (D0_DONE) {
+    pf_issue<NT64>(pf, &R.d1, Kg, 64);
+    const int rr = tid() >> 5, q = tid() & 31;   // 16 rows x 64 float4: 2 per thread
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c4 = q + 32 * i;
+      const f32x4 v = gr_valid(g0 + rr, n) ? *gp(reinterpret_cast<const f32x4*>(
+                          convout + (size_t)(g0 + rr) * kConvRowFloats + kConvMapFloats) + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(a.W + rr * LDW + 4 * c4) = v;
+    }
+  } else {
+    pf_issue<NT256>(pf, &R.d0, kConvMapFloats, LAT);
+    dense16<NT256, NT64>(R.d0, kConvMapFloats, LAT, convout + (size_t)g0 * kConvRowFloats, kConvRowFloats, a.W, LDW,
+                         pf, &R.d1, Kg, 64, true);
+  }
   __syncthreads();
   ln16<LAT, LN_RELU>(a.W, LDW, a.W, LDW, R.ln3);
   dense16<NT64, NT64>(R.d1, Kg, 64, a.E, LDE, a.X, LD, pf, &R.d2, 64, 64);

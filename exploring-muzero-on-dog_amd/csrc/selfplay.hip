@@ -476,7 +476,7 @@ static size_t sp_carve(char* base, int n, int C, int S, SpWs* w) {
   };
   SpWs t;
   t.tree = take((size_t)search_workspace_bytes(n, S));
-  t.conv = (float*)take(n16 * 3584 * 4);
+  t.conv = (float*)take(n16 * kConvRowFloats * 4);
   t.obs = (float*)take(n16 * C * kCells * 4);
   t.legal = (uint32_t*)take((size_t)n * 4);
   t.legal_c = (uint32_t*)take((size_t)n * 4);

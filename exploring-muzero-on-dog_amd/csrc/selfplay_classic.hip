@@ -240,7 +240,7 @@ static size_t cs_carve(char* base, int n, int C, int S, CsWs* w) {
   };
   CsWs t;
   t.tree = take((size_t)stochastic_workspace_bytes(n, S));
-  t.conv = (float*)take(n16 * 3584 * 4);
+  t.conv = (float*)take(n16 * kConvRowFloats * 4);
   t.obs = (float*)take(n16 * C * kCells * 4);
   t.legal = (uint32_t*)take((size_t)n * 4);
   t.legal_c = (uint32_t*)take((size_t)n * 4);

@@ -284,3 +284,198 @@ def evaluate_agent_parallel(agents, batch_size: int = 20, num_simulations: int =
     return {"games": n, "winners": win_tab.tolist(), "average_progress": prog_tab.tolist(),
             "wins_per_player": win_tab.sum(dim=0).tolist(), "progress_per_player": (prog_tab.sum(dim=0) / 4).tolist(),
             "finished": int((env.done != 0).sum()), "final_state": env}
+
+
+# ---- classic MADN: MuZero_Classic_MADN/evaluate_agent_stochastic.py ------------------------------------------------
+# evaluate_agent_stochastic.py:938-948 (the keys it leaves out take env_reset's defaults: no dice rethrow)
+CLASSIC_RULES = dict(enable_teams=True, enable_initial_free_pin=True, enable_circular_board=False,
+                     enable_friendly_fire=True, enable_start_blocking=False, enable_jump_in_goal_area=True,
+                     enable_start_on_1=True, enable_bonus_turn_on_6=True, must_traverse_start=False,
+                     enable_dice_rethrow=False)
+# do_rule_based of play_eval_loop_jitted (806-866); NUM_SIMULATIONS / MAX_DEPTH / TEMPERATURE of 950-952
+CLASSIC_RULE_AGENT = dict(temperature=0.25, goal_bonus=5.0, out_many=3.0, out_few=2.0, hit_bonus=2.5)
+CLASSIC_SIMULATIONS, CLASSIC_DEPTH = 75, 50
+
+
+def classic_policy_action(env, legal: torch.Tensor, mode: str, seed: int, turn: int, agent: dict | None = None,
+                          game_id: torch.Tensor | None = None) -> torch.Tensor:
+    """The classic random ('random_agent', do_random 800-804) or rule-based ('rule_based_agent', do_rule_based
+    806-866) pin of every game for the die in the state (int32 [B], -1 without a legal pin), one launch
+    (muz_classic_policy_action)."""
+    m = {"random_agent": 0, "rule_based_agent": 1}[mode]
+    a = dict(CLASSIC_RULE_AGENT if agent is None else agent)
+    ag = _L.MuzRuleAgent(a["temperature"], a["goal_bonus"], a["out_many"], a["out_few"], a["hit_bonus"])
+    out = torch.empty((env.batch,), dtype=torch.int32, device=env.board.device)
+    gid = None if game_id is None else game_id.to(device=out.device, dtype=torch.int32).contiguous()
+    _L.check(_L.load().muz_classic_policy_action(env.rules, env.soa(), _L.ptr(legal.contiguous()), m, ag,
+                                                 int(seed) & ((1 << 64) - 1), int(turn), _L.ptr(gid), _L.ptr(out),
+                                                 env.batch, _L.stream_ptr()), "muz_classic_policy_action")
+    return out
+
+
+def _csub(env, idx: torch.Tensor):
+    from . import classic as CL
+    return CL.ClassicMADNState(env.board[:, idx].contiguous(), env.pins[:, idx].contiguous(),
+                               env.current_player[idx].contiguous(), env.reward[idx].contiguous(),
+                               env.done[idx].contiguous(), env.die[idx].contiguous(), env.rules, env.num_players)
+
+
+def _cput(env, idx: torch.Tensor, sub):
+    env.board[:, idx] = sub.board
+    env.pins[:, idx] = sub.pins
+    env.current_player[idx] = sub.current_player
+    env.reward[idx] = sub.reward
+    env.done[idx] = sub.done
+    env.die[idx] = sub.die
+
+
+def _classic_turn(env, seats, gid, turn, seed, gen, num_simulations, max_depth, temperature, rule_agent, ws,
+                  throw=True):
+    """One turn of every unfinished game (play_eval_loop_jitted's body_fn, 754-900): throw_die (its dice_probabilities,
+    soft lock aware), then per game the agent of its current player -- a stochastic MuZero search ('mcts': a
+    DeviceClassicNet), 'random_agent' or 'rule_based_agent' -- and env_step, or no_step without a legal pin."""
+    from . import classic as CL
+    from . import stochastic as ST
+    n = env.batch
+    active = env.done == 0
+    if throw:
+        # the uniform draws of the die: torch's generator (the reference's jax key is not restated)
+        CL.throw_die(env, torch.rand((n,), generator=gen, device=env.board.device))
+    bits = CL.legal_bits(env)
+    cp = env.current_player.long()
+    has = (bits & 15) != 0
+    mover = active & has
+    act = torch.full((n,), -1, dtype=torch.int32, device=env.board.device)
+    for s, a in enumerate(seats):
+        sel = mover & (cp == s)
+        if not bool(sel.any()):
+            continue
+        if isinstance(a, str):
+            act = torch.where(sel, classic_policy_action(env, bits, a, seed, turn, rule_agent, gid), act)
+        else:
+            idx = sel.nonzero().flatten()
+            sub = _csub(env, idx)
+            out = ST.stochastic_muzero_mcts(a, CL.encode_board(sub), bits[idx], num_simulations, max_depth,
+                                            temperature, seed=seed, turn=turn, game_id=gid[idx], workspace=ws)
+            act[idx] = out[0]
+    step = mover.nonzero().flatten()
+    if step.numel():
+        sub = _csub(env, step)
+        CL.env_step(sub, act[step])
+        _cput(env, step, sub)
+    nos = (active & ~has).nonzero().flatten()
+    if nos.numel():
+        sub = _csub(env, nos)
+        CL.no_step(sub)
+        _cput(env, nos, sub)
+    return bool(active.any())
+
+
+def _classic_seat(a, C, i, seed, device):
+    from . import stochastic as ST
+    if a is None:     # a Stochastic MuZero agent with randomly initialised params
+        return ST.DeviceClassicNet(ST.init_classic_params(C, seed=1_000_003 * (seed + 1) + i), C, device=device)
+    if isinstance(a, str):
+        if a not in ("rule_based_agent", "random_agent"):
+            raise ValueError(f"unknown agent {a!r}")
+        return a
+    return ST.as_device_classic_net(a, C, device=device)
+
+
+@torch.no_grad()
+def evaluate_agent_parallel_classic(agents, batch_size: int = 150, num_simulations: int = CLASSIC_SIMULATIONS,
+                                    max_depth: int = CLASSIC_DEPTH, temperature: float = 0.0, seed: int = 0,
+                                    rules: dict | None = None, max_turns: int = 2000, rule_agent: dict | None = None,
+                                    device="cuda") -> dict:
+    """evaluate_agent_parallel (evaluate_agent_stochastic.py:253-315) with play_n_games_for_eval_jitted /
+    play_eval_loop_jitted (717-936): `agents` = the four seats, each a DeviceClassicNet / Flax params (Stochastic
+    MuZero, temperature 0, S 75, D 50), None (randomly initialised params), 'rule_based_agent' or 'random_agent';
+    4 x batch_size games, block i started by player i; the die thrown every turn; at most 2000 turns.  Returns
+    winners[start][player] and average_progress[start][player] as the reference prints them, and their totals."""
+    from . import classic as CL
+    from . import stochastic as ST
+    r = dict(CLASSIC_RULES if rules is None else rules)
+    P = 4
+    C = CL.num_channels(P)
+    seats = [_classic_seat(a, C, i, seed, device) for i, a in enumerate(agents)]
+    n = 4 * batch_size
+    env = CL.env_reset(n, num_players=P, device=device, **r)
+    for sp in range(1, 4):
+        idx = torch.arange(sp * batch_size, (sp + 1) * batch_size, device=device)
+        _cput(env, idx, CL.env_reset(batch_size, num_players=P, starting_player=sp, device=device, **r))
+    gid = torch.arange(n, device=device, dtype=torch.int32)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    ws = None
+    if any(not isinstance(x, str) for x in seats):
+        ws = torch.empty((_L.load().muz_stochastic_workspace_bytes(n, num_simulations),), dtype=torch.uint8,
+                         device=device)
+    for turn in range(max_turns):
+        if not _classic_turn(env, seats, gid, turn, seed, gen, num_simulations, max_depth, temperature, rule_agent,
+                             ws):
+            break
+    w = winners(env, bool(r.get("enable_teams", False))) & (env.done != 0)[:, None]
+    prog = calculate_progress(env, bool(r.get("must_traverse_start", False)))
+    win_tab = w.long().reshape(4, batch_size, P).sum(dim=1)
+    prog_tab = prog.reshape(4, batch_size, P).mean(dim=1)
+    return {"games": n, "winners": win_tab.tolist(), "average_progress": prog_tab.tolist(),
+            "wins_per_player": win_tab.sum(dim=0).tolist(), "progress_per_player": (prog_tab.sum(dim=0) / 4).tolist(),
+            "finished": int((env.done != 0).sum()), "final_state": env}
+
+
+@torch.no_grad()
+def play_vs_random_classic(agent, num_games: int, num_simulations: int = CLASSIC_SIMULATIONS,
+                           max_depth: int = CLASSIC_DEPTH, seed: int = 42, max_turns: int = 2000,
+                           rules: dict | None = None, device="cuda") -> dict:
+    """One batch of test_agent_vs_random (evaluate_agent_stochastic.py:387-476): the agent at seat 0 (+ seat 2, its
+    partner, with teams) -- a Stochastic MuZero searching at temperature 0 (multiactor_step_with_random_agent_v2,
+    478-650), or 'rule_based_agent' / 'random_agent' -- the other seats random; a random starting player per game
+    (env_reset's seed); wins counted at seat 0.  The die is thrown every turn as play_eval_loop_jitted does: the v2
+    step as written never throws it, so its games keep env_reset's die 0, have no legal pin and end only at
+    MAX_STEPS (oracle/classic_madn.py: valid_action of a fresh state with die 0 is all False)."""
+    from . import classic as CL
+    r = dict(CLASSIC_RULES if rules is None else rules)
+    P = 4
+    C = CL.num_channels(P)
+    teams = bool(r.get("enable_teams", False))
+    ag = _classic_seat(agent, C, 0, seed, device)
+    seats = [ag, "random_agent", ag if teams else "random_agent", "random_agent"]
+    g = torch.Generator().manual_seed(seed)
+    seeds = torch.randint(0, 1_000_000, (num_games,), generator=g).tolist()
+    env = CL.env_reset(num_games, num_players=P, starting_player=-1, device=device, seeds=seeds, **r)
+    gid = torch.arange(num_games, device=device, dtype=torch.int32)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    ws = None
+    if not isinstance(ag, str):
+        ws = torch.empty((_L.load().muz_stochastic_workspace_bytes(num_games, num_simulations),), dtype=torch.uint8,
+                         device=device)
+    for turn in range(max_turns):
+        if not _classic_turn(env, seats, gid, turn, seed, gen, num_simulations, max_depth, 0.0, None, ws):
+            break
+    w = winners(env, teams) & (env.done != 0)[:, None]
+    prog = calculate_progress(env, bool(r.get("must_traverse_start", False)))
+    return {"games": num_games, "wins": int(w[:, 0].sum()), "seat_wins": w.sum(dim=0).tolist(),
+            "finished": int((env.done != 0).sum()), "progress": prog.mean(dim=0).tolist()}
+
+
+def test_agent_vs_random_classic(agent, num_games: int, batch_size: int = 100, seed: int = 42, **kw) -> tuple:
+    """test_agent_vs_random (evaluate_agent_stochastic.py:387-476) -> (wins at seat 0, mean final pin distance per
+    seat over the batches)."""
+    wins, prog, nb = 0, None, 0
+    for b in range(0, num_games, batch_size):
+        r = play_vs_random_classic(agent, min(batch_size, num_games - b), seed=seed + b, **kw)
+        wins += r["wins"]
+        p = torch.tensor(r["progress"])
+        prog = p if prog is None else prog + p
+        nb += 1
+    return wins, (prog / max(nb, 1)).tolist()
+
+
+def compare_agents_statistically_classic(agent1, agent2, num_games: int = 1000, batch_size: int = 100,
+                                         seed: int = 42, **kw) -> dict:
+    """compare_agents_statistically (evaluate_agent_stochastic.py:652-717): both agents against random opponents on
+    the same seeds, then the two-proportion z-test."""
+    w1, _ = test_agent_vs_random_classic(agent1, num_games, batch_size, seed, **kw)
+    w2, _ = test_agent_vs_random_classic(agent2, num_games, batch_size, seed, **kw)
+    return z_test(w1, w2, num_games)

@@ -8,6 +8,10 @@
   calculate_progress  calculate_progress (129-195): rotated pin positions, sorted, greedily matched to the
                       rotated goal cells 40..43 by repeated masked argmin of |pin - goal|
   manual_get_winner   16-45
+  classic_*           the classic agents of MuZero_Classic_MADN/evaluate_agent_stochastic.py play_eval_loop_jitted:
+                      do_random (800-804) and do_rule_based (806-866: per pin, the landing cell of cur + die of the
+                      UNSUBSTITUTED current player, goal 5 / out 3 or 2 / hit 2.5, base 0, temperature 0.25), sampled
+                      with the first 4 of the same counter Gumbel draws
 Parity of the random SOURCE is unpinned (the reference draws with jax threefry); given the draws the
 restatement is exact.
 """
@@ -109,3 +113,53 @@ def manual_get_winner(env):
     if (t0 & t1) or not (t0 | t1):
         return np.zeros(4, bool)
     return np.array([True, False, True, False]) if t0 else np.array([False, True, False, True])
+
+
+# ---- classic MADN agents (MuZero_Classic_MADN/evaluate_agent_stochastic.py) -------------------------------------
+CLASSIC_RULE_AGENT = dict(temperature=0.25, goal_bonus=5.0, out_many=3.0, out_few=2.0, hit_bonus=2.5)   # 806-866
+
+
+def classic_random_action(env, seed, game, turn):
+    """do_random (evaluate_agent_stochastic.py:800-804) over the 4 pins."""
+    from oracle import classic_madn as cm
+    va = cm.valid_action(env)
+    if not va.any():
+        return -1
+    logits = np.where(va, F32(0.0), F32(-1e9)).astype(F32)
+    return int(np.argmax((logits + policy_gumbel(seed, game, turn)[:4]).astype(F32)))
+
+
+def classic_rule_based_scores(env, agent=CLASSIC_RULE_AGENT):
+    """do_rule_based (806-866): the score (4,) of every pin before masking, and the legal mask."""
+    from oracle import classic_madn as cm
+    va = cm.valid_action(env)
+    cp = env.current_player
+    P = env.num_players
+    bs = env.board_size
+    cur = env.pins[cp].astype(np.int64)
+    moved = cur + int(env.die)
+    fitted = moved % bs
+    x = moved - int(env.target[cp]) - int(env.rules["must_traverse_start"])
+    goal = env.goal[cp].astype(np.int64)
+    gx = goal[np.clip(np.where(x - 1 < 0, x - 1 + 4, x - 1), 0, 3)]
+    start = int(env.start[cp])
+    new = np.where(cur < 0, start,
+                   np.where(cur >= bs, moved, np.where((4 >= x) & (x > 0) & (cur <= int(env.target[cp])), gx, fitted)))
+    opp = np.ones((P, 4), bool)
+    opp[cp] = False
+    if env.rules["enable_teams"]:
+        opp[(cp + 2) % 4] = False
+    opp_pins = np.where(opp, env.pins, -1).flatten()
+    home = int((cur < 0).sum())
+    gb = np.where(np.isin(new, goal) & (cur < bs), F32(agent["goal_bonus"]), F32(0.0))
+    ob = np.where((cur < 0) & (new == start), F32(agent["out_many"] if home >= 2 else agent["out_few"]), F32(0.0))
+    hb = np.where((new != cur) & np.isin(new, opp_pins), F32(agent["hit_bonus"]), F32(0.0))
+    return (((np.zeros(4, F32) + gb).astype(F32) + ob).astype(F32) + hb).astype(F32), va
+
+
+def classic_rule_based_action(env, seed, game, turn, agent=CLASSIC_RULE_AGENT):
+    sc, va = classic_rule_based_scores(env, agent)
+    if not va.any():
+        return -1
+    logits = np.where(va, (sc / F32(agent["temperature"])).astype(F32), F32(-np.inf))
+    return int(np.argmax((logits + policy_gumbel(seed, game, turn)[:4]).astype(F32)))

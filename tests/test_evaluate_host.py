@@ -42,3 +42,25 @@ def test_manual_get_winner_matches_host_winners():
         e = dm.env_reset(num_players=4, **dm.SELFPLAY_RULES)
         e = e.replace(pins=p, board=dm.set_pins_on_board(e.board, p))
         assert np.array_equal(got[g], OE.manual_get_winner(e)), g
+
+
+def test_classic_rule_based_scores_crafted_state():
+    """do_rule_based of the classic eval loop (evaluate_agent_stochastic.py:806-866) on a crafted state: pin 1 enters
+    the goal (+5), pin 2 hits an opponent (+2.5), the two home pins score the out-of-home bonus (3.0 with >= 2 at home)
+    but are illegal with a 3; the sampled pin is always a legal one."""
+    from oracle import classic_madn as cm
+    rules = dict(enable_teams=True, enable_initial_free_pin=False, enable_circular_board=False,
+                 enable_friendly_fire=True, enable_start_blocking=False, enable_jump_in_goal_area=True,
+                 enable_start_on_1=True, enable_bonus_turn_on_6=True, must_traverse_start=False,
+                 enable_dice_rethrow=False)
+    e = cm.env_reset(num_players=4, **rules)
+    pins = -np.ones((4, 4), np.int8)
+    pins[0] = [-1, 38, 5, -1]
+    pins[1, 0] = 8
+    e = e.replace(pins=pins, board=cm.set_pins_on_board(-np.ones_like(e.board), pins), die=3)
+    sc, va = OE.classic_rule_based_scores(e)
+    assert sc.tolist() == [3.0, 5.0, 2.5, 3.0]
+    assert va.tolist() == [False, True, True, False]
+    picks = {OE.classic_rule_based_action(e, 1, g, 0) for g in range(64)}
+    assert picks <= {1, 2} and 1 in picks
+    assert {OE.classic_random_action(e, 1, g, 0) for g in range(64)} == {1, 2}
