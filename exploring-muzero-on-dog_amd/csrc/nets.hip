@@ -16,8 +16,11 @@ constexpr int kPreLd = 64 + 4;
 // Conv_1 / Conv_2 input rows (32 / 64 channels) padded by 8 floats: the MFMA A-fragment reads (ds_read_b128, 16 rows
 // per fragment) then hit 16 different bank groups -- with unpadded rows (a multiple of 64 floats apart) every row of a
 // fragment started in the same banks (round 6; the search kernel's tiles measured the same)
-constexpr int kC1Ld = 32 + 8;
-constexpr int kC2Ld = 64 + 8;
+#ifndef MUZ_CONV_PAD
+#define MUZ_CONV_PAD 8   // (A/B switch: 0 = the unpadded rows of round 5)
+#endif
+constexpr int kC1Ld = 32 + MUZ_CONV_PAD;
+constexpr int kC2Ld = 64 + MUZ_CONV_PAD;
 
 // LayerNorm over channels for 56 positions, 4 lanes per position.
 template <int N, int LDO>

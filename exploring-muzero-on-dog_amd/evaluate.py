@@ -443,6 +443,7 @@ def play_vs_random_classic(agent, num_games: int, num_simulations: int = CLASSIC
     g = torch.Generator().manual_seed(seed)
     seeds = torch.randint(0, 1_000_000, (num_games,), generator=g).tolist()
     env = CL.env_reset(num_games, num_players=P, starting_player=-1, device=device, seeds=seeds, **r)
+    env.rules = CL.make_rules(P, starting_player=0, **r)   # (the seat is in the state now; the kernels take 0..P-1)
     gid = torch.arange(num_games, device=device, dtype=torch.int32)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
@@ -479,3 +480,91 @@ def compare_agents_statistically_classic(agent1, agent2, num_games: int = 1000, 
     w1, _ = test_agent_vs_random_classic(agent1, num_games, batch_size, seed, **kw)
     w2, _ = test_agent_vs_random_classic(agent2, num_games, batch_size, seed, **kw)
     return z_test(w1, w2, num_games)
+
+
+# ---- DOG: MuZero_DOG/evaluate_agent.py --------------------------------------------------------------------------
+# evaluate_agent.py:530-541; NUM_SIMULATIONS / MAX_DEPTH 544-545, TEMPERATURE 0.20 (552: the value the script runs with)
+DOG_RULES = dict(enable_teams=True, enable_initial_free_pin=False, enable_circular_board=True, enable_friendly_fire=True,
+                 enable_start_blocking=True, enable_jump_in_goal_area=False, must_traverse_start=True,
+                 disable_swapping=False, disable_hot_seven=False, disable_joker=False)
+DOG_SIMULATIONS, DOG_DEPTH, DOG_TEMPERATURE = 100, 50, 0.2
+
+
+def _dog_seat(a, i, seed, device):
+    from . import muzero_dog as MD
+    if a is None:     # a MuZero agent with randomly initialised params (the DOG slice's networks)
+        return MD.DeviceDogNet(MD.init_muzero_params(1_000_003 * (seed + 1) + i), device=device)
+    if isinstance(a, str):
+        if a == "rule_based_agent":
+            # do_rule_based (evaluate_agent.py:403-480) is det-MADN's agent copied: valid_mask.reshape(4, 6) of the
+            # 806-action DOG mask cannot run, so the reference has no DOG rule-based agent to restate
+            raise ValueError("MuZero_DOG/evaluate_agent.py's rule-based agent reshapes the 806-action mask to (4, 6) "
+                             "and cannot run; use 'random_agent' or a MuZero agent")
+        if a != "random_agent":
+            raise ValueError(f"unknown agent {a!r}")
+        return a
+    return MD.as_device_net(a, device=device)
+
+
+@torch.no_grad()
+def evaluate_agent_parallel_dog(agents, batch_size: int = 20, num_simulations: int = DOG_SIMULATIONS,
+                                max_depth: int = DOG_DEPTH, temperature: float = DOG_TEMPERATURE, seed: int = 0,
+                                rules: dict | None = None, max_turns: int = 2000, device="cuda") -> dict:
+    """evaluate_agent_parallel (MuZero_DOG/evaluate_agent.py:255-313) with play_n_games_for_eval_jitted /
+    play_eval_loop_jitted (315-527): `agents` = the four seats, each the DOG slice's MuZero (a DeviceDogNet or its
+    flat params; None = randomly initialised params; run_muzero_mcts at A = 806, S 100, D 50, temperature 0.2) or
+    'random_agent' (do_random: a uniform legal action); 4 x batch_size games, block i started by player i, at most
+    2000 turns; a game without a legal action applies no_step.  Every game steps in its own lane each turn (a finished
+    game's lane applies no_step, which leaves its pins alone), so a game's deals are keyed by its own index.  Returns
+    winners[start][player] and average_progress[start][player] as the reference prints them, and their totals.
+    Win-rate parity is unpinned: the reference's DOG networks and inference functions are `pass`."""
+    from . import dog as DOG
+    from . import muzero_dog as MD
+    r = dict(DOG_RULES if rules is None else rules)
+    P = 4
+    seats = [_dog_seat(a, i, seed, device) for i, a in enumerate(agents)]
+    n = 4 * batch_size
+    env = DOG.env_reset(n, num_players=P, seed=seed, device=device, **r)
+    for sp in range(1, 4):   # block sp started by player sp (its deals keyed by seed + sp)
+        blk = DOG.env_reset(batch_size, num_players=P, starting_player=sp, seed=seed + sp, device=device, **r)
+        sl = slice(sp * batch_size, (sp + 1) * batch_size)
+        for k in ("board", "pins", "deck", "hands", "swap_choices"):
+            getattr(env, k)[:, sl] = getattr(blk, k)
+        for k in ("current_player", "round_starter", "phase", "hand_size", "reward", "done", "deal"):
+            getattr(env, k)[sl] = getattr(blk, k)
+    ws = MD.SearchWorkspace(n, num_simulations, device) if any(not isinstance(x, str) for x in seats) else None
+    for turn in range(max_turns):
+        active = env.done == 0
+        if not bool(active.any()):
+            break
+        legal = DOG.legal_mask(env)
+        has = (legal != 0).any(dim=1)
+        mover = active & has
+        cp = env.current_player.long()
+        act = torch.full((n,), -1, dtype=torch.int32, device=device)
+        for s, a in enumerate(seats):
+            sel = mover & (cp == s)
+            if not bool(sel.any()):
+                continue
+            if isinstance(a, str):
+                act = torch.where(sel, DOG.random_action(legal, seed=seed, turn=turn), act)
+            else:
+                idx = sel.nonzero().flatten()
+                sub = DOG.DOGState(*(getattr(env, k)[:, idx].contiguous() if getattr(env, k).dim() == 2 else
+                                     getattr(env, k)[idx].contiguous()
+                                     for k in ("board", "pins", "deck", "hands", "swap_choices", "current_player",
+                                               "round_starter", "phase", "hand_size", "reward", "done", "deal")),
+                                   rules=env.rules, num_players=P, seed=env.seed)
+                lg, v, e = MD.root_inference_fn(a, MD.encode_board(sub), scratch=ws.scratch)
+                pol, _ = MD.gumbel_muzero_policy(a, lg, v, e, legal[idx], num_simulations, max_depth, temperature,
+                                                 seed=seed, turn=turn, workspace=ws)
+                act[idx] = pol.action
+        act = torch.where(active, act, torch.full_like(act, -1))
+        DOG.env_step(env, act)   # negative: no_step (a game without a legal action, or a finished one)
+    w = winners(env, bool(r.get("enable_teams", False))) & (env.done != 0)[:, None]
+    prog = calculate_progress(env, bool(r.get("must_traverse_start", False)))
+    win_tab = w.long().reshape(4, batch_size, P).sum(dim=1)
+    prog_tab = prog.reshape(4, batch_size, P).mean(dim=1)
+    return {"games": n, "winners": win_tab.tolist(), "average_progress": prog_tab.tolist(),
+            "wins_per_player": win_tab.sum(dim=0).tolist(), "progress_per_player": (prog_tab.sum(dim=0) / 4).tolist(),
+            "finished": int((env.done != 0).sum()), "turns": turn + 1, "final_state": env}
