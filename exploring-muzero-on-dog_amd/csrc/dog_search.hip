@@ -383,6 +383,7 @@ struct WEntry {
   int a, n, child;   // child index, visit count, the node it leads to
   float p, c;        // prior, transformed completed Q
   float r, d;        // reward, discount
+  float e;           // exp(prior - the node's max prior), cached in the record (NaN: not computed yet)
 };
 
 // record l of a node's visited list into e (a = -1 when l >= vc) and its q = reward + discount * value
@@ -390,7 +391,7 @@ __device__ __forceinline__ float wrec_load(WEntry& e, const WTree& T, int g, int
   e.a = -1;
   e.n = 0;
   e.child = -1;
-  e.p = e.c = e.r = e.d = 0.f;
+  e.p = e.c = e.r = e.d = e.e = 0.f;
   float q = 0.f;
   if (l < vc) {
     const AS1 f32x4* rp = T.vr(g, node) + 2 * l;
@@ -401,6 +402,7 @@ __device__ __forceinline__ float wrec_load(WEntry& e, const WTree& T, int g, int
     e.r = r1[0];
     e.d = r1[1];
     e.child = __float_as_int(r1[2]);
+    e.e = r1[3];
     q = r1[0] + r1[1] * r0[3];   // q = reward + discount * value (Tree.qvalues)
   }
   return q;
@@ -422,10 +424,7 @@ __device__ __forceinline__ bool wnode_compact(WNode& nd, const WTree& T, int g, 
   }
   const float q = wrec_load(en, T, g, node, sub, vc);
   ST(ST_PASS);   // (diagnostic builds: node loads)
-  if (en.a >= 0) {
-    nd.pr[en.a] = en.p;
-    nd.cq[en.a] = q;
-  }
+  if (en.a >= 0) nd.cq[en.a] = q;
   // this lane's visited slots: the list entries whose child sits in this lane
   unsigned vm = 0;
   for (int k = 0; k < vc; ++k) {
@@ -440,6 +439,18 @@ __device__ __forceinline__ bool wnode_compact(WNode& nd, const WTree& T, int g, 
   if (__popc(bits) < 2) return false;
   const int k1 = __ffs(bits) - 1, k2 = __ffs(bits & (bits - 1u)) - 1;
   nd.pm = __shfl(tp, 0, kRowLanes);   // the list's first prior is the node's largest
+  // the visited children's exp(prior - max prior), kept in their records from the first time a walk needs them (the
+  // node's priors and maximum do not change until it is expanded again, which resets the cache through a full load):
+  // the Q transform's prior probabilities and the certified selection's normaliser read them instead of recomputing
+  // the correctly rounded exponentials at every level of every walk.  nd.pr holds them (not the priors) for
+  // wnode_tail<true>.
+  if (en.a >= 0) {
+    if (en.e != en.e) {
+      en.e = exp_cr_w(en.p - nd.pm);
+      tree_st(reinterpret_cast<AS1 float*>(T.vr(g, node) + 2 * sub + 1) + 3, en.e);
+    }
+    nd.pr[en.a] = en.e;
+  }
   nd.u1 = __shfl(tp, k1, kRowLanes);
   nd.ui = __shfl(ti, k1, kRowLanes);
   nd.u2 = __shfl(tp, k2, kRowLanes);
@@ -455,11 +466,12 @@ __device__ __forceinline__ bool wnode_compact(WNode& nd, const WTree& T, int g, 
 // The mixed value needs the prior probabilities of the VISITED children only: sum_probs and weighted_q are summed
 // over this lane's visited slots (a bit mask, in slot order) -- the unvisited ones add exact zeros in the
 // restatement's order (lane_tree_sum), which change no partial sum -- so their exponentials are not recomputed.
-__device__ __forceinline__ void wnode_tail(WNode& nd, int sub, float raw, const SearchArgs& sa) {
+// exps (the compact load): nd.pr holds the visited children's exp(prior - max prior) instead of their priors.
+__device__ __forceinline__ void wnode_tail(WNode& nd, int sub, float raw, const SearchArgs& sa, bool exps) {
 #pragma clang fp contract(off)
   const float pm = nd.pm, es = nd.es;
   const unsigned vm = nd.vm;
-  auto ppa = [&](int a) { return fmaxf(kTinyF, exp_cr_w(nd.pr[a] - pm) / es); };
+  auto ppa = [&](int a) { return fmaxf(kTinyF, (exps ? nd.pr[a] : exp_cr_w(nd.pr[a] - pm)) / es); };
   float spl = 0.f;
   for (unsigned m = vm; m; m &= m - 1u) spl = spl + ppa(sub + kRowLanes * (__ffs(m) - 1));
   const float sp = row_sum(spl);
@@ -498,8 +510,11 @@ __device__ __forceinline__ void wentries(const WNode& nd, const WTree& T, int g,
   if (en.a >= 0) {
     en.p = nd.pr[en.a];
     en.c = nd.cq[en.a];
-    // (the record's prior refreshed: the node's priors change when it is expanded again at the depth limit)
+    en.e = exp_cr_w(en.p - nd.pm);
+    // (the record's prior and cached exponential refreshed: the node's priors change when it is expanded again at
+    // the depth limit)
     tree_st(reinterpret_cast<AS1 float*>(T.vr(g, node) + 2 * sub) + 2, en.p);
+    tree_st(reinterpret_cast<AS1 float*>(T.vr(g, node) + 2 * sub + 1) + 3, en.e);
   }
 }
 
@@ -529,7 +544,7 @@ __device__ __forceinline__ int wselect_certified(const WNode& nd, const WEntry& 
   const float zm = fmaxf(row_max(z), zU);   // fl(p + K) is monotone in p: zU is the unvisited maximum
   const float ez = has ? exp_cr_w(z - zm) : 0.f;
   const float sez = row_sum(ez);
-  const float sep = row_sum(has ? exp_cr_w(en.p - nd.pm) : 0.f);
+  const float sep = row_sum(has ? en.e : 0.f);   // en.e = exp_cr_w(en.p - nd.pm) (wnode_compact / wentries)
   const double f = exp((double)K + (double)nd.pm - (double)zm);
   const double zsa = (double)sez + f * fmax((double)nd.es - (double)sep, 0.0);
   // per-element relative error of the argument roundings <= 2^-24 (c0 + 3 d) e^-d summed (d e^-d <= 1/e over 806
@@ -701,7 +716,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
 #pragma unroll 1
         for (int pass = 0; pass < 2 && bi < 0; ++pass) {
           if (!compact) wnode_full(nd, T, g, node, sub, s_ces[row]);
-          wnode_tail(nd, sub, s_raw[row][node], sa);
+          wnode_tail(nd, sub, s_raw[row][node], sa, compact);
           if (depth == 0) {
             // gumbel_muzero_root_action_selection: score_considered + masked_argmax
             const int cv = wconsidered_visit(ncons, sa.S, nd.sv);
@@ -883,7 +898,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
             const int cnode = (l == d - 1) ? nx : p_node[row][l + 1];
             AS1 f32x4* rp = T.vr(g, parent) + 2 * k;
             tree_st(rp, f32x4{__int_as_float(pact), __int_as_float(cvis + 1), p_prior[row][l], child_v});
-            tree_st(rp + 1, f32x4{r, dsc, __int_as_float(cnode), 0.f});
+            if (cvis == 0) {   // a new record: its cached exponential not computed yet
+              tree_st(rp + 1, f32x4{r, dsc, __int_as_float(cnode), __builtin_nanf("")});
+            } else {           // (keep the record's cached exponential)
+              AS1 float* r1 = reinterpret_cast<AS1 float*>(rp + 1);
+              tree_st(r1, r);
+              tree_st(r1 + 1, dsc);
+              tree_st(r1 + 2, __int_as_float(cnode));
+            }
           }
         }
         carry = __shfl(leaf, 0, kRowLanes);
@@ -901,7 +923,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_dog_search(muz_dog_net_w Wt, Se
     nd.pr = smem + row * kDogA;
     nd.cq = smem + (kRows + row) * kDogA;
     wnode_full(nd, T, g, 0, sub, s_ces[row]);
-    wnode_tail(nd, sub, s_raw[row][0], sa);
+    wnode_tail(nd, sub, s_raw[row][0], sa, false);
     wfill_unvisited(nd, sub);
     const int bi = wroot_argmax(T, g, sub, nd.cq, [&](int j) { return nd.vis(j); }, nd.mv, legal_of);   // considered_visit = max(visits)
     // action_weights = softmax(_mask_invalid_actions(prior + completed_q))
