@@ -29,9 +29,10 @@ def report(buf, wg_sims, header):
 
 
 def games_per_wg(B):
-    """k_dog_search's games per workgroup: one per wave (8) up to 2048 games unless MUZ_DOG_TILE_ROWS says 16."""
-    rows = os.environ.get("MUZ_DOG_TILE_ROWS")
-    return 8 if (rows == "8" if rows else B <= 2048) else 16
+    """k_dog_search's games per workgroup as the library launches it (muz_dog_search_games_per_workgroup; round 5's
+    logs divided by ceil(B / 8) workgroups while 1500 games ran on 250 of 6: their cycles per workgroup-simulation
+    are 250 / 188 = 1.33x too high, the shares unaffected)."""
+    return int(L.load().muz_dog_search_games_per_workgroup(B))
 
 
 def main():
