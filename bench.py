@@ -703,7 +703,10 @@ def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, 
     from exploring_muzero_on_dog_amd import pipeline as PL
     from exploring_muzero_on_dog_amd import transfer as TR
     s_play = torch.cuda.Stream(device=device) if is_actor else None
-    s_learn = torch.cuda.Stream(device=device) if is_learner else None
+    # MUZ_LEARNER_PRIORITY=1: the learner's stream at the highest priority (its kernels dispatched ahead of the
+    # self-play stream's when both wait for CUs; round-6 A/B, profiles/r6j_*)
+    prio = -1 if os.environ.get("MUZ_LEARNER_PRIORITY") == "1" else 0
+    s_learn = torch.cuda.Stream(device=device, priority=prio) if is_learner else None
     steps = {"n": 2}
 
     def play(g):
