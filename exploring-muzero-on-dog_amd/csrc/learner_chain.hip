@@ -37,30 +37,84 @@ constexpr int N = 256, R = 16, LD = N + 4, NTH = 64 * NWAVE, KB = N / 16, D = MU
 constexpr int TPR = NTH / R, E = N / TPR;   // row phases: threads per row, columns per thread
 static_assert(NWAVE == 8 || NWAVE == 16, "8 or 16 waves");
 constexpr int kLayers = 6;   // Dense + LayerNorm layers; weight layer 6 = the projection
+// The per-layer vectors (LayerNorm scale / bias, Dense bias) staged in LDS once per launch, and the backward's saved
+// values loaded a layer ahead: bit-identical, and measured neutral (forward 407 -> 402 us, backward 431 -> 434 us,
+// profiles/r6l_chain_bench.log) -- the row phases were not waiting on those loads; the DPP row sums below were
+// what paid.  Forward, per group: gamma[6], beta[6], bias[7], LayerNorm_0 scale, LayerNorm_0 bias; backward:
+// gamma[6], LayerNorm_0 scale.
+constexpr int kPf = 21 * N, kPfBeta = 6 * N, kPfBias = 12 * N, kPfL0g = 19 * N, kPfL0b = 20 * N;
+constexpr int kPb = 7 * N, kPbL0g = 6 * N;
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float row_sum(float v) {
+// Row reductions over the TPR lanes of a row.  MUZ_CHAIN_DPP (default): on the DPP / permlane network -- xor-1, xor-2
+// (quad_perm), half-row and row mirrors, then v_permlane16_swap across the two 16-lane rows -- instead of a
+// ds_bpermute butterfly through the LDS crossbar (5 dependent round trips per sum).  Every step combines a
+// commutative pair in both lanes, so all lanes of a row end with the same bits (a different summation order from the
+// butterfly's: not bit-identical to the round-5 kernels; the learner tests bound it).  Forward 402.8 -> 389.6 us,
+// backward 434.6 -> 421.3 us; det step 1.585 -> 1.548 ms (profiles/r6m_chain_bench.log, r6m_steps.log).
+#ifndef MUZ_CHAIN_DPP
+#define MUZ_CHAIN_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ unsigned dppu(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <class T, class F>
+__device__ __forceinline__ T row_reduce(T v, F f) {
+  if constexpr (MUZ_CHAIN_DPP && TPR == 32) {
+    auto step = [&](unsigned o) { v = f(v, __builtin_bit_cast(T, o)); };
+    step(dppu<0xB1>(__builtin_bit_cast(unsigned, v)));    // xor 1
+    step(dppu<0x4E>(__builtin_bit_cast(unsigned, v)));    // xor 2
+    step(dppu<0x141>(__builtin_bit_cast(unsigned, v)));   // half-row mirror
+    step(dppu<0x140>(__builtin_bit_cast(unsigned, v)));   // row mirror
+    const auto p = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                    false, false);
+    const unsigned lo = p[0], hi = p[1];
+    return f(__builtin_bit_cast(T, lo), __builtin_bit_cast(T, hi));
+  } else {
 #pragma unroll
-  for (int o = TPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+    for (int o = TPR / 2; o >= 1; o >>= 1) v = f(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+}
+
+__device__ __forceinline__ float row_sum(float v) {
+  return row_reduce(v, [](float x, float y) { return x + y; });
 }
 
 __device__ __forceinline__ int row_isum(int v) {
-#pragma unroll
-  for (int o = TPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return row_reduce(v, [](int x, int y) { return x + y; });
 }
 
-// the lowest column of the row's extremum (k_minmax_fwd's wave_argext over the TPR lanes of a row)
+// the lowest column of the row's extremum (k_minmax_fwd's wave_argext over the TPR lanes of a row); the pair rides
+// the same network as one 64-bit value (value bits low, column high)
 __device__ __forceinline__ void row_argext(float& v, int& i, bool is_max) {
+  if constexpr (MUZ_CHAIN_DPP && TPR == 32) {
+    auto pick = [is_max](float a, int ia, float b, int ib, float& r, int& ir) {
+      const bool take_b = (is_max ? b > a : b < a) || (b == a && ib < ia);
+      r = take_b ? b : a;
+      ir = take_b ? ib : ia;
+    };
+    auto step = [&](unsigned ov, unsigned oi) { pick(v, i, __builtin_bit_cast(float, ov), (int)oi, v, i); };
+    step(dppu<0xB1>(__builtin_bit_cast(unsigned, v)), dppu<0xB1>((unsigned)i));
+    step(dppu<0x4E>(__builtin_bit_cast(unsigned, v)), dppu<0x4E>((unsigned)i));
+    step(dppu<0x141>(__builtin_bit_cast(unsigned, v)), dppu<0x141>((unsigned)i));
+    step(dppu<0x140>(__builtin_bit_cast(unsigned, v)), dppu<0x140>((unsigned)i));
+    const auto pv = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                     false, false);
+    const auto pi = __builtin_amdgcn_permlane16_swap((unsigned)i, (unsigned)i, false, false);
+    const unsigned vlo = pv[0], vhi = pv[1], ilo = pi[0], ihi = pi[1];
+    pick(__builtin_bit_cast(float, vlo), (int)ilo, __builtin_bit_cast(float, vhi), (int)ihi, v, i);
+  } else {
 #pragma unroll
-  for (int o = TPR / 2; o >= 1; o >>= 1) {
-    const float ov = __shfl_xor(v, o, 64);
-    const int oi = __shfl_xor(i, o, 64);
-    if ((is_max ? ov > v : ov < v) || (ov == v && oi < i)) v = ov, i = oi;
+    for (int o = TPR / 2; o >= 1; o >>= 1) {
+      const float ov = __shfl_xor(v, o, 64);
+      const int oi = __shfl_xor(i, o, 64);
+      if ((is_max ? ov > v : ov < v) || (ov == v && oi < i)) v = ov, i = oi;
+    }
   }
 }
 
@@ -148,18 +202,32 @@ __device__ __forceinline__ float rstd_of(float s, float s2) {
   return 1.0f / sqrtf(fmaxf(0.f, s2 / (float)N - mean * mean) + 1e-6f);
 }
 
+// one f4 of a group's per-layer vectors per thread and step (forward: kPf floats, backward: kPb)
+template <bool FWD>
+__device__ __forceinline__ void stage_params(const AS4 muz_chain_args* a, float* prm) {
+  constexpr int P4 = (FWD ? kPf : kPb) / 4;
+  for (int q = threadIdx.x; q < a->ngroups * P4; q += NTH) {
+    const int g = q / P4, s = (q % P4) / (N / 4), c = 4 * (q % (N / 4));
+    const AS4 muz_chain_group* G = &a->group[g];
+    const float* src;
+    if (FWD)
+      src = s < 6 ? G->gamma[s] : s < 12 ? G->beta[s - 6] : s < 19 ? G->bias[s - 12] : s == 19 ? G->ln0_gamma
+                                                                                                  : G->ln0_beta;
+    else
+      src = s < 6 ? G->gamma[s] : G->ln0_gamma;
+    *reinterpret_cast<f4*>(prm + g * (FWD ? kPf : kPb) + s * N + c) = *reinterpret_cast<const AS1 f4*>(gp(src + c));
+  }
+}
+
 // ---- forward ---------------------------------------------------------------------------------------------
-// Every row phase's global operands are loaded BEFORE the next matrix is primed: loads retire in order for
-// s_waitcnt vmcnt, so an operand issued behind the prime's 14 loads would wait for all of them.
-struct Ln0Ops {   // LayerNorm_0 + FiLM of one application
-  float ga[E], be[E], sc[E], sh[E];
+// Loads retire in order for s_waitcnt vmcnt: a global operand is issued right AFTER a prime, so the GEMM's first
+// k-blocks do not wait for it, and early enough that the GEMM's later k-blocks find it arrived.
+struct Ln0Ops {   // the FiLM operands of one application
+  float sc[E], sh[E];
 };
 
 __device__ __forceinline__ void load_ln0(const AS4 muz_chain_args* a, int i, size_t MN, size_t o, bool live,
-                                         int c0, Ln0Ops& p) {
-  const AS4 muz_chain_group* G = &a->group[a->app[i]];
-  ldEg(G->ln0_gamma + c0, p.ga);
-  ldEg(G->ln0_beta + c0, p.be);
+                                         Ln0Ops& p) {
   if (live) {
     ldEg(a->scale1 + i * MN + o, p.sc);
     ldEg(a->shift + i * MN + o, p.sh);
@@ -176,11 +244,13 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
   __shared__ __attribute__((aligned(16))) float ys[R * LD];    // its output (+ bias)
   __shared__ __attribute__((aligned(16))) float rs[R * LD];    // the current ResBlock's input
   __shared__ __attribute__((aligned(16))) float lat[R * LD];   // x_i
+  __shared__ __attribute__((aligned(16))) float prm[2 * kPf];   // the groups' per-layer vectors
   const int tid = threadIdx.x, M = a->M, T = a->T;
   const int row = tid / TPR, c0 = E * (tid % TPR), m = blockIdx.x * R + row;
   const bool live = m < M;
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
   const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
+  stage_params<true>(a, prm);
   {
     float v[E] = {};
     if (live) ldEg(a->latent0 + o, v);
@@ -188,18 +258,22 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
     stE(lat + row * LD + c0, v);
   }
   Ln0Ops n0;
-  load_ln0(a, 0, MN, o, live, c0, n0);
+  load_ln0(a, 0, MN, o, live, n0);
   Ring rg;
   rg.prime(a->group[a->app[0]].wf[0]);
+  __syncthreads();   // prm
 #pragma unroll 1
   for (int i = 0; i < T; ++i) {
     const AS4 muz_chain_group* G = &a->group[a->app[i]];
+    const float* pg = prm + a->app[i] * kPf;
     const size_t js = (size_t)a->slot[i] * MN + o;     // this row's offset in the group's stacks
     float* st = a->stats + (size_t)i * 7 * 2 * M;
     // LayerNorm_0 + FiLM (k_ln_fwd<256, true>)
     {
-      float v[E];
+      float v[E], ga[E], be[E];
       ldE(lat + row * LD + c0, v);
+      ldE(pg + kPfL0g + c0, ga);
+      ldE(pg + kPfL0b + c0, be);
       float s = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -212,7 +286,7 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
       float ln[E], f[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        ln[e] = (v[e] - mean) * (rstd * n0.ga[e]) + n0.be[e];
+        ln[e] = (v[e] - mean) * (rstd * ga[e]) + be[e];
         float p = ln[e] * n0.sc[e];
         asm volatile("" : "+v"(p));   // a multiply, then an add (torch's addcmul; no fma)
         f[e] = n0.sh[e] + p;
@@ -229,24 +303,25 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_fwd(muz_chain_args) {
     for (int l = 0; l <= kLayers; ++l) {
       f4 acc[NT];
       gemm(rg, xs, acc);
-      float ga[E], be[E];
       f4 bb[NT] = {};
       if (l < kLayers) {
-        ldEg(G->gamma[l] + c0, ga);
-        ldEg(G->beta[l] + c0, be);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) bb[t] = *reinterpret_cast<const AS1 f4*>(gp(G->bias[l] + 16 * NT * w + 16 * t + 4 * lg));
         rg.prime(G->wf[l + 1]);   // the next GEMM's matrix flies during the row phase
-      } else {
-        ldEg(G->bias[6] + c0, ga);
-        if (i + 1 < T) {
-          load_ln0(a, i + 1, MN, o, live, c0, n0);
-          rg.prime(a->group[a->app[i + 1]].wf[0]);
-        }
+        if (l == 2 && i + 1 < T) load_ln0(a, i + 1, MN, o, live, n0);   // (behind the prime: see above)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bb[t] = *reinterpret_cast<const f4*>(pg + kPfBias + l * N + 16 * NT * w + 16 * t + 4 * lg);
+      } else if (i + 1 < T) {
+        rg.prime(a->group[a->app[i + 1]].wf[0]);
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t) *reinterpret_cast<f4*>(ys + li * LD + 16 * NT * w + 16 * t + 4 * lg) = acc[t] + bb[t];
       __syncthreads();
+      float ga[E], be[E];
+      if (l < kLayers) {
+        ldE(pg + l * N + c0, ga);
+        ldE(pg + kPfBeta + l * N + c0, be);
+      } else {
+        ldE(pg + kPfBias + 6 * N + c0, ga);
+      }
       if (l < kLayers) {
         // Dense epilogue (k_ln_fwd): z = y + bias, LayerNorm, ReLU / residual ReLU
         const bool resid = l == 3 || l == 5;
@@ -345,10 +420,35 @@ __device__ __forceinline__ void partials(const float* pgs, const float* pbs, con
 struct MmOps {   // min-max backward of one application; lohi = (min, max) of q
   float g[E], q[E], h[E], lohi[2];
 };
-struct RowOps {  // a Dense + LayerNorm layer's saved forward values (LayerNorm_0: out = its output)
-  float out[E], z[E], ga[E];
+struct RowOps {  // a Dense + LayerNorm layer's saved forward values (LayerNorm_0: out = its output, sc = its FiLM scale)
+  float out[E], z[E], sc[E];
   float mean, rstd;
 };
+
+// The saved values of dense layer k (k >= 0) or, k < 0, of LayerNorm_0, of application i.  Loaded one layer ahead
+// of the row phase that uses them (they come from HBM / MALL: the forward wrote them a whole chain earlier).
+__device__ __forceinline__ void load_rows(const AS4 muz_chain_args* a, int i, int k, size_t MN, size_t o, int m,
+                                          bool live, RowOps& r) {
+  if (live) {
+    const int M = a->M;
+    const AS1 float* st = gp(a->stats) + (size_t)i * 7 * 2 * M;
+    if (k >= 0) {
+      const AS4 muz_chain_group* G = &a->group[a->app[i]];
+      ldEg(G->X[k + 1] + (size_t)a->slot[i] * MN + o, r.out);
+      ldEg(a->z + ((size_t)i * kLayers + k) * MN + o, r.z);
+      r.mean = st[(2 + 2 * k) * M + m], r.rstd = st[(3 + 2 * k) * M + m];
+    } else {
+      ldEg(a->ln0_out + i * MN + o, r.out);
+      ldEg((i == 0 ? a->latent0 : a->out + (i - 1) * MN) + o, r.z);
+      r.mean = st[m], r.rstd = st[M + m];
+      ldEg(a->scale1 + i * MN + o, r.sc);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) r.out[e] = r.z[e] = r.sc[e] = 0.f;
+    r.mean = r.rstd = 0.f;
+  }
+}
 
 __device__ __forceinline__ void load_mm(const AS4 muz_chain_args* a, int i, size_t MN, size_t o, int m, bool live,
                                         MmOps& p) {
@@ -375,22 +475,28 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
   __shared__ __attribute__((aligned(16))) float carry[R * LD];   // dq of application i, then + dz of its LayerNorm_0
   __shared__ __attribute__((aligned(16))) float pgs[R * N];      // per-row do * xhat, do (column partials)
   __shared__ __attribute__((aligned(16))) float pbs[R * N];
+  __shared__ __attribute__((aligned(16))) float prm[2 * kPb];    // the groups' LayerNorm scales
   const int tid = threadIdx.x, M = a->M, T = a->T;
   const int row = tid / TPR, c0 = E * (tid % TPR), m = blockIdx.x * R + row;
   const bool live = m < M;
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
   const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
   const int tiles = (M + R - 1) / R;
+  stage_params<false>(a, prm);   // (published by the barrier after the first min-max phase)
   MmOps mm;
   load_mm(a, T - 1, MN, o, m, live, mm);
   Ring rg;
   rg.prime(a->group[a->app[T - 1]].wb[6]);
+  // ro: the saved values of the row phase after the current GEMM; nx: of the one after that, loaded a whole layer
+  // ahead (ro = nx right after a GEMM: nx's loads are older than the GEMM's weight loads, so they have arrived)
+  RowOps ro, nx;
+  load_rows(a, T - 1, kLayers - 1, MN, o, m, live, nx);
 #pragma unroll 1
   for (int i = T - 1; i >= 0; --i) {
     const AS4 muz_chain_group* G = &a->group[a->app[i]];
+    const float* pg = prm + a->app[i] * kPb;
     const size_t js = (size_t)a->slot[i] * MN + o;
     const size_t pj = ((size_t)a->slot[i] * tiles + blockIdx.x) * 3 * N;   // this tile's partial block
-    const float* st = a->stats + (size_t)i * 7 * 2 * M;
     // min-max backward (k_minmax_bwd): d = (g + carry) x scale + h
     {
       float d[E];
@@ -439,40 +545,21 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
       if (live) stEg(G->DZ[6] + js, dq);
     }
     __syncthreads();
-    RowOps ro;
-    float sc0[E];   // LayerNorm_0's FiLM scale (loaded with its other operands)
 #pragma unroll 1
     for (int l = kLayers; l >= 0; --l) {
       // GEMM: dx = dz W_l^T (+ the residual gradient after a ResBlock's first layer)
       f4 acc[NT];
       gemm(rg, dzs, acc);
-      // the next row phase's operands, then the next matrix
+      // the next matrix, then the saved values of the row phase after next
       const int k = l - 1;
+      ro = nx;
       if (l > 0) {
-        ldEg(G->gamma[k] + c0, ro.ga);
-        if (live) {
-          ldEg(G->X[k + 1] + js, ro.out);
-          ldEg(a->z + ((size_t)i * kLayers + k) * MN + o, ro.z);
-          ro.mean = gp(st)[(2 + 2 * k) * M + m], ro.rstd = gp(st)[(3 + 2 * k) * M + m];
-        }
         rg.prime(G->wb[k]);
-      } else {
-        ldEg(G->ln0_gamma + c0, ro.ga);
-        if (live) {
-          ldEg(a->ln0_out + i * MN + o, ro.out);
-          ldEg((i == 0 ? a->latent0 : a->out + (i - 1) * MN) + o, ro.z);
-          ro.mean = gp(st)[m], ro.rstd = gp(st)[M + m];
-          ldEg(a->scale1 + i * MN + o, sc0);
-        }
-        if (i > 0) {
-          load_mm(a, i - 1, MN, o, m, live, mm);
-          rg.prime(a->group[a->app[i - 1]].wb[6]);
-        }
-      }
-      if (!live) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) ro.out[e] = ro.z[e] = 0.f;
-        ro.mean = ro.rstd = 0.f;
+        load_rows(a, i, k - 1, MN, o, m, live, nx);   // (k - 1 < 0: LayerNorm_0's)
+        if (l == 3 && i > 0) load_mm(a, i - 1, MN, o, m, live, mm);   // (mm was consumed by this application)
+      } else if (i > 0) {
+        rg.prime(a->group[a->app[i - 1]].wb[6]);
+        load_rows(a, i - 1, kLayers - 1, MN, o, m, live, nx);
       }
       const bool add_res = l == 2 || l == 4;
       const int mr = blockIdx.x * R + li;
@@ -491,14 +578,15 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
       if (l == 0) break;
       // LayerNorm / ReLU backward of Dense layer k (k_dense_ln_bwd's row half)
       const bool resid = k == 3 || k == 5;
-      float d[E];
+      float d[E], ga[E];
       ldE(dxs + row * LD + c0, d);
+      ldE(pg + k * N + c0, ga);
       float xh[E], gg[E], sa = 0.f, sb = 0.f;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if (!(ro.out[e] > 0.f)) d[e] = 0.f;
         xh[e] = (ro.z[e] - ro.mean) * ro.rstd;
-        gg[e] = d[e] * ro.ga[e];
+        gg[e] = d[e] * ga[e];
         sa += gg[e];
         sb += gg[e] * xh[e];
       }
@@ -520,15 +608,16 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
     // LayerNorm_0 + FiLM backward (k_ln_bwd<256, true>; ro = its saved values, scale1 below); then
     // carry = dz_0 + dq, the gradient of x_i
     {
-      float d[E];
+      float d[E], ga[E];
       ldE(dxs + row * LD + c0, d);
+      ldE(pg + kPbL0g + c0, ga);
       float ds[E], xh[E], gg[E], sa = 0.f, sb = 0.f;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         ds[e] = d[e] * ro.out[e];
-        d[e] = d[e] * (live ? sc0[e] : 0.f);
+        d[e] = d[e] * (live ? ro.sc[e] : 0.f);
         xh[e] = (ro.z[e] - ro.mean) * ro.rstd;
-        gg[e] = d[e] * ro.ga[e];
+        gg[e] = d[e] * ga[e];
         sa += gg[e];
         sb += gg[e] * xh[e];
       }
@@ -569,13 +658,24 @@ __global__ __launch_bounds__(NTH, 1) void k_chain_bwd(muz_chain_args) {
 // The same tile, GEMM loop and row arithmetic as the chain: weight layer l = 2 b + k of block b; the ResBlock input
 // stays in LDS (rs) for the second layer's residual.
 struct RowOpsRb {   // a layer's saved forward values for its backward rows; ms = (mean, rstd)
-  float out[E], z[E], ga[E], ms[2];
+  float out[E], z[E], ms[2];
 };
 
+// the stack's per-layer vectors in LDS (as the chain's): forward gamma / beta / bias of each layer, backward gamma
+constexpr int kRbMax = 2 * MUZ_RBSTACK_MAX, kRbBeta = kRbMax * N, kRbBias = 2 * kRbMax * N;
+template <bool FWD>
+__device__ __forceinline__ void stage_rb_params(const AS4 muz_rbstack_args* a, float* prm) {
+  const int L = 2 * a->nb;
+  for (int q = threadIdx.x; q < (FWD ? 3 : 1) * L * (N / 4); q += NTH) {
+    const int s = q / (N / 4), c = 4 * (q % (N / 4)), v = s / L, l = s % L;
+    const float* src = v == 0 ? a->gamma[l] : v == 1 ? a->beta[l] : a->bias[l];
+    *reinterpret_cast<f4*>(prm + v * kRbMax * N + l * N + c) = *reinterpret_cast<const AS1 f4*>(gp(src + c));
+  }
+}
+
 __device__ __forceinline__ void load_rb_rows(const AS4 muz_rbstack_args* a, int l, size_t MN, size_t o, int m,
-                                             bool live, int c0, RowOpsRb& p) {
+                                             bool live, RowOpsRb& p) {
   const int L = 2 * a->nb, M = a->M;
-  ldEg(a->gamma[l] + c0, p.ga);
   if (live) {
     ldEg((l + 1 < L ? a->X + (l + 1) * MN : a->out) + o, p.out);
     ldEg(a->z + l * MN + o, p.z);
@@ -594,11 +694,13 @@ __global__ __launch_bounds__(NTH, 1) void k_rbstack_fwd(muz_rbstack_args) {
   __shared__ __attribute__((aligned(16))) float xs[R * LD];    // the current GEMM's input
   __shared__ __attribute__((aligned(16))) float ys[R * LD];    // its output (+ bias)
   __shared__ __attribute__((aligned(16))) float rs[R * LD];    // the current ResBlock's input
+  __shared__ __attribute__((aligned(16))) float prm[3 * kRbMax * N];
   const int tid = threadIdx.x, M = a->M, L = 2 * a->nb;
   const int row = tid / TPR, c0 = E * (tid % TPR), m = blockIdx.x * R + row;
   const bool live = m < M;
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
   const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
+  stage_rb_params<true>(a, prm);   // (published by the barrier below)
   {
     float v[E] = {};
     if (live) ldEg(a->x + o, v);
@@ -615,16 +717,16 @@ __global__ __launch_bounds__(NTH, 1) void k_rbstack_fwd(muz_rbstack_args) {
     gemm(rg, xs, acc);
     float ga[E], be[E];
     f4 bb[NT];
-    ldEg(a->gamma[l] + c0, ga);
-    ldEg(a->beta[l] + c0, be);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) bb[t] = *reinterpret_cast<const AS1 f4*>(gp(a->bias[l] + 16 * NT * w + 16 * t + 4 * lg));
     if (l + 1 < L) rg.prime(a->wf[l + 1]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) bb[t] = *reinterpret_cast<const f4*>(prm + kRbBias + l * N + 16 * NT * w + 16 * t + 4 * lg);
 #pragma unroll
     for (int t = 0; t < NT; ++t) *reinterpret_cast<f4*>(ys + li * LD + 16 * NT * w + 16 * t + 4 * lg) = acc[t] + bb[t];
     __syncthreads();
     const bool resid = l & 1;
     float v[E], res[E];
+    ldE(prm + l * N + c0, ga);
+    ldE(prm + kRbBeta + l * N + c0, be);
     ldE(ys + row * LD + c0, v);
     if (resid) ldE(rs + row * LD + c0, res);
     float s = 0.f, s2 = 0.f;
@@ -661,34 +763,40 @@ __global__ __launch_bounds__(NTH, 1) void k_rbstack_bwd(muz_rbstack_args) {
   __shared__ __attribute__((aligned(16))) float dres[R * LD];    // the ResBlock's residual gradient
   __shared__ __attribute__((aligned(16))) float pgs[R * N];      // per-row do * xhat, do (column partials)
   __shared__ __attribute__((aligned(16))) float pbs[R * N];
+  __shared__ __attribute__((aligned(16))) float prm[kRbMax * N];   // the layers' LayerNorm scales
   const int tid = threadIdx.x, M = a->M, L = 2 * a->nb;
   const int row = tid / TPR, c0 = E * (tid % TPR), m = blockIdx.x * R + row;
   const bool live = m < M;
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4, w = tid >> 6;
   const size_t MN = (size_t)M * N, o = (size_t)m * N + c0;
   const int tiles = (M + R - 1) / R;
+  stage_rb_params<false>(a, prm);
   {
     float v[E] = {};
     if (live) ldEg(a->g + o, v);
     stE(dxs + row * LD + c0, v);
   }
-  RowOpsRb ro;
-  load_rb_rows(a, L - 1, MN, o, m, live, c0, ro);
+  // ro: the saved values of the current row phase; nx: of the next one, loaded a layer ahead (ro = nx right after
+  // a GEMM, whose later weight loads are younger than nx's)
+  RowOpsRb ro, nx;
+  load_rb_rows(a, L - 1, MN, o, m, live, ro);
   Ring rg;
   rg.prime(a->wb[L - 1]);
+  if (L > 1) load_rb_rows(a, L - 2, MN, o, m, live, nx);
   __syncthreads();
 #pragma unroll 1
   for (int l = L - 1; l >= 0; --l) {
     // LayerNorm / ReLU backward of layer l (k_dense_ln_bwd's row half); odd l: the residual ReLU
     const bool resid = l & 1;
-    float d[E];
+    float d[E], ga[E];
     ldE(dxs + row * LD + c0, d);
+    ldE(prm + l * N + c0, ga);
     float xh[E], gg[E], sa = 0.f, sb = 0.f;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       if (!(ro.out[e] > 0.f)) d[e] = 0.f;
       xh[e] = (ro.z[e] - ro.ms[0]) * ro.ms[1];
-      gg[e] = d[e] * ro.ga[e];
+      gg[e] = d[e] * ga[e];
       sa += gg[e];
       sb += gg[e] * xh[e];
     }
@@ -710,8 +818,9 @@ __global__ __launch_bounds__(NTH, 1) void k_rbstack_bwd(muz_rbstack_args) {
     f4 acc[NT];
     gemm(rg, dzs, acc);
     if (l > 0) {
-      load_rb_rows(a, l - 1, MN, o, m, live, c0, ro);
+      ro = nx;
       rg.prime(a->wb[l - 1]);
+      if (l > 1) load_rb_rows(a, l - 2, MN, o, m, live, nx);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {

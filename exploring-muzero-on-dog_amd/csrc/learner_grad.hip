@@ -11,9 +11,13 @@
 //   of every 8-row step s) with 2 x 2 v_mfma_f32_16x16x4_f32 accumulators (A = X^T: lane l reads X[m + l/16][k + l%16], B = dZ: lane l reads
 //   dZ[m + l/16][n + l%16], so each operand load is a 64-byte row segment).  Loads are issued 8 steps ahead of
 //   their MFMAs (one memory latency per 64 rows instead of per 8); the 64 x 64 tile halves the L2 re-reads of
-//   X and dZ against 32 x 32 tiles.  The two halves add their partials through LDS in a fixed order; a problem with one segment writes dW directly, longer ones write per-segment partials
-//   to scratch, which the column-sum launch below adds in segment order (deterministic: graph-captured and
-//   eager steps stay bit-identical).
+//   X and dZ against 32 x 32 tiles.  The two halves add their partials through LDS in a fixed order; a problem with
+//   one segment writes dW directly, longer ones write per-segment partials to scratch, which k_seg_sum adds in
+//   segment order (deterministic: graph-captured and eager steps stay bit-identical).
+// k_seg_sum: one thread per output element, p_0 + p_1 + ... in segment order (the sum k_colsum_grouped's kind 1
+//   formed for these partials, bit for bit, with one thread per element instead of a 1024-thread workgroup per 64
+//   columns: the round-5 512-row segments measured wgrad 107 -> 69 us but the partial sums 16 -> 118 us that way,
+//   profiles/r5q_wgrad_seg.log).
 // k_colsum_grouped: one workgroup per (problem, output, 64-column chunk); kind 0 reduces muz_ln_bwd_rows'
 //   per-block partials [nblk][3][N] into dgamma / dbeta / dbias (k_ln_colsum's order), kind 1 sums the rows of
 //   a matrix (a dZ into a bias gradient, or a weight gradient's segment partials).
@@ -25,7 +29,7 @@ typedef float f32x4_g __attribute__((ext_vector_type(4)));
 
 constexpr int kWgMax = 48;    // problems per launch (kernel-argument table)
 #ifndef MUZ_WGRAD_SEG
-#define MUZ_WGRAD_SEG 2048
+#define MUZ_WGRAD_SEG 256   // det / DOG learner step, profiles/r6p_steps.log: 2048 1.543 / 1.782 ms, 512 1.522 / 1.731, 256 1.512 / 1.729
 #endif
 constexpr int kWgSeg = MUZ_WGRAD_SEG;  // rows per workgroup (a multiple of 64)
 static_assert(kWgSeg % 64 == 0, "segments are whole 64-row steps");
@@ -115,6 +119,34 @@ __global__ __launch_bounds__(512) void k_wgrad_grouped(WgradTable t) {
     }
 }
 
+struct SegSumTable {
+  const float* part[kWgMax];
+  float* out[kWgMax];
+  int segs[kWgMax], kn[kWgMax], wg0[kWgMax + 1];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void k_seg_sum(SegSumTable t) {
+  const int wg = blockIdx.x;
+  int p = 0;
+  while (p + 1 < t.count && t.wg0[p + 1] <= wg) ++p;
+  const int kn = t.kn[p], e = (wg - t.wg0[p]) * 256 + threadIdx.x;
+  if (e >= kn) return;
+  const float* __restrict__ src = t.part[p] + e;
+  const int segs = t.segs[p];
+  float acc = 0.f;
+  // 8 partials in flight, then added in segment order (a load-add chain would wait one memory latency per segment)
+  for (int q0 = 0; q0 < segs; q0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = q0 + u < segs ? src[(size_t)(q0 + u) * kn] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (q0 + u < segs) acc += v[u];
+  }
+  t.out[p][e] = acc;
+}
+
 struct ColsumTable {
   const float* src[kWgMax];
   float* out[kWgMax][3];
@@ -164,6 +196,8 @@ using namespace muz;
 
 extern "C" {
 
+int32_t muz_wgrad_segment_rows(void) { return kWgSeg; }
+
 int64_t muz_wgrad_scratch_floats(const muz_wgrad_problem* probs, int32_t count) {
   if (count < 0 || (count > 0 && !probs)) return -1;
   int64_t n = 0;
@@ -179,13 +213,13 @@ int muz_wgrad_grouped(const muz_wgrad_problem* probs, int32_t count, float* scra
   MUZ_HOST_CHECK(count >= 0 && (count == 0 || probs));
   const int64_t need = muz_wgrad_scratch_floats(probs, count);
   MUZ_HOST_CHECK(need >= 0 && scratch_floats >= need && (need == 0 || scratch));
-  // the segment partials are summed by the column-sum kernel (kind 1: rows = segments), one launch per chunk
-  muz_colsum_problem red[kWgMax];
+  // the segment partials are summed by k_seg_sum, one launch per chunk of problems
   int64_t off = 0;
   for (int s = 0; s < count; s += kWgMax) {
     WgradTable t{};
+    SegSumTable r{};
     t.count = 0;
-    int wgs = 0, nred = 0;
+    int wgs = 0, nred = 0, rwgs = 0;
     for (int i = s; i < count && t.count < kWgMax; ++i) {
       const muz_wgrad_problem& q = probs[i];
       MUZ_HOST_CHECK((q.M == 0 || (q.x && q.dz)) && q.out && q.M >= 0 && q.K > 0 && q.N > 0 && q.ldx >= q.K &&
@@ -204,7 +238,9 @@ int muz_wgrad_grouped(const muz_wgrad_problem* probs, int32_t count, float* scra
         float* part = scratch + off;
         off += (int64_t)segs * q.K * q.N;
         t.out[c] = part;
-        red[nred++] = muz_colsum_problem{part, q.out, nullptr, nullptr, 1, segs, q.K * q.N, q.K * q.N};
+        r.part[nred] = part, r.out[nred] = q.out, r.segs[nred] = segs, r.kn[nred] = q.K * q.N;
+        r.wg0[nred++] = rwgs;
+        rwgs += (q.K * q.N + 255) / 256;
       }
     }
     t.wg0[t.count] = wgs;
@@ -213,7 +249,10 @@ int muz_wgrad_grouped(const muz_wgrad_problem* probs, int32_t count, float* scra
     int rc = muz_last_launch_error();
     if (rc) return rc;
     if (nred) {
-      rc = muz_colsum_grouped(red, nred, stream);
+      r.count = nred;
+      r.wg0[nred] = rwgs;
+      k_seg_sum<<<rwgs, 256, 0, (hipStream_t)stream>>>(r);
+      rc = muz_last_launch_error();
       if (rc) return rc;
     }
   }

@@ -144,6 +144,164 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
   for (int i = tid; i < kConvMapFloats; i += 256) dst[i] = c2in[i];   // flatten (w, ch) -> w*64 + ch
 }
 
+// Two games per workgroup (MUZ_CONV_PAIR 1: 4 waves, 2: 8 waves): their 112 positions are exactly 7 MFMA row tiles,
+// where one game per workgroup pads its 56 positions to 64 (1/8 of Conv_1 / Conv_2's MFMAs on padding rows).  Lane r
+// of row tile t computes position R = 16 t + r, i.e. position R % 56 of game R / 56, and reads that game's rows: each
+// game keeps its own zero rows around its positions, so every output is the same sum in the same order as
+// k_repr_conv's.  With 8 waves, waves w and w + 4 own the same 16 output channels, w tiles 0-3 and w + 4 tiles 4-6
+// (one SIMD carries both: the same MFMAs per SIMD, twice the waves to hide the row phases' latency).
+#ifndef MUZ_CONV_PAIR
+#define MUZ_CONV_PAIR 1   // root conv kernel traces, profiles/r6p_root_*: one game 146.8 us, pairs on 4 waves 141.4, on 8 142.2
+#endif
+constexpr int kPairThreads = MUZ_CONV_PAIR == 2 ? 512 : 256;
+constexpr int kPairRows = 112, kPairTiles = 7;
+constexpr int kG0 = 58, kG1 = 58, kG2 = 60;   // rows per game: Conv_0 / Conv_1 input (1 zero row each side), Conv_2 (2)
+
+// LayerNorm of 112 positions (4 lanes each; 2 passes with 256 threads), output row (R / 56) * GR + PAD + R % 56
+template <int N, int LDO, int GR, int PAD>
+__device__ __forceinline__ void ln_pair(const float* pre, float* out, const AS4 muz_ln& P) {
+  const int q = threadIdx.x & 3;
+  constexpr int PER = N / 4;
+#pragma unroll
+  for (int pass = 0; pass < 512 / kPairThreads; ++pass) {
+    const int pos = (threadIdx.x >> 2) + (kPairThreads / 4) * pass;
+    if (pos >= kPairRows) break;
+    float v[PER], s = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      v[i] = pre[pos * kPreLd + q + 4 * i];
+      s += v[i];
+      s2 = fmaf(v[i], v[i], s2);
+    }
+    s += dpp<DPP_XOR1>(s);
+    s += dpp<DPP_XOR2>(s);
+    s2 += dpp<DPP_XOR1>(s2);
+    s2 += dpp<DPP_XOR2>(s2);
+    const float mean = s / (float)N, mean2 = s2 / (float)N;
+    const float inv = ln_rstd(fmaxf(0.f, fmaf(-mean, mean, mean2)) + 1e-6f);
+    const int gm = pos >= 56 ? 1 : 0, orow = gm * GR + PAD + pos - 56 * gm;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = q + 4 * i;
+      out[orow * LDO + c] = fmaxf(fmaf(v[i] - mean, inv * gp(P.scale)[c], gp(P.bias)[c]), 0.f);
+    }
+  }
+}
+
+// conv_mfma over NT of the pair's 7 row tiles from tile T0 (wave wv's 16 output channels: wv % 4); GR = input rows
+// per game
+template <int KB, int CIN, int LDI, int GR, int T0, int NT>
+__device__ __forceinline__ void conv_mfma_pair(const AS4 muz_dense& L, const float* in, float* pre) {
+  static_assert(CIN % 16 == 0, "a k-block within one tap");
+  const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) & 3;
+  const int r = lane & 15, g = lane >> 4;
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(L.w)) + (size_t)wv * KB * 64 + lane;
+  int roff[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int R = (T0 + t) * 16 + r, gm = R >= 56 ? 1 : 0;
+    roff[t] = (gm * GR + R - 56 * gm) * LDI + 4 * g;
+  }
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 w0 = wp[0], w1 = KB > 1 ? wp[64] : w0, w2;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    if (kb + 2 < KB) w2 = wp[(kb + 2) * 64];
+    f32x4 a[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      a[t] = *reinterpret_cast<const f32x4*>(in + roff[t] + ((kb * 16) / CIN) * LDI + (kb * 16) % CIN);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma4(w0[j], a[t][j], acc[t]);
+    w0 = w1;
+    w1 = w2;
+  }
+  const AS1 f32x4* bias4 = gp(reinterpret_cast<const f32x4*>(L.b));
+  const f32x4 bb = bias4[(16 * wv + 4 * g) >> 2];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    *reinterpret_cast<f32x4*>(pre + ((T0 + t) * 16 + r) * kPreLd + 16 * wv + 4 * g) = acc[t] + bb;
+}
+
+template <int KB, int CIN, int LDI, int GR>
+__device__ __forceinline__ void conv_pair(const AS4 muz_dense& L, const float* in, float* pre) {
+  if (kPairThreads == 256)
+    conv_mfma_pair<KB, CIN, LDI, GR, 0, kPairTiles>(L, in, pre);
+  else if (threadIdx.x < 256)
+    conv_mfma_pair<KB, CIN, LDI, GR, 0, 4>(L, in, pre);
+  else
+    conv_mfma_pair<KB, CIN, LDI, GR, 4, 3>(L, in, pre);
+}
+
+__global__ __launch_bounds__(kPairThreads) void k_repr_conv2(muz_repr_w Rarg, const float* __restrict__ obs, int C, int n,
+                                                    const int* __restrict__ n_dev, float* __restrict__ convout,
+                                                    int32_t* host_counts) {
+  if (host_counts && blockIdx.x == 0 && threadIdx.x == 0) {   // (n_dev set: the self-play turn's counts)
+    __hip_atomic_store(&host_counts[0], n_dev[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host_counts[1], n_dev[1], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (n_dev) n = *n_dev;
+  const int g0 = 2 * (int)blockIdx.x;
+  if (g0 >= n) return;
+  const int ng = g0 + 1 < n ? 2 : 1;
+  const AS4 muz_repr_w& R = *kernarg0<muz_repr_w>();   // == Rarg, read through the kernarg segment
+  // LDS: pre + one buffer holding in0 | c1in until Conv_1 has read them, then c2in, then the flattened maps (65 KB)
+  __shared__ __attribute__((aligned(16))) float pre[kPairRows * kPreLd];
+  __shared__ __attribute__((aligned(16))) float buf[2 * kG2 * kC2Ld];
+  float* in0 = buf;                 // [2][58][6]
+  float* c1in = buf + 704;          // [2][58][kC1Ld]
+  float* c2in = buf;                // [2][60][kC2Ld]
+  static_assert(704 >= 2 * kG0 * 6 && 704 + 2 * kG1 * kC1Ld <= 2 * kG2 * kC2Ld && kPairRows * 64 <= 2 * kG2 * kC2Ld,
+                "pair conv LDS carve");
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 2 * kG0 * 6; i += kPairThreads) {
+    const int gm = i / (kG0 * 6), j = i % (kG0 * 6), w = j / 6 - 1, ch = j % 6;
+    in0[i] = (gm < ng && w >= 0 && w < 56) ? obs[((size_t)(g0 + gm) * C + ch) * 56 + w] : 0.f;
+  }
+  for (int i = tid; i < 2 * kG1 * kC1Ld; i += kPairThreads) c1in[i] = 0.f;
+  __syncthreads();
+  // Conv_0 (K = 3*6 = 18, N = 32) on VALU: a thread keeps one output channel, its 18 weights in registers
+  {
+    const int co = tid & 31;
+    float wk[18];
+#pragma unroll
+    for (int k = 0; k < 18; ++k) wk[k] = gp(R.conv0.w)[k * 32 + co];
+    const float bco = gp(R.conv0.b)[co];
+    for (int p = tid >> 5; p < kPairRows; p += kPairThreads / 32) {
+      const int gm = p >= 56 ? 1 : 0;
+      const float* x = in0 + gm * kG0 * 6 + (p - 56 * gm) * 6;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 18; ++k) s = fmaf(x[k], wk[k], s);
+      pre[p * kPreLd + co] = s + bco;
+    }
+  }
+  __syncthreads();
+  ln_pair<32, kC1Ld, kG1, 1>(pre, c1in, R.ln0);
+  __syncthreads();
+  conv_pair<6, 32, kC1Ld, kG1>(R.conv1, c1in, pre);
+  __syncthreads();
+  // c2in now reuses in0 | c1in: zero each game's pad rows (0, 1, 58, 59; the LayerNorm writes rows 2..57)
+  for (int i = tid; i < 8 * kC2Ld; i += kPairThreads) {
+    const int rr = i / kC2Ld, row = (rr >> 2) * kG2 + ((rr & 3) < 2 ? (rr & 3) : 56 + (rr & 3));
+    c2in[row * kC2Ld + i % kC2Ld] = 0.f;
+  }
+  ln_pair<64, kC2Ld, kG2, 2>(pre, c2in, R.ln1);
+  __syncthreads();
+  conv_pair<20, 64, kC2Ld, kG2>(R.conv2, c2in, pre);
+  __syncthreads();
+  ln_pair<64, 64, 56, 0>(pre, c2in, R.ln2);   // reuse c2in as the flattened output [2][56][64] (dense rows)
+  __syncthreads();
+  for (int i = tid; i < ng * kConvMapFloats; i += kPairThreads) {
+    const int gm = i >= kConvMapFloats ? 1 : 0;
+    convout[(size_t)(g0 + gm) * kConvRowFloats + i - gm * kConvMapFloats] = c2in[i];
+  }
+}
+
 // RepresentationNetwork2's Dense_0 (3584 -> 256, muzero_deterministic_madn.py:107) for every game as ONE GEMM over
 // 64-row x 64-column output tiles.  k_root_dense used to run it on its 16-row tiles, each tile streaming the layer's
 // 3.67 MB of weights from L2 for 16 rows (~80 us of a 4096-game root inference at the L2-served rate,
@@ -350,7 +508,10 @@ int check_net(const muz_net_w* w) {
 int launch_repr_conv(const muz_repr_w& r, const float* obs, int C, int n, const int* n_dev, float* conv,
                      hipStream_t s, int32_t* host_counts) {
   if (host_counts && !n_dev) return MUZ_E_INVALID;
-  k_repr_conv<<<n, 256, 0, s>>>(r, obs, C, n, n_dev, conv, host_counts);
+  if (MUZ_CONV_PAIR)
+    k_repr_conv2<<<(n + 1) / 2, kPairThreads, 0, s>>>(r, obs, C, n, n_dev, conv, host_counts);
+  else
+    k_repr_conv<<<n, 256, 0, s>>>(r, obs, C, n, n_dev, conv, host_counts);
   return muz_last_launch_error();
 }
 

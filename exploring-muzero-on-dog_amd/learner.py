@@ -470,6 +470,10 @@ def _ln_fwd(y, bias, gamma, beta, res, mode, out=None):
 # whole rows for the LayerNorm, so one CU streams the full weight matrix and carries the tile's 1024 MFMAs
 # (>= 3.4 us at 32 cycles each), where the library spreads the columns over 2-4x more CUs.
 FUSED_FWD = False
+# ... except for the narrow layers (N <= 64: the three convolutions as GEMMs over B x 56 rows, the global-feature
+# Dense_1 / Dense_2): there the whole row is 2-4 MFMA column tiles and the fused launch replaces the library GEMM +
+# muz_ln_fwd pair (MUZ_FUSED_FWD_NARROW=0: the pair, for A/B timing)
+FUSED_FWD_NARROW = os.environ.get("MUZ_FUSED_FWD_NARROW", "1") == "1"
 FUSED_BWD = True
 FUSED_DENSE = True   # False: neither (A/B timing)
 RESBLOCK_NODE = True  # False: a ResBlock as two _DenseLN nodes + autograd's residual add (A/B timing)
@@ -478,7 +482,8 @@ RESBLOCK_STACK = True  # False: consecutive ResBlocks as one node each instead o
 
 def _fusable(K, Nn, fwd=False):
     """csrc/learner_fused.hip's shapes: K <= 512 inputs, N in {32, 64, 128, 256} outputs."""
-    return FUSED_DENSE and (FUSED_FWD if fwd else FUSED_BWD) and 0 < K <= 512 and Nn in (32, 64, 128, 256)
+    on = (FUSED_FWD or (FUSED_FWD_NARROW and Nn <= 64)) if fwd else FUSED_BWD
+    return FUSED_DENSE and on and 0 < K <= 512 and Nn in (32, 64, 128, 256)
 
 
 def _ln_scratch_floats(M, Nn, K):

@@ -385,6 +385,7 @@ SIGNATURES = {
                                               ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, vp, vp]),
     "muz_im2col_bwd": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp]),
     "muz_wgrad_scratch_floats": (ctypes.c_int64, [vp, ctypes.c_int32]),
+    "muz_wgrad_segment_rows": (ctypes.c_int32, []),
     "muz_wgrad_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp, ctypes.c_int64, vp]),
     "muz_colsum_grouped": (ctypes.c_int, [vp, ctypes.c_int32, vp]),
     "muz_loss_heads": (ctypes.c_int, [vp, vp]),

@@ -774,9 +774,10 @@ typedef struct {
   float* out2;
   int32_t kind, rows, N, ld;
 } muz_colsum_problem;
-/* scratch: muz_wgrad_scratch_floats(problems, count) device floats (problems over 2048 rows are split into
- * 2048-row segments whose partials are added in segment order). */
+/* scratch: muz_wgrad_scratch_floats(problems, count) device floats (problems over muz_wgrad_segment_rows() rows
+ * are split into segments of that many rows whose partials are added in segment order). */
 int64_t muz_wgrad_scratch_floats(const muz_wgrad_problem* problems, int32_t count);
+int32_t muz_wgrad_segment_rows(void);
 int muz_wgrad_grouped(const muz_wgrad_problem* problems, int32_t count, float* scratch, int64_t scratch_floats,
                       void* stream);
 int muz_colsum_grouped(const muz_colsum_problem* problems, int32_t count, void* stream);

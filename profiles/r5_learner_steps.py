@@ -4,6 +4,8 @@ td 50.  Prints the mean step time over `steps` replays (HIP events); under rocpr
 dispatches follow the last k_ring_sample (profiles/r5_learner_trace.sh).
 
     python profiles/r5_learner_steps.py [steps] [det|dog]
+
+MUZ_DUMP=path.npz: also save the trained parameters (bit-for-bit comparisons of library builds).
 """
 import os
 import sys
@@ -47,3 +49,5 @@ e1.record()
 torch.cuda.synchronize()
 print(f"{game} train_step_from (sample into the graph inputs + graph replay): {e0.elapsed_time(e1) / steps:.3f} ms "
       f"per step over {steps} steps; loss {float(out['total_loss']):.4f}", flush=True)
+if os.environ.get("MUZ_DUMP"):
+    np.savez(os.environ["MUZ_DUMP"], **{k: np.asarray(v) for k, v in lr.nets.numpy().items()})

@@ -103,8 +103,9 @@ def test_host_rejects_bad_problems(cuda):
     L = _L()
     bad = L.MuzWgradProblem(0, 0, 0, 4, 4, 4, 4, 4)          # null pointers
     assert L.load().muz_wgrad_grouped(ctypes.byref(bad), 1, None, 0, L.stream_ptr()) != 0
-    big = L.MuzWgradProblem(1, 1, 1, 5000, 4, 4, 4, 4)        # 3 segments: needs scratch, none given
-    assert L.load().muz_wgrad_scratch_floats(ctypes.byref(big), 1) == 3 * 16
+    big = L.MuzWgradProblem(1, 1, 1, 5000, 4, 4, 4, 4)        # several segments: needs scratch, none given
+    seg = L.load().muz_wgrad_segment_rows()
+    assert seg % 64 == 0 and L.load().muz_wgrad_scratch_floats(ctypes.byref(big), 1) == -(-5000 // seg) * 16
     assert L.load().muz_wgrad_grouped(ctypes.byref(big), 1, None, 0, L.stream_ptr()) != 0
     bad = L.MuzColsumProblem(0, 0, 0, 0, 3, 4, 4, 4)         # unknown kind
     assert L.load().muz_colsum_grouped(ctypes.byref(bad), 1, L.stream_ptr()) != 0

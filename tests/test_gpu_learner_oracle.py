@@ -44,8 +44,12 @@ TAU = 1e-6     # > the fp32 forward's deviation from float64 at a decision (meas
 # profiles/r6a_parity.log): DOG prediction/Dense_5/bias 4.89x (device 2.24e-7 relative Frobenius, fp32 4.6e-8);
 # classic dynamics/discount_head/kernel 3.48x (2.44e-7 vs 7.0e-8) and /bias 3.21x (1.07e-7 vs 3.3e-8); det: none.
 FLOOR_OK = {
+    # the value head's one-element bias in every game: its relative error is that of a single float, ~1e-7 = 0.84-0.9
+    # ulp on the device since the chain's DPP row sums (det 1.00e-7, classic 1.06e-7), where the fp32 restatement
+    # happens to land within 2.4e-9 / 1.3e-8
+    "det": ("prediction/Dense_5/bias",),
     "DOG": ("prediction/Dense_5/bias",),
-    "classic": ("dynamics/discount_head/kernel", "dynamics/discount_head/bias"),
+    "classic": ("prediction/Dense_5/bias", "dynamics/discount_head/kernel", "dynamics/discount_head/bias"),
 }
 ULP_FLOOR = 4 * 2.0 ** -23   # relative Frobenius error of 4 fp32 ulps
 
