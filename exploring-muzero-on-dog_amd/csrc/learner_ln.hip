@@ -8,6 +8,8 @@
 //   z = y + bias;  Flax LayerNorm (eps 1e-6, fast variance E[z^2] - E[z]^2, as nn.hpp's ln16);
 //   o = (z - mean) * (rstd * gamma) + beta;  out = o (PLAIN) | relu(o) (RELU) | relu(res + o) (RESID_RELU).
 // Saved for the backward: z, mean, rstd and out (the ReLU mask).
+// Split-K form (muz_ln_fwd_parts): y is `parts` planes of partial products (a long-K GEMM as a batched GEMM over K
+// chunks), summed here in plane order before the bias.
 // FiLM variant (the first op of a dynamics trunk, muzero_deterministic_madn.py:421-427: LayerNorm_0 of the latent,
 // then x * (1 + scale) + shift): PLAIN LayerNorm without a bias, plus film = shift + out * scale1 (scale1 = 1 + scale);
 // its backward takes d(film) and writes dscale = d(film) * out beside the LayerNorm backward of d(film) * scale1
@@ -38,7 +40,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ y, con
                                                 float* __restrict__ z, float* __restrict__ mean_out,
                                                 float* __restrict__ rstd_out, const float* __restrict__ scale1 = nullptr,
                                                 const float* __restrict__ shift = nullptr,
-                                                float* __restrict__ film = nullptr) {
+                                                float* __restrict__ film = nullptr, int parts = 1) {
   // no fma contraction: the row kernels and their fused boundary forms round identically
 #pragma clang fp contract(off)
   constexpr int E = (N + 63) / 64;
@@ -51,7 +53,21 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ y, con
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const int c = lane + 64 * i;
-    v[i] = c < N ? (FILM ? y[row + c] : y[row + c] + bias[c]) : 0.f;
+    float yc = 0.f;
+    if (c < N) {
+      yc = y[row + c];
+      if (!FILM && parts > 1) {   // plane order; the loads issued before the adds
+        float pv[16];
+        for (int q0 = 1; q0 < parts; q0 += 16) {
+#pragma unroll
+          for (int u = 0; u < 16; ++u) pv[u] = q0 + u < parts ? y[(size_t)(q0 + u) * M * N + row + c] : 0.f;
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (q0 + u < parts) yc = yc + pv[u];
+        }
+      }
+    }
+    v[i] = c < N ? (FILM ? yc : yc + bias[c]) : 0.f;
     s += v[i];
     s2 += v[i] * v[i];
   }
@@ -472,15 +488,18 @@ using namespace muz;
 
 extern "C" {
 
-int muz_ln_fwd(const float* y, const float* bias, const float* gamma, const float* beta, const float* res, int32_t M,
-               int32_t N, int32_t mode, float* out, float* z, float* mean, float* rstd, void* stream) {
+int muz_ln_fwd_parts(const float* y, int32_t parts, const float* bias, const float* gamma, const float* beta,
+                     const float* res, int32_t M, int32_t N, int32_t mode, float* out, float* z, float* mean, float* rstd,
+                     void* stream) {
   if (!ln_width_ok(N) || mode < 0 || mode > 2) return MUZ_E_UNSUPPORTED;
-  MUZ_HOST_CHECK(M >= 0 && y && bias && gamma && beta && out && z && mean && rstd);
+  MUZ_HOST_CHECK(M >= 0 && parts >= 1 && y && bias && gamma && beta && out && z && mean && rstd);
   MUZ_HOST_CHECK((mode == LN_MODE_RESID_RELU) == (res != nullptr));
   if (M == 0) return MUZ_OK;
   hipStream_t s = (hipStream_t)stream;
   const int grid = (M + 3) / 4;
-#define MUZ_LN_FWD(n) k_ln_fwd<n><<<grid, 256, 0, s>>>(y, bias, gamma, beta, res, M, mode, out, z, mean, rstd)
+#define MUZ_LN_FWD(n)                                                                                          \
+  k_ln_fwd<n><<<grid, 256, 0, s>>>(y, bias, gamma, beta, res, M, mode, out, z, mean, rstd, nullptr, nullptr, \
+                                   nullptr, parts)
   switch (N) {
     case 32: MUZ_LN_FWD(32); break;
     case 64: MUZ_LN_FWD(64); break;
@@ -489,6 +508,11 @@ int muz_ln_fwd(const float* y, const float* bias, const float* gamma, const floa
   }
 #undef MUZ_LN_FWD
   return muz_last_launch_error();
+}
+
+int muz_ln_fwd(const float* y, const float* bias, const float* gamma, const float* beta, const float* res, int32_t M,
+               int32_t N, int32_t mode, float* out, float* z, float* mean, float* rstd, void* stream) {
+  return muz_ln_fwd_parts(y, 1, bias, gamma, beta, res, M, N, mode, out, z, mean, rstd, stream);
 }
 
 int64_t muz_ln_bwd_scratch_floats(int32_t M, int32_t N) {

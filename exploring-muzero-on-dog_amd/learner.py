@@ -450,16 +450,34 @@ class _Im2col(torch.autograd.Function):
         return dx, None
 
 
-def _ln_fwd(y, bias, gamma, beta, res, mode, out=None):
+# A long-K layer on few rows (the representation's Dense_0: K = 3584, N = 256, batch 128 rows) gets one library tile
+# per 32 x 32 outputs and runs its whole K serially (20 us for 0.24 GFLOP, profiles/r6q_learner_step_sequence_det.txt);
+# MUZ_SPLITK_DENSE=1 runs it as a batched GEMM over K chunks of 256 whose partial planes the LayerNorm launch sums in
+# chunk order (muz_ln_fwd_parts).  Off by default: deterministic (profiles/r6t_diag_splitk.log) and 10 us faster per
+# step (profiles/r6r_steps.log), but its different rounding (8.9e-7 relative against the single GEMM) moved one
+# classic-learner row's fp32 forward past the tests' decision margin TAU = 1e-6 (the fused and per-layer paths then
+# route that row's min-max / ReLU gradient differently: 4.9e-5 on every dynamics tensor,
+# test_fused_kernels_match_per_layer_path_end_to_end[classic], profiles/r6s_per_layer_sk1.log).
+SPLITK_DENSE = os.environ.get("MUZ_SPLITK_DENSE", "0") == "1"
+
+
+def _splitk_parts(M, K):
+    if not SPLITK_DENSE or K < 1024 or M > 1024:
+        return 1
+    return next((S for S in (14, 16, 12, 8) if K % S == 0 and K // S >= 128), 1)
+
+
+def _ln_fwd(y, bias, gamma, beta, res, mode, out=None, parts=1):
     """Fused bias + LayerNorm (+ ReLU / residual ReLU) forward: -> (out, z, mean, rstd) (no autograd).
     `out`: a preallocated contiguous [M, N] destination (a row block of a stacked buffer)."""
-    M, Nn = y.shape
-    out = torch.empty_like(y) if out is None else out
-    z = torch.empty_like(y)
+    M, Nn = y.shape[-2:]
+    out = torch.empty((M, Nn), dtype=y.dtype, device=y.device) if out is None else out
+    z = torch.empty((M, Nn), dtype=y.dtype, device=y.device)
     mean = torch.empty((M,), dtype=y.dtype, device=y.device)
     rstd = torch.empty_like(mean)
-    _L.check(_L.load().muz_ln_fwd(_L.ptr(y), _L.ptr(bias), _L.ptr(gamma), _L.ptr(beta), _L.ptr(res), M, Nn, mode,
-                                  _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.stream_ptr()), "muz_ln_fwd")
+    _L.check(_L.load().muz_ln_fwd_parts(_L.ptr(y), parts, _L.ptr(bias), _L.ptr(gamma), _L.ptr(beta), _L.ptr(res), M,
+                                        Nn, mode, _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.stream_ptr()),
+             "muz_ln_fwd_parts")
     return out, z, mean, rstd
 
 
@@ -541,6 +559,10 @@ def _dense_ln_fwd(x, W, bias, gamma, beta, res, mode, out=None):
     M, K = x.shape
     Nn = W.shape[1]
     if not _fusable(K, Nn, fwd=True):
+        S = _splitk_parts(M, K) if x.is_contiguous() and W.is_contiguous() else 1
+        if S > 1:   # [S][M][N] partial planes: x's K chunks times W's row chunks
+            y = torch.bmm(x.view(M, S, K // S).transpose(0, 1), W.view(S, K // S, Nn))
+            return _ln_fwd(y, bias, gamma, beta, res, mode, out=out, parts=S)
         return _ln_fwd(x @ W, bias, gamma, beta, res, mode, out=out)
     x, W = x.contiguous(), W.contiguous()
     wt = _WT.get(W) if _WT is not None else None

@@ -359,6 +359,8 @@ SIGNATURES = {
                                             ctypes.c_int64, ctypes.POINTER(MuzSpStats), vp]),
     "muz_ln_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp,
                                   vp]),
+    "muz_ln_fwd_parts": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_int32, vp, vp, vp, vp, vp]),
     "muz_ln_bwd_scratch_floats": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     "muz_ln_bwd_rows": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                        vp, vp]),

@@ -692,6 +692,11 @@ int muz_ring_save_packed(muz_ring ring, muz_traj packed, const muz_traj_chance* 
  * mode 2, and dres for its backward).  z, mean, rstd, out are the forward's saved values. */
 int muz_ln_fwd(const float* y, const float* bias, const float* gamma, const float* beta, const float* res, int32_t M,
                int32_t N, int32_t mode, float* out, float* z, float* mean, float* rstd, void* stream);
+/* muz_ln_fwd of y = the sum of `parts` [M][N] planes (consecutive in y), added in plane order: the epilogue of a
+ * long-K GEMM run as a batched GEMM over K chunks (the learner's representation Dense_0, K = 3584). */
+int muz_ln_fwd_parts(const float* y, int32_t parts, const float* bias, const float* gamma, const float* beta,
+                     const float* res, int32_t M, int32_t N, int32_t mode, float* out, float* z, float* mean, float* rstd,
+                     void* stream);
 /* device float scratch muz_ln_bwd needs for M rows of width N (-1 for an unsupported N). */
 int64_t muz_ln_bwd_scratch_floats(int32_t M, int32_t N);
 /* The backward's two halves: muz_ln_bwd_rows writes dz (and dres) and the per-block column partials into
