@@ -723,7 +723,7 @@ def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, 
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(steps["n"]):
-                learner.train_step_from(ring)
+                learner.train_step_from(ring, losses=False)
             e1.record()
             e1.synchronize()
             stats["learner_ms"] += e0.elapsed_time(e1)
@@ -758,7 +758,7 @@ def _train_overlapped(args, rank, world, dist, device, eng, ring, learner, net, 
         # capture the learner's HIP graph before any iteration runs self-play in another thread (a capture
         # must not see the other thread's synchronising HIP calls)
         with torch.cuda.stream(s_learn):
-            learner.train_step_from(ring)
+            learner.train_step_from(ring, losses=False)
         s_learn.synchronize()
     for w in range(max(args.warmup, 1)):
         loop.step()
@@ -840,7 +840,7 @@ def run_train(args):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(train_steps):
-                learner.train_step_from(ring)
+                learner.train_step_from(ring, losses=False)
             e1.record()
             e1.synchronize()
             stats["learner_ms"] += e0.elapsed_time(e1)

@@ -138,8 +138,9 @@ struct Ring {
 };
 
 // muz_trunk_chain_pack: one thread per packed float4 of one matrix and direction
+constexpr int kPackMax = 32;   // matrices per launch: the det step's chain (7) + ResBlock stacks (12 + 4) in one
 struct PackTable {
-  const float* src[16];
+  const float* src[kPackMax];
   int count;
 };
 
@@ -872,9 +873,9 @@ extern "C" {
 
 int muz_trunk_chain_pack(const float* const* W, int32_t count, float* fwd, float* bwd, void* stream) {
   MUZ_HOST_CHECK(count >= 0 && (count == 0 || (W && fwd && bwd)));
-  for (int s0 = 0; s0 < count; s0 += 16) {
+  for (int s0 = 0; s0 < count; s0 += chain::kPackMax) {
     chain::PackTable tb{};
-    tb.count = count - s0 < 16 ? count - s0 : 16;
+    tb.count = count - s0 < chain::kPackMax ? count - s0 : chain::kPackMax;
     for (int i = 0; i < tb.count; ++i) {
       MUZ_HOST_CHECK(W[s0 + i] != nullptr);
       tb.src[i] = W[s0 + i];

@@ -467,6 +467,17 @@ def _splitk_parts(M, K):
     return next((S for S in (14, 16, 12, 8) if K % S == 0 and K // S >= 128), 1)
 
 
+def _loss_row(vals):
+    """[total, part_1, ...] as one [n] tensor: a view of the fused loss kernel's parts row when vals[1:] are its
+    consecutive entries 1.. (its entry 0 holds the total), else a stack."""
+    p1 = vals[1] if len(vals) > 1 else None
+    if p1 is not None and all(v.dim() == 0 and v.dtype == p1.dtype for v in vals) and p1.storage_offset() >= 1 and \
+            all(vals[i].untyped_storage().data_ptr() == p1.untyped_storage().data_ptr() and
+                vals[i].storage_offset() == p1.storage_offset() + i - 1 for i in range(1, len(vals))):
+        return p1.as_strided((len(vals),), (1,), p1.storage_offset() - 1)
+    return torch.stack(vals)
+
+
 def _ln_fwd(y, bias, gamma, beta, res, mode, out=None, parts=1):
     """Fused bias + LayerNorm (+ ReLU / residual ReLU) forward: -> (out, z, mean, rstd) (no autograd).
     `out`: a preallocated contiguous [M, N] destination (a row block of a stacked buffer)."""
@@ -1747,22 +1758,30 @@ class Learner:
             self._g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g):
                 self._out = self._step(self._static)
-                # the losses packed into one buffer inside the graph, so a replay hands them out with one copy
-                self._packed = torch.stack(list(self._out.values()))
+                # the losses packed into one buffer inside the graph, so a replay hands them out with one copy: the
+                # fused loss kernel's own [total, parts...] row when the outputs are its consecutive entries
+                # (muz_loss_args: parts[0] = total), else one stack launch
+                self._packed = _loss_row(list(self._out.values()))
         for k in self.KEYS:
             self._static[k].copy_(batch[k])
         self._g.replay()
         return self._outputs()
 
-    def _outputs(self) -> dict:
+    def _outputs(self, losses: bool = True):
+        if not losses:
+            return None
+        return self._outputs_copy()
+
+    def _outputs_copy(self) -> dict:
         """The captured losses are overwritten by the next replay: one copy of the packed buffer, handed out as
         per-key views so a caller may keep them."""
         c = self._packed.clone()
         return {k: c[i] for i, k in enumerate(self._out)}
 
-    def train_step_from(self, ring) -> dict:
+    def train_step_from(self, ring, losses: bool = True):
         """train_step on the next batch of a device ring (``ring.sample_batch()``).  Once the step is captured,
-        the ring writes the batch straight into the graph's static inputs (no per-key copy)."""
+        the ring writes the batch straight into the graph's static inputs (no per-key copy).  losses=False: a
+        captured step hands out nothing (no copy of the loss row; a loop that does not log every step)."""
         if self.graph and self._g is not None:
             ep, t = ring.draw_indices()
             if not getattr(self, "_static_full", False):    # the batch fields the step does not read
@@ -1773,7 +1792,7 @@ class Learner:
                 self._static_full = True
             ring.sample_at(ep, t, out=self._static)
             self._g.replay()
-            return self._outputs()
+            return self._outputs(losses)
         return self.train_step(ring.sample_batch())
 
     def push_to(self, net: "N.DeviceNet"):

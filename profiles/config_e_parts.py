@@ -88,12 +88,12 @@ def main(games):
             del buf, packed, play
             torch.cuda.empty_cache()
         for _ in range(20):
-            learner.train_step_from(ring)
+            learner.train_step_from(ring, losses=False)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(300):
-            learner.train_step_from(ring)
+            learner.train_step_from(ring, losses=False)
         e1.record()
         e1.synchronize()
         step_ms = e0.elapsed_time(e1) / 300

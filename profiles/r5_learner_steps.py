@@ -41,13 +41,16 @@ else:
 for _ in range(3):
     lr.train_step_from(ring)
 torch.cuda.synchronize()
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(steps):
-    out = lr.train_step_from(ring)
-e1.record()
-torch.cuda.synchronize()
-print(f"{game} train_step_from (sample into the graph inputs + graph replay): {e0.elapsed_time(e1) / steps:.3f} ms "
-      f"per step over {steps} steps; loss {float(out['total_loss']):.4f}", flush=True)
+for losses in (True, False):   # with the per-step copy of the loss row (a logging loop) / without (the bench's loop)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        out = lr.train_step_from(ring, losses=losses)
+    e1.record()
+    torch.cuda.synchronize()
+    tag = "" if losses else ", no loss handout"
+    last = f"; loss {float(out['total_loss']):.4f}" if losses else ""
+    print(f"{game} train_step_from (sample into the graph inputs + graph replay{tag}): "
+          f"{e0.elapsed_time(e1) / steps:.3f} ms per step over {steps} steps{last}", flush=True)
 if os.environ.get("MUZ_DUMP"):
     np.savez(os.environ["MUZ_DUMP"], **{k: np.asarray(v) for k, v in lr.nets.numpy().items()})
