@@ -233,7 +233,7 @@ __global__ __launch_bounds__(2 * N) void k_dense_ln_bwd(const float* __restrict_
                                                         const float* __restrict__ W, int K,
                                                         const float* __restrict__ acc_in, float* __restrict__ dz,
                                                         float* __restrict__ dres, float* __restrict__ dx,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, int ldd) {
   constexpr int NW = N / 32, NTH = 64 * NW, TPR = NTH / kFRows;
   constexpr int LDZ = N + 4;
   __shared__ float dzs[kFRows][LDZ];
@@ -261,8 +261,9 @@ __global__ __launch_bounds__(2 * N) void k_dense_ln_bwd(const float* __restrict_
     const size_t o = (size_t)m * N + c0;
     const float mean = mean_in[m], rstd = rstd_in[m];
     float ov[8], zv[8];
-    *reinterpret_cast<f32x4_u*>(d) = *reinterpret_cast<const f32x4_u*>(dout + o);
-    *reinterpret_cast<f32x4_u*>(d + 4) = *reinterpret_cast<const f32x4_u*>(dout + o + 4);
+    const float* dr = dout + (size_t)m * ldd + c0;   // (rows ldd apart: a column slice of a wider gradient)
+    *reinterpret_cast<f32x4_u*>(d) = *reinterpret_cast<const f32x4_u*>(dr);
+    *reinterpret_cast<f32x4_u*>(d + 4) = *reinterpret_cast<const f32x4_u*>(dr + 4);
     *reinterpret_cast<f32x4_u*>(ov) = *reinterpret_cast<const f32x4_u*>(out + o);
     *reinterpret_cast<f32x4_u*>(ov + 4) = *reinterpret_cast<const f32x4_u*>(out + o + 4);
     *reinterpret_cast<f32x4_u*>(zv) = *reinterpret_cast<const f32x4_u*>(z + o);
@@ -418,11 +419,12 @@ int64_t muz_dense_ln_bwd_scratch_floats(int32_t M, int32_t N) {
   return (int64_t)((M + kFRows - 1) / kFRows) * 3 * N;
 }
 
-int muz_dense_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
-                     const float* gamma, int32_t M, int32_t N, int32_t mode, const float* W, int32_t K,
-                     const float* acc, float* dz, float* dres, float* dx, float* scratch, void* stream) {
+int muz_dense_ln_bwd_ld(const float* dout, int32_t ldd, const float* out, const float* z, const float* mean,
+                        const float* rstd, const float* gamma, int32_t M, int32_t N, int32_t mode, const float* W,
+                        int32_t K, const float* acc, float* dz, float* dres, float* dx, float* scratch, void* stream) {
   if (!fused_width_ok(N) || mode < 0 || mode > 2) return MUZ_E_UNSUPPORTED;
   MUZ_HOST_CHECK(M >= 0 && dout && out && z && mean && rstd && gamma && dz && scratch);
+  MUZ_HOST_CHECK(ldd >= N && ldd % 4 == 0 && ((uintptr_t)dout & 15u) == 0);   // (16-byte row loads)
   MUZ_HOST_CHECK((mode == FLN_RESID_RELU) == (dres != nullptr));
   MUZ_HOST_CHECK(!dx || (W && K > 0));
   MUZ_HOST_CHECK(!acc || dx);
@@ -431,7 +433,8 @@ int muz_dense_ln_bwd(const float* dout, const float* out, const float* z, const 
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((M + kFRows - 1) / kFRows, kblocks);
 #define MUZ_DLB(n) \
-  k_dense_ln_bwd<n><<<grid, 2 * n, 0, s>>>(dout, out, z, mean, rstd, gamma, M, mode, W, K, acc, dz, dres, dx, scratch)
+  k_dense_ln_bwd<n><<<grid, 2 * n, 0, s>>>(dout, out, z, mean, rstd, gamma, M, mode, W, K, acc, dz, dres, dx, scratch, \
+                                           ldd)
   switch (N) {
     case 32: MUZ_DLB(32); break;
     case 64: MUZ_DLB(64); break;
@@ -440,6 +443,12 @@ int muz_dense_ln_bwd(const float* dout, const float* out, const float* z, const 
   }
 #undef MUZ_DLB
   return muz_last_launch_error();
+}
+
+int muz_dense_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
+                     const float* gamma, int32_t M, int32_t N, int32_t mode, const float* W, int32_t K,
+                     const float* acc, float* dz, float* dres, float* dx, float* scratch, void* stream) {
+  return muz_dense_ln_bwd_ld(dout, N, out, z, mean, rstd, gamma, M, N, mode, W, K, acc, dz, dres, dx, scratch, stream);
 }
 
 }  // extern "C"

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dout, 
                                                 const float* __restrict__ rstd_in, const float* __restrict__ gamma,
                                                 int M, int mode, float* __restrict__ dz, float* __restrict__ dres,
                                                 float* __restrict__ part, const float* __restrict__ scale1 = nullptr,
-                                                float* __restrict__ dscale = nullptr) {
+                                                float* __restrict__ dscale = nullptr, int ldd = N) {
   // no fma contraction: the row kernels and their fused boundary forms round identically
 #pragma clang fp contract(off)
   constexpr int E = (N + 63) / 64;
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dout, 
       const int c = lane + 64 * i;
       d[i] = xh[i] = g[i] = 0.f;
       if (c >= N) continue;
-      float t = dout[row + c];
+      float t = dout[(size_t)m * ldd + c];   // (dout rows ldd apart: a column slice of a wider gradient)
       if constexpr (FILM) {
         dscale[row + c] = t * out[row + c];
         t = t * scale1[row + c];
@@ -520,16 +520,18 @@ int64_t muz_ln_bwd_scratch_floats(int32_t M, int32_t N) {
   return (int64_t)((M + kLnRowsPerBlock - 1) / kLnRowsPerBlock) * 3 * N;
 }
 
-int muz_ln_bwd_rows(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
-                    const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
-                    void* stream) {
+int muz_ln_bwd_rows_ld(const float* dout, int32_t ldd, const float* out, const float* z, const float* mean,
+                       const float* rstd, const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres,
+                       float* scratch, void* stream) {
   if (!ln_width_ok(N) || mode < 0 || mode > 2) return MUZ_E_UNSUPPORTED;
-  MUZ_HOST_CHECK(M >= 0 && dout && out && z && mean && rstd && gamma && dz && scratch);
+  MUZ_HOST_CHECK(M >= 0 && ldd >= N && dout && out && z && mean && rstd && gamma && dz && scratch);
   MUZ_HOST_CHECK((mode == LN_MODE_RESID_RELU) == (dres != nullptr));
   hipStream_t s = (hipStream_t)stream;
   const int nblk = (M + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
   if (M > 0) {
-#define MUZ_LN_BWD(n) k_ln_bwd<n><<<nblk, 256, 0, s>>>(dout, out, z, mean, rstd, gamma, M, mode, dz, dres, scratch)
+#define MUZ_LN_BWD(n)                                                                                        \
+  k_ln_bwd<n><<<nblk, 256, 0, s>>>(dout, out, z, mean, rstd, gamma, M, mode, dz, dres, scratch, nullptr, nullptr, \
+                                   ldd)
     switch (N) {
       case 32: MUZ_LN_BWD(32); break;
       case 64: MUZ_LN_BWD(64); break;
@@ -540,6 +542,12 @@ int muz_ln_bwd_rows(const float* dout, const float* out, const float* z, const f
     return muz_last_launch_error();
   }
   return MUZ_OK;
+}
+
+int muz_ln_bwd_rows(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
+                    const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
+                    void* stream) {
+  return muz_ln_bwd_rows_ld(dout, N, out, z, mean, rstd, gamma, M, N, mode, dz, dres, scratch, stream);
 }
 
 int muz_ln_colsum(const float* scratch, int64_t nblk, int32_t N, float* dgamma, float* dbeta, float* dbias,

@@ -588,6 +588,17 @@ def _dense_ln_fwd(x, W, bias, gamma, beta, res, mode, out=None):
     return out, z, mean, rstd
 
 
+def _rows_view(t, align):
+    """(t, its row stride) when t is a 2-D row-major view with unit column stride whose rows the backward kernels
+    can read in place (a column slice of a concatenation's gradient: no copy), else (a contiguous copy, its width).
+    align: the row stride multiple (and 4 x align-byte base alignment) the kernel's row loads need."""
+    if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1] and t.stride(0) % align == 0 and \
+            t.data_ptr() % (4 * align) == 0:
+        return t, t.stride(0)
+    t = t.contiguous()
+    return t, t.shape[1]
+
+
 def _dense_ln_bwd(dout, fwd, gamma, mode, W, scratch, dz=None, acc=None, dx_out=None, need_dx=True):
     """Backward of _dense_ln_fwd up to the layer input: -> (dz, dres or None, dx = dz @ W^T (+ acc) or None);
     column partials into scratch (_ln_scratch_floats).  One launch (muz_dense_ln_bwd) where fusable."""
@@ -601,15 +612,16 @@ def _dense_ln_bwd(dout, fwd, gamma, mode, W, scratch, dz=None, acc=None, dx_out=
         if acc is None:
             return dz, dres, torch.mm(dz, W.t(), out=dx_out) if dx_out is not None else dz @ W.t()
         return dz, dres, torch.addmm(acc, dz, W.t(), out=dx_out) if dx_out is not None else torch.addmm(acc, dz, W.t())
-    dout, W = dout.contiguous(), W.contiguous()
+    dout, ldd = _rows_view(dout, 4)
+    W = W.contiguous()
     dz = torch.empty_like(out) if dz is None else dz
     dres = torch.empty_like(out) if mode == LN_RESID_RELU else None
     dx = None
     if need_dx:
         dx = torch.empty((M, K), dtype=out.dtype, device=out.device) if dx_out is None else dx_out
-    _L.check(_L.load().muz_dense_ln_bwd(_L.ptr(dout), *(_L.ptr(t) for t in fwd), _L.ptr(gamma), M, Nn, mode, _L.ptr(W),
-                                        K, _L.ptr(acc), _L.ptr(dz), _L.ptr(dres), _L.ptr(dx), _L.ptr(scratch),
-                                        _L.stream_ptr()), "muz_dense_ln_bwd")
+    _L.check(_L.load().muz_dense_ln_bwd_ld(_L.ptr(dout), ldd, *(_L.ptr(t) for t in fwd), _L.ptr(gamma), M, Nn, mode,
+                                           _L.ptr(W), K, _L.ptr(acc), _L.ptr(dz), _L.ptr(dres), _L.ptr(dx),
+                                           _L.ptr(scratch), _L.stream_ptr()), "muz_dense_ln_bwd_ld")
     return dz, dres, dx
 
 
@@ -618,12 +630,12 @@ def _ln_bwd_rows(dout, fwd, gamma, mode, scratch, dz=None):
     preallocated contiguous destination."""
     out, z, mean, rstd = fwd
     M, Nn = out.shape
-    dout = dout.contiguous()
+    dout, ldd = _rows_view(dout, 1)
     dz = torch.empty_like(out) if dz is None else dz
     dres = torch.empty_like(out) if mode == LN_RESID_RELU else None
-    _L.check(_L.load().muz_ln_bwd_rows(_L.ptr(dout), _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd), _L.ptr(gamma),
-                                       M, Nn, mode, _L.ptr(dz), _L.ptr(dres), _L.ptr(scratch), _L.stream_ptr()),
-             "muz_ln_bwd_rows")
+    _L.check(_L.load().muz_ln_bwd_rows_ld(_L.ptr(dout), ldd, _L.ptr(out), _L.ptr(z), _L.ptr(mean), _L.ptr(rstd),
+                                          _L.ptr(gamma), M, Nn, mode, _L.ptr(dz), _L.ptr(dres), _L.ptr(scratch),
+                                          _L.stream_ptr()), "muz_ln_bwd_rows_ld")
     return dz, dres
 
 

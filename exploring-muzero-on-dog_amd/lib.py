@@ -364,6 +364,8 @@ SIGNATURES = {
     "muz_ln_bwd_scratch_floats": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     "muz_ln_bwd_rows": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                        vp, vp]),
+    "muz_ln_bwd_rows_ld": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int32, vp, vp, vp, vp]),
     "muz_ln_colsum": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp, vp]),
     "muz_ln_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
                                   vp, vp, vp, vp]),
@@ -399,6 +401,8 @@ SIGNATURES = {
     "muz_dense_ln_bwd_scratch_floats": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     "muz_dense_ln_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp,
                                         ctypes.c_int32, vp, vp, vp, vp, vp, vp]),
+    "muz_dense_ln_bwd_ld": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_int32, vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp]),
     "muz_trunk_chain_pack": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp]),
     "muz_trunk_chain_fwd": (ctypes.c_int, [ctypes.POINTER(MuzChainArgs), vp]),
     "muz_rbstack_fwd": (ctypes.c_int, [ctypes.POINTER(MuzRbstackArgs), vp]),

@@ -705,6 +705,11 @@ int64_t muz_ln_bwd_scratch_floats(int32_t M, int32_t N);
 int muz_ln_bwd_rows(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
                     const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres, float* scratch,
                     void* stream);
+/* muz_ln_bwd_rows with dout's rows ldd >= N floats apart (a column slice of a wider gradient, e.g. of a
+ * concatenation's input: no copy to a contiguous block). */
+int muz_ln_bwd_rows_ld(const float* dout, int32_t ldd, const float* out, const float* z, const float* mean,
+                       const float* rstd, const float* gamma, int32_t M, int32_t N, int32_t mode, float* dz, float* dres,
+                       float* scratch, void* stream);
 int muz_ln_colsum(const float* scratch, int64_t nblk, int32_t N, float* dgamma, float* dbeta, float* dbias,
                   void* stream);
 /* dz = d(y) (= the GEMM output's gradient); dgamma / dbeta / dbias: column sums (deterministic order). */
@@ -867,6 +872,10 @@ int64_t muz_dense_ln_bwd_scratch_floats(int32_t M, int32_t N);
 int muz_dense_ln_bwd(const float* dout, const float* out, const float* z, const float* mean, const float* rstd,
                      const float* gamma, int32_t M, int32_t N, int32_t mode, const float* W, int32_t K,
                      const float* acc, float* dz, float* dres, float* dx, float* scratch, void* stream);
+/* muz_dense_ln_bwd with dout's rows ldd floats apart (ldd >= N, a multiple of 4; dout 16-byte aligned). */
+int muz_dense_ln_bwd_ld(const float* dout, int32_t ldd, const float* out, const float* z, const float* mean,
+                        const float* rstd, const float* gamma, int32_t M, int32_t N, int32_t mode, const float* W,
+                        int32_t K, const float* acc, float* dz, float* dres, float* dx, float* scratch, void* stream);
 /* The unrolled dynamics chain of a learner step as ONE launch each way (csrc/learner_chain.hip; replaces
  * learner._TrunkChain's per-layer launch train of library GEMMs and row kernels; reference:
  * train_with_reward.py:98-107 (one trunk, K applications), train_stochastic.py:95-121 (act / chance trunks
