@@ -151,7 +151,8 @@ __global__ __launch_bounds__(256) void k_repr_conv(muz_repr_w Rarg, const float*
 // k_repr_conv's.  With 8 waves, waves w and w + 4 own the same 16 output channels, w tiles 0-3 and w + 4 tiles 4-6
 // (one SIMD carries both: the same MFMAs per SIMD, twice the waves to hide the row phases' latency).
 #ifndef MUZ_CONV_PAIR
-#define MUZ_CONV_PAIR 1   // root conv kernel traces, profiles/r6p_root_*: one game 146.8 us, pairs on 4 waves 141.4, on 8 142.2
+#define MUZ_CONV_PAIR 3   // root conv kernel traces, profiles/r6p_root_*: one game 146.8 us, pairs on 4 waves 141.4, on 8 142.2;
+                          // r6z_root_kernel_stats_*: pairs on 4 waves 139.0, register-resident LayerNorms (3) 125.9
 #endif
 constexpr int kPairThreads = MUZ_CONV_PAIR == 2 ? 512 : 256;
 constexpr int kPairRows = 112, kPairTiles = 7;
@@ -300,6 +301,190 @@ __global__ __launch_bounds__(kPairThreads) void k_repr_conv2(muz_repr_w Rarg, co
     const int gm = i >= kConvMapFloats ? 1 : 0;
     convout[(size_t)(g0 + gm) * kConvRowFloats + i - gm * kConvMapFloats] = c2in[i];
   }
+}
+
+// MUZ_CONV_PAIR 3: the pair kernel with Conv_1 / Conv_2's outputs kept in the MFMA accumulators.  Their LayerNorms
+// run from registers: each wave sums its 16 channels of a position (4 values per lane, then the permlane swaps across
+// the 4 lane groups), the 4 waves' partials meet in a 3.5 KB LDS table, and every lane normalises its own values and
+// stores them -- into Conv_2's input rows, or (Conv_2) straight into the flattened maps in HBM.  No [112][68]
+// pre-activation buffer and one LDS round trip less per convolution: 39 KB of LDS, so 4 pairs (8 games) per CU
+// instead of 2.  The LayerNorm sums run in another order than ln_pair's (same formula and eps): not bit-identical to
+// k_repr_conv / k_repr_conv2 (the root tests bound it; the search and self-play parity tests give the oracle the
+// GPU's own root outputs).
+constexpr int kC1Ld3 = 36, kC2Ld3 = 68, kP0Ld = 36;   // +4-float row pads: the 16-row fragments hit distinct banks
+constexpr int kIn0F = 704, kPre0At = kIn0F, kC1At = kPre0At + kPairRows * kP0Ld, kStatAt = kC1At + 2 * kG1 * kC1Ld3;
+constexpr int kConv3Floats = kStatAt + kPairRows * 8;
+static_assert(2 * kG0 * 6 <= kIn0F && 2 * kG2 * kC2Ld3 <= kStatAt && kConv3Floats * 4 <= 40 * 1024, "conv3 LDS carve");
+
+// LayerNorm over the 32 channels of 112 positions read from pre0 (4 lanes per position, 2 passes of 64)
+template <int N, int LDI, int LDO, int GR, int PAD>
+__device__ __forceinline__ void ln_pair_ld(const float* pre, float* out, const AS4 muz_ln& P) {
+  const int q = threadIdx.x & 3;
+  constexpr int PER = N / 4;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int pos = (threadIdx.x >> 2) + 64 * pass;
+    if (pos >= kPairRows) break;
+    float v[PER], s = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      v[i] = pre[pos * LDI + q + 4 * i];
+      s += v[i];
+      s2 = fmaf(v[i], v[i], s2);
+    }
+    s += dpp<DPP_XOR1>(s);
+    s += dpp<DPP_XOR2>(s);
+    s2 += dpp<DPP_XOR1>(s2);
+    s2 += dpp<DPP_XOR2>(s2);
+    const float mean = s / (float)N, mean2 = s2 / (float)N;
+    const float inv = ln_rstd(fmaxf(0.f, fmaf(-mean, mean, mean2)) + 1e-6f);
+    const int gm = pos >= 56 ? 1 : 0, orow = gm * GR + PAD + pos - 56 * gm;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = q + 4 * i;
+      out[orow * LDO + c] = fmaxf(fmaf(v[i] - mean, inv * gp(P.scale)[c], gp(P.bias)[c]), 0.f);
+    }
+  }
+}
+
+// one convolution of the pair into the accumulators (+ bias): lane (r, g) of wave wv holds channels 16 wv + 4 g .. + 3
+// of positions 16 t + r, t < 7; then the per-wave (sum, sum of squares) of each position into st[pos][wv]
+template <int KB, int CIN, int LDI, int GR>
+__device__ __forceinline__ void conv_acc_pair(const AS4 muz_dense& L, const float* in, f32x4 (&acc)[kPairTiles],
+                                              float* st) {
+  static_assert(CIN % 16 == 0, "a k-block within one tap");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const AS1 f32x4* wp = gp(reinterpret_cast<const f32x4*>(L.w)) + (size_t)wv * KB * 64 + lane;
+  int roff[kPairTiles];
+#pragma unroll
+  for (int t = 0; t < kPairTiles; ++t) {
+    const int R = t * 16 + r, gm = R >= 56 ? 1 : 0;
+    roff[t] = (gm * GR + R - 56 * gm) * LDI + 4 * g;
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  f32x4 w0 = wp[0], w1 = KB > 1 ? wp[64] : w0, w2;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    if (kb + 2 < KB) w2 = wp[(kb + 2) * 64];
+    f32x4 a[kPairTiles];
+#pragma unroll
+    for (int t = 0; t < kPairTiles; ++t)
+      a[t] = *reinterpret_cast<const f32x4*>(in + roff[t] + ((kb * 16) / CIN) * LDI + (kb * 16) % CIN);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < kPairTiles; ++t) acc[t] = mfma4(w0[j], a[t][j], acc[t]);
+    w0 = w1;
+    w1 = w2;
+  }
+  const f32x4 bb = gp(reinterpret_cast<const f32x4*>(L.b))[(16 * wv + 4 * g) >> 2];
+#pragma unroll
+  for (int t = 0; t < kPairTiles; ++t) {
+    acc[t] += bb;
+    float s = (acc[t][0] + acc[t][1]) + (acc[t][2] + acc[t][3]);
+    float s2 = fmaf(acc[t][3], acc[t][3], fmaf(acc[t][2], acc[t][2], fmaf(acc[t][1], acc[t][1], acc[t][0] * acc[t][0])));
+    LoHi<float> p = swap16(s);     // lane groups g, g ^ 1
+    s = p.lo + p.hi;
+    p = swap16(s2);
+    s2 = p.lo + p.hi;
+    p = swap32(s);                 // g < 2 with g >= 2
+    s = p.lo + p.hi;
+    p = swap32(s2);
+    s2 = p.lo + p.hi;
+    if (g == 0) *reinterpret_cast<float2*>(st + (t * 16 + r) * 8 + 2 * wv) = make_float2(s, s2);
+  }
+}
+
+// the LayerNorm of the accumulators (after a barrier has published st): mean / rstd from the 4 waves' partials
+// (in wave order), then relu(LN) of the lane's 4 channels of each position, handed to out(pos, channel0, value4)
+template <class F>
+__device__ __forceinline__ void ln_acc_pair(const f32x4 (&acc)[kPairTiles], const float* st, const AS4 muz_ln& P,
+                                            F out) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4, c0 = 16 * wv + 4 * g;
+  const f32x4 ga = gp(reinterpret_cast<const f32x4*>(P.scale))[c0 >> 2];
+  const f32x4 be = gp(reinterpret_cast<const f32x4*>(P.bias))[c0 >> 2];
+#pragma unroll
+  for (int t = 0; t < kPairTiles; ++t) {
+    const int pos = t * 16 + r;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(st + pos * 8);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(st + pos * 8 + 4);
+    const float s = ((a[0] + a[2]) + b[0]) + b[2], s2 = ((a[1] + a[3]) + b[1]) + b[3];
+    const float mean = s / 64.f, mean2 = s2 / 64.f;
+    const float inv = ln_rstd(fmaxf(0.f, fmaf(-mean, mean, mean2)) + 1e-6f);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fmaxf(fmaf(acc[t][j] - mean, inv * ga[j], be[j]), 0.f);
+    out(pos, c0, o);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_repr_conv3(muz_repr_w Rarg, const float* __restrict__ obs, int C, int n,
+                                                    const int* __restrict__ n_dev, float* __restrict__ convout,
+                                                    int32_t* host_counts) {
+  if (host_counts && blockIdx.x == 0 && threadIdx.x == 0) {   // (n_dev set: the self-play turn's counts)
+    __hip_atomic_store(&host_counts[0], n_dev[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host_counts[1], n_dev[1], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (n_dev) n = *n_dev;
+  const int g0 = 2 * (int)blockIdx.x;
+  if (g0 >= n) return;
+  const int ng = g0 + 1 < n ? 2 : 1;
+  const AS4 muz_repr_w& R = *kernarg0<muz_repr_w>();   // == Rarg, read through the kernarg segment
+  __shared__ __attribute__((aligned(16))) float sm[kConv3Floats];
+  float* in0 = sm;                 // [2][58][6]
+  float* pre0 = sm + kPre0At;      // [112][36] Conv_0 output
+  float* c1in = sm + kC1At;        // [2][58][36]
+  float* c2in = sm;                // [2][60][68] (over in0 | pre0 | c1in once Conv_1 has read them)
+  float* st = sm + kStatAt;        // [112][4 waves][sum, sum of squares]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 2 * kG0 * 6; i += 256) {
+    const int gm = i / (kG0 * 6), j = i % (kG0 * 6), w = j / 6 - 1, ch = j % 6;
+    in0[i] = (gm < ng && w >= 0 && w < 56) ? obs[((size_t)(g0 + gm) * C + ch) * 56 + w] : 0.f;
+  }
+  for (int i = tid; i < 4 * kC1Ld3; i += 256) {   // Conv_1 input pad rows 0 and 57 of each game
+    const int rr = i / kC1Ld3;
+    c1in[((rr >> 1) * kG1 + (rr & 1) * 57) * kC1Ld3 + i % kC1Ld3] = 0.f;
+  }
+  __syncthreads();
+  {  // Conv_0 (K = 3*6 = 18, N = 32) on VALU: a thread keeps one output channel, its 18 weights in registers
+    const int co = tid & 31;
+    float wk[18];
+#pragma unroll
+    for (int k = 0; k < 18; ++k) wk[k] = gp(R.conv0.w)[k * 32 + co];
+    const float bco = gp(R.conv0.b)[co];
+    for (int p = tid >> 5; p < kPairRows; p += 8) {
+      const int gm = p >= 56 ? 1 : 0;
+      const float* x = in0 + gm * kG0 * 6 + (p - 56 * gm) * 6;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 18; ++k) s = fmaf(x[k], wk[k], s);
+      pre0[p * kP0Ld + co] = s + bco;
+    }
+  }
+  __syncthreads();
+  ln_pair_ld<32, kP0Ld, kC1Ld3, kG1, 1>(pre0, c1in, R.ln0);
+  __syncthreads();
+  f32x4 acc[kPairTiles];
+  conv_acc_pair<6, 32, kC1Ld3, kG1>(R.conv1, c1in, acc, st);
+  __syncthreads();   // st published; every Conv_1 read of c1in done
+  for (int i = tid; i < 8 * kC2Ld3; i += 256) {   // Conv_2 input pad rows 0, 1, 58, 59 of each game
+    const int rr = i / kC2Ld3, row = (rr >> 2) * kG2 + ((rr & 3) < 2 ? (rr & 3) : 56 + (rr & 3));
+    c2in[row * kC2Ld3 + i % kC2Ld3] = 0.f;
+  }
+  ln_acc_pair(acc, st, R.ln1, [&](int pos, int c0, const f32x4& o) {
+    const int gm = pos >= 56 ? 1 : 0;
+    *reinterpret_cast<f32x4*>(c2in + (gm * kG2 + 2 + pos - 56 * gm) * kC2Ld3 + c0) = o;
+  });
+  __syncthreads();   // c2in complete; st read
+  conv_acc_pair<20, 64, kC2Ld3, kG2>(R.conv2, c2in, acc, st);
+  __syncthreads();
+  ln_acc_pair(acc, st, R.ln2, [&](int pos, int c0, const f32x4& o) {   // flatten (w, ch) -> w*64 + ch
+    const int gm = pos >= 56 ? 1 : 0;
+    if (gm < ng)
+      *reinterpret_cast<f32x4*>(convout + (size_t)(g0 + gm) * kConvRowFloats + (pos - 56 * gm) * 64 + c0) = o;
+  });
 }
 
 // RepresentationNetwork2's Dense_0 (3584 -> 256, muzero_deterministic_madn.py:107) for every game as ONE GEMM over
@@ -508,7 +693,9 @@ int check_net(const muz_net_w* w) {
 int launch_repr_conv(const muz_repr_w& r, const float* obs, int C, int n, const int* n_dev, float* conv,
                      hipStream_t s, int32_t* host_counts) {
   if (host_counts && !n_dev) return MUZ_E_INVALID;
-  if (MUZ_CONV_PAIR)
+  if (MUZ_CONV_PAIR == 3)
+    k_repr_conv3<<<(n + 1) / 2, 256, 0, s>>>(r, obs, C, n, n_dev, conv, host_counts);
+  else if (MUZ_CONV_PAIR)
     k_repr_conv2<<<(n + 1) / 2, kPairThreads, 0, s>>>(r, obs, C, n, n_dev, conv, host_counts);
   else
     k_repr_conv<<<n, 256, 0, s>>>(r, obs, C, n, n_dev, conv, host_counts);
