@@ -297,12 +297,15 @@ def setup(args):
     backend = os.environ.get("MUZ_BENCH_BACKEND", "nccl")
     if backend == "gloo":      # CPU rehearsal of the launcher / reduction path (tests/test_bench_launcher.py)
         device = torch.device("cpu")
+    elif backend == "gloo_gpu":   # N ranks sharing the visible GPU(s), gloo collectives: a one-GPU rehearsal of the
+        device = torch.device("cuda", local % torch.cuda.device_count())   # N-rank job (launch, barriers, reductions)
+        torch.cuda.set_device(device)
     else:
         device = torch.device("cuda", local)
         torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as tdist
-        tdist.init_process_group(backend, init_method="env://")
+        tdist.init_process_group("gloo" if backend == "gloo_gpu" else backend, init_method="env://")
         dist = tdist
     return rank, world, dist, device
 
@@ -346,6 +349,8 @@ def sum_max(dist, device, sums, elapsed):
     import torch
     if dist is None:
         return sums, elapsed
+    if dist.get_backend() == "gloo":
+        device = torch.device("cpu")
     t = torch.tensor([float(x) for x in sums], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     m = torch.tensor([elapsed], dtype=torch.float64, device=device)
