@@ -233,7 +233,22 @@ MEASURED = {
     "loop": "profiles/r5i_loop_bench.log",            # the weight-stream MFMA loop alone (profiles/loop_bench.hip)
     "dog_traffic": "profiles/r6b_dog_traffic.json",   # HBM bytes per k_dog_search launch (FETCH_SIZE x2 + WRITE_SIZE), 6 games / WG
     "classic_traffic": "profiles/r6b_classic_traffic.json",   # the same for k_stochastic_search (config c)
+    "dog_kernel_stats": "profiles/r6ae_dog_kernel_stats.csv",  # rocprofv3 --kernel-trace --stats of the DOG MuZero line
 }
+
+
+def measured_kernel_avg_ms(key, kernel):
+    """The average duration (ms) of `kernel` in a committed rocprofv3 kernel-stats CSV of the same bench command:
+    (ms, source) or (None, None)."""
+    import csv
+    path = os.path.join(ROOT, MEASURED[key])
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel in r.get("Name", ""):
+                return float(r["AverageNs"]) / 1e6, MEASURED[key]
+    return None, None
 
 
 def _measured_json(key, kernel):
@@ -495,6 +510,8 @@ def run_dog_muzero(args):
     achieved = args.batch * args.sims * DOG_MZ_EXEC_FLOP_PER_SIM / (avg_ms * 1e-3) / 1e12
     achieved_alg = args.batch * args.sims * DOG_MZ_FLOP_PER_SIM / (avg_ms * 1e-3) / 1e12
     traffic, traffic_src = measured_traffic("dog_traffic", "k_dog_search")
+    # the same kernel's average by rocprofv3 on this command (frac on both timing bases)
+    prof_ms, prof_src = measured_kernel_avg_ms("dog_kernel_stats", "k_dog_search")
     # k_dog_search's games per workgroup as the library launches it (was hard-coded)
     gpw = int(clib.muz_dog_search_games_per_workgroup(args.batch))
     out = {
@@ -514,6 +531,11 @@ def run_dog_muzero(args):
                      "flop_per_sim": DOG_MZ_EXEC_FLOP_PER_SIM, "flop_counted": "executed (one-hot rows as gathers)",
                      "reference_form_flop_per_sim": DOG_MZ_FLOP_PER_SIM,
                      "reference_form_frac": round(achieved_alg / PEAK_FP32_MFMA_TFLOPS, 4),
+                     "frac_rocprof": None if prof_ms is None else round(
+                         args.batch * args.sims * DOG_MZ_EXEC_FLOP_PER_SIM / (prof_ms * 1e-3) / 1e12 /
+                         PEAK_FP32_MFMA_TFLOPS, 4),
+                     "rocprof_avg_launch_ms": None if prof_ms is None else round(prof_ms, 4),
+                     "rocprof_source": prof_src,
                      "workgroups": -(-args.batch // gpw), "games_per_workgroup": gpw,
                      "traffic": None if traffic is None else round(traffic),
                      "traffic_achieved_tbs": None if traffic is None else round(traffic / (avg_ms * 1e-3) / 1e12, 3),
