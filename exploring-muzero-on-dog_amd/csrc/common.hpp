@@ -19,7 +19,13 @@
 // Root scratch row (muz_nets_root_scratch_bytes): RepresentationNetwork2's flattened conv maps (k_repr_conv) and, after
 // them, its Dense_0 output before LayerNorm_3 (k_dense0) -- one row per game
 constexpr int kConvMapFloats = 56 * 64;
-constexpr int kConvRowFloats = kConvMapFloats + 256;
+// k_dense0 splits Dense_0's K = 3584 over kD0KSplit workgroups per output tile (2: 512 workgroups, 2 per CU); each
+// writes its partial plane after the maps, the consumer (repr16<.., true>) adds them in plane order, then the bias
+#ifndef MUZ_D0_KSPLIT
+#define MUZ_D0_KSPLIT 2
+#endif
+constexpr int kD0KSplit = MUZ_D0_KSPLIT;
+constexpr int kConvRowFloats = kConvMapFloats + 256 * kD0KSplit;
 
 static inline int muz_last_launch_error() {
   hipError_t e = hipGetLastError();

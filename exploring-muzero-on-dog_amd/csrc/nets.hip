@@ -558,13 +558,17 @@ __global__ __launch_bounds__(512) void k_dense0(muz_dense d0, int n, const int* 
   f32x4 acc[TW];
 #pragma unroll
   for (int tt = 0; tt < TW; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  gload(0);
+  // this workgroup's share of the k chunks (blockIdx.y of kD0KSplit)
+  constexpr int kPer = kD0Chunks / kD0KSplit;
+  static_assert(kD0Chunks % kD0KSplit == 0, "Dense_0 k split");
+  const int cbeg = (int)blockIdx.y * kPer;
+  gload(cbeg);
   lstore(0);
   __syncthreads();
 #pragma unroll 1
-  for (int c = 0; c < kD0Chunks; ++c) {
+  for (int c = 0; c < kPer; ++c) {
     const int b = c & 1;
-    if (c + 1 < kD0Chunks) gload(c + 1);
+    if (c + 1 < kPer) gload(cbeg + c + 1);
 #pragma unroll
     for (int kb = 0; kb < kD0KC; ++kb) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(&sA[b][(rt * 16 + r) * kD0Ld + kb * 16 + 4 * g]);
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(512) void k_dense0(muz_dense d0, int n, const int* 
 #pragma unroll
         for (int tt = 0; tt < TW; ++tt) acc[tt] = mfma4(w[tt][j], a[j], acc[tt]);   // D = W^T A^T, dense16's order
     }
-    if (c + 1 < kD0Chunks) lstore(b ^ 1);
+    if (c + 1 < kPer) lstore(b ^ 1);
     __syncthreads();
   }
   const int row = row0 + rt * 16 + r;
@@ -588,7 +592,9 @@ __global__ __launch_bounds__(512) void k_dense0(muz_dense d0, int n, const int* 
 #pragma unroll
     for (int tt = 0; tt < TW; ++tt) {
       const int col = kD0NG == 2 ? (2 * cb + part) * 32 + tt * 16 + 4 * g : cb * 32 + part * 16 + 4 * g;
-      *reinterpret_cast<f32x4*>(conv + (size_t)row * kConvRowFloats + kConvMapFloats + col) = acc[tt] + bias4[col >> 2];
+      float* dst = conv + (size_t)row * kConvRowFloats + kConvMapFloats + 256 * blockIdx.y + col;
+      // (split: partial planes without the bias, which the consumer adds after the planes)
+      *reinterpret_cast<f32x4*>(dst) = kD0KSplit > 1 ? acc[tt] : acc[tt] + bias4[col >> 2];
     }
   }
 }
@@ -596,7 +602,7 @@ __global__ __launch_bounds__(512) void k_dense0(muz_dense d0, int n, const int* 
 int launch_dense0(const muz_dense& d0, int n, const int* n_dev, float* conv, hipStream_t s) {
   const int rbs = (n + kD0Rows - 1) / kD0Rows;
   const int wgs = (rbs + 7) / 8 * 8 * kD0CB;   // kD0CB column blocks per row block, row blocks dealt over the 8 XCDs
-  k_dense0<<<wgs, 512, 0, s>>>(d0, n, n_dev, conv);
+  k_dense0<<<dim3(wgs, kD0KSplit), 512, 0, s>>>(d0, n, n_dev, conv);
   return muz_last_launch_error();
 }
 

@@ -1055,8 +1055,15 @@ __device__ __forceinline__ void repr16(const AS4 muz_repr_w& R, const float* __r
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c4 = q + 32 * i;
-      const f32x4 v = gr_valid(g0 + rr, n) ? *gp(reinterpret_cast<const f32x4*>(
-                          convout + (size_t)(g0 + rr) * kConvRowFloats + kConvMapFloats) + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (gr_valid(g0 + rr, n)) {
+        const AS1 f32x4* src = gp(reinterpret_cast<const f32x4*>(convout + (size_t)(g0 + rr) * kConvRowFloats +
+                                                                 kConvMapFloats)) + c4;
+        v = src[0];
+#pragma unroll
+        for (int s = 1; s < kD0KSplit; ++s) v = v + src[64 * s];   // k_dense0's partial planes, in plane order
+        if (kD0KSplit > 1) v = v + gp(reinterpret_cast<const f32x4*>(R.d0.b))[c4];
+      }
       *reinterpret_cast<f32x4*>(a.W + rr * LDW + 4 * c4) = v;
     }
   } else {
